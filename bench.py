@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""bench.py — GB/s of layer data chunk-hashed + deduped on MI355X.
+
+Workload (BASELINE.json configs[1]): one synthetic 16 GiB
+layer tar = 4096 regular files x 4 MiB of random bytes (real ustar/PAX
+headers in between), PackOption.ChunkSize 1 MiB, blake3, no chunk dict.
+The layer is resident in HBM before timing; one "step" = one pass of the hot
+path over the layer through the C ABI (ngpu_process_device: BLAKE3 digests of
+all 16384 chunks + intra-layer dedup decisions + stats readback) plus the D2H
+copy of the 1 MiB result table.
+
+Multi-GPU (torchrun, one process per GPU): every rank converts its own layer
+(weak scaling, layers are independent — SURVEY.md §8(e)); no collective is in
+the data path.  value = bytes of file data all ranks digested / max-over-ranks
+time.
+
+The JSON line also carries:
+  roofline     — the dominant kernel (b3_groups) against the integer-VALU
+                 peak: algorithmic ops (680 per BLAKE3 compression) per launch
+                 / its HIP-event duration;
+  cpu_baseline — the CPU digest+dedup stage (oracle/cpu_baseline.c: official
+                 BLAKE3 C with AVX-512 dispatch, pthreads, stream-order dedup)
+                 on a bounded sample of the same layer, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tarfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "nydus-snapshotter_amd"))
+
+MiB = 1 << 20
+# gfx950: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md; the FP32
+# vector peak 157.3 TF = this x 2 FLOP/FMA).  One int32 VALU op per lane/clk.
+PEAK_INT_OPS = 256 * 4 * 32 * 2.4e9
+PEAK_HBM = 8.0e12
+OPS_PER_COMPRESSION = 680  # 7 rounds x 8 G x 12 ops + 8 output xors
+
+
+def synthetic_layout(n_files: int, file_size: int, chunk_size: int):
+    """Tar layout of the synthetic layer: header bytes per file, data offsets,
+    and the chunk descriptors ngpu_tar_chunks would produce for it (checked by
+    tests/test_bench.py against the real parser on a small instance)."""
+    import nydus_gpu
+    headers = np.zeros((n_files, 512), np.uint8)
+    for i in range(n_files):
+        ti = tarfile.TarInfo(f"usr/lib/file-{i:05d}.bin")
+        ti.size = file_size
+        ti.mtime = 0
+        ti.uid = ti.gid = 0
+        ti.uname = ti.gname = "root"
+        ti.mode = 0o644
+        hb = ti.tobuf(format=tarfile.GNU_FORMAT)
+        assert len(hb) == 512
+        headers[i] = np.frombuffer(hb, np.uint8)
+    stride = 512 + (file_size + 511) // 512 * 512
+    total = n_files * stride + 1024
+    per_file = (file_size + chunk_size - 1) // chunk_size
+    ch = np.zeros(n_files * per_file, nydus_gpu.CHUNK_DTYPE)
+    k = np.arange(per_file, dtype=np.uint64)
+    for i in range(n_files):
+        s = slice(i * per_file, (i + 1) * per_file)
+        ch["offset"][s] = i * stride + 512 + k * chunk_size
+        ch["length"][s] = np.minimum(chunk_size, file_size - k * chunk_size)
+        ch["file_index"][s] = i
+        ch["file_offset"][s] = k * chunk_size
+    return headers, stride, total, ch
+
+
+def build_layer_on_gpu(torch, n_files, file_size, chunk_size, seed, dup_every=0):
+    headers, stride, total, ch = synthetic_layout(n_files, file_size, chunk_size)
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    step = 1 << 30
+    for s in range(0, total, step):
+        buf[s:min(total, s + step)].random_(0, 256, generator=g)
+    body = buf[: n_files * stride].view(n_files, stride)
+    body[:, :512].copy_(torch.from_numpy(headers).cuda())
+    buf[n_files * stride:].zero_()
+    if dup_every:  # plant duplicate files (whole-file copies)
+        for i in range(dup_every, n_files, dup_every):
+            body[i, 512:].copy_(body[i - 1, 512:])
+    torch.cuda.synchronize()
+    return buf, ch
+
+
+def cpu_baseline(host_sample: np.ndarray, ch: np.ndarray, digester: str, threads: int):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py
+    chs = ch.view(oracle_py.CHUNK_DTYPE)
+    nbytes = int(chs["length"].sum())
+    oracle_py.cpu_digest_dedup(host_sample, chs[:16], digester, 1)  # load libs
+    t0 = time.perf_counter()
+    oracle_py.cpu_digest_dedup(host_sample, chs, digester, 1)
+    t_single = time.perf_counter() - t0
+    reps = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle_py.cpu_digest_dedup(host_sample, chs, digester, threads)
+        reps += 1
+        if time.perf_counter() - t0 > 3.0 or reps >= 20:
+            break
+    t_multi = (time.perf_counter() - t0) / reps
+    return {"value": round(nbytes / t_multi / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"first {nbytes / MiB:.0f} MiB of file data of the same layer "
+                      f"({len(chs)} chunks), digest+dedup, {oracle_py.cpu_impl()}; "
+                      f"{reps} reps on {threads} threads",
+            "single_stream_gbs": round(nbytes / t_single / 1e9, 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5", "small"])
+    ap.add_argument("--lanes", type=int, default=0, help="leaves per lane (0=auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-mib", type=int, default=2048)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import nydus_gpu
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    wl = {"c2": dict(n_files=4096, file_size=4 * MiB, chunk=MiB, digester="blake3", dup=0),
+          "c3": dict(n_files=4096, file_size=4 * MiB, chunk=MiB, digester="sha256", dup=0),
+          "c5": dict(n_files=1024, file_size=16 * MiB, chunk=64 * 1024, digester="blake3", dup=0),
+          "small": dict(n_files=256, file_size=4 * MiB, chunk=MiB, digester="blake3", dup=0)}[args.workload]
+    buf, ch = build_layer_on_gpu(torch, wl["n_files"], wl["file_size"], wl["chunk"], seed=0x6E79647573 + rank)
+    n = len(ch)
+    file_bytes = int(ch["length"].sum())
+    d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+    d_out = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    h_out = torch.empty(n * 64, dtype=torch.uint8, pin_memory=True)
+    eng = nydus_gpu.Engine(device=local, digester=wl["digester"], chunk_size=wl["chunk"],
+                           leaves_per_lane=args.lanes, timing=True)
+    stream = torch.cuda.Stream()
+
+    def step():
+        with torch.cuda.stream(stream):
+            eng.process_device(buf.data_ptr(), buf.numel(), d_ch.data_ptr(), n, d_out.data_ptr(),
+                               stream=stream.cuda_stream)
+            h_out.copy_(d_out, non_blocking=True)
+        return eng.last_timing()
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timings = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        timings.append(step())
+    stream.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness spot check of the last step (no planted dups -> all NEW)
+    res = h_out.numpy().view(nydus_gpu.RESULT_DTYPE)
+    assert (res["kind"] == nydus_gpu.NEW).all() and (res["index"] == np.arange(n)).all()
+
+    total_bytes = file_bytes * args.steps * world
+    value = total_bytes / elapsed / 1e9
+    dig_ms = float(np.mean([t["digest_ms"] for t in timings]))
+    tree_ms = float(np.mean([t["tree_ms"] for t in timings]))
+    dedup_ms = float(np.mean([t["dedup_ms"] for t in timings]))
+    D = timings[-1]["group_log2"]
+    if wl["digester"] == "blake3":
+        leaves = int(((ch["length"].astype(np.int64) + 1023) // 1024).sum())
+        blocks = int(((ch["length"].astype(np.int64) + 63) // 64).sum())
+        groups = int((((ch["length"].astype(np.int64) + 1023) // 1024 + (1 << D) - 1) >> D).sum())
+        # compressions done by b3_groups: all leaf blocks + in-group parents
+        comp = blocks + (leaves - groups)
+        achieved = comp * OPS_PER_COMPRESSION / (dig_ms / 1e3)
+        roof = {"bound": "valu", "kernel": f"b3_groups<{D}>", "achieved": round(achieved / 1e12, 3),
+                "peak": round(PEAK_INT_OPS / 1e12, 3), "unit": "Tops/s",
+                "frac": round(achieved / PEAK_INT_OPS, 4), "traffic": None,
+                "hbm_gbs": round(file_bytes / (dig_ms / 1e3) / 1e9, 1),
+                "hbm_frac": round(file_bytes / (dig_ms / 1e3) / PEAK_HBM, 4)}
+    else:
+        blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).sum())
+        ops = blocks * 1384  # SURVEY.md §8(d) SHA-256 op count
+        achieved = ops / (dig_ms / 1e3)
+        roof = {"bound": "valu", "kernel": "sha256_chunks", "achieved": round(achieved / 1e12, 3),
+                "peak": round(PEAK_INT_OPS / 1e12, 3), "unit": "Tops/s",
+                "frac": round(achieved / PEAK_INT_OPS, 4), "traffic": None,
+                "hbm_gbs": round(file_bytes / (dig_ms / 1e3) / 1e9, 1),
+                "occupancy_ceiling": f"{n} lanes = {n / (256 * 4 * 64):.3f} waves per SIMD"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sample_files = max(1, min(wl["n_files"], (args.cpu_sample_mib * MiB) // wl["file_size"]))
+        headers, stride, _, _ = synthetic_layout(1, wl["file_size"], wl["chunk"])
+        host = buf[: sample_files * stride].cpu().numpy()
+        per_file = (wl["file_size"] + wl["chunk"] - 1) // wl["chunk"]
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(host, ch[: sample_files * per_file], wl["digester"], threads)
+
+    line = {
+        "metric": "GB/s of layer data chunk-hashed+deduped (node)",
+        "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (random bytes on GPU, real tar headers)",
+        "config": {"workload": {"c2": "C2: 16 GiB layer tar, 4096 x 4 MiB files, 1 MiB chunks, "
+                                      "blake3, no chunk dict",
+                                "c3": "C3-shape digest: 16 GiB layer, 1 MiB chunks, sha256, no dict",
+                                "c5": "C5-shape: 16 GiB layer, 64 KiB chunks, blake3, no dict",
+                                "small": "1 GiB layer, 1 MiB chunks, blake3"}[args.workload],
+                   "layer_bytes": int(buf.numel()), "file_bytes_per_gpu": file_bytes, "chunks": n,
+                   "chunk_size": wl["chunk"], "digester": wl["digester"],
+                   "leaves_per_lane": 1 << D, "parallelism": f"layer-sharded x{world}"},
+        "stage_ms": {"digest": round(dig_ms, 3), "tree": round(tree_ms, 3), "dedup": round(dedup_ms, 3)},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    if cpu:
+        line["speedup_vs_cpu"] = round(value / cpu["value"], 2)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

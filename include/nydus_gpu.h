@@ -1,0 +1,202 @@
+/*
+ * nydus_gpu.h — C ABI of the MI355X chunk digest + dedup engine
+ * (libnydusgpu.so).  Plain pointers and sizes only; no C++ or torch types.
+ *
+ * What this boundary replaces:
+ *   The reference hands the digest/dedup stage to an external process:
+ *   pkg/converter/tool/builder.go:148-178 (tool.Pack) execs
+ *   `nydus-image create --type tar-rafs [--chunk-dict bootstrap=P]
+ *    [--chunk-size S] ...` (argv built at builder.go:78-146) over FIFOs set up
+ *   by packFromTar (pkg/converter/convert_unix.go:443-539).  Inside that
+ *   process, per chunk: RafsDigest::from_buf + Node::deduplicate_chunk
+ *   ([nydus v2.3.0] utils/src/digest.rs, builder/src/core/node.rs).
+ *   This library performs exactly that stage in-process on the GPU; the Go
+ *   side binds it from a new pkg/gpu cgo package.
+ *
+ * Errors: every function returns 0 on success or a negative NGPU_E* code;
+ * ngpu_last_error() gives the per-engine message (Go wraps both into an
+ * `error`, as builder.go:169-175 wraps the process exit status).  No
+ * exceptions cross the ABI.  A missing or unusable GPU is an error
+ * (NGPU_ENODEV): there is no CPU fallback in this library.
+ *
+ * Threading: an engine serialises its own calls internally; use one engine
+ * per goroutine pool / per device for concurrency.
+ */
+#ifndef NYDUS_GPU_H
+#define NYDUS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NGPU_ABI_VERSION 1
+
+/* PackOption.Digester (API extension; maps to nydus-image --digester). */
+enum ngpu_digester { NGPU_DIGEST_BLAKE3 = 0, NGPU_DIGEST_SHA256 = 1 };
+
+/* Per-chunk dedup outcome ([nydus v2.3.0] Node::deduplicate_chunk). */
+enum ngpu_kind {
+  NGPU_NEW = 0,   /* first occurrence: new data in this layer's blob */
+  NGPU_INTRA = 1, /* duplicate of an earlier NEW chunk of this layer */
+  NGPU_DICT = 2   /* found in the chunk dict (PackOption.ChunkDictPath) */
+};
+
+enum ngpu_error {
+  NGPU_OK = 0,
+  NGPU_EINVAL = -1,    /* bad argument (e.g. ChunkSize not a power of two) */
+  NGPU_EHIP = -2,      /* HIP runtime error */
+  NGPU_ENOMEM = -3,    /* device or pinned allocation failed */
+  NGPU_ETAR = -4,      /* malformed / truncated tar stream */
+  NGPU_EUNSUPP = -5,   /* unsupported input (GNU sparse tar entry) */
+  NGPU_ENODEV = -6,    /* no usable gfx950 device */
+  NGPU_EIO = -7,       /* file I/O (chunk-dict bootstrap) */
+  NGPU_EFORMAT = -8    /* not a RAFS v6 bootstrap / bad chunk table */
+};
+
+typedef struct ngpu_engine ngpu_engine;
+
+/* Mirrors the PackOption fields this stage consumes
+ * (pkg/converter/types.go:58-90). */
+typedef struct {
+  int32_t device;         /* HIP device ordinal */
+  uint32_t digester;      /* enum ngpu_digester (default blake3) */
+  uint32_t chunk_size;    /* PackOption.ChunkSize: power of two in
+                             [0x1000, 0x1000000] (types.go:76); 0 -> 0x100000 */
+  uint32_t fs_version;    /* PackOption.FsVersion 5 or 6; 0 -> 6
+                             (builder.go:79-81).  v6 aligns uncompressed
+                             offsets of NEW chunks to 4 KiB. */
+  uint64_t staging_bytes; /* pinned staging slot size for host-buffer calls;
+                             0 -> 256 MiB (two slots are allocated) */
+  uint32_t leaves_per_lane; /* BLAKE3 tuning: 1 KiB leaves hashed per lane
+                               (1, 2, 4, 8 or 16); 0 -> auto */
+  uint32_t flags;         /* NGPU_FLAG_* */
+} ngpu_config;
+
+/* ngpu_config.flags */
+#define NGPU_FLAG_TIMING 0x1u /* record HIP events around each stage */
+
+/* Per-stage device time of the last process call (NGPU_FLAG_TIMING). */
+typedef struct {
+  float digest_ms;   /* leaf/group digest kernel (b3_groups / sha256_chunks) */
+  float tree_ms;     /* BLAKE3 upper-tree kernel (0 for sha256) */
+  float dedup_ms;    /* dict probe + intra-layer dedup + scans + finalize */
+  float total_ms;    /* whole enqueue, first to last kernel */
+  uint32_t group_log2; /* leaves-per-lane log2 used (BLAKE3) */
+  uint32_t reserved;
+} ngpu_timing;
+
+/* One chunk of layer file data. 24 bytes. */
+typedef struct {
+  uint64_t offset;      /* byte offset of the chunk in the data buffer */
+  uint32_t length;      /* 1 .. chunk_size bytes */
+  uint32_t file_index;  /* ordinal of the owning regular file in the tar */
+  uint64_t file_offset; /* offset of the chunk inside its file */
+} ngpu_chunk;
+
+/* Per-chunk result. 64 bytes. */
+typedef struct {
+  uint8_t digest[32];   /* BLAKE3-256 or SHA-256 of the raw chunk bytes
+                           (RafsV5/V6 ChunkInfo block_id) */
+  uint32_t kind;        /* enum ngpu_kind */
+  uint32_t index;       /* NEW: sequential chunk index in this layer's blob;
+                           INTRA: index of the referenced NEW chunk;
+                           DICT: the dict entry's chunk index */
+  uint64_t ref;         /* NEW: own chunk id; INTRA: chunk id of the first
+                           occurrence; DICT: dict entry id (table order) */
+  uint32_t blob_index;  /* real blob index, allocated in first-hit order */
+  uint32_t reserved;
+  uint64_t uncompressed_offset; /* NEW/INTRA: offset in the layer blob */
+} ngpu_result;
+
+/* Summary of one layer. */
+typedef struct {
+  uint64_t chunks, new_chunks, intra_chunks, dict_chunks;
+  uint64_t new_bytes;        /* uncompressed bytes of NEW chunks */
+  uint32_t own_blob_index;   /* UINT32_MAX if the layer has no NEW chunk */
+  uint32_t blobs;            /* blob-table entries this layer references */
+  uint64_t uncompressed_size;/* end of the last NEW chunk (v6: 4K aligned) */
+} ngpu_layer_stats;
+
+int ngpu_abi_version(void);
+
+/* Engine lifetime.  Replaces the per-Pack builder process spawn
+ * (builder.go:163 exec.CommandContext). */
+int ngpu_create(const ngpu_config *cfg, ngpu_engine **out);
+void ngpu_destroy(ngpu_engine *eng);
+const char *ngpu_last_error(const ngpu_engine *eng);
+int ngpu_device_count(void);
+
+/* Pinned host memory owned by the engine (cgo must not hand Go-heap memory
+ * to async DMA). */
+int ngpu_alloc_pinned(ngpu_engine *eng, uint64_t bytes, void **out);
+int ngpu_free_pinned(ngpu_engine *eng, void *ptr);
+
+/* ---- chunk dict (PackOption.ChunkDictPath; builder.go:122-124) ---------- */
+/* Load n dict entries in chunk-table order into an HBM-resident hash table.
+ * First entry wins for duplicate digests.  usize == 0 matches any size.
+ * blob_index: the dict's inner blob index per entry; chunk_index: the
+ * entry's RAFS chunk index (copied into DICT results). */
+int ngpu_dict_load(ngpu_engine *eng, const uint8_t *digests /* n x 32 */,
+                   const uint32_t *usize, const uint32_t *blob_index,
+                   const uint32_t *chunk_index, uint64_t n);
+/* Parse a RAFS v6 bootstrap's chunk table (80-B records at the extended
+ * superblock's chunk_table_offset; pkg/layout/layout.go:25-27) and load it. */
+int ngpu_dict_load_bootstrap(ngpu_engine *eng, const char *path);
+int ngpu_dict_clear(ngpu_engine *eng);
+uint64_t ngpu_dict_size(const ngpu_engine *eng);
+
+/* ---- tar front end (host) ------------------------------------------------ */
+/* Enumerate the chunks of a tar-rafs layer.  Writes at
+ * most cap chunks; *n_chunks receives the full count (call again with a
+ * larger array if it exceeds cap).  *n_files: regular files seen. */
+int ngpu_tar_chunks(const void *tar, uint64_t len, uint32_t chunk_size,
+                    ngpu_chunk *out, uint64_t cap, uint64_t *n_chunks,
+                    uint64_t *n_files);
+
+/* ---- digest + dedup ------------------------------------------------------- */
+/* Host buffers in, host results out (synchronous).  `data` is the layer's
+ * bytes (e.g. the uncompressed tar), `chunks` index into it.  Data moves to
+ * HBM through the engine's pinned staging slots with hipMemcpyAsync. */
+int ngpu_process(ngpu_engine *eng, const void *data, uint64_t len,
+                 const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
+                 ngpu_layer_stats *stats);
+
+/* Device-resident variant: data, chunks and out are device pointers; work is
+ * enqueued on `stream` (a hipStream_t, or NULL for the engine's stream) and
+ * the call returns without synchronising.  stats may be NULL; if not NULL the
+ * call synchronises the stream to fill it. */
+int ngpu_process_device(ngpu_engine *eng, const void *d_data, uint64_t len,
+                        const ngpu_chunk *d_chunks, uint64_t n,
+                        ngpu_result *d_out, void *stream,
+                        ngpu_layer_stats *stats);
+
+/* Whole tar layer in host memory -> chunk list + results (tar parse on the
+ * host, digest/dedup on the GPU).  *chunks_out / *results_out are allocated
+ * with malloc and must be released with ngpu_free_host. */
+int ngpu_pack_tar(ngpu_engine *eng, const void *tar, uint64_t len,
+                  ngpu_chunk **chunks_out, ngpu_result **results_out,
+                  uint64_t *n_out, ngpu_layer_stats *stats);
+void ngpu_free_host(void *p);
+
+/* Stage timings of the last ngpu_process / ngpu_process_device call on this
+ * engine (synchronises on the recorded events).  NGPU_EINVAL unless the
+ * engine was created with NGPU_FLAG_TIMING. */
+int ngpu_last_timing(ngpu_engine *eng, ngpu_timing *out);
+
+/* ---- RAFS v6 chunk table ---------------------------- */
+/* Serialise the layer's unique chunk records (NEW chunks in index order) as
+ * 80-byte RAFS v6 chunk-info entries.  compressor "none": compressed size =
+ * uncompressed size, compressed offsets packed back to back.  `blob_index`
+ * of each record is the result's real blob index.  Writes at most cap
+ * records; *n_records receives the count. */
+int ngpu_chunk_table(const ngpu_chunk *chunks, const ngpu_result *results,
+                     uint64_t n, uint8_t *out /* cap x 80 */, uint64_t cap,
+                     uint64_t *n_records);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NYDUS_GPU_H */

@@ -1,0 +1,325 @@
+// dedup.hip — chunk-dict probe and intra-layer dedup decisions on gfx950.
+//
+// Restates, data-parallel, the stream-order semantics of
+// [nydus v2.3.0] Node::deduplicate_chunk + HashChunkDict (external, VERIFY;
+// SURVEY.md §8(a) a5/a6):
+//   1. global dict (PackOption.ChunkDictPath, builder.go:122-124): hit iff
+//      the digest is present and (dict usize == 0 || == chunk size); the dict
+//      keeps the FIRST chunk-table entry per digest;
+//   2. else the layered dict = earlier NEW chunks of this layer, same size
+//      rule, first insertion kept;
+//   3. else NEW with the next sequential index; v6 uncompressed offsets are
+//      the running sum of 4 KiB-rounded sizes.
+// Sequential "first occurrence" becomes an atomic MIN over chunk ids in an
+// HBM hash table; sequential index assignment becomes an exclusive scan;
+// blob-index allocation in first-hit order becomes a rank over first-hit
+// positions.  Results are bit-identical to the sequential restatement
+// (oracle/dedup_ref.c) for any schedule.
+//
+// Hash table: open addressing, linear probing over 8-byte slots
+// {tag = digest word 2 : id}; bucket = (digest words 0,1) * golden ratio.
+// Roofline: HBM-bound probes.
+#include "common.hpp"
+
+namespace ngpu {
+namespace {
+
+template <int STRIDE>
+__device__ __forceinline__ void load_digest(const uint8_t *keys, uint64_t id,
+                                            uint32_t d[8]) {
+  const uint4 *p = reinterpret_cast<const uint4 *>(keys + id * STRIDE);
+  uint4 a = p[0], b = p[1];
+  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+  d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
+template <int STRIDE>
+__device__ __forceinline__ bool digest_eq(const uint8_t *keys, uint64_t id,
+                                          const uint32_t d[8]) {
+  uint32_t e[8];
+  load_digest<STRIDE>(keys, id, e);
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x |= e[i] ^ d[i];
+  return x == 0;
+}
+
+// Insert id; for an existing identical digest keep the smallest id.
+template <int STRIDE>
+__device__ void ht_insert_min(uint64_t *table, uint64_t mask,
+                              const uint8_t *keys, uint32_t id) {
+  uint32_t d[8];
+  load_digest<STRIDE>(keys, id, d);
+  const uint32_t tag = digest_tag(d);
+  const uint64_t mine = ((uint64_t)tag << 32) | id;
+  for (uint64_t p = digest_bucket(d) & mask;; p = (p + 1) & mask) {
+    uint64_t s = __hip_atomic_load(table + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s == kEmpty) {
+      const uint64_t old = atomicCAS((unsigned long long *)(table + p),
+                                     (unsigned long long)kEmpty,
+                                     (unsigned long long)mine);
+      if (old == kEmpty) return;
+      s = old;
+    }
+    if ((uint32_t)(s >> 32) == tag && digest_eq<STRIDE>(keys, (uint32_t)s, d)) {
+      if ((uint32_t)s > id) atomicMin((unsigned long long *)(table + p), (unsigned long long)mine);
+      return;
+    }
+  }
+}
+
+// Returns the stored (smallest) id for digest d, or kNone.
+template <int STRIDE>
+__device__ uint32_t ht_lookup(const uint64_t *table, uint64_t mask,
+                              const uint8_t *keys, const uint32_t d[8]) {
+  const uint32_t tag = digest_tag(d);
+  for (uint64_t p = digest_bucket(d) & mask;; p = (p + 1) & mask) {
+    const uint64_t s = table[p];
+    if (s == kEmpty) return kNone;
+    if ((uint32_t)(s >> 32) == tag && digest_eq<STRIDE>(keys, (uint32_t)s, d))
+      return (uint32_t)s;
+  }
+}
+
+__global__ void dict_insert(const uint8_t *__restrict__ digests, uint64_t m,
+                            uint64_t *__restrict__ table, uint64_t mask) {
+  const uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (e < m) ht_insert_min<32>(table, mask, digests, (uint32_t)e);
+}
+
+// Stage 1: dict probe + reset of the per-chunk state.
+__global__ void dedup_probe(const ngpu_chunk *__restrict__ chunks, uint64_t n,
+                            DictDevice dict, ngpu_result *__restrict__ out,
+                            uint64_t *__restrict__ newflag,
+                            uint32_t *__restrict__ blob_first) {
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  ngpu_result &r = out[c];
+  uint32_t kind = NGPU_NEW;
+  if (dict.m) {
+    uint32_t d[8];
+    load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
+    const uint32_t e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
+    if (e != kNone) {
+      const uint32_t us = dict.usize[e];
+      if (us == 0 || us == chunks[c].length) {
+        kind = NGPU_DICT;
+        r.ref = e;
+        r.index = dict.index[e];
+        r.blob_index = dict.blob[e];  // inner index; remapped in finalize
+        r.uncompressed_offset = 0;
+        atomicMin(blob_first + dict.blob[e], (uint32_t)c);
+      }
+    }
+  }
+  r.kind = kind;
+  r.reserved = 0;
+  newflag[c] = 0;
+}
+
+__global__ void dedup_insert(const ngpu_result *__restrict__ out, uint64_t n,
+                             uint64_t *__restrict__ table, uint64_t mask) {
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (c >= n || out[c].kind == NGPU_DICT) return;
+  ht_insert_min<sizeof(ngpu_result)>(table, mask,
+                                     reinterpret_cast<const uint8_t *>(out), (uint32_t)c);
+}
+
+__global__ void dedup_resolve(const ngpu_chunk *__restrict__ chunks, uint64_t n,
+                              const uint64_t *__restrict__ table, uint64_t mask,
+                              ngpu_result *__restrict__ out, uint32_t align,
+                              uint64_t *__restrict__ newflag,
+                              uint64_t *__restrict__ uoff,
+                              uint32_t *__restrict__ own_first) {
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  ngpu_result &r = out[c];
+  uoff[c] = 0;
+  if (c == 0) { newflag[n] = 0; uoff[n] = 0; }
+  if (r.kind == NGPU_DICT) return;
+  uint32_t d[8];
+  load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
+  const uint32_t f = ht_lookup<sizeof(ngpu_result)>(
+      table, mask, reinterpret_cast<const uint8_t *>(out), d);
+  const uint32_t len = chunks[c].length;
+  if (f != (uint32_t)c && f != kNone && chunks[f].length == len) {
+    r.kind = NGPU_INTRA;
+    r.ref = f;
+    return;
+  }
+  r.kind = NGPU_NEW;
+  r.ref = c;
+  newflag[c] = 1;
+  uoff[c] = ((uint64_t)len + align - 1) / align * align;
+  atomicMin(own_first, (uint32_t)c);
+}
+
+// Blob-table order: each dict blob gets a real index at its first hit, the
+// layer's own blob at its first NEW chunk ([nydus v2.3.0] BlobManager
+// alloc_index / get_or_create_current_blob).  nb <= a few thousand.
+__global__ void blob_rank(const uint32_t *__restrict__ first, uint32_t nb_plus_own,
+                          uint32_t *__restrict__ real, uint64_t *__restrict__ stats) {
+  for (uint32_t b = threadIdx.x; b < nb_plus_own; b += blockDim.x) {
+    const uint32_t fb = first[b];
+    uint32_t rank = kNone;
+    if (fb != kNone) {
+      rank = 0;
+      for (uint32_t o = 0; o < nb_plus_own; ++o) rank += first[o] < fb;
+    }
+    real[b] = rank;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t used = 0;
+    for (uint32_t b = 0; b < nb_plus_own; ++b) used += first[b] != kNone;
+    stats[5] = real[nb_plus_own - 1];  // own blob (kNone -> 0xFFFFFFFF)
+    stats[6] = used;
+  }
+}
+
+__global__ void dedup_finalize(const ngpu_chunk *__restrict__ chunks, uint64_t n,
+                               const uint64_t *__restrict__ newidx,
+                               const uint64_t *__restrict__ uoff,
+                               const uint32_t *__restrict__ real, uint32_t own_slot,
+                               ngpu_result *__restrict__ out,
+                               uint64_t *__restrict__ stats) {
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (c == 0) { stats[0] = n; stats[8] = uoff[n]; stats[1] = newidx[n]; }
+  if (c >= n) return;
+  ngpu_result &r = out[c];
+  const uint32_t own = real[own_slot];
+  if (r.kind == NGPU_NEW) {
+    r.index = (uint32_t)newidx[c];
+    r.uncompressed_offset = uoff[c];
+    r.blob_index = own;
+    atomicAdd((unsigned long long *)(stats + 4), (unsigned long long)chunks[c].length);
+  } else if (r.kind == NGPU_INTRA) {
+    const uint64_t f = r.ref;
+    r.index = (uint32_t)newidx[f];
+    r.uncompressed_offset = uoff[f];
+    r.blob_index = own;
+    atomicAdd((unsigned long long *)(stats + 2), 1ull);
+  } else {
+    r.blob_index = real[r.blob_index];
+    atomicAdd((unsigned long long *)(stats + 3), 1ull);
+  }
+}
+
+// ---- exclusive scan over u64 (n+1 entries, in place) ----------------------
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *total) {
+  __shared__ uint64_t wsum[kScanThreads / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kScanThreads / 64; ++w) {
+    if (w < wid) pre += wsum[w];
+    tot += wsum[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_reduce(const uint64_t *__restrict__ a,
+                                                            uint64_t m, uint64_t *__restrict__ tmp) {
+  const uint64_t base = blockIdx.x * (uint64_t)kScanTile + threadIdx.x * kScanItems;
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i)
+    if (base + i < m) s += a[base + i];
+  uint64_t tot;
+  block_exclusive_scan(s, &tot);
+  if (threadIdx.x == 0) tmp[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_top(uint64_t *__restrict__ tmp, uint64_t nb) {
+  uint64_t carry = 0;
+  for (uint64_t t0 = 0; t0 < nb; t0 += kScanThreads) {
+    const uint64_t i = t0 + threadIdx.x;
+    const uint64_t v = i < nb ? tmp[i] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_exclusive_scan(v, &tot);
+    if (i < nb) tmp[i] = carry + ex;
+    carry += tot;
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_apply(uint64_t *__restrict__ a, uint64_t m,
+                                                           const uint64_t *__restrict__ tmp) {
+  const uint64_t base = blockIdx.x * (uint64_t)kScanTile + threadIdx.x * kScanItems;
+  uint64_t v[kScanItems], s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    v[i] = base + i < m ? a[base + i] : 0;
+    s += v[i];
+  }
+  uint64_t tot;
+  uint64_t run = block_exclusive_scan(s, &tot) + tmp[blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    if (base + i < m) a[base + i] = run;
+    run += v[i];
+  }
+}
+
+}  // namespace
+
+uint64_t scan_tmp_words(uint64_t n) { return (n + 1 + kScanTile - 1) / kScanTile + 1; }
+
+void launch_scan_u64(uint64_t *a, uint64_t n, uint64_t *tmp, hipStream_t s) {
+  const uint64_t m = n + 1;
+  const uint64_t nb = (m + kScanTile - 1) / kScanTile;
+  hipLaunchKernelGGL(scan_reduce, dim3((unsigned)nb), dim3(kScanThreads), 0, s, a, m, tmp);
+  hipLaunchKernelGGL(scan_top, dim3(1), dim3(kScanThreads), 0, s, tmp, nb);
+  hipLaunchKernelGGL(scan_apply, dim3((unsigned)nb), dim3(kScanThreads), 0, s, a, m, tmp);
+}
+
+void launch_dict_build(const uint8_t *digests, uint64_t m, uint64_t *table,
+                       uint64_t cap, hipStream_t s) {
+  hipMemsetAsync(table, 0xFF, cap * sizeof(uint64_t), s);
+  if (m == 0) return;
+  const uint64_t blocks = (m + 255) / 256;
+  hipLaunchKernelGGL(dict_insert, dim3((unsigned)blocks), dim3(256), 0, s, digests, m,
+                     table, cap - 1);
+}
+
+void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
+                  uint32_t align, Workspace &ws, ngpu_result *out, hipStream_t s) {
+  const uint32_t nbo = dict.n_blobs + 1;  // dict blobs + own blob (last slot)
+  hipMemsetAsync(ws.blob_first, 0xFF, sizeof(uint32_t) * nbo, s);
+  if (n) {
+    hipMemsetAsync(ws.intra, 0xFF, ws.intra_cap * sizeof(uint64_t), s);
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(dedup_probe, dim3(blocks), dim3(256), 0, s, chunks, n, dict, out,
+                       ws.newflag, ws.blob_first);
+    hipLaunchKernelGGL(dedup_insert, dim3(blocks), dim3(256), 0, s, out, n, ws.intra,
+                       ws.intra_cap - 1);
+    hipLaunchKernelGGL(dedup_resolve, dim3(blocks), dim3(256), 0, s, chunks, n, ws.intra,
+                       ws.intra_cap - 1, out, align, ws.newflag, ws.uoff,
+                       ws.blob_first + dict.n_blobs);
+  } else {
+    hipMemsetAsync(ws.newflag, 0, sizeof(uint64_t), s);
+    hipMemsetAsync(ws.uoff, 0, sizeof(uint64_t), s);
+  }
+  launch_scan_u64(ws.newflag, n, ws.scan_tmp, s);
+  launch_scan_u64(ws.uoff, n, ws.scan_tmp, s);
+  hipLaunchKernelGGL(blob_rank, dim3(1), dim3(256), 0, s, ws.blob_first, nbo, ws.blob_real,
+                     ws.stats);
+  const unsigned blocks = (unsigned)((n + 255) / 256) + 1;
+  hipLaunchKernelGGL(dedup_finalize, dim3(blocks), dim3(256), 0, s, chunks, n, ws.newflag,
+                     ws.uoff, ws.blob_real, dict.n_blobs, out, ws.stats);
+}
+
+}  // namespace ngpu

@@ -1,0 +1,416 @@
+// engine.hip — the C ABI of libnydusgpu.so (include/nydus_gpu.h): engine
+// lifetime, HBM workspace, chunk dict residency and the per-layer
+// digest -> dedup pipeline on one HIP stream.
+//
+// Replaces the per-layer `nydus-image create` process of
+// pkg/converter/tool/builder.go:148-178 for the digest/dedup stage; the
+// option validation mirrors pkg/converter/types.go:58-90 (ChunkSize power of
+// two in [0x1000, 0x1000000], FsVersion "5"/"6", default "6").
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+using namespace ngpu;
+
+struct ngpu_engine {
+  ngpu_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  Workspace ws;
+  // chunk dict, HBM resident
+  uint8_t *d_dict_digest = nullptr;
+  uint32_t *d_dict_usize = nullptr, *d_dict_blob = nullptr, *d_dict_index = nullptr;
+  uint64_t *d_dict_table = nullptr;
+  DictDevice dict;
+  // host-path device buffers
+  uint8_t *d_data = nullptr;
+  uint64_t d_data_cap = 0;
+  ngpu_chunk *d_chunks = nullptr;
+  ngpu_result *d_results = nullptr;
+  uint64_t d_chunk_cap = 0;
+  uint64_t *h_stats = nullptr;  // pinned
+  // NGPU_FLAG_TIMING: 0 start, 1 digest start, 2 digest end, 3 tree end, 4 end
+  hipEvent_t ev[5] = {};
+  bool timed = false;
+  int last_D = 0;
+  std::string err;
+  std::mutex mu;
+};
+
+namespace {
+
+int fail(ngpu_engine *e, int code, const char *fmt, ...) {
+  if (e) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    e->err = buf;
+  }
+  return code;
+}
+
+#define HIP_TRY(e, call)                                                        \
+  do {                                                                          \
+    hipError_t _st = (call);                                                    \
+    if (_st != hipSuccess)                                                      \
+      return fail((e), _st == hipErrorOutOfMemory ? NGPU_ENOMEM : NGPU_EHIP,   \
+                  "%s: %s (%s:%d)", #call, hipGetErrorString(_st), __FILE__,   \
+                  __LINE__);                                                    \
+  } while (0)
+
+template <typename T>
+int grow(ngpu_engine *e, T **p, uint64_t &cap, uint64_t want, uint64_t elem_bytes = sizeof(T)) {
+  if (want <= cap && *p) return 0;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  cap = 0;
+  uint64_t c = want < 1024 ? 1024 : want;
+  HIP_TRY(e, hipMalloc((void **)p, c * elem_bytes));
+  cap = c;
+  return 0;
+}
+
+uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+int pick_group_log2(const ngpu_engine *e, uint64_t data_len) {
+  switch (e->cfg.leaves_per_lane) {
+    case 1: return 0;
+    case 2: return 1;
+    case 4: return 2;
+    case 8: return 3;
+    case 16: return 4;
+    default: break;
+  }
+  // auto: enough lanes to fill 256 CUs several times, but at most the
+  // chunk's own leaf count (whole chunk per lane for small chunk sizes).
+  const uint64_t leaves = data_len / kLeaf + 1;
+  int D = 0;
+  while (D < 3 && (leaves >> (D + 1)) >= (1ull << 20)) ++D;
+  int cap = 0;
+  while (cap < 4 && (1ull << (cap + 1)) * kLeaf <= e->cfg.chunk_size) ++cap;
+  return D < cap ? D : cap;
+}
+
+int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D) {
+  Workspace &ws = e->ws;
+  if (n + 1 > ws.cap_n || !ws.groups) {
+    uint64_t cn = n + 1 < 4096 ? 4096 : n + 1;
+    uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    if (grow(e, &ws.groups, c0, cn)) return NGPU_ENOMEM;
+    if (grow(e, &ws.newflag, c1, cn)) return NGPU_ENOMEM;
+    if (grow(e, &ws.uoff, c2, cn)) return NGPU_ENOMEM;
+    if (grow(e, &ws.scan_tmp, c3, scan_tmp_words(cn))) return NGPU_ENOMEM;
+    uint64_t icap = next_pow2(2 * cn);
+    uint64_t ic = 0;
+    if (ws.intra) (void)hipFree(ws.intra), ws.intra = nullptr;
+    if (grow(e, &ws.intra, ic, icap)) return NGPU_ENOMEM;
+    ws.intra_cap = icap;
+    ws.cap_n = cn;
+  }
+  if (!ws.stats) {
+    uint64_t c = 0;
+    if (grow(e, &ws.stats, c, 16)) return NGPU_ENOMEM;
+  }
+  const uint64_t nb = e->dict.n_blobs + 1;
+  if (nb > ws.cap_blobs || !ws.blob_first) {
+    uint64_t c0 = 0, c1 = 0;
+    if (ws.blob_first) hipFree(ws.blob_first), ws.blob_first = nullptr;
+    if (ws.blob_real) hipFree(ws.blob_real), ws.blob_real = nullptr;
+    if (grow(e, &ws.blob_first, c0, nb)) return NGPU_ENOMEM;
+    if (grow(e, &ws.blob_real, c1, nb)) return NGPU_ENOMEM;
+    ws.cap_blobs = c0;
+  }
+  if (e->cfg.digester == NGPU_DIGEST_BLAKE3) {
+    const uint64_t g = blake3_max_groups(n, data_len, D);
+    if (g > ws.cap_g || !ws.cv) {
+      uint64_t c0 = 0, c1 = 0;
+      if (ws.cv) hipFree(ws.cv), ws.cv = nullptr;
+      if (ws.group_chunk) hipFree(ws.group_chunk), ws.group_chunk = nullptr;
+      if (grow(e, &ws.cv, c0, g, 32)) return NGPU_ENOMEM;
+      if (grow(e, &ws.group_chunk, c1, g)) return NGPU_ENOMEM;
+      ws.cap_g = c0 < c1 ? c0 : c1;
+    }
+  }
+  return 0;
+}
+
+void free_dict(ngpu_engine *e) {
+  (void)hipFree(e->d_dict_digest);
+  (void)hipFree(e->d_dict_usize);
+  (void)hipFree(e->d_dict_blob);
+  (void)hipFree(e->d_dict_index);
+  (void)hipFree(e->d_dict_table);
+  e->d_dict_digest = nullptr;
+  e->d_dict_usize = e->d_dict_blob = e->d_dict_index = nullptr;
+  e->d_dict_table = nullptr;
+  e->dict = DictDevice{};
+}
+
+int enqueue(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
+            const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+            hipStream_t s) {
+  const int D = pick_group_log2(e, len);
+  int rc = ensure_workspace(e, n, len, D);
+  if (rc) return rc;
+  const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
+  if (tm) HIP_TRY(e, hipEventRecord(e->ev[0], s));
+  HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 16 * sizeof(uint64_t), s));
+  if (e->cfg.digester == NGPU_DIGEST_SHA256) {
+    if (tm) HIP_TRY(e, hipEventRecord(e->ev[1], s));
+    launch_sha256(d_data, len, d_chunks, n, d_out, e->ws.stats + 7, s);
+    if (tm) HIP_TRY(e, hipEventRecord(e->ev[2], s));
+  } else {
+    launch_blake3(d_data, d_chunks, n, len, D, e->ws, d_out, s, tm ? e->ev[1] : nullptr,
+                  tm ? e->ev[2] : nullptr);
+  }
+  if (tm) HIP_TRY(e, hipEventRecord(e->ev[3], s));
+  const uint32_t align = e->cfg.fs_version == 6 ? 4096u : 1u;
+  launch_dedup(d_chunks, n, e->dict, align, e->ws, d_out, s);
+  if (tm) HIP_TRY(e, hipEventRecord(e->ev[4], s));
+  HIP_TRY(e, hipGetLastError());
+  e->timed = tm && n > 0;
+  e->last_D = D;
+  return 0;
+}
+
+int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st) {
+  HIP_TRY(e, hipMemcpyAsync(e->h_stats, e->ws.stats, 16 * sizeof(uint64_t),
+                            hipMemcpyDeviceToHost, s));
+  HIP_TRY(e, hipStreamSynchronize(s));
+  const uint64_t *h = e->h_stats;
+  if (h[7]) return fail(e, NGPU_EINVAL, "%llu chunk descriptor(s) outside the data buffer",
+                        (unsigned long long)h[7]);
+  if (st) {
+    st->chunks = h[0];
+    st->new_chunks = h[1];
+    st->intra_chunks = h[2];
+    st->dict_chunks = h[3];
+    st->new_bytes = h[4];
+    st->own_blob_index = (uint32_t)h[5];
+    st->blobs = (uint32_t)h[6];
+    st->uncompressed_size = h[8];
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ngpu_abi_version(void) { return NGPU_ABI_VERSION; }
+
+// internal (host.cpp), not part of nydus_gpu.h
+uint32_t ngpu_engine_chunk_size(const ngpu_engine *e) { return e->cfg.chunk_size; }
+
+int ngpu_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
+  if (!out) return NGPU_EINVAL;
+  *out = nullptr;
+  ngpu_config c{};
+  if (cfg) c = *cfg;
+  if (c.chunk_size == 0) c.chunk_size = 0x100000;
+  if (c.fs_version == 0) c.fs_version = 6;
+  if (c.staging_bytes == 0) c.staging_bytes = 256ull << 20;
+  if ((c.chunk_size & (c.chunk_size - 1)) || c.chunk_size < 0x1000 || c.chunk_size > 0x1000000)
+    return NGPU_EINVAL;  // types.go:76
+  if (c.fs_version != 5 && c.fs_version != 6) return NGPU_EINVAL;
+  if (c.digester != NGPU_DIGEST_BLAKE3 && c.digester != NGPU_DIGEST_SHA256) return NGPU_EINVAL;
+  if (c.leaves_per_lane & (c.leaves_per_lane - 1) || c.leaves_per_lane > 16) return NGPU_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return NGPU_ENODEV;
+  if (c.device < 0 || c.device >= ndev) return NGPU_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) return NGPU_ENODEV;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NGPU_ENODEV;
+  ngpu_engine *e = new ngpu_engine();
+  e->cfg = c;
+  e->device = c.device;
+  if (hipSetDevice(c.device) != hipSuccess) {
+    delete e;
+    return NGPU_EHIP;
+  }
+  if (c.flags & NGPU_FLAG_TIMING)
+    for (auto &ev : e->ev)
+      if (hipEventCreate(&ev) != hipSuccess) {
+        delete e;
+        return NGPU_EHIP;
+      }
+  if (
+      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc((void **)&e->h_stats, 16 * sizeof(uint64_t), hipHostMallocDefault) !=
+          hipSuccess) {
+    delete e;
+    return NGPU_EHIP;
+  }
+  *out = e;
+  return NGPU_OK;
+}
+
+void ngpu_destroy(ngpu_engine *e) {
+  if (!e) return;
+  hipSetDevice(e->device);
+  if (e->stream) hipStreamSynchronize(e->stream);
+  free_dict(e);
+  Workspace &ws = e->ws;
+  void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.scan_tmp,
+                  ws.intra, ws.blob_first, ws.blob_real, ws.stats,
+                  e->d_data, e->d_chunks, e->d_results};
+  for (void *p : bufs)
+    if (p) (void)hipFree(p);
+  if (e->h_stats) (void)hipHostFree(e->h_stats);
+  for (auto ev : e->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->stream) hipStreamDestroy(e->stream);
+  delete e;
+}
+
+const char *ngpu_last_error(const ngpu_engine *e) { return e ? e->err.c_str() : "null engine"; }
+
+int ngpu_alloc_pinned(ngpu_engine *e, uint64_t bytes, void **out) {
+  if (!e || !out) return NGPU_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  HIP_TRY(e, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  return 0;
+}
+
+int ngpu_free_pinned(ngpu_engine *e, void *p) {
+  if (!e) return NGPU_EINVAL;
+  HIP_TRY(e, hipHostFree(p));
+  return 0;
+}
+
+int ngpu_dict_load(ngpu_engine *e, const uint8_t *digests, const uint32_t *usize,
+                   const uint32_t *blob_index, const uint32_t *chunk_index, uint64_t n) {
+  if (!e || (n && (!digests || !usize || !blob_index))) return NGPU_EINVAL;
+  if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "dict too large (%llu entries)",
+                                      (unsigned long long)n);
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  HIP_TRY(e, hipStreamSynchronize(e->stream));
+  free_dict(e);
+  if (n == 0) return 0;
+  uint32_t nb = 0;
+  for (uint64_t i = 0; i < n; ++i)
+    if (blob_index[i] + 1 > nb) nb = blob_index[i] + 1;
+  if (nb > (1u << 20)) return fail(e, NGPU_EINVAL, "dict blob index %u too large", nb - 1);
+  const uint64_t cap = next_pow2(2 * n + 16);
+  HIP_TRY(e, hipMalloc((void **)&e->d_dict_digest, n * 32));
+  HIP_TRY(e, hipMalloc((void **)&e->d_dict_usize, n * 4));
+  HIP_TRY(e, hipMalloc((void **)&e->d_dict_blob, n * 4));
+  HIP_TRY(e, hipMalloc((void **)&e->d_dict_index, n * 4));
+  HIP_TRY(e, hipMalloc((void **)&e->d_dict_table, cap * 8));
+  HIP_TRY(e, hipMemcpyAsync(e->d_dict_digest, digests, n * 32, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(e, hipMemcpyAsync(e->d_dict_usize, usize, n * 4, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(e, hipMemcpyAsync(e->d_dict_blob, blob_index, n * 4, hipMemcpyHostToDevice, e->stream));
+  if (chunk_index)
+    HIP_TRY(e, hipMemcpyAsync(e->d_dict_index, chunk_index, n * 4, hipMemcpyHostToDevice, e->stream));
+  else
+    HIP_TRY(e, hipMemsetAsync(e->d_dict_index, 0, n * 4, e->stream));
+  launch_dict_build(e->d_dict_digest, n, e->d_dict_table, cap, e->stream);
+  HIP_TRY(e, hipGetLastError());
+  HIP_TRY(e, hipStreamSynchronize(e->stream));
+  e->dict.digests = e->d_dict_digest;
+  e->dict.usize = e->d_dict_usize;
+  e->dict.blob = e->d_dict_blob;
+  e->dict.index = e->d_dict_index;
+  e->dict.table = e->d_dict_table;
+  e->dict.mask = cap - 1;
+  e->dict.m = n;
+  e->dict.n_blobs = nb;
+  return 0;
+}
+
+int ngpu_dict_clear(ngpu_engine *e) {
+  if (!e) return NGPU_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  HIP_TRY(e, hipStreamSynchronize(e->stream));
+  free_dict(e);
+  return 0;
+}
+
+uint64_t ngpu_dict_size(const ngpu_engine *e) { return e ? e->dict.m : 0; }
+
+int ngpu_process_device(ngpu_engine *e, const void *d_data, uint64_t len,
+                        const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+                        void *stream, ngpu_layer_stats *stats) {
+  if (!e || (n && (!d_data || !d_chunks || !d_out))) return NGPU_EINVAL;
+  if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too many chunks in one call");
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  int rc = enqueue(e, (const uint8_t *)d_data, len, d_chunks, n, d_out, s);
+  if (rc) return rc;
+  if (stats) return read_stats(e, s, stats);
+  return 0;
+}
+
+int ngpu_process(ngpu_engine *e, const void *data, uint64_t len, const ngpu_chunk *chunks,
+                 uint64_t n, ngpu_result *out, ngpu_layer_stats *stats) {
+  if (!e || (n && (!data || !chunks || !out))) return NGPU_EINVAL;
+  if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too many chunks in one call");
+  for (uint64_t i = 0; i < n; ++i) {
+    if (chunks[i].offset > len || chunks[i].length > len - chunks[i].offset)
+      return fail(e, NGPU_EINVAL, "chunk %llu outside the data buffer", (unsigned long long)i);
+    if (chunks[i].length > e->cfg.chunk_size)
+      return fail(e, NGPU_EINVAL, "chunk %llu longer than chunk_size", (unsigned long long)i);
+  }
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  hipStream_t s = e->stream;
+  uint64_t c0 = e->d_data_cap;
+  if (grow(e, &e->d_data, c0, len + 64)) return NGPU_ENOMEM;
+  e->d_data_cap = c0;
+  if (n + 1 > e->d_chunk_cap || !e->d_chunks) {
+    uint64_t a = 0, b = 0;
+    if (e->d_chunks) hipFree(e->d_chunks), e->d_chunks = nullptr;
+    if (e->d_results) hipFree(e->d_results), e->d_results = nullptr;
+    if (grow(e, &e->d_chunks, a, n + 1)) return NGPU_ENOMEM;
+    if (grow(e, &e->d_results, b, n + 1)) return NGPU_ENOMEM;
+    e->d_chunk_cap = a < b ? a : b;
+  }
+  if (len) HIP_TRY(e, hipMemcpyAsync(e->d_data, data, len, hipMemcpyHostToDevice, s));
+  if (n) HIP_TRY(e, hipMemcpyAsync(e->d_chunks, chunks, n * sizeof(ngpu_chunk),
+                                   hipMemcpyHostToDevice, s));
+  int rc = enqueue(e, e->d_data, len, e->d_chunks, n, e->d_results, s);
+  if (rc) return rc;
+  if (n) HIP_TRY(e, hipMemcpyAsync(out, e->d_results, n * sizeof(ngpu_result),
+                                   hipMemcpyDeviceToHost, s));
+  return read_stats(e, s, stats);
+}
+
+int ngpu_last_timing(ngpu_engine *e, ngpu_timing *out) {
+  if (!e || !out) return NGPU_EINVAL;
+  if (!(e->cfg.flags & NGPU_FLAG_TIMING))
+    return fail(e, NGPU_EINVAL, "engine created without NGPU_FLAG_TIMING");
+  std::lock_guard<std::mutex> g(e->mu);
+  memset(out, 0, sizeof *out);
+  if (!e->timed) return 0;
+  HIP_TRY(e, hipEventSynchronize(e->ev[4]));
+  HIP_TRY(e, hipEventElapsedTime(&out->digest_ms, e->ev[1], e->ev[2]));
+  HIP_TRY(e, hipEventElapsedTime(&out->tree_ms, e->ev[2], e->ev[3]));
+  HIP_TRY(e, hipEventElapsedTime(&out->dedup_ms, e->ev[3], e->ev[4]));
+  HIP_TRY(e, hipEventElapsedTime(&out->total_ms, e->ev[0], e->ev[4]));
+  out->group_log2 = (uint32_t)e->last_D;
+  return 0;
+}
+
+}  // extern "C"

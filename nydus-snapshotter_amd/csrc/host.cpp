@@ -1,0 +1,280 @@
+// host.cpp — host side of libnydusgpu.so around the GPU stage:
+//   * tar-rafs chunk enumeration,
+//   * RAFS v6 chunk-table reader for PackOption.ChunkDictPath and writer for
+//     the layer's chunk records (§8(a) a7, §8(f) next-2),
+//   * ngpu_pack_tar: tar in host memory -> chunks -> GPU digest/dedup.
+//
+// Tar rules follow what `nydus-image create --type tar-rafs` consumes
+// (pkg/converter/tool/builder.go:97-110, fed by packFromTar,
+// pkg/converter/convert_unix.go:443-539): POSIX ustar headers, GNU base-256
+// sizes, GNU long name/link ('L'/'K'), PAX extended headers ('x' may override
+// the next entry's size; 'g' skipped); regular files ('0', '\0', '7') of
+// non-zero size are cut into fixed-size chunks that never span files;
+// hardlinks, symlinks, directories, devices and fifos carry no chunks;
+// whiteouts are plain entries (`--whiteout-spec none`, builder.go:91-92);
+// GNU sparse ('S') is unsupported.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "nydus_gpu.h"
+
+namespace {
+
+bool zero_block(const uint8_t *p) {
+  for (int i = 0; i < 512; ++i)
+    if (p[i]) return false;
+  return true;
+}
+
+// Numeric header field: octal ASCII (space/NUL padded) or GNU base-256.
+bool tar_number(const uint8_t *f, size_t n, uint64_t *v) {
+  if (f[0] & 0x80) {
+    uint64_t x = f[0] & 0x7f;
+    for (size_t i = 1; i < n; ++i) {
+      if (x >> 56) return false;
+      x = (x << 8) | f[i];
+    }
+    *v = x;
+    return true;
+  }
+  size_t i = 0;
+  while (i < n && (f[i] == ' ' || f[i] == 0)) ++i;
+  uint64_t x = 0;
+  for (; i < n && f[i] >= '0' && f[i] <= '7'; ++i) x = (x << 3) | (uint64_t)(f[i] - '0');
+  for (; i < n; ++i)
+    if (f[i] != ' ' && f[i] != 0) return false;
+  *v = x;
+  return true;
+}
+
+bool header_checksum_ok(const uint8_t *h) {
+  uint64_t want;
+  if (!tar_number(h + 148, 8, &want)) return false;
+  uint64_t u = 0;
+  int64_t sgn = 0;
+  for (int i = 0; i < 512; ++i) {
+    const uint8_t c = (i >= 148 && i < 156) ? ' ' : h[i];
+    u += c;
+    sgn += (int8_t)c;
+  }
+  return u == want || (uint64_t)sgn == want;
+}
+
+// PAX records "len key=value\n"; returns 1 and *size if a size record exists.
+int pax_size_record(const uint8_t *p, uint64_t n, uint64_t *size) {
+  int found = 0;
+  uint64_t i = 0;
+  while (i < n) {
+    uint64_t rl = 0, j = i;
+    while (j < n && p[j] >= '0' && p[j] <= '9') rl = rl * 10 + (p[j++] - '0');
+    if (j >= n || p[j] != ' ' || rl == 0 || i + rl > n) break;
+    const uint8_t *kv = p + j + 1, *end = p + i + rl - 1;
+    if (end - kv > 5 && memcmp(kv, "size=", 5) == 0) {
+      uint64_t v = 0;
+      for (const uint8_t *q = kv + 5; q < end; ++q) {
+        if (*q < '0' || *q > '9') return -1;
+        v = v * 10 + (uint64_t)(*q - '0');
+      }
+      *size = v;
+      found = 1;
+    }
+    i += rl;
+  }
+  return found;
+}
+
+#pragma pack(push, 1)
+struct RafsV6ChunkInfo {  // 80 B, decoded from the v6 fixture
+  uint8_t block_id[32];
+  uint32_t blob_index;
+  uint32_t flags;
+  uint32_t compressed_size;
+  uint32_t uncompressed_size;
+  uint64_t compressed_offset;
+  uint64_t uncompressed_offset;
+  uint64_t file_offset;
+  uint32_t index;
+  uint32_t reserved;
+};
+#pragma pack(pop)
+static_assert(sizeof(RafsV6ChunkInfo) == 80, "RAFS v6 chunk info is 80 bytes");
+
+constexpr uint32_t kRafsV6Magic = 0xE0F5E1E2u;  // pkg/layout/layout.go:24
+constexpr uint64_t kRafsV6SuperBlockOffset = 1024;  // layout.go:26
+constexpr uint64_t kRafsV6ExtSuperBlockOffset = 1024 + 128;
+
+}  // namespace
+
+extern "C" {
+
+uint32_t ngpu_engine_chunk_size(const ngpu_engine *);  // engine.hip (internal)
+
+int ngpu_tar_chunks(const void *tar_v, uint64_t len, uint32_t chunk_size, ngpu_chunk *out,
+                    uint64_t cap, uint64_t *n_chunks, uint64_t *n_files) {
+  if ((!tar_v && len) || chunk_size == 0) return NGPU_EINVAL;
+  const uint8_t *tar = (const uint8_t *)tar_v;
+  uint64_t pos = 0, n = 0, files = 0, pax_sz = 0;
+  bool have_pax = false;
+  while (pos + 512 <= len) {
+    const uint8_t *h = tar + pos;
+    if (zero_block(h)) break;
+    if (!header_checksum_ok(h)) return NGPU_ETAR;
+    uint64_t size;
+    if (!tar_number(h + 124, 12, &size)) return NGPU_ETAR;
+    const char type = (char)h[156];
+    const uint64_t data = pos + 512;
+    switch (type) {
+      case 'x': {
+        if (size > len - data) return NGPU_ETAR;
+        const int r = pax_size_record(tar + data, size, &pax_sz);
+        if (r < 0) return NGPU_ETAR;
+        if (r > 0) have_pax = true;
+        break;
+      }
+      case 'g':
+      case 'L':
+      case 'K':
+        if (size > len - data) return NGPU_ETAR;
+        break;
+      case 'S':
+        return NGPU_EUNSUPP;
+      default: {
+        if (have_pax) size = pax_sz;
+        have_pax = false;
+        if (type == '0' || type == '\0' || type == '7') {
+          if (size > len - data) return NGPU_ETAR;
+          for (uint64_t off = 0; off < size; off += chunk_size) {
+            if (n < cap && out) {
+              out[n].offset = data + off;
+              out[n].length = (uint32_t)(size - off < chunk_size ? size - off : chunk_size);
+              out[n].file_index = (uint32_t)files;
+              out[n].file_offset = off;
+            }
+            ++n;
+          }
+          ++files;
+        }
+      }
+    }
+    const uint64_t adv = (size + 511) & ~511ull;
+    if (adv < size || data + adv < data) return NGPU_ETAR;
+    pos = data + adv;
+  }
+  if (n_chunks) *n_chunks = n;
+  if (n_files) *n_files = files;
+  return NGPU_OK;
+}
+
+void ngpu_free_host(void *p) { free(p); }
+
+int ngpu_pack_tar(ngpu_engine *eng, const void *tar, uint64_t len, ngpu_chunk **chunks_out,
+                  ngpu_result **results_out, uint64_t *n_out, ngpu_layer_stats *stats) {
+  if (!eng || !chunks_out || !results_out || !n_out) return NGPU_EINVAL;
+  *chunks_out = nullptr;
+  *results_out = nullptr;
+  *n_out = 0;
+  const uint32_t cs = ngpu_engine_chunk_size(eng);
+  uint64_t n = 0, files = 0;
+  int rc = ngpu_tar_chunks(tar, len, cs, nullptr, 0, &n, &files);
+  if (rc) return rc;
+  ngpu_chunk *ch = (ngpu_chunk *)malloc(sizeof(ngpu_chunk) * (n ? n : 1));
+  ngpu_result *res = (ngpu_result *)malloc(sizeof(ngpu_result) * (n ? n : 1));
+  if (!ch || !res) {
+    free(ch);
+    free(res);
+    return NGPU_ENOMEM;
+  }
+  rc = ngpu_tar_chunks(tar, len, cs, ch, n, &n, &files);
+  if (!rc) rc = ngpu_process(eng, tar, len, ch, n, res, stats);
+  if (rc) {
+    free(ch);
+    free(res);
+    return rc;
+  }
+  *chunks_out = ch;
+  *results_out = res;
+  *n_out = n;
+  return NGPU_OK;
+}
+
+int ngpu_chunk_table(const ngpu_chunk *chunks, const ngpu_result *results, uint64_t n,
+                     uint8_t *out, uint64_t cap, uint64_t *n_records) {
+  if ((n && (!chunks || !results)) || !n_records) return NGPU_EINVAL;
+  // NEW chunks in index order; compressor "none": csize = usize, compressed
+  // offsets packed back to back (the fixture's coff rule with csize = usize).
+  std::vector<uint64_t> order;
+  for (uint64_t i = 0; i < n; ++i)
+    if (results[i].kind == NGPU_NEW) order.push_back(i);
+  // NEW indices are assigned in stream order, so order is already sorted by
+  // index; verify rather than assume.
+  for (uint64_t k = 0; k < order.size(); ++k)
+    if (results[order[k]].index != k) return NGPU_EINVAL;
+  uint64_t coff = 0;
+  for (uint64_t k = 0; k < order.size() && k < cap && out; ++k) {
+    const uint64_t i = order[k];
+    RafsV6ChunkInfo r;
+    memset(&r, 0, sizeof r);
+    memcpy(r.block_id, results[i].digest, 32);
+    r.blob_index = results[i].blob_index;
+    r.flags = 0;  // not compressed
+    r.compressed_size = chunks[i].length;
+    r.uncompressed_size = chunks[i].length;
+    r.compressed_offset = coff;
+    r.uncompressed_offset = results[i].uncompressed_offset;
+    r.file_offset = chunks[i].file_offset;
+    r.index = results[i].index;
+    memcpy(out + 80 * k, &r, 80);
+    coff += chunks[i].length;
+  }
+  *n_records = order.size();
+  return NGPU_OK;
+}
+
+// Reads the chunk table of a RAFS v6 bootstrap (ChunkDictPath) and loads it
+// as the chunk dict, table order preserved (first entry wins).
+int ngpu_dict_load_bootstrap(ngpu_engine *eng, const char *path) {
+  if (!eng || !path) return NGPU_EINVAL;
+  FILE *f = fopen(path, "rb");
+  if (!f) return NGPU_EIO;
+  uint8_t sb[kRafsV6ExtSuperBlockOffset + 256];
+  if (fread(sb, 1, sizeof sb, f) != sizeof sb) {
+    fclose(f);
+    return NGPU_EFORMAT;
+  }
+  uint32_t magic;
+  memcpy(&magic, sb + kRafsV6SuperBlockOffset, 4);
+  if (magic != kRafsV6Magic) {
+    fclose(f);
+    return NGPU_EFORMAT;
+  }
+  const uint8_t *ext = sb + kRafsV6ExtSuperBlockOffset;
+  uint64_t cto, cts;
+  memcpy(&cto, ext + 24, 8);  // RafsV6ChunkInfoOffset = 1024+128+24 (layout.go:27)
+  memcpy(&cts, ext + 32, 8);
+  if (cts % 80) {
+    fclose(f);
+    return NGPU_EFORMAT;
+  }
+  const uint64_t m = cts / 80;
+  std::vector<RafsV6ChunkInfo> recs(m);
+  if (m && (fseeko(f, (off_t)cto, SEEK_SET) != 0 ||
+            fread(recs.data(), 80, m, f) != m)) {
+    fclose(f);
+    return NGPU_EFORMAT;
+  }
+  fclose(f);
+  std::vector<uint8_t> dig(m * 32);
+  std::vector<uint32_t> us(m), blob(m), idx(m);
+  for (uint64_t i = 0; i < m; ++i) {
+    memcpy(&dig[i * 32], recs[i].block_id, 32);
+    us[i] = recs[i].uncompressed_size;
+    blob[i] = recs[i].blob_index;
+    idx[i] = recs[i].index;
+  }
+  return ngpu_dict_load(eng, dig.data(), us.data(), blob.data(), idx.data(), m);
+}
+
+}  // extern "C"

@@ -1,0 +1,11 @@
+"""nydus_gpu — MI355X chunk digest + dedup engine for the nydus conversion path.
+
+Python view of libnydusgpu.so (C ABI in include/nydus_gpu.h).  The engine
+replaces the digest/dedup stage that pkg/converter hands to
+`nydus-image create` (pkg/converter/tool/builder.go:148-178).
+"""
+from ._lib import (CHUNK_DTYPE, DICT, DIGESTERS, EXPORTS, INTRA, KIND_NAMES, NEW,  # noqa: F401
+                   RESULT_DTYPE, Engine, NgpuError, chunk_table, lib, tar_chunks)
+
+__all__ = ["Engine", "NgpuError", "tar_chunks", "chunk_table", "lib", "CHUNK_DTYPE",
+           "RESULT_DTYPE", "NEW", "INTRA", "DICT", "KIND_NAMES", "DIGESTERS", "EXPORTS"]

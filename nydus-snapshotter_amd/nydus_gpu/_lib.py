@@ -1,0 +1,260 @@
+"""ctypes binding of libnydusgpu.so (include/nydus_gpu.h).
+
+The library is the product: it is loaded from the package directory (built
+in-tree by ``make``); there is no fallback implementation — if the .so or a
+gfx950 GPU is missing the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libnydusgpu.so")
+
+DIGESTERS = {"blake3": 0, "sha256": 1}
+KIND_NAMES = {0: "NEW", 1: "INTRA", 2: "DICT"}
+NEW, INTRA, DICT = 0, 1, 2
+
+ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ETAR", -5: "EUNSUPP",
+          -6: "ENODEV", -7: "EIO", -8: "EFORMAT"}
+
+CHUNK_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u4"), ("file_index", "<u4"),
+                        ("file_offset", "<u8")])
+RESULT_DTYPE = np.dtype([("digest", "u1", (32,)), ("kind", "<u4"), ("index", "<u4"),
+                         ("ref", "<u8"), ("blob_index", "<u4"), ("reserved", "<u4"),
+                         ("uncompressed_offset", "<u8")])
+assert CHUNK_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 64
+
+# Every symbol include/nydus_gpu.h declares (checked by tests/test_abi.py).
+EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
+           "ngpu_device_count", "ngpu_alloc_pinned", "ngpu_free_pinned", "ngpu_dict_load",
+           "ngpu_dict_load_bootstrap", "ngpu_dict_clear", "ngpu_dict_size", "ngpu_tar_chunks",
+           "ngpu_process", "ngpu_process_device", "ngpu_pack_tar", "ngpu_free_host",
+           "ngpu_chunk_table", "ngpu_last_timing"]
+
+
+class NgpuConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("digester", ctypes.c_uint32),
+                ("chunk_size", ctypes.c_uint32), ("fs_version", ctypes.c_uint32),
+                ("staging_bytes", ctypes.c_uint64), ("leaves_per_lane", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+
+
+FLAG_TIMING = 0x1
+
+
+class NgpuTiming(ctypes.Structure):
+    _fields_ = [("digest_ms", ctypes.c_float), ("tree_ms", ctypes.c_float),
+                ("dedup_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
+                ("group_log2", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+class NgpuLayerStats(ctypes.Structure):
+    _fields_ = [("chunks", ctypes.c_uint64), ("new_chunks", ctypes.c_uint64),
+                ("intra_chunks", ctypes.c_uint64), ("dict_chunks", ctypes.c_uint64),
+                ("new_bytes", ctypes.c_uint64), ("own_blob_index", ctypes.c_uint32),
+                ("blobs", ctypes.c_uint32), ("uncompressed_size", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class NgpuError(RuntimeError):
+    def __init__(self, code, msg=""):
+        self.code = code
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}" if msg else ERRORS.get(code, str(code)))
+
+
+_lib = None
+
+
+def lib():
+    """Load libnydusgpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run `make -C {PKG_DIR}` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    pu64 = ctypes.POINTER(u64)
+    L.ngpu_abi_version.restype = i32
+    L.ngpu_create.argtypes = [ctypes.POINTER(NgpuConfig), ctypes.POINTER(vp)]
+    L.ngpu_destroy.argtypes = [vp]
+    L.ngpu_destroy.restype = None
+    L.ngpu_last_error.argtypes = [vp]
+    L.ngpu_last_error.restype = ctypes.c_char_p
+    L.ngpu_device_count.restype = i32
+    L.ngpu_alloc_pinned.argtypes = [vp, u64, ctypes.POINTER(vp)]
+    L.ngpu_free_pinned.argtypes = [vp, vp]
+    L.ngpu_dict_load.argtypes = [vp, vp, vp, vp, vp, u64]
+    L.ngpu_dict_load_bootstrap.argtypes = [vp, ctypes.c_char_p]
+    L.ngpu_dict_clear.argtypes = [vp]
+    L.ngpu_dict_size.argtypes = [vp]
+    L.ngpu_dict_size.restype = u64
+    L.ngpu_tar_chunks.argtypes = [vp, u64, u32, vp, u64, pu64, pu64]
+    L.ngpu_process.argtypes = [vp, vp, u64, vp, u64, vp, ctypes.POINTER(NgpuLayerStats)]
+    L.ngpu_process_device.argtypes = [vp, vp, u64, vp, u64, vp, vp, ctypes.POINTER(NgpuLayerStats)]
+    L.ngpu_pack_tar.argtypes = [vp, vp, u64, ctypes.POINTER(vp), ctypes.POINTER(vp), pu64,
+                                ctypes.POINTER(NgpuLayerStats)]
+    L.ngpu_free_host.argtypes = [vp]
+    L.ngpu_free_host.restype = None
+    L.ngpu_chunk_table.argtypes = [vp, vp, u64, vp, u64, pu64]
+    L.ngpu_last_timing.argtypes = [vp, ctypes.POINTER(NgpuTiming)]
+    _lib = L
+    return L
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None and a.size else None
+
+
+def _buf(data):
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return np.frombuffer(data, dtype=np.uint8)
+
+
+def tar_chunks(tar, chunk_size: int = 0x100000):
+    """Host tar front end: tar bytes -> CHUNK_DTYPE array (no GPU needed)."""
+    L = lib()
+    buf = _buf(tar)
+    n, nf = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = L.ngpu_tar_chunks(_ptr(buf), buf.size, chunk_size, None, 0, ctypes.byref(n), ctypes.byref(nf))
+    if rc:
+        raise NgpuError(rc, "tar parse")
+    out = np.zeros(n.value, dtype=CHUNK_DTYPE)
+    rc = L.ngpu_tar_chunks(_ptr(buf), buf.size, chunk_size, _ptr(out), n.value, ctypes.byref(n),
+                           ctypes.byref(nf))
+    if rc:
+        raise NgpuError(rc, "tar parse")
+    return out
+
+
+def chunk_table(chunks, results) -> np.ndarray:
+    """RAFS v6 chunk-info records (n x 80 bytes) of the layer's NEW chunks."""
+    L = lib()
+    ch = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+    rs = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
+    n = ctypes.c_uint64(0)
+    rc = L.ngpu_chunk_table(_ptr(ch), _ptr(rs), len(ch), None, 0, ctypes.byref(n))
+    if rc:
+        raise NgpuError(rc, "chunk table")
+    out = np.zeros((n.value, 80), dtype=np.uint8)
+    rc = L.ngpu_chunk_table(_ptr(ch), _ptr(rs), len(ch), _ptr(out), n.value, ctypes.byref(n))
+    if rc:
+        raise NgpuError(rc, "chunk table")
+    return out
+
+
+class Engine:
+    """One GPU engine (ngpu_engine*).  Mirrors the PackOption fields the
+    digest/dedup stage consumes (pkg/converter/types.go:58-90)."""
+
+    def __init__(self, device: int = 0, digester: str = "blake3", chunk_size: int = 0x100000,
+                 fs_version: int = 6, leaves_per_lane: int = 0, staging_bytes: int = 0,
+                 timing: bool = False):
+        L = lib()
+        if digester not in DIGESTERS:
+            raise ValueError(f"unsupported digester {digester!r}")
+        cfg = NgpuConfig(device=device, digester=DIGESTERS[digester], chunk_size=chunk_size,
+                         fs_version=fs_version, staging_bytes=staging_bytes,
+                         leaves_per_lane=leaves_per_lane, flags=FLAG_TIMING if timing else 0)
+        h = ctypes.c_void_p()
+        rc = L.ngpu_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc:
+            raise NgpuError(rc, "ngpu_create")
+        self._h = h
+        self.digester = digester
+        self.chunk_size = chunk_size
+        self.fs_version = fs_version
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ngpu_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc:
+            msg = lib().ngpu_last_error(self._h)
+            raise NgpuError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def dict_load(self, digests, usize, blob_index, chunk_index=None):
+        d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1, 32)
+        us = np.ascontiguousarray(usize, dtype=np.uint32)
+        bl = np.ascontiguousarray(blob_index, dtype=np.uint32)
+        ci = None if chunk_index is None else np.ascontiguousarray(chunk_index, dtype=np.uint32)
+        self._check(lib().ngpu_dict_load(self._h, _ptr(d), _ptr(us), _ptr(bl), _ptr(ci), len(us)),
+                    "dict_load")
+
+    def dict_load_bootstrap(self, path: str):
+        self._check(lib().ngpu_dict_load_bootstrap(self._h, path.encode()), "dict_load_bootstrap")
+
+    def dict_clear(self):
+        self._check(lib().ngpu_dict_clear(self._h), "dict_clear")
+
+    @property
+    def dict_size(self) -> int:
+        return lib().ngpu_dict_size(self._h)
+
+    def process(self, data, chunks):
+        """Host data + chunk descriptors -> (RESULT_DTYPE array, stats dict)."""
+        buf = _buf(data)
+        ch = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+        out = np.zeros(len(ch), dtype=RESULT_DTYPE)
+        st = NgpuLayerStats()
+        self._check(lib().ngpu_process(self._h, _ptr(buf), buf.size, _ptr(ch), len(ch), _ptr(out),
+                                       ctypes.byref(st)), "process")
+        return out, st.as_dict()
+
+    def process_device(self, d_data: int, length: int, d_chunks: int, n: int, d_out: int,
+                       stream: int = 0, want_stats: bool = False):
+        """Device pointers in (ints), enqueue on `stream`; returns stats if asked
+        (which synchronises)."""
+        st = NgpuLayerStats()
+        self._check(lib().ngpu_process_device(self._h, ctypes.c_void_p(d_data), length,
+                                              ctypes.c_void_p(d_chunks), n, ctypes.c_void_p(d_out),
+                                              ctypes.c_void_p(stream) if stream else None,
+                                              ctypes.byref(st) if want_stats else None),
+                    "process_device")
+        return st.as_dict() if want_stats else None
+
+    def last_timing(self) -> dict:
+        t = NgpuTiming()
+        self._check(lib().ngpu_last_timing(self._h, ctypes.byref(t)), "last_timing")
+        return t.as_dict()
+
+    def pack_tar(self, tar):
+        """Whole tar layer -> (chunks, results, stats)."""
+        L = lib()
+        buf = _buf(tar)
+        pc, pr = ctypes.c_void_p(), ctypes.c_void_p()
+        n = ctypes.c_uint64(0)
+        st = NgpuLayerStats()
+        self._check(L.ngpu_pack_tar(self._h, _ptr(buf), buf.size, ctypes.byref(pc), ctypes.byref(pr),
+                                    ctypes.byref(n), ctypes.byref(st)), "pack_tar")
+        try:
+            nn = n.value
+            ch = np.empty(nn, dtype=CHUNK_DTYPE)
+            rs = np.empty(nn, dtype=RESULT_DTYPE)
+            if nn:
+                ctypes.memmove(ch.ctypes.data, pc, nn * CHUNK_DTYPE.itemsize)
+                ctypes.memmove(rs.ctypes.data, pr, nn * RESULT_DTYPE.itemsize)
+        finally:
+            L.ngpu_free_host(pc)
+            L.ngpu_free_host(pr)
+        return ch, rs, st.as_dict()

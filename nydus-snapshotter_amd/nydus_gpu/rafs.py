@@ -1,0 +1,108 @@
+"""RAFS v6 bootstrap chunk-table helpers (host side, no GPU).
+
+Layout (pkg/layout/layout.go:18-27; record format decoded from the
+reference fixture pkg/filesystem/testdata/v6-bootstrap-chunk-pos-438272.tar.gz,
+SURVEY.md §8(c)):
+
+* v6 super block at 1024 (magic 0xE0F5E1E2), extended super block at 1152:
+  ``flags u64, blob_table_offset u64, blob_table_size u32, chunk_size u32,
+  chunk_table_offset u64 (@1176 = RafsV6ChunkInfoOffset), chunk_table_size u64,
+  prefetch_table_offset u64, prefetch_table_size u32``;
+* chunk table = 80-byte records (CHUNK_INFO_DTYPE).
+
+``canonical`` gives the inspect-equivalent comparison form: the table as a set
+keyed by digest (nydus writes it in hash-map iteration order, so byte order is
+meaningless).
+"""
+from __future__ import annotations
+
+import struct
+import tarfile
+
+import numpy as np
+
+RAFS_V6_MAGIC = 0xE0F5E1E2
+RAFS_V5_MAGIC = 0x52414653
+SUPER_OFFSET = 1024
+EXT_OFFSET = 1024 + 128
+CHUNK_INFO_OFFSET = 1024 + 128 + 24  # layout.go:27
+
+CHUNK_INFO_DTYPE = np.dtype([("block_id", "u1", (32,)), ("blob_index", "<u4"), ("flags", "<u4"),
+                             ("compressed_size", "<u4"), ("uncompressed_size", "<u4"),
+                             ("compressed_offset", "<u8"), ("uncompressed_offset", "<u8"),
+                             ("file_offset", "<u8"), ("index", "<u4"), ("reserved", "<u4")])
+assert CHUNK_INFO_DTYPE.itemsize == 80
+
+CHUNK_FLAG_COMPRESSED = 0x1
+
+
+def detect_fs_version(header: bytes) -> str:
+    """Port of DetectFsVersion (pkg/layout/layout.go:60-76)."""
+    if len(header) < 8:
+        raise ValueError("header buffer to DetectFsVersion is too small")
+    magic, ver = struct.unpack_from("<II", header, 0)
+    if magic == RAFS_V5_MAGIC and ver == 0x500:
+        return "v5"
+    if len(header) >= 1024 + 128 + 256 and struct.unpack_from("<I", header, SUPER_OFFSET)[0] == RAFS_V6_MAGIC:
+        return "v6"
+    raise ValueError("unknown file system header")
+
+
+def read_v6(boot: bytes) -> dict:
+    if detect_fs_version(boot) != "v6":
+        raise ValueError("not a RAFS v6 bootstrap")
+    flags, bto, bts, cs, cto, cts, pto, pts = struct.unpack_from("<QQIIQQQI", boot, EXT_OFFSET)
+    if cts % 80:
+        raise ValueError("chunk table size is not a multiple of 80")
+    table = np.frombuffer(boot, dtype=CHUNK_INFO_DTYPE, count=cts // 80, offset=cto).copy()
+    return {"flags": flags, "blob_table_offset": bto, "blob_table_size": bts, "chunk_size": cs,
+            "chunk_table_offset": cto, "chunk_table_size": cts, "chunks": table}
+
+
+def read_v6_from_targz(path: str) -> dict:
+    """The reference fixtures ship image/image.boot inside a .tar.gz."""
+    with tarfile.open(path, "r:gz") as tf:
+        for m in tf.getmembers():
+            if m.name.endswith("image.boot"):
+                return read_v6(tf.extractfile(m).read())
+    raise ValueError("no image.boot in archive")
+
+
+def write_v6_bootstrap(records: np.ndarray, chunk_size: int, flags: int = 0x4) -> bytes:
+    """Minimal RAFS v6 bootstrap holding only the super blocks + a chunk table
+    (enough for ChunkDictPath loading and chunk-table comparison)."""
+    recs = np.ascontiguousarray(records).view(CHUNK_INFO_DTYPE)
+    cto = 4096
+    buf = bytearray(cto + recs.nbytes)
+    struct.pack_into("<I", buf, SUPER_OFFSET, RAFS_V6_MAGIC)
+    struct.pack_into("<QQIIQQQI", buf, EXT_OFFSET, flags, 0, 0, chunk_size, cto, recs.nbytes, 0, 0)
+    buf[cto:] = recs.tobytes()
+    return bytes(buf)
+
+
+def canonical(records: np.ndarray):
+    """inspect-equivalent canonical form: sorted by digest."""
+    recs = np.asarray(records).view(CHUNK_INFO_DTYPE).reshape(-1)
+    rows = [(bytes(r["block_id"]).hex(), int(r["blob_index"]), int(r["flags"]),
+             int(r["compressed_size"]), int(r["uncompressed_size"]), int(r["compressed_offset"]),
+             int(r["uncompressed_offset"]), int(r["file_offset"]), int(r["index"])) for r in recs]
+    return sorted(rows)
+
+
+def check_offset_rules(records: np.ndarray, align: int = 4096):
+    """The layout rules the v6 fixture obeys (and our writer must): indices are a
+    permutation of 0..n-1; in index order, uncompressed offsets advance by the
+    align-rounded size and compressed offsets by the compressed size."""
+    recs = np.asarray(records).view(CHUNK_INFO_DTYPE).reshape(-1)
+    order = np.argsort(recs["index"], kind="stable")
+    r = recs[order]
+    if not np.array_equal(r["index"], np.arange(len(r))):
+        return False
+    uo = r["uncompressed_offset"].astype(np.int64)
+    us = r["uncompressed_size"].astype(np.int64)
+    co = r["compressed_offset"].astype(np.int64)
+    cs = r["compressed_size"].astype(np.int64)
+    exp_u = np.concatenate([[uo[0] if len(uo) else 0], (uo[:-1] + us[:-1] + align - 1) // align * align])
+    exp_c = np.concatenate([[co[0] if len(co) else 0], co[:-1] + cs[:-1]])
+    return bool(np.array_equal(uo, exp_u) and np.array_equal(co, exp_c))
+

@@ -1,0 +1,289 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden fixtures
+and the CPU oracle, bit-exact.  Run on a gfx950 box: pytest -m gpu."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+import nydus_gpu
+from nydus_gpu import rafs
+
+from conftest import kat_input
+
+pytestmark = pytest.mark.gpu
+
+LANES = [1, 2, 4, 8, 16]
+
+
+@pytest.fixture(scope="module")
+def engines():
+    cache = {}
+
+    def get(digester="blake3", chunk_size=0x100000, lanes=0, fs_version=6):
+        k = (digester, chunk_size, lanes, fs_version)
+        if k not in cache:
+            cache[k] = nydus_gpu.Engine(digester=digester, chunk_size=chunk_size,
+                                        leaves_per_lane=lanes, fs_version=fs_version)
+        return cache[k]
+    yield get
+    for e in cache.values():
+        e.close()
+
+
+def one_chunk(n, off=0):
+    ch = np.zeros(1, nydus_gpu.CHUNK_DTYPE)
+    ch["offset"], ch["length"] = off, n
+    return ch
+
+
+@pytest.mark.parametrize("digester", ["blake3", "sha256"])
+def test_kat_single_chunk(engines, kat, digester):
+    for lanes in (LANES if digester == "blake3" else [0]):
+        eng = engines(digester, 0x1000000, lanes)
+        for v in kat["vectors"]:
+            if v["len"] == 0:
+                continue  # nydus never emits empty chunks
+            out, st = eng.process(kat_input(v["len"]), one_chunk(v["len"]))
+            assert out["digest"][0].tobytes().hex() == v[digester], (lanes, v["len"])
+            assert st["new_chunks"] == 1
+
+
+def test_kat_batched_all_lengths(engines, kat):
+    """All KAT inputs in ONE call, packed back to back at odd offsets."""
+    vecs = [v for v in kat["vectors"] if v["len"]]
+    parts, chunks, off = [], [], 0
+    for v in vecs:
+        pad = 7
+        parts.append(b"\x55" * pad)
+        off += pad
+        parts.append(kat_input(v["len"]))
+        chunks.append((off, v["len"], 0, 0))
+        off += v["len"]
+    data = b"".join(parts)
+    ch = np.array(chunks, dtype=nydus_gpu.CHUNK_DTYPE)
+    for digester in ("blake3", "sha256"):
+        for lanes in (LANES if digester == "blake3" else [0]):
+            out, _ = engines(digester, 0x1000000, lanes).process(data, ch)
+            got = [o.tobytes().hex() for o in out["digest"]]
+            assert got == [v[digester] for v in vecs], (digester, lanes)
+
+
+def _decisions(out):
+    return [(int(o["kind"]), int(o["index"]), int(o["ref"]), int(o["blob_index"]),
+             int(o["uncompressed_offset"])) for o in out]
+
+
+def _expected(dec):
+    kinds = {"NEW": 0, "INTRA": 1, "DICT": 2}
+    return [(kinds[k], i, r, b, u) for (k, i, r, b, u) in dec]
+
+
+def test_golden_layers(engines, golden_layers, tars):
+    for case in golden_layers["cases"]:
+        for lanes in (LANES if case["digester"] == "blake3" else [0]):
+            eng = engines(case["digester"], case["chunk_size"], lanes)
+            ch, out, st = eng.pack_tar(tars[case["layer"]])
+            assert [tuple(int(x) for x in c) for c in ch] == [tuple(c) for c in case["chunks"]]
+            assert [d.tobytes().hex() for d in out["digest"]] == case["digests"], case["layer"]
+            assert _decisions(out) == _expected(case["decisions"]), case["layer"]
+            own = st["own_blob_index"]
+            assert (None if own == 0xFFFFFFFF else own) == case["own_blob"]
+
+
+def _dict_arrays(tp):
+    dd = np.frombuffer(b"".join(bytes.fromhex(e[0]) for e in tp["dict"]), np.uint8).reshape(-1, 32)
+    return (dd, np.array([e[1] for e in tp["dict"]], np.uint32),
+            np.array([e[2] for e in tp["dict"]], np.uint32), np.array([e[3] for e in tp["dict"]], np.uint32))
+
+
+def test_testpack_with_chunk_dict(engines, golden_layers, tars):
+    """tests/converter_test.go:459-528 outcome: lower all-DICT, upper own blob,
+    merged blob list [dict, upper]."""
+    tp = golden_layers["testpack"]
+    eng = nydus_gpu.Engine(chunk_size=0x100000)
+    try:
+        eng.dict_load(*_dict_arrays(tp))
+        assert eng.dict_size == len(tp["dict"])
+        blobs = []
+        for name, lay in tp["layers"].items():
+            ch, out, st = eng.pack_tar(tars[name])
+            assert _decisions(out) == _expected(lay["decisions"]), name
+            for o in out:
+                tag = "dict" if o["kind"] == nydus_gpu.DICT else name
+                if tag not in blobs:
+                    blobs.append(tag)
+        assert blobs == tp["expected_blobs"]
+    finally:
+        eng.close()
+
+
+def test_chunk_dict_bootstrap_roundtrip(tars, oracle):
+    """Pack the dict layer, write its chunk table into a RAFS v6 bootstrap,
+    load it as ChunkDictPath, pack the lower layer: every chunk is a DICT hit."""
+    eng = nydus_gpu.Engine(chunk_size=0x1000)
+    try:
+        ch, out, _ = eng.pack_tar(tars["chunk_dict"])
+        tab = nydus_gpu.chunk_table(ch, out)
+        with tempfile.TemporaryDirectory() as d:
+            p = os.path.join(d, "dict-bootstrap")
+            with open(p, "wb") as f:
+                f.write(rafs.write_v6_bootstrap(tab.view(rafs.CHUNK_INFO_DTYPE).reshape(-1), 0x1000))
+            eng.dict_load_bootstrap(p)
+        ch2, out2, st2 = eng.pack_tar(tars["oci_lower"])
+        assert (out2["kind"] == nydus_gpu.DICT).all()
+        assert st2["own_blob_index"] == 0xFFFFFFFF and st2["blobs"] == 1
+        # oracle agrees on every field
+        dig = oracle.digest_chunks(tars["oci_lower"], ch2.view(oracle.CHUNK_DTYPE), "blake3")
+        recs = tab.view(rafs.CHUNK_INFO_DTYPE).reshape(-1)
+        dec, _ = oracle.dedup(dig, ch2["length"], recs["block_id"], recs["uncompressed_size"],
+                              recs["blob_index"], recs["index"])
+        assert np.array_equal(out2["digest"], dig)
+        for f in ("kind", "index", "ref", "blob_index"):
+            assert np.array_equal(out2[f], dec[f]), f
+    finally:
+        eng.close()
+
+
+def _random_layer(rng, total, chunk_size, dup_frac=0.2, unaligned=False):
+    """Random data + chunk list (random lengths, some duplicated contents)."""
+    data = bytearray(rng.integers(0, 256, total, dtype=np.uint8).tobytes())
+    chunks, off = [], 0
+    while True:
+        ln = int(rng.integers(1, chunk_size + 1)) if rng.random() < 0.5 else chunk_size
+        if unaligned:
+            off += int(rng.integers(0, 16))
+        if off + ln > total:
+            break
+        chunks.append([off, ln, 0, 0])
+        off += ln
+        off = (off + 511) // 512 * 512 if not unaligned else off
+    # plant duplicates: copy an earlier chunk's bytes over a later same-length one
+    n = len(chunks)
+    for _ in range(int(n * dup_frac)):
+        a, b = sorted(rng.integers(0, n, 2))
+        la = chunks[a][1]
+        if a != b and la <= chunks[b][1]:
+            chunks[b][1] = la
+            data[chunks[b][0]:chunks[b][0] + la] = data[chunks[a][0]:chunks[a][0] + la]
+    return bytes(data), np.array([tuple(c) for c in chunks], dtype=nydus_gpu.CHUNK_DTYPE)
+
+
+@pytest.mark.parametrize("seed,chunk_size,unaligned", [
+    (1, 0x1000, False), (2, 0x4000, True), (3, 0x10000, False), (4, 0x100000, False),
+    (5, 0x100000, True), (6, 0x1000000, False)])
+def test_random_vs_oracle(engines, oracle, seed, chunk_size, unaligned):
+    rng = np.random.default_rng(seed)
+    total = 48 << 20 if chunk_size >= 0x100000 else 8 << 20
+    data, ch = _random_layer(rng, total, chunk_size, unaligned=unaligned)
+    for digester in ("blake3", "sha256"):
+        exp_d = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), digester)
+        exp, own = oracle.dedup(exp_d, ch["length"])
+        for lanes in ([0, 1, 16] if digester == "blake3" else [0]):
+            out, st = engines(digester, chunk_size, lanes).process(data, ch)
+            assert np.array_equal(out["digest"], exp_d), (digester, lanes)
+            for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+                assert np.array_equal(out[f], exp[f]), (digester, lanes, f)
+            assert st["intra_chunks"] == int((exp["kind"] == 1).sum())
+            assert st["new_chunks"] == int((exp["kind"] == 0).sum())
+
+
+def test_random_dict_vs_oracle(oracle):
+    """Dict with duplicates (first wins), usize 0 wildcard, size mismatches and
+    several inner blobs: decisions and blob allocation order match the oracle."""
+    rng = np.random.default_rng(11)
+    data, ch = _random_layer(rng, 16 << 20, 0x10000, dup_frac=0.3)
+    dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    n = len(ch)
+    pick = rng.choice(n, n // 2, replace=False)
+    dd = np.concatenate([dig[pick], rng.integers(0, 256, (5000, 32), dtype=np.uint8), dig[pick[:50]]])
+    ds = np.concatenate([ch["length"][pick], rng.integers(1, 1 << 16, 5000).astype(np.uint32),
+                         np.zeros(50, np.uint32)]).astype(np.uint32)
+    ds[: n // 20] = 0  # wildcard sizes
+    ds[n // 20: n // 10] += 1  # size mismatch -> miss
+    db = rng.integers(0, 7, len(dd)).astype(np.uint32)
+    di = rng.integers(0, 1 << 20, len(dd)).astype(np.uint32)
+    exp, own = oracle.dedup(dig, ch["length"], dd, ds, db, di)
+    eng = nydus_gpu.Engine(chunk_size=0x10000)
+    try:
+        eng.dict_load(dd, ds, db, di)
+        out, st = eng.process(data, ch)
+    finally:
+        eng.close()
+    for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+        assert np.array_equal(out[f], exp[f]), f
+    assert st["dict_chunks"] == int((exp["kind"] == 2).sum()) > 0
+
+
+def test_device_path_matches_host_path(engines):
+    import torch
+    rng = np.random.default_rng(5)
+    data, ch = _random_layer(rng, 32 << 20, 0x100000)
+    eng = engines("blake3", 0x100000, 0)
+    out_h, st_h = eng.process(data, ch)
+    d_data = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).cuda()
+    d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+    d_out = torch.zeros(len(ch) * 64, dtype=torch.uint8, device="cuda")
+    st = eng.process_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), len(ch),
+                            d_out.data_ptr(), stream=torch.cuda.current_stream().cuda_stream,
+                            want_stats=True)
+    out_d = d_out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+    assert out_d.tobytes() == out_h.tobytes()
+    assert st == st_h
+
+
+def test_bad_descriptor_device_path(engines):
+    import torch
+    eng = engines("blake3", 0x100000, 0)
+    d_data = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    ch = one_chunk(4096, off=1024)  # runs past the end of the buffer
+    d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+    d_out = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(nydus_gpu.NgpuError):
+        eng.process_device(d_data.data_ptr(), 4096, d_ch.data_ptr(), 1, d_out.data_ptr(),
+                           want_stats=True)
+    with pytest.raises(nydus_gpu.NgpuError):
+        eng.process(bytes(4096), ch)
+
+
+def test_empty_layer(engines):
+    out, st = engines().process(b"", np.zeros(0, nydus_gpu.CHUNK_DTYPE))
+    assert len(out) == 0 and st["chunks"] == 0 and st["own_blob_index"] == 0xFFFFFFFF
+
+
+def test_large_layer_properties(oracle):
+    """BASELINE configs[1]-shaped at 4 GiB (device resident): planted duplicates
+    are INTRA, NEW indices/offsets are the prefix sums, and a sample of chunks
+    digests equal the oracle's (size-independent properties)."""
+    import torch
+    S = 0x100000
+    n = 4096
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    d_data = torch.randint(0, 256, (n * S,), dtype=torch.uint8, device="cuda", generator=g)
+    # every 10th chunk copies chunk i-7
+    for i in range(10, n, 10):
+        d_data[i * S:(i + 1) * S] = d_data[(i - 7) * S:(i - 6) * S]
+    ch = np.zeros(n, nydus_gpu.CHUNK_DTYPE)
+    ch["offset"] = np.arange(n, dtype=np.uint64) * S
+    ch["length"] = S
+    d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+    d_out = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    eng = nydus_gpu.Engine(chunk_size=S)
+    try:
+        st = eng.process_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), n,
+                                d_out.data_ptr(), want_stats=True)
+    finally:
+        eng.close()
+    out = d_out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+    dup = np.zeros(n, bool)
+    dup[10::10] = True
+    assert (out["kind"][dup] == nydus_gpu.INTRA).all()
+    assert (out["ref"][dup] == np.nonzero(dup)[0] - 7).all()
+    assert (out["kind"][~dup] == nydus_gpu.NEW).all()
+    assert np.array_equal(out["index"][~dup], np.arange((~dup).sum()))
+    assert np.array_equal(out["uncompressed_offset"][~dup], np.arange((~dup).sum(), dtype=np.uint64) * S)
+    assert st["new_chunks"] == (~dup).sum() and st["intra_chunks"] == dup.sum()
+    rng = np.random.default_rng(0)
+    for i in rng.choice(n, 24, replace=False):
+        blob = d_data[i * S:(i + 1) * S].cpu().numpy().tobytes()
+        assert out["digest"][i].tobytes() == oracle.blake3(blob), i

@@ -1,0 +1,104 @@
+"""CPU-side checks of libnydusgpu.so: the C ABI loads and exports every symbol
+include/nydus_gpu.h declares, the host tar front end matches the oracle and the
+golden chunk lists, and the RAFS v6 chunk-table rules hold.  No compute call
+touches a GPU here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import nydus_gpu
+from nydus_gpu import rafs
+
+from conftest import GOLDEN, ROOT
+
+
+def test_header_symbols_exported():
+    hdr = open(os.path.join(ROOT, "include", "nydus_gpu.h")).read()
+    declared = sorted(set(re.findall(
+        r"^(?:int|void|uint64_t|uint32_t|const char)\s*\*?\s*(ngpu_\w+)\s*\(", hdr, re.M)))
+    assert declared == sorted(nydus_gpu.EXPORTS)
+    L = nydus_gpu.lib()
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.ngpu_abi_version() == 1
+
+
+def test_struct_sizes():
+    assert nydus_gpu.CHUNK_DTYPE.itemsize == 24
+    assert nydus_gpu.RESULT_DTYPE.itemsize == 64
+    assert ctypes.sizeof(nydus_gpu._lib.NgpuConfig) == 32
+
+
+def test_tar_chunks_match_golden_and_oracle(golden_layers, tars, oracle):
+    for case in golden_layers["cases"]:
+        tb = tars[case["layer"]]
+        got = nydus_gpu.tar_chunks(tb, case["chunk_size"])
+        ref = oracle.tar_chunks(tb, case["chunk_size"])
+        exp = [tuple(c) for c in case["chunks"]]
+        assert [tuple(int(x) for x in r) for r in got] == exp, case["layer"]
+        assert got.tobytes() == ref.tobytes()
+
+
+def test_tar_edge_errors():
+    with pytest.raises(nydus_gpu.NgpuError) as e:
+        nydus_gpu.tar_chunks(b"y" * 1024, 0x1000)  # bad checksum
+    assert e.value.code == -4
+    assert len(nydus_gpu.tar_chunks(b"", 0x1000)) == 0
+
+
+def test_tar_truncated(tars):
+    tb = tars["oci_upper"]
+    with pytest.raises(nydus_gpu.NgpuError) as e:
+        nydus_gpu.tar_chunks(tb[: len(tb) // 2], 0x100000)
+    assert e.value.code == -4
+
+
+def test_engine_requires_gpu_here():
+    """No CPU fallback: without a gfx950 device the engine refuses to start."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present; covered by the gpu tests")
+    with pytest.raises(nydus_gpu.NgpuError) as e:
+        nydus_gpu.Engine()
+    assert e.value.code == -6  # ENODEV
+
+
+def test_engine_option_validation():
+    # ChunkSize must be a power of two in [0x1000, 0x1000000] (types.go:76)
+    for bad in (0x800, 0x1001, 0x2000000):
+        with pytest.raises(nydus_gpu.NgpuError) as e:
+            nydus_gpu.Engine(chunk_size=bad)
+        assert e.value.code == -1
+
+
+def test_v6_fixture_layout():
+    """The reference's real v6 bootstrap: chunk table rules our writer follows."""
+    b = rafs.read_v6_from_targz(os.path.join(GOLDEN, "v6-bootstrap-chunk-pos-438272.tar.gz"))
+    assert b["chunk_size"] == 0x100000
+    assert b["chunk_table_offset"] == 0x6B000 and b["chunk_table_size"] == 2515 * 80
+    assert rafs.check_offset_rules(b["chunks"], 4096)
+    assert len(set(bytes(x).hex() for x in b["chunks"]["block_id"])) == 2515
+
+
+def test_chunk_table_writer(oracle, tars):
+    """Chunk table built from oracle results obeys the fixture's rules and
+    round-trips through the bootstrap reader."""
+    tb = tars["alpine_like"]
+    ch = nydus_gpu.tar_chunks(tb, 0x10000)
+    dig = oracle.digest_chunks(tb, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    dec, own = oracle.dedup(dig, ch["length"])
+    res = np.zeros(len(ch), nydus_gpu.RESULT_DTYPE)
+    res["digest"] = dig
+    for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+        res[f] = dec[f]
+    tab = nydus_gpu.chunk_table(ch, res)
+    assert len(tab) == int((dec["kind"] == 0).sum())
+    recs = tab.view(rafs.CHUNK_INFO_DTYPE).reshape(-1)
+    assert rafs.check_offset_rules(recs, 4096)
+    boot = rafs.write_v6_bootstrap(recs, 0x10000)
+    back = rafs.read_v6(boot)
+    assert rafs.canonical(back["chunks"]) == rafs.canonical(recs)
+    assert rafs.detect_fs_version(boot) == "v6"
