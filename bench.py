@@ -37,9 +37,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "nydus-snapshotter_amd"))
 
 MiB = 1 << 20
-# gfx950: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md; the FP32
-# vector peak 157.3 TF = this x 2 FLOP/FMA).  One int32 VALU op per lane/clk.
-PEAK_INT_OPS = 256 * 4 * 32 * 2.4e9
+# gfx950 integer VALU peak: 256 CU x 4 SIMD x 16 lane-ops/clk x 2.4 GHz =
+# 39.3 T int32 ops/s.  Measured, not assumed: a wave64 v_add3/v_xor/v_alignbit
+# takes 4 SIMD cycles (rocprofv3: SQ_INSTS_VALU x 4 / 1024 SIMDs = the whole
+# b3_groups duration at the GRBM clock; DESIGN.md §Roofline, profiles/).
+PEAK_INT_OPS = 256 * 4 * 16 * 2.4e9
 PEAK_HBM = 8.0e12
 OPS_PER_COMPRESSION = 680  # 7 rounds x 8 G x 12 ops + 8 output xors
 

@@ -77,6 +77,9 @@ typedef struct {
 
 /* ngpu_config.flags */
 #define NGPU_FLAG_TIMING 0x1u /* record HIP events around each stage */
+/* Tuning (benchmarks only): bits 8..10 = 1 + BLAKE3 load mode
+ * (bit0 non-temporal loads, bit1 next-block prefetch); 0 = library default. */
+#define NGPU_FLAG_LOAD_MODE_SHIFT 8
 
 /* Per-stage device time of the last process call (NGPU_FLAG_TIMING). */
 typedef struct {

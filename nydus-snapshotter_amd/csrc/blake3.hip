@@ -87,11 +87,18 @@ __device__ __forceinline__ void set_iv(uint32_t cv[8]) {
 }
 
 // Load one message block of `nbytes` (<= 64) little-endian, zero padded.
+// NT: non-temporal (read-once streaming) loads.
+template <bool NT>
 __device__ __forceinline__ void load_block(const uint8_t *p, uint32_t nbytes,
                                            uint32_t m[16]) {
   if (nbytes == 64 && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
-    const u32x4 a = load_nt16(p), b = load_nt16(p + 16);
-    const u32x4 c = load_nt16(p + 32), d = load_nt16(p + 48);
+    u32x4 a, b, c, d;
+    if (NT) {
+      a = load_nt16(p); b = load_nt16(p + 16); c = load_nt16(p + 32); d = load_nt16(p + 48);
+    } else {
+      const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
+      a = q[0]; b = q[1]; c = q[2]; d = q[3];
+    }
     m[0] = a.x; m[1] = a.y; m[2] = a.z; m[3] = a.w;
     m[4] = b.x; m[5] = b.y; m[6] = b.z; m[7] = b.w;
     m[8] = c.x; m[9] = c.y; m[10] = c.z; m[11] = c.w;
@@ -136,7 +143,10 @@ __global__ void b3_fill_group_chunk(const uint64_t *__restrict__ gbase,
   }
 }
 
-template <int D>
+// LM (load mode): bit0 = non-temporal loads, bit1 = prefetch the next 64-B
+// block of the lane's byte stream while the current one is compressed,
+// 4 = diagnostic: no global loads at all (wrong digests; VALU ceiling only).
+template <int D, int LM>
 __global__ __launch_bounds__(256) void b3_groups(
     const uint8_t *__restrict__ data, uint64_t data_len,
     const ngpu_chunk *__restrict__ chunks, uint64_t n,
@@ -163,6 +173,13 @@ __global__ __launch_bounds__(256) void b3_groups(
   const bool root_group = (ng == 1);
   const uint8_t *src = data + ch.offset;
 
+  constexpr bool NT = (LM & 1) != 0, PF = (LM & 2) != 0, NOLOAD = LM == 4;
+  // The lane's bytes [pos, gend) are one contiguous stream of 64-B blocks.
+  const uint32_t gend = min(len, (first + cnt) * kLeaf);
+  uint32_t pos = first * kLeaf;
+  uint32_t m[16];
+  if (PF) load_block<NT>(src + pos, min(64u, gend - pos), m);
+
   uint32_t cur[8];
   uint32_t stk[SD][8];
   uint32_t depth = 0;
@@ -176,21 +193,35 @@ __global__ __launch_bounds__(256) void b3_groups(
       const uint32_t bl = min(64u, llen - (b << 6));
       uint32_t flags = (b == 0 ? CHUNK_START : 0) | (b + 1 == nb ? CHUNK_END : 0);
       if (b + 1 == nb && root_group && nleaves == 1) flags |= ROOT;
-      uint32_t m[16];
-      load_block(src + off + (b << 6), bl, m);
-      compress(cur, m, leaf, bl, flags);
+      if (NOLOAD) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m[i] = pos * 0x9E3779B9u + i;
+        compress(cur, m, leaf, bl, flags);
+        pos += 64;
+      } else if (PF) {
+        uint32_t nx[16];
+        const uint32_t np = pos + 64;
+        if (np < gend) load_block<NT>(src + np, min(64u, gend - np), nx);
+        compress(cur, m, leaf, bl, flags);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m[i] = nx[i];
+        pos = np;
+      } else {
+        load_block<NT>(src + off + (b << 6), bl, m);
+        compress(cur, m, leaf, bl, flags);
+      }
     }
     if (D > 0) {
       const bool last = (k + 1 == cnt);
       const uint32_t nm = last ? depth : (uint32_t)__builtin_ctz(k + 1);
       for (uint32_t q = 0; q < nm; ++q) {
-        uint32_t m[16];
+        uint32_t pm[16];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { m[i] = stk[0][i]; m[8 + i] = cur[i]; }
+        for (int i = 0; i < 8; ++i) { pm[i] = stk[0][i]; pm[8 + i] = cur[i]; }
         const uint32_t flags =
             PARENT | ((last && root_group && q + 1 == nm) ? ROOT : 0);
         set_iv(cur);
-        compress(cur, m, 0, 64, flags);
+        compress(cur, pm, 0, 64, flags);
 #pragma unroll
         for (int l = 0; l + 1 < SD; ++l)
 #pragma unroll
@@ -295,14 +326,27 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
 
 }  // namespace
 
+template <int D, int LM>
+static void launch_groups_lm(const uint8_t *data, uint64_t data_len,
+                             const ngpu_chunk *chunks, uint64_t n, Workspace &ws,
+                             ngpu_result *out, hipStream_t s) {
+  const uint64_t blocks = (ws.cap_g + 255) / 256;
+  hipLaunchKernelGGL((b3_groups<D, LM>), dim3((unsigned)blocks), dim3(256), 0, s, data,
+                     data_len, chunks, n, ws.groups, ws.group_chunk, ws.cap_g,
+                     ws.cv, out, ws.stats + 7);
+}
+
 template <int D>
 static void launch_groups(const uint8_t *data, uint64_t data_len,
                           const ngpu_chunk *chunks, uint64_t n, Workspace &ws,
                           ngpu_result *out, hipStream_t s) {
-  const uint64_t blocks = (ws.cap_g + 255) / 256;
-  hipLaunchKernelGGL(b3_groups<D>, dim3((unsigned)blocks), dim3(256), 0, s, data,
-                     data_len, chunks, n, ws.groups, ws.group_chunk, ws.cap_g,
-                     ws.cv, out, ws.stats + 7);
+  switch (ws.load_mode) {
+    case 0: launch_groups_lm<D, 0>(data, data_len, chunks, n, ws, out, s); break;
+    case 1: launch_groups_lm<D, 1>(data, data_len, chunks, n, ws, out, s); break;
+    case 2: launch_groups_lm<D, 2>(data, data_len, chunks, n, ws, out, s); break;
+    case 3: launch_groups_lm<D, 3>(data, data_len, chunks, n, ws, out, s); break;
+    default: launch_groups_lm<D, 4>(data, data_len, chunks, n, ws, out, s); break;
+  }
 }
 
 // Upper bound on leaf groups for n chunks inside a buffer of data_len bytes.

@@ -165,6 +165,9 @@ int enqueue(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
   int rc = ensure_workspace(e, n, len, D);
   if (rc) return rc;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
+  // tuning override: flags bits 8..10 = 1 + BLAKE3 load mode (0 = default)
+  const uint32_t lm = (e->cfg.flags >> 8) & 7;
+  e->ws.load_mode = lm ? (int)(lm - 1) : 2;
   if (tm) HIP_TRY(e, hipEventRecord(e->ev[0], s));
   HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 16 * sizeof(uint64_t), s));
   if (e->cfg.digester == NGPU_DIGEST_SHA256) {

@@ -159,13 +159,14 @@ class Engine:
 
     def __init__(self, device: int = 0, digester: str = "blake3", chunk_size: int = 0x100000,
                  fs_version: int = 6, leaves_per_lane: int = 0, staging_bytes: int = 0,
-                 timing: bool = False):
+                 timing: bool = False, flags: int = 0):
         L = lib()
         if digester not in DIGESTERS:
             raise ValueError(f"unsupported digester {digester!r}")
         cfg = NgpuConfig(device=device, digester=DIGESTERS[digester], chunk_size=chunk_size,
                          fs_version=fs_version, staging_bytes=staging_bytes,
-                         leaves_per_lane=leaves_per_lane, flags=FLAG_TIMING if timing else 0)
+                         leaves_per_lane=leaves_per_lane,
+                         flags=flags | (FLAG_TIMING if timing else 0))
         h = ctypes.c_void_p()
         rc = L.ngpu_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc:

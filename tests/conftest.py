@@ -2,6 +2,11 @@ import json
 import os
 import sys
 
+# Load torch (and with it torch's bundled HIP runtime, libamdhip64.so.7) before
+# libnydusgpu.so: both resolve the same SONAME, so the first loaded runtime
+# serves the whole process ("One HIP runtime per process").
+import torch  # noqa: F401
+
 import numpy as np
 import pytest
 
