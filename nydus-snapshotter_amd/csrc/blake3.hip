@@ -119,6 +119,12 @@ __device__ __forceinline__ void load_block(const uint8_t *p, uint32_t nbytes,
   }
 }
 
+// A chunk with several leaf groups whose groups all fall in one 256-group
+// window (one b3_groups workgroup) is finished inside that workgroup.
+__device__ __forceinline__ bool tree_in_workgroup(uint64_t base, uint64_t ng) {
+  return ng > 1 && (base >> 8) == ((base + ng - 1) >> 8);
+}
+
 // Leaf groups per chunk (exclusive-scanned afterwards).
 __global__ void b3_count_groups(const ngpu_chunk *__restrict__ chunks,
                                 uint64_t n, int D, uint64_t *__restrict__ groups) {
@@ -146,33 +152,33 @@ __global__ void b3_fill_group_chunk(const uint64_t *__restrict__ gbase,
 // LM (load mode): bit0 = non-temporal loads, bit1 = prefetch the next 64-B
 // block of the lane's byte stream while the current one is compressed,
 // 4 = diagnostic: no global loads at all (wrong digests; VALU ceiling only).
+//
+// Hashes leaf group g.  Returns 0 (no work), 1 (cur = root digest: the
+// chunk fits this group) or 2 (cur = the group's subtree CV).
 template <int D, int LM>
-__global__ __launch_bounds__(256) void b3_groups(
-    const uint8_t *__restrict__ data, uint64_t data_len,
-    const ngpu_chunk *__restrict__ chunks, uint64_t n,
-    const uint64_t *__restrict__ gbase, const uint32_t *__restrict__ gchunk,
-    uint64_t cap_g, uint32_t *__restrict__ cv_out,
-    ngpu_result *__restrict__ out, uint64_t *__restrict__ err) {
+__device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64_t data_len,
+                                        const ngpu_chunk *__restrict__ chunks,
+                                        const uint64_t *__restrict__ gbase,
+                                        const uint32_t *__restrict__ gchunk, uint64_t g,
+                                        uint64_t *__restrict__ err, uint32_t cur[8],
+                                        uint32_t &c, uint64_t &base, uint64_t &ng,
+                                        uint32_t &j) {
   constexpr int SD = D > 0 ? D : 1;
-  const uint64_t total = gbase[n];
-  const uint64_t g = blockIdx.x * 256ull + threadIdx.x;
-  if (g >= total || g >= cap_g) return;
-  const uint32_t c = gchunk[g];
-  const uint64_t base = gbase[c];
-  const uint64_t ng = gbase[c + 1] - base;
-  const uint32_t j = (uint32_t)(g - base);
+  c = gchunk[g];
+  base = gbase[c];
+  ng = gbase[c + 1] - base;
+  j = (uint32_t)(g - base);
   const ngpu_chunk ch = chunks[c];
   const uint32_t len = ch.length;
   if (ch.offset > data_len || len > data_len - ch.offset) {  // bad descriptor
     if (j == 0) atomicAdd((unsigned long long *)err, 1ull);
-    return;
+    return 0;
   }
   const uint32_t nleaves = len == 0 ? 1 : (len + kLeaf - 1) / kLeaf;
   const uint32_t first = j << D;
   const uint32_t cnt = min(1u << D, nleaves - first);
   const bool root_group = (ng == 1);
   const uint8_t *src = data + ch.offset;
-
   constexpr bool NT = (LM & 1) != 0, PF = (LM & 2) != 0, NOLOAD = LM == 4;
   // The lane's bytes [pos, gend) are one contiguous stream of 64-B blocks.
   const uint32_t gend = min(len, (first + cnt) * kLeaf);
@@ -180,7 +186,6 @@ __global__ __launch_bounds__(256) void b3_groups(
   uint32_t m[16];
   if (PF) load_block<NT>(src + pos, min(64u, gend - pos), m);
 
-  uint32_t cur[8];
   uint32_t stk[SD][8];
   uint32_t depth = 0;
   for (uint32_t k = 0; k < cnt; ++k) {
@@ -239,14 +244,76 @@ __global__ __launch_bounds__(256) void b3_groups(
       }
     }
   }
-  if (root_group) {
+  return root_group ? 1 : 2;
+}
+
+template <int D, int LM>
+__global__ __launch_bounds__(256) void b3_groups(
+    const uint8_t *__restrict__ data, uint64_t data_len,
+    const ngpu_chunk *__restrict__ chunks, uint64_t n,
+    const uint64_t *__restrict__ gbase, const uint32_t *__restrict__ gchunk,
+    uint64_t cap_g, uint32_t *__restrict__ cv_out,
+    ngpu_result *__restrict__ out, uint64_t *__restrict__ err) {
+  __shared__ uint32_t lcv[256 * 8];
+  const uint64_t total = gbase[n];
+  const uint64_t g0 = blockIdx.x * 256ull;
+  const uint64_t g = g0 + threadIdx.x;
+  uint32_t cur[8], c = 0, j = 0;
+  uint64_t base = 0, ng = 0;
+  const int st = (g < total && g < cap_g)
+                     ? group_cv<D, LM>(data, data_len, chunks, gbase, gchunk, g, err, cur, c,
+                                       base, ng, j)
+                     : 0;
+  if (st == 1) {
     uint4 *d = reinterpret_cast<uint4 *>(out[c].digest);
     d[0] = make_uint4(cur[0], cur[1], cur[2], cur[3]);
     d[1] = make_uint4(cur[4], cur[5], cur[6], cur[7]);
-  } else {
+  }
+  // Chunks whose groups all sit in this workgroup finish here: the upper
+  // levels of their tree are reduced in LDS (pairwise, odd tail promoted).
+  // Others publish their group CV for b3_tree.
+  const bool inwg = st == 2 && tree_in_workgroup(base, ng);
+  if (st == 2 && !inwg) {
     uint4 *d = reinterpret_cast<uint4 *>(cv_out + g * 8);
     d[0] = make_uint4(cur[0], cur[1], cur[2], cur[3]);
     d[1] = make_uint4(cur[4], cur[5], cur[6], cur[7]);
+  }
+  if (!__syncthreads_or(inwg)) return;
+  const uint32_t o = (uint32_t)(base - g0);  // chunk's first slot in lcv
+  uint32_t k = inwg ? (uint32_t)ng : 1;
+  if (inwg) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lcv[8 * threadIdx.x + i] = cur[i];
+  }
+  for (;;) {
+    const bool active = k > 1;
+    if (!__syncthreads_or(active)) break;
+    uint32_t r[8];
+    const uint32_t p = k >> 1;
+    const bool comp = active && j < p;
+    const bool odd = active && (k & 1) && j == p;
+    if (comp) {
+      uint32_t m[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m[i] = lcv[8 * (o + 2 * j) + i];
+      set_iv(r);
+      compress(r, m, 0, 64, PARENT | (k == 2 ? ROOT : 0));
+    }
+    if (odd) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] = lcv[8 * (o + k - 1) + i];
+    }
+    __syncthreads();
+    if (comp || odd) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lcv[8 * (o + j) + i] = r[i];
+    }
+    if (comp && k == 2) {
+      uint4 *d = reinterpret_cast<uint4 *>(out[c].digest);
+      d[0] = make_uint4(r[0], r[1], r[2], r[3]);
+      d[1] = make_uint4(r[4], r[5], r[6], r[7]);
+    }
+    k = active ? p + (k & 1) : 1;
   }
 }
 
@@ -262,7 +329,7 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
   for (uint64_t c = blockIdx.x; c < n; c += gridDim.x) {
     const uint64_t base = gbase[c];
     uint64_t k = gbase[c + 1] - base;
-    if (k <= 1 || base + k > cap_g) continue;
+    if (k <= 1 || base + k > cap_g || tree_in_workgroup(base, k)) continue;
     uint32_t *a = cv + base * 8;
     for (;;) {
       const bool final_pass = k <= kTile;
@@ -380,7 +447,7 @@ void launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
   }
   if (ev_end) (void)hipEventRecord(ev_end, s);
   {
-    uint64_t blocks = n < 65536 ? n : 65536;
+    uint64_t blocks = n < 2048 ? n : 2048;
     hipLaunchKernelGGL(b3_tree, dim3((unsigned)blocks), dim3(kTreeThreads), 0, s,
                        ws.groups, n, ws.cap_g, ws.cv, out);
   }

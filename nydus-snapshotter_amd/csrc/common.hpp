@@ -84,7 +84,7 @@ struct Workspace {
   uint32_t *blob_real = nullptr;
   uint64_t *stats = nullptr;      // device-side counters (ngpu_layer_stats)
   uint64_t cap_n = 0, cap_g = 0, cap_blobs = 0;
-  int load_mode = 2;              // b3_groups load mode (see blake3.hip)
+  int load_mode = 0;              // b3_groups load mode (see blake3.hip)
 };
 
 }  // namespace ngpu

@@ -93,14 +93,13 @@ int pick_group_log2(const ngpu_engine *e, uint64_t data_len) {
     case 16: return 4;
     default: break;
   }
-  // auto: enough lanes to fill 256 CUs several times, but at most the
-  // chunk's own leaf count (whole chunk per lane for small chunk sizes).
-  const uint64_t leaves = data_len / kLeaf + 1;
+  // auto: up to 8 leaves per lane (tuned: profiles/r1/tune_*) (never more than a chunk holds), fewer
+  // when the layer is too small to give >= 4 waves per SIMD at that size.
   int D = 0;
-  while (D < 3 && (leaves >> (D + 1)) >= (1ull << 20)) ++D;
-  int cap = 0;
-  while (cap < 4 && (1ull << (cap + 1)) * kLeaf <= e->cfg.chunk_size) ++cap;
-  return D < cap ? D : cap;
+  while (D < 3 && (2ull << D) * kLeaf <= e->cfg.chunk_size) ++D;
+  const uint64_t leaves = data_len / kLeaf + 1;
+  while (D > 0 && (leaves >> D) < (1ull << 18)) --D;
+  return D;
 }
 
 int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D) {
@@ -167,7 +166,7 @@ int enqueue(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   // tuning override: flags bits 8..10 = 1 + BLAKE3 load mode (0 = default)
   const uint32_t lm = (e->cfg.flags >> 8) & 7;
-  e->ws.load_mode = lm ? (int)(lm - 1) : 2;
+  e->ws.load_mode = lm ? (int)(lm - 1) : 0;
   if (tm) HIP_TRY(e, hipEventRecord(e->ev[0], s));
   HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 16 * sizeof(uint64_t), s));
   if (e->cfg.digester == NGPU_DIGEST_SHA256) {

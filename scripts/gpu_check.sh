@@ -25,13 +25,12 @@ ok $? smoke
 timeout -k 10 600 python bench.py --steps 10 --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
 ok $? bench
 cat "$OUT/bench.json"
-if [ "${2:-}" != "quick" ]; then
-  for L in 1 2 4 8 16; do
-    timeout -k 10 300 python bench.py --steps 5 --warmup 2 --lanes $L --no-cpu-baseline > "$OUT/bench_lanes$L.json" 2>> "$OUT/bench.err"
-    ok $? bench-lanes$L
-  done
-fi
+for W in c3 c5; do
+  timeout -k 10 600 python bench.py --workload $W --steps 5 --warmup 2 > "$OUT/bench_$W.json" 2>> "$OUT/bench.err"
+  ok $? bench-$W
+  cat "$OUT/bench_$W.json"
+done
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1
 ok $? rocprof
 find "$OUT/prof" -name '*stats*' | head
