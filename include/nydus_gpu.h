@@ -176,6 +176,42 @@ int ngpu_process_device(ngpu_engine *eng, const void *d_data, uint64_t len,
                         ngpu_result *d_out, void *stream,
                         ngpu_layer_stats *stats);
 
+/* ---- split stages (device pointers, async on `stream`) -------------------
+ * For callers that route dict probes themselves, e.g. a chunk dict
+ * partitioned across GPUs by digest prefix:
+ *   ngpu_digest_device     -> digests only (d_out[i].digest);
+ *   ngpu_dict_probe_device -> look digests up in THIS engine's dict;
+ *   ngpu_dedup_device      -> dedup decisions from digests + given dict hits.
+ * ngpu_process_device == digest + dedup against the engine's own dict. */
+typedef struct {
+  uint32_t entry;  /* dict entry id (chunk-table order) or 0xFFFFFFFF: miss */
+  uint32_t index;  /* the entry's RAFS chunk index */
+  uint32_t blob;   /* the entry's inner blob index */
+  uint32_t usize;  /* the entry's uncompressed size (0 = any) */
+} ngpu_dict_hit;
+
+int ngpu_digest_device(ngpu_engine *eng, const void *d_data, uint64_t len,
+                       const ngpu_chunk *d_chunks, uint64_t n,
+                       ngpu_result *d_out, void *stream);
+/* d_digests: n digests at byte stride `stride` (32 for packed, 64 to read
+ * ngpu_result.digest in place).  No size rule is applied here: the hit
+ * carries usize and the requester's dedup applies it. */
+int ngpu_dict_probe_device(ngpu_engine *eng, const uint8_t *d_digests,
+                           uint64_t stride, uint64_t n,
+                           ngpu_dict_hit *d_hits, void *stream);
+/* d_hits: per-chunk dict hits (NULL: probe this engine's dict).
+ * n_dict_blobs: number of inner blobs of the (global) chunk dict; 0 = use
+ * this engine's dict.  stats as in ngpu_process_device. */
+int ngpu_dedup_device(ngpu_engine *eng, const ngpu_chunk *d_chunks, uint64_t n,
+                      ngpu_result *d_out, const ngpu_dict_hit *d_hits,
+                      uint32_t n_dict_blobs, void *stream,
+                      ngpu_layer_stats *stats);
+/* Build the dict from device-resident arrays (entry order = table order). */
+int ngpu_dict_load_device(ngpu_engine *eng, const uint8_t *d_digests,
+                          const uint32_t *d_usize, const uint32_t *d_blob_index,
+                          const uint32_t *d_chunk_index, uint64_t n,
+                          uint32_t n_blobs);
+
 /* Whole tar layer in host memory -> chunk list + results (tar parse on the
  * host, digest/dedup on the GPU).  *chunks_out / *results_out are allocated
  * with malloc and must be released with ngpu_free_host. */

@@ -63,9 +63,13 @@ struct DictDevice {
 // dedup.hip
 void launch_dict_build(const uint8_t *digests, uint64_t m, uint64_t *table,
                        uint64_t cap, hipStream_t s);
+// hits == nullptr: probe `dict`; otherwise use the given per-chunk hits.
+// n_blobs: inner blobs of the (global) dict.
 void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
-                  uint32_t align, Workspace &ws, ngpu_result *out,
-                  hipStream_t s);
+                  const ngpu_dict_hit *hits, uint32_t n_blobs, uint32_t align,
+                  Workspace &ws, ngpu_result *out, hipStream_t s);
+void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
+                       const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s);
 void launch_scan_u64(uint64_t *data, uint64_t n, uint64_t *tmp,
                      hipStream_t s);  // exclusive, in place, n+1 entries used
 uint64_t scan_tmp_words(uint64_t n);

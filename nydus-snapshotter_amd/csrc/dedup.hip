@@ -87,30 +87,50 @@ __global__ void dict_insert(const uint8_t *__restrict__ digests, uint64_t m,
   if (e < m) ht_insert_min<32>(table, mask, digests, (uint32_t)e);
 }
 
-// Stage 1: dict probe + reset of the per-chunk state.
+// Look n digests (byte stride `stride`) up in the dict.
+__global__ void dict_probe_records(const uint8_t *__restrict__ digests, uint64_t stride,
+                                   uint64_t n, DictDevice dict,
+                                   ngpu_dict_hit *__restrict__ hits) {
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  ngpu_dict_hit h{kNone, 0, 0, 0};
+  if (dict.m) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(digests + q * stride);
+    const uint4 a = p[0], b = p[1];
+    const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const uint32_t e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
+    if (e != kNone) h = ngpu_dict_hit{e, dict.index[e], dict.blob[e], dict.usize[e]};
+  }
+  hits[q] = h;
+}
+
+// Stage 1: dict decision (from given hits, or by probing the local dict) +
+// reset of the per-chunk state.
 __global__ void dedup_probe(const ngpu_chunk *__restrict__ chunks, uint64_t n,
-                            DictDevice dict, ngpu_result *__restrict__ out,
+                            DictDevice dict, const ngpu_dict_hit *__restrict__ hits,
+                            ngpu_result *__restrict__ out,
                             uint64_t *__restrict__ newflag,
-                            uint32_t *__restrict__ blob_first) {
+                            uint32_t *__restrict__ blob_first, uint32_t n_blobs) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (c >= n) return;
   ngpu_result &r = out[c];
   uint32_t kind = NGPU_NEW;
-  if (dict.m) {
+  ngpu_dict_hit h{kNone, 0, 0, 0};
+  if (hits) {
+    h = hits[c];
+  } else if (dict.m) {
     uint32_t d[8];
     load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
     const uint32_t e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
-    if (e != kNone) {
-      const uint32_t us = dict.usize[e];
-      if (us == 0 || us == chunks[c].length) {
-        kind = NGPU_DICT;
-        r.ref = e;
-        r.index = dict.index[e];
-        r.blob_index = dict.blob[e];  // inner index; remapped in finalize
-        r.uncompressed_offset = 0;
-        atomicMin(blob_first + dict.blob[e], (uint32_t)c);
-      }
-    }
+    if (e != kNone) h = ngpu_dict_hit{e, dict.index[e], dict.blob[e], dict.usize[e]};
+  }
+  if (h.entry != kNone && (h.usize == 0 || h.usize == chunks[c].length) && h.blob < n_blobs) {
+    kind = NGPU_DICT;
+    r.ref = h.entry;
+    r.index = h.index;
+    r.blob_index = h.blob;  // inner index; remapped in finalize
+    r.uncompressed_offset = 0;
+    atomicMin(blob_first + h.blob, (uint32_t)c);
   }
   r.kind = kind;
   r.reserved = 0;
@@ -295,20 +315,28 @@ void launch_dict_build(const uint8_t *digests, uint64_t m, uint64_t *table,
                      table, cap - 1);
 }
 
+void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
+                       const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(dict_probe_records, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     digests, stride, n, dict, hits);
+}
+
 void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
-                  uint32_t align, Workspace &ws, ngpu_result *out, hipStream_t s) {
-  const uint32_t nbo = dict.n_blobs + 1;  // dict blobs + own blob (last slot)
+                  const ngpu_dict_hit *hits, uint32_t n_blobs, uint32_t align,
+                  Workspace &ws, ngpu_result *out, hipStream_t s) {
+  const uint32_t nbo = n_blobs + 1;  // dict blobs + own blob (last slot)
   hipMemsetAsync(ws.blob_first, 0xFF, sizeof(uint32_t) * nbo, s);
   if (n) {
     hipMemsetAsync(ws.intra, 0xFF, ws.intra_cap * sizeof(uint64_t), s);
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(dedup_probe, dim3(blocks), dim3(256), 0, s, chunks, n, dict, out,
-                       ws.newflag, ws.blob_first);
+    hipLaunchKernelGGL(dedup_probe, dim3(blocks), dim3(256), 0, s, chunks, n, dict, hits, out,
+                       ws.newflag, ws.blob_first, n_blobs);
     hipLaunchKernelGGL(dedup_insert, dim3(blocks), dim3(256), 0, s, out, n, ws.intra,
                        ws.intra_cap - 1);
     hipLaunchKernelGGL(dedup_resolve, dim3(blocks), dim3(256), 0, s, chunks, n, ws.intra,
                        ws.intra_cap - 1, out, align, ws.newflag, ws.uoff,
-                       ws.blob_first + dict.n_blobs);
+                       ws.blob_first + n_blobs);
   } else {
     hipMemsetAsync(ws.newflag, 0, sizeof(uint64_t), s);
     hipMemsetAsync(ws.uoff, 0, sizeof(uint64_t), s);
@@ -319,7 +347,7 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                      ws.stats);
   const unsigned blocks = (unsigned)((n + 255) / 256) + 1;
   hipLaunchKernelGGL(dedup_finalize, dim3(blocks), dim3(256), 0, s, chunks, n, ws.newflag,
-                     ws.uoff, ws.blob_real, dict.n_blobs, out, ws.stats);
+                     ws.uoff, ws.blob_real, n_blobs, out, ws.stats);
 }
 
 }  // namespace ngpu

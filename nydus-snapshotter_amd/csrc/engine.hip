@@ -102,7 +102,8 @@ int pick_group_log2(const ngpu_engine *e, uint64_t data_len) {
   return D;
 }
 
-int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D) {
+int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
+                     uint32_t n_blobs) {
   Workspace &ws = e->ws;
   if (n + 1 > ws.cap_n || !ws.groups) {
     uint64_t cn = n + 1 < 4096 ? 4096 : n + 1;
@@ -122,7 +123,7 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D) {
     uint64_t c = 0;
     if (grow(e, &ws.stats, c, 16)) return NGPU_ENOMEM;
   }
-  const uint64_t nb = e->dict.n_blobs + 1;
+  const uint64_t nb = (uint64_t)n_blobs + 1;
   if (nb > ws.cap_blobs || !ws.blob_first) {
     uint64_t c0 = 0, c1 = 0;
     if (ws.blob_first) hipFree(ws.blob_first), ws.blob_first = nullptr;
@@ -157,11 +158,12 @@ void free_dict(ngpu_engine *e) {
   e->dict = DictDevice{};
 }
 
-int enqueue(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
-            const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
-            hipStream_t s) {
+// Digest stage: resets the layer stats, runs the digest kernels.
+int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
+                   const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+                   hipStream_t s) {
   const int D = pick_group_log2(e, len);
-  int rc = ensure_workspace(e, n, len, D);
+  int rc = ensure_workspace(e, n, len, D, e->dict.n_blobs);
   if (rc) return rc;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   // tuning override: flags bits 8..10 = 1 + BLAKE3 load mode (0 = default)
@@ -178,13 +180,36 @@ int enqueue(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
                   tm ? e->ev[2] : nullptr);
   }
   if (tm) HIP_TRY(e, hipEventRecord(e->ev[3], s));
+  HIP_TRY(e, hipGetLastError());
+  e->last_D = D;
+  return 0;
+}
+
+// Dedup stage: dict decisions (given hits or the engine's dict), intra-layer
+// dedup, NEW indices / offsets, blob order, stats.
+int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+                  const ngpu_dict_hit *d_hits, uint32_t n_blobs, hipStream_t s) {
+  if (!d_hits) n_blobs = e->dict.n_blobs;
+  int rc = ensure_workspace(e, n, 0, 0, n_blobs);
+  if (rc) return rc;
+  const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   const uint32_t align = e->cfg.fs_version == 6 ? 4096u : 1u;
-  launch_dedup(d_chunks, n, e->dict, align, e->ws, d_out, s);
+  // reset the dedup counters; stats[7] (bad descriptors) belongs to the digest stage
+  HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 7 * sizeof(uint64_t), s));
+  HIP_TRY(e, hipMemsetAsync(e->ws.stats + 8, 0, 8 * sizeof(uint64_t), s));
+  launch_dedup(d_chunks, n, e->dict, d_hits, n_blobs, align, e->ws, d_out, s);
   if (tm) HIP_TRY(e, hipEventRecord(e->ev[4], s));
   HIP_TRY(e, hipGetLastError());
   e->timed = tm && n > 0;
-  e->last_D = D;
   return 0;
+}
+
+int enqueue(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
+            const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+            hipStream_t s) {
+  int rc = enqueue_digest(e, d_data, len, d_chunks, n, d_out, s);
+  if (rc) return rc;
+  return enqueue_dedup(e, d_chunks, n, d_out, nullptr, 0, s);
 }
 
 int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st) {
@@ -337,6 +362,83 @@ int ngpu_dict_load(ngpu_engine *e, const uint8_t *digests, const uint32_t *usize
   e->dict.mask = cap - 1;
   e->dict.m = n;
   e->dict.n_blobs = nb;
+  return 0;
+}
+
+int ngpu_dict_load_device(ngpu_engine *e, const uint8_t *d_digests, const uint32_t *d_usize,
+                          const uint32_t *d_blob_index, const uint32_t *d_chunk_index,
+                          uint64_t n, uint32_t n_blobs) {
+  if (!e || (n && (!d_digests || !d_usize || !d_blob_index))) return NGPU_EINVAL;
+  if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "dict too large");
+  if (n_blobs == 0 || n_blobs > (1u << 20)) return fail(e, NGPU_EINVAL, "bad n_blobs %u", n_blobs);
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  HIP_TRY(e, hipStreamSynchronize(e->stream));
+  free_dict(e);
+  if (n == 0) return 0;
+  const uint64_t cap = next_pow2(2 * n + 16);
+  HIP_TRY(e, hipMalloc((void **)&e->d_dict_digest, n * 32));
+  HIP_TRY(e, hipMalloc((void **)&e->d_dict_usize, n * 4));
+  HIP_TRY(e, hipMalloc((void **)&e->d_dict_blob, n * 4));
+  HIP_TRY(e, hipMalloc((void **)&e->d_dict_index, n * 4));
+  HIP_TRY(e, hipMalloc((void **)&e->d_dict_table, cap * 8));
+  const hipMemcpyKind k = hipMemcpyDeviceToDevice;
+  HIP_TRY(e, hipMemcpyAsync(e->d_dict_digest, d_digests, n * 32, k, e->stream));
+  HIP_TRY(e, hipMemcpyAsync(e->d_dict_usize, d_usize, n * 4, k, e->stream));
+  HIP_TRY(e, hipMemcpyAsync(e->d_dict_blob, d_blob_index, n * 4, k, e->stream));
+  if (d_chunk_index)
+    HIP_TRY(e, hipMemcpyAsync(e->d_dict_index, d_chunk_index, n * 4, k, e->stream));
+  else
+    HIP_TRY(e, hipMemsetAsync(e->d_dict_index, 0, n * 4, e->stream));
+  launch_dict_build(e->d_dict_digest, n, e->d_dict_table, cap, e->stream);
+  HIP_TRY(e, hipGetLastError());
+  HIP_TRY(e, hipStreamSynchronize(e->stream));
+  e->dict.digests = e->d_dict_digest;
+  e->dict.usize = e->d_dict_usize;
+  e->dict.blob = e->d_dict_blob;
+  e->dict.index = e->d_dict_index;
+  e->dict.table = e->d_dict_table;
+  e->dict.mask = cap - 1;
+  e->dict.m = n;
+  e->dict.n_blobs = n_blobs;
+  return 0;
+}
+
+int ngpu_digest_device(ngpu_engine *e, const void *d_data, uint64_t len,
+                       const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+                       void *stream) {
+  if (!e || (n && (!d_data || !d_chunks || !d_out))) return NGPU_EINVAL;
+  if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too many chunks in one call");
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  return enqueue_digest(e, (const uint8_t *)d_data, len, d_chunks, n, d_out,
+                        stream ? (hipStream_t)stream : e->stream);
+}
+
+int ngpu_dict_probe_device(ngpu_engine *e, const uint8_t *d_digests, uint64_t stride,
+                           uint64_t n, ngpu_dict_hit *d_hits, void *stream) {
+  if (!e || (n && (!d_digests || !d_hits)) || stride < 32 || (stride & 15))
+    return NGPU_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  launch_dict_probe(d_digests, stride, n, e->dict, d_hits,
+                    stream ? (hipStream_t)stream : e->stream);
+  HIP_TRY(e, hipGetLastError());
+  return 0;
+}
+
+int ngpu_dedup_device(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n,
+                      ngpu_result *d_out, const ngpu_dict_hit *d_hits, uint32_t n_dict_blobs,
+                      void *stream, ngpu_layer_stats *stats) {
+  if (!e || (n && (!d_chunks || !d_out))) return NGPU_EINVAL;
+  if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too many chunks in one call");
+  if (d_hits && n_dict_blobs == 0) n_dict_blobs = e->dict.n_blobs ? e->dict.n_blobs : 1;
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  int rc = enqueue_dedup(e, d_chunks, n, d_out, d_hits, n_dict_blobs, s);
+  if (rc) return rc;
+  if (stats) return read_stats(e, s, stats);
   return 0;
 }
 

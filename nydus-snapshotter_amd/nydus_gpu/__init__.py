@@ -4,8 +4,8 @@ Python view of libnydusgpu.so (C ABI in include/nydus_gpu.h).  The engine
 replaces the digest/dedup stage that pkg/converter hands to
 `nydus-image create` (pkg/converter/tool/builder.go:148-178).
 """
-from ._lib import (CHUNK_DTYPE, DICT, DIGESTERS, EXPORTS, INTRA, KIND_NAMES, NEW,  # noqa: F401
-                   RESULT_DTYPE, Engine, NgpuError, chunk_table, lib, tar_chunks)
+from ._lib import (CHUNK_DTYPE, DICT, DIGESTERS, EXPORTS, HIT_DTYPE, INTRA, KIND_NAMES, MISS,  # noqa: F401
+                   NEW, RESULT_DTYPE, Engine, NgpuError, chunk_table, lib, tar_chunks)
 
 __all__ = ["Engine", "NgpuError", "tar_chunks", "chunk_table", "lib", "CHUNK_DTYPE",
-           "RESULT_DTYPE", "NEW", "INTRA", "DICT", "KIND_NAMES", "DIGESTERS", "EXPORTS"]
+           "RESULT_DTYPE", "HIT_DTYPE", "MISS", "NEW", "INTRA", "DICT", "KIND_NAMES", "DIGESTERS", "EXPORTS"]

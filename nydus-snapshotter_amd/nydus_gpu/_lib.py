@@ -33,7 +33,11 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_device_count", "ngpu_alloc_pinned", "ngpu_free_pinned", "ngpu_dict_load",
            "ngpu_dict_load_bootstrap", "ngpu_dict_clear", "ngpu_dict_size", "ngpu_tar_chunks",
            "ngpu_process", "ngpu_process_device", "ngpu_pack_tar", "ngpu_free_host",
-           "ngpu_chunk_table", "ngpu_last_timing"]
+           "ngpu_chunk_table", "ngpu_last_timing", "ngpu_digest_device",
+           "ngpu_dict_probe_device", "ngpu_dedup_device", "ngpu_dict_load_device"]
+
+HIT_DTYPE = np.dtype([("entry", "<u4"), ("index", "<u4"), ("blob", "<u4"), ("usize", "<u4")])
+MISS = 0xFFFFFFFF
 
 
 class NgpuConfig(ctypes.Structure):
@@ -107,6 +111,10 @@ def lib():
     L.ngpu_free_host.restype = None
     L.ngpu_chunk_table.argtypes = [vp, vp, u64, vp, u64, pu64]
     L.ngpu_last_timing.argtypes = [vp, ctypes.POINTER(NgpuTiming)]
+    L.ngpu_digest_device.argtypes = [vp, vp, u64, vp, u64, vp, vp]
+    L.ngpu_dict_probe_device.argtypes = [vp, vp, u64, u64, vp, vp]
+    L.ngpu_dedup_device.argtypes = [vp, vp, u64, vp, vp, u32, vp, ctypes.POINTER(NgpuLayerStats)]
+    L.ngpu_dict_load_device.argtypes = [vp, vp, vp, vp, vp, u64, u32]
     _lib = L
     return L
 
@@ -233,6 +241,34 @@ class Engine:
                                               ctypes.byref(st) if want_stats else None),
                     "process_device")
         return st.as_dict() if want_stats else None
+
+    # ---- split stages, device pointers (ints) ---------------------------------
+    @staticmethod
+    def _vp(x):
+        return ctypes.c_void_p(x) if x else None
+
+    def digest_device(self, d_data: int, length: int, d_chunks: int, n: int, d_out: int,
+                      stream: int = 0):
+        self._check(lib().ngpu_digest_device(self._h, self._vp(d_data), length, self._vp(d_chunks),
+                                             n, self._vp(d_out), self._vp(stream)), "digest_device")
+
+    def dict_probe_device(self, d_digests: int, stride: int, n: int, d_hits: int, stream: int = 0):
+        self._check(lib().ngpu_dict_probe_device(self._h, self._vp(d_digests), stride, n,
+                                                 self._vp(d_hits), self._vp(stream)), "dict_probe_device")
+
+    def dedup_device(self, d_chunks: int, n: int, d_out: int, d_hits: int = 0, n_dict_blobs: int = 0,
+                     stream: int = 0, want_stats: bool = False):
+        st = NgpuLayerStats()
+        self._check(lib().ngpu_dedup_device(self._h, self._vp(d_chunks), n, self._vp(d_out),
+                                            self._vp(d_hits), n_dict_blobs, self._vp(stream),
+                                            ctypes.byref(st) if want_stats else None), "dedup_device")
+        return st.as_dict() if want_stats else None
+
+    def dict_load_device(self, d_digests: int, d_usize: int, d_blob: int, d_index: int, n: int,
+                         n_blobs: int):
+        self._check(lib().ngpu_dict_load_device(self._h, self._vp(d_digests), self._vp(d_usize),
+                                                self._vp(d_blob), self._vp(d_index), n, n_blobs),
+                    "dict_load_device")
 
     def last_timing(self) -> dict:
         t = NgpuTiming()

@@ -1,0 +1,143 @@
+"""Multi-GPU chunk dict: partitioned by digest prefix, probed through an
+all-to-all exchange.
+
+One process per GPU (torchrun); backend "nccl" is RCCL over xGMI on the GPU
+node, "gloo" on CPU for tests.  Layers are sharded over ranks by the caller
+(each rank packs its own layers, no collective); the only data-path exchange
+is the dict probe:
+
+  1. each rank digests its chunks (engine.digest_device);
+  2. owner(d) = top bits of the digest's first two bytes
+     ((d0 << 8 | d1) * world >> 16; for power-of-two worlds the top
+     log2(world) bits of byte 0);
+  3. records are sorted by owner and exchanged with one all_to_all_single
+     (32 B per query out, 16 B per hit back) — payload is tiny
+     (1 MiB chunks: 16384 x 48 B per 16 GiB layer), so the exchange is
+     latency-bound, not link-bound;
+  4. the owner probes its partition (engine.dict_probe_device) and returns
+     ngpu_dict_hit records with GLOBAL entry ids (chunk-table order);
+  5. each rank runs its own layer dedup with those hits (engine.dedup_device).
+
+A partition keeps its entries in global table order, so "first entry wins"
+for duplicate digests is preserved: duplicates share a digest, hence an owner.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+MISS = 0xFFFFFFFF
+
+
+def owner_of(digests: torch.Tensor, world: int) -> torch.Tensor:
+    """digests: (n, 32) uint8 -> (n,) int64 owner rank."""
+    hi = digests[:, 0].to(torch.int64) << 8 | digests[:, 1].to(torch.int64)
+    return (hi * world) >> 16
+
+
+class ShardedChunkDict:
+    """Digest-prefix partition of a chunk dict across ranks.
+
+    probe_fn(local_digests (m, 32) uint8) -> (m, 4) int32 hits in LOCAL entry
+    ids ([entry, index, blob, usize], entry == -1 for a miss).  On the GPU
+    path this is ``engine_probe_fn(engine)``.
+    """
+
+    def __init__(self, rank: int, world: int, group=None, comm_device=None):
+        """comm_device: device the all-to-all runs on (None = the tensors' own;
+        "cpu" when the process group is gloo and the data lives on a GPU)."""
+        self.rank, self.world, self.group = rank, world, group
+        self.comm_device = comm_device
+        self.local_to_global: Optional[torch.Tensor] = None
+        self.n_blobs = 0
+        self.probe_fn: Optional[Callable[[torch.Tensor], torch.Tensor]] = None
+
+    def partition(self, digests: torch.Tensor):
+        """Stable selection of the entries this rank owns (global table order
+        preserved) -> (index tensor of owned global entry ids)."""
+        own = owner_of(digests, self.world) == self.rank
+        return torch.nonzero(own, as_tuple=False).flatten()
+
+    def load(self, digests, usize, blob, index, n_blobs: int, load_fn):
+        """Keep this rank's partition.  load_fn(d, us, bl, ix) builds the local
+        table from the owned rows (engine.dict_load_device on the GPU)."""
+        ids = self.partition(digests)
+        self.local_to_global = ids.to(torch.int64)
+        self.n_blobs = n_blobs
+        load_fn(digests[ids].contiguous(), usize[ids].contiguous(), blob[ids].contiguous(),
+                index[ids].contiguous())
+        return int(ids.numel())
+
+    def _a2a(self, out, inp, out_splits, in_splits):
+        import torch.distributed as dist
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
+    def probe(self, digests: torch.Tensor) -> torch.Tensor:
+        """digests (n, 32) uint8 -> hits (n, 4) int32 with global entry ids."""
+        n = digests.shape[0]
+        dev = digests.device
+        if self.world == 1:
+            return self._local(digests)
+        cdev = torch.device(self.comm_device) if self.comm_device else dev
+        own = owner_of(digests, self.world)
+        order = torch.argsort(own, stable=True)
+        send = digests[order].contiguous().to(cdev)
+        counts = torch.bincount(own, minlength=self.world).to(torch.int64).to(cdev)
+        rcounts = torch.empty_like(counts)
+        self._a2a(rcounts, counts, None, None)
+        in_splits = counts.tolist()
+        out_splits = rcounts.tolist()
+        recv = torch.empty((sum(out_splits), 32), dtype=torch.uint8, device=cdev)
+        self._a2a(recv, send, out_splits, in_splits)
+        hits = self._local(recv.to(dev)).to(cdev)  # (sum(out_splits), 4)
+        back = torch.empty((n, 4), dtype=torch.int32, device=cdev)
+        self._a2a(back, hits.contiguous(), in_splits, out_splits)
+        res = torch.empty((n, 4), dtype=torch.int32, device=dev)
+        res[order] = back.to(dev)
+        return res
+
+    def _local(self, digests: torch.Tensor) -> torch.Tensor:
+        if digests.shape[0] == 0 or self.local_to_global is None or self.local_to_global.numel() == 0:
+            h = torch.zeros((digests.shape[0], 4), dtype=torch.int32, device=digests.device)
+            h[:, 0] = -1
+            return h
+        h = self.probe_fn(digests).clone()
+        hit = h[:, 0] != -1
+        loc = h[:, 0].to(torch.int64)
+        glob = torch.where(hit, self.local_to_global.to(digests.device)[torch.where(hit, loc, 0)],
+                           torch.full_like(loc, -1))
+        h[:, 0] = glob.to(torch.int32)
+        return h
+
+
+def engine_probe_fn(engine, stream_fn=None):
+    """Probe through the C ABI (ngpu_dict_probe_device) on device tensors."""
+
+    def probe(d: torch.Tensor) -> torch.Tensor:
+        d = d.contiguous()
+        hits = torch.empty((d.shape[0], 4), dtype=torch.int32, device=d.device)
+        s = stream_fn() if stream_fn else torch.cuda.current_stream().cuda_stream
+        engine.dict_probe_device(d.data_ptr(), 32, d.shape[0], hits.data_ptr(), stream=s)
+        return hits
+    return probe
+
+
+def engine_load_fn(engine, n_blobs: int):
+    def load(d, us, bl, ix):
+        torch.cuda.current_stream().synchronize()
+        engine.dict_load_device(d.data_ptr(), us.data_ptr(), bl.data_ptr(), ix.data_ptr(),
+                                d.shape[0], n_blobs)
+    return load
+
+
+def sharded_process(engine, sdict: ShardedChunkDict, d_data: torch.Tensor, d_chunks: torch.Tensor,
+                    n: int, d_out: torch.Tensor, want_stats: bool = False):
+    """digest -> prefix-routed dict probe -> dedup, all on the current stream."""
+    s = torch.cuda.current_stream().cuda_stream
+    engine.digest_device(d_data.data_ptr(), d_data.numel(), d_chunks.data_ptr(), n, d_out.data_ptr(),
+                         stream=s)
+    digests = d_out.view(n, 64)[:, :32]
+    hits = sdict.probe(digests)
+    return engine.dedup_device(d_chunks.data_ptr(), n, d_out.data_ptr(), hits.data_ptr(),
+                               n_dict_blobs=max(1, sdict.n_blobs), stream=s, want_stats=want_stats)
