@@ -118,13 +118,57 @@ def cpu_baseline(host_sample: np.ndarray, ch: np.ndarray, digester: str, threads
             "single_stream_gbs": round(nbytes / t_single / 1e9, 3)}
 
 
+WORKLOADS = {
+    "c2": dict(desc="C2: 16 GiB layer tar, 4096 x 4 MiB files, 1 MiB chunks, blake3, no chunk dict",
+               n_files=4096, file_size=4 * MiB, chunk=MiB, digester="blake3", layers=1),
+    "c3": dict(desc="C3: 16 GiB layer, 1 MiB chunks, sha256, vs 200M-entry chunk dict in HBM "
+                    "(30% of the layer's chunks planted)",
+               n_files=4096, file_size=4 * MiB, chunk=MiB, digester="sha256", layers=1,
+               dict_entries=200_000_000, plant=0.3),
+    "c3-blake3": dict(desc="C3 with blake3: 16 GiB layer, 1 MiB chunks, 200M-entry chunk dict",
+                      n_files=4096, file_size=4 * MiB, chunk=MiB, digester="blake3", layers=1,
+                      dict_entries=200_000_000, plant=0.3),
+    "c4": dict(desc="C4 per GPU: 16 x 1 GiB layers, 1 MiB chunks, blake3, 30% of chunks from a "
+                    "shared pool of 1024 contents; chunk dict (pool + 16M filler) partitioned by "
+                    "digest prefix over the GPUs, probes routed by all-to-all",
+               n_files=4096, file_size=4 * MiB, chunk=MiB, digester="blake3", layers=16,
+               pool=1024, dict_entries=16_000_000, sharded=True),
+    "c5": dict(desc="C5-shape: 16 GiB layer, 64 KiB chunks, blake3, no dict",
+               n_files=1024, file_size=16 * MiB, chunk=64 * 1024, digester="blake3", layers=1),
+    "small": dict(desc="1 GiB layer, 1 MiB chunks, blake3", n_files=256, file_size=4 * MiB,
+                  chunk=MiB, digester="blake3", layers=1),
+}
+
+
+def plant_pool(torch, buf, ch, stride, wl, seed):
+    """C4: copy pool contents (same seed on every rank) over ~30% of the chunks."""
+    S = wl["chunk"]
+    per_file = wl["file_size"] // S
+    g = torch.Generator(device="cuda").manual_seed(0x9001)
+    pool = torch.empty((wl["pool"], S), dtype=torch.uint8, device="cuda")
+    pool.random_(0, 256, generator=g)
+    n = len(ch)
+    rows = buf[: wl["n_files"] * stride].view(wl["n_files"], stride)[:, 512:].view(wl["n_files"], per_file, S)
+    rng = np.random.default_rng(seed)
+    sel = np.nonzero(rng.random(n) < 0.3)[0]
+    src = rng.integers(0, wl["pool"], len(sel))
+    for a in range(0, len(sel), 256):
+        f = torch.from_numpy(sel[a:a + 256] // per_file).cuda()
+        k = torch.from_numpy(sel[a:a + 256] % per_file).cuda()
+        rows[f, k] = pool[torch.from_numpy(src[a:a + 256]).cuda()]
+    torch.cuda.synchronize()
+    del pool
+    return None, len(sel)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5", "small"])
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--lanes", type=int, default=0, help="leaves per lane (0=auto)")
+    ap.add_argument("--dict-entries", type=int, default=0, help="override dict size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-mib", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -142,11 +186,11 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    wl = {"c2": dict(n_files=4096, file_size=4 * MiB, chunk=MiB, digester="blake3", dup=0),
-          "c3": dict(n_files=4096, file_size=4 * MiB, chunk=MiB, digester="sha256", dup=0),
-          "c5": dict(n_files=1024, file_size=16 * MiB, chunk=64 * 1024, digester="blake3", dup=0),
-          "small": dict(n_files=256, file_size=4 * MiB, chunk=MiB, digester="blake3", dup=0)}[args.workload]
+    wl = dict(WORKLOADS[args.workload])
+    if args.dict_entries:
+        wl["dict_entries"] = args.dict_entries
     buf, ch = build_layer_on_gpu(torch, wl["n_files"], wl["file_size"], wl["chunk"], seed=0x6E79647573 + rank)
+    _, stride, _, _ = synthetic_layout(1, wl["file_size"], wl["chunk"])
     n = len(ch)
     file_bytes = int(ch["length"].sum())
     d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
@@ -155,11 +199,83 @@ def main():
     eng = nydus_gpu.Engine(device=local, digester=wl["digester"], chunk_size=wl["chunk"],
                            leaves_per_lane=args.lanes, timing=True)
     stream = torch.cuda.Stream()
+    extra = {}
+    n_layers = wl["layers"]
+    per_layer = n // n_layers
+    planted = 0
+    if wl.get("pool"):
+        _, planted = plant_pool(torch, buf, ch, stride, wl, seed=rank)
+
+    sdict = None
+    if wl.get("dict_entries"):
+        # digests of the layer (and of the pool) decide what gets planted in the dict
+        m = wl["dict_entries"]
+        g = torch.Generator(device="cuda").manual_seed(0xD1C7)
+        dd = torch.empty((m, 32), dtype=torch.uint8, device="cuda")
+        dd.random_(0, 256, generator=g)
+        if wl.get("pool"):
+            pool_eng = nydus_gpu.Engine(device=local, digester=wl["digester"], chunk_size=wl["chunk"])
+            gpool = torch.Generator(device="cuda").manual_seed(0x9001)
+            praw = torch.empty((wl["pool"], wl["chunk"]), dtype=torch.uint8, device="cuda")
+            praw.random_(0, 256, generator=gpool)
+            pch = np.zeros(wl["pool"], nydus_gpu.CHUNK_DTYPE)
+            pch["offset"] = np.arange(wl["pool"], dtype=np.uint64) * wl["chunk"]
+            pch["length"] = wl["chunk"]
+            d_pch = torch.from_numpy(pch.view(np.uint8).copy()).cuda()
+            pout = torch.empty(wl["pool"] * 64, dtype=torch.uint8, device="cuda")
+            pool_eng.digest_device(praw.data_ptr(), praw.numel(), d_pch.data_ptr(), wl["pool"], pout.data_ptr())
+            torch.cuda.synchronize()
+            dd[: wl["pool"]] = pout.view(-1, 64)[:, :32]
+            del praw, pout
+            pool_eng.close()
+            expect_dict = planted
+        else:
+            eng.digest_device(buf.data_ptr(), buf.numel(), d_ch.data_ptr(), n, d_out.data_ptr())
+            torch.cuda.synchronize()
+            k = int(n * wl["plant"])
+            sel = torch.randperm(n, device="cuda", generator=g)[:k]
+            rows = torch.randint(0, m, (k,), device="cuda", generator=g).unique()
+            sel = sel[: rows.numel()]
+            dd[rows] = d_out.view(n, 64)[sel, :32]
+            expect_dict = int(rows.numel())
+        us = torch.full((m,), wl["chunk"], dtype=torch.int32, device="cuda")
+        bl = torch.randint(0, 8, (m,), dtype=torch.int32, device="cuda", generator=g)
+        ix = torch.arange(m, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if wl.get("sharded"):
+            from nydus_gpu.dist import ShardedChunkDict, engine_load_fn, engine_probe_fn
+            sdict = ShardedChunkDict(rank, world)
+            local_m = sdict.load(dd, us, bl, ix, 8, engine_load_fn(eng, 8))
+            sdict.probe_fn = engine_probe_fn(eng, stream_fn=lambda: stream.cuda_stream)
+        else:
+            eng.dict_load_device(dd.data_ptr(), us.data_ptr(), bl.data_ptr(), ix.data_ptr(), m, 8)
+            local_m = m
+        torch.cuda.synchronize()
+        build_s = time.perf_counter() - t0
+        del dd, us, bl, ix
+        torch.cuda.empty_cache()
+        extra["dict"] = {"entries": m, "entries_this_gpu": local_m, "build_s": round(build_s, 3),
+                         "build_Mentries_s": round(local_m / build_s / 1e6, 1),
+                         "expected_dict_hits": expect_dict}
+
+    h_hits = None
 
     def step():
         with torch.cuda.stream(stream):
-            eng.process_device(buf.data_ptr(), buf.numel(), d_ch.data_ptr(), n, d_out.data_ptr(),
-                               stream=stream.cuda_stream)
+            s = stream.cuda_stream
+            if sdict is None and n_layers == 1:
+                eng.process_device(buf.data_ptr(), buf.numel(), d_ch.data_ptr(), n, d_out.data_ptr(),
+                                   stream=s)
+            else:
+                eng.digest_device(buf.data_ptr(), buf.numel(), d_ch.data_ptr(), n, d_out.data_ptr(),
+                                  stream=s)
+                hits = sdict.probe(d_out.view(n, 64)[:, :32]) if sdict is not None else None
+                for l in range(n_layers):
+                    a = l * per_layer
+                    eng.dedup_device(d_ch.data_ptr() + a * 24, per_layer, d_out.data_ptr() + a * 64,
+                                     hits.data_ptr() + a * 16 if hits is not None else 0,
+                                     n_dict_blobs=8 if hits is not None else 0, stream=s)
             h_out.copy_(d_out, non_blocking=True)
         return eng.last_timing()
 
@@ -185,9 +301,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # correctness spot check of the last step (no planted dups -> all NEW)
+    # correctness spot checks of the last step
     res = h_out.numpy().view(nydus_gpu.RESULT_DTYPE)
-    assert (res["kind"] == nydus_gpu.NEW).all() and (res["index"] == np.arange(n)).all()
+    kinds = np.bincount(res["kind"], minlength=3)
+    if not wl.get("dict_entries") and not wl.get("pool"):
+        assert kinds[0] == n and (res["index"] == np.arange(n)).all()
+    if wl.get("dict_entries"):
+        extra["dict"]["dict_hits"] = int(kinds[2])
+        assert kinds[2] >= extra["dict"]["expected_dict_hits"] * 0.99, (kinds, extra)
+    extra["decisions"] = {"NEW": int(kinds[0]), "INTRA": int(kinds[1]), "DICT": int(kinds[2])}
 
     total_bytes = file_bytes * args.steps * world
     value = total_bytes / elapsed / 1e9
@@ -231,16 +353,13 @@ def main():
         "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-        "data": "synthetic (random bytes on GPU, real tar headers)",
-        "config": {"workload": {"c2": "C2: 16 GiB layer tar, 4096 x 4 MiB files, 1 MiB chunks, "
-                                      "blake3, no chunk dict",
-                                "c3": "C3-shape digest: 16 GiB layer, 1 MiB chunks, sha256, no dict",
-                                "c5": "C5-shape: 16 GiB layer, 64 KiB chunks, blake3, no dict",
-                                "small": "1 GiB layer, 1 MiB chunks, blake3"}[args.workload],
+        "data": "synthetic (random bytes generated on the GPU, real GNU tar headers)",
+        "config": {"workload": wl["desc"], "name": args.workload,
                    "layer_bytes": int(buf.numel()), "file_bytes_per_gpu": file_bytes, "chunks": n,
                    "chunk_size": wl["chunk"], "digester": wl["digester"],
                    "leaves_per_lane": 1 << D, "parallelism": f"layer-sharded x{world}"},
         "stage_ms": {"digest": round(dig_ms, 3), "tree": round(tree_ms, 3), "dedup": round(dedup_ms, 3)},
+        **extra,
         "roofline": roof,
         "cpu_baseline": cpu,
     }

@@ -20,71 +20,9 @@
 #include <vector>
 
 #include "nydus_gpu.h"
+#include "tarstream.hpp"
 
 namespace {
-
-bool zero_block(const uint8_t *p) {
-  for (int i = 0; i < 512; ++i)
-    if (p[i]) return false;
-  return true;
-}
-
-// Numeric header field: octal ASCII (space/NUL padded) or GNU base-256.
-bool tar_number(const uint8_t *f, size_t n, uint64_t *v) {
-  if (f[0] & 0x80) {
-    uint64_t x = f[0] & 0x7f;
-    for (size_t i = 1; i < n; ++i) {
-      if (x >> 56) return false;
-      x = (x << 8) | f[i];
-    }
-    *v = x;
-    return true;
-  }
-  size_t i = 0;
-  while (i < n && (f[i] == ' ' || f[i] == 0)) ++i;
-  uint64_t x = 0;
-  for (; i < n && f[i] >= '0' && f[i] <= '7'; ++i) x = (x << 3) | (uint64_t)(f[i] - '0');
-  for (; i < n; ++i)
-    if (f[i] != ' ' && f[i] != 0) return false;
-  *v = x;
-  return true;
-}
-
-bool header_checksum_ok(const uint8_t *h) {
-  uint64_t want;
-  if (!tar_number(h + 148, 8, &want)) return false;
-  uint64_t u = 0;
-  int64_t sgn = 0;
-  for (int i = 0; i < 512; ++i) {
-    const uint8_t c = (i >= 148 && i < 156) ? ' ' : h[i];
-    u += c;
-    sgn += (int8_t)c;
-  }
-  return u == want || (uint64_t)sgn == want;
-}
-
-// PAX records "len key=value\n"; returns 1 and *size if a size record exists.
-int pax_size_record(const uint8_t *p, uint64_t n, uint64_t *size) {
-  int found = 0;
-  uint64_t i = 0;
-  while (i < n) {
-    uint64_t rl = 0, j = i;
-    while (j < n && p[j] >= '0' && p[j] <= '9') rl = rl * 10 + (p[j++] - '0');
-    if (j >= n || p[j] != ' ' || rl == 0 || i + rl > n) break;
-    const uint8_t *kv = p + j + 1, *end = p + i + rl - 1;
-    if (end - kv > 5 && memcmp(kv, "size=", 5) == 0) {
-      uint64_t v = 0;
-      for (const uint8_t *q = kv + 5; q < end; ++q) {
-        if (*q < '0' || *q > '9') return -1;
-        v = v * 10 + (uint64_t)(*q - '0');
-      }
-      *size = v;
-      found = 1;
-    }
-    i += rl;
-  }
-  return found;
-}
 
 #pragma pack(push, 1)
 struct RafsV6ChunkInfo {  // 80 B, decoded from the v6 fixture
@@ -115,56 +53,24 @@ uint32_t ngpu_engine_chunk_size(const ngpu_engine *);  // engine.hip (internal)
 int ngpu_tar_chunks(const void *tar_v, uint64_t len, uint32_t chunk_size, ngpu_chunk *out,
                     uint64_t cap, uint64_t *n_chunks, uint64_t *n_files) {
   if ((!tar_v && len) || chunk_size == 0) return NGPU_EINVAL;
-  const uint8_t *tar = (const uint8_t *)tar_v;
-  uint64_t pos = 0, n = 0, files = 0, pax_sz = 0;
-  bool have_pax = false;
-  while (pos + 512 <= len) {
-    const uint8_t *h = tar + pos;
-    if (zero_block(h)) break;
-    if (!header_checksum_ok(h)) return NGPU_ETAR;
-    uint64_t size;
-    if (!tar_number(h + 124, 12, &size)) return NGPU_ETAR;
-    const char type = (char)h[156];
-    const uint64_t data = pos + 512;
-    switch (type) {
-      case 'x': {
-        if (size > len - data) return NGPU_ETAR;
-        const int r = pax_size_record(tar + data, size, &pax_sz);
-        if (r < 0) return NGPU_ETAR;
-        if (r > 0) have_pax = true;
-        break;
-      }
-      case 'g':
-      case 'L':
-      case 'K':
-        if (size > len - data) return NGPU_ETAR;
-        break;
-      case 'S':
-        return NGPU_EUNSUPP;
-      default: {
-        if (have_pax) size = pax_sz;
-        have_pax = false;
-        if (type == '0' || type == '\0' || type == '7') {
-          if (size > len - data) return NGPU_ETAR;
-          for (uint64_t off = 0; off < size; off += chunk_size) {
-            if (n < cap && out) {
-              out[n].offset = data + off;
-              out[n].length = (uint32_t)(size - off < chunk_size ? size - off : chunk_size);
-              out[n].file_index = (uint32_t)files;
-              out[n].file_offset = off;
-            }
-            ++n;
-          }
-          ++files;
-        }
-      }
+  struct Rec : ngpu::TarSink {
+    ngpu_chunk *out;
+    uint64_t cap, n = 0;
+    int chunk(uint64_t off, uint32_t l, uint32_t fi, uint64_t fo) override {
+      if (n < cap && out) out[n] = ngpu_chunk{off, l, fi, fo};
+      ++n;
+      return 0;
     }
-    const uint64_t adv = (size + 511) & ~511ull;
-    if (adv < size || data + adv < data) return NGPU_ETAR;
-    pos = data + adv;
-  }
-  if (n_chunks) *n_chunks = n;
-  if (n_files) *n_files = files;
+    int data(const uint8_t *, uint64_t) override { return 0; }
+  } rec;
+  rec.out = out;
+  rec.cap = cap;
+  ngpu::TarScanner sc(chunk_size);
+  int rc = sc.feed((const uint8_t *)tar_v, len, rec);
+  if (!rc) rc = sc.finish();
+  if (rc) return rc;
+  if (n_chunks) *n_chunks = rec.n;
+  if (n_files) *n_files = sc.files();
   return NGPU_OK;
 }
 

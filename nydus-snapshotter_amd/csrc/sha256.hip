@@ -32,6 +32,13 @@ __device__ __forceinline__ uint32_t bswap(uint32_t x) {
   return __builtin_amdgcn_perm(x, x, 0x00010203u);
 }
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // symmetric truth table
+}
+
+// One 64-B block.  Per round: Sigma1/Sigma0 = 3 v_alignbit + 1 v_bitop3 (xor3),
+// Ch = v_bfi, Maj = v_bitop3, h+K+W and T1 as two v_add3 -> ~13 VALU ops;
+// schedule: sigma0/sigma1 = 2 v_alignbit + v_lshr + v_bitop3, W = v_add3 + v_add.
 __device__ __forceinline__ void sha_block(uint32_t h[8], uint32_t w[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
   uint32_t e = h[4], f = h[5], g = h[6], hh = h[7];
@@ -42,18 +49,18 @@ __device__ __forceinline__ void sha_block(uint32_t h[8], uint32_t w[16]) {
       wt = w[t];
     } else {
       const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
       wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
       w[t & 15] = wt;
     }
-    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t hkw = hh + kK[t] + wt;
+    const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
     const uint32_t ch = (e & f) ^ (~e & g);
-    const uint32_t t1 = hh + S1 + ch + kK[t] + wt;
-    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t t1 = hkw + S1 + ch;
+    const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
     const uint32_t mj = (a & b) | (c & (a | b));
-    const uint32_t t2 = S0 + mj;
-    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
   }
   h[0] += a; h[1] += b; h[2] += c; h[3] += d;
   h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
