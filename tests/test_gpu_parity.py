@@ -307,8 +307,9 @@ def test_split_stages_equal_process(oracle):
     di = np.arange(len(pick), dtype=np.uint32) + 7
     eng = nydus_gpu.Engine(chunk_size=0x10000)
     try:
-        eng.dict_load_device(_to_dev(dd).data_ptr(), _to_dev(ds).data_ptr(), _to_dev(db).data_ptr(),
-                             _to_dev(di).data_ptr(), len(pick), 3)
+        keep = [_to_dev(x) for x in (dd, ds, db, di)]  # alive until the engine has copied them
+        torch.cuda.synchronize()
+        eng.dict_load_device(*(t.data_ptr() for t in keep), len(pick), 3)
         torch.cuda.synchronize()
         d_data, d_ch = _to_dev(np.frombuffer(data, np.uint8)), _to_dev(ch)
         n = len(ch)
