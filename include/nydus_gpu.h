@@ -225,6 +225,24 @@ void ngpu_free_host(void *p);
  * engine was created with NGPU_FLAG_TIMING. */
 int ngpu_last_timing(ngpu_engine *eng, ngpu_timing *out);
 
+/* ---- streaming Pack (converter.Pack, pkg/converter/convert_unix.go:325) ----
+ * The reference returns an io.WriteCloser fed with the uncompressed layer tar
+ * (packFromTar :443-539 pipes it to nydus-image through a FIFO).  Here:
+ * open -> write (copying) or reserve/commit (zero-copy into engine-pinned
+ * staging) in any split -> close.  Full staging slots are copied to HBM and
+ * digested while the caller keeps writing; dedup runs at close in stream
+ * order.  close (success or not) and abort release the pack; *chunks_out /
+ * *results_out are malloc'd (ngpu_free_host).  A malformed or truncated tar
+ * fails with NGPU_ETAR / NGPU_EUNSUPP at write/commit or close. */
+typedef struct ngpu_pack ngpu_pack;
+int ngpu_pack_open(ngpu_engine *eng, ngpu_pack **out);
+int ngpu_pack_write(ngpu_pack *p, const void *buf, uint64_t len);
+int ngpu_pack_reserve(ngpu_pack *p, void **ptr, uint64_t *avail);
+int ngpu_pack_commit(ngpu_pack *p, uint64_t n);
+int ngpu_pack_close(ngpu_pack *p, ngpu_chunk **chunks_out, ngpu_result **results_out,
+                    uint64_t *n_out, ngpu_layer_stats *stats);
+void ngpu_pack_abort(ngpu_pack *p);
+
 /* ---- RAFS v6 chunk table ---------------------------- */
 /* Serialise the layer's unique chunk records (NEW chunks in index order) as
  * 80-byte RAFS v6 chunk-info entries.  compressor "none": compressed size =

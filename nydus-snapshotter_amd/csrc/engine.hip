@@ -14,36 +14,11 @@
 #include <string>
 #include <vector>
 
-#include "common.hpp"
+#include "engine_internal.hpp"
 
 using namespace ngpu;
 
-struct ngpu_engine {
-  ngpu_config cfg{};
-  int device = 0;
-  hipStream_t stream = nullptr;
-  Workspace ws;
-  // chunk dict, HBM resident
-  uint8_t *d_dict_digest = nullptr;
-  uint32_t *d_dict_usize = nullptr, *d_dict_blob = nullptr, *d_dict_index = nullptr;
-  uint64_t *d_dict_table = nullptr;
-  DictDevice dict;
-  // host-path device buffers
-  uint8_t *d_data = nullptr;
-  uint64_t d_data_cap = 0;
-  ngpu_chunk *d_chunks = nullptr;
-  ngpu_result *d_results = nullptr;
-  uint64_t d_chunk_cap = 0;
-  uint64_t *h_stats = nullptr;  // pinned
-  // NGPU_FLAG_TIMING: 0 start, 1 digest start, 2 digest end, 3 tree end, 4 end
-  hipEvent_t ev[5] = {};
-  bool timed = false;
-  int last_D = 0;
-  std::string err;
-  std::mutex mu;
-};
-
-namespace {
+namespace ngpu {
 
 int fail(ngpu_engine *e, int code, const char *fmt, ...) {
   if (e) {
@@ -56,15 +31,6 @@ int fail(ngpu_engine *e, int code, const char *fmt, ...) {
   }
   return code;
 }
-
-#define HIP_TRY(e, call)                                                        \
-  do {                                                                          \
-    hipError_t _st = (call);                                                    \
-    if (_st != hipSuccess)                                                      \
-      return fail((e), _st == hipErrorOutOfMemory ? NGPU_ENOMEM : NGPU_EHIP,   \
-                  "%s: %s (%s:%d)", #call, hipGetErrorString(_st), __FILE__,   \
-                  __LINE__);                                                    \
-  } while (0)
 
 template <typename T>
 int grow(ngpu_engine *e, T **p, uint64_t &cap, uint64_t want, uint64_t elem_bytes = sizeof(T)) {
@@ -232,7 +198,7 @@ int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st) {
   return 0;
 }
 
-}  // namespace
+}  // namespace ngpu
 
 extern "C" {
 

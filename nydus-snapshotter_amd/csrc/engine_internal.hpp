@@ -1,0 +1,56 @@
+// engine_internal.hpp — engine state and stage helpers shared by
+// engine.hip (C ABI) and pack.hip (streaming Pack writer).  Not installed.
+#pragma once
+
+#include <mutex>
+#include <string>
+
+#include "common.hpp"
+
+struct ngpu_engine {
+  ngpu_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  ngpu::Workspace ws;
+  // chunk dict, HBM resident
+  uint8_t *d_dict_digest = nullptr;
+  uint32_t *d_dict_usize = nullptr, *d_dict_blob = nullptr, *d_dict_index = nullptr;
+  uint64_t *d_dict_table = nullptr;
+  ngpu::DictDevice dict;
+  // host-path device buffers
+  uint8_t *d_data = nullptr;
+  uint64_t d_data_cap = 0;
+  ngpu_chunk *d_chunks = nullptr;
+  ngpu_result *d_results = nullptr;
+  uint64_t d_chunk_cap = 0;
+  uint64_t *h_stats = nullptr;  // pinned
+  // NGPU_FLAG_TIMING: 0 start, 1 digest start, 2 digest end, 3 tree end, 4 end
+  hipEvent_t ev[5] = {};
+  bool timed = false;
+  int last_D = 0;
+  std::string err;
+  std::mutex mu;
+};
+
+
+namespace ngpu {
+
+int fail(ngpu_engine *e, int code, const char *fmt, ...);
+int pick_group_log2(const ngpu_engine *e, uint64_t data_len);
+int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D, uint32_t n_blobs);
+int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
+                   const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out, hipStream_t s);
+int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+                  const ngpu_dict_hit *d_hits, uint32_t n_blobs, hipStream_t s);
+int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st);
+
+}  // namespace ngpu
+
+#define HIP_TRY(e, call)                                                        \
+  do {                                                                          \
+    hipError_t _st = (call);                                                    \
+    if (_st != hipSuccess)                                                      \
+      return ::ngpu::fail((e), _st == hipErrorOutOfMemory ? NGPU_ENOMEM : NGPU_EHIP, \
+                          "%s: %s (%s:%d)", #call, hipGetErrorString(_st), __FILE__, \
+                          __LINE__);                                            \
+  } while (0)

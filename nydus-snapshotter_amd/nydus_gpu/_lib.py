@@ -34,7 +34,9 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_dict_load_bootstrap", "ngpu_dict_clear", "ngpu_dict_size", "ngpu_tar_chunks",
            "ngpu_process", "ngpu_process_device", "ngpu_pack_tar", "ngpu_free_host",
            "ngpu_chunk_table", "ngpu_last_timing", "ngpu_digest_device",
-           "ngpu_dict_probe_device", "ngpu_dedup_device", "ngpu_dict_load_device"]
+           "ngpu_dict_probe_device", "ngpu_dedup_device", "ngpu_dict_load_device",
+           "ngpu_pack_open", "ngpu_pack_write", "ngpu_pack_reserve", "ngpu_pack_commit",
+           "ngpu_pack_close", "ngpu_pack_abort"]
 
 HIT_DTYPE = np.dtype([("entry", "<u4"), ("index", "<u4"), ("blob", "<u4"), ("usize", "<u4")])
 MISS = 0xFFFFFFFF
@@ -115,6 +117,14 @@ def lib():
     L.ngpu_dict_probe_device.argtypes = [vp, vp, u64, u64, vp, vp]
     L.ngpu_dedup_device.argtypes = [vp, vp, u64, vp, vp, u32, vp, ctypes.POINTER(NgpuLayerStats)]
     L.ngpu_dict_load_device.argtypes = [vp, vp, vp, vp, vp, u64, u32]
+    L.ngpu_pack_open.argtypes = [vp, ctypes.POINTER(vp)]
+    L.ngpu_pack_write.argtypes = [vp, vp, u64]
+    L.ngpu_pack_reserve.argtypes = [vp, ctypes.POINTER(vp), pu64]
+    L.ngpu_pack_commit.argtypes = [vp, u64]
+    L.ngpu_pack_close.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), pu64,
+                                  ctypes.POINTER(NgpuLayerStats)]
+    L.ngpu_pack_abort.argtypes = [vp]
+    L.ngpu_pack_abort.restype = None
     _lib = L
     return L
 
@@ -275,6 +285,10 @@ class Engine:
         self._check(lib().ngpu_last_timing(self._h, ctypes.byref(t)), "last_timing")
         return t.as_dict()
 
+    def pack(self) -> "PackWriter":
+        """Streaming Pack (converter.Pack mirror): returns a writer."""
+        return PackWriter(self)
+
     def pack_tar(self, tar):
         """Whole tar layer -> (chunks, results, stats)."""
         L = lib()
@@ -284,6 +298,72 @@ class Engine:
         st = NgpuLayerStats()
         self._check(L.ngpu_pack_tar(self._h, _ptr(buf), buf.size, ctypes.byref(pc), ctypes.byref(pr),
                                     ctypes.byref(n), ctypes.byref(st)), "pack_tar")
+        try:
+            nn = n.value
+            ch = np.empty(nn, dtype=CHUNK_DTYPE)
+            rs = np.empty(nn, dtype=RESULT_DTYPE)
+            if nn:
+                ctypes.memmove(ch.ctypes.data, pc, nn * CHUNK_DTYPE.itemsize)
+                ctypes.memmove(rs.ctypes.data, pr, nn * RESULT_DTYPE.itemsize)
+        finally:
+            L.ngpu_free_host(pc)
+            L.ngpu_free_host(pr)
+        return ch, rs, st.as_dict()
+
+
+class PackWriter:
+    """Mirror of the io.WriteCloser returned by converter.Pack
+    (pkg/converter/convert_unix.go:325): write() the uncompressed layer tar in
+    any split, close() -> (chunks, results, stats).  Errors raise NgpuError;
+    a failed writer is released (like Close() reporting the builder error)."""
+
+    def __init__(self, engine: Engine):
+        self._eng = engine
+        h = ctypes.c_void_p()
+        engine._check(lib().ngpu_pack_open(engine._h, ctypes.byref(h)), "pack_open")
+        self._p = h
+
+    def write(self, data) -> int:
+        buf = _buf(data)
+        rc = lib().ngpu_pack_write(self._p, _ptr(buf), buf.size)
+        if rc:
+            self.abort()
+            self._eng._check(rc, "pack_write")
+        return buf.size
+
+    def write_zero_copy(self, data) -> int:
+        """Copy into the engine's pinned staging via reserve/commit."""
+        L = lib()
+        buf = _buf(data)
+        off = 0
+        while off < buf.size:
+            ptr, avail = ctypes.c_void_p(), ctypes.c_uint64(0)
+            rc = L.ngpu_pack_reserve(self._p, ctypes.byref(ptr), ctypes.byref(avail))
+            if rc:
+                self.abort()
+                self._eng._check(rc, "pack_reserve")
+            take = min(avail.value, buf.size - off)
+            ctypes.memmove(ptr.value, buf.ctypes.data + off, take)
+            rc = L.ngpu_pack_commit(self._p, take)
+            if rc:
+                self.abort()
+                self._eng._check(rc, "pack_commit")
+            off += take
+        return buf.size
+
+    def abort(self):
+        if self._p:
+            lib().ngpu_pack_abort(self._p)
+            self._p = None
+
+    def close(self):
+        L = lib()
+        pc, pr = ctypes.c_void_p(), ctypes.c_void_p()
+        n = ctypes.c_uint64(0)
+        st = NgpuLayerStats()
+        p, self._p = self._p, None
+        self._eng._check(L.ngpu_pack_close(p, ctypes.byref(pc), ctypes.byref(pr), ctypes.byref(n),
+                                           ctypes.byref(st)), "pack_close")
         try:
             nn = n.value
             ch = np.empty(nn, dtype=CHUNK_DTYPE)

@@ -397,3 +397,88 @@ def test_sharded_dict_two_ranks_one_gpu():
     mp.spawn(_sharded_worker, args=(2, port, ret), nprocs=2, join=True)
     assert ret[0][0] and ret[1][0]
     assert ret[0][1] > 0 and ret[1][1] > 0
+
+
+# ---- streaming Pack (converter.Pack mirror) --------------------------------
+
+def _stream(eng, tb, rng, zero_copy):
+    w = eng.pack()
+    pos = 0
+    while pos < len(tb):
+        k = int(rng.integers(1, 300_000))
+        piece = tb[pos:pos + k]
+        (w.write_zero_copy if zero_copy else w.write)(piece)
+        pos += len(piece)
+    return w.close()
+
+
+def test_streaming_pack_matches_pack_tar(golden_layers, tars):
+    rng = np.random.default_rng(77)
+    for case in golden_layers["cases"]:
+        cs = case["chunk_size"]
+        # staging = 4 chunks: forces many slot switches and carried chunks
+        eng = nydus_gpu.Engine(digester=case["digester"], chunk_size=cs, staging_bytes=4 * cs)
+        try:
+            tb = tars[case["layer"]]
+            ref = eng.pack_tar(tb)
+            for zc in (False, True):
+                ch, out, st = _stream(eng, tb, rng, zc)
+                assert ch.tobytes() == ref[0].tobytes(), case["layer"]
+                assert out.tobytes() == ref[1].tobytes(), case["layer"]
+                assert st == ref[2]
+                assert [d.tobytes().hex() for d in out["digest"]] == case["digests"]
+        finally:
+            eng.close()
+
+
+def test_streaming_pack_large_random_layer(oracle):
+    """~200 MiB tar of random files through 8 MiB staging slots."""
+    import io
+    import tarfile
+    rng = np.random.default_rng(8)
+    bio = io.BytesIO()
+    tf = tarfile.open(fileobj=bio, mode="w", format=tarfile.GNU_FORMAT)
+    blobs = []
+    for i in range(300):
+        n = int(rng.choice([0, 100, 5000, 70000, 1 << 20, 3 << 20]) + rng.integers(0, 3000))
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes() if i % 7 else (blobs[-1] if blobs else b"")
+        blobs.append(data)
+        ti = tarfile.TarInfo(f"f{i}")
+        ti.size = len(data)
+        tf.addfile(ti, io.BytesIO(data))
+    tf.close()
+    tb = bio.getvalue()
+    eng = nydus_gpu.Engine(chunk_size=0x100000, staging_bytes=8 << 20)
+    try:
+        ch, out, st = _stream(eng, tb, rng, True)
+    finally:
+        eng.close()
+    ref_ch = oracle.tar_chunks(tb, 0x100000)
+    assert ch.tobytes() == ref_ch.tobytes()
+    dig = oracle.digest_chunks(tb, ref_ch, "blake3")
+    assert np.array_equal(out["digest"], dig)
+    dec, _ = oracle.dedup(dig, ref_ch["length"])
+    for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+        assert np.array_equal(out[f], dec[f]), f
+    assert st["intra_chunks"] > 0
+
+
+def test_streaming_pack_errors(tars):
+    eng = nydus_gpu.Engine(chunk_size=0x100000)
+    try:
+        tb = tars["oci_upper"]
+        w = eng.pack()
+        w.write(tb[: len(tb) // 2])
+        with pytest.raises(nydus_gpu.NgpuError) as e:
+            w.close()
+        assert e.value.code == -4  # truncated inside file data
+        w = eng.pack()
+        with pytest.raises(nydus_gpu.NgpuError):
+            w.write(b"z" * 2048)  # bad header checksum
+        w = eng.pack()
+        w.write(tars["oci_lower"])
+        w.abort()
+        ch, out, st = eng.pack().close()  # empty stream is an empty layer
+        assert len(ch) == 0 and st["chunks"] == 0
+    finally:
+        eng.close()
