@@ -161,6 +161,48 @@ def plant_pool(torch, buf, ch, stride, wl, seed):
     return None, len(sel)
 
 
+def end_to_end(torch, nydus_gpu, buf, wl, stride, device, sample_bytes=2 << 30):
+    """PCIe-inclusive rates on the first `sample_files` files of the layer, held
+    in engine-pinned host memory (never the headline value):
+      host_path   — ngpu_pack_tar: host tar parse + one H2D copy + digest + dedup;
+      streaming   — ngpu_pack write/close through two pinned staging slots
+                    (H2D of slot k overlaps the digest of slot k-1), bytes
+                    memcpy'd into staging by the caller."""
+    import ctypes
+    sample_files = max(1, sample_bytes // stride)
+    nbytes = sample_files * stride
+    eng = nydus_gpu.Engine(device=device, digester=wl["digester"], chunk_size=wl["chunk"],
+                           staging_bytes=64 << 20)
+    L = nydus_gpu.lib()
+    hp = ctypes.c_void_p()
+    assert L.ngpu_alloc_pinned(eng._h, nbytes + 1024, ctypes.byref(hp)) == 0
+    host = np.ctypeslib.as_array((ctypes.c_uint8 * (nbytes + 1024)).from_address(hp.value))
+    host[:nbytes] = buf[:nbytes].cpu().numpy()
+    host[nbytes:] = 0
+    file_bytes = sample_files * wl["file_size"]
+    res = {"sample_bytes": nbytes + 1024}
+    try:
+        eng.pack_tar(host)  # warm
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            ch, out, st = eng.pack_tar(host)
+        res["host_path_gbs"] = round(file_bytes * reps / (time.perf_counter() - t0) / 1e9, 1)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            w = eng.pack()
+            for a in range(0, host.size, 32 << 20):
+                w.write_zero_copy(host[a:a + (32 << 20)])
+            ch2, out2, st2 = w.close()
+        res["streaming_gbs"] = round(file_bytes * reps / (time.perf_counter() - t0) / 1e9, 1)
+        assert out2.tobytes() == out.tobytes()
+        res["bound"] = "PCIe Gen5 x16 H2D (~50-55 GB/s) and host memcpy into staging"
+    finally:
+        L.ngpu_free_pinned(eng._h, hp)
+        eng.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -170,6 +212,7 @@ def main():
     ap.add_argument("--lanes", type=int, default=0, help="leaves per lane (0=auto)")
     ap.add_argument("--dict-entries", type=int, default=0, help="override dict size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-sample-mib", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=0)
     args = ap.parse_args()
@@ -339,6 +382,10 @@ def main():
                 "hbm_gbs": round(file_bytes / (dig_ms / 1e3) / 1e9, 1),
                 "occupancy_ceiling": f"{n} lanes = {n / (256 * 4 * 64):.3f} waves per SIMD"}
 
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e and not wl.get("dict_entries"):
+        e2e = end_to_end(torch, nydus_gpu, buf, wl, stride, local)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sample_files = max(1, min(wl["n_files"], (args.cpu_sample_mib * MiB) // wl["file_size"]))
@@ -362,6 +409,7 @@ def main():
         **extra,
         "roofline": roof,
         "cpu_baseline": cpu,
+        "e2e_pcie": e2e,
     }
     if cpu:
         line["speedup_vs_cpu"] = round(value / cpu["value"], 2)

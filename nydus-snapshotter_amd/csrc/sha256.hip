@@ -66,73 +66,137 @@ __device__ __forceinline__ void sha_block(uint32_t h[8], uint32_t w[16]) {
   h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
 
-__global__ __launch_bounds__(64) void sha256_chunks(
-    const uint8_t *__restrict__ data, uint64_t data_len,
-    const ngpu_chunk *__restrict__ chunks, uint64_t n,
-    ngpu_result *__restrict__ out, uint64_t *__restrict__ err) {
-  const uint64_t c = blockIdx.x * 64ull + threadIdx.x;
-  if (c >= n) return;
-  const ngpu_chunk ch = chunks[c];
-  if (ch.offset > data_len || ch.length > data_len - ch.offset) {
-    atomicAdd((unsigned long long *)err, 1ull);
-    return;
-  }
-  const uint8_t *p = data + ch.offset;
-  const uint32_t len = ch.length;
-  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+// Message block `b` of a chunk (b < full: data; else the padding tail),
+// big-endian words.
+__device__ __forceinline__ void sha_load_block(const uint8_t *p, uint32_t len, uint32_t b,
+                                               uint32_t w[16]) {
   const uint32_t full = len >> 6;
-  uint32_t w[16];
-  if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
-    const uint8_t *q = p;
-    for (uint32_t b = 0; b < full; ++b, q += 64) {
+  if (b < full) {
+    const uint8_t *q = p + 64ull * b;
+    if ((reinterpret_cast<uintptr_t>(q) & 15) == 0) {
       const u32x4 x0 = load_nt16(q), x1 = load_nt16(q + 16);
       const u32x4 x2 = load_nt16(q + 32), x3 = load_nt16(q + 48);
       w[0] = bswap(x0.x); w[1] = bswap(x0.y); w[2] = bswap(x0.z); w[3] = bswap(x0.w);
       w[4] = bswap(x1.x); w[5] = bswap(x1.y); w[6] = bswap(x1.z); w[7] = bswap(x1.w);
       w[8] = bswap(x2.x); w[9] = bswap(x2.y); w[10] = bswap(x2.z); w[11] = bswap(x2.w);
       w[12] = bswap(x3.x); w[13] = bswap(x3.y); w[14] = bswap(x3.z); w[15] = bswap(x3.w);
-      sha_block(h, w);
-    }
-  } else {
-    for (uint32_t b = 0; b < full; ++b) {
+    } else {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint8_t *s = p + 64 * b + 4 * i;
-        w[i] = ((uint32_t)s[0] << 24) | ((uint32_t)s[1] << 16) |
-               ((uint32_t)s[2] << 8) | (uint32_t)s[3];
-      }
-      sha_block(h, w);
+      for (int i = 0; i < 16; ++i)
+        w[i] = ((uint32_t)q[4 * i] << 24) | ((uint32_t)q[4 * i + 1] << 16) |
+               ((uint32_t)q[4 * i + 2] << 8) | (uint32_t)q[4 * i + 3];
     }
+    return;
   }
   // Tail: remaining bytes, 0x80, zero pad, 64-bit big-endian bit length.
   const uint32_t rem = len & 63;
-  const uint8_t *tp = p + 64 * full;
+  const uint32_t tb = b - full;  // 0 or 1
   const uint32_t tail_blocks = rem + 9 <= 64 ? 1 : 2;
-  const uint64_t bits = (uint64_t)len * 8;
-  for (uint32_t tb = 0; tb < tail_blocks; ++tb) {
+  const uint8_t *tp = p + 64ull * full;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      uint32_t x = 0;
+  for (int i = 0; i < 16; ++i) {
+    uint32_t x = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t pos = 64 * tb + 4 * i + k;
-        uint32_t byte = 0;
-        if (pos < rem) byte = tp[pos];
-        else if (pos == rem) byte = 0x80;
-        x = (x << 8) | byte;
-      }
-      w[i] = x;
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t pos = 64 * tb + 4 * i + k;
+      uint32_t byte = 0;
+      if (pos < rem) byte = tp[pos];
+      else if (pos == rem) byte = 0x80;
+      x = (x << 8) | byte;
     }
-    if (tb + 1 == tail_blocks) {
-      w[14] = (uint32_t)(bits >> 32);
-      w[15] = (uint32_t)bits;
-    }
-    sha_block(h, w);
+    w[i] = x;
   }
-  uint4 *d = reinterpret_cast<uint4 *>(out[c].digest);
-  d[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
-  d[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
+  if (tb + 1 == tail_blocks) {
+    const uint64_t bits = (uint64_t)len * 8;
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+  }
+}
+
+// Two waves per 64 chunks (SURVEY.md §7 hard part (c): SHA-256 has one
+// independent stream per chunk, so at 1 MiB chunks a 16 GiB layer fills one
+// wave per CU).  Wave 1 ("schedule") loads block k+1 and expands its message
+// schedule into K[t]+W[t] in LDS while wave 0 ("rounds") runs the 64 rounds
+// of block k from LDS: the per-chunk instruction stream on the critical wave
+// drops from ~1440 to ~900 VALU ops per block, and the two waves run on two
+// SIMDs.  One workgroup barrier per block; LDS ping-pong [2][64 t][64 lanes].
+__global__ __launch_bounds__(128) void sha256_split(
+    const uint8_t *__restrict__ data, uint64_t data_len,
+    const ngpu_chunk *__restrict__ chunks, uint64_t n,
+    ngpu_result *__restrict__ out, uint64_t *__restrict__ err) {
+  __shared__ uint32_t kw[2][64][64];
+  const uint32_t lane = threadIdx.x & 63;
+  const bool rounds = threadIdx.x < 64;
+  const uint64_t c = blockIdx.x * 64ull + lane;
+  bool valid = c < n;
+  uint32_t len = 0;
+  const uint8_t *p = data;
+  if (valid) {
+    const ngpu_chunk ch = chunks[c];
+    if (ch.offset > data_len || ch.length > data_len - ch.offset) {
+      if (rounds) atomicAdd((unsigned long long *)err, 1ull);
+      valid = false;
+    } else {
+      len = ch.length;
+      p = data + ch.offset;
+    }
+  }
+  const uint32_t nb = valid ? (len + 8) / 64 + 1 : 0;
+  uint32_t nbmax = nb;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, o, 64));
+
+  auto produce = [&](uint32_t b, int buf) {
+    uint32_t w[16];
+    sha_load_block(p, len, b, w);
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      uint32_t wt;
+      if (t < 16) {
+        wt = w[t];
+      } else {
+        const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+        const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+        const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+        wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+        w[t & 15] = wt;
+      }
+      kw[buf][t][lane] = wt + kK[t];
+    }
+  };
+
+  if (!rounds && nb > 0) produce(0, 0);
+  __syncthreads();
+  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  for (uint32_t k = 0; k < nbmax; ++k) {
+    if (rounds) {
+      if (k < nb) {
+        const int buf = k & 1;
+        uint32_t a = h[0], b = h[1], cc = h[2], d = h[3];
+        uint32_t e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+        for (int t = 0; t < 64; ++t) {
+          const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+          const uint32_t ch = (e & f) ^ (~e & g);
+          const uint32_t t1 = hh + kw[buf][t][lane] + S1 + ch;
+          const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+          const uint32_t mj = (a & b) | (cc & (a | b));
+          hh = g; g = f; f = e; e = d + t1; d = cc; cc = b; b = a; a = t1 + S0 + mj;
+        }
+        h[0] += a; h[1] += b; h[2] += cc; h[3] += d;
+        h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+      }
+    } else if (k + 1 < nb) {
+      produce(k + 1, (k + 1) & 1);
+    }
+    __syncthreads();
+  }
+  if (rounds && valid) {
+    uint4 *dd = reinterpret_cast<uint4 *>(out[c].digest);
+    dd[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
+    dd[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
+  }
 }
 
 }  // namespace
@@ -142,7 +206,7 @@ void launch_sha256(const uint8_t *data, uint64_t data_len,
                    uint64_t *err, hipStream_t s) {
   if (n == 0) return;
   const uint64_t blocks = (n + 63) / 64;
-  hipLaunchKernelGGL(sha256_chunks, dim3((unsigned)blocks), dim3(64), 0, s, data,
+  hipLaunchKernelGGL(sha256_split, dim3((unsigned)blocks), dim3(128), 0, s, data,
                      data_len, chunks, n, out, err);
 }
 

@@ -31,6 +31,6 @@ for W in c3 c5; do
   cat "$OUT/bench_$W.json"
 done
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-e2e > "$OUT/prof.log" 2>&1
 ok $? rocprof
 find "$OUT/prof" -name '*stats*' | head
