@@ -302,7 +302,10 @@ def main():
                          "build_Mentries_s": round(local_m / build_s / 1e6, 1),
                          "expected_dict_hits": expect_dict}
 
-    h_hits = None
+    layer_first = (np.arange(n_layers + 1, dtype=np.int64) * per_layer)
+    d_first = torch.from_numpy(layer_first).cuda()
+    d_lstats = torch.zeros(n_layers * nydus_gpu.LAYER_STATS_DTYPE.itemsize, dtype=torch.uint8,
+                           device="cuda")
 
     def step():
         with torch.cuda.stream(stream):
@@ -314,11 +317,11 @@ def main():
                 eng.digest_device(buf.data_ptr(), buf.numel(), d_ch.data_ptr(), n, d_out.data_ptr(),
                                   stream=s)
                 hits = sdict.probe(d_out.view(n, 64)[:, :32]) if sdict is not None else None
-                for l in range(n_layers):
-                    a = l * per_layer
-                    eng.dedup_device(d_ch.data_ptr() + a * 24, per_layer, d_out.data_ptr() + a * 64,
-                                     hits.data_ptr() + a * 16 if hits is not None else 0,
-                                     n_dict_blobs=8 if hits is not None else 0, stream=s)
+                # all layers in one launch set (per-layer semantics, shared dict)
+                eng.dedup_layers_device(d_ch.data_ptr(), n, d_out.data_ptr(), d_first.data_ptr(),
+                                        n_layers, d_lstats.data_ptr(),
+                                        d_hits=hits.data_ptr() if hits is not None else 0,
+                                        n_dict_blobs=8 if hits is not None else 0, stream=s)
             h_out.copy_(d_out, non_blocking=True)
         return eng.last_timing()
 

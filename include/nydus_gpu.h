@@ -206,6 +206,20 @@ int ngpu_dedup_device(ngpu_engine *eng, const ngpu_chunk *d_chunks, uint64_t n,
                       ngpu_result *d_out, const ngpu_dict_hit *d_hits,
                       uint32_t n_dict_blobs, void *stream,
                       ngpu_layer_stats *stats);
+/* Many layers per call (e.g. 1000 small layers against one chunk dict):
+ * layer l owns chunks [d_layer_first[l], d_layer_first[l+1]) (device u64
+ * array of n_layers+1, d_layer_first[n_layers] == n).  Each layer is deduped
+ * exactly as if it were packed alone (its own layered dict, NEW indices,
+ * offsets and blob order); the chunk dict is shared.  d_stats: device
+ * ngpu_layer_stats[n_layers] (written asynchronously), or NULL. */
+int ngpu_dedup_layers_device(ngpu_engine *eng, const ngpu_chunk *d_chunks, uint64_t n,
+                             ngpu_result *d_out, const ngpu_dict_hit *d_hits,
+                             uint32_t n_dict_blobs, const uint64_t *d_layer_first,
+                             uint64_t n_layers, ngpu_layer_stats *d_stats, void *stream);
+int ngpu_process_layers_device(ngpu_engine *eng, const void *d_data, uint64_t len,
+                               const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+                               const uint64_t *d_layer_first, uint64_t n_layers,
+                               ngpu_layer_stats *d_stats, void *stream);
 /* Build the dict from device-resident arrays (entry order = table order). */
 int ngpu_dict_load_device(ngpu_engine *eng, const uint8_t *d_digests,
                           const uint32_t *d_usize, const uint32_t *d_blob_index,

@@ -64,10 +64,13 @@ struct DictDevice {
 void launch_dict_build(const uint8_t *digests, uint64_t m, uint64_t *table,
                        uint64_t cap, hipStream_t s);
 // hits == nullptr: probe `dict`; otherwise use the given per-chunk hits.
-// n_blobs: inner blobs of the (global) dict.
+// n_blobs: inner blobs of the (global) dict.  L layers; layer l owns chunks
+// [lfirst[l], lfirst[l+1]) (device array); st: device ngpu_layer_stats[L].
 void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                   const ngpu_dict_hit *hits, uint32_t n_blobs, uint32_t align,
-                  Workspace &ws, ngpu_result *out, hipStream_t s);
+                  const uint64_t *lfirst, uint64_t L, Workspace &ws, ngpu_result *out,
+                  ngpu_layer_stats *st, hipStream_t s);
+void launch_set_single_layer(uint64_t *lfirst, uint64_t n, hipStream_t s);
 void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
                        const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s);
 void launch_scan_u64(uint64_t *data, uint64_t n, uint64_t *tmp,
@@ -84,8 +87,12 @@ struct Workspace {
   uint64_t *scan_tmp = nullptr;
   uint64_t *intra = nullptr;      // intra-layer hash table
   uint64_t intra_cap = 0;
-  uint32_t *blob_first = nullptr; // dict blobs + 1: first chunk hitting each
+  uint32_t *blob_first = nullptr; // per layer: dict blobs + 1: first chunk hitting each
   uint32_t *blob_real = nullptr;
+  uint32_t *chunk_layer = nullptr;   // n: layer of each chunk
+  uint64_t *lfirst1 = nullptr;       // {0, n} for single-layer calls
+  ngpu_layer_stats *lstats = nullptr;// per-layer stats (internal, cap_layers)
+  uint64_t cap_layers = 0;
   uint64_t *stats = nullptr;      // device-side counters (ngpu_layer_stats)
   uint64_t cap_n = 0, cap_g = 0, cap_blobs = 0;
   int load_mode = 0;              // b3_groups load mode (see blake3.hip)

@@ -104,10 +104,30 @@ __global__ void dict_probe_records(const uint8_t *__restrict__ digests, uint64_t
   hits[q] = h;
 }
 
+// ---- layered dedup -----------------------------------------------------------
+// A call covers L >= 1 layers; layer l owns chunks [first[l], first[l+1]).
+// Everything except the chunk dict restarts per layer: the layered
+// (intra-build) dict, NEW indices, uncompressed offsets and blob order.  The
+// intra table is shared by all layers of a call: its key is (layer, digest).
+
+__device__ __forceinline__ uint64_t layer_bucket(const uint32_t *d, uint32_t layer) {
+  return digest_bucket(d) + (uint64_t)layer * 0xC2B2AE3D27D4EB4Full;
+}
+
+// chunk -> layer map; one wave per layer, lanes stride over its chunks.
+__global__ void layer_fill(const uint64_t *__restrict__ first, uint64_t L,
+                           uint32_t *__restrict__ chunk_layer) {
+  const uint64_t waves = (gridDim.x * (uint64_t)blockDim.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t l = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6; l < L; l += waves)
+    for (uint64_t c = first[l] + lane; c < first[l + 1]; c += 64) chunk_layer[c] = (uint32_t)l;
+}
+
 // Stage 1: dict decision (from given hits, or by probing the local dict) +
 // reset of the per-chunk state.
 __global__ void dedup_probe(const ngpu_chunk *__restrict__ chunks, uint64_t n,
                             DictDevice dict, const ngpu_dict_hit *__restrict__ hits,
+                            const uint32_t *__restrict__ chunk_layer,
                             ngpu_result *__restrict__ out,
                             uint64_t *__restrict__ newflag,
                             uint32_t *__restrict__ blob_first, uint32_t n_blobs) {
@@ -130,27 +150,52 @@ __global__ void dedup_probe(const ngpu_chunk *__restrict__ chunks, uint64_t n,
     r.index = h.index;
     r.blob_index = h.blob;  // inner index; remapped in finalize
     r.uncompressed_offset = 0;
-    atomicMin(blob_first + h.blob, (uint32_t)c);
+    atomicMin(blob_first + (uint64_t)chunk_layer[c] * (n_blobs + 1) + h.blob, (uint32_t)c);
   }
   r.kind = kind;
   r.reserved = 0;
   newflag[c] = 0;
 }
 
+__device__ __forceinline__ bool same_key(const ngpu_result *out, const uint32_t *chunk_layer,
+                                         uint32_t id, const uint32_t d[8], uint32_t layer) {
+  return chunk_layer[id] == layer &&
+         digest_eq<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), id, d);
+}
+
 __global__ void dedup_insert(const ngpu_result *__restrict__ out, uint64_t n,
+                             const uint32_t *__restrict__ chunk_layer,
                              uint64_t *__restrict__ table, uint64_t mask) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (c >= n || out[c].kind == NGPU_DICT) return;
-  ht_insert_min<sizeof(ngpu_result)>(table, mask,
-                                     reinterpret_cast<const uint8_t *>(out), (uint32_t)c);
+  uint32_t d[8];
+  load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
+  const uint32_t layer = chunk_layer[c];
+  const uint32_t tag = digest_tag(d);
+  const uint32_t id = (uint32_t)c;
+  const uint64_t mine = ((uint64_t)tag << 32) | id;
+  for (uint64_t p = layer_bucket(d, layer) & mask;; p = (p + 1) & mask) {
+    uint64_t s = __hip_atomic_load(table + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s == kEmpty) {
+      const uint64_t old = atomicCAS((unsigned long long *)(table + p),
+                                     (unsigned long long)kEmpty, (unsigned long long)mine);
+      if (old == kEmpty) return;
+      s = old;
+    }
+    if ((uint32_t)(s >> 32) == tag && same_key(out, chunk_layer, (uint32_t)s, d, layer)) {
+      if ((uint32_t)s > id) atomicMin((unsigned long long *)(table + p), (unsigned long long)mine);
+      return;
+    }
+  }
 }
 
 __global__ void dedup_resolve(const ngpu_chunk *__restrict__ chunks, uint64_t n,
+                              const uint32_t *__restrict__ chunk_layer,
                               const uint64_t *__restrict__ table, uint64_t mask,
                               ngpu_result *__restrict__ out, uint32_t align,
                               uint64_t *__restrict__ newflag,
                               uint64_t *__restrict__ uoff,
-                              uint32_t *__restrict__ own_first) {
+                              uint32_t *__restrict__ blob_first, uint32_t n_blobs) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (c >= n) return;
   ngpu_result &r = out[c];
@@ -159,8 +204,17 @@ __global__ void dedup_resolve(const ngpu_chunk *__restrict__ chunks, uint64_t n,
   if (r.kind == NGPU_DICT) return;
   uint32_t d[8];
   load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
-  const uint32_t f = ht_lookup<sizeof(ngpu_result)>(
-      table, mask, reinterpret_cast<const uint8_t *>(out), d);
+  const uint32_t layer = chunk_layer[c];
+  const uint32_t tag = digest_tag(d);
+  uint32_t f = kNone;
+  for (uint64_t p = layer_bucket(d, layer) & mask;; p = (p + 1) & mask) {
+    const uint64_t s = table[p];
+    if (s == kEmpty) break;
+    if ((uint32_t)(s >> 32) == tag && same_key(out, chunk_layer, (uint32_t)s, d, layer)) {
+      f = (uint32_t)s;
+      break;
+    }
+  }
   const uint32_t len = chunks[c].length;
   if (f != (uint32_t)c && f != kNone && chunks[f].length == len) {
     r.kind = NGPU_INTRA;
@@ -171,57 +225,72 @@ __global__ void dedup_resolve(const ngpu_chunk *__restrict__ chunks, uint64_t n,
   r.ref = c;
   newflag[c] = 1;
   uoff[c] = ((uint64_t)len + align - 1) / align * align;
-  atomicMin(own_first, (uint32_t)c);
+  atomicMin(blob_first + (uint64_t)layer * (n_blobs + 1) + n_blobs, (uint32_t)c);
 }
 
-// Blob-table order: each dict blob gets a real index at its first hit, the
-// layer's own blob at its first NEW chunk ([nydus v2.3.0] BlobManager
-// alloc_index / get_or_create_current_blob).  nb <= a few thousand.
-__global__ void blob_rank(const uint32_t *__restrict__ first, uint32_t nb_plus_own,
-                          uint32_t *__restrict__ real, uint64_t *__restrict__ stats) {
-  for (uint32_t b = threadIdx.x; b < nb_plus_own; b += blockDim.x) {
+// Blob-table order per layer (one workgroup per layer): each dict blob gets a
+// real index at its first hit, the layer's own blob at its first NEW chunk
+// ([nydus v2.3.0] BlobManager alloc_index / get_or_create_current_blob).
+__global__ void blob_rank(const uint32_t *__restrict__ first_all, uint32_t nbo,
+                          uint32_t *__restrict__ real_all, const uint64_t *__restrict__ lfirst,
+                          const uint64_t *__restrict__ newidx, const uint64_t *__restrict__ uoff,
+                          ngpu_layer_stats *__restrict__ st) {
+  const uint64_t l = blockIdx.x;
+  const uint32_t *first = first_all + l * nbo;
+  uint32_t *real = real_all + l * nbo;
+  for (uint32_t b = threadIdx.x; b < nbo; b += blockDim.x) {
     const uint32_t fb = first[b];
     uint32_t rank = kNone;
     if (fb != kNone) {
       rank = 0;
-      for (uint32_t o = 0; o < nb_plus_own; ++o) rank += first[o] < fb;
+      for (uint32_t o = 0; o < nbo; ++o) rank += first[o] < fb;
     }
     real[b] = rank;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t used = 0;
-    for (uint32_t b = 0; b < nb_plus_own; ++b) used += first[b] != kNone;
-    stats[5] = real[nb_plus_own - 1];  // own blob (kNone -> 0xFFFFFFFF)
-    stats[6] = used;
+    for (uint32_t b = 0; b < nbo; ++b) used += first[b] != kNone;
+    const uint64_t a = lfirst[l], e = lfirst[l + 1];
+    st[l].chunks = e - a;
+    st[l].new_chunks = newidx[e] - newidx[a];
+    st[l].own_blob_index = real[nbo - 1];  // kNone -> 0xFFFFFFFF
+    st[l].blobs = used;
+    st[l].uncompressed_size = uoff[e] - uoff[a];
   }
 }
 
 __global__ void dedup_finalize(const ngpu_chunk *__restrict__ chunks, uint64_t n,
+                               const uint32_t *__restrict__ chunk_layer,
+                               const uint64_t *__restrict__ lfirst,
                                const uint64_t *__restrict__ newidx,
                                const uint64_t *__restrict__ uoff,
-                               const uint32_t *__restrict__ real, uint32_t own_slot,
+                               const uint32_t *__restrict__ real_all, uint32_t nbo,
                                ngpu_result *__restrict__ out,
-                               uint64_t *__restrict__ stats) {
+                               ngpu_layer_stats *__restrict__ st) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c == 0) { stats[0] = n; stats[8] = uoff[n]; stats[1] = newidx[n]; }
   if (c >= n) return;
   ngpu_result &r = out[c];
-  const uint32_t own = real[own_slot];
+  const uint32_t layer = chunk_layer[c];
+  const uint32_t *real = real_all + (uint64_t)layer * nbo;
+  const uint64_t a = lfirst[layer];
+  const uint64_t ib = newidx[a], ob = uoff[a];
+  const uint32_t own = real[nbo - 1];
+  ngpu_layer_stats &ls = st[layer];
   if (r.kind == NGPU_NEW) {
-    r.index = (uint32_t)newidx[c];
-    r.uncompressed_offset = uoff[c];
+    r.index = (uint32_t)(newidx[c] - ib);
+    r.uncompressed_offset = uoff[c] - ob;
     r.blob_index = own;
-    atomicAdd((unsigned long long *)(stats + 4), (unsigned long long)chunks[c].length);
+    atomicAdd((unsigned long long *)&ls.new_bytes, (unsigned long long)chunks[c].length);
   } else if (r.kind == NGPU_INTRA) {
     const uint64_t f = r.ref;
-    r.index = (uint32_t)newidx[f];
-    r.uncompressed_offset = uoff[f];
+    r.index = (uint32_t)(newidx[f] - ib);
+    r.uncompressed_offset = uoff[f] - ob;
     r.blob_index = own;
-    atomicAdd((unsigned long long *)(stats + 2), 1ull);
+    atomicAdd((unsigned long long *)&ls.intra_chunks, 1ull);
   } else {
     r.blob_index = real[r.blob_index];
-    atomicAdd((unsigned long long *)(stats + 3), 1ull);
+    atomicAdd((unsigned long long *)&ls.dict_chunks, 1ull);
   }
 }
 
@@ -294,7 +363,16 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply(uint64_t *__restrict_
   }
 }
 
+__global__ void set_single_layer(uint64_t *lfirst, uint64_t n) {
+  lfirst[0] = 0;
+  lfirst[1] = n;
+}
+
 }  // namespace
+
+void launch_set_single_layer(uint64_t *lfirst, uint64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(set_single_layer, dim3(1), dim3(1), 0, s, lfirst, n);
+}
 
 uint64_t scan_tmp_words(uint64_t n) { return (n + 1 + kScanTile - 1) / kScanTile + 1; }
 
@@ -324,30 +402,38 @@ void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
 
 void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                   const ngpu_dict_hit *hits, uint32_t n_blobs, uint32_t align,
-                  Workspace &ws, ngpu_result *out, hipStream_t s) {
-  const uint32_t nbo = n_blobs + 1;  // dict blobs + own blob (last slot)
-  hipMemsetAsync(ws.blob_first, 0xFF, sizeof(uint32_t) * nbo, s);
+                  const uint64_t *lfirst, uint64_t L, Workspace &ws, ngpu_result *out,
+                  ngpu_layer_stats *st, hipStream_t s) {
+  const uint32_t nbo = n_blobs + 1;  // dict blobs + own blob (last slot), per layer
+  (void)hipMemsetAsync(ws.blob_first, 0xFF, sizeof(uint32_t) * nbo * L, s);
+  (void)hipMemsetAsync(st, 0, sizeof(ngpu_layer_stats) * L, s);
   if (n) {
-    hipMemsetAsync(ws.intra, 0xFF, ws.intra_cap * sizeof(uint64_t), s);
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(dedup_probe, dim3(blocks), dim3(256), 0, s, chunks, n, dict, hits, out,
-                       ws.newflag, ws.blob_first, n_blobs);
-    hipLaunchKernelGGL(dedup_insert, dim3(blocks), dim3(256), 0, s, out, n, ws.intra,
-                       ws.intra_cap - 1);
-    hipLaunchKernelGGL(dedup_resolve, dim3(blocks), dim3(256), 0, s, chunks, n, ws.intra,
-                       ws.intra_cap - 1, out, align, ws.newflag, ws.uoff,
-                       ws.blob_first + n_blobs);
+    {
+      const uint64_t waves = L < 16384 ? L : 16384;
+      hipLaunchKernelGGL(layer_fill, dim3((unsigned)((waves * 64 + 255) / 256)), dim3(256), 0, s,
+                         lfirst, L, ws.chunk_layer);
+    }
+    (void)hipMemsetAsync(ws.intra, 0xFF, ws.intra_cap * sizeof(uint64_t), s);
+    hipLaunchKernelGGL(dedup_probe, dim3(blocks), dim3(256), 0, s, chunks, n, dict, hits,
+                       ws.chunk_layer, out, ws.newflag, ws.blob_first, n_blobs);
+    hipLaunchKernelGGL(dedup_insert, dim3(blocks), dim3(256), 0, s, out, n, ws.chunk_layer,
+                       ws.intra, ws.intra_cap - 1);
+    hipLaunchKernelGGL(dedup_resolve, dim3(blocks), dim3(256), 0, s, chunks, n, ws.chunk_layer,
+                       ws.intra, ws.intra_cap - 1, out, align, ws.newflag, ws.uoff,
+                       ws.blob_first, n_blobs);
   } else {
-    hipMemsetAsync(ws.newflag, 0, sizeof(uint64_t), s);
-    hipMemsetAsync(ws.uoff, 0, sizeof(uint64_t), s);
+    (void)hipMemsetAsync(ws.newflag, 0, sizeof(uint64_t), s);
+    (void)hipMemsetAsync(ws.uoff, 0, sizeof(uint64_t), s);
   }
   launch_scan_u64(ws.newflag, n, ws.scan_tmp, s);
   launch_scan_u64(ws.uoff, n, ws.scan_tmp, s);
-  hipLaunchKernelGGL(blob_rank, dim3(1), dim3(256), 0, s, ws.blob_first, nbo, ws.blob_real,
-                     ws.stats);
-  const unsigned blocks = (unsigned)((n + 255) / 256) + 1;
-  hipLaunchKernelGGL(dedup_finalize, dim3(blocks), dim3(256), 0, s, chunks, n, ws.newflag,
-                     ws.uoff, ws.blob_real, n_blobs, out, ws.stats);
+  hipLaunchKernelGGL(blob_rank, dim3((unsigned)L), dim3(256), 0, s, ws.blob_first, nbo,
+                     ws.blob_real, lfirst, ws.newflag, ws.uoff, st);
+  if (n)
+    hipLaunchKernelGGL(dedup_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       chunks, n, ws.chunk_layer, lfirst, ws.newflag, ws.uoff, ws.blob_real,
+                       nbo, out, st);
 }
 
 }  // namespace ngpu

@@ -69,11 +69,12 @@ int pick_group_log2(const ngpu_engine *e, uint64_t data_len) {
 }
 
 int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
-                     uint32_t n_blobs) {
+                     uint32_t n_blobs, uint64_t L) {
   Workspace &ws = e->ws;
   if (n + 1 > ws.cap_n || !ws.groups) {
     uint64_t cn = n + 1 < 4096 ? 4096 : n + 1;
-    uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+    if (grow(e, &ws.chunk_layer, c4, cn)) return NGPU_ENOMEM;
     if (grow(e, &ws.groups, c0, cn)) return NGPU_ENOMEM;
     if (grow(e, &ws.newflag, c1, cn)) return NGPU_ENOMEM;
     if (grow(e, &ws.uoff, c2, cn)) return NGPU_ENOMEM;
@@ -86,14 +87,20 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
     ws.cap_n = cn;
   }
   if (!ws.stats) {
-    uint64_t c = 0;
+    uint64_t c = 0, c1 = 0;
     if (grow(e, &ws.stats, c, 16)) return NGPU_ENOMEM;
+    if (grow(e, &ws.lfirst1, c1, 2)) return NGPU_ENOMEM;
   }
-  const uint64_t nb = (uint64_t)n_blobs + 1;
+  if (L > ws.cap_layers || !ws.lstats) {
+    uint64_t c = ws.cap_layers;
+    if (grow(e, &ws.lstats, c, L)) return NGPU_ENOMEM;
+    ws.cap_layers = c;
+  }
+  const uint64_t nb = ((uint64_t)n_blobs + 1) * (L ? L : 1);
   if (nb > ws.cap_blobs || !ws.blob_first) {
     uint64_t c0 = 0, c1 = 0;
-    if (ws.blob_first) hipFree(ws.blob_first), ws.blob_first = nullptr;
-    if (ws.blob_real) hipFree(ws.blob_real), ws.blob_real = nullptr;
+    if (ws.blob_first) (void)hipFree(ws.blob_first), ws.blob_first = nullptr;
+    if (ws.blob_real) (void)hipFree(ws.blob_real), ws.blob_real = nullptr;
     if (grow(e, &ws.blob_first, c0, nb)) return NGPU_ENOMEM;
     if (grow(e, &ws.blob_real, c1, nb)) return NGPU_ENOMEM;
     ws.cap_blobs = c0;
@@ -129,7 +136,7 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
                    const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
                    hipStream_t s) {
   const int D = pick_group_log2(e, len);
-  int rc = ensure_workspace(e, n, len, D, e->dict.n_blobs);
+  int rc = ensure_workspace(e, n, len, D, e->dict.n_blobs, 1);
   if (rc) return rc;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   // tuning override: flags bits 8..10 = 1 + BLAKE3 load mode (0 = default)
@@ -154,16 +161,20 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
 // Dedup stage: dict decisions (given hits or the engine's dict), intra-layer
 // dedup, NEW indices / offsets, blob order, stats.
 int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
-                  const ngpu_dict_hit *d_hits, uint32_t n_blobs, hipStream_t s) {
+                  const ngpu_dict_hit *d_hits, uint32_t n_blobs, hipStream_t s,
+                  const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats) {
   if (!d_hits) n_blobs = e->dict.n_blobs;
-  int rc = ensure_workspace(e, n, 0, 0, n_blobs);
+  if (!d_lfirst) L = 1;
+  int rc = ensure_workspace(e, n, 0, 0, n_blobs, L);
   if (rc) return rc;
+  if (!d_lfirst) {
+    launch_set_single_layer(e->ws.lfirst1, n, s);
+    d_lfirst = e->ws.lfirst1;
+  }
+  if (!d_stats) d_stats = e->ws.lstats;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   const uint32_t align = e->cfg.fs_version == 6 ? 4096u : 1u;
-  // reset the dedup counters; stats[7] (bad descriptors) belongs to the digest stage
-  HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 7 * sizeof(uint64_t), s));
-  HIP_TRY(e, hipMemsetAsync(e->ws.stats + 8, 0, 8 * sizeof(uint64_t), s));
-  launch_dedup(d_chunks, n, e->dict, d_hits, n_blobs, align, e->ws, d_out, s);
+  launch_dedup(d_chunks, n, e->dict, d_hits, n_blobs, align, d_lfirst, L, e->ws, d_out, d_stats, s);
   if (tm) HIP_TRY(e, hipEventRecord(e->ev[4], s));
   HIP_TRY(e, hipGetLastError());
   e->timed = tm && n > 0;
@@ -175,26 +186,21 @@ int enqueue(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
             hipStream_t s) {
   int rc = enqueue_digest(e, d_data, len, d_chunks, n, d_out, s);
   if (rc) return rc;
-  return enqueue_dedup(e, d_chunks, n, d_out, nullptr, 0, s);
+  return enqueue_dedup(e, d_chunks, n, d_out, nullptr, 0, s, nullptr, 1, nullptr);
 }
 
+// Layer stats of a single-layer call (internal lstats[0]) + the digest
+// stage's bad-descriptor counter.
 int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st) {
   HIP_TRY(e, hipMemcpyAsync(e->h_stats, e->ws.stats, 16 * sizeof(uint64_t),
                             hipMemcpyDeviceToHost, s));
+  HIP_TRY(e, hipMemcpyAsync(e->h_stats + 16, e->ws.lstats, sizeof(ngpu_layer_stats),
+                            hipMemcpyDeviceToHost, s));
   HIP_TRY(e, hipStreamSynchronize(s));
-  const uint64_t *h = e->h_stats;
-  if (h[7]) return fail(e, NGPU_EINVAL, "%llu chunk descriptor(s) outside the data buffer",
-                        (unsigned long long)h[7]);
-  if (st) {
-    st->chunks = h[0];
-    st->new_chunks = h[1];
-    st->intra_chunks = h[2];
-    st->dict_chunks = h[3];
-    st->new_bytes = h[4];
-    st->own_blob_index = (uint32_t)h[5];
-    st->blobs = (uint32_t)h[6];
-    st->uncompressed_size = h[8];
-  }
+  if (e->h_stats[7])
+    return fail(e, NGPU_EINVAL, "%llu chunk descriptor(s) outside the data buffer",
+                (unsigned long long)e->h_stats[7]);
+  if (st) memcpy(st, e->h_stats + 16, sizeof(ngpu_layer_stats));
   return 0;
 }
 
@@ -247,7 +253,7 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
       }
   if (
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc((void **)&e->h_stats, 16 * sizeof(uint64_t), hipHostMallocDefault) !=
+      hipHostMalloc((void **)&e->h_stats, 32 * sizeof(uint64_t), hipHostMallocDefault) !=
           hipSuccess) {
     delete e;
     return NGPU_EHIP;
@@ -263,7 +269,8 @@ void ngpu_destroy(ngpu_engine *e) {
   free_dict(e);
   Workspace &ws = e->ws;
   void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.scan_tmp,
-                  ws.intra, ws.blob_first, ws.blob_real, ws.stats,
+                  ws.intra, ws.blob_first, ws.blob_real, ws.stats, ws.chunk_layer,
+                  ws.lfirst1, ws.lstats,
                   e->d_data, e->d_chunks, e->d_results};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
@@ -402,10 +409,39 @@ int ngpu_dedup_device(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n,
   std::lock_guard<std::mutex> g(e->mu);
   hipSetDevice(e->device);
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  int rc = enqueue_dedup(e, d_chunks, n, d_out, d_hits, n_dict_blobs, s);
+  int rc = enqueue_dedup(e, d_chunks, n, d_out, d_hits, n_dict_blobs, s, nullptr, 1, nullptr);
   if (rc) return rc;
   if (stats) return read_stats(e, s, stats);
   return 0;
+}
+
+int ngpu_dedup_layers_device(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n,
+                             ngpu_result *d_out, const ngpu_dict_hit *d_hits,
+                             uint32_t n_dict_blobs, const uint64_t *d_layer_first,
+                             uint64_t n_layers, ngpu_layer_stats *d_stats, void *stream) {
+  if (!e || !d_layer_first || n_layers == 0 || (n && (!d_chunks || !d_out))) return NGPU_EINVAL;
+  if (n >= 0xFFFFFFFFull || n_layers >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too large");
+  if (d_hits && n_dict_blobs == 0) n_dict_blobs = e->dict.n_blobs ? e->dict.n_blobs : 1;
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  return enqueue_dedup(e, d_chunks, n, d_out, d_hits, n_dict_blobs,
+                       stream ? (hipStream_t)stream : e->stream, d_layer_first, n_layers,
+                       d_stats);
+}
+
+int ngpu_process_layers_device(ngpu_engine *e, const void *d_data, uint64_t len,
+                               const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+                               const uint64_t *d_layer_first, uint64_t n_layers,
+                               ngpu_layer_stats *d_stats, void *stream) {
+  if (!e || !d_layer_first || n_layers == 0 || (n && (!d_data || !d_chunks || !d_out)))
+    return NGPU_EINVAL;
+  if (n >= 0xFFFFFFFFull || n_layers >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too large");
+  std::lock_guard<std::mutex> g(e->mu);
+  hipSetDevice(e->device);
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  int rc = enqueue_digest(e, (const uint8_t *)d_data, len, d_chunks, n, d_out, s);
+  if (rc) return rc;
+  return enqueue_dedup(e, d_chunks, n, d_out, nullptr, 0, s, d_layer_first, n_layers, d_stats);
 }
 
 int ngpu_dict_clear(ngpu_engine *e) {

@@ -37,11 +37,14 @@ namespace ngpu {
 
 int fail(ngpu_engine *e, int code, const char *fmt, ...);
 int pick_group_log2(const ngpu_engine *e, uint64_t data_len);
-int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D, uint32_t n_blobs);
+int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D, uint32_t n_blobs,
+                     uint64_t L);
 int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
                    const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out, hipStream_t s);
+// d_lfirst == nullptr: one layer of n chunks (stats -> internal lstats[0]).
 int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
-                  const ngpu_dict_hit *d_hits, uint32_t n_blobs, hipStream_t s);
+                  const ngpu_dict_hit *d_hits, uint32_t n_blobs, hipStream_t s,
+                  const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats);
 int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st);
 
 }  // namespace ngpu

@@ -179,7 +179,7 @@ int ngpu_pack_open(ngpu_engine *e, ngpu_pack **out) {
          hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
   }
   // size the digest workspace once so no slot dispatch reallocates it
-  if (ok) ok = ensure_workspace(e, p->max_ch, cap, pick_group_log2(e, cap), e->dict.n_blobs) == 0;
+  if (ok) ok = ensure_workspace(e, p->max_ch, cap, pick_group_log2(e, cap), e->dict.n_blobs, 1) == 0;
   if (!ok) {
     release(p);
     return fail(e, NGPU_ENOMEM, "pack: staging allocation failed");
@@ -264,7 +264,7 @@ int ngpu_pack_close(ngpu_pack *p, ngpu_chunk **chunks_out, ngpu_result **results
                          e->stream) != hipSuccess)
         rc = fail(e, NGPU_EHIP, "pack: chunk table copy failed");
     }
-    if (!rc) rc = enqueue_dedup(e, p->d_all, n, p->d_res, nullptr, 0, e->stream);
+    if (!rc) rc = enqueue_dedup(e, p->d_all, n, p->d_res, nullptr, 0, e->stream, nullptr, 1, nullptr);
     if (!rc && n &&
         hipMemcpyAsync(res, p->d_res, n * sizeof(ngpu_result), hipMemcpyDeviceToHost,
                        e->stream) != hipSuccess)

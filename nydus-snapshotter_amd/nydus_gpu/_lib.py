@@ -36,7 +36,12 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_chunk_table", "ngpu_last_timing", "ngpu_digest_device",
            "ngpu_dict_probe_device", "ngpu_dedup_device", "ngpu_dict_load_device",
            "ngpu_pack_open", "ngpu_pack_write", "ngpu_pack_reserve", "ngpu_pack_commit",
-           "ngpu_pack_close", "ngpu_pack_abort"]
+           "ngpu_pack_close", "ngpu_pack_abort", "ngpu_dedup_layers_device",
+           "ngpu_process_layers_device"]
+
+LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
+                              ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
+                              ("blobs", "<u4"), ("uncompressed_size", "<u8")])
 
 HIT_DTYPE = np.dtype([("entry", "<u4"), ("index", "<u4"), ("blob", "<u4"), ("usize", "<u4")])
 MISS = 0xFFFFFFFF
@@ -117,6 +122,8 @@ def lib():
     L.ngpu_dict_probe_device.argtypes = [vp, vp, u64, u64, vp, vp]
     L.ngpu_dedup_device.argtypes = [vp, vp, u64, vp, vp, u32, vp, ctypes.POINTER(NgpuLayerStats)]
     L.ngpu_dict_load_device.argtypes = [vp, vp, vp, vp, vp, u64, u32]
+    L.ngpu_dedup_layers_device.argtypes = [vp, vp, u64, vp, vp, u32, vp, u64, vp, vp]
+    L.ngpu_process_layers_device.argtypes = [vp, vp, u64, vp, u64, vp, vp, u64, vp, vp]
     L.ngpu_pack_open.argtypes = [vp, ctypes.POINTER(vp)]
     L.ngpu_pack_write.argtypes = [vp, vp, u64]
     L.ngpu_pack_reserve.argtypes = [vp, ctypes.POINTER(vp), pu64]
@@ -273,6 +280,22 @@ class Engine:
                                             self._vp(d_hits), n_dict_blobs, self._vp(stream),
                                             ctypes.byref(st) if want_stats else None), "dedup_device")
         return st.as_dict() if want_stats else None
+
+    def dedup_layers_device(self, d_chunks: int, n: int, d_out: int, d_layer_first: int,
+                            n_layers: int, d_stats: int = 0, d_hits: int = 0, n_dict_blobs: int = 0,
+                            stream: int = 0):
+        self._check(lib().ngpu_dedup_layers_device(self._h, self._vp(d_chunks), n, self._vp(d_out),
+                                                   self._vp(d_hits), n_dict_blobs,
+                                                   self._vp(d_layer_first), n_layers, self._vp(d_stats),
+                                                   self._vp(stream)), "dedup_layers_device")
+
+    def process_layers_device(self, d_data: int, length: int, d_chunks: int, n: int, d_out: int,
+                              d_layer_first: int, n_layers: int, d_stats: int = 0, stream: int = 0):
+        self._check(lib().ngpu_process_layers_device(self._h, self._vp(d_data), length,
+                                                     self._vp(d_chunks), n, self._vp(d_out),
+                                                     self._vp(d_layer_first), n_layers,
+                                                     self._vp(d_stats), self._vp(stream)),
+                    "process_layers_device")
 
     def dict_load_device(self, d_digests: int, d_usize: int, d_blob: int, d_index: int, n: int,
                          n_blobs: int):

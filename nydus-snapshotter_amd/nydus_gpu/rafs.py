@@ -35,6 +35,18 @@ assert CHUNK_INFO_DTYPE.itemsize == 80
 
 CHUNK_FLAG_COMPRESSED = 0x1
 
+# RAFS v6 blob table entry (256 B), decoded from the same fixture: 64 ASCII hex
+# chars of blob id, then blob_index, chunk_size, chunk_count,
+# compression_algo, digest_algo, features (u32 each), compressed_size,
+# uncompressed_size (u64), rest meta-info fields (zero here).
+BLOB_DTYPE = np.dtype([("blob_id", "S64"), ("blob_index", "<u4"), ("chunk_size", "<u4"),
+                       ("chunk_count", "<u4"), ("compression_algo", "<u4"), ("digest_algo", "<u4"),
+                       ("features", "<u4"), ("compressed_size", "<u8"), ("uncompressed_size", "<u8"),
+                       ("reserved", "u1", (152,))])
+assert BLOB_DTYPE.itemsize == 256
+DIGEST_ALGO = {"blake3": 0, "sha256": 1}
+COMPRESSOR_NONE = 0
+
 
 def detect_fs_version(header: bytes) -> str:
     """Port of DetectFsVersion (pkg/layout/layout.go:60-76)."""
@@ -55,8 +67,11 @@ def read_v6(boot: bytes) -> dict:
     if cts % 80:
         raise ValueError("chunk table size is not a multiple of 80")
     table = np.frombuffer(boot, dtype=CHUNK_INFO_DTYPE, count=cts // 80, offset=cto).copy()
+    blobs = np.frombuffer(boot, dtype=BLOB_DTYPE, count=bts // 256, offset=bto).copy() if bts else \
+        np.zeros(0, BLOB_DTYPE)
     return {"flags": flags, "blob_table_offset": bto, "blob_table_size": bts, "chunk_size": cs,
-            "chunk_table_offset": cto, "chunk_table_size": cts, "chunks": table}
+            "chunk_table_offset": cto, "chunk_table_size": cts, "chunks": table, "blobs": blobs,
+            "blob_ids": [b.decode() for b in blobs["blob_id"]]}
 
 
 def read_v6_from_targz(path: str) -> dict:
@@ -68,14 +83,34 @@ def read_v6_from_targz(path: str) -> dict:
     raise ValueError("no image.boot in archive")
 
 
-def write_v6_bootstrap(records: np.ndarray, chunk_size: int, flags: int = 0x4) -> bytes:
-    """Minimal RAFS v6 bootstrap holding only the super blocks + a chunk table
-    (enough for ChunkDictPath loading and chunk-table comparison)."""
+def make_blob_table(blob_ids, chunk_size, counts=None, digester="blake3", sizes=None) -> np.ndarray:
+    t = np.zeros(len(blob_ids), BLOB_DTYPE)
+    for i, bid in enumerate(blob_ids):
+        t[i]["blob_id"] = bid.encode() if isinstance(bid, str) else bid
+        t[i]["blob_index"] = i
+        t[i]["chunk_size"] = chunk_size
+        t[i]["chunk_count"] = counts[i] if counts is not None else 0
+        t[i]["compression_algo"] = COMPRESSOR_NONE
+        t[i]["digest_algo"] = DIGEST_ALGO[digester]
+        if sizes is not None:
+            t[i]["compressed_size"] = t[i]["uncompressed_size"] = sizes[i]
+    return t
+
+
+def write_v6_bootstrap(records: np.ndarray, chunk_size: int, flags: int = 0x4,
+                       blobs: np.ndarray = None) -> bytes:
+    """Minimal RAFS v6 bootstrap: super blocks + blob table (at 0x1000, as in
+    the reference fixture) + chunk table.  Enough for ChunkDictPath loading,
+    Merge's blob bookkeeping and chunk-table comparison (no inodes)."""
     recs = np.ascontiguousarray(records).view(CHUNK_INFO_DTYPE)
-    cto = 4096
+    blobs = np.zeros(0, BLOB_DTYPE) if blobs is None else np.ascontiguousarray(blobs, BLOB_DTYPE)
+    bto = 4096
+    cto = bto + (blobs.nbytes + 4095) // 4096 * 4096
     buf = bytearray(cto + recs.nbytes)
     struct.pack_into("<I", buf, SUPER_OFFSET, RAFS_V6_MAGIC)
-    struct.pack_into("<QQIIQQQI", buf, EXT_OFFSET, flags, 0, 0, chunk_size, cto, recs.nbytes, 0, 0)
+    struct.pack_into("<QQIIQQQI", buf, EXT_OFFSET, flags, bto if blobs.size else 0, blobs.nbytes,
+                     chunk_size, cto, recs.nbytes, 0, 0)
+    buf[bto:bto + blobs.nbytes] = blobs.tobytes()
     buf[cto:] = recs.tobytes()
     return bytes(buf)
 

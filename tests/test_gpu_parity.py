@@ -482,3 +482,86 @@ def test_streaming_pack_errors(tars):
         assert len(ch) == 0 and st["chunks"] == 0
     finally:
         eng.close()
+
+
+def test_multi_layer_dedup_matches_per_layer(oracle):
+    """One launch set over 40 layers == each layer packed alone (oracle per
+    layer), with a shared chunk dict and cross-layer duplicate contents."""
+    import torch
+    rng = np.random.default_rng(31)
+    data, ch = _random_layer(rng, 40 << 20, 0x10000, dup_frac=0.4)
+    n = len(ch)
+    cuts = np.sort(rng.choice(np.arange(1, n), 39, replace=False))
+    first = np.concatenate([[0], cuts, [n]]).astype(np.uint64)
+    first[5] = first[4]  # an empty layer
+    dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    pick = rng.choice(n, n // 5, replace=False)
+    dd, ds = dig[pick], ch["length"][pick].astype(np.uint32)
+    db = (np.arange(len(pick)) % 5).astype(np.uint32)
+    di = np.arange(len(pick), dtype=np.uint32)
+    eng = nydus_gpu.Engine(chunk_size=0x10000)
+    try:
+        eng.dict_load(dd, ds, db, di)
+        d_data, d_ch = _to_dev(np.frombuffer(data, np.uint8)), _to_dev(ch)
+        d_first = torch.from_numpy(first.view(np.int64).copy()).cuda()
+        out = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+        st = torch.zeros(40 * nydus_gpu.LAYER_STATS_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        eng.process_layers_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), n, out.data_ptr(),
+                                  d_first.data_ptr(), 40, st.data_ptr())
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+        stats = st.cpu().numpy().view(nydus_gpu.LAYER_STATS_DTYPE)
+    finally:
+        eng.close()
+    assert np.array_equal(got["digest"], dig)
+    for l in range(40):
+        a, b = int(first[l]), int(first[l + 1])
+        exp, own = oracle.dedup(dig[a:b], ch["length"][a:b], dd, ds, db, di)
+        g = got[a:b]
+        assert np.array_equal(g["kind"], exp["kind"]), l
+        assert np.array_equal(g["index"], exp["index"]), l
+        assert np.array_equal(g["blob_index"], exp["blob_index"]), l
+        assert np.array_equal(g["uncompressed_offset"], exp["uncompressed_offset"]), l
+        # refs: DICT -> dict entry, INTRA/NEW -> chunk id (global in the call)
+        r = exp["ref"].astype(np.int64)
+        r[exp["kind"] != 2] += a
+        assert np.array_equal(g["ref"].astype(np.int64), r), l
+        assert stats[l]["chunks"] == b - a
+        assert stats[l]["new_chunks"] == (exp["kind"] == 0).sum()
+        assert stats[l]["intra_chunks"] == (exp["kind"] == 1).sum()
+        assert stats[l]["dict_chunks"] == (exp["kind"] == 2).sum()
+        assert stats[l]["own_blob_index"] == (0xFFFFFFFF if own is None else own)
+
+
+def test_converter_testpack_flow(tars, tmp_path):
+    """tests/converter_test.go:420-528 through the converter mirror:
+    buildChunkDict (Pack + Merge), Pack lower/upper against the dict bootstrap,
+    Merge -> blob list [dict blob, upper blob]."""
+    import io as _io
+    from nydus_gpu import converter as cv
+
+    def pack(tar, dict_path=""):
+        out = _io.BytesIO()
+        w = cv.Pack(out, cv.PackOption(FsVersion="6", ChunkDictPath=dict_path))
+        for a in range(0, len(tar), 100_000):
+            w.write(tar[a:a + 100_000])
+        res = w.close()
+        return out.getvalue(), res
+
+    dict_boot, dres = pack(tars["chunk_dict"])
+    merged = _io.BytesIO()
+    blobs = cv.Merge([dict_boot], merged, cv.MergeOption())
+    assert blobs == ["sha256:" + dres["own_blob_id"]]          # converter_test.go:440
+    dict_path = str(tmp_path / "dict-bootstrap")
+    with open(dict_path, "wb") as f:
+        f.write(merged.getvalue())
+
+    lower_boot, lres = pack(tars["oci_lower"], dict_path)
+    upper_boot, ures = pack(tars["oci_upper"], dict_path)
+    assert (lres["results"]["kind"] == nydus_gpu.DICT).all()
+    assert lres["blob_ids"] == [dres["own_blob_id"]]
+    out = _io.BytesIO()
+    blobs = cv.Merge([lower_boot, upper_boot], out, cv.MergeOption(ChunkDictPath=dict_path))
+    assert blobs == ["sha256:" + dres["own_blob_id"], "sha256:" + ures["own_blob_id"]]  # :513-519
+    b = rafs.read_v6(out.getvalue())
+    assert b["blob_ids"] == [dres["own_blob_id"], ures["own_blob_id"]]

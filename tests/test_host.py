@@ -102,3 +102,31 @@ def test_chunk_table_writer(oracle, tars):
     back = rafs.read_v6(boot)
     assert rafs.canonical(back["chunks"]) == rafs.canonical(recs)
     assert rafs.detect_fs_version(boot) == "v6"
+
+
+def test_converter_options():
+    from nydus_gpu import converter as cv
+    assert cv.parse_chunk_size("") == 0x100000
+    assert cv.parse_chunk_size("0x10000") == 0x10000
+    assert cv.parse_chunk_size("4096") == 4096
+    for bad in ("0x800", "0x1001", "0x2000000"):
+        with pytest.raises(cv.ConverterError):
+            cv.parse_chunk_size(bad)
+
+
+def test_merge_blob_bookkeeping():
+    """Merge returns blobs in first-appearance order; chunk blob indices are
+    remapped into the merged blob table (builder.go:220-294 output JSON)."""
+    import io as _io
+    from nydus_gpu import converter as cv
+    recs = np.zeros(3, rafs.CHUNK_INFO_DTYPE)
+    recs["blob_index"] = [0, 1, 1]
+    a = rafs.write_v6_bootstrap(recs, 0x100000, blobs=rafs.make_blob_table(["aa" * 32, "bb" * 32], 0x100000))
+    recs2 = np.zeros(1, rafs.CHUNK_INFO_DTYPE)
+    b = rafs.write_v6_bootstrap(recs2, 0x100000, blobs=rafs.make_blob_table(["cc" * 32], 0x100000))
+    c = rafs.write_v6_bootstrap(recs2, 0x100000, blobs=rafs.make_blob_table(["bb" * 32], 0x100000))
+    out = _io.BytesIO()
+    blobs = cv.Merge([a, b, c], out, cv.MergeOption())
+    assert blobs == ["sha256:" + "aa" * 32, "sha256:" + "bb" * 32, "sha256:" + "cc" * 32]
+    m = rafs.read_v6(out.getvalue())
+    assert list(m["chunks"]["blob_index"]) == [0, 1, 1, 2, 1]
