@@ -133,6 +133,12 @@ WORKLOADS = {
                     "digest prefix over the GPUs, probes routed by all-to-all",
                n_files=4096, file_size=4 * MiB, chunk=MiB, digester="blake3", layers=16,
                pool=1024, dict_entries=16_000_000, sharded=True),
+    "c5-1000": dict(desc="C5: 1000 layers x 64 MiB (16 x 4 MiB files), 64 KiB chunks, blake3, 30% of "
+                         "chunks from a shared pool of 1024 contents; chunk dict (pool + 1M filler) "
+                         "partitioned by digest prefix; layers split over the GPUs; one multi-layer "
+                         "dedup launch set per step",
+                    n_files=16, file_size=4 * MiB, chunk=64 * 1024, digester="blake3",
+                    layers_total=1000, pool=1024, dict_entries=1_000_000, sharded=True),
     "c5": dict(desc="C5-shape: 16 GiB layer, 64 KiB chunks, blake3, no dict",
                n_files=1024, file_size=16 * MiB, chunk=64 * 1024, digester="blake3", layers=1),
     "small": dict(desc="1 GiB layer, 1 MiB chunks, blake3", n_files=256, file_size=4 * MiB,
@@ -232,6 +238,10 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     if args.dict_entries:
         wl["dict_entries"] = args.dict_entries
+    if wl.get("layers_total"):  # split the layer set over the ranks
+        mine = len(range(rank, wl["layers_total"], world))
+        wl["layers"] = mine
+        wl["n_files"] = wl["n_files"] * mine
     buf, ch = build_layer_on_gpu(torch, wl["n_files"], wl["file_size"], wl["chunk"], seed=0x6E79647573 + rank)
     _, stride, _, _ = synthetic_layout(1, wl["file_size"], wl["chunk"])
     n = len(ch)

@@ -90,6 +90,7 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
     uint64_t c = 0, c1 = 0;
     if (grow(e, &ws.stats, c, 16)) return NGPU_ENOMEM;
     if (grow(e, &ws.lfirst1, c1, 2)) return NGPU_ENOMEM;
+    HIP_TRY(e, hipMemset(ws.stats, 0, c * sizeof(uint64_t)));  // no stale error counter
   }
   if (L > ws.cap_layers || !ws.lstats) {
     uint64_t c = ws.cap_layers;
