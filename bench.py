@@ -167,6 +167,22 @@ def plant_pool(torch, buf, ch, stride, wl, seed):
     return None, len(sel)
 
 
+def pmc_traffic(path, workload, kernel):
+    """HBM bytes per launch of the dominant kernel from a committed rocprofv3
+    PMC summary of the same bench command (scripts/gpu_pmc.sh ->
+    scripts/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected)."""
+    import glob
+    if not path:
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{workload}.json")))
+        path = cands[-1] if cands else ""
+    if not path or not os.path.exists(path):
+        return None, None
+    d = json.load(open(path))
+    if "traffic_bytes" not in d or kernel.split("<")[0] not in (d.get("kernel") or ""):
+        return None, None
+    return d["traffic_bytes"], os.path.relpath(path, ROOT)
+
+
 def end_to_end(torch, nydus_gpu, buf, wl, stride, device, sample_bytes=2 << 30):
     """PCIe-inclusive rates on the first `sample_files` files of the layer, held
     in engine-pinned host memory (never the headline value):
@@ -219,6 +235,8 @@ def main():
     ap.add_argument("--dict-entries", type=int, default=0, help="override dict size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--pmc-json", default="", help="PMC summary for roofline.traffic "
+                    "(default: newest profiles/r*/pmc_<workload>.json)")
     ap.add_argument("--cpu-sample-mib", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=0)
     args = ap.parse_args()
@@ -389,7 +407,7 @@ def main():
         blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).sum())
         ops = blocks * 1384  # SURVEY.md §8(d) SHA-256 op count
         achieved = ops / (dig_ms / 1e3)
-        roof = {"bound": "valu", "kernel": "sha256_chunks", "achieved": round(achieved / 1e12, 3),
+        roof = {"bound": "valu", "kernel": "sha256_split", "achieved": round(achieved / 1e12, 3),
                 "peak": round(PEAK_INT_OPS / 1e12, 3), "unit": "Tops/s",
                 "frac": round(achieved / PEAK_INT_OPS, 4), "traffic": None,
                 "hbm_gbs": round(file_bytes / (dig_ms / 1e3) / 1e9, 1),
@@ -398,6 +416,8 @@ def main():
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e and not wl.get("dict_entries"):
         e2e = end_to_end(torch, nydus_gpu, buf, wl, stride, local)
+
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(args.pmc_json, args.workload, roof["kernel"])
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
