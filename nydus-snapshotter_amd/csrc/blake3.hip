@@ -274,6 +274,7 @@ __global__ __launch_bounds__(256) void b3_groups(
   // Others publish their group CV for b3_tree.
   const bool inwg = st == 2 && tree_in_workgroup(base, ng);
   if (st == 2 && !inwg) {
+    if (j == 0) err[2] = 1;  // err + 2 == stats[9]: some chunk needs b3_tree
     uint4 *d = reinterpret_cast<uint4 *>(cv_out + g * 8);
     d[0] = make_uint4(cur[0], cur[1], cur[2], cur[3]);
     d[1] = make_uint4(cur[4], cur[5], cur[6], cur[7]);
@@ -323,9 +324,11 @@ constexpr int kTile = 1024;  // CVs per LDS tile (32 KiB)
 
 __global__ __launch_bounds__(kTreeThreads) void b3_tree(
     const uint64_t *__restrict__ gbase, uint64_t n, uint64_t cap_g,
-    uint32_t *__restrict__ cv, ngpu_result *__restrict__ out) {
+    uint32_t *__restrict__ cv, ngpu_result *__restrict__ out,
+    const uint64_t *__restrict__ needed) {
   __shared__ uint32_t t[kTile * 8];
   const int tid = threadIdx.x;
+  if (*needed == 0) return;  // every chunk was finished inside b3_groups
   for (uint64_t c = blockIdx.x; c < n; c += gridDim.x) {
     const uint64_t base = gbase[c];
     uint64_t k = gbase[c + 1] - base;
@@ -449,7 +452,7 @@ void launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
   {
     uint64_t blocks = n < 2048 ? n : 2048;
     hipLaunchKernelGGL(b3_tree, dim3((unsigned)blocks), dim3(kTreeThreads), 0, s,
-                       ws.groups, n, ws.cap_g, ws.cv, out);
+                       ws.groups, n, ws.cap_g, ws.cv, out, ws.stats + 9);
   }
 }
 
