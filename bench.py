@@ -214,7 +214,7 @@ def end_to_end(torch, nydus_gpu, buf, wl, stride, device, sample_bytes=2 << 30):
         for _ in range(reps):
             w = eng.pack()
             for a in range(0, host.size, 32 << 20):
-                w.write_zero_copy(host[a:a + (32 << 20)])
+                w.write(host[a:a + (32 << 20)])
             ch2, out2, st2 = w.close()
         res["streaming_gbs"] = round(file_bytes * reps / (time.perf_counter() - t0) / 1e9, 1)
         assert out2.tobytes() == out.tobytes()

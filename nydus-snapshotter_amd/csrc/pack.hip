@@ -20,6 +20,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <condition_variable>
+#include <thread>
 #include <vector>
 
 #include "engine_internal.hpp"
@@ -39,6 +41,59 @@ struct Slot {
   bool busy = false;
 };
 
+// A few persistent threads that split large host copies into the pinned
+// staging slot (one memcpy thread tops out well below PCIe Gen5 H2D).
+class CopyPool {
+ public:
+  explicit CopyPool(unsigned n) {
+    for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { work(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  unsigned size() const { return (unsigned)th_.size(); }
+  void copy(uint8_t *dst, const uint8_t *src, uint64_t n) {
+    const unsigned parts = size() + 1;
+    const uint64_t step = ((n + parts - 1) / parts + 4095) & ~4095ull;
+    std::unique_lock<std::mutex> g(m_);
+    for (uint64_t off = step; off < n; off += step)
+      jobs_.push_back({dst + off, src + off, off + step < n ? step : n - off});
+    pending_ = jobs_.size();
+    g.unlock();
+    cv_.notify_all();
+    memcpy(dst, src, step < n ? step : n);  // the caller takes the first part
+    g.lock();
+    done_.wait(g, [this] { return pending_ == 0; });
+  }
+
+ private:
+  struct Job { uint8_t *dst; const uint8_t *src; uint64_t n; };
+  void work() {
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [this] { return stop_ || !jobs_.empty(); });
+      if (stop_) return;
+      Job j = jobs_.back();
+      jobs_.pop_back();
+      g.unlock();
+      memcpy(j.dst, j.src, j.n);
+      g.lock();
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::vector<Job> jobs_;
+  uint64_t pending_ = 0;
+  bool stop_ = false;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+};
+
 }  // namespace
 
 struct ngpu_pack : TarSink {
@@ -53,6 +108,7 @@ struct ngpu_pack : TarSink {
   uint64_t res_cap = 0;
   ngpu_chunk *d_all = nullptr;
   hipStream_t copy = nullptr;
+  CopyPool *pool = nullptr;  // created on the first large write
   int err = 0;
 
   explicit ngpu_pack(ngpu_engine *eng) : e(eng), sc(eng->cfg.chunk_size) {}
@@ -85,6 +141,7 @@ void release(ngpu_pack *p) {
   if (p->d_res) (void)hipFree(p->d_res);
   if (p->d_all) (void)hipFree(p->d_all);
   if (p->copy) (void)hipStreamDestroy(p->copy);
+  delete p->pool;
   delete p;
 }
 
@@ -223,7 +280,15 @@ int ngpu_pack_write(ngpu_pack *p, const void *buf, uint64_t len) {
     int rc = ngpu_pack_reserve(p, &dst, &avail);
     if (rc) return rc;
     const uint64_t take = len < avail ? len : avail;
-    memcpy(dst, b, take);
+    if (take >= (8ull << 20)) {
+      if (!p->pool) {
+        unsigned hw = std::thread::hardware_concurrency();
+        p->pool = new CopyPool(hw >= 16 ? 7 : (hw > 2 ? hw / 2 - 1 : 1));
+      }
+      p->pool->copy((uint8_t *)dst, b, take);
+    } else {
+      memcpy(dst, b, take);
+    }
     rc = ngpu_pack_commit(p, take);
     if (rc) return rc;
     b += take;
