@@ -19,6 +19,8 @@
 // Hash table: open addressing, linear probing over 8-byte slots
 // {tag = digest word 2 : id}; bucket = (digest words 0,1) * golden ratio.
 // Roofline: HBM-bound probes.
+#include <stddef.h>
+
 #include "common.hpp"
 
 namespace ngpu {
@@ -114,13 +116,19 @@ __device__ __forceinline__ uint64_t layer_bucket(const uint32_t *d, uint32_t lay
   return digest_bucket(d) + (uint64_t)layer * 0xC2B2AE3D27D4EB4Full;
 }
 
-// chunk -> layer map; one wave per layer, lanes stride over its chunks.
-__global__ void layer_fill(const uint64_t *__restrict__ first, uint64_t L,
+// chunk -> layer map: thread per chunk, binary search in lfirst[0..L]
+// (last layer whose first chunk <= c; empty layers are skipped naturally).
+__global__ void layer_fill(const uint64_t *__restrict__ first, uint64_t L, uint64_t n,
                            uint32_t *__restrict__ chunk_layer) {
-  const uint64_t waves = (gridDim.x * (uint64_t)blockDim.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t l = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6; l < L; l += waves)
-    for (uint64_t c = first[l] + lane; c < first[l + 1]; c += 64) chunk_layer[c] = (uint32_t)l;
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  uint64_t lo = 0, hi = L;  // invariant: first[lo] <= c < first[hi]
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (first[mid] <= c) lo = mid;
+    else hi = mid;
+  }
+  chunk_layer[c] = (uint32_t)lo;
 }
 
 // Stage 1: dict decision (from given hits, or by probing the local dict) +
@@ -155,6 +163,33 @@ __global__ void dedup_probe(const ngpu_chunk *__restrict__ chunks, uint64_t n,
   r.kind = kind;
   r.reserved = 0;
   newflag[c] = 0;
+}
+
+// Per-layer counters: lanes of a wave usually share one layer, so reduce in
+// the wave and issue ONE atomic (per-lane atomics on one address serialise:
+// 16K of them cost ~0.2 ms).  Every lane of the wave must call these.
+__device__ __forceinline__ void layer_add_u64(unsigned long long *base, size_t stride_words,
+                                              uint32_t layer, uint64_t v) {
+  const uint32_t l0 = __builtin_amdgcn_readfirstlane(layer);
+  if (__all(layer == l0)) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(base + (size_t)l0 * stride_words, (unsigned long long)v);
+  } else if (v) {
+    atomicAdd(base + (size_t)layer * stride_words, (unsigned long long)v);
+  }
+}
+
+__device__ __forceinline__ void layer_min_u32(uint32_t *base, size_t stride, uint32_t layer,
+                                              uint32_t v) {
+  const uint32_t l0 = __builtin_amdgcn_readfirstlane(layer);
+  if (__all(layer == l0)) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    if ((threadIdx.x & 63) == 0 && v != kNone) atomicMin(base + (size_t)l0 * stride, v);
+  } else if (v != kNone) {
+    atomicMin(base + (size_t)layer * stride, v);
+  }
 }
 
 __device__ __forceinline__ bool same_key(const ngpu_result *out, const uint32_t *chunk_layer,
@@ -197,35 +232,40 @@ __global__ void dedup_resolve(const ngpu_chunk *__restrict__ chunks, uint64_t n,
                               uint64_t *__restrict__ uoff,
                               uint32_t *__restrict__ blob_first, uint32_t n_blobs) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  ngpu_result &r = out[c];
-  uoff[c] = 0;
-  if (c == 0) { newflag[n] = 0; uoff[n] = 0; }
-  if (r.kind == NGPU_DICT) return;
-  uint32_t d[8];
-  load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
-  const uint32_t layer = chunk_layer[c];
-  const uint32_t tag = digest_tag(d);
-  uint32_t f = kNone;
-  for (uint64_t p = layer_bucket(d, layer) & mask;; p = (p + 1) & mask) {
-    const uint64_t s = table[p];
-    if (s == kEmpty) break;
-    if ((uint32_t)(s >> 32) == tag && same_key(out, chunk_layer, (uint32_t)s, d, layer)) {
-      f = (uint32_t)s;
-      break;
+  const bool live = c < n;
+  uint32_t layer = 0, first_new = kNone;
+  if (live) {
+    ngpu_result &r = out[c];
+    layer = chunk_layer[c];
+    uoff[c] = 0;
+    if (c == 0) { newflag[n] = 0; uoff[n] = 0; }
+    if (r.kind != NGPU_DICT) {
+      uint32_t d[8];
+      load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
+      const uint32_t tag = digest_tag(d);
+      uint32_t f = kNone;
+      for (uint64_t p = layer_bucket(d, layer) & mask;; p = (p + 1) & mask) {
+        const uint64_t s = table[p];
+        if (s == kEmpty) break;
+        if ((uint32_t)(s >> 32) == tag && same_key(out, chunk_layer, (uint32_t)s, d, layer)) {
+          f = (uint32_t)s;
+          break;
+        }
+      }
+      const uint32_t len = chunks[c].length;
+      if (f != (uint32_t)c && f != kNone && chunks[f].length == len) {
+        r.kind = NGPU_INTRA;
+        r.ref = f;
+      } else {
+        r.kind = NGPU_NEW;
+        r.ref = c;
+        newflag[c] = 1;
+        uoff[c] = ((uint64_t)len + align - 1) / align * align;
+        first_new = (uint32_t)c;
+      }
     }
   }
-  const uint32_t len = chunks[c].length;
-  if (f != (uint32_t)c && f != kNone && chunks[f].length == len) {
-    r.kind = NGPU_INTRA;
-    r.ref = f;
-    return;
-  }
-  r.kind = NGPU_NEW;
-  r.ref = c;
-  newflag[c] = 1;
-  uoff[c] = ((uint64_t)len + align - 1) / align * align;
-  atomicMin(blob_first + (uint64_t)layer * (n_blobs + 1) + n_blobs, (uint32_t)c);
+  layer_min_u32(blob_first + n_blobs, n_blobs + 1, layer, first_new);
 }
 
 // Blob-table order per layer (one workgroup per layer): each dict blob gets a
@@ -269,29 +309,36 @@ __global__ void dedup_finalize(const ngpu_chunk *__restrict__ chunks, uint64_t n
                                ngpu_result *__restrict__ out,
                                ngpu_layer_stats *__restrict__ st) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  ngpu_result &r = out[c];
-  const uint32_t layer = chunk_layer[c];
-  const uint32_t *real = real_all + (uint64_t)layer * nbo;
-  const uint64_t a = lfirst[layer];
-  const uint64_t ib = newidx[a], ob = uoff[a];
-  const uint32_t own = real[nbo - 1];
-  ngpu_layer_stats &ls = st[layer];
-  if (r.kind == NGPU_NEW) {
-    r.index = (uint32_t)(newidx[c] - ib);
-    r.uncompressed_offset = uoff[c] - ob;
-    r.blob_index = own;
-    atomicAdd((unsigned long long *)&ls.new_bytes, (unsigned long long)chunks[c].length);
-  } else if (r.kind == NGPU_INTRA) {
-    const uint64_t f = r.ref;
-    r.index = (uint32_t)(newidx[f] - ib);
-    r.uncompressed_offset = uoff[f] - ob;
-    r.blob_index = own;
-    atomicAdd((unsigned long long *)&ls.intra_chunks, 1ull);
-  } else {
-    r.blob_index = real[r.blob_index];
-    atomicAdd((unsigned long long *)&ls.dict_chunks, 1ull);
+  uint32_t layer = 0;
+  uint64_t new_bytes = 0, intra = 0, dict = 0;
+  if (c < n) {
+    ngpu_result &r = out[c];
+    layer = chunk_layer[c];
+    const uint32_t *real = real_all + (uint64_t)layer * nbo;
+    const uint64_t a = lfirst[layer];
+    const uint64_t ib = newidx[a], ob = uoff[a];
+    const uint32_t own = real[nbo - 1];
+    if (r.kind == NGPU_NEW) {
+      r.index = (uint32_t)(newidx[c] - ib);
+      r.uncompressed_offset = uoff[c] - ob;
+      r.blob_index = own;
+      new_bytes = chunks[c].length;
+    } else if (r.kind == NGPU_INTRA) {
+      const uint64_t f = r.ref;
+      r.index = (uint32_t)(newidx[f] - ib);
+      r.uncompressed_offset = uoff[f] - ob;
+      r.blob_index = own;
+      intra = 1;
+    } else {
+      r.blob_index = real[r.blob_index];
+      dict = 1;
+    }
   }
+  constexpr size_t W = sizeof(ngpu_layer_stats) / 8;
+  unsigned long long *base = reinterpret_cast<unsigned long long *>(st);
+  layer_add_u64(base + offsetof(ngpu_layer_stats, new_bytes) / 8, W, layer, new_bytes);
+  layer_add_u64(base + offsetof(ngpu_layer_stats, intra_chunks) / 8, W, layer, intra);
+  layer_add_u64(base + offsetof(ngpu_layer_stats, dict_chunks) / 8, W, layer, dict);
 }
 
 // ---- exclusive scan over u64 (n+1 entries, in place) ----------------------
@@ -409,11 +456,7 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
   (void)hipMemsetAsync(st, 0, sizeof(ngpu_layer_stats) * L, s);
   if (n) {
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    {
-      const uint64_t waves = L < 16384 ? L : 16384;
-      hipLaunchKernelGGL(layer_fill, dim3((unsigned)((waves * 64 + 255) / 256)), dim3(256), 0, s,
-                         lfirst, L, ws.chunk_layer);
-    }
+    hipLaunchKernelGGL(layer_fill, dim3(blocks), dim3(256), 0, s, lfirst, L, n, ws.chunk_layer);
     (void)hipMemsetAsync(ws.intra, 0xFF, ws.intra_cap * sizeof(uint64_t), s);
     hipLaunchKernelGGL(dedup_probe, dim3(blocks), dim3(256), 0, s, chunks, n, dict, hits,
                        ws.chunk_layer, out, ws.newflag, ws.blob_first, n_blobs);
