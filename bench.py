@@ -235,6 +235,8 @@ def main():
     ap.add_argument("--dict-entries", type=int, default=0, help="override dict size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on a node; gloo to "
+                    "rehearse several ranks on one GPU")
     ap.add_argument("--pmc-json", default="", help="PMC summary for roofline.traffic "
                     "(default: newest profiles/r*/pmc_<workload>.json)")
     ap.add_argument("--cpu-sample-mib", type=int, default=2048)
@@ -246,12 +248,15 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     wl = dict(WORKLOADS[args.workload])
     if args.dict_entries:
@@ -316,7 +321,8 @@ def main():
         t0 = time.perf_counter()
         if wl.get("sharded"):
             from nydus_gpu.dist import ShardedChunkDict, engine_load_fn, engine_probe_fn
-            sdict = ShardedChunkDict(rank, world)
+            sdict = ShardedChunkDict(rank, world,
+                                     comm_device=None if args.dist_backend == "nccl" else "cpu")
             local_m = sdict.load(dd, us, bl, ix, 8, engine_load_fn(eng, 8))
             sdict.probe_fn = engine_probe_fn(eng, stream_fn=lambda: stream.cuda_stream)
         else:
@@ -371,7 +377,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

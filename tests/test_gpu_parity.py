@@ -565,3 +565,19 @@ def test_converter_testpack_flow(tars, tmp_path):
     assert blobs == ["sha256:" + dres["own_blob_id"], "sha256:" + ures["own_blob_id"]]  # :513-519
     b = rafs.read_v6(out.getvalue())
     assert b["blob_ids"] == [dres["own_blob_id"], ures["own_blob_id"]]
+
+
+def test_fs_version_5_offsets(oracle):
+    """RAFS v5 (FsVersion "5"): NEW chunks packed without 4 KiB alignment."""
+    rng = np.random.default_rng(55)
+    data, ch = _random_layer(rng, 8 << 20, 0x10000, dup_frac=0.2)
+    dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    exp, _ = oracle.dedup(dig, ch["length"], align=1)
+    eng = nydus_gpu.Engine(chunk_size=0x10000, fs_version=5)
+    try:
+        out, st = eng.process(data, ch)
+    finally:
+        eng.close()
+    for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+        assert np.array_equal(out[f], exp[f]), f
+    assert st["uncompressed_size"] == int(ch["length"][exp["kind"] == 0].sum())
