@@ -581,3 +581,50 @@ def test_fs_version_5_offsets(oracle):
     for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
         assert np.array_equal(out[f], exp[f]), f
     assert st["uncompressed_size"] == int(ch["length"][exp["kind"] == 0].sum())
+
+
+def test_plain_c_client(tars, golden_layers, tmp_path):
+    """A plain-C program (what the cgo binding does) links libnydusgpu.so and
+    gets the golden digests and decisions."""
+    import subprocess
+    from conftest import ROOT
+    exe = str(tmp_path / "abi_client")
+    subprocess.check_call(["gcc", "-O1", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "abi_client.c"), "-o", exe,
+                           "-L", os.path.join(ROOT, "nydus-snapshotter_amd"), "-lnydusgpu",
+                           "-Wl,-rpath," + os.path.join(ROOT, "nydus-snapshotter_amd")])
+    case = next(c for c in golden_layers["cases"] if c["layer"] == "edge_pax" and c["chunk_size"] == 0x10000)
+    tp = tmp_path / "l.tar"
+    tp.write_bytes(tars["edge_pax"])
+    out = subprocess.check_output([exe, str(tp), str(0x10000), "0"], text=True).splitlines()
+    rows = [line.split(",") for line in out[:-1]]
+    assert [r[2] for r in rows] == case["digests"]
+    kinds = {"NEW": 0, "INTRA": 1, "DICT": 2}
+    assert [int(r[3]) for r in rows] == [kinds[d[0]] for d in case["decisions"]]
+    assert out[-1].startswith(f"STATS {len(rows)} ")
+
+
+def test_engine_thread_safety(oracle):
+    """Concurrent calls on one engine serialise internally (threads as
+    goroutines sharing an engine)."""
+    import threading
+    rng = np.random.default_rng(90)
+    layers = [_random_layer(rng, 6 << 20, 0x10000) for _ in range(4)]
+    eng = nydus_gpu.Engine(chunk_size=0x10000)
+    errs = []
+
+    def run(i):
+        try:
+            data, ch = layers[i]
+            for _ in range(3):
+                out, _ = eng.process(data, ch)
+                exp = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
+                if not np.array_equal(out["digest"], exp):
+                    errs.append(i)
+        except Exception as e:  # pragma: no cover
+            errs.append(repr(e))
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    eng.close()
+    assert not errs
