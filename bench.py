@@ -41,6 +41,9 @@ MiB = 1 << 20
 # 39.3 T int32 ops/s.  Measured, not assumed: a wave64 v_add3/v_xor/v_alignbit
 # takes 4 SIMD cycles (rocprofv3: SQ_INSTS_VALU x 4 / 1024 SIMDs = the whole
 # b3_groups duration at the GRBM clock; DESIGN.md §Roofline, profiles/).
+SHA_MODES = {"auto": 0, "split": 1, "pair": 2}
+SHA_PAIR_MAX_CHUNKS = 256 * 4 * 32  # launch_sha256's auto rule (sha256.hip)
+CLOCK_HZ = 2.4e9
 PEAK_INT_OPS = 256 * 4 * 16 * 2.4e9
 PEAK_HBM = 8.0e12
 OPS_PER_COMPRESSION = 680  # 7 rounds x 8 G x 12 ops + 8 output xors
@@ -125,6 +128,10 @@ WORKLOADS = {
                     "(30% of the layer's chunks planted)",
                n_files=4096, file_size=4 * MiB, chunk=MiB, digester="sha256", layers=1,
                dict_entries=200_000_000, plant=0.3),
+    "c3-64k": dict(desc="C3 layer with 64 KiB chunks: 16 GiB, sha256, 200M-entry chunk dict "
+                        "(262144 chunks: one lane per chunk fills the chip)",
+                   n_files=4096, file_size=4 * MiB, chunk=64 * 1024, digester="sha256", layers=1,
+                   dict_entries=200_000_000, plant=0.3),
     "c3-blake3": dict(desc="C3 with blake3: 16 GiB layer, 1 MiB chunks, 200M-entry chunk dict",
                       n_files=4096, file_size=4 * MiB, chunk=MiB, digester="blake3", layers=1,
                       dict_entries=200_000_000, plant=0.3),
@@ -232,6 +239,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--lanes", type=int, default=0, help="leaves per lane (0=auto)")
+    ap.add_argument("--sha-mode", choices=["auto", "split", "pair"], default="auto",
+                    help="SHA-256 kernel: one lane per chunk (split) or two (pair)")
     ap.add_argument("--dict-entries", type=int, default=0, help="override dict size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -273,7 +282,8 @@ def main():
     d_out = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
     h_out = torch.empty(n * 64, dtype=torch.uint8, pin_memory=True)
     eng = nydus_gpu.Engine(device=local, digester=wl["digester"], chunk_size=wl["chunk"],
-                           leaves_per_lane=args.lanes, timing=True)
+                           leaves_per_lane=args.lanes, timing=True,
+                           flags=SHA_MODES[args.sha_mode] << 11)
     stream = torch.cuda.Stream()
     extra = {}
     n_layers = wl["layers"]
@@ -414,11 +424,23 @@ def main():
         blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).sum())
         ops = blocks * 1384  # SURVEY.md §8(d) SHA-256 op count
         achieved = ops / (dig_ms / 1e3)
-        roof = {"bound": "valu", "kernel": "sha256_split", "achieved": round(achieved / 1e12, 3),
+        pair = args.sha_mode == "pair" or (args.sha_mode == "auto" and n <= SHA_PAIR_MAX_CHUNKS)
+        # SHA-256 is serial within a chunk: with fewer chunks than the chip has
+        # lanes, a chunk's round chain (VALU ops on its critical wave, 4 cycles
+        # per wave64 op) bounds the kernel, not chip-wide VALU throughput.
+        chain_ops = 66 * 9 if pair else 64 * 14  # VALU ops per block on the round wave
+        lanes_used = n * (2 if pair else 1)
+        max_blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).max())
+        chain_s = max_blocks * chain_ops * 4 / CLOCK_HZ
+        roof = {"bound": "valu", "kernel": "sha256_pair" if pair else "sha256_split",
+                "achieved": round(achieved / 1e12, 3),
                 "peak": round(PEAK_INT_OPS / 1e12, 3), "unit": "Tops/s",
                 "frac": round(achieved / PEAK_INT_OPS, 4), "traffic": None,
                 "hbm_gbs": round(file_bytes / (dig_ms / 1e3) / 1e9, 1),
-                "occupancy_ceiling": f"{n} lanes = {n / (256 * 4 * 64):.3f} waves per SIMD"}
+                "chain_bound_gbs": round(file_bytes / chain_s / 1e9, 1),
+                "chain_frac": round(chain_s / (dig_ms / 1e3), 4),
+                "occupancy_ceiling": f"{lanes_used} lanes = {lanes_used / (256 * 4 * 64):.3f} "
+                                     "waves per SIMD"}
 
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e and not wl.get("dict_entries"):

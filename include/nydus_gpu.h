@@ -80,6 +80,10 @@ typedef struct {
 /* Tuning (benchmarks only): bits 8..10 = 1 + BLAKE3 load mode
  * (bit0 non-temporal loads, bit1 next-block prefetch); 0 = library default. */
 #define NGPU_FLAG_LOAD_MODE_SHIFT 8
+/* Tuning (benchmarks only): bits 11..13 = 1 + SHA-256 kernel (0: one lane per
+ * chunk, 1: two lanes per chunk, 2/3: diagnostics with wrong digests);
+ * 0 = library default (by chunk count). */
+#define NGPU_FLAG_SHA_MODE_SHIFT 11
 
 /* Per-stage device time of the last process call (NGPU_FLAG_TIMING). */
 typedef struct {

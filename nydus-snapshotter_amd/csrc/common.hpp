@@ -47,7 +47,7 @@ uint64_t blake3_max_groups(uint64_t n, uint64_t data_len, int group_log2);
 // sha256.hip
 void launch_sha256(const uint8_t *data, uint64_t data_len,
                    const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
-                   uint64_t *err, hipStream_t s);
+                   uint64_t *err, int variant, hipStream_t s);
 
 struct DictDevice {
   const uint8_t *digests = nullptr;  // m x 32

@@ -147,7 +147,10 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
   HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 16 * sizeof(uint64_t), s));
   if (e->cfg.digester == NGPU_DIGEST_SHA256) {
     if (tm) HIP_TRY(e, hipEventRecord(e->ev[1], s));
-    launch_sha256(d_data, len, d_chunks, n, d_out, e->ws.stats + 7, s);
+    // tuning override: flags bits 11..13 = 1 + SHA-256 variant (0 split,
+    // 1 pair, 2/3 pair diagnostics)
+    const uint32_t sv = (e->cfg.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7;
+    launch_sha256(d_data, len, d_chunks, n, d_out, e->ws.stats + 7, sv ? (int)sv - 1 : -1, s);
     if (tm) HIP_TRY(e, hipEventRecord(e->ev[2], s));
   } else {
     launch_blake3(d_data, d_chunks, n, len, D, e->ws, d_out, s, tm ? e->ev[1] : nullptr,

@@ -124,9 +124,13 @@ __global__ __launch_bounds__(128) void sha256_split(
     const uint8_t *__restrict__ data, uint64_t data_len,
     const ngpu_chunk *__restrict__ chunks, uint64_t n,
     ngpu_result *__restrict__ out, uint64_t *__restrict__ err) {
-  __shared__ uint32_t kw[2][64][64];
+  // K+W per lane, lane-major with a 68-word stride: 16-B LDS accesses, and a
+  // whole block's 64 values are read into registers before its rounds start.
+  __shared__ u32x4 kw[2][64][17];
   const uint32_t lane = threadIdx.x & 63;
   const bool rounds = threadIdx.x < 64;
+  // the round wave is the critical path: win issue arbitration on a shared SIMD
+  if (rounds) __builtin_amdgcn_s_setprio(3);
   const uint64_t c = blockIdx.x * 64ull + lane;
   bool valid = c < n;
   uint32_t len = 0;
@@ -149,6 +153,7 @@ __global__ __launch_bounds__(128) void sha256_split(
   auto produce = [&](uint32_t b, int buf) {
     uint32_t w[16];
     sha_load_block(p, len, b, w);
+    u32x4 q;
 #pragma unroll
     for (int t = 0; t < 64; ++t) {
       uint32_t wt;
@@ -161,7 +166,8 @@ __global__ __launch_bounds__(128) void sha256_split(
         wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
         w[t & 15] = wt;
       }
-      kw[buf][t][lane] = wt + kK[t];
+      q[t & 3] = wt + kK[t];
+      if ((t & 3) == 3) kw[buf][lane][t >> 2] = q;
     }
   };
 
@@ -173,13 +179,16 @@ __global__ __launch_bounds__(128) void sha256_split(
     if (rounds) {
       if (k < nb) {
         const int buf = k & 1;
+        u32x4 kv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) kv[j] = kw[buf][lane][j];
         uint32_t a = h[0], b = h[1], cc = h[2], d = h[3];
         uint32_t e = h[4], f = h[5], g = h[6], hh = h[7];
 #pragma unroll
         for (int t = 0; t < 64; ++t) {
           const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
           const uint32_t ch = (e & f) ^ (~e & g);
-          const uint32_t t1 = hh + kw[buf][t][lane] + S1 + ch;
+          const uint32_t t1 = hh + kv[t >> 2][t & 3] + S1 + ch;
           const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
           const uint32_t mj = (a & b) | (cc & (a | b));
           hh = g; g = f; f = e; e = d + t1; d = cc; cc = b; b = a; a = t1 + S0 + mj;
@@ -199,12 +208,221 @@ __global__ __launch_bounds__(128) void sha256_split(
   }
 }
 
+// Two lanes per chunk for the rounds (few, long chunks: the per-chunk round
+// chain is the whole critical path, so shortening it is the only lever once
+// every chunk has a lane).
+//
+// With A_t / E_t the new a / e of round t (d = A_{t-4}, h = E_{t-4}):
+//   E_t = Sigma1(E_{t-1}) + Ch(E_{t-1}, E_{t-2}, E_{t-3}) + E_{t-4} + K_t + W_t + A_{t-4}
+//   A_t = Sigma0(A_{t-1}) + Maj(A_{t-1}, A_{t-2}, A_{t-3}) + E_t - A_{t-4}
+// The "E lane" of a chunk walks the E recurrence, the "A lane" the A one, TWO
+// ROUNDS BEHIND: in iteration i the E lane makes E_i and the A lane A_{i-2}.
+// Both hold their last four values in P0..P3 (newest first), so the values
+// each needs from its partner -- A_{i-4} for the E lane, E_{i-2} for the A
+// lane -- are both the partner's P1: ONE row_ror:8 DPP add (partner 8 lanes
+// away in the 16-lane row) serves both sides, off the critical path:
+//   Z   = ((P3 ^ M) + KW) + dpp(P1)  E: E_{i-4} + K+W + A_{i-4}   A: -A_{i-6} + E_{i-2}
+//   S   = rotr(P0,r1) ^ rotr(P0,r2) ^ rotr(P0,r3)        (per-lane rotate amounts)
+//   sel = P0 ^ (P2 & M)              E: e                  A: a ^ c
+//   cm  = bfi(sel, P1, P2)           E: Ch(e,f,g)          A: Maj(a,b,c) = bfi(a^c, b, c)
+//   X   = S + cm + Z                 E: E_i                A: A_{i-2}
+// 9 VALU ops per round (14 with one lane per chunk) and a 3-deep dependency
+// chain.  66 iterations per block: in 0-1 the A lane computes values that are
+// discarded (its P0/P1 hold H2/H3 = A_{-3}/A_{-4} for the E lane to read, and
+// its registers are reset to H0..H3 at iteration 2); in 64-65 the E lane does.
+//
+// Waves: wave 0 rounds (32 chunks), wave 1 message schedule for the same 32
+// chunks, two blocks per phase (lanes 0-31 the even block, 32-63 the odd one),
+// with the next pair of blocks prefetched into registers.  KW[set][half][chunk][t]
+// in LDS; chunk row 32 holds the constant 1 the A lanes add (~x + 1 = -x).
+constexpr uint32_t kDppRowRor8 = 0x128;
+
+__device__ __forceinline__ uint32_t bswap_words(u32x4 v, int i) {
+  return bswap(i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
+}
+
+// R round waves + R schedule waves per workgroup (R groups of 32 chunks), so
+// one workgroup per CU puts every wave on its own SIMD.
+// DIAG (benchmarks only, wrong digests): 1 = no cross-lane exchange,
+// 2 = the schedule waves do no work (round waves alone).
+template <int R, int DIAG>
+__global__ __launch_bounds__(128 * R) void sha256_pair(
+    const uint8_t *__restrict__ data, uint64_t data_len,
+    const ngpu_chunk *__restrict__ chunks, uint64_t n,
+    ngpu_result *__restrict__ out, uint64_t *__restrict__ err) {
+  __shared__ u32x4 kws[R][2][2][33][17];  // [group][set][half][chunk | 32 = ones][t/4]
+  __shared__ uint32_t s_nbmax;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = threadIdx.x >> 6;
+  const bool rounds = wave < R;
+  const uint32_t grp = rounds ? wave : wave - R;
+  auto &kw = kws[grp];
+  // the round wave is the critical path: win issue arbitration on a shared SIMD
+  if (rounds) __builtin_amdgcn_s_setprio(3);
+  const uint32_t side = rounds ? (lane >> 3) & 1 : 0;  // 1 = A lane
+  const uint32_t ci = rounds ? (lane >> 4) * 8 + (lane & 7) : lane & 31;
+  const uint32_t half = rounds ? 0 : lane >> 5;
+  const uint64_t c = (blockIdx.x * (uint64_t)R + grp) * 32ull + ci;
+  bool valid = c < n;
+  uint32_t len = 0;
+  const uint8_t *p = data;
+  if (threadIdx.x == 0) s_nbmax = 0;
+  if (valid) {
+    const ngpu_chunk ch = chunks[c];
+    if (ch.offset > data_len || ch.length > data_len - ch.offset) {
+      if (rounds && side == 0) atomicAdd((unsigned long long *)err, 1ull);
+      valid = false;
+    } else {
+      len = ch.length;
+      p = data + ch.offset;
+    }
+  }
+  const uint32_t nb = valid ? (len + 8) / 64 + 1 : 0;
+  uint32_t nbmax = nb;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, o, 64));
+  if (R > 1) {  // every wave of the workgroup runs the same number of phases
+    __syncthreads();
+    if (lane == 0) atomicMax(&s_nbmax, nbmax);
+    __syncthreads();
+    nbmax = s_nbmax;
+  }
+  const uint32_t phases = (nbmax + 1) / 2;
+
+  // Schedule wave state: its next block (b + 2) prefetched into registers.
+  const uint32_t full = len >> 6;
+  const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  u32x4 pf0 = {}, pf1 = {}, pf2 = {}, pf3 = {};
+  bool have_pf = false;
+  auto prefetch = [&](uint32_t b) {
+    have_pf = aligned && b < full;
+    if (have_pf) {
+      const u32x4 *q = reinterpret_cast<const u32x4 *>(p + 64ull * b);
+      pf0 = q[0]; pf1 = q[1]; pf2 = q[2]; pf3 = q[3];
+    }
+  };
+  auto produce = [&](uint32_t b, int set) {
+    if (b >= nb) return;
+    uint32_t w[16];
+    if (have_pf) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        w[i] = bswap_words(pf0, i); w[4 + i] = bswap_words(pf1, i);
+        w[8 + i] = bswap_words(pf2, i); w[12 + i] = bswap_words(pf3, i);
+      }
+    } else {
+      sha_load_block(p, len, b, w);
+    }
+    prefetch(b + 2);
+    u32x4 *dst = kw[set][half][ci];
+    u32x4 q;
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      uint32_t wt;
+      if (t < 16) {
+        wt = w[t];
+      } else {
+        const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+        const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+        const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+        wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+        w[t & 15] = wt;
+      }
+      q[t & 3] = wt + kK[t];
+      if ((t & 3) == 3) dst[t >> 2] = q;
+    }
+  };
+
+  if (!rounds) {
+    for (uint32_t i = lane; i < 2 * 2 * 17; i += 64)
+      kw[i / 34][(i / 17) & 1][32][i % 17] = u32x4{1u, 1u, 1u, 1u};
+    if (nb > half) {
+      prefetch(half);
+      produce(half, 0);
+    }
+  }
+  __syncthreads();
+
+  const uint32_t M = side ? 0xFFFFFFFFu : 0u;
+  const uint32_t r1 = side ? 2 : 6, r2 = side ? 13 : 11, r3 = side ? 22 : 25;
+  uint32_t H0 = side ? 0x6a09e667u : 0x510e527fu, H1 = side ? 0xbb67ae85u : 0x9b05688cu;
+  uint32_t H2 = side ? 0x3c6ef372u : 0x1f83d9abu, H3 = side ? 0xa54ff53au : 0x5be0cd19u;
+  const uint32_t kcol = side ? 32 : ci;
+  for (uint32_t ph = 0; ph < phases; ++ph) {
+    const int set = ph & 1;
+    if (rounds) {
+#pragma unroll 1
+      for (uint32_t hb = 0; hb < 2; ++hb) {
+        if (2 * ph + hb < nb) {
+          u32x4 kv[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) kv[j] = kw[set][hb][kcol][j];
+          uint32_t P0 = side ? H2 : H0, P1 = side ? H3 : H1, P2 = H2, P3 = H3;
+          uint32_t F0 = 0, F1 = 0, F2 = 0, F3 = 0;
+#pragma unroll
+          for (int it = 0; it < 66; ++it) {
+            if (it == 2) {  // the A lane starts its rounds: a,b,c,d = H0..H3
+              P0 = side ? H0 : P0; P1 = side ? H1 : P1;
+              P2 = side ? H2 : P2; P3 = side ? H3 : P3;
+            }
+            const uint32_t kwv = it < 64 ? kv[it >> 2][it & 3] : side;
+            uint32_t Y = (P3 ^ M) + kwv;
+            asm("" : "+v"(Y));  // keep the DPP add a separate VOP2 op
+            uint32_t Z =
+                Y + (DIAG == 1 ? P1 : (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P1, kDppRowRor8,
+                                                                            0xf, 0xf, false));
+            asm("" : "+v"(Z));
+            const uint32_t S = xor3(rotr32(P0, r1), rotr32(P0, r2), rotr32(P0, r3));
+            // bitop3 truth-table index is S0<<2 | S1<<1 | S2: 0x78 = a ^ (b & c)
+            const uint32_t sel = __builtin_amdgcn_bitop3_b32(P0, P2, M, 0x78);
+            const uint32_t cm = (sel & P1) | (~sel & P2);
+            const uint32_t X = S + cm + Z;
+            P3 = P2; P2 = P1; P1 = P0; P0 = X;
+            if (it == 63) { F0 = P0; F1 = P1; F2 = P2; F3 = P3; }  // E lane final e,f,g,h
+          }
+          H0 += side ? P0 : F0; H1 += side ? P1 : F1;
+          H2 += side ? P2 : F2; H3 += side ? P3 : F3;
+        }
+      }
+    } else if (DIAG != 2) {
+      produce(2 * ph + 2 + half, set ^ 1);
+    }
+    __syncthreads();
+  }
+  if (rounds && valid) {
+    uint4 *dd = reinterpret_cast<uint4 *>(out[c].digest) + (side ? 0 : 1);
+    *dd = make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));
+  }
+}
+
 }  // namespace
 
 void launch_sha256(const uint8_t *data, uint64_t data_len,
                    const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
-                   uint64_t *err, hipStream_t s) {
+                   uint64_t *err, int variant, hipStream_t s) {
   if (n == 0) return;
+  // Auto: two lanes per chunk while one lane per chunk leaves SIMDs idle
+  // (<= one round wave per SIMD: 256 CUs x 4 SIMDs x 32 chunks).  Measured
+  // (profiles/r1/sha_variants.jsonl): 16384 x 1 MiB chunks 785 vs 538 GB/s,
+  // 65536 x 256 KiB chunks 989 vs 1111 GB/s.
+  if (variant < 0) variant = n <= 256ull * 4 * 32 ? 1 : 0;
+  if (variant >= 1) {
+    const dim3 g2((unsigned)((n + 63) / 64)), g1((unsigned)((n + 31) / 32));
+    switch (variant) {
+      case 2:  // diagnostics
+        hipLaunchKernelGGL((sha256_pair<2, 1>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
+        break;
+      case 3:
+        hipLaunchKernelGGL((sha256_pair<2, 2>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
+        break;
+      case 4:  // one group per workgroup
+        hipLaunchKernelGGL((sha256_pair<1, 0>), g1, dim3(128), 0, s, data, data_len, chunks, n, out, err);
+        break;
+      default:
+        hipLaunchKernelGGL((sha256_pair<2, 0>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
+    }
+    return;
+  }
   const uint64_t blocks = (n + 63) / 64;
   hipLaunchKernelGGL(sha256_split, dim3((unsigned)blocks), dim3(128), 0, s, data,
                      data_len, chunks, n, out, err);

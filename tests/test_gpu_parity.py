@@ -14,17 +14,23 @@ from conftest import kat_input
 pytestmark = pytest.mark.gpu
 
 LANES = [1, 2, 4, 8, 16]
+# SHA-256 kernels, forced through ngpu_config.flags bits 11..12 (1 + variant):
+# 0 = auto, one lane per chunk ("split"), two lanes per chunk ("pair").
+# "pair" runs two chunk groups per workgroup; 5 forces one group per workgroup.
+SHA_SPLIT, SHA_PAIR, SHA_PAIR_R1 = 1 << 11, 2 << 11, 5 << 11
+SHA_FLAGS = [0, SHA_SPLIT, SHA_PAIR, SHA_PAIR_R1]
 
 
 @pytest.fixture(scope="module")
 def engines():
     cache = {}
 
-    def get(digester="blake3", chunk_size=0x100000, lanes=0, fs_version=6):
-        k = (digester, chunk_size, lanes, fs_version)
+    def get(digester="blake3", chunk_size=0x100000, lanes=0, fs_version=6, flags=0):
+        k = (digester, chunk_size, lanes, fs_version, flags)
         if k not in cache:
             cache[k] = nydus_gpu.Engine(digester=digester, chunk_size=chunk_size,
-                                        leaves_per_lane=lanes, fs_version=fs_version)
+                                        leaves_per_lane=lanes, fs_version=fs_version,
+                                        flags=flags)
         return cache[k]
     yield get
     for e in cache.values():
@@ -39,13 +45,14 @@ def one_chunk(n, off=0):
 
 @pytest.mark.parametrize("digester", ["blake3", "sha256"])
 def test_kat_single_chunk(engines, kat, digester):
-    for lanes in (LANES if digester == "blake3" else [0]):
-        eng = engines(digester, 0x1000000, lanes)
+    for lanes, fl in ([(l, 0) for l in LANES] if digester == "blake3" else
+                      [(0, f) for f in SHA_FLAGS]):
+        eng = engines(digester, 0x1000000, lanes, flags=fl)
         for v in kat["vectors"]:
             if v["len"] == 0:
                 continue  # nydus never emits empty chunks
             out, st = eng.process(kat_input(v["len"]), one_chunk(v["len"]))
-            assert out["digest"][0].tobytes().hex() == v[digester], (lanes, v["len"])
+            assert out["digest"][0].tobytes().hex() == v[digester], (lanes, fl, v["len"])
             assert st["new_chunks"] == 1
 
 
@@ -63,10 +70,11 @@ def test_kat_batched_all_lengths(engines, kat):
     data = b"".join(parts)
     ch = np.array(chunks, dtype=nydus_gpu.CHUNK_DTYPE)
     for digester in ("blake3", "sha256"):
-        for lanes in (LANES if digester == "blake3" else [0]):
-            out, _ = engines(digester, 0x1000000, lanes).process(data, ch)
+        for lanes, fl in ([(l, 0) for l in LANES] if digester == "blake3" else
+                          [(0, f) for f in SHA_FLAGS]):
+            out, _ = engines(digester, 0x1000000, lanes, flags=fl).process(data, ch)
             got = [o.tobytes().hex() for o in out["digest"]]
-            assert got == [v[digester] for v in vecs], (digester, lanes)
+            assert got == [v[digester] for v in vecs], (digester, lanes, fl)
 
 
 def _decisions(out):
@@ -179,13 +187,43 @@ def test_random_vs_oracle(engines, oracle, seed, chunk_size, unaligned):
     for digester in ("blake3", "sha256"):
         exp_d = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), digester)
         exp, own = oracle.dedup(exp_d, ch["length"])
-        for lanes in ([0, 1, 16] if digester == "blake3" else [0]):
-            out, st = engines(digester, chunk_size, lanes).process(data, ch)
-            assert np.array_equal(out["digest"], exp_d), (digester, lanes)
+        for lanes, fl in ([(0, 0), (1, 0), (16, 0)] if digester == "blake3" else
+                          [(0, f) for f in SHA_FLAGS]):
+            out, st = engines(digester, chunk_size, lanes, flags=fl).process(data, ch)
+            assert np.array_equal(out["digest"], exp_d), (digester, lanes, fl)
             for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
-                assert np.array_equal(out[f], exp[f]), (digester, lanes, f)
+                assert np.array_equal(out[f], exp[f]), (digester, lanes, fl, f)
             assert st["intra_chunks"] == int((exp["kind"] == 1).sum())
             assert st["new_chunks"] == int((exp["kind"] == 0).sum())
+
+
+@pytest.mark.parametrize("fl", [SHA_SPLIT, SHA_PAIR, SHA_PAIR_R1])
+def test_sha256_ragged_wave(engines, oracle, fl):
+    """Chunks of very different block counts in one wave (lanes finish at
+    different blocks), lengths around the 55/56/64-byte padding edges, odd
+    offsets (byte-load path), a count that is not a multiple of 32/64, and a
+    bad descriptor in the middle of a wave."""
+    rng = np.random.default_rng(21)
+    lens = [1, 55, 56, 63, 64, 65, 119, 120, 128, 4096, 70000, 1 << 20, 3, 200000]
+    lens += [int(x) for x in rng.integers(1, 300000, 83)]
+    parts, chunks, off = [], [], 0
+    for i, n in enumerate(lens):
+        pad = int(rng.integers(0, 20)) if i % 3 == 0 else (-off) % 16
+        parts.append(rng.integers(0, 256, pad, dtype=np.uint8).tobytes())
+        off += pad
+        parts.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        chunks.append((off, n, i, 0))
+        off += n
+    data = b"".join(parts)
+    ch = np.array(chunks, dtype=nydus_gpu.CHUNK_DTYPE)
+    exp_d = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "sha256")
+    eng = engines("sha256", 0x1000000, 0, flags=fl)
+    out, _ = eng.process(data, ch)
+    assert np.array_equal(out["digest"], exp_d)
+    bad = ch.copy()
+    bad[40]["length"] = len(data)  # runs past the buffer
+    with pytest.raises(nydus_gpu.NgpuError):
+        eng.process(data, bad)
 
 
 def test_random_dict_vs_oracle(oracle):
