@@ -17,7 +17,7 @@ ok() { # test failures (1) are data; anything else ends the session
 }
 
 rocminfo 2>/dev/null | grep -m1 -o 'gfx9[0-9a-z]*' > "$OUT/arch.txt"
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 ok $? pytest-gpu
 tail -5 "$OUT/pytest_gpu.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
