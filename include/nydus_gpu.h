@@ -53,7 +53,9 @@ enum ngpu_error {
   NGPU_EUNSUPP = -5,   /* unsupported input (GNU sparse tar entry) */
   NGPU_ENODEV = -6,    /* no usable gfx950 device */
   NGPU_EIO = -7,       /* file I/O (chunk-dict bootstrap) */
-  NGPU_EFORMAT = -8    /* not a RAFS v6 bootstrap / bad chunk table */
+  NGPU_EFORMAT = -8,   /* not a RAFS v6 bootstrap / bad chunk table */
+  NGPU_ENOTFOUND = -9  /* entry not found in a nydus blob (ErrNotFound,
+                          pkg/converter/types.go:33-35) */
 };
 
 typedef struct ngpu_engine ngpu_engine;
@@ -114,7 +116,8 @@ typedef struct {
   uint64_t ref;         /* NEW: own chunk id; INTRA: chunk id of the first
                            occurrence; DICT: dict entry id (table order) */
   uint32_t blob_index;  /* real blob index, allocated in first-hit order */
-  uint32_t reserved;
+  uint32_t dict_blob;   /* DICT: the entry's inner blob index in the chunk
+                           dict (its blob table); otherwise 0 */
   uint64_t uncompressed_offset; /* NEW/INTRA: offset in the layer blob */
 } ngpu_result;
 
@@ -270,6 +273,93 @@ void ngpu_pack_abort(ngpu_pack *p);
 int ngpu_chunk_table(const ngpu_chunk *chunks, const ngpu_result *results,
                      uint64_t n, uint8_t *out /* cap x 80 */, uint64_t cap,
                      uint64_t *n_records);
+
+/* ---- nydus blob stream: converter.Pack's output --
+ * The stream nydus-image writes for `--type tar-rafs --blob-inline-meta
+ * --features blob-toc` (builder.go:97-110) and packFromTar copies to `dest`
+ * (convert_unix.go:486-495): `data | tar_header | ... | toc | tar_header`
+ * (convert_unix.go:296-300).  Entries: image.blob (the layer's NEW chunks in
+ * index order, each compressed on its own, raw when compression does not
+ * shrink it), image.boot (RAFS v6 bootstrap: blob table + chunk table),
+ * rafs.blob.toc (128-B TOCEntry records, types.go:147-163).  Compression and
+ * SHA-256 run on the host (north star: compression stays on the host path). */
+
+/* PackOption.Compressor / TOCEntry.Flags values (types.go:22-31). */
+enum ngpu_compressor {
+  NGPU_COMPRESSOR_NONE = 0x1,
+  NGPU_COMPRESSOR_ZSTD = 0x2,
+  NGPU_COMPRESSOR_LZ4_BLOCK = 0x4
+};
+
+/* io.Writer: return 0 after consuming all len bytes, non-zero on error. */
+typedef int (*ngpu_write_fn)(void *ctx, const void *buf, uint64_t len);
+/* content.ReaderAt: bytes read (> 0) or a negative error. */
+typedef int64_t (*ngpu_read_at_fn)(void *ctx, void *buf, uint64_t len, uint64_t off);
+
+typedef struct {
+  uint32_t compressor;   /* enum ngpu_compressor; 0 -> zstd */
+  int32_t level;         /* compressor level; 0 -> library default (zstd: 1) */
+  uint32_t threads;      /* host compression threads; 0 -> min(16, cores) */
+  uint32_t digester;     /* ngpu_blob_write only: bootstrap digest flag */
+  uint32_t chunk_size;   /* ngpu_blob_write only: bootstrap chunk size */
+  uint32_t n_dict_blobs; /* records in dict_blobs */
+  const uint8_t *dict_blobs; /* the chunk dict's blob table (n x 256-B RAFS v6
+                                blob records, inner-index order), or NULL;
+                                ngpu_pack_finish defaults to the table
+                                ngpu_dict_load_bootstrap read */
+} ngpu_blob_options;
+
+typedef struct {
+  uint64_t stream_bytes;      /* bytes written to dest */
+  uint64_t blob_bytes;        /* image.blob: compressed chunk data */
+  uint64_t bootstrap_bytes;   /* image.boot */
+  uint64_t blob_chunks;       /* chunk records in the bootstrap (NEW chunks) */
+  uint64_t compressed_chunks; /* of which stored compressed */
+  uint8_t stream_digest[32];  /* sha256 of the whole stream: the layer blob
+                                 digest (LayerConvertFunc, convert_unix.go:870-914) */
+  uint8_t blob_digest[32];    /* sha256 of image.blob (the own blob's id) */
+  uint8_t toc_digest[32];     /* sha256 of the TOC (calcBlobTOCDigest :541-555) */
+} ngpu_blob_info;
+
+/* Thread-local message of the last failing engine-less call below. */
+const char *ngpu_host_error(void);
+
+/* Host: write the stream of one packed layer whose bytes are in host memory
+ * (chunks/results/stats as returned by ngpu_pack_tar / ngpu_process). */
+int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
+                    const ngpu_result *results, uint64_t n, const ngpu_layer_stats *stats,
+                    const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx,
+                    ngpu_blob_info *info);
+
+/* Streaming Pack that writes the stream at the end: NGPU_PACK_RETAIN keeps the
+ * layer bytes in HBM (288 GB) instead of recycling the device slots, so that
+ * ngpu_pack_finish can gather the NEW chunks on the GPU, copy only those to
+ * the host and compress them.  ngpu_pack_finish = ngpu_pack_close + stream
+ * (releases the pack in every case). */
+#define NGPU_PACK_RETAIN 0x1u
+int ngpu_pack_open_ex(ngpu_engine *eng, uint32_t flags, ngpu_pack **out);
+int ngpu_pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx,
+                     ngpu_chunk **chunks_out, ngpu_result **results_out, uint64_t *n_out,
+                     ngpu_layer_stats *stats, ngpu_blob_info *info);
+
+/* UnpackEntry (convert_unix.go:284-320): find `name` through the TOC
+ * (seekFileByTOC :219-276; entry compressor none or zstd), else by walking
+ * the tar headers from the tail (seekFileByTarHeader :162-213), and copy its
+ * data to w.  toc_entry_out (128 B, may be NULL) receives the TOC entry, or
+ * zeros when found by tar header.  NGPU_ENOTFOUND = ErrNotFound. */
+int ngpu_unpack_entry(ngpu_read_at_fn ra, void *ctx, uint64_t size, const char *name,
+                      ngpu_write_fn w, void *wctx, uint8_t *toc_entry_out);
+
+/* converter.Merge's blob bookkeeping (convert_unix.go:560-666, tool.Merge
+ * builder.go:220-294): merge per-layer bootstraps (the image.boot entries)
+ * into one written to w.  A layer's own blob (any blob not in the chunk dict
+ * bootstrap's blob table) is named layer_digests[l] (hex of Layer.Digest, the
+ * bootstrap file name the reference passes to nydus-image merge); at most one
+ * per layer.  *blob_ids_out (malloc'd, ngpu_free_host) = comma-separated blob
+ * ids in first-appearance order (the output JSON's "Blobs"). */
+int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
+               const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
+               uint64_t dict_size, ngpu_write_fn w, void *ctx, char **blob_ids_out);
 
 #ifdef __cplusplus
 }

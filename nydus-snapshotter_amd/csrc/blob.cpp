@@ -1,0 +1,767 @@
+// blob.cpp — host blob stream of converter.Pack (SURVEY.md §8(f) next-3,
+// §8(a) a9): what `nydus-image create --type tar-rafs --blob-inline-meta
+// --features blob-toc` (pkg/converter/tool/builder.go:97-110) writes to the
+// FIFO that packFromTar copies to `dest` (convert_unix.go:486-495), and the
+// host readers converter.Merge needs (UnpackEntry, convert_unix.go:162-320).
+//
+// Stream layout (the reference reader's contract, convert_unix.go:296-300):
+//   image.blob data | ustar hdr | image.boot | ustar hdr | TOC | ustar hdr
+// * image.blob: the layer's NEW chunks in index order, each compressed on its
+//   own (none / zstd / lz4_block) and stored raw when compression does not
+//   shrink it (chunk flag bit 0 clear) — both rules as the reference v6
+//   fixture shows them; compressed offsets back to back.
+// * image.boot: RAFS v6 super block + extended super block, blob table at
+//   4096 (256-B records) and chunk table (80-B records), as decoded from the
+//   fixture.  The layer's own blob id is the sha256 of its image.blob data;
+//   Merge renames it to the layer digest (see ngpu_merge).
+// * rafs.blob.toc: 128-B TOCEntry records (types.go:147-163) for image.blob
+//   and image.boot; calcBlobTOCDigest (convert_unix.go:541-555) = sha256 of it.
+// Entry data is not padded: the reader walks back by size + 512
+// (convert_unix.go:162-213).
+//
+// Compression stays on the host (north star): zstd / lz4 are the system
+// libzstd.so.1 / liblz4.so.1, loaded with dlopen; SHA-256 is OpenSSL.
+// Not byte-pinned against nydus-image (unavailable here): compressed chunk
+// bytes depend on the compressor library version; the pinned properties are
+// the layout rules above and the reference reader's ability to find and
+// decode every entry (tests/test_blob.py).
+#include <dlfcn.h>
+#include <openssl/evp.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+
+#include "blob.hpp"
+
+namespace ngpu {
+namespace {
+
+thread_local std::string g_host_err;
+
+int host_fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int host_fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_host_err = buf;
+  return code;
+}
+
+// ---- compressors ----------------------------------------------------------
+struct Codecs {
+  size_t (*zstd_compress)(void *, size_t, const void *, size_t, int) = nullptr;
+  size_t (*zstd_decompress)(void *, size_t, const void *, size_t) = nullptr;
+  size_t (*zstd_bound)(size_t) = nullptr;
+  unsigned (*zstd_is_error)(size_t) = nullptr;
+  int (*lz4_compress)(const char *, char *, int, int) = nullptr;
+  int (*lz4_bound)(int) = nullptr;
+};
+
+const Codecs &codecs() {
+  static Codecs c;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    if (void *z = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL)) {
+      c.zstd_compress = (decltype(c.zstd_compress))dlsym(z, "ZSTD_compress");
+      c.zstd_decompress = (decltype(c.zstd_decompress))dlsym(z, "ZSTD_decompress");
+      c.zstd_bound = (decltype(c.zstd_bound))dlsym(z, "ZSTD_compressBound");
+      c.zstd_is_error = (decltype(c.zstd_is_error))dlsym(z, "ZSTD_isError");
+    }
+    if (void *l = dlopen("liblz4.so.1", RTLD_NOW | RTLD_LOCAL)) {
+      c.lz4_compress = (decltype(c.lz4_compress))dlsym(l, "LZ4_compress_default");
+      c.lz4_bound = (decltype(c.lz4_bound))dlsym(l, "LZ4_compressBound");
+    }
+  });
+  return c;
+}
+
+uint64_t compress_bound(uint32_t kind, uint32_t n) {
+  const Codecs &c = codecs();
+  if (kind == NGPU_COMPRESSOR_ZSTD) return c.zstd_bound(n);
+  if (kind == NGPU_COMPRESSOR_LZ4_BLOCK) return (uint64_t)c.lz4_bound((int)n);
+  return n;
+}
+
+// Compressed size, or 0 when the chunk is to be stored raw.
+uint64_t compress_one(uint32_t kind, int level, const uint8_t *src, uint32_t n, uint8_t *dst,
+                      uint64_t cap) {
+  const Codecs &c = codecs();
+  uint64_t r = 0;
+  if (kind == NGPU_COMPRESSOR_ZSTD) {
+    const size_t z = c.zstd_compress(dst, cap, src, n, level ? level : 1);
+    r = c.zstd_is_error(z) ? 0 : z;
+  } else if (kind == NGPU_COMPRESSOR_LZ4_BLOCK) {
+    const int z = c.lz4_compress((const char *)src, (char *)dst, (int)n, (int)cap);
+    r = z > 0 ? (uint64_t)z : 0;
+  }
+  return r < n ? r : 0;  // no gain: store raw (fixture: flags 0, csize == usize)
+}
+
+// nydus compress::Algorithm numbering in the blob table (fixture: lz4_block = 1)
+uint32_t blob_compression_algo(uint32_t kind) {
+  switch (kind) {
+    case NGPU_COMPRESSOR_LZ4_BLOCK: return 1;
+    case NGPU_COMPRESSOR_ZSTD: return 3;
+    default: return 0;
+  }
+}
+
+// RafsSuperFlags (fixture ext-SB flags 0x6 = lz4 0x2 | blake3 0x4)
+uint64_t super_flags(uint32_t kind, uint32_t digester) {
+  uint64_t f = digester == NGPU_DIGEST_SHA256 ? 0x8 : 0x4;
+  if (kind == NGPU_COMPRESSOR_LZ4_BLOCK) f |= 0x2;
+  else if (kind == NGPU_COMPRESSOR_ZSTD) f |= 0x80;
+  else f |= 0x1;
+  return f;
+}
+
+// ---- SHA-256 (OpenSSL EVP) -------------------------------------------------
+struct Sha {
+  EVP_MD_CTX *c = EVP_MD_CTX_new();
+  Sha() { EVP_DigestInit_ex(c, EVP_sha256(), nullptr); }
+  ~Sha() { EVP_MD_CTX_free(c); }
+  void update(const void *p, uint64_t n) { EVP_DigestUpdate(c, p, n); }
+  void final(uint8_t out[32]) {
+    unsigned int l = 32;
+    EVP_DigestFinal_ex(c, out, &l);
+  }
+  void copy_from(const Sha &o) { EVP_MD_CTX_copy_ex(c, o.c); }
+};
+
+void sha256(const void *p, uint64_t n, uint8_t out[32]) {
+  Sha s;
+  s.update(p, n);
+  s.final(out);
+}
+
+std::string hex(const uint8_t *d, int n) {
+  static const char *x = "0123456789abcdef";
+  std::string s(2 * n, '0');
+  for (int i = 0; i < n; ++i) {
+    s[2 * i] = x[d[i] >> 4];
+    s[2 * i + 1] = x[d[i] & 15];
+  }
+  return s;
+}
+
+// ---- ustar headers ---------------------------------------------------------
+void put_octal(char *f, int width, uint64_t v) {  // width-1 digits + NUL
+  for (int i = width - 2; i >= 0; --i, v >>= 3) f[i] = (char)('0' + (v & 7));
+  f[width - 1] = 0;
+}
+
+void tar_header(uint8_t h[512], const char *name, uint64_t size) {
+  memset(h, 0, 512);
+  char *b = (char *)h;
+  strncpy(b, name, 100);
+  put_octal(b + 100, 8, 0644);
+  put_octal(b + 108, 8, 0);
+  put_octal(b + 116, 8, 0);
+  if (size < (1ull << 33)) {
+    put_octal(b + 124, 12, size);
+  } else {  // GNU base-256 (archive/tar parseNumeric accepts it)
+    h[124] = 0x80;
+    for (int i = 11; i >= 1; --i, size >>= 8) h[124 + i] = (uint8_t)size;
+  }
+  put_octal(b + 136, 12, 0);
+  b[156] = '0';
+  memcpy(b + 257, "ustar\0" "00", 8);
+  memset(b + 148, ' ', 8);
+  uint32_t sum = 0;
+  for (int i = 0; i < 512; ++i) sum += h[i];
+  put_octal(b + 148, 7, sum);
+  b[155] = ' ';
+}
+
+int64_t parse_numeric(const uint8_t *f, int w) {
+  if (f[0] & 0x80) {  // base-256
+    uint64_t v = f[0] & 0x7f;
+    for (int i = 1; i < w; ++i) v = (v << 8) | f[i];
+    return (int64_t)v;
+  }
+  int64_t v = 0;
+  int i = 0;
+  while (i < w && (f[i] == ' ' || f[i] == 0)) ++i;
+  for (; i < w && f[i] >= '0' && f[i] <= '7'; ++i) v = v * 8 + (f[i] - '0');
+  return v;
+}
+
+// Parses one header block: name and size.  Returns false if it is not a
+// valid tar header (checksum), as archive/tar's Reader.Next would fail.
+bool read_header(const uint8_t h[512], std::string *name, int64_t *size) {
+  uint32_t sum = 0;
+  for (int i = 0; i < 512; ++i) sum += (i >= 148 && i < 156) ? ' ' : h[i];
+  if ((int64_t)sum != parse_numeric(h + 148, 8)) return false;
+  const char *b = (const char *)h;
+  std::string nm(b, strnlen(b, 100));
+  if (memcmp(b + 257, "ustar", 5) == 0 && b[345]) {  // ustar prefix
+    std::string pre(b + 345, strnlen(b + 345, 155));
+    nm = pre + "/" + nm;
+  }
+  *name = nm;
+  *size = parse_numeric(h + 124, 12);
+  return *size >= 0;
+}
+
+// ---- small thread pool for per-chunk compression ---------------------------
+class Pool {
+ public:
+  explicit Pool(unsigned n) {
+    for (unsigned i = 0; i + 1 < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  // Runs f(i) for i in [0, n) on the pool and the calling thread.
+  template <typename F>
+  void run(uint64_t n, F &&f) {
+    std::function<void(uint64_t)> fn = f;
+    std::atomic<uint64_t> next{0};
+    auto body = [&] {
+      for (uint64_t i; (i = next.fetch_add(1)) < n;) fn(i);
+    };
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = [&] { body(); };
+      gen_++;
+      active_ = (unsigned)th_.size();
+    }
+    cv_.notify_all();
+    body();
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return active_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      auto job = job_;
+      g.unlock();
+      job();
+      g.lock();
+      if (--active_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::function<void()> job_;
+  uint64_t gen_ = 0;
+  unsigned active_ = 0;
+  bool stop_ = false;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+};
+
+}  // namespace
+
+const char *host_error() { return g_host_err.c_str(); }
+
+std::string blob_id_of(const RafsV6BlobInfo &b) {
+  return std::string(b.blob_id, strnlen(b.blob_id, sizeof b.blob_id));
+}
+
+int parse_bootstrap(const uint8_t *p, uint64_t n, Bootstrap *out) {
+  if (n < kRafsV6ExtSuperBlockOffset + 64) return host_fail(NGPU_EFORMAT, "bootstrap too small");
+  uint32_t magic;
+  memcpy(&magic, p + kRafsV6SuperBlockOffset, 4);
+  if (magic != kRafsV6Magic) return host_fail(NGPU_EFORMAT, "not a RAFS v6 bootstrap");
+  const uint8_t *x = p + kRafsV6ExtSuperBlockOffset;
+  uint64_t bto, cto, cts;
+  uint32_t bts;
+  memcpy(&out->flags, x, 8);
+  memcpy(&bto, x + 8, 8);
+  memcpy(&bts, x + 16, 4);
+  memcpy(&out->chunk_size, x + 20, 4);
+  memcpy(&cto, x + 24, 8);  // RafsV6ChunkInfoOffset = 1024+128+24 (layout.go:27)
+  memcpy(&cts, x + 32, 8);
+  if (bts % sizeof(RafsV6BlobInfo) || cts % sizeof(RafsV6ChunkInfo) || bto > n ||
+      bts > n - bto || cto > n || cts > n - cto)
+    return host_fail(NGPU_EFORMAT, "bad blob/chunk table bounds");
+  out->blobs.resize(bts / sizeof(RafsV6BlobInfo));
+  if (bts) memcpy(out->blobs.data(), p + bto, bts);
+  out->chunks.resize(cts / sizeof(RafsV6ChunkInfo));
+  if (cts) memcpy(out->chunks.data(), p + cto, cts);
+  return 0;
+}
+
+std::vector<uint8_t> write_bootstrap(const Bootstrap &b) {
+  const uint64_t bts = b.blobs.size() * sizeof(RafsV6BlobInfo);
+  const uint64_t cto = kBlobTableOffset + (bts + 4095) / 4096 * 4096;
+  const uint64_t cts = b.chunks.size() * sizeof(RafsV6ChunkInfo);
+  std::vector<uint8_t> v(cto + cts, 0);
+  memcpy(&v[kRafsV6SuperBlockOffset], &kRafsV6Magic, 4);
+  uint8_t *x = &v[kRafsV6ExtSuperBlockOffset];
+  const uint64_t bto = bts ? kBlobTableOffset : 0;
+  const uint32_t bts32 = (uint32_t)bts;
+  memcpy(x, &b.flags, 8);
+  memcpy(x + 8, &bto, 8);
+  memcpy(x + 16, &bts32, 4);
+  memcpy(x + 20, &b.chunk_size, 4);
+  memcpy(x + 24, &cto, 8);
+  memcpy(x + 32, &cts, 8);
+  if (bts) memcpy(&v[kBlobTableOffset], b.blobs.data(), bts);
+  if (cts) memcpy(&v[cto], b.chunks.data(), cts);
+  return v;
+}
+
+// ---- BlobWriter --------------------------------------------------------------
+struct BlobWriter::Impl {
+  ngpu_blob_options opt;
+  ngpu_write_fn w;
+  void *ctx;
+  std::vector<RafsV6BlobInfo> dict_blobs;
+  std::unique_ptr<Pool> pool;
+  Sha blob_sha;      // image.blob data
+  Sha stream_sha;    // whole stream (continued from blob_sha)
+  uint64_t written = 0;
+  std::vector<uint32_t> csize;  // per NEW chunk (index order)
+  std::vector<uint8_t> cflag;
+  uint64_t compressed_chunks = 0;
+  // batch buffers: per-chunk scratch slots, compacted into `out`
+  std::vector<uint8_t> scratch, out;
+  std::vector<uint64_t> slot_off;
+  std::vector<uint64_t> clen;
+  int rc = 0;
+
+  int emit(const void *p, uint64_t n) {
+    if (!n) return 0;
+    if (w && w(ctx, p, n) != 0) return host_fail(NGPU_EIO, "pack: dest write failed");
+    written += n;
+    return 0;
+  }
+};
+
+BlobWriter::BlobWriter(const ngpu_blob_options &opt, ngpu_write_fn w, void *ctx,
+                       std::vector<RafsV6BlobInfo> dict_blobs)
+    : im_(new Impl) {
+  im_->opt = opt;
+  if (!im_->opt.compressor) im_->opt.compressor = NGPU_COMPRESSOR_ZSTD;
+  im_->w = w;
+  im_->ctx = ctx;
+  im_->dict_blobs = std::move(dict_blobs);
+}
+
+BlobWriter::~BlobWriter() = default;
+
+int BlobWriter::init() {
+  const uint32_t k = im_->opt.compressor;
+  const Codecs &c = codecs();
+  if (k == NGPU_COMPRESSOR_ZSTD && !(c.zstd_compress && c.zstd_bound && c.zstd_is_error))
+    return host_fail(NGPU_EUNSUPP, "zstd compressor unavailable (libzstd.so.1)");
+  if (k == NGPU_COMPRESSOR_LZ4_BLOCK && !(c.lz4_compress && c.lz4_bound))
+    return host_fail(NGPU_EUNSUPP, "lz4_block compressor unavailable (liblz4.so.1)");
+  if (k != NGPU_COMPRESSOR_NONE && k != NGPU_COMPRESSOR_ZSTD && k != NGPU_COMPRESSOR_LZ4_BLOCK)
+    return host_fail(NGPU_EINVAL, "unsupported compressor 0x%x", k);
+  unsigned t = im_->opt.threads;
+  if (!t) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    t = hw ? std::min(16u, hw) : 4u;
+  }
+  im_->pool.reset(new Pool(t));
+  return 0;
+}
+
+int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) {
+  Impl &m = *im_;
+  if (m.rc) return m.rc;
+  const uint32_t kind = m.opt.compressor;
+  // batches of <= 64 MiB of input keep the scratch bounded
+  uint64_t a = 0;
+  while (a < k) {
+    uint64_t b = a, bytes = 0;
+    while (b < k && (b == a || bytes + len[b] <= (64ull << 20))) bytes += len[b++];
+    const uint64_t nb = b - a;
+    if (kind == NGPU_COMPRESSOR_NONE) {
+      m.out.resize(bytes);
+      m.slot_off.resize(nb + 1);
+      m.slot_off[0] = 0;
+      for (uint64_t i = 0; i < nb; ++i) m.slot_off[i + 1] = m.slot_off[i] + len[a + i];
+      m.pool->run(nb, [&](uint64_t i) { memcpy(&m.out[m.slot_off[i]], src[a + i], len[a + i]); });
+      for (uint64_t i = 0; i < nb; ++i) {
+        m.csize.push_back(len[a + i]);
+        m.cflag.push_back(0);
+      }
+    } else {
+      m.slot_off.resize(nb + 1);
+      m.slot_off[0] = 0;
+      for (uint64_t i = 0; i < nb; ++i)
+        m.slot_off[i + 1] = m.slot_off[i] + compress_bound(kind, len[a + i]);
+      m.scratch.resize(m.slot_off[nb]);
+      m.clen.assign(nb, 0);
+      m.pool->run(nb, [&](uint64_t i) {
+        m.clen[i] = compress_one(kind, m.opt.level, src[a + i], len[a + i], &m.scratch[m.slot_off[i]],
+                                 m.slot_off[i + 1] - m.slot_off[i]);
+      });
+      uint64_t total = 0;
+      for (uint64_t i = 0; i < nb; ++i) total += m.clen[i] ? m.clen[i] : len[a + i];
+      m.out.resize(total);
+      uint64_t o = 0;
+      for (uint64_t i = 0; i < nb; ++i) {
+        const bool z = m.clen[i] != 0;
+        const uint64_t c = z ? m.clen[i] : len[a + i];
+        memcpy(&m.out[o], z ? &m.scratch[m.slot_off[i]] : src[a + i], c);
+        o += c;
+        m.csize.push_back((uint32_t)c);
+        m.cflag.push_back(z ? 1 : 0);
+        m.compressed_chunks += z;
+      }
+    }
+    m.blob_sha.update(m.out.data(), m.out.size());
+    if ((m.rc = m.emit(m.out.data(), m.out.size()))) return m.rc;
+    a = b;
+  }
+  return 0;
+}
+
+int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_t n,
+                       const ngpu_layer_stats &st, ngpu_blob_info *info) {
+  Impl &m = *im_;
+  if (m.rc) return m.rc;
+  const uint32_t kind = m.opt.compressor;
+  const uint64_t blob_bytes = m.written;
+  // image.blob digest; the stream digest continues from the same state
+  uint8_t blob_dig[32], boot_dig[32], toc_dig[32], stream_dig[32];
+  m.stream_sha.copy_from(m.blob_sha);
+  m.blob_sha.final(blob_dig);
+
+  // chunk table: NEW chunks in index order with their compressed placement
+  Bootstrap b;
+  b.flags = super_flags(kind, m.opt.digester);
+  b.chunk_size = m.opt.chunk_size;
+  uint64_t k = 0, coff = 0, uend = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const ngpu_result &r = res[i];
+    if (r.kind != NGPU_NEW) continue;
+    if (r.index != k || k >= m.csize.size())
+      return host_fail(NGPU_EINVAL, "pack: NEW chunk %llu out of index order",
+                       (unsigned long long)i);
+    RafsV6ChunkInfo c;
+    memset(&c, 0, sizeof c);
+    memcpy(c.block_id, r.digest, 32);
+    c.blob_index = r.blob_index;
+    c.flags = m.cflag[k];
+    c.compressed_size = m.csize[k];
+    c.uncompressed_size = chunks[i].length;
+    c.compressed_offset = coff;
+    c.uncompressed_offset = r.uncompressed_offset;
+    c.file_offset = chunks[i].file_offset;
+    c.index = r.index;
+    b.chunks.push_back(c);
+    coff += m.csize[k];
+    uend = std::max<uint64_t>(uend, r.uncompressed_offset + chunks[i].length);
+    ++k;
+  }
+  if (k != m.csize.size()) return host_fail(NGPU_EINVAL, "pack: %llu chunk bodies for %llu NEW chunks",
+                                            (unsigned long long)m.csize.size(),
+                                            (unsigned long long)k);
+  // blob table in real-index (first-hit) order
+  b.blobs.assign(st.blobs, RafsV6BlobInfo{});
+  std::vector<bool> set(st.blobs, false);
+  if (st.own_blob_index != 0xFFFFFFFFu) {
+    if (st.own_blob_index >= st.blobs) return host_fail(NGPU_EINVAL, "pack: bad own blob index");
+    RafsV6BlobInfo &o = b.blobs[st.own_blob_index];
+    const std::string id = hex(blob_dig, 32);
+    memcpy(o.blob_id, id.data(), 64);
+    o.chunk_size = m.opt.chunk_size;
+    o.chunk_count = (uint32_t)k;
+    o.compression_algo = blob_compression_algo(kind);
+    o.digest_algo = m.opt.digester == NGPU_DIGEST_SHA256 ? 1 : 0;
+    o.features = 1;
+    o.compressed_size = coff;
+    o.uncompressed_size = (uend + 4095) / 4096 * 4096;
+    set[st.own_blob_index] = true;
+  }
+  for (uint64_t i = 0; i < n; ++i) {
+    const ngpu_result &r = res[i];
+    if (r.kind != NGPU_DICT) continue;
+    if (r.blob_index >= st.blobs) return host_fail(NGPU_EINVAL, "pack: bad dict blob index");
+    if (set[r.blob_index]) continue;
+    RafsV6BlobInfo &d = b.blobs[r.blob_index];
+    if (r.dict_blob < m.dict_blobs.size()) {
+      d = m.dict_blobs[r.dict_blob];
+    } else {  // dict given as arrays without a blob table: a stable placeholder id
+      char id[65];
+      snprintf(id, sizeof id, "%064x", r.dict_blob);
+      memcpy(d.blob_id, id, 64);
+      d.chunk_size = m.opt.chunk_size;
+    }
+    set[r.blob_index] = true;
+  }
+  for (uint32_t i = 0; i < st.blobs; ++i) {
+    if (!set[i]) return host_fail(NGPU_EINVAL, "pack: blob %u never referenced", i);
+    b.blobs[i].blob_index = i;
+  }
+  const std::vector<uint8_t> boot = write_bootstrap(b);
+  sha256(boot.data(), boot.size(), boot_dig);
+
+  // tail: hdr(image.blob) | image.boot | hdr(image.boot) | TOC | hdr(toc)
+  TocEntry toc[2];
+  memset(toc, 0, sizeof toc);
+  toc[0].flags = NGPU_COMPRESSOR_NONE;
+  strncpy(toc[0].name, "image.blob", sizeof toc[0].name);
+  memcpy(toc[0].uncompressed_digest, blob_dig, 32);
+  toc[0].compressed_offset = 0;
+  toc[0].compressed_size = toc[0].uncompressed_size = blob_bytes;
+  toc[1].flags = NGPU_COMPRESSOR_NONE;
+  strncpy(toc[1].name, "image.boot", sizeof toc[1].name);
+  memcpy(toc[1].uncompressed_digest, boot_dig, 32);
+  toc[1].compressed_offset = blob_bytes + 512;
+  toc[1].compressed_size = toc[1].uncompressed_size = boot.size();
+  sha256(toc, sizeof toc, toc_dig);
+
+  std::vector<uint8_t> tail(512 + boot.size() + 512 + sizeof toc + 512);
+  uint8_t *t = tail.data();
+  tar_header(t, "image.blob", blob_bytes);
+  memcpy(t + 512, boot.data(), boot.size());
+  tar_header(t + 512 + boot.size(), "image.boot", boot.size());
+  memcpy(t + 1024 + boot.size(), toc, sizeof toc);
+  tar_header(t + 1024 + boot.size() + sizeof toc, "rafs.blob.toc", sizeof toc);
+  m.stream_sha.update(tail.data(), tail.size());
+  m.stream_sha.final(stream_dig);
+  if ((m.rc = m.emit(tail.data(), tail.size()))) return m.rc;
+  if (info) {
+    memset(info, 0, sizeof *info);
+    info->stream_bytes = m.written;
+    info->blob_bytes = blob_bytes;
+    info->bootstrap_bytes = boot.size();
+    info->blob_chunks = k;
+    info->compressed_chunks = m.compressed_chunks;
+    memcpy(info->stream_digest, stream_dig, 32);
+    memcpy(info->blob_digest, blob_dig, 32);
+    memcpy(info->toc_digest, toc_dig, 32);
+  }
+  return 0;
+}
+
+namespace {
+
+// ---- UnpackEntry (convert_unix.go:162-320) ---------------------------------
+struct Reader {
+  ngpu_read_at_fn ra;
+  void *ctx;
+  uint64_t size;
+  int read(void *buf, uint64_t n, uint64_t off) const {
+    if (off > size || n > size - off) return host_fail(NGPU_EFORMAT, "read beyond end");
+    uint8_t *p = (uint8_t *)buf;
+    while (n) {
+      const int64_t r = ra(ctx, p, n, off);
+      if (r <= 0) return host_fail(NGPU_EIO, "read_at failed at %llu", (unsigned long long)off);
+      p += r;
+      off += (uint64_t)r;
+      n -= (uint64_t)r;
+    }
+    return 0;
+  }
+};
+
+// seekFileByTarHeader (convert_unix.go:162-213): walk headers from the tail.
+int seek_by_tar_header(const Reader &r, const std::string &target, int64_t max_size,
+                       uint64_t *off, uint64_t *len) {
+  if (r.size < 512) return host_fail(NGPU_EFORMAT, "invalid nydus tar size %llu",
+                                     (unsigned long long)r.size);
+  int64_t cur = (int64_t)r.size - 512;
+  for (;;) {
+    uint8_t h[512];
+    int rc = r.read(h, 512, (uint64_t)cur);
+    if (rc) return rc;
+    std::string name;
+    int64_t sz;
+    if (!read_header(h, &name, &sz)) return host_fail(NGPU_EFORMAT, "parse nydus tar header");
+    if (cur < sz) return host_fail(NGPU_EFORMAT, "invalid nydus tar data, name %s, size %lld",
+                                   name.c_str(), (long long)sz);
+    if (name == target) {
+      if (max_size >= 0 && sz > max_size)
+        return host_fail(NGPU_EFORMAT, "invalid nydus tar size %llu", (unsigned long long)r.size);
+      *off = (uint64_t)(cur - sz);
+      *len = (uint64_t)sz;
+      return 0;
+    }
+    cur = cur - sz - 512;
+    if (cur < 0) break;
+  }
+  return host_fail(NGPU_ENOTFOUND, "can't find target %s by seeking tar", target.c_str());
+}
+
+int copy_range(const Reader &r, uint64_t off, uint64_t len, ngpu_write_fn w, void *wctx) {
+  std::vector<uint8_t> buf(std::min<uint64_t>(len, 8ull << 20) + 1);
+  while (len) {
+    const uint64_t k = std::min<uint64_t>(len, buf.size());
+    int rc = r.read(buf.data(), k, off);
+    if (rc) return rc;
+    if (w && w(wctx, buf.data(), k) != 0) return host_fail(NGPU_EIO, "copy target data to writer");
+    off += k;
+    len -= k;
+  }
+  return 0;
+}
+
+}  // namespace
+}  // namespace ngpu
+
+using namespace ngpu;
+
+extern "C" {
+
+const char *ngpu_host_error(void) { return host_error(); }
+
+int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
+                    const ngpu_result *results, uint64_t n, const ngpu_layer_stats *stats,
+                    const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx,
+                    ngpu_blob_info *info) {
+  if ((n && (!data || !chunks || !results)) || !stats || !opt || !w)
+    return host_fail(NGPU_EINVAL, "ngpu_blob_write: bad argument");
+  std::vector<RafsV6BlobInfo> dict(opt->n_dict_blobs);
+  if (opt->n_dict_blobs) {
+    if (!opt->dict_blobs) return host_fail(NGPU_EINVAL, "ngpu_blob_write: dict_blobs is NULL");
+    memcpy(dict.data(), opt->dict_blobs, dict.size() * sizeof(RafsV6BlobInfo));
+  }
+  BlobWriter bw(*opt, w, ctx, std::move(dict));
+  int rc = bw.init();
+  if (rc) return rc;
+  std::vector<const uint8_t *> src;
+  std::vector<uint32_t> lens;
+  const uint8_t *base = (const uint8_t *)data;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (results[i].kind != NGPU_NEW) continue;
+    if (chunks[i].offset > len || chunks[i].length > len - chunks[i].offset)
+      return host_fail(NGPU_EINVAL, "ngpu_blob_write: chunk %llu out of bounds",
+                       (unsigned long long)i);
+    src.push_back(base + chunks[i].offset);
+    lens.push_back(chunks[i].length);
+  }
+  rc = bw.add(src.data(), lens.data(), src.size());
+  if (!rc) rc = bw.finish(chunks, results, n, *stats, info);
+  return rc;
+}
+
+int ngpu_unpack_entry(ngpu_read_at_fn ra, void *ctx, uint64_t size, const char *name,
+                      ngpu_write_fn w, void *wctx, uint8_t *toc_entry_out) {
+  if (!ra || !name) return host_fail(NGPU_EINVAL, "ngpu_unpack_entry: bad argument");
+  Reader r{ra, ctx, size};
+  if (toc_entry_out) memset(toc_entry_out, 0, sizeof(TocEntry));
+  // seekFileByTOC (convert_unix.go:219-276)
+  uint64_t toff = 0, tlen = 0;
+  int rc = seek_by_tar_header(r, "rafs.blob.toc", 1 << 20, &toff, &tlen);
+  if (rc == 0) {
+    if (tlen % sizeof(TocEntry)) return host_fail(NGPU_EFORMAT, "invalid entries length %llu",
+                                                  (unsigned long long)tlen);
+    std::vector<TocEntry> toc(tlen / sizeof(TocEntry));
+    if ((rc = r.read(toc.data(), tlen, toff))) return rc;
+    for (const TocEntry &e : toc) {
+      if (std::string(e.name, strnlen(e.name, sizeof e.name)) != name) continue;
+      const uint32_t comp = e.flags & 0xf;
+      if (comp == NGPU_COMPRESSOR_NONE) {
+        rc = copy_range(r, e.compressed_offset, e.compressed_size, w, wctx);
+      } else if (comp == NGPU_COMPRESSOR_ZSTD) {
+        const Codecs &c = codecs();
+        if (!c.zstd_decompress) return host_fail(NGPU_EUNSUPP, "zstd unavailable");
+        std::vector<uint8_t> in(e.compressed_size), out(e.uncompressed_size + 1);
+        if ((rc = r.read(in.data(), in.size(), e.compressed_offset))) return rc;
+        const size_t z = c.zstd_decompress(out.data(), out.size(), in.data(), in.size());
+        if (c.zstd_is_error(z)) return host_fail(NGPU_EFORMAT, "zstd: bad entry %s", name);
+        if (w && z && w(wctx, out.data(), z) != 0) return host_fail(NGPU_EIO, "write failed");
+      } else {
+        return host_fail(NGPU_EUNSUPP, "unsupported compressor %x", comp);
+      }
+      if (rc) return rc;
+      if (toc_entry_out) memcpy(toc_entry_out, &e, sizeof e);
+      return 0;
+    }
+  } else if (rc != NGPU_ENOTFOUND) {
+    return rc;
+  }
+  // seekFile fallback: old rafs blob format, by tar header (convert_unix.go:302-320)
+  uint64_t off = 0, len = 0;
+  if ((rc = seek_by_tar_header(r, name, -1, &off, &len))) return rc;
+  return copy_range(r, off, len, w, wctx);
+}
+
+int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
+               const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
+               uint64_t dict_size, ngpu_write_fn w, void *ctx, char **blob_ids_out) {
+  if ((n && (!bootstraps || !sizes)) || !blob_ids_out)
+    return host_fail(NGPU_EINVAL, "ngpu_merge: bad argument");
+  *blob_ids_out = nullptr;
+  std::vector<std::string> dict_ids;
+  if (dict_bootstrap) {
+    Bootstrap d;
+    int rc = parse_bootstrap((const uint8_t *)dict_bootstrap, dict_size, &d);
+    if (rc) return rc;
+    for (auto &b : d.blobs) dict_ids.push_back(blob_id_of(b));
+  }
+  Bootstrap out;
+  std::vector<std::string> ids;
+  for (uint64_t l = 0; l < n; ++l) {
+    Bootstrap b;
+    int rc = parse_bootstrap((const uint8_t *)bootstraps[l], sizes[l], &b);
+    if (rc) return rc;
+    if (!out.chunk_size) {
+      out.chunk_size = b.chunk_size;
+      out.flags = b.flags;
+    }
+    std::vector<uint32_t> local(b.blobs.size());
+    int own = 0;
+    for (size_t i = 0; i < b.blobs.size(); ++i) {
+      std::string id = blob_id_of(b.blobs[i]);
+      // A layer's own (non-dict) blob is named after the layer: the digest of
+      // its whole nydus tar stream, which Merge receives as Layer.Digest and
+      // uses as the bootstrap file name (convert_unix.go:567-573, 595-599).
+      const bool is_dict = std::find(dict_ids.begin(), dict_ids.end(), id) != dict_ids.end();
+      if (!is_dict) {
+        if (++own > 1)
+          return host_fail(NGPU_EFORMAT, "layer %llu has more than one non-dict blob",
+                           (unsigned long long)l);
+        if (layer_digests && layer_digests[l] && layer_digests[l][0]) id = layer_digests[l];
+      }
+      auto it = std::find(ids.begin(), ids.end(), id);
+      if (it == ids.end()) {
+        ids.push_back(id);
+        RafsV6BlobInfo nb = b.blobs[i];
+        memset(nb.blob_id, 0, sizeof nb.blob_id);
+        memcpy(nb.blob_id, id.data(), std::min<size_t>(id.size(), 64));
+        nb.blob_index = (uint32_t)out.blobs.size();
+        out.blobs.push_back(nb);
+        local[i] = nb.blob_index;
+      } else {
+        local[i] = (uint32_t)(it - ids.begin());
+      }
+    }
+    for (RafsV6ChunkInfo c : b.chunks) {
+      if (c.blob_index >= local.size()) return host_fail(NGPU_EFORMAT, "chunk blob index out of range");
+      c.blob_index = local[c.blob_index];
+      out.chunks.push_back(c);
+    }
+  }
+  if (!out.chunk_size) out.chunk_size = 0x100000;
+  const std::vector<uint8_t> boot = write_bootstrap(out);
+  if (w && w(ctx, boot.data(), boot.size()) != 0) return host_fail(NGPU_EIO, "write failed");
+  std::string s;
+  for (size_t i = 0; i < ids.size(); ++i) s += (i ? "," : "") + ids[i];
+  char *o = (char *)malloc(s.size() + 1);
+  if (!o) return NGPU_ENOMEM;
+  memcpy(o, s.c_str(), s.size() + 1);
+  *blob_ids_out = o;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+// blob.hpp — host side of converter.Pack's output stream (SURVEY.md §8(f)
+// next-3, §8(a) a9): per-chunk compression of the layer's NEW chunks, the
+// nydus tar-like stream `data | tar_header | ... | toc | tar_header`
+// (pkg/converter/convert_unix.go:296-300, 314-321) and the image.boot
+// bootstrap.  Shared by blob.cpp (C ABI) and pack.hip (streaming Pack finish).
+// Not installed.
+#pragma once
+
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "nydus_gpu.h"
+
+namespace ngpu {
+
+// RAFS v6 on-disk records (decoded from the reference fixture
+// pkg/filesystem/testdata/v6-bootstrap-chunk-pos-438272.tar.gz).
+#pragma pack(push, 1)
+struct RafsV6ChunkInfo {  // 80 B
+  uint8_t block_id[32];
+  uint32_t blob_index;
+  uint32_t flags;  // bit 0: chunk data compressed
+  uint32_t compressed_size;
+  uint32_t uncompressed_size;
+  uint64_t compressed_offset;
+  uint64_t uncompressed_offset;
+  uint64_t file_offset;
+  uint32_t index;
+  uint32_t reserved;
+};
+struct RafsV6BlobInfo {  // 256 B
+  char blob_id[64];      // 64 ASCII hex chars
+  uint32_t blob_index;
+  uint32_t chunk_size;
+  uint32_t chunk_count;
+  uint32_t compression_algo;  // nydus compress::Algorithm (fixture: lz4_block = 1)
+  uint32_t digest_algo;       // 0 blake3, 1 sha256
+  uint32_t features;          // fixture: 1 (4K-aligned uncompressed chunks)
+  uint64_t compressed_size;   // end of the chunk data
+  uint64_t uncompressed_size; // 4K-aligned end of the uncompressed chunks
+  uint8_t meta[152];          // blob.meta location fields (zero: not emitted)
+};
+struct TocEntry {  // 128 B, pkg/converter/types.go:147-163
+  uint32_t flags;  // compressor of the entry data (types.go:22-31)
+  uint32_t reserved1;
+  char name[16];
+  uint8_t uncompressed_digest[32];  // sha256 of the uncompressed entry data
+  uint64_t compressed_offset;
+  uint64_t compressed_size;
+  uint64_t uncompressed_size;
+  uint8_t reserved2[48];  // Go reads the first 124 B of each 128-B entry (types.go:147-163, convert_unix.go:220)
+};
+#pragma pack(pop)
+static_assert(sizeof(RafsV6ChunkInfo) == 80, "RAFS v6 chunk info is 80 bytes");
+static_assert(sizeof(RafsV6BlobInfo) == 256, "RAFS v6 blob info is 256 bytes");
+static_assert(sizeof(TocEntry) == 128, "TOC entry is 128 bytes");
+
+constexpr uint32_t kRafsV6Magic = 0xE0F5E1E2u;        // pkg/layout/layout.go:24
+constexpr uint64_t kRafsV6SuperBlockOffset = 1024;     // layout.go:26
+constexpr uint64_t kRafsV6ExtSuperBlockOffset = 1152;  // 1024 + 128
+constexpr uint64_t kBlobTableOffset = 4096;            // as in the reference fixture
+
+// Parsed (minimal) RAFS v6 bootstrap: blob table + chunk table.
+struct Bootstrap {
+  uint64_t flags = 0;
+  uint32_t chunk_size = 0;
+  std::vector<RafsV6BlobInfo> blobs;
+  std::vector<RafsV6ChunkInfo> chunks;
+};
+int parse_bootstrap(const uint8_t *p, uint64_t n, Bootstrap *out);
+std::vector<uint8_t> write_bootstrap(const Bootstrap &b);
+std::string blob_id_of(const RafsV6BlobInfo &b);
+
+// Sequential writer of the nydus formatted stream for one layer.
+class BlobWriter {
+ public:
+  // dict_blobs: the chunk dict's blob table (its inner-index order).
+  BlobWriter(const ngpu_blob_options &opt, ngpu_write_fn w, void *ctx,
+             std::vector<RafsV6BlobInfo> dict_blobs);
+  ~BlobWriter();
+  int init();  // loads the compressor; NGPU_EUNSUPP if unavailable
+  // NEW chunks in index order (src[k] = host bytes of chunk with index
+  // base+k).  The bytes may be reused as soon as the call returns.
+  int add(const uint8_t *const *src, const uint32_t *len, uint64_t k);
+  // Writes image.blob's header, image.boot and the TOC.
+  int finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_t n,
+             const ngpu_layer_stats &st, ngpu_blob_info *info);
+  const std::string &error() const { return err_; }
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> im_;
+  std::string err_;
+};
+
+}  // namespace ngpu

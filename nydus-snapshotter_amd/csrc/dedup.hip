@@ -161,7 +161,7 @@ __global__ void dedup_probe(const ngpu_chunk *__restrict__ chunks, uint64_t n,
     atomicMin(blob_first + (uint64_t)chunk_layer[c] * (n_blobs + 1) + h.blob, (uint32_t)c);
   }
   r.kind = kind;
-  r.reserved = 0;
+  r.dict_blob = kind == NGPU_DICT ? h.blob : 0u;
   newflag[c] = 0;
 }
 

@@ -130,6 +130,7 @@ void free_dict(ngpu_engine *e) {
   e->d_dict_usize = e->d_dict_blob = e->d_dict_index = nullptr;
   e->d_dict_table = nullptr;
   e->dict = DictDevice{};
+  e->dict_blobs.clear();
 }
 
 // Digest stage: resets the layer stats, runs the digest kernels.
@@ -216,6 +217,10 @@ int ngpu_abi_version(void) { return NGPU_ABI_VERSION; }
 
 // internal (host.cpp), not part of nydus_gpu.h
 uint32_t ngpu_engine_chunk_size(const ngpu_engine *e) { return e->cfg.chunk_size; }
+void ngpu_engine_set_dict_blobs(ngpu_engine *e, const uint8_t *rec, uint64_t bytes) {
+  std::lock_guard<std::mutex> g(e->mu);
+  e->dict_blobs.assign(rec, rec + bytes);
+}
 
 int ngpu_device_count(void) {
   int n = 0;

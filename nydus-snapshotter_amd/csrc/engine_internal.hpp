@@ -4,6 +4,7 @@
 
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "common.hpp"
 
@@ -17,6 +18,9 @@ struct ngpu_engine {
   uint32_t *d_dict_usize = nullptr, *d_dict_blob = nullptr, *d_dict_index = nullptr;
   uint64_t *d_dict_table = nullptr;
   ngpu::DictDevice dict;
+  // blob table (256-B RAFS v6 records) of a bootstrap-loaded dict, for the
+  // blob writer's DICT blob entries (host copy; empty for array-loaded dicts)
+  std::vector<uint8_t> dict_blobs;
   // host-path device buffers
   uint8_t *d_data = nullptr;
   uint64_t d_data_cap = 0;

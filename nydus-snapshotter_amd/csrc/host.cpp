@@ -19,36 +19,19 @@
 
 #include <vector>
 
+#include "blob.hpp"
 #include "nydus_gpu.h"
 #include "tarstream.hpp"
 
-namespace {
-
-#pragma pack(push, 1)
-struct RafsV6ChunkInfo {  // 80 B, decoded from the v6 fixture
-  uint8_t block_id[32];
-  uint32_t blob_index;
-  uint32_t flags;
-  uint32_t compressed_size;
-  uint32_t uncompressed_size;
-  uint64_t compressed_offset;
-  uint64_t uncompressed_offset;
-  uint64_t file_offset;
-  uint32_t index;
-  uint32_t reserved;
-};
-#pragma pack(pop)
-static_assert(sizeof(RafsV6ChunkInfo) == 80, "RAFS v6 chunk info is 80 bytes");
-
-constexpr uint32_t kRafsV6Magic = 0xE0F5E1E2u;  // pkg/layout/layout.go:24
-constexpr uint64_t kRafsV6SuperBlockOffset = 1024;  // layout.go:26
-constexpr uint64_t kRafsV6ExtSuperBlockOffset = 1024 + 128;
-
-}  // namespace
+using ngpu::RafsV6ChunkInfo;
+using ngpu::kRafsV6ExtSuperBlockOffset;
+using ngpu::kRafsV6Magic;
+using ngpu::kRafsV6SuperBlockOffset;
 
 extern "C" {
 
 uint32_t ngpu_engine_chunk_size(const ngpu_engine *);  // engine.hip (internal)
+void ngpu_engine_set_dict_blobs(ngpu_engine *, const uint8_t *, uint64_t);
 
 int ngpu_tar_chunks(const void *tar_v, uint64_t len, uint32_t chunk_size, ngpu_chunk *out,
                     uint64_t cap, uint64_t *n_chunks, uint64_t *n_files) {
@@ -157,10 +140,13 @@ int ngpu_dict_load_bootstrap(ngpu_engine *eng, const char *path) {
     return NGPU_EFORMAT;
   }
   const uint8_t *ext = sb + kRafsV6ExtSuperBlockOffset;
-  uint64_t cto, cts;
+  uint64_t bto, cto, cts;
+  uint32_t bts;
+  memcpy(&bto, ext + 8, 8);
+  memcpy(&bts, ext + 16, 4);
   memcpy(&cto, ext + 24, 8);  // RafsV6ChunkInfoOffset = 1024+128+24 (layout.go:27)
   memcpy(&cts, ext + 32, 8);
-  if (cts % 80) {
+  if (cts % 80 || bts % 256) {
     fclose(f);
     return NGPU_EFORMAT;
   }
@@ -168,6 +154,11 @@ int ngpu_dict_load_bootstrap(ngpu_engine *eng, const char *path) {
   std::vector<RafsV6ChunkInfo> recs(m);
   if (m && (fseeko(f, (off_t)cto, SEEK_SET) != 0 ||
             fread(recs.data(), 80, m, f) != m)) {
+    fclose(f);
+    return NGPU_EFORMAT;
+  }
+  std::vector<uint8_t> blobs(bts);
+  if (bts && (fseeko(f, (off_t)bto, SEEK_SET) != 0 || fread(blobs.data(), 1, bts, f) != bts)) {
     fclose(f);
     return NGPU_EFORMAT;
   }
@@ -180,7 +171,9 @@ int ngpu_dict_load_bootstrap(ngpu_engine *eng, const char *path) {
     blob[i] = recs[i].blob_index;
     idx[i] = recs[i].index;
   }
-  return ngpu_dict_load(eng, dig.data(), us.data(), blob.data(), idx.data(), m);
+  const int rc = ngpu_dict_load(eng, dig.data(), us.data(), blob.data(), idx.data(), m);
+  if (rc == 0) ngpu_engine_set_dict_blobs(eng, blobs.data(), blobs.size());
+  return rc;
 }
 
 }  // extern "C"

@@ -17,6 +17,13 @@
 //   contiguous in exactly one slot.  While slot A is copied and hashed the
 //   caller fills slot B.  Dedup needs stream order over the whole layer, so it
 //   runs once at close over the device-resident digests.
+//
+// NGPU_PACK_RETAIN (ngpu_pack_finish): each slot is
+// copied into its own device segment that stays resident until the end (the
+// whole layer lives in HBM), so after dedup the NEW chunks are gathered on the
+// GPU into window buffers in blob (index) order and only those bytes cross
+// PCIe, window k+1's gather + D2H overlapping the host compression of window k
+// (blob.cpp BlobWriter).
 #include <stdlib.h>
 #include <string.h>
 
@@ -24,10 +31,13 @@
 #include <thread>
 #include <vector>
 
+#include "blob.hpp"
 #include "engine_internal.hpp"
 #include "tarstream.hpp"
 
 using namespace ngpu;
+
+extern "C" const char *ngpu_host_error(void);
 
 namespace {
 
@@ -40,6 +50,35 @@ struct Slot {
   hipEvent_t copied = nullptr, done = nullptr;
   bool busy = false;
 };
+
+// A retained device copy of one dispatched slot (NGPU_PACK_RETAIN).
+struct Seg {
+  uint8_t *d = nullptr;
+  uint64_t base = 0;     // stream offset of d[0]
+  uint64_t a = 0, b = 0; // chunks [a, b) live here
+};
+
+// Copies chunk k (src[k], len[k] bytes) to dst + doff[k] (16-B aligned).
+// One workgroup per chunk, grid-stride over chunks.
+__global__ __launch_bounds__(256) void gather_chunks(const uint64_t *__restrict__ src,
+                                                     const uint32_t *__restrict__ len,
+                                                     const uint64_t *__restrict__ doff,
+                                                     uint64_t count, uint8_t *__restrict__ dst) {
+  for (uint64_t k = blockIdx.x; k < count; k += gridDim.x) {
+    const uint8_t *s = reinterpret_cast<const uint8_t *>(src[k]);
+    uint8_t *d = dst + doff[k];
+    const uint32_t n = len[k];
+    uint32_t done = 0;
+    if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {
+      const uint32_t v = n >> 4;
+      const uint4 *s4 = reinterpret_cast<const uint4 *>(s);
+      uint4 *d4 = reinterpret_cast<uint4 *>(d);
+      for (uint32_t i = threadIdx.x; i < v; i += blockDim.x) d4[i] = s4[i];
+      done = v << 4;
+    }
+    for (uint32_t i = done + threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
+  }
+}
 
 // A few persistent threads that split large host copies into the pinned
 // staging slot (one memcpy thread tops out well below PCIe Gen5 H2D).
@@ -109,6 +148,8 @@ struct ngpu_pack : TarSink {
   ngpu_chunk *d_all = nullptr;
   hipStream_t copy = nullptr;
   CopyPool *pool = nullptr;  // created on the first large write
+  bool retain = false;       // NGPU_PACK_RETAIN: device segments kept to the end
+  std::vector<Seg> segs;
   int err = 0;
 
   explicit ngpu_pack(ngpu_engine *eng) : e(eng), sc(eng->cfg.chunk_size) {}
@@ -138,6 +179,7 @@ void release(ngpu_pack *p) {
     if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.done) (void)hipEventDestroy(s.done);
   }
+  for (Seg &g : p->segs) (void)hipFree(g.d);
   if (p->d_res) (void)hipFree(p->d_res);
   if (p->d_all) (void)hipFree(p->d_all);
   if (p->copy) (void)hipStreamDestroy(p->copy);
@@ -174,12 +216,22 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
   }
   int rc = grow_results(p, b);
   if (rc) return rc;
-  HIP_TRY(e, hipMemcpyAsync(s.d, s.h, s.fill, hipMemcpyHostToDevice, p->copy));
+  uint8_t *dev = s.d;
+  if (p->retain) {  // this slot's bytes get their own resident segment
+    Seg g;
+    HIP_TRY(e, hipMalloc((void **)&g.d, s.fill));
+    g.base = s.base;
+    g.a = a;
+    g.b = b;
+    p->segs.push_back(g);
+    dev = g.d;
+  }
+  HIP_TRY(e, hipMemcpyAsync(dev, s.h, s.fill, hipMemcpyHostToDevice, p->copy));
   HIP_TRY(e, hipMemcpyAsync(s.d_ch, s.h_ch, nch * sizeof(ngpu_chunk), hipMemcpyHostToDevice,
                             p->copy));
   HIP_TRY(e, hipEventRecord(s.copied, p->copy));
   HIP_TRY(e, hipStreamWaitEvent(e->stream, s.copied, 0));
-  rc = enqueue_digest(e, s.d, s.fill, s.d_ch, nch, p->d_res + a, e->stream);
+  rc = enqueue_digest(e, dev, s.fill, s.d_ch, nch, p->d_res + a, e->stream);
   if (rc) return rc;
   HIP_TRY(e, hipEventRecord(s.done, e->stream));
   s.busy = true;
@@ -211,16 +263,135 @@ int switch_slot(ngpu_pack *p) {
   return 0;
 }
 
+// After dedup: gather the NEW chunks from the retained segments in blob
+// (index) order into window buffers, copy each window to the host and hand it
+// to the BlobWriter; window k+1's gather + D2H run while the host compresses
+// window k.  Called with e->mu held.
+int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, void *ctx,
+                 const ngpu_chunk *ch, const ngpu_result *res, uint64_t n,
+                 const ngpu_layer_stats &st, ngpu_blob_info *info) {
+  ngpu_engine *e = p->e;
+  ngpu_blob_options o = opt;
+  o.digester = e->cfg.digester;
+  o.chunk_size = e->cfg.chunk_size;
+  std::vector<RafsV6BlobInfo> dict;
+  const uint8_t *rec = opt.dict_blobs;
+  uint64_t nrec = opt.n_dict_blobs;
+  if (!rec || !nrec) {
+    rec = e->dict_blobs.data();
+    nrec = e->dict_blobs.size() / sizeof(RafsV6BlobInfo);
+  }
+  dict.resize(nrec);
+  if (nrec) memcpy(dict.data(), rec, nrec * sizeof(RafsV6BlobInfo));
+  BlobWriter bw(o, w, ctx, std::move(dict));
+  int rc = bw.init();
+  if (rc) return fail(e, rc, "pack: %s", ngpu_host_error());
+
+  // device address of every NEW chunk (index order == stream order)
+  std::vector<uint64_t> src;
+  std::vector<uint32_t> len;
+  size_t g = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (res[i].kind != NGPU_NEW) continue;
+    while (g < p->segs.size() && p->segs[g].b <= i) ++g;
+    if (g == p->segs.size()) return fail(e, NGPU_EINVAL, "pack: chunk %llu has no segment",
+                                         (unsigned long long)i);
+    const Seg &sg = p->segs[g];
+    src.push_back((uint64_t)(uintptr_t)(sg.d + (ch[i].offset - sg.base)));
+    len.push_back(ch[i].length);
+  }
+  const uint64_t k = src.size();
+  // windows of <= cap bytes (16-B aligned placement) and <= maxk chunks
+  const uint64_t cap = p->cap, maxk = 1ull << 18;
+  std::vector<uint64_t> wstart{0};
+  std::vector<uint64_t> doff(k);
+  for (uint64_t i = 0, used = 0, cnt = 0; i < k; ++i) {
+    const uint64_t need = (len[i] + 15) & ~15ull;
+    if (cnt && (used + need > cap || cnt == maxk)) {
+      wstart.push_back(i);
+      used = cnt = 0;
+    }
+    doff[i] = used;
+    used += need;
+    ++cnt;
+  }
+  wstart.push_back(k);
+  const uint64_t nw = k ? wstart.size() - 1 : 0;  // no NEW chunk: no window
+  uint8_t *dwin[2] = {}, *ddesc[2] = {}, *hdesc[2] = {};
+  hipEvent_t ev[2] = {};
+  const uint64_t desc_bytes = maxk * (8 + 8 + 4);
+  auto cleanup = [&] {
+    (void)hipStreamSynchronize(e->stream);
+    for (int i = 0; i < 2; ++i) {
+      if (dwin[i]) (void)hipFree(dwin[i]);
+      if (ddesc[i]) (void)hipFree(ddesc[i]);
+      if (hdesc[i]) (void)hipHostFree(hdesc[i]);
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+    }
+  };
+  bool ok = true;
+  for (int i = 0; i < 2 && ok; ++i)
+    ok = hipMalloc((void **)&dwin[i], cap) == hipSuccess &&
+         hipMalloc((void **)&ddesc[i], desc_bytes) == hipSuccess &&
+         hipHostMalloc((void **)&hdesc[i], desc_bytes, hipHostMallocDefault) == hipSuccess &&
+         hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    cleanup();
+    return fail(e, NGPU_ENOMEM, "pack: blob window allocation failed");
+  }
+  auto enqueue = [&](uint64_t wi) -> int {
+    const int b = wi & 1;
+    const uint64_t a = wstart[wi], c = wstart[wi + 1] - a;
+    uint64_t *hs = (uint64_t *)hdesc[b];
+    uint64_t *ho = hs + maxk;
+    uint32_t *hl = (uint32_t *)(ho + maxk);
+    memcpy(hs, &src[a], c * 8);
+    for (uint64_t i = 0; i < c; ++i) ho[i] = doff[a + i];
+    memcpy(hl, &len[a], c * 4);
+    uint64_t *ds = (uint64_t *)ddesc[b];
+    HIP_TRY(e, hipMemcpyAsync(ds, hs, desc_bytes, hipMemcpyHostToDevice, e->stream));
+    const unsigned grid = (unsigned)(c < 2048 ? c : 2048);
+    hipLaunchKernelGGL(gather_chunks, dim3(grid), dim3(256), 0, e->stream, ds, (uint32_t *)(ds + 2 * maxk),
+                       ds + maxk, c, dwin[b]);
+    HIP_TRY(e, hipGetLastError());
+    const uint64_t bytes = doff[a + c - 1] + len[a + c - 1];
+    HIP_TRY(e, hipMemcpyAsync(p->slot[b].h, dwin[b], bytes, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipEventRecord(ev[b], e->stream));
+    return 0;
+  };
+  std::vector<const uint8_t *> hp;
+  if (nw) rc = enqueue(0);
+  for (uint64_t wi = 0; wi < nw && !rc; ++wi) {
+    if (wi + 1 < nw && (rc = enqueue(wi + 1))) break;
+    const int b = wi & 1;
+    if (hipEventSynchronize(ev[b]) != hipSuccess) {
+      rc = fail(e, NGPU_EHIP, "pack: blob window copy failed");
+      break;
+    }
+    const uint64_t a = wstart[wi], c = wstart[wi + 1] - a;
+    hp.resize(c);
+    for (uint64_t i = 0; i < c; ++i) hp[i] = p->slot[b].h + doff[a + i];
+    if ((rc = bw.add(hp.data(), &len[a], c))) rc = fail(e, rc, "pack: %s", ngpu_host_error());
+  }
+  cleanup();
+  if (rc) return rc;
+  if ((rc = bw.finish(ch, res, n, st, info))) return fail(e, rc, "pack: %s", ngpu_host_error());
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
 
-int ngpu_pack_open(ngpu_engine *e, ngpu_pack **out) {
-  if (!e || !out) return NGPU_EINVAL;
+int ngpu_pack_open(ngpu_engine *e, ngpu_pack **out) { return ngpu_pack_open_ex(e, 0, out); }
+
+int ngpu_pack_open_ex(ngpu_engine *e, uint32_t flags, ngpu_pack **out) {
+  if (!e || !out || (flags & ~NGPU_PACK_RETAIN)) return NGPU_EINVAL;
   *out = nullptr;
   std::lock_guard<std::mutex> g(e->mu);
   HIP_TRY(e, hipSetDevice(e->device));
   ngpu_pack *p = new ngpu_pack(e);
+  p->retain = flags & NGPU_PACK_RETAIN;
   uint64_t cap = e->cfg.staging_bytes;
   if (cap < 4ull * e->cfg.chunk_size) cap = 4ull * e->cfg.chunk_size;
   p->cap = cap;
@@ -230,7 +401,7 @@ int ngpu_pack_open(ngpu_engine *e, ngpu_pack **out) {
     ok = ok && hipHostMalloc((void **)&s.h, cap, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc((void **)&s.h_ch, p->max_ch * sizeof(ngpu_chunk), hipHostMallocDefault) ==
              hipSuccess &&
-         hipMalloc((void **)&s.d, cap) == hipSuccess &&
+         (p->retain || hipMalloc((void **)&s.d, cap) == hipSuccess) &&
          hipMalloc((void **)&s.d_ch, p->max_ch * sizeof(ngpu_chunk)) == hipSuccess &&
          hipEventCreateWithFlags(&s.copied, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
@@ -301,7 +472,14 @@ void ngpu_pack_abort(ngpu_pack *p) { release(p); }
 
 int ngpu_pack_close(ngpu_pack *p, ngpu_chunk **chunks_out, ngpu_result **results_out,
                     uint64_t *n_out, ngpu_layer_stats *stats) {
-  if (!p || !chunks_out || !results_out || !n_out) {
+  return ngpu_pack_finish(p, nullptr, nullptr, nullptr, chunks_out, results_out, n_out, stats,
+                          nullptr);
+}
+
+int ngpu_pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx,
+                     ngpu_chunk **chunks_out, ngpu_result **results_out, uint64_t *n_out,
+                     ngpu_layer_stats *stats, ngpu_blob_info *info) {
+  if (!p || !chunks_out || !results_out || !n_out || (w && !opt)) {
     release(p);
     return NGPU_EINVAL;
   }
@@ -310,9 +488,12 @@ int ngpu_pack_close(ngpu_pack *p, ngpu_chunk **chunks_out, ngpu_result **results
   *n_out = 0;
   ngpu_engine *e = p->e;
   int rc = p->err ? p->err : p->sc.finish();
+  if (!rc && w && !p->retain)
+    rc = fail(e, NGPU_EINVAL, "pack: writing the blob stream needs ngpu_pack_open_ex(NGPU_PACK_RETAIN)");
   const uint64_t n = p->chunks.size();
   ngpu_chunk *ch = nullptr;
   ngpu_result *res = nullptr;
+  ngpu_layer_stats st{};
   if (!rc) {
     std::lock_guard<std::mutex> g(e->mu);
     (void)hipSetDevice(e->device);
@@ -334,7 +515,8 @@ int ngpu_pack_close(ngpu_pack *p, ngpu_chunk **chunks_out, ngpu_result **results
         hipMemcpyAsync(res, p->d_res, n * sizeof(ngpu_result), hipMemcpyDeviceToHost,
                        e->stream) != hipSuccess)
       rc = fail(e, NGPU_EHIP, "pack: result copy failed");
-    if (!rc) rc = read_stats(e, e->stream, stats);
+    if (!rc) rc = read_stats(e, e->stream, &st);
+    if (!rc && w) rc = write_stream(p, *opt, w, ctx, ch, res, n, st, info);
   }
   release(p);
   if (rc) {
@@ -342,6 +524,7 @@ int ngpu_pack_close(ngpu_pack *p, ngpu_chunk **chunks_out, ngpu_result **results
     free(res);
     return rc;
   }
+  if (stats) *stats = st;
   *chunks_out = ch;
   *results_out = res;
   *n_out = n;

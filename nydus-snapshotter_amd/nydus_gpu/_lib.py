@@ -19,12 +19,28 @@ KIND_NAMES = {0: "NEW", 1: "INTRA", 2: "DICT"}
 NEW, INTRA, DICT = 0, 1, 2
 
 ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ETAR", -5: "EUNSUPP",
-          -6: "ENODEV", -7: "EIO", -8: "EFORMAT"}
+          -6: "ENODEV", -7: "EIO", -8: "EFORMAT", -9: "ENOTFOUND"}
+ENOTFOUND = -9
+
+# PackOption.Compressor -> TOCEntry flag values (pkg/converter/types.go:22-31);
+# "" is nydus-image's default (zstd).
+COMPRESSORS = {"": 0x2, "none": 0x1, "zstd": 0x2, "lz4_block": 0x4}
+PACK_RETAIN = 0x1
+
+WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+READ_AT_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                              ctypes.c_uint64)
+
+TOC_ENTRY_DTYPE = np.dtype([("flags", "<u4"), ("reserved1", "<u4"), ("name", "S16"),
+                            ("uncompressed_digest", "u1", (32,)), ("compressed_offset", "<u8"),
+                            ("compressed_size", "<u8"), ("uncompressed_size", "<u8"),
+                            ("reserved2", "u1", (48,))])
+assert TOC_ENTRY_DTYPE.itemsize == 128
 
 CHUNK_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u4"), ("file_index", "<u4"),
                         ("file_offset", "<u8")])
 RESULT_DTYPE = np.dtype([("digest", "u1", (32,)), ("kind", "<u4"), ("index", "<u4"),
-                         ("ref", "<u8"), ("blob_index", "<u4"), ("reserved", "<u4"),
+                         ("ref", "<u8"), ("blob_index", "<u4"), ("dict_blob", "<u4"),
                          ("uncompressed_offset", "<u8")])
 assert CHUNK_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 64
 
@@ -37,7 +53,8 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_dict_probe_device", "ngpu_dedup_device", "ngpu_dict_load_device",
            "ngpu_pack_open", "ngpu_pack_write", "ngpu_pack_reserve", "ngpu_pack_commit",
            "ngpu_pack_close", "ngpu_pack_abort", "ngpu_dedup_layers_device",
-           "ngpu_process_layers_device"]
+           "ngpu_process_layers_device", "ngpu_host_error", "ngpu_blob_write",
+           "ngpu_pack_open_ex", "ngpu_pack_finish", "ngpu_unpack_entry", "ngpu_merge"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
@@ -74,6 +91,26 @@ class NgpuLayerStats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class NgpuBlobOptions(ctypes.Structure):
+    _fields_ = [("compressor", ctypes.c_uint32), ("level", ctypes.c_int32),
+                ("threads", ctypes.c_uint32), ("digester", ctypes.c_uint32),
+                ("chunk_size", ctypes.c_uint32), ("n_dict_blobs", ctypes.c_uint32),
+                ("dict_blobs", ctypes.c_void_p)]
+
+
+class NgpuBlobInfo(ctypes.Structure):
+    _fields_ = [("stream_bytes", ctypes.c_uint64), ("blob_bytes", ctypes.c_uint64),
+                ("bootstrap_bytes", ctypes.c_uint64), ("blob_chunks", ctypes.c_uint64),
+                ("compressed_chunks", ctypes.c_uint64), ("stream_digest", ctypes.c_uint8 * 32),
+                ("blob_digest", ctypes.c_uint8 * 32), ("toc_digest", ctypes.c_uint8 * 32)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_[:5]}
+        for k in ("stream_digest", "blob_digest", "toc_digest"):
+            d[k] = bytes(getattr(self, k)).hex()
+        return d
 
 
 class NgpuError(RuntimeError):
@@ -132,6 +169,17 @@ def lib():
                                   ctypes.POINTER(NgpuLayerStats)]
     L.ngpu_pack_abort.argtypes = [vp]
     L.ngpu_pack_abort.restype = None
+    L.ngpu_host_error.restype = ctypes.c_char_p
+    L.ngpu_blob_write.argtypes = [vp, u64, vp, vp, u64, ctypes.POINTER(NgpuLayerStats),
+                                  ctypes.POINTER(NgpuBlobOptions), WRITE_FN, vp,
+                                  ctypes.POINTER(NgpuBlobInfo)]
+    L.ngpu_pack_open_ex.argtypes = [vp, u32, ctypes.POINTER(vp)]
+    L.ngpu_pack_finish.argtypes = [vp, ctypes.POINTER(NgpuBlobOptions), WRITE_FN, vp,
+                                   ctypes.POINTER(vp), ctypes.POINTER(vp), pu64,
+                                   ctypes.POINTER(NgpuLayerStats), ctypes.POINTER(NgpuBlobInfo)]
+    L.ngpu_unpack_entry.argtypes = [READ_AT_FN, vp, u64, ctypes.c_char_p, WRITE_FN, vp, vp]
+    L.ngpu_merge.argtypes = [ctypes.POINTER(vp), pu64, ctypes.POINTER(ctypes.c_char_p), u64, vp,
+                             u64, WRITE_FN, vp, ctypes.POINTER(vp)]
     _lib = L
     return L
 
@@ -176,6 +224,114 @@ def chunk_table(chunks, results) -> np.ndarray:
     if rc:
         raise NgpuError(rc, "chunk table")
     return out
+
+
+def _host_check(rc, what):
+    if rc:
+        msg = lib().ngpu_host_error()
+        raise NgpuError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+
+class _Sink:
+    """io.Writer -> ngpu_write_fn (exceptions are kept and re-raised)."""
+
+    def __init__(self, dest):
+        self.dest, self.exc = dest, None
+
+        def fn(_ctx, buf, n):
+            try:
+                self.dest.write(ctypes.string_at(buf, n))
+                return 0
+            except BaseException as e:  # noqa: BLE001 - re-raised by the caller
+                self.exc = e
+                return 1
+        self.fn = WRITE_FN(fn)
+
+    def reraise(self):
+        if self.exc is not None:
+            raise self.exc
+
+
+def blob_options(compressor: str = "", level: int = 0, threads: int = 0, digester: str = "blake3",
+                 chunk_size: int = 0x100000, dict_blobs: np.ndarray = None):
+    if compressor not in COMPRESSORS:
+        raise ValueError(f"unsupported compressor {compressor!r}")
+    o = NgpuBlobOptions(compressor=COMPRESSORS[compressor], level=level, threads=threads,
+                        digester=DIGESTERS[digester], chunk_size=chunk_size)
+    keep = None
+    if dict_blobs is not None and len(dict_blobs):
+        keep = np.ascontiguousarray(dict_blobs).view(np.uint8).reshape(-1)
+        o.n_dict_blobs = keep.size // 256
+        o.dict_blobs = keep.ctypes.data
+    return o, keep
+
+
+def blob_write(data, chunks, results, stats: dict, dest, compressor: str = "", level: int = 0,
+               threads: int = 0, digester: str = "blake3", chunk_size: int = 0x100000,
+               dict_blobs: np.ndarray = None) -> dict:
+    """Host: write the nydus blob stream of a packed layer to `dest` (a
+    writable file-like); returns the ngpu_blob_info as a dict."""
+    L = lib()
+    buf = _buf(data)
+    ch = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+    rs = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
+    st = NgpuLayerStats(**{k: stats[k] for k, _ in NgpuLayerStats._fields_})
+    o, keep = blob_options(compressor, level, threads, digester, chunk_size, dict_blobs)
+    sink = _Sink(dest)
+    info = NgpuBlobInfo()
+    rc = L.ngpu_blob_write(_ptr(buf), buf.size, _ptr(ch), _ptr(rs), len(ch), ctypes.byref(st),
+                           ctypes.byref(o), sink.fn, None, ctypes.byref(info))
+    sink.reraise()
+    _host_check(rc, "blob_write")
+    del keep
+    return info.as_dict()
+
+
+def unpack_entry(blob, name: str):
+    """UnpackEntry (convert_unix.go:284-320) over bytes / a numpy buffer:
+    returns (entry data, TOC entry record or None when found by tar header).
+    Raises NgpuError(ENOTFOUND) like ErrNotFound."""
+    L = lib()
+    src = _buf(blob)
+
+    def ra(_ctx, buf, n, off):
+        n = min(n, src.size - off)
+        if n <= 0:
+            return -1
+        ctypes.memmove(buf, src.ctypes.data + off, n)
+        return n
+    rfn = READ_AT_FN(ra)
+    out = []
+    sink = _Sink(type("W", (), {"write": lambda _s, b: out.append(b)})())
+    toc = np.zeros(1, TOC_ENTRY_DTYPE)
+    rc = L.ngpu_unpack_entry(rfn, None, src.size, name.encode(), sink.fn, None, _ptr(toc))
+    sink.reraise()
+    _host_check(rc, f"unpack_entry {name}")
+    return b"".join(out), (toc[0] if toc[0]["name"] else None)
+
+
+def merge(bootstraps, layer_digests, dict_bootstrap: bytes = None):
+    """ngpu_merge: per-layer bootstraps (bytes) + layer digest hex strings ->
+    (merged bootstrap bytes, [blob ids in first-appearance order])."""
+    L = lib()
+    bufs = [_buf(b) for b in bootstraps]
+    n = len(bufs)
+    ptrs = (ctypes.c_void_p * max(1, n))(*[b.ctypes.data for b in bufs])
+    sizes = (ctypes.c_uint64 * max(1, n))(*[b.size for b in bufs])
+    digs = (ctypes.c_char_p * max(1, n))(*[(d or "").encode() for d in layer_digests])
+    dbuf = _buf(dict_bootstrap) if dict_bootstrap is not None else None
+    out = []
+    sink = _Sink(type("W", (), {"write": lambda _s, b: out.append(b)})())
+    ids = ctypes.c_void_p()
+    rc = L.ngpu_merge(ptrs, sizes, digs, n, _ptr(dbuf) if dbuf is not None else None,
+                      dbuf.size if dbuf is not None else 0, sink.fn, None, ctypes.byref(ids))
+    sink.reraise()
+    _host_check(rc, "merge")
+    try:
+        s = ctypes.string_at(ids).decode()
+    finally:
+        L.ngpu_free_host(ids)
+    return b"".join(out), (s.split(",") if s else [])
 
 
 class Engine:
@@ -308,9 +464,10 @@ class Engine:
         self._check(lib().ngpu_last_timing(self._h, ctypes.byref(t)), "last_timing")
         return t.as_dict()
 
-    def pack(self) -> "PackWriter":
-        """Streaming Pack (converter.Pack mirror): returns a writer."""
-        return PackWriter(self)
+    def pack(self, retain: bool = False) -> "PackWriter":
+        """Streaming Pack (converter.Pack mirror): returns a writer.  retain=True
+        keeps the layer in HBM so finish() can write the nydus blob stream."""
+        return PackWriter(self, retain)
 
     def pack_tar(self, tar):
         """Whole tar layer -> (chunks, results, stats)."""
@@ -340,10 +497,11 @@ class PackWriter:
     any split, close() -> (chunks, results, stats).  Errors raise NgpuError;
     a failed writer is released (like Close() reporting the builder error)."""
 
-    def __init__(self, engine: Engine):
+    def __init__(self, engine: Engine, retain: bool = False):
         self._eng = engine
         h = ctypes.c_void_p()
-        engine._check(lib().ngpu_pack_open(engine._h, ctypes.byref(h)), "pack_open")
+        engine._check(lib().ngpu_pack_open_ex(engine._h, PACK_RETAIN if retain else 0,
+                                              ctypes.byref(h)), "pack_open")
         self._p = h
 
     def write(self, data) -> int:
@@ -380,13 +538,35 @@ class PackWriter:
             self._p = None
 
     def close(self):
+        ch, rs, st, _ = self._finish(None)
+        return ch, rs, st
+
+    def finish(self, dest, compressor: str = "", level: int = 0, threads: int = 0,
+               dict_blobs: np.ndarray = None):
+        """close() + write the nydus blob stream to `dest` (needs retain=True).
+        Returns (chunks, results, stats, blob info dict)."""
+        return self._finish(dest, compressor, level, threads, dict_blobs)
+
+    def _finish(self, dest, compressor="", level=0, threads=0, dict_blobs=None):
         L = lib()
         pc, pr = ctypes.c_void_p(), ctypes.c_void_p()
         n = ctypes.c_uint64(0)
         st = NgpuLayerStats()
+        info = NgpuBlobInfo()
         p, self._p = self._p, None
-        self._eng._check(L.ngpu_pack_close(p, ctypes.byref(pc), ctypes.byref(pr), ctypes.byref(n),
-                                           ctypes.byref(st)), "pack_close")
+        if dest is None:
+            rc = L.ngpu_pack_finish(p, None, WRITE_FN(), None, ctypes.byref(pc), ctypes.byref(pr),
+                                    ctypes.byref(n), ctypes.byref(st), None)
+            sink = None
+        else:
+            o, keep = blob_options(compressor, level, threads, self._eng.digester,
+                                   self._eng.chunk_size, dict_blobs)
+            sink = _Sink(dest)
+            rc = L.ngpu_pack_finish(p, ctypes.byref(o), sink.fn, None, ctypes.byref(pc),
+                                    ctypes.byref(pr), ctypes.byref(n), ctypes.byref(st),
+                                    ctypes.byref(info))
+            sink.reraise()
+        self._eng._check(rc, "pack_finish")
         try:
             nn = n.value
             ch = np.empty(nn, dtype=CHUNK_DTYPE)
@@ -397,4 +577,4 @@ class PackWriter:
         finally:
             L.ngpu_free_host(pc)
             L.ngpu_free_host(pr)
-        return ch, rs, st.as_dict()
+        return ch, rs, st.as_dict(), (info.as_dict() if dest is not None else None)

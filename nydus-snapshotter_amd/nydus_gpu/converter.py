@@ -1,41 +1,63 @@
 """Host-side mirror of the reference's converter API for the digest/dedup path.
 
 Mirrors pkg/converter (Go) names, argument meaning and error behaviour for the
-part this engine replaces:
+part this engine replaces; the work itself happens in libnydusgpu.so (GPU
+digest/dedup, host C++ blob writer, reader and merge):
 
-* ``PackOption`` / ``MergeOption`` — pkg/converter/types.go:58-133 (fields the
-  path consumes; ``Digester`` is the API extension);
+* ``PackOption`` / ``MergeOption`` / ``Layer`` — pkg/converter/types.go:37-133
+  (fields the path consumes; ``Digester`` is the API extension);
 * ``Pack(dest, opt)`` — convert_unix.go:325: returns a write-closer; the caller
   streams the uncompressed layer tar into it; ``close()`` must be checked (it
   raises the builder error, convert_unix.go:323-324).  The GPU engine does the
-  chunking/digest/dedup (libnydusgpu.so ``ngpu_pack_*``); ``close()`` writes a
-  RAFS v6 bootstrap with the layer's blob table and chunk table to ``dest``;
-* ``Merge(layers, dest, opt)`` — convert_unix.go:560 + tool.Merge
-  (builder.go:220-294): blob bookkeeping only (merge does not
-  re-hash).  Returns the referenced blob digests in first-appearance order,
-  e.g. ``[dict, upper]`` for TestPack (tests/converter_test.go:513-519).
-
-Out of scope here: compression and the blob data /
-TOC stream.  The layer's own blob ID is therefore derived from its content
-identity — SHA-256 over the NEW chunks' digests in index order — instead of
-the SHA-256 of the compressed blob nydus-image would write.
+  chunking/digest/dedup (``ngpu_pack_*``) with the layer kept in HBM;
+  ``close()`` writes the nydus formatted stream `data | tar_header | ... |
+  toc | tar_header` to ``dest`` (``ngpu_pack_finish``: NEW chunks gathered on
+  the GPU, compressed on the host per ``Compressor``, image.boot, TOC);
+* ``UnpackEntry(ra, name, target)`` — convert_unix.go:284-320 (TOC first,
+  tar-header walk as fallback);
+* ``Merge(layers, dest, opt)`` — convert_unix.go:560-666 + tool.Merge
+  (builder.go:220-294): unpacks each layer's image.boot, merges the blob and
+  chunk tables (no re-hashing) and returns the referenced blob
+  digests in first-appearance order; a layer's own blob is named after
+  ``Layer.Digest`` (the sha256 of its whole Pack output), so TestPack's
+  ``[dict blob, upper blob]`` (tests/converter_test.go:513-519) holds exactly.
 """
 from __future__ import annotations
 
-import hashlib
 from dataclasses import dataclass, field
 from typing import BinaryIO, List, Optional, Sequence
 
 import numpy as np
 
-from . import rafs
-from ._lib import DICT, NEW, Engine, NgpuError, chunk_table
+import io
+import tarfile
+
+from ._lib import COMPRESSORS, DICT, ENOTFOUND, NEW, Engine, NgpuError, merge, unpack_entry
+
+EntryBlob = "image.blob"            # convert_unix.go:45
+EntryBootstrap = "image.boot"       # :46
+EntryBlobMeta = "blob.meta"         # :47
+EntryBlobMetaHeader = "blob.meta.header"  # :48
+EntryTOC = "rafs.blob.toc"          # :49
 
 _ENGINES = {}
 
 
 class ConverterError(RuntimeError):
     pass
+
+
+class ErrNotFound(ConverterError):
+    """types.go:33-35."""
+
+
+@dataclass
+class Layer:
+    """types.go:37-44: Digest of the whole nydus tar blob ("sha256:<hex>") and
+    its bytes (ReaderAt)."""
+    Digest: str
+    ReaderAt: bytes
+    OriginalDigest: Optional[str] = None
 
 
 @dataclass
@@ -93,54 +115,26 @@ def _engine(opt: PackOption) -> Engine:
     return _ENGINES[key]
 
 
-def _own_blob_id(chunks: np.ndarray, results: np.ndarray) -> str:
-    new = results[results["kind"] == NEW]
-    return hashlib.sha256(new["digest"].tobytes()).hexdigest()
-
-
 class _PackWriteCloser:
     def __init__(self, dest: BinaryIO, opt: PackOption):
         self._dest, self._opt = dest, opt
+        if (opt.Compressor or "") not in COMPRESSORS:
+            raise ConverterError(f"unsupported compressor {opt.Compressor!r}")
         self._eng = _engine(opt)
-        self._dict_ids: List[str] = []
-        self._dict_blob: Optional[np.ndarray] = None
         if opt.ChunkDictPath:
-            with open(opt.ChunkDictPath, "rb") as f:
-                boot = rafs.read_v6(f.read())
-            self._dict_ids = boot["blob_ids"]
-            self._dict_blob = boot["chunks"]["blob_index"].astype(np.int64)
             self._eng.dict_load_bootstrap(opt.ChunkDictPath)
         else:
             self._eng.dict_clear()
-        self._w = self._eng.pack()
+        self._w = self._eng.pack(retain=True)
         self.result = None
 
     def write(self, data) -> int:
         return self._w.write(data)
 
     def close(self):
-        ch, res, st = self._w.close()
-        # blob table in real-index order (first-hit allocation, VERIFY semantics)
-        nblobs = int(st["blobs"])
-        ids: List[Optional[str]] = [None] * nblobs
-        own = st["own_blob_index"]
-        own_id = _own_blob_id(ch, res) if own != 0xFFFFFFFF else None
-        if own != 0xFFFFFFFF:
-            ids[own] = own_id
-        d = res[res["kind"] == DICT]
-        for r in d:
-            inner = int(self._dict_blob[int(r["ref"])])
-            ids[int(r["blob_index"])] = self._dict_ids[inner] if inner < len(self._dict_ids) else \
-                f"{inner:064x}"
-        if any(i is None for i in ids):
-            raise ConverterError("inconsistent blob table")
-        cs = parse_chunk_size(self._opt.ChunkSize)
-        counts = [int((res["kind"] == NEW).sum()) if i == own else 0 for i in range(nblobs)]
-        blobs = rafs.make_blob_table(ids, cs, counts, self._opt.Digester or "blake3")
-        recs = chunk_table(ch, res).view(rafs.CHUNK_INFO_DTYPE).reshape(-1)
-        flags = 0x4 if (self._opt.Digester or "blake3") == "blake3" else 0x0
-        self._dest.write(rafs.write_v6_bootstrap(recs, cs, flags=flags, blobs=blobs))
-        self.result = {"chunks": ch, "results": res, "stats": st, "blob_ids": ids, "own_blob_id": own_id}
+        ch, res, st, info = self._w.finish(self._dest, compressor=self._opt.Compressor or "")
+        self.result = {"chunks": ch, "results": res, "stats": st, "info": info,
+                       "digest": "sha256:" + info["stream_digest"]}
         return self.result
 
 
@@ -152,30 +146,50 @@ def Pack(dest: BinaryIO, opt: PackOption) -> _PackWriteCloser:
     return _PackWriteCloser(dest, opt)
 
 
-def Merge(layers: Sequence[bytes], dest: BinaryIO, opt: MergeOption) -> List[str]:
-    """convert_unix.go:560 — merge per-layer bootstraps; returns the referenced
-    blob digests (sha256:<id>) in first-appearance order.  Each layer may hold
-    dict blobs plus at most one blob of its own ([nydus v2.3.0] merge.rs)."""
-    blob_ids: List[str] = []
-    chunks = []
-    cs = 0
-    for boot_bytes in layers:
-        boot = rafs.read_v6(boot_bytes)
-        cs = cs or boot["chunk_size"]
-        local = []
-        for bid in boot["blob_ids"]:
-            if bid not in blob_ids:
-                blob_ids.append(bid)
-            local.append(blob_ids.index(bid))
-        recs = boot["chunks"].copy()
-        if len(recs):
-            recs["blob_index"] = np.asarray(local, np.uint32)[recs["blob_index"]]
-        chunks.append(recs)
-    allrecs = np.concatenate(chunks) if chunks else np.zeros(0, rafs.CHUNK_INFO_DTYPE)
-    counts = [int((allrecs["blob_index"] == i).sum()) for i in range(len(blob_ids))]
-    dest.write(rafs.write_v6_bootstrap(allrecs, cs or 0x100000,
-                                       blobs=rafs.make_blob_table(blob_ids, cs or 0x100000, counts)))
-    return ["sha256:" + b for b in blob_ids]
+def UnpackEntry(ra: bytes, targetName: str, target: BinaryIO):
+    """convert_unix.go:284-293: copy entry data to target; returns the TOC
+    entry (None when found by tar header).  Raises ErrNotFound."""
+    try:
+        data, toc = unpack_entry(ra, targetName)
+    except NgpuError as e:
+        if e.code == ENOTFOUND:
+            raise ErrNotFound(str(e)) from e
+        raise
+    target.write(data)
+    return toc
 
 
-__all__ = ["PackOption", "MergeOption", "Pack", "Merge", "ConverterError", "NgpuError", "parse_chunk_size"]
+def Merge(layers: Sequence[Layer], dest: BinaryIO, opt: MergeOption) -> List[str]:
+    """convert_unix.go:560-666 — merge per-layer bootstraps; returns the
+    referenced blob digests (sha256:<id>) in first-appearance order."""
+    boots, digests = [], []
+    for layer in layers:
+        b = io.BytesIO()
+        try:
+            UnpackEntry(layer.ReaderAt, EntryBootstrap, b)
+        except ConverterError as e:
+            raise ConverterError(f"unpack all bootstraps: unpack nydus tar: {e}") from e
+        boots.append(b.getvalue())
+        digests.append(layer.Digest.split(":", 1)[-1])
+    dict_boot = None
+    if opt.ChunkDictPath:
+        with open(opt.ChunkDictPath, "rb") as f:
+            dict_boot = f.read()
+    merged, ids = merge(boots, digests, dict_boot)
+    if opt.WithTar:  # packToTar (utils.go:92-160): image/ + image/image.boot
+        out = io.BytesIO()
+        with tarfile.open(fileobj=out, mode="w", format=tarfile.PAX_FORMAT) as tw:
+            d = tarfile.TarInfo("image")
+            d.type, d.mode = tarfile.DIRTYPE, 0o755
+            tw.addfile(d)
+            h = tarfile.TarInfo("image/" + EntryBootstrap)
+            h.mode, h.size = 0o444, len(merged)
+            tw.addfile(h, io.BytesIO(merged))
+        dest.write(out.getvalue())
+    else:
+        dest.write(merged)
+    return ["sha256:" + i for i in ids]
+
+
+__all__ = ["PackOption", "MergeOption", "Layer", "Pack", "Merge", "UnpackEntry", "ConverterError",
+           "ErrNotFound", "NgpuError", "parse_chunk_size", "EntryBlob", "EntryBootstrap", "EntryTOC"]

@@ -1,0 +1,280 @@
+"""Blob stream (converter.Pack output):
+the product's host writer / reader / merge (libnydusgpu.so) checked against
+the reference reader restated in oracle/blob_ref.py, on CPU.
+
+Decisions here come from the CPU oracle (tar walk, digests, dedup), so these
+tests need no GPU; tests/test_gpu_parity.py checks that the GPU Pack path
+writes the very same stream.  Pinning: the reader is the reference's Go code
+restated (convert_unix.go:162-320); the chunk-record rules are pinned on the
+reference v6 fixture below; compressed chunk BYTES are not pinned against
+nydus-image (unavailable; they depend on the compressor library version) —
+they are pinned by round trip (decompress == chunk bytes, digest == block_id).
+"""
+import hashlib
+import io
+import os
+
+import numpy as np
+import pytest
+
+import blob_ref
+import nydus_gpu
+from nydus_gpu import converter as cv
+from nydus_gpu import rafs
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+COMPRESSOR_FLAG = {"none": 0x1, "zstd": 0x2, "lz4_block": 0x4}
+
+
+def test_fixture_obeys_record_rules():
+    """The rules check_record_rules encodes hold on the reference fixture."""
+    b = rafs.read_v6_from_targz(os.path.join(GOLDEN, "v6-bootstrap-chunk-pos-438272.tar.gz"))
+    blob = b["blobs"][0]
+    assert blob_ref.check_record_rules(b["chunks"], blob["compressed_size"], blob["uncompressed_size"])
+    assert blob["compression_algo"] == 1 and b["flags"] == 0x6  # lz4_block, blake3
+    assert blob["chunk_count"] == len(b["chunks"])
+
+
+def cpu_results(oracle, tar, chunk, digester="blake3", dict_boot=None):
+    """ngpu_result/stats from the CPU oracle (decisions the GPU must match)."""
+    ch = oracle.tar_chunks(tar, chunk)
+    dig = oracle.digest_chunks(tar, ch, digester)
+    kw = {}
+    if dict_boot is not None:
+        d = rafs.read_v6(dict_boot)["chunks"]
+        kw = dict(dict_digests=d["block_id"], dict_sizes=d["uncompressed_size"],
+                  dict_blob=d["blob_index"], dict_index=d["index"])
+    dec, own = oracle.dedup(dig, ch["length"], **kw)
+    res = np.zeros(len(ch), nydus_gpu.RESULT_DTYPE)
+    res["digest"] = dig
+    for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+        res[f] = dec[f]
+    if dict_boot is not None:
+        dmask = dec["kind"] == nydus_gpu.DICT
+        res["dict_blob"][dmask] = kw["dict_blob"][dec["ref"][dmask].astype(np.int64)]
+    new = dec["kind"] == nydus_gpu.NEW
+    ends = dec["uncompressed_offset"][new].astype(np.int64) + ch["length"][new]
+    st = {"chunks": len(ch), "new_chunks": int(new.sum()),
+          "intra_chunks": int((dec["kind"] == nydus_gpu.INTRA).sum()),
+          "dict_chunks": int((dec["kind"] == nydus_gpu.DICT).sum()),
+          "new_bytes": int(ch["length"][new].sum()),
+          "own_blob_index": 0xFFFFFFFF if own is None else own,
+          "blobs": len(np.unique(dec["blob_index"])) if len(dec) else 0,
+          "uncompressed_size": int((ends.max() + 4095) // 4096 * 4096) if new.any() else 0}
+    return ch, res, st
+
+
+def cpu_stream(oracle, tar, chunk, compressor, digester="blake3", dict_boot=None):
+    ch, res, st = cpu_results(oracle, tar, chunk, digester, dict_boot)
+    dict_blobs = rafs.read_v6(dict_boot)["blobs"] if dict_boot is not None else None
+    out = io.BytesIO()
+    info = nydus_gpu.blob_write(tar, ch, res, st, out, compressor=compressor, digester=digester,
+                                chunk_size=chunk, dict_blobs=dict_blobs)
+    return out.getvalue(), info, ch, res, st
+
+
+def check_stream(oracle, stream, info, tar, ch, res, compressor, digester="blake3"):
+    """Everything the reference reader and the fixture rules say about a Pack
+    output, plus round trip of every chunk record."""
+    assert info["stream_bytes"] == len(stream)
+    assert info["stream_digest"] == hashlib.sha256(stream).hexdigest()       # a9
+    assert info["toc_digest"] == blob_ref.calc_blob_toc_digest(stream)
+    boot, e_boot = blob_ref.unpack_entry(stream, blob_ref.ENTRY_BOOTSTRAP)
+    blob, e_blob = blob_ref.unpack_entry(stream, blob_ref.ENTRY_BLOB)
+    assert e_boot is not None and e_blob is not None                          # found via the TOC
+    assert e_boot["uncompressed_digest"] == hashlib.sha256(boot).hexdigest()
+    assert e_blob["uncompressed_digest"] == hashlib.sha256(blob).hexdigest() == info["blob_digest"]
+    # the tar-header fallback finds the same bytes
+    o, n = blob_ref.seek_file_by_tar_header(stream, blob_ref.ENTRY_BOOTSTRAP)
+    assert stream[o:o + n] == boot
+    # product reader == restated reader
+    for name in (blob_ref.ENTRY_BOOTSTRAP, blob_ref.ENTRY_BLOB):
+        data, toc = nydus_gpu.unpack_entry(stream, name)
+        assert data == blob_ref.unpack_entry(stream, name)[0]
+        assert toc is not None and toc["name"].decode() == name
+    b = rafs.read_v6(boot)
+    assert b["flags"] & (0x8 if digester == "sha256" else 0x4)
+    recs = b["chunks"]
+    new = np.nonzero(res["kind"] == nydus_gpu.NEW)[0]
+    assert len(recs) == len(new) == info["blob_chunks"]
+    own = [i for i, bb in enumerate(b["blobs"]) if bb["blob_id"].decode() == info["blob_digest"]]
+    if len(new):
+        assert len(own) == 1
+        ob = b["blobs"][own[0]]
+        assert blob_ref.check_record_rules(recs, ob["compressed_size"], ob["uncompressed_size"])
+        assert ob["compressed_size"] == len(blob) == info["blob_bytes"]
+        assert ob["chunk_count"] == len(new)
+    flag = COMPRESSOR_FLAG[compressor or "zstd"]
+    buf = np.frombuffer(tar, np.uint8) if not isinstance(tar, np.ndarray) else tar
+    for r, i in zip(recs[np.argsort(recs["index"])], new):
+        assert bytes(r["block_id"]) == bytes(res["digest"][i])
+        assert r["index"] == res["index"][i] and r["uncompressed_offset"] == res["uncompressed_offset"][i]
+        assert r["file_offset"] == ch["file_offset"][i] and r["uncompressed_size"] == ch["length"][i]
+        body = blob_ref.chunk_bytes(blob, r, flag)
+        src = buf[ch["offset"][i]:ch["offset"][i] + ch["length"][i]].tobytes()
+        assert body == src
+        assert oracle.digest(body, digester) == bytes(r["block_id"])
+    assert int((recs["flags"] & 1).sum()) == info["compressed_chunks"]
+    return b
+
+
+@pytest.mark.parametrize("compressor", ["none", "zstd", "lz4_block", ""])
+def test_blob_stream_roundtrip(oracle, tars, compressor):
+    tar = tars["oci_upper"]
+    stream, info, ch, res, st = cpu_stream(oracle, tar, 0x100000, compressor)
+    b = check_stream(oracle, stream, info, tar, ch, res, compressor)
+    if compressor == "none":
+        assert info["compressed_chunks"] == 0
+        assert b["blobs"][0]["compression_algo"] == 0
+    else:
+        # hugeString: the zero halves compress, the random halves are stored raw
+        assert 0 < info["compressed_chunks"] < len(b["chunks"])
+        assert b["blobs"][0]["compression_algo"] == {"zstd": 3, "": 3, "lz4_block": 1}[compressor]
+
+
+@pytest.mark.parametrize("name,chunk,digester", [("edge_pax", 0x10000, "blake3"),
+                                                  ("edge_gnu", 0x10000, "sha256"),
+                                                  ("alpine_like", 0x100000, "blake3")])
+def test_blob_stream_edge_layers(oracle, tars, name, chunk, digester):
+    tar = tars[name]
+    stream, info, ch, res, st = cpu_stream(oracle, tar, chunk, "zstd", digester)
+    check_stream(oracle, stream, info, tar, ch, res, "zstd", digester)
+
+
+def test_blob_stream_empty_layer(oracle):
+    import layers
+    tar = layers.empty_tar() if hasattr(layers, "empty_tar") else b"\0" * 1024
+    stream, info, ch, res, st = cpu_stream(oracle, tar, 0x100000, "zstd")
+    assert len(ch) == 0 and info["blob_bytes"] == 0 and info["blob_chunks"] == 0
+    boot, _ = blob_ref.unpack_entry(stream, blob_ref.ENTRY_BOOTSTRAP)
+    assert len(rafs.read_v6(boot)["chunks"]) == 0
+
+
+def test_blob_stream_deterministic(oracle, tars):
+    """Same inputs -> identical bytes regardless of compression thread count."""
+    tar = tars["oci_upper"]
+    ch, res, st = cpu_results(oracle, tar, 0x10000)
+    outs = []
+    for t in (1, 3, 16):
+        o = io.BytesIO()
+        nydus_gpu.blob_write(tar, ch, res, st, o, compressor="zstd", threads=t, chunk_size=0x10000)
+        outs.append(o.getvalue())
+    assert outs[0] == outs[1] == outs[2]
+
+
+def test_unpack_entry_not_found_and_corrupt(oracle, tars):
+    stream, *_ = cpu_stream(oracle, tars["oci_lower"], 0x100000, "zstd")
+    with pytest.raises(nydus_gpu.NgpuError) as e:
+        nydus_gpu.unpack_entry(stream, "blob.meta")
+    assert e.value.code == nydus_gpu.ENOTFOUND
+    with pytest.raises(blob_ref.NotFound):
+        blob_ref.unpack_entry(stream, "blob.meta")
+    bad = bytearray(stream)
+    bad[-512 + 148] ^= 0x1  # checksum of the last header
+    with pytest.raises(nydus_gpu.NgpuError):
+        nydus_gpu.unpack_entry(bytes(bad), blob_ref.ENTRY_BOOTSTRAP)
+    with pytest.raises(ValueError):
+        blob_ref.unpack_entry(bytes(bad), blob_ref.ENTRY_BOOTSTRAP)
+    with pytest.raises(nydus_gpu.NgpuError):
+        nydus_gpu.unpack_entry(b"\0" * 100, blob_ref.ENTRY_BOOTSTRAP)
+
+
+def test_unpack_entry_legacy_tar_header_format():
+    """A blob without TOC (old rafs format): found by the tar-header walk."""
+    import tarfile
+    boot = b"B" * 5000
+    blob = b"D" * 777
+    s = io.BytesIO()
+    for name, data in (("image.blob", blob), ("image.boot", boot)):
+        s.write(data)
+        ti = tarfile.TarInfo(name)
+        ti.size = len(data)
+        s.write(ti.tobuf(format=tarfile.USTAR_FORMAT))
+    stream = s.getvalue()
+    data, toc = nydus_gpu.unpack_entry(stream, "image.boot")
+    assert data == boot and toc is None
+    assert blob_ref.unpack_entry(stream, "image.boot") == (boot, None)
+    assert nydus_gpu.unpack_entry(stream, "image.blob")[0] == blob
+
+
+def test_testpack_flow_cpu_decisions(oracle, tars, tmp_path):
+    """tests/converter_test.go:420-528 with oracle decisions and the product's
+    blob writer + Merge: buildChunkDict's Merge returns [sha256(dict Pack
+    output)] (:446-448); lower is all DICT (no own blob); Merge(lower, upper)
+    returns [dict blob, sha256(upper Pack output)] (:513-519)."""
+    dstream, dinfo, *_ = cpu_stream(oracle, tars["chunk_dict"], 0x100000, "zstd")
+    ddig = "sha256:" + hashlib.sha256(dstream).hexdigest()
+    merged = io.BytesIO()
+    blobs = cv.Merge([cv.Layer(ddig, dstream)], merged, cv.MergeOption())
+    assert blobs == [ddig]
+    dict_boot = merged.getvalue()
+    assert rafs.read_v6(dict_boot)["blob_ids"] == [ddig[7:]]
+    dict_path = str(tmp_path / "dict-bootstrap")
+    with open(dict_path, "wb") as f:
+        f.write(dict_boot)
+
+    lstream, linfo, lch, lres, lst = cpu_stream(oracle, tars["oci_lower"], 0x100000, "zstd",
+                                                dict_boot=dict_boot)
+    ustream, uinfo, uch, ures, ust = cpu_stream(oracle, tars["oci_upper"], 0x100000, "zstd",
+                                                dict_boot=dict_boot)
+    assert (lres["kind"] == nydus_gpu.DICT).all() and lst["own_blob_index"] == 0xFFFFFFFF
+    assert linfo["blob_bytes"] == 0
+    check_stream(oracle, ustream, uinfo, tars["oci_upper"], uch, ures, "zstd")
+    ldig = "sha256:" + hashlib.sha256(lstream).hexdigest()
+    udig = "sha256:" + hashlib.sha256(ustream).hexdigest()
+    out = io.BytesIO()
+    blobs = cv.Merge([cv.Layer(ldig, lstream), cv.Layer(udig, ustream)], out,
+                     cv.MergeOption(ChunkDictPath=dict_path))
+    assert blobs == [ddig, udig]
+    m = rafs.read_v6(out.getvalue())
+    assert m["blob_ids"] == [ddig[7:], udig[7:]]
+    # every merged chunk record points at the blob that holds its data
+    nu = int((ures["kind"] == nydus_gpu.NEW).sum())
+    assert (m["chunks"]["blob_index"][-nu:] == 1).all()
+    # WithTar: image/ + image/image.boot (utils.go:92-160)
+    out2 = io.BytesIO()
+    cv.Merge([cv.Layer(ldig, lstream), cv.Layer(udig, ustream)], out2,
+             cv.MergeOption(ChunkDictPath=dict_path, WithTar=True))
+    import tarfile
+    with tarfile.open(fileobj=io.BytesIO(out2.getvalue())) as tf:
+        assert tf.getnames() == ["image", "image/image.boot"]
+        assert tf.extractfile("image/image.boot").read() == out.getvalue()
+
+
+def test_merge_errors():
+    import struct
+    with pytest.raises(nydus_gpu.NgpuError):
+        nydus_gpu.merge([b"not a bootstrap" * 100], ["aa" * 32])
+    # two non-dict blobs in one layer
+    recs = np.zeros(2, rafs.CHUNK_INFO_DTYPE)
+    recs["blob_index"] = [0, 1]
+    boot = rafs.write_v6_bootstrap(recs, 0x100000, blobs=rafs.make_blob_table(["aa" * 32, "bb" * 32], 0x100000))
+    with pytest.raises(nydus_gpu.NgpuError):
+        nydus_gpu.merge([boot], ["cc" * 32])
+    # ...fine when one of them is the dict's
+    dboot = rafs.write_v6_bootstrap(np.zeros(0, rafs.CHUNK_INFO_DTYPE), 0x100000,
+                                    blobs=rafs.make_blob_table(["aa" * 32], 0x100000))
+    merged, ids = nydus_gpu.merge([boot], ["cc" * 32], dboot)
+    assert ids == ["aa" * 32, "cc" * 32]
+    assert struct.unpack_from("<I", merged, 1024)[0] == rafs.RAFS_V6_MAGIC
+
+
+def test_blob_write_rejects_bad_input(oracle, tars):
+    tar = tars["oci_lower"]
+    ch, res, st = cpu_results(oracle, tar, 0x100000)
+    with pytest.raises(ValueError):
+        nydus_gpu.blob_write(tar, ch, res, st, io.BytesIO(), compressor="gzip")
+    bad = res.copy()
+    bad["index"][bad["kind"] == nydus_gpu.NEW] += 1
+    with pytest.raises(nydus_gpu.NgpuError):
+        nydus_gpu.blob_write(tar, ch, bad, st, io.BytesIO(), compressor="none")
+    ch2 = ch.copy()
+    ch2["offset"][0] = len(tar)
+    with pytest.raises(nydus_gpu.NgpuError):
+        nydus_gpu.blob_write(tar, ch2, res, st, io.BytesIO(), compressor="none")
+
+    class Broken:
+        def write(self, b):
+            raise OSError("disk full")
+    with pytest.raises(OSError):
+        nydus_gpu.blob_write(tar, ch, res, st, Broken(), compressor="none")

@@ -571,12 +571,16 @@ def test_multi_layer_dedup_matches_per_layer(oracle):
         assert stats[l]["own_blob_index"] == (0xFFFFFFFF if own is None else own)
 
 
-def test_converter_testpack_flow(tars, tmp_path):
-    """tests/converter_test.go:420-528 through the converter mirror:
-    buildChunkDict (Pack + Merge), Pack lower/upper against the dict bootstrap,
-    Merge -> blob list [dict blob, upper blob]."""
+def test_converter_testpack_flow(tars, oracle, tmp_path):
+    """tests/converter_test.go:420-528 through the converter mirror on the GPU:
+    buildChunkDict (Pack + Merge -> [sha256(dict Pack output)], :446-448),
+    Pack lower/upper against the dict bootstrap, Merge -> [dict blob,
+    sha256(upper Pack output)] (:513-519).  Every Pack output is byte-equal to
+    the host writer fed with the CPU oracle's decisions."""
+    import hashlib
     import io as _io
     from nydus_gpu import converter as cv
+    from test_blob import check_stream, cpu_stream
 
     def pack(tar, dict_path=""):
         out = _io.BytesIO()
@@ -584,25 +588,117 @@ def test_converter_testpack_flow(tars, tmp_path):
         for a in range(0, len(tar), 100_000):
             w.write(tar[a:a + 100_000])
         res = w.close()
-        return out.getvalue(), res
+        s = out.getvalue()
+        assert res["digest"] == "sha256:" + hashlib.sha256(s).hexdigest()
+        return s, res
 
-    dict_boot, dres = pack(tars["chunk_dict"])
+    dstream, dres = pack(tars["chunk_dict"])
+    assert dstream == cpu_stream(oracle, tars["chunk_dict"], 0x100000, "zstd")[0]
     merged = _io.BytesIO()
-    blobs = cv.Merge([dict_boot], merged, cv.MergeOption())
-    assert blobs == ["sha256:" + dres["own_blob_id"]]          # converter_test.go:440
+    blobs = cv.Merge([cv.Layer(dres["digest"], dstream)], merged, cv.MergeOption())
+    assert blobs == [dres["digest"]]
     dict_path = str(tmp_path / "dict-bootstrap")
     with open(dict_path, "wb") as f:
         f.write(merged.getvalue())
 
-    lower_boot, lres = pack(tars["oci_lower"], dict_path)
-    upper_boot, ures = pack(tars["oci_upper"], dict_path)
+    lstream, lres = pack(tars["oci_lower"], dict_path)
+    ustream, ures = pack(tars["oci_upper"], dict_path)
     assert (lres["results"]["kind"] == nydus_gpu.DICT).all()
-    assert lres["blob_ids"] == [dres["own_blob_id"]]
+    for tar, stream, res in ((tars["oci_lower"], lstream, lres), (tars["oci_upper"], ustream, ures)):
+        ref = cpu_stream(oracle, tar, 0x100000, "zstd", dict_boot=merged.getvalue())
+        assert stream == ref[0]
+        check_stream(oracle, stream, res["info"], tar, res["chunks"], res["results"], "zstd")
     out = _io.BytesIO()
-    blobs = cv.Merge([lower_boot, upper_boot], out, cv.MergeOption(ChunkDictPath=dict_path))
-    assert blobs == ["sha256:" + dres["own_blob_id"], "sha256:" + ures["own_blob_id"]]  # :513-519
+    blobs = cv.Merge([cv.Layer(lres["digest"], lstream), cv.Layer(ures["digest"], ustream)], out,
+                     cv.MergeOption(ChunkDictPath=dict_path))
+    assert blobs == [dres["digest"], ures["digest"]]
     b = rafs.read_v6(out.getvalue())
-    assert b["blob_ids"] == [dres["own_blob_id"], ures["own_blob_id"]]
+    assert b["blob_ids"] == [dres["digest"][7:], ures["digest"][7:]]
+
+
+@pytest.mark.parametrize("compressor", ["none", "zstd", "lz4_block"])
+def test_pack_stream_matches_host_writer(golden_layers, tars, oracle, compressor):
+    """GPU Pack with the layer retained in HBM (NEW chunks gathered on the GPU,
+    copied to the host window by window) writes exactly the stream the host
+    writer produces from the oracle's decisions; tiny staging forces many
+    segments and blob windows."""
+    import io as _io
+    from test_blob import check_stream, cpu_stream
+    rng = np.random.default_rng(5)
+    for case in golden_layers["cases"]:
+        cs, dg = case["chunk_size"], case["digester"]
+        tb = tars[case["layer"]]
+        ref, rinfo, rch, rres, _ = cpu_stream(oracle, tb, cs, compressor, dg)
+        eng = nydus_gpu.Engine(digester=dg, chunk_size=cs, staging_bytes=4 * cs)
+        try:
+            w = eng.pack(retain=True)
+            pos = 0
+            while pos < len(tb):
+                k = int(rng.integers(1, 300_000))
+                w.write(tb[pos:pos + k])
+                pos += k
+            out = _io.BytesIO()
+            ch, res, st, info = w.finish(out, compressor=compressor)
+        finally:
+            eng.close()
+        assert ch.tobytes() == rch.tobytes(), case["layer"]
+        assert out.getvalue() == ref, (case["layer"], compressor)
+        assert info == rinfo
+        check_stream(oracle, out.getvalue(), info, tb, ch, res, compressor, dg)
+
+
+def test_pack_stream_large_random_layer(oracle):
+    """~200 MiB tar (random + repeated + compressible files) through 8 MiB
+    staging slots with the blob stream written at the end."""
+    import io
+    import tarfile
+    from test_blob import check_stream
+    rng = np.random.default_rng(18)
+    bio = io.BytesIO()
+    tf = tarfile.open(fileobj=bio, mode="w", format=tarfile.GNU_FORMAT)
+    prev = b""
+    for i in range(260):
+        n = int(rng.choice([0, 100, 5000, 70000, 1 << 20, 3 << 20]) + rng.integers(0, 3000))
+        if i % 7 == 0:
+            data = prev
+        elif i % 5 == 0:
+            data = bytes(n)  # compressible
+        else:
+            data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        prev = data
+        ti = tarfile.TarInfo(f"f{i}")
+        ti.size = len(data)
+        tf.addfile(ti, io.BytesIO(data))
+    tf.close()
+    tb = bio.getvalue()
+    eng = nydus_gpu.Engine(chunk_size=0x100000, staging_bytes=8 << 20)
+    try:
+        w = eng.pack(retain=True)
+        for a in range(0, len(tb), 5 << 20):
+            w.write_zero_copy(tb[a:a + (5 << 20)])
+        out = io.BytesIO()
+        ch, res, st, info = w.finish(out, compressor="zstd")
+    finally:
+        eng.close()
+    ref_ch = oracle.tar_chunks(tb, 0x100000)
+    assert ch.tobytes() == ref_ch.tobytes()
+    dig = oracle.digest_chunks(tb, ref_ch, "blake3")
+    assert np.array_equal(res["digest"], dig)
+    check_stream(oracle, out.getvalue(), info, tb, ch, res, "zstd")
+    assert 0 < info["compressed_chunks"] < info["blob_chunks"]
+
+
+def test_pack_finish_needs_retain(tars):
+    import io
+    eng = nydus_gpu.Engine(chunk_size=0x100000)
+    try:
+        w = eng.pack()
+        w.write(tars["oci_lower"])
+        with pytest.raises(nydus_gpu.NgpuError) as e:
+            w.finish(io.BytesIO())
+        assert e.value.code == -1
+    finally:
+        eng.close()
 
 
 def test_fs_version_5_offsets(oracle):

@@ -115,21 +115,25 @@ def test_converter_options():
 
 
 def test_merge_blob_bookkeeping():
-    """Merge returns blobs in first-appearance order; chunk blob indices are
-    remapped into the merged blob table (builder.go:220-294 output JSON)."""
-    import io as _io
-    from nydus_gpu import converter as cv
+    """ngpu_merge: blobs in first-appearance order; chunk blob indices are
+    remapped into the merged blob table (builder.go:220-294 output JSON); a
+    layer's non-dict blob takes the layer digest (convert_unix.go:567-573)."""
     recs = np.zeros(3, rafs.CHUNK_INFO_DTYPE)
     recs["blob_index"] = [0, 1, 1]
     a = rafs.write_v6_bootstrap(recs, 0x100000, blobs=rafs.make_blob_table(["aa" * 32, "bb" * 32], 0x100000))
     recs2 = np.zeros(1, rafs.CHUNK_INFO_DTYPE)
     b = rafs.write_v6_bootstrap(recs2, 0x100000, blobs=rafs.make_blob_table(["cc" * 32], 0x100000))
     c = rafs.write_v6_bootstrap(recs2, 0x100000, blobs=rafs.make_blob_table(["bb" * 32], 0x100000))
-    out = _io.BytesIO()
-    blobs = cv.Merge([a, b, c], out, cv.MergeOption())
-    assert blobs == ["sha256:" + "aa" * 32, "sha256:" + "bb" * 32, "sha256:" + "cc" * 32]
-    m = rafs.read_v6(out.getvalue())
+    d = rafs.write_v6_bootstrap(np.zeros(0, rafs.CHUNK_INFO_DTYPE), 0x100000,
+                                blobs=rafs.make_blob_table(["aa" * 32, "bb" * 32], 0x100000))
+    merged, ids = nydus_gpu.merge([a, b, c], ["11" * 32, "dd" * 32, "22" * 32], d)
+    assert ids == ["aa" * 32, "bb" * 32, "dd" * 32]
+    m = rafs.read_v6(merged)
+    assert m["blob_ids"] == ids
     assert list(m["chunks"]["blob_index"]) == [0, 1, 1, 2, 1]
+    # without digests the ids are kept
+    merged, ids = nydus_gpu.merge([b], [""])
+    assert ids == ["cc" * 32]
 
 
 def test_tar_scanner_fuzz_agrees_with_oracle(tars, oracle):
