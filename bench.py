@@ -226,6 +226,26 @@ def end_to_end(torch, nydus_gpu, buf, wl, stride, device, sample_bytes=2 << 30):
         res["streaming_gbs"] = round(file_bytes * reps / (time.perf_counter() - t0) / 1e9, 1)
         assert out2.tobytes() == out.tobytes()
         res["bound"] = "PCIe Gen5 x16 H2D (~50-55 GB/s) and host memcpy into staging"
+        # converter.Pack end to end: tar in -> nydus blob stream out (layer kept
+        # in HBM, NEW chunks gathered on the GPU and copied back, per-chunk host
+        # compression, host SHA-256 of the stream), written to /dev/null
+        import hashlib
+        fd = os.open(os.devnull, os.O_WRONLY)
+        try:
+            for comp in ("none", "zstd"):
+                t0 = time.perf_counter()
+                w = eng.pack(retain=True)
+                for a in range(0, host.size, 32 << 20):
+                    w.write(host[a:a + (32 << 20)])
+                _, _, _, info = w.finish(nydus_gpu.FdWriter(fd), compressor=comp)
+                res[f"pack_stream_{comp}_gbs"] = round(file_bytes / (time.perf_counter() - t0) / 1e9, 2)
+        finally:
+            os.close(fd)
+        t0 = time.perf_counter()
+        hashlib.sha256(memoryview(host[:1 << 30])).digest()
+        res["host_sha256_gbs"] = round((1 << 30) / (time.perf_counter() - t0) / 1e9, 2)
+        res["pack_stream_bound"] = ("host SHA-256 of the output stream (sequential; the layer "
+                                    "digest, SURVEY.md §8(a) a9) and host compression")
     finally:
         L.ngpu_free_pinned(eng._h, hp)
         eng.close()

@@ -323,6 +323,8 @@ typedef struct {
 
 /* Thread-local message of the last failing engine-less call below. */
 const char *ngpu_host_error(void);
+/* A ready-made ngpu_write_fn: ctx is a file descriptor ((void *)(intptr_t)fd). */
+int ngpu_write_fd(void *ctx, const void *buf, uint64_t len);
 
 /* Host: write the stream of one packed layer whose bytes are in host memory
  * (chunks/results/stats as returned by ngpu_pack_tar / ngpu_process). */

@@ -26,11 +26,13 @@
 // the layout rules above and the reference reader's ability to find and
 // decode every entry (tests/test_blob.py).
 #include <dlfcn.h>
+#include <errno.h>
 #include <openssl/evp.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -623,6 +625,21 @@ using namespace ngpu;
 extern "C" {
 
 const char *ngpu_host_error(void) { return host_error(); }
+
+int ngpu_write_fd(void *ctx, const void *buf, uint64_t len) {
+  const int fd = (int)(intptr_t)ctx;
+  const uint8_t *p = (const uint8_t *)buf;
+  while (len) {
+    const ssize_t r = write(fd, p, len > (1ull << 30) ? (1ull << 30) : len);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return host_fail(NGPU_EIO, "write(fd %d): %s", fd, strerror(errno));
+    }
+    p += r;
+    len -= (uint64_t)r;
+  }
+  return 0;
+}
 
 int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
                     const ngpu_result *results, uint64_t n, const ngpu_layer_stats *stats,

@@ -54,7 +54,8 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_pack_open", "ngpu_pack_write", "ngpu_pack_reserve", "ngpu_pack_commit",
            "ngpu_pack_close", "ngpu_pack_abort", "ngpu_dedup_layers_device",
            "ngpu_process_layers_device", "ngpu_host_error", "ngpu_blob_write",
-           "ngpu_pack_open_ex", "ngpu_pack_finish", "ngpu_unpack_entry", "ngpu_merge"]
+           "ngpu_pack_open_ex", "ngpu_pack_finish", "ngpu_unpack_entry", "ngpu_merge",
+           "ngpu_write_fd"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
@@ -232,11 +233,24 @@ def _host_check(rc, what):
         raise NgpuError(rc, f"{what}: {msg.decode() if msg else ''}")
 
 
+class FdWriter:
+    """dest for blob streams written straight from C (ngpu_write_fd) to a file
+    descriptor, without a Python callback per batch."""
+
+    def __init__(self, fd: int):
+        self.fd = fd
+
+
 class _Sink:
     """io.Writer -> ngpu_write_fn (exceptions are kept and re-raised)."""
 
     def __init__(self, dest):
         self.dest, self.exc = dest, None
+        if isinstance(dest, FdWriter):
+            self.fn = WRITE_FN(ctypes.cast(lib().ngpu_write_fd, ctypes.c_void_p).value)
+            self.ctx = ctypes.c_void_p(dest.fd)
+            return
+        self.ctx = None
 
         def fn(_ctx, buf, n):
             try:
@@ -280,7 +294,7 @@ def blob_write(data, chunks, results, stats: dict, dest, compressor: str = "", l
     sink = _Sink(dest)
     info = NgpuBlobInfo()
     rc = L.ngpu_blob_write(_ptr(buf), buf.size, _ptr(ch), _ptr(rs), len(ch), ctypes.byref(st),
-                           ctypes.byref(o), sink.fn, None, ctypes.byref(info))
+                           ctypes.byref(o), sink.fn, sink.ctx, ctypes.byref(info))
     sink.reraise()
     _host_check(rc, "blob_write")
     del keep
@@ -562,7 +576,7 @@ class PackWriter:
             o, keep = blob_options(compressor, level, threads, self._eng.digester,
                                    self._eng.chunk_size, dict_blobs)
             sink = _Sink(dest)
-            rc = L.ngpu_pack_finish(p, ctypes.byref(o), sink.fn, None, ctypes.byref(pc),
+            rc = L.ngpu_pack_finish(p, ctypes.byref(o), sink.fn, sink.ctx, ctypes.byref(pc),
                                     ctypes.byref(pr), ctypes.byref(n), ctypes.byref(st),
                                     ctypes.byref(info))
             sink.reraise()

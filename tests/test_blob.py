@@ -278,3 +278,22 @@ def test_blob_write_rejects_bad_input(oracle, tars):
             raise OSError("disk full")
     with pytest.raises(OSError):
         nydus_gpu.blob_write(tar, ch, res, st, Broken(), compressor="none")
+
+
+def test_fd_writer_matches_python_writer(oracle, tars, tmp_path):
+    """ngpu_write_fd (the C-level dest) writes the same bytes as a Python io.Writer."""
+    tar = tars["oci_upper"]
+    ch, res, st = cpu_results(oracle, tar, 0x10000)
+    a = io.BytesIO()
+    nydus_gpu.blob_write(tar, ch, res, st, a, compressor="lz4_block", chunk_size=0x10000)
+    path = tmp_path / "blob"
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
+    try:
+        info = nydus_gpu.blob_write(tar, ch, res, st, nydus_gpu.FdWriter(fd), compressor="lz4_block",
+                                    chunk_size=0x10000)
+    finally:
+        os.close(fd)
+    assert path.read_bytes() == a.getvalue()
+    assert info["stream_bytes"] == len(a.getvalue())
+    with pytest.raises(nydus_gpu.NgpuError):  # closed descriptor
+        nydus_gpu.blob_write(tar, ch, res, st, nydus_gpu.FdWriter(fd), compressor="none")
