@@ -1,0 +1,288 @@
+// converter.cpp — see converter.hpp.  Only the C ABI is used.
+#include "converter.hpp"
+
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
+
+#include "nydus_gpu.h"
+
+namespace nydus {
+namespace converter {
+
+const char *const EntryBlob = "image.blob";
+const char *const EntryBootstrap = "image.boot";
+const char *const EntryBlobMeta = "blob.meta";
+const char *const EntryTOC = "rafs.blob.toc";
+
+namespace {
+
+Error err(int code, const std::string &msg) { return Error{code ? code : NGPU_EINVAL, msg}; }
+
+std::string hex(const uint8_t *d, int n) {
+  static const char *x = "0123456789abcdef";
+  std::string s;
+  for (int i = 0; i < n; ++i) {
+    s += x[d[i] >> 4];
+    s += x[d[i] & 15];
+  }
+  return s;
+}
+
+int write_trampoline(void *ctx, const void *buf, uint64_t len) {
+  Writer *w = static_cast<Writer *>(ctx);
+  return w->Write(buf, (size_t)len) ? 1 : 0;
+}
+
+int64_t read_trampoline(void *ctx, void *buf, uint64_t len, uint64_t off) {
+  return static_cast<ReaderAt *>(ctx)->ReadAt(buf, (size_t)len, off);
+}
+
+Error parse_chunk_size(const std::string &s, uint32_t *out) {
+  if (s.empty()) {
+    *out = 0x100000;
+    return {};
+  }
+  char *end = nullptr;
+  const unsigned long long v = strtoull(s.c_str(), &end, 0);
+  if (!end || *end || (v & (v - 1)) || v < 0x1000 || v > 0x1000000)
+    return err(NGPU_EINVAL, "invalid chunk size " + s + ": must be power of two in [0x1000, 0x1000000]");
+  *out = (uint32_t)v;
+  return {};
+}
+
+Error compressor_of(const std::string &s, uint32_t *out) {
+  if (s.empty() || s == "zstd") *out = NGPU_COMPRESSOR_ZSTD;  // nydus-image default
+  else if (s == "none") *out = NGPU_COMPRESSOR_NONE;
+  else if (s == "lz4_block") *out = NGPU_COMPRESSOR_LZ4_BLOCK;
+  else return err(NGPU_EINVAL, "unsupported compressor " + s);
+  return {};
+}
+
+// One engine per (device, digester, chunk size, fs version), like the Python
+// mirror; an engine serialises its own calls.
+std::mutex g_mu;
+std::map<std::tuple<int, uint32_t, uint32_t, uint32_t>, ngpu_engine *> g_engines;
+
+Error engine_for(const PackOption &opt, ngpu_engine **out) {
+  uint32_t cs = 0;
+  if (Error e = parse_chunk_size(opt.ChunkSize, &cs)) return e;
+  const std::string fv = opt.FsVersion.empty() ? "6" : opt.FsVersion;  // convert_unix.go:326-328
+  if (fv != "5" && fv != "6") return err(NGPU_EINVAL, "invalid fs version " + opt.FsVersion);
+  uint32_t dg;
+  if (opt.Digester.empty() || opt.Digester == "blake3") dg = NGPU_DIGEST_BLAKE3;
+  else if (opt.Digester == "sha256") dg = NGPU_DIGEST_SHA256;
+  else return err(NGPU_EINVAL, "unsupported digester " + opt.Digester);
+  const auto key = std::make_tuple(opt.Device, dg, cs, (uint32_t)(fv[0] - '0'));
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_engines.find(key);
+  if (it == g_engines.end()) {
+    ngpu_config cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.device = opt.Device;
+    cfg.digester = dg;
+    cfg.chunk_size = cs;
+    cfg.fs_version = std::get<3>(key);
+    ngpu_engine *e = nullptr;
+    if (int rc = ngpu_create(&cfg, &e)) return err(rc, "gpu engine: create failed");
+    it = g_engines.emplace(key, e).first;
+  }
+  *out = it->second;
+  return {};
+}
+
+class GpuPackWriteCloser : public PackWriteCloser {
+ public:
+  GpuPackWriteCloser(ngpu_engine *e, ngpu_pack *p, Writer &dest, uint32_t comp)
+      : e_(e), p_(p), dest_(dest), comp_(comp) {}
+  ~GpuPackWriteCloser() override {
+    if (p_) ngpu_pack_abort(p_);
+  }
+  Error Write(const void *p, size_t n) override {
+    if (!p_) return err(NGPU_EINVAL, "write to a closed pack");
+    if (!n) return {};
+    if (int rc = ngpu_pack_write(p_, p, n)) {
+      p_ = nullptr;  // released by the library
+      return err(rc, std::string("pack write: ") + ngpu_last_error(e_));
+    }
+    return {};
+  }
+  Error Close() override {
+    if (!p_) return err(NGPU_EINVAL, "pack already closed");
+    ngpu_blob_options o;
+    memset(&o, 0, sizeof o);
+    o.compressor = comp_;
+    ngpu_chunk *ch = nullptr;
+    ngpu_result *res = nullptr;
+    uint64_t n = 0;
+    ngpu_layer_stats st;
+    ngpu_blob_info info;
+    ngpu_pack *p = p_;
+    p_ = nullptr;
+    const int rc = ngpu_pack_finish(p, &o, write_trampoline, &dest_, &ch, &res, &n, &st, &info);
+    if (rc) return err(rc, std::string("convert nydus ref: ") + ngpu_last_error(e_));
+    ngpu_free_host(ch);
+    ngpu_free_host(res);
+    stats_.Digest = "sha256:" + hex(info.stream_digest, 32);
+    stats_.Chunks = st.chunks;
+    stats_.NewChunks = st.new_chunks;
+    stats_.IntraChunks = st.intra_chunks;
+    stats_.DictChunks = st.dict_chunks;
+    stats_.StreamBytes = info.stream_bytes;
+    stats_.BlobBytes = info.blob_bytes;
+    return {};
+  }
+  const PackStats &Stats() const override { return stats_; }
+
+ private:
+  ngpu_engine *e_;
+  ngpu_pack *p_;
+  Writer &dest_;
+  uint32_t comp_;
+  PackStats stats_;
+};
+
+// packToTar (utils.go:92-160) without compression: image/ + image/<name>.
+void tar_header(uint8_t h[512], const char *name, uint64_t size, char type, unsigned mode) {
+  memset(h, 0, 512);
+  char *b = (char *)h;
+  snprintf(b, 100, "%s", name);
+  snprintf(b + 100, 8, "%07o", mode);
+  snprintf(b + 108, 8, "%07o", 0);
+  snprintf(b + 116, 8, "%07o", 0);
+  snprintf(b + 124, 12, "%011llo", (unsigned long long)size);
+  snprintf(b + 136, 12, "%011o", 0);
+  b[156] = type;
+  memcpy(b + 257, "ustar\0" "00", 8);
+  memset(b + 148, ' ', 8);
+  unsigned sum = 0;
+  for (int i = 0; i < 512; ++i) sum += h[i];
+  snprintf(b + 148, 8, "%06o", sum);
+  b[155] = ' ';
+}
+
+}  // namespace
+
+Error BufferWriter::Write(const void *p, size_t n) {
+  const uint8_t *b = static_cast<const uint8_t *>(p);
+  data.insert(data.end(), b, b + n);
+  return {};
+}
+
+int64_t BytesReaderAt::ReadAt(void *p, size_t n, uint64_t off) {
+  if (off >= n_) return -1;
+  if (n > n_ - off) n = (size_t)(n_ - off);
+  memcpy(p, p_ + off, n);
+  return (int64_t)n;
+}
+
+std::string TOCEntry::GetName() const {  // types.go:181-191
+  std::string s;
+  for (uint8_t c : Name) {
+    if (!c) break;
+    s += (char)c;
+  }
+  return s;
+}
+
+Error TOCEntry::GetCompressor(Compressor *out) const {  // types.go:167-179
+  switch (Flags & CompressorMask) {
+    case CompressorNone: *out = CompressorNone; return {};
+    case CompressorZstd: *out = CompressorZstd; return {};
+    case CompressorLz4Block: *out = CompressorLz4Block; return {};
+  }
+  char b[64];
+  snprintf(b, sizeof b, "unsupported compressor, entry flags %x", Flags);
+  return err(NGPU_EUNSUPP, b);
+}
+
+std::string TOCEntry::GetUncompressedDigest() const { return hex(UncompressedDigest, 32); }
+
+bool IsNotFound(const Error &e) { return e.code == NGPU_ENOTFOUND; }
+
+Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser> *out) {
+  out->reset();
+  if (opt.OCIRef) return err(NGPU_EUNSUPP, "OCIRef packing has no chunk digest stage");
+  uint32_t comp = 0;
+  if (Error e = compressor_of(opt.Compressor, &comp)) return e;
+  ngpu_engine *e = nullptr;
+  if (Error x = engine_for(opt, &e)) return x;
+  int rc = opt.ChunkDictPath.empty() ? ngpu_dict_clear(e)
+                                     : ngpu_dict_load_bootstrap(e, opt.ChunkDictPath.c_str());
+  if (rc) return err(rc, "load chunk dict " + opt.ChunkDictPath + ": " + ngpu_last_error(e));
+  ngpu_pack *p = nullptr;
+  if ((rc = ngpu_pack_open_ex(e, NGPU_PACK_RETAIN, &p)))
+    return err(rc, std::string("pack open: ") + ngpu_last_error(e));
+  out->reset(new GpuPackWriteCloser(e, p, dest, comp));
+  return {};
+}
+
+Error UnpackEntry(ReaderAt &ra, const std::string &targetName, Writer &target, TOCEntry *entry) {
+  TOCEntry t;
+  const int rc = ngpu_unpack_entry(read_trampoline, &ra, ra.Size(), targetName.c_str(),
+                                   write_trampoline, &target, reinterpret_cast<uint8_t *>(&t));
+  if (rc) return err(rc, ngpu_host_error());
+  if (entry) *entry = t;
+  return {};
+}
+
+Error Merge(const std::vector<Layer> &layers, Writer &dest, const MergeOption &opt,
+            std::vector<std::string> *blobDigests) {
+  blobDigests->clear();
+  std::vector<BufferWriter> boots(layers.size());
+  std::vector<std::string> hexes(layers.size());
+  for (size_t i = 0; i < layers.size(); ++i) {
+    if (!layers[i].ReaderAt) return err(NGPU_EINVAL, "layer without reader");
+    if (Error e = UnpackEntry(*layers[i].ReaderAt, EntryBootstrap, boots[i], nullptr))
+      return err(e.code, "unpack all bootstraps: unpack nydus tar: " + e.msg);
+    const std::string &d = layers[i].Digest;
+    hexes[i] = d.compare(0, 7, "sha256:") == 0 ? d.substr(7) : d;
+  }
+  std::vector<uint8_t> dict;
+  if (!opt.ChunkDictPath.empty()) {
+    FILE *f = fopen(opt.ChunkDictPath.c_str(), "rb");
+    if (!f) return err(NGPU_EIO, "open chunk dict " + opt.ChunkDictPath);
+    uint8_t buf[1 << 16];
+    size_t r;
+    while ((r = fread(buf, 1, sizeof buf, f)) > 0) dict.insert(dict.end(), buf, buf + r);
+    fclose(f);
+  }
+  std::vector<const void *> ptrs;
+  std::vector<uint64_t> sizes;
+  std::vector<const char *> names;
+  for (size_t i = 0; i < layers.size(); ++i) {
+    ptrs.push_back(boots[i].data.data());
+    sizes.push_back(boots[i].data.size());
+    names.push_back(hexes[i].c_str());
+  }
+  BufferWriter merged;
+  char *ids = nullptr;
+  const int rc = ngpu_merge(ptrs.data(), sizes.data(), names.data(), layers.size(),
+                            dict.empty() ? nullptr : dict.data(), dict.size(), write_trampoline,
+                            &merged, &ids);
+  if (rc) return err(rc, std::string("merge bootstrap: ") + ngpu_host_error());
+  for (const char *s = ids; s && *s;) {
+    const char *c = strchr(s, ',');
+    const std::string id = c ? std::string(s, c - s) : std::string(s);
+    blobDigests->push_back("sha256:" + id);
+    s = c ? c + 1 : nullptr;
+  }
+  ngpu_free_host(ids);
+  if (!opt.WithTar) return dest.Write(merged.data.data(), merged.data.size());
+  uint8_t h[512];
+  tar_header(h, "image", 0, '5', 0755);
+  if (Error e = dest.Write(h, 512)) return e;
+  tar_header(h, "image/image.boot", merged.data.size(), '0', 0444);
+  if (Error e = dest.Write(h, 512)) return e;
+  if (Error e = dest.Write(merged.data.data(), merged.data.size())) return e;
+  static const uint8_t zeros[1024] = {};
+  const size_t pad = (512 - merged.data.size() % 512) % 512;
+  if (Error e = dest.Write(zeros, pad)) return e;
+  return dest.Write(zeros, 1024);  // end-of-archive (tar.Writer.Close)
+}
+
+}  // namespace converter
+}  // namespace nydus

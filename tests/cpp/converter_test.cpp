@@ -1,0 +1,151 @@
+// converter_test.cpp — TestPack (tests/converter_test.go:276-300, 420-528)
+// restated against the C++ converter mirror (nydus-snapshotter_amd/host/
+// converter.hpp) on the GPU.  Reads the three layer tars the Python harness
+// writes (chunk dict, lower, upper), packs and merges exactly as the Go test
+// does, and checks the same assertions with REQUIRE (require.*).
+// usage: converter_test DICT.tar LOWER.tar UPPER.tar WORKDIR [COMPRESSOR]
+// Prints "digest <name> sha256:<hex>" lines and "PASS"; exit 1 on failure.
+#include <openssl/evp.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <string>
+#include <vector>
+
+#include "converter.hpp"
+
+using namespace nydus::converter;
+
+#define REQUIRE(c, ...)                                              \
+  do {                                                               \
+    if (!(c)) {                                                      \
+      fprintf(stderr, "REQUIRE failed at %s:%d: %s: ", __FILE__, __LINE__, #c); \
+      fprintf(stderr, __VA_ARGS__);                                  \
+      fprintf(stderr, "\n");                                         \
+      exit(1);                                                       \
+    }                                                                \
+  } while (0)
+#define REQUIRE_NOERR(e) REQUIRE(!(e), "error %d: %s", (e).code, (e).msg.c_str())
+
+static std::vector<uint8_t> read_file(const std::string &p) {
+  FILE *f = fopen(p.c_str(), "rb");
+  REQUIRE(f, "open %s", p.c_str());
+  std::vector<uint8_t> v;
+  uint8_t b[1 << 16];
+  size_t r;
+  while ((r = fread(b, 1, sizeof b, f)) > 0) v.insert(v.end(), b, b + r);
+  fclose(f);
+  return v;
+}
+
+static void write_file(const std::string &p, const std::vector<uint8_t> &v) {
+  FILE *f = fopen(p.c_str(), "wb");
+  REQUIRE(f && fwrite(v.data(), 1, v.size(), f) == v.size(), "write %s", p.c_str());
+  fclose(f);
+}
+
+// digest.Canonical.Digester() over the Pack output
+static std::string sha256_digest(const std::vector<uint8_t> &v) {
+  uint8_t d[32];
+  unsigned int l = 32;
+  EVP_MD_CTX *c = EVP_MD_CTX_new();
+  EVP_DigestInit_ex(c, EVP_sha256(), nullptr);
+  EVP_DigestUpdate(c, v.data(), v.size());
+  EVP_DigestFinal_ex(c, d, &l);
+  EVP_MD_CTX_free(c);
+  static const char *x = "0123456789abcdef";
+  std::string s = "sha256:";
+  for (uint8_t b : d) {
+    s += x[b >> 4];
+    s += x[b & 15];
+  }
+  return s;
+}
+
+struct Packed {
+  std::vector<uint8_t> data;
+  std::string digest;
+  PackStats stats;
+};
+
+// packLayer (converter_test.go:276-300): Pack, copy the source in, Close.
+static Packed packLayer(const std::vector<uint8_t> &source, const std::string &chunkDict,
+                        const std::string &compressor) {
+  BufferWriter data;
+  PackOption opt;
+  opt.ChunkDictPath = chunkDict;
+  opt.FsVersion = "6";
+  opt.Compressor = compressor;
+  std::unique_ptr<PackWriteCloser> twc;
+  REQUIRE_NOERR(Pack(data, opt, &twc));
+  for (size_t a = 0; a < source.size(); a += 100000) {  // io.Copy in pieces
+    const size_t n = source.size() - a < 100000 ? source.size() - a : 100000;
+    REQUIRE_NOERR(twc->Write(source.data() + a, n));
+  }
+  REQUIRE_NOERR(twc->Close());
+  Packed p{data.data, sha256_digest(data.data), twc->Stats()};
+  REQUIRE(p.digest == p.stats.Digest, "stream digest %s vs %s", p.digest.c_str(),
+          p.stats.Digest.c_str());
+  return p;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 5) return 2;
+  const std::vector<uint8_t> dictTar = read_file(argv[1]), lowerTar = read_file(argv[2]),
+                             upperTar = read_file(argv[3]);
+  const std::string workDir = argv[4];
+  const std::string comp = argc > 5 ? argv[5] : "";
+
+  // buildChunkDict (converter_test.go:420-455)
+  Packed dict = packLayer(dictTar, "", comp);
+  write_file(workDir + "/" + dict.digest.substr(7), dict.data);
+  std::vector<Layer> layers{{dict.digest, std::make_shared<BytesReaderAt>(dict.data.data(),
+                                                                           dict.data.size())}};
+  BufferWriter dictBoot;
+  std::vector<std::string> blobDigests;
+  REQUIRE_NOERR(Merge(layers, dictBoot, MergeOption{}, &blobDigests));
+  REQUIRE(blobDigests.size() == 1 && blobDigests[0] == dict.digest, "dict blob digests");
+  const std::string chunkDictBootstrapPath = workDir + "/dict-bootstrap";
+  write_file(chunkDictBootstrapPath, dictBoot.data);
+
+  // testPack (converter_test.go:459-528)
+  Packed lower = packLayer(lowerTar, chunkDictBootstrapPath, comp);
+  Packed upper = packLayer(upperTar, chunkDictBootstrapPath, comp);
+  REQUIRE(lower.stats.DictChunks == lower.stats.Chunks && lower.stats.NewChunks == 0,
+          "lower layer is all chunk-dict hits");
+  REQUIRE(upper.stats.NewChunks > 0, "upper layer brings new chunks");
+  std::vector<Layer> two{
+      {lower.digest, std::make_shared<BytesReaderAt>(lower.data.data(), lower.data.size())},
+      {upper.digest, std::make_shared<BytesReaderAt>(upper.data.data(), upper.data.size())}};
+  BufferWriter bootstrap;
+  MergeOption mo;
+  mo.ChunkDictPath = chunkDictBootstrapPath;
+  REQUIRE_NOERR(Merge(two, bootstrap, mo, &blobDigests));
+  REQUIRE(blobDigests.size() == 2 && blobDigests[0] == dict.digest &&
+              blobDigests[1] == upper.digest,
+          "expectedBlobDigests := [chunkDictBlobDigest, upperNydusBlobDigest]");
+  write_file(workDir + "/bootstrap", bootstrap.data);
+
+  // UnpackEntry finds the bootstrap through the TOC; ErrNotFound otherwise
+  BytesReaderAt ra(upper.data.data(), upper.data.size());
+  BufferWriter boot;
+  TOCEntry e;
+  REQUIRE_NOERR(UnpackEntry(ra, EntryBootstrap, boot, &e));
+  Compressor c = 0;
+  REQUIRE(e.GetName() == EntryBootstrap && !e.GetCompressor(&c) && c == CompressorNone, "toc");
+  BufferWriter none;
+  Error nf = UnpackEntry(ra, EntryBlobMeta, none, nullptr);
+  REQUIRE(IsNotFound(nf), "ErrNotFound for a missing entry (got %d)", nf.code);
+
+  // option errors come back as errors, like the Go API
+  PackOption bad;
+  bad.ChunkSize = "0x1001";
+  std::unique_ptr<PackWriteCloser> w;
+  BufferWriter sink;
+  REQUIRE(Pack(sink, bad, &w).code == -1 && !w, "invalid chunk size is an error");
+
+  printf("digest dict %s\ndigest lower %s\ndigest upper %s\n", dict.digest.c_str(),
+         lower.digest.c_str(), upper.digest.c_str());
+  printf("PASS\n");
+  return 0;
+}
