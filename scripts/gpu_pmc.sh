@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 ok() { local rc=$1 what=$2; echo "$what rc=$rc"; if [ "$rc" -ne 0 ]; then echo "stopping after $what"; exit "$rc"; fi; }
-K='b3_groups|sha256_split'
+K='b3_groups|sha256_split|sha256_pair'
 P=0
 for SET in "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_WAVES SQ_WAIT_ANY SQ_WAVE_CYCLES"; do
   P=$((P+1))
