@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -339,17 +340,82 @@ struct BlobWriter::Impl {
   std::vector<uint32_t> csize;  // per NEW chunk (index order)
   std::vector<uint8_t> cflag;
   uint64_t compressed_chunks = 0;
-  // batch buffers: per-chunk scratch slots, compacted into `out`
-  std::vector<uint8_t> scratch, out;
+  // batch buffers: per-chunk scratch slots, compacted into an output batch
+  std::vector<uint8_t> scratch;
   std::vector<uint64_t> slot_off;
   std::vector<uint64_t> clen;
   int rc = 0;
+  // Sink thread: SHA-256 + dest write of finished batches, so the single
+  // sequential hash overlaps the next batch's compression / copy and the
+  // GPU gather of the next window (at most kDepth batches in flight).
+  static constexpr size_t kDepth = 2;
+  std::thread sink;
+  std::mutex qm;
+  std::condition_variable qcv;
+  std::deque<std::vector<uint8_t>> q, free_bufs;
+  bool busy = false, stop = false;
+  int sink_rc = 0;
+  std::string sink_err;
 
   int emit(const void *p, uint64_t n) {
     if (!n) return 0;
     if (w && w(ctx, p, n) != 0) return host_fail(NGPU_EIO, "pack: dest write failed");
     written += n;
     return 0;
+  }
+  void sink_loop() {
+    std::unique_lock<std::mutex> g(qm);
+    for (;;) {
+      qcv.wait(g, [&] { return stop || !q.empty(); });
+      if (q.empty()) return;
+      std::vector<uint8_t> b = std::move(q.front());
+      q.pop_front();
+      busy = true;
+      const bool failed = sink_rc != 0;
+      g.unlock();
+      int r = 0;
+      if (!failed) {
+        blob_sha.update(b.data(), b.size());
+        r = emit(b.data(), b.size());
+      }
+      g.lock();
+      if (r && !sink_rc) {
+        sink_rc = r;
+        sink_err = host_error();
+      }
+      busy = false;
+      free_bufs.push_back(std::move(b));
+      qcv.notify_all();
+    }
+  }
+  std::vector<uint8_t> take_buffer() {
+    std::unique_lock<std::mutex> g(qm);
+    qcv.wait(g, [&] { return q.size() < kDepth; });
+    if (free_bufs.empty()) return {};
+    std::vector<uint8_t> b = std::move(free_bufs.front());
+    free_bufs.pop_front();
+    return b;
+  }
+  int submit(std::vector<uint8_t> &&b) {
+    std::lock_guard<std::mutex> g(qm);
+    if (sink_rc) return host_fail(sink_rc, "%s", sink_err.c_str());
+    q.push_back(std::move(b));
+    qcv.notify_all();
+    return 0;
+  }
+  int drain() {  // wait for the sink; its error becomes this thread's
+    std::unique_lock<std::mutex> g(qm);
+    qcv.wait(g, [&] { return q.empty() && !busy; });
+    if (sink_rc) return host_fail(sink_rc, "%s", sink_err.c_str());
+    return 0;
+  }
+  ~Impl() {
+    {
+      std::lock_guard<std::mutex> g(qm);
+      stop = true;
+    }
+    qcv.notify_all();
+    if (sink.joinable()) sink.join();
   }
 };
 
@@ -380,6 +446,8 @@ int BlobWriter::init() {
     t = hw ? std::min(16u, hw) : 4u;
   }
   im_->pool.reset(new Pool(t));
+  Impl *m = im_.get();
+  m->sink = std::thread([m] { m->sink_loop(); });
   return 0;
 }
 
@@ -393,12 +461,13 @@ int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) 
     uint64_t b = a, bytes = 0;
     while (b < k && (b == a || bytes + len[b] <= (64ull << 20))) bytes += len[b++];
     const uint64_t nb = b - a;
+    std::vector<uint8_t> out = m.take_buffer();
     if (kind == NGPU_COMPRESSOR_NONE) {
-      m.out.resize(bytes);
+      out.resize(bytes);
       m.slot_off.resize(nb + 1);
       m.slot_off[0] = 0;
       for (uint64_t i = 0; i < nb; ++i) m.slot_off[i + 1] = m.slot_off[i] + len[a + i];
-      m.pool->run(nb, [&](uint64_t i) { memcpy(&m.out[m.slot_off[i]], src[a + i], len[a + i]); });
+      m.pool->run(nb, [&](uint64_t i) { memcpy(&out[m.slot_off[i]], src[a + i], len[a + i]); });
       for (uint64_t i = 0; i < nb; ++i) {
         m.csize.push_back(len[a + i]);
         m.cflag.push_back(0);
@@ -416,20 +485,19 @@ int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) 
       });
       uint64_t total = 0;
       for (uint64_t i = 0; i < nb; ++i) total += m.clen[i] ? m.clen[i] : len[a + i];
-      m.out.resize(total);
+      out.resize(total);
       uint64_t o = 0;
       for (uint64_t i = 0; i < nb; ++i) {
         const bool z = m.clen[i] != 0;
         const uint64_t c = z ? m.clen[i] : len[a + i];
-        memcpy(&m.out[o], z ? &m.scratch[m.slot_off[i]] : src[a + i], c);
+        memcpy(&out[o], z ? &m.scratch[m.slot_off[i]] : src[a + i], c);
         o += c;
         m.csize.push_back((uint32_t)c);
         m.cflag.push_back(z ? 1 : 0);
         m.compressed_chunks += z;
       }
     }
-    m.blob_sha.update(m.out.data(), m.out.size());
-    if ((m.rc = m.emit(m.out.data(), m.out.size()))) return m.rc;
+    if ((m.rc = m.submit(std::move(out)))) return m.rc;
     a = b;
   }
   return 0;
@@ -439,6 +507,7 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
                        const ngpu_layer_stats &st, ngpu_blob_info *info) {
   Impl &m = *im_;
   if (m.rc) return m.rc;
+  if ((m.rc = m.drain())) return m.rc;
   const uint32_t kind = m.opt.compressor;
   const uint64_t blob_bytes = m.written;
   // image.blob digest; the stream digest continues from the same state
