@@ -34,3 +34,4 @@ cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-e2e > "$OUT/prof.log" 2>&1
 ok $? rocprof
 find "$OUT/prof" -name '*stats*' | head
+python3 "$ROOT/scripts/prof_agree.py" "$OUT/prof" 'b3_groups' "$OUT/prof.log" "$OUT/rocprof_agreement.json"
