@@ -418,6 +418,10 @@ void launch_sha256(const uint8_t *data, uint64_t data_len,
       case 4:  // one group per workgroup
         hipLaunchKernelGGL((sha256_pair<1, 0>), g1, dim3(128), 0, s, data, data_len, chunks, n, out, err);
         break;
+      case 5:  // four groups per workgroup: a round and a schedule wave share each SIMD
+        hipLaunchKernelGGL((sha256_pair<4, 0>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0, s,
+                           data, data_len, chunks, n, out, err);
+        break;
       default:
         hipLaunchKernelGGL((sha256_pair<2, 0>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
     }

@@ -20,7 +20,7 @@ ch["length"] = S
 d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
 d_out = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
 ref = None
-for v, name in [(1, "split"), (2, "pair"), (5, "pair-r1"), (3, "pair-nodpp"), (4, "pair-nosched")]:
+for v, name in [(1, "split"), (2, "pair"), (5, "pair-r1"), (6, "pair-r4"), (3, "pair-nodpp"), (4, "pair-nosched")]:
     eng = nydus_gpu.Engine(digester="sha256", chunk_size=S, flags=v << 11)
     s = torch.cuda.Stream()
     for _ in range(2):
