@@ -452,6 +452,10 @@ def main():
         lanes_used = n * (2 if pair else 1)
         max_blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).max())
         chain_s = max_blocks * chain_ops * 4 / CLOCK_HZ
+        # a wave alone on its SIMD issues one VALU op per ~5 cycles, not 4
+        # (tools/valu_ops.hip, profiles/r1/valu_ops_issue_rates.jsonl); the
+        # round wave is alone on its SIMD by design
+        lone_s = max_blocks * chain_ops * 5 / CLOCK_HZ
         roof = {"bound": "valu", "kernel": "sha256_pair" if pair else "sha256_split",
                 "achieved": round(achieved / 1e12, 3),
                 "peak": round(PEAK_INT_OPS / 1e12, 3), "unit": "Tops/s",
@@ -459,6 +463,8 @@ def main():
                 "hbm_gbs": round(file_bytes / (dig_ms / 1e3) / 1e9, 1),
                 "chain_bound_gbs": round(file_bytes / chain_s / 1e9, 1),
                 "chain_frac": round(chain_s / (dig_ms / 1e3), 4),
+                "lone_wave_issue_bound_gbs": round(file_bytes / lone_s / 1e9, 1),
+                "lone_wave_issue_frac": round(lone_s / (dig_ms / 1e3), 4),
                 "occupancy_ceiling": f"{lanes_used} lanes = {lanes_used / (256 * 4 * 64):.3f} "
                                      "waves per SIMD"}
 
