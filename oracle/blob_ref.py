@@ -77,7 +77,8 @@ def parse_toc(data: bytes):
     out = []
     for i in range(len(data) // TOC_ENTRY_SIZE):
         f = TOC_ENTRY.unpack_from(data, i * TOC_ENTRY_SIZE)
-        name = f[2].split(b"\0", 1)[0].decode()
+        # TOCEntry.GetName (types.go:181-191): bytes up to the first NUL, one rune each
+        name = "".join(chr(c) for c in f[2].split(b"\0", 1)[0])
         out.append({"flags": f[0], "name": name, "uncompressed_digest": f[3].hex(),
                     "compressed_offset": f[4], "compressed_size": f[5], "uncompressed_size": f[6]})
     return out
@@ -92,6 +93,8 @@ def seek_file_by_toc(ra: bytes, target: str):
         comp = e["flags"] & COMPRESSOR_MASK
         if comp not in (COMPRESSOR_NONE, COMPRESSOR_ZSTD, COMPRESSOR_LZ4_BLOCK):
             raise ValueError(f"unsupported compressor, entry flags {e['flags']:x}")
+        # io.NewSectionReader + io.Copy: a range past the end yields the bytes
+        # that exist (EOF ends the copy without an error)
         raw = ra[e["compressed_offset"]:e["compressed_offset"] + e["compressed_size"]]
         if comp == COMPRESSOR_ZSTD:
             data = zstd_decompress(raw, e["uncompressed_size"])

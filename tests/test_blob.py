@@ -297,3 +297,62 @@ def test_fd_writer_matches_python_writer(oracle, tars, tmp_path):
     assert info["stream_bytes"] == len(a.getvalue())
     with pytest.raises(nydus_gpu.NgpuError):  # closed descriptor
         nydus_gpu.blob_write(tar, ch, res, st, nydus_gpu.FdWriter(fd), compressor="none")
+
+
+def test_reader_mutation_fuzz_asan(oracle, tars, tmp_path):
+    """Mutated Pack streams (tail byte flips, truncations, header size digits,
+    TOC fields) through the product reader + merge built with ASan/UBSan
+    (tests/cpp/blob_fuzz.cpp, host only): no memory error, and every outcome
+    agrees with the reference reader (oracle/blob_ref.py) — same bytes when
+    both succeed.  One documented deviation: a TOC entry whose range runs past
+    the end of the stream is an error here (EFORMAT), where Go's
+    io.NewSectionReader + io.Copy silently copies the bytes that exist."""
+    import subprocess
+    from conftest import ROOT
+    exe = str(tmp_path / "blob_fuzz")
+    csrc = os.path.join(ROOT, "nydus-snapshotter_amd", "csrc")
+    subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
+                           "-fno-sanitize-recover=all", "-I", os.path.join(ROOT, "include"),
+                           "-I", csrc, os.path.join(ROOT, "tests", "cpp", "blob_fuzz.cpp"),
+                           os.path.join(csrc, "blob.cpp"), "-o", exe, "-lcrypto", "-ldl",
+                           "-lpthread"])
+    stream, *_ = cpu_stream(oracle, tars["edge_pax"], 0x10000, "zstd")
+    sp = tmp_path / "s"
+    sp.write_bytes(stream)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0")
+    out = subprocess.run([exe, str(sp), "1500", "11"], capture_output=True, text=True, env=env,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+
+    def fnv(b):
+        h = 1469598103934665603
+        for x in b:
+            h = ((h ^ x) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+        return h
+    seen = {"ok": 0, "both_fail": 0, "past_end": 0}
+    for line in out.stdout.splitlines():
+        head, res = line.split("|")
+        size, _, ed = head.partition(" ")
+        s = bytearray(stream[:int(size)])
+        for e in filter(None, ed.split(",")):
+            p, v = e.split(":")
+            s[int(p)] = int(v)
+        s = bytes(s)
+        for name, r in zip((blob_ref.ENTRY_BOOTSTRAP, blob_ref.ENTRY_BLOB), res.split(";")):
+            rc, ln, h = map(int, r.split(","))
+            try:
+                data, toc = blob_ref.unpack_entry(s, name)
+                ok = True
+            except (ValueError, blob_ref.NotFound):
+                ok = False
+            if rc == 0:
+                assert ok, (line, name)
+                assert len(data) == ln and (ln > 100_000 or fnv(data) == h), (line, name)
+                seen["ok"] += 1
+            elif ok:
+                assert rc == -8 and toc is not None and \
+                    toc["compressed_offset"] + toc["compressed_size"] > len(s), (line, name)
+                seen["past_end"] += 1
+            else:
+                seen["both_fail"] += 1
+    assert seen["ok"] > 500 and seen["both_fail"] > 100, seen
