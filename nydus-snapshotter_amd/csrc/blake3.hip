@@ -125,15 +125,80 @@ __device__ __forceinline__ bool tree_in_workgroup(uint64_t base, uint64_t ng) {
   return ng > 1 && (base >> 8) == ((base + ng - 1) >> 8);
 }
 
-// Leaf groups per chunk (exclusive-scanned afterwards).
-__global__ void b3_count_groups(const ngpu_chunk *__restrict__ chunks,
-                                uint64_t n, int D, uint64_t *__restrict__ groups) {
-  uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c > n) return;
-  if (c == n) { groups[n] = 0; return; }
-  uint32_t len = chunks[c].length;
-  uint32_t leaves = len == 0 ? 1 : (len + kLeaf - 1) / kLeaf;
-  groups[c] = (leaves + (1u << D) - 1) >> D;
+// Single-group chunks (<= 2^D leaves: the whole chunk is one lane's work) are
+// taken out of the chunk-ordered group space and processed after the
+// multi-group chunks' groups, sorted by their 64-B block count, largest
+// first: lanes of a wave then carry near-equal work (a 4-KiB file next to a
+// full 8-KiB group would leave most of the wave idle).  Counting sort over
+// block counts 1 .. 16 * 2^D (kMaxKey for D <= 4).
+constexpr int kMaxKey = 16 << 4;
+
+// 0: a multi-group chunk; else the chunk's 64-B block count (its work).
+__device__ __forceinline__ uint32_t small_key(const ngpu_chunk &ch, int D) {
+  const uint32_t len = ch.length;
+  const uint32_t leaves = len == 0 ? 1 : (len + kLeaf - 1) / kLeaf;
+  if (leaves > (1u << D)) return 0;
+  return len == 0 ? 1 : (len + 63) / 64;
+}
+
+// Leaf groups per multi-group chunk (0 for single-group chunks; exclusive-
+// scanned afterwards) and the histogram of single-group block counts.
+__global__ __launch_bounds__(256) void b3_count_groups(const ngpu_chunk *__restrict__ chunks,
+                                                       uint64_t n, int D,
+                                                       uint64_t *__restrict__ groups,
+                                                       uint32_t *__restrict__ hist) {
+  __shared__ uint32_t h[kMaxKey + 1];
+  for (int i = threadIdx.x; i <= kMaxKey; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (c < n) {
+    const uint32_t key = small_key(chunks[c], D);
+    if (key) {
+      groups[c] = 0;
+      atomicAdd(&h[key], 1u);
+    } else {
+      const uint32_t len = chunks[c].length;
+      groups[c] = (((len + kLeaf - 1) / kLeaf) + (1u << D) - 1) >> D;
+    }
+  } else if (c == n) {
+    groups[n] = 0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i <= kMaxKey; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// Bucket start offsets, largest block count first; *nsmall = number of
+// single-group chunks.
+__global__ void b3_small_offsets(const uint32_t *__restrict__ hist,
+                                 uint32_t *__restrict__ cursor, uint64_t *__restrict__ nsmall) {
+  if (threadIdx.x != 0) return;
+  uint32_t acc = 0;
+  for (int k = kMaxKey; k >= 1; --k) {
+    cursor[k] = acc;
+    acc += hist[k];
+  }
+  *nsmall = acc;
+}
+
+// small[] = single-group chunk ids sorted by block count (descending; order
+// inside a bucket is arbitrary, results do not depend on it).
+__global__ __launch_bounds__(256) void b3_small_scatter(const ngpu_chunk *__restrict__ chunks,
+                                                        uint64_t n, int D,
+                                                        uint32_t *__restrict__ cursor,
+                                                        uint32_t *__restrict__ small) {
+  __shared__ uint32_t h[kMaxKey + 1], base[kMaxKey + 1];
+  for (int i = threadIdx.x; i <= kMaxKey; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint32_t key = c < n ? small_key(chunks[c], D) : 0;
+  uint32_t rank = 0;
+  if (key) rank = atomicAdd(&h[key], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i <= kMaxKey; i += blockDim.x)
+    if (h[i]) base[i] = atomicAdd(&cursor[i], h[i]);
+  __syncthreads();
+  if (key) small[base[key] + rank] = (uint32_t)c;
 }
 
 // group -> chunk map; one wave per chunk, lanes stride over its groups.
@@ -153,21 +218,14 @@ __global__ void b3_fill_group_chunk(const uint64_t *__restrict__ gbase,
 // block of the lane's byte stream while the current one is compressed,
 // 4 = diagnostic: no global loads at all (wrong digests; VALU ceiling only).
 //
-// Hashes leaf group g.  Returns 0 (no work), 1 (cur = root digest: the
-// chunk fits this group) or 2 (cur = the group's subtree CV).
+// Hashes leaf group j of chunk c (ng groups).  Returns 0 (no work), 1 (cur =
+// root digest: the chunk fits this group) or 2 (cur = the group's subtree CV).
 template <int D, int LM>
 __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64_t data_len,
-                                        const ngpu_chunk *__restrict__ chunks,
-                                        const uint64_t *__restrict__ gbase,
-                                        const uint32_t *__restrict__ gchunk, uint64_t g,
-                                        uint64_t *__restrict__ err, uint32_t cur[8],
-                                        uint32_t &c, uint64_t &base, uint64_t &ng,
-                                        uint32_t &j) {
+                                        const ngpu_chunk *__restrict__ chunks, uint32_t c,
+                                        uint64_t ng, uint32_t j, uint64_t *__restrict__ err,
+                                        uint32_t cur[8]) {
   constexpr int SD = D > 0 ? D : 1;
-  c = gchunk[g];
-  base = gbase[c];
-  ng = gbase[c + 1] - base;
-  j = (uint32_t)(g - base);
   const ngpu_chunk ch = chunks[c];
   const uint32_t len = ch.length;
   if (ch.offset > data_len || len > data_len - ch.offset) {  // bad descriptor
@@ -253,17 +311,31 @@ __global__ __launch_bounds__(256) void b3_groups(
     const ngpu_chunk *__restrict__ chunks, uint64_t n,
     const uint64_t *__restrict__ gbase, const uint32_t *__restrict__ gchunk,
     uint64_t cap_g, uint32_t *__restrict__ cv_out,
-    ngpu_result *__restrict__ out, uint64_t *__restrict__ err) {
+    ngpu_result *__restrict__ out, uint64_t *__restrict__ err,
+    const uint32_t *__restrict__ small, const uint64_t *__restrict__ nsmall) {
   __shared__ uint32_t lcv[256 * 8];
-  const uint64_t total = gbase[n];
+  // groups [0, gm): multi-group chunks in chunk order; [gm, gm + ns): the
+  // single-group chunks, largest first
+  const uint64_t gm = gbase[n];
+  const uint64_t total = gm + *nsmall;
   const uint64_t g0 = blockIdx.x * 256ull;
   const uint64_t g = g0 + threadIdx.x;
   uint32_t cur[8], c = 0, j = 0;
   uint64_t base = 0, ng = 0;
-  const int st = (g < total && g < cap_g)
-                     ? group_cv<D, LM>(data, data_len, chunks, gbase, gchunk, g, err, cur, c,
-                                       base, ng, j)
-                     : 0;
+  int st = 0;
+  if (g < total && g < cap_g) {
+    if (g < gm) {
+      c = gchunk[g];
+      base = gbase[c];
+      ng = gbase[c + 1] - base;
+      j = (uint32_t)(g - base);
+    } else {
+      c = small[g - gm];
+      base = g;
+      ng = 1;
+    }
+    st = group_cv<D, LM>(data, data_len, chunks, c, ng, j, err, cur);
+  }
   if (st == 1) {
     uint4 *d = reinterpret_cast<uint4 *>(out[c].digest);
     d[0] = make_uint4(cur[0], cur[1], cur[2], cur[3]);
@@ -403,7 +475,7 @@ static void launch_groups_lm(const uint8_t *data, uint64_t data_len,
   const uint64_t blocks = (ws.cap_g + 255) / 256;
   hipLaunchKernelGGL((b3_groups<D, LM>), dim3((unsigned)blocks), dim3(256), 0, s, data,
                      data_len, chunks, n, ws.groups, ws.group_chunk, ws.cap_g,
-                     ws.cv, out, ws.stats + 7);
+                     ws.cv, out, ws.stats + 7, ws.small, ws.stats + 10);
 }
 
 template <int D>
@@ -430,8 +502,13 @@ void launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
   if (n == 0) return;
   {
     const uint64_t blocks = (n + 1 + 255) / 256;
+    uint32_t *hist = ws.small_hist, *cursor = ws.small_hist + (kMaxKey + 1);
+    (void)hipMemsetAsync(hist, 0, (kMaxKey + 1) * sizeof(uint32_t), s);
     hipLaunchKernelGGL(b3_count_groups, dim3((unsigned)blocks), dim3(256), 0, s,
-                       chunks, n, D, ws.groups);
+                       chunks, n, D, ws.groups, hist);
+    hipLaunchKernelGGL(b3_small_offsets, dim3(1), dim3(64), 0, s, hist, cursor, ws.stats + 10);
+    hipLaunchKernelGGL(b3_small_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       chunks, n, D, cursor, ws.small);
   }
   launch_scan_u64(ws.groups, n, ws.scan_tmp, s);
   {

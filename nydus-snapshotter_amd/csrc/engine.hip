@@ -75,6 +75,9 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
     uint64_t cn = n + 1 < 4096 ? 4096 : n + 1;
     uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
     if (grow(e, &ws.chunk_layer, c4, cn)) return NGPU_ENOMEM;
+    uint64_t c5 = 0, c6 = 0;
+    if (grow(e, &ws.small, c5, cn)) return NGPU_ENOMEM;
+    if (!ws.small_hist && grow(e, &ws.small_hist, c6, 1024)) return NGPU_ENOMEM;
     if (grow(e, &ws.groups, c0, cn)) return NGPU_ENOMEM;
     if (grow(e, &ws.newflag, c1, cn)) return NGPU_ENOMEM;
     if (grow(e, &ws.uoff, c2, cn)) return NGPU_ENOMEM;
@@ -279,7 +282,7 @@ void ngpu_destroy(ngpu_engine *e) {
   Workspace &ws = e->ws;
   void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.scan_tmp,
                   ws.intra, ws.blob_first, ws.blob_real, ws.stats, ws.chunk_layer,
-                  ws.lfirst1, ws.lstats,
+                  ws.lfirst1, ws.lstats, ws.small, ws.small_hist,
                   e->d_data, e->d_chunks, e->d_results};
   for (void *p : bufs)
     if (p) (void)hipFree(p);

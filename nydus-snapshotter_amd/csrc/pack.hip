@@ -349,7 +349,9 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
     for (uint64_t i = 0; i < c; ++i) ho[i] = doff[a + i];
     memcpy(hl, &len[a], c * 4);
     uint64_t *ds = (uint64_t *)ddesc[b];
-    HIP_TRY(e, hipMemcpyAsync(ds, hs, desc_bytes, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(ds, hs, c * 8, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(ds + maxk, ho, c * 8, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(ds + 2 * maxk, hl, c * 4, hipMemcpyHostToDevice, e->stream));
     const unsigned grid = (unsigned)(c < 2048 ? c : 2048);
     hipLaunchKernelGGL(gather_chunks, dim3(grid), dim3(256), 0, e->stream, ds, (uint32_t *)(ds + 2 * maxk),
                        ds + maxk, c, dwin[b]);

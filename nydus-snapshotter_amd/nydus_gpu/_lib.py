@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libnydusgpu.so")
+# NYDUS_GPU_LIB: an alternative build of the same library (A/B benchmarking)
+LIB_PATH = os.environ.get("NYDUS_GPU_LIB") or os.path.join(PKG_DIR, "libnydusgpu.so")
 
 DIGESTERS = {"blake3": 0, "sha256": 1}
 KIND_NAMES = {0: "NEW", 1: "INTRA", 2: "DICT"}
