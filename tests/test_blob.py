@@ -356,3 +356,38 @@ def test_reader_mutation_fuzz_asan(oracle, tars, tmp_path):
             else:
                 seen["both_fail"] += 1
     assert seen["ok"] > 500 and seen["both_fail"] > 100, seen
+
+
+def test_inspect_canonical_dump(oracle, tars, tmp_path):
+    """nydus_gpu.inspect: the inspect-equivalent comparison form (chunk table
+    as a set keyed by digest, blob indices replaced by blob ids) of a
+    bootstrap or of a whole Pack stream."""
+    from nydus_gpu import inspect as ni
+    stream, info, ch, res, st = cpu_stream(oracle, tars["oci_upper"], 0x100000, "zstd")
+    boot, _ = blob_ref.unpack_entry(stream, blob_ref.ENTRY_BOOTSTRAP)
+    a = ni.canonical(ni.load_bootstrap(stream))
+    b = ni.canonical(ni.load_bootstrap(boot))
+    assert a == b and len(a["chunks"]) == info["blob_chunks"]
+    assert a["blobs"] == [info["blob_digest"]]
+    keys = [(r["digest"], r["blob_id"], r["index"]) for r in a["chunks"]]
+    assert keys == sorted(keys)
+    # table order does not matter; a changed record does
+    t = rafs.read_v6(boot)
+    shuffled = rafs.write_v6_bootstrap(t["chunks"][::-1].copy(), t["chunk_size"], flags=t["flags"],
+                                       blobs=t["blobs"])
+    assert ni.canonical(ni.load_bootstrap(shuffled)) == a
+    recs = t["chunks"].copy()
+    recs["uncompressed_size"][0] += 1
+    changed = rafs.write_v6_bootstrap(recs, t["chunk_size"], flags=t["flags"], blobs=t["blobs"])
+    paths = []
+    for name, data in (("stream", stream), ("shuffled", shuffled), ("changed", changed)):
+        p = tmp_path / name
+        p.write_bytes(data)
+        paths.append(str(p))
+    assert ni.main(["--diff", paths[0], paths[1]]) == 0
+    assert ni.main(["--diff", paths[0], paths[2]]) == 1
+    # the reference fixture
+    fx = ni.canonical(rafs.read_v6_from_targz(os.path.join(GOLDEN, "v6-bootstrap-chunk-pos-438272.tar.gz")))
+    assert len(fx["chunks"]) == 2515 and fx["chunk_size"] == 0x100000 and len(fx["blobs"]) == 1
+    with pytest.raises(ValueError):
+        ni.load_bootstrap(b"\0" * 4096)

@@ -785,3 +785,42 @@ def test_engine_thread_safety(oracle):
     [t.join() for t in ts]
     eng.close()
     assert not errs
+
+
+@pytest.mark.parametrize("chunk_size,median,files", [(0x100000, 4096, 4000), (0x10000, 16384, 1200),
+                                                     (0x100000, 1500, 4000)])
+def test_small_file_mix_vs_oracle(engines, oracle, chunk_size, median, files):
+    """Log-normal file sizes (most files a few KiB, a long tail): single-group
+    chunks go through the block-count-sorted lane path of b3_groups, the rest
+    through the chunk-ordered groups; every lanes-per-thread setting must give
+    the oracle's digests and decisions."""
+    rng = np.random.default_rng(median)
+    sizes = np.minimum(8 << 20, np.maximum(1, rng.lognormal(np.log(median), 1.6, files))).astype(np.int64)
+    stride = 512 + (sizes + 511) // 512 * 512
+    starts = np.concatenate([[0], np.cumsum(stride)[:-1]]) + 512
+    total = int(stride.sum()) + 1024
+    data = bytearray(rng.integers(0, 256, total, dtype=np.uint8).tobytes())
+    for i in range(7, len(sizes), 9):  # whole-file duplicates -> INTRA chunks
+        j = i - 5
+        if sizes[j] == sizes[i]:
+            continue
+        sizes[i] = sizes[j]
+        data[starts[i]:starts[i] + sizes[i]] = data[starts[j]:starts[j] + sizes[j]]
+    per = (sizes + chunk_size - 1) // chunk_size
+    n = int(per.sum())
+    ch = np.zeros(n, nydus_gpu.CHUNK_DTYPE)
+    fi = np.repeat(np.arange(len(sizes)), per)
+    k = np.arange(n) - np.repeat(np.cumsum(per) - per, per)
+    ch["offset"] = starts[fi] + k * chunk_size
+    ch["length"] = np.minimum(chunk_size, sizes[fi] - k * chunk_size)
+    ch["file_index"] = fi
+    ch["file_offset"] = k * chunk_size
+    data = bytes(data)
+    dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    dec, _ = oracle.dedup(dig, ch["length"])
+    assert (dec["kind"] == 1).sum() > 0
+    for lanes in LANES:
+        out, st = engines("blake3", chunk_size, lanes).process(data, ch)
+        assert np.array_equal(out["digest"], dig), lanes
+        for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+            assert np.array_equal(out[f], dec[f]), (lanes, f)
