@@ -312,7 +312,8 @@ __global__ __launch_bounds__(256) void b3_groups(
     const uint64_t *__restrict__ gbase, const uint32_t *__restrict__ gchunk,
     uint64_t cap_g, uint32_t *__restrict__ cv_out,
     ngpu_result *__restrict__ out, uint64_t *__restrict__ err,
-    const uint32_t *__restrict__ small, const uint64_t *__restrict__ nsmall) {
+    const uint32_t *__restrict__ small, const uint64_t *__restrict__ nsmall,
+    uint32_t *__restrict__ tree_list) {
   __shared__ uint32_t lcv[256 * 8];
   // groups [0, gm): multi-group chunks in chunk order; [gm, gm + ns): the
   // single-group chunks, largest first
@@ -346,7 +347,10 @@ __global__ __launch_bounds__(256) void b3_groups(
   // Others publish their group CV for b3_tree.
   const bool inwg = st == 2 && tree_in_workgroup(base, ng);
   if (st == 2 && !inwg) {
-    if (j == 0) err[2] = 1;  // err + 2 == stats[9]: some chunk needs b3_tree
+    if (j == 0) {  // err + 2 == stats[9]: chunks queued for b3_tree
+      const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long *>(err + 2), 1ull);
+      tree_list[q] = c;
+    }
     uint4 *d = reinterpret_cast<uint4 *>(cv_out + g * 8);
     d[0] = make_uint4(cur[0], cur[1], cur[2], cur[3]);
     d[1] = make_uint4(cur[4], cur[5], cur[6], cur[7]);
@@ -395,13 +399,14 @@ constexpr int kTreeThreads = 256;
 constexpr int kTile = 1024;  // CVs per LDS tile (32 KiB)
 
 __global__ __launch_bounds__(kTreeThreads) void b3_tree(
-    const uint64_t *__restrict__ gbase, uint64_t n, uint64_t cap_g,
-    uint32_t *__restrict__ cv, ngpu_result *__restrict__ out,
-    const uint64_t *__restrict__ needed) {
+    const uint64_t *__restrict__ gbase, const uint32_t *__restrict__ tree_list,
+    const uint64_t *__restrict__ queued, uint64_t cap_g,
+    uint32_t *__restrict__ cv, ngpu_result *__restrict__ out) {
   __shared__ uint32_t t[kTile * 8];
   const int tid = threadIdx.x;
-  if (*needed == 0) return;  // every chunk was finished inside b3_groups
-  for (uint64_t c = blockIdx.x; c < n; c += gridDim.x) {
+  const uint64_t nq = *queued;  // 0: every chunk was finished inside b3_groups
+  for (uint64_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+    const uint32_t c = tree_list[qi];
     const uint64_t base = gbase[c];
     uint64_t k = gbase[c + 1] - base;
     if (k <= 1 || base + k > cap_g || tree_in_workgroup(base, k)) continue;
@@ -475,7 +480,7 @@ static void launch_groups_lm(const uint8_t *data, uint64_t data_len,
   const uint64_t blocks = (ws.cap_g + 255) / 256;
   hipLaunchKernelGGL((b3_groups<D, LM>), dim3((unsigned)blocks), dim3(256), 0, s, data,
                      data_len, chunks, n, ws.groups, ws.group_chunk, ws.cap_g,
-                     ws.cv, out, ws.stats + 7, ws.small, ws.stats + 10);
+                     ws.cv, out, ws.stats + 7, ws.small, ws.stats + 10, ws.tree_list);
 }
 
 template <int D>
@@ -529,7 +534,7 @@ void launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
   {
     uint64_t blocks = n < 2048 ? n : 2048;
     hipLaunchKernelGGL(b3_tree, dim3((unsigned)blocks), dim3(kTreeThreads), 0, s,
-                       ws.groups, n, ws.cap_g, ws.cv, out, ws.stats + 9);
+                       ws.groups, ws.tree_list, ws.stats + 9, ws.cap_g, ws.cv, out);
   }
 }
 

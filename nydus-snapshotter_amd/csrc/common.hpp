@@ -84,6 +84,7 @@ struct Workspace {
   uint32_t *cv = nullptr;         // G_max x 8 words: subtree chaining values
   uint32_t *small = nullptr;      // n: single-group chunks sorted by work (blake3.hip)
   uint32_t *small_hist = nullptr; // 2 x (16*16 + 1): block-count histogram + cursors
+  uint32_t *tree_list = nullptr;  // n: chunks whose groups straddle a workgroup window
   uint64_t *newflag = nullptr;    // n+1: NEW flag -> scan = NEW index
   uint64_t *uoff = nullptr;       // n+1: aligned NEW size -> scan = offset
   uint64_t *scan_tmp = nullptr;

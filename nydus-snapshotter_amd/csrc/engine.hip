@@ -77,6 +77,8 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
     if (grow(e, &ws.chunk_layer, c4, cn)) return NGPU_ENOMEM;
     uint64_t c5 = 0, c6 = 0;
     if (grow(e, &ws.small, c5, cn)) return NGPU_ENOMEM;
+    uint64_t c7 = 0;
+    if (grow(e, &ws.tree_list, c7, cn)) return NGPU_ENOMEM;
     if (!ws.small_hist && grow(e, &ws.small_hist, c6, 1024)) return NGPU_ENOMEM;
     if (grow(e, &ws.groups, c0, cn)) return NGPU_ENOMEM;
     if (grow(e, &ws.newflag, c1, cn)) return NGPU_ENOMEM;
@@ -282,7 +284,7 @@ void ngpu_destroy(ngpu_engine *e) {
   Workspace &ws = e->ws;
   void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.scan_tmp,
                   ws.intra, ws.blob_first, ws.blob_real, ws.stats, ws.chunk_layer,
-                  ws.lfirst1, ws.lstats, ws.small, ws.small_hist,
+                  ws.lfirst1, ws.lstats, ws.small, ws.small_hist, ws.tree_list,
                   e->d_data, e->d_chunks, e->d_results};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
