@@ -87,11 +87,14 @@ __device__ __forceinline__ void set_iv(uint32_t cv[8]) {
 }
 
 // Load one message block of `nbytes` (<= 64) little-endian, zero padded.
-// NT: non-temporal (read-once streaming) loads.
+// NT: non-temporal (read-once streaming) loads.  A partial block (a chunk's
+// tail) still takes the 16-B vector path when the 64 bytes lie inside the
+// caller's buffer (`end`): the bytes past the chunk are loaded and masked off,
+// so lanes at their tail do not diverge into 64 byte loads.
 template <bool NT>
-__device__ __forceinline__ void load_block(const uint8_t *p, uint32_t nbytes,
+__device__ __forceinline__ void load_block(const uint8_t *p, uint32_t nbytes, const uint8_t *end,
                                            uint32_t m[16]) {
-  if (nbytes == 64 && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
+  if (((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (nbytes == 64 || p + 64 <= end)) {
     u32x4 a, b, c, d;
     if (NT) {
       a = load_nt16(p); b = load_nt16(p + 16); c = load_nt16(p + 32); d = load_nt16(p + 48);
@@ -103,10 +106,17 @@ __device__ __forceinline__ void load_block(const uint8_t *p, uint32_t nbytes,
     m[4] = b.x; m[5] = b.y; m[6] = b.z; m[7] = b.w;
     m[8] = c.x; m[9] = c.y; m[10] = c.z; m[11] = c.w;
     m[12] = d.x; m[13] = d.y; m[14] = d.z; m[15] = d.w;
+    if (nbytes < 64) {
+#pragma unroll
+      for (int w = 0; w < 16; ++w) {
+        const int v = (int)nbytes - 4 * w;  // valid bytes of word w
+        m[w] = v >= 4 ? m[w] : v <= 0 ? 0u : m[w] & ((1u << (8 * v)) - 1u);
+      }
+    }
     return;
   }
-  // Tail / unaligned path: byte loads of the valid bytes only (never reads
-  // past the chunk, so never past the end of the caller's buffer).
+  // Unaligned, or the last bytes of the buffer: byte loads of the valid bytes
+  // only (never reads past the chunk, so never past the caller's buffer).
 #pragma unroll
   for (int w = 0; w < 16; ++w) {
     uint32_t x = 0;
@@ -242,7 +252,8 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
   const uint32_t gend = min(len, (first + cnt) * kLeaf);
   uint32_t pos = first * kLeaf;
   uint32_t m[16];
-  if (PF) load_block<NT>(src + pos, min(64u, gend - pos), m);
+  const uint8_t *end = data + data_len;
+  if (PF) load_block<NT>(src + pos, min(64u, gend - pos), end, m);
 
   uint32_t stk[SD][8];
   uint32_t depth = 0;
@@ -264,13 +275,13 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
       } else if (PF) {
         uint32_t nx[16];
         const uint32_t np = pos + 64;
-        if (np < gend) load_block<NT>(src + np, min(64u, gend - np), nx);
+        if (np < gend) load_block<NT>(src + np, min(64u, gend - np), end, nx);
         compress(cur, m, leaf, bl, flags);
 #pragma unroll
         for (int i = 0; i < 16; ++i) m[i] = nx[i];
         pos = np;
       } else {
-        load_block<NT>(src + off + (b << 6), bl, m);
+        load_block<NT>(src + off + (b << 6), bl, end, m);
         compress(cur, m, leaf, bl, flags);
       }
     }

@@ -4,12 +4,14 @@ opposed to bench.py's uniform 4 MiB files.  Shows how lane imbalance inside a
 wave (a small chunk next to a full 8-KiB leaf group) costs throughput.
 python tools/mixed_sizes.py [total_GiB] [median_KiB] [chunk_size]"""
 import json
+import os
 import sys
 
 import numpy as np
 import torch
 
-sys.path.insert(0, "nydus-snapshotter_amd")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "nydus-snapshotter_amd"))
 import nydus_gpu  # noqa: E402
 
 
