@@ -45,22 +45,48 @@ constexpr Sched make_sched() {
 }
 constexpr Sched kSched = make_sched();
 
-#define B3_G(a, b, c, d, x, y)       \
-  do {                               \
-    a = a + b + (x);                 \
-    d = rotr32(d ^ a, 16);           \
-    c = c + d;                       \
-    b = rotr32(b ^ c, 12);           \
-    a = a + b + (y);                 \
-    d = rotr32(d ^ a, 8);            \
-    c = c + d;                       \
-    b = rotr32(b ^ c, 7);            \
+// In-place compression: cv <- first 8 output words.
+//
+// The VALU issue order is fixed by hand (inline asm, one op per statement;
+// volatile statements keep their order): the 4 independent G of a column /
+// diagonal step advance in lockstep, so the 2-cycle ops (v_xor, v_add) issue
+// in runs of 4 and 8 between runs of 4-cycle ops (v_add3, v_alignbit).  The
+// compiler's own schedule of the same G macro alternates them one by one and
+// is 6 % slower on the box (5.89 -> 5.52 ms per 16 GiB C2 launch,
+// profiles/r1/ab_issue_order.jsonl); SDWA rotr16 and split v_add3 were
+// measured there too and lose, and two leaves per lane in lockstep (runs of
+// 8, 108 VGPRs) gain nothing over runs of 4.
+#define B3_OP3(op, a, b, x) asm volatile(op " %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(x))
+#define B3_OP2(op, a, b) asm volatile(op " %0, %0, %1" : "+v"(a) : "v"(b))
+#define B3_ROT(a, n) asm volatile("v_alignbit_b32 %0, %0, %0, " #n : "+v"(a))
+// One column or diagonal step (4 G in lockstep).
+#define B3_G4(a0, b0, c0, d0, a1, b1, c1, d1, a2, b2, c2, d2, a3, b3, c3, d3, x0, x1, x2, x3, \
+              y0, y1, y2, y3)                                                               \
+  do {                                                                                      \
+    B3_OP3("v_add3_u32", a0, b0, x0); B3_OP3("v_add3_u32", a1, b1, x1);                    \
+    B3_OP3("v_add3_u32", a2, b2, x2); B3_OP3("v_add3_u32", a3, b3, x3);                    \
+    B3_OP2("v_xor_b32", d0, a0); B3_OP2("v_xor_b32", d1, a1);                              \
+    B3_OP2("v_xor_b32", d2, a2); B3_OP2("v_xor_b32", d3, a3);                              \
+    B3_ROT(d0, 16); B3_ROT(d1, 16); B3_ROT(d2, 16); B3_ROT(d3, 16);                         \
+    B3_OP2("v_add_u32", c0, d0); B3_OP2("v_add_u32", c1, d1);                              \
+    B3_OP2("v_add_u32", c2, d2); B3_OP2("v_add_u32", c3, d3);                              \
+    B3_OP2("v_xor_b32", b0, c0); B3_OP2("v_xor_b32", b1, c1);                              \
+    B3_OP2("v_xor_b32", b2, c2); B3_OP2("v_xor_b32", b3, c3);                              \
+    B3_ROT(b0, 12); B3_ROT(b1, 12); B3_ROT(b2, 12); B3_ROT(b3, 12);                         \
+    B3_OP3("v_add3_u32", a0, b0, y0); B3_OP3("v_add3_u32", a1, b1, y1);                    \
+    B3_OP3("v_add3_u32", a2, b2, y2); B3_OP3("v_add3_u32", a3, b3, y3);                    \
+    B3_OP2("v_xor_b32", d0, a0); B3_OP2("v_xor_b32", d1, a1);                              \
+    B3_OP2("v_xor_b32", d2, a2); B3_OP2("v_xor_b32", d3, a3);                              \
+    B3_ROT(d0, 8); B3_ROT(d1, 8); B3_ROT(d2, 8); B3_ROT(d3, 8);                             \
+    B3_OP2("v_add_u32", c0, d0); B3_OP2("v_add_u32", c1, d1);                              \
+    B3_OP2("v_add_u32", c2, d2); B3_OP2("v_add_u32", c3, d3);                              \
+    B3_OP2("v_xor_b32", b0, c0); B3_OP2("v_xor_b32", b1, c1);                              \
+    B3_OP2("v_xor_b32", b2, c2); B3_OP2("v_xor_b32", b3, c3);                              \
+    B3_ROT(b0, 7); B3_ROT(b1, 7); B3_ROT(b2, 7); B3_ROT(b3, 7);                             \
   } while (0)
 
-// In-place compression: cv <- first 8 output words.
 __device__ __forceinline__ void compress(uint32_t cv[8], const uint32_t m[16],
-                                         uint32_t counter, uint32_t blen,
-                                         uint32_t flags) {
+                                         uint32_t counter, uint32_t blen, uint32_t flags) {
   uint32_t v0 = cv[0], v1 = cv[1], v2 = cv[2], v3 = cv[3];
   uint32_t v4 = cv[4], v5 = cv[5], v6 = cv[6], v7 = cv[7];
   uint32_t v8 = IV0, v9 = IV1, v10 = IV2, v11 = IV3;
@@ -68,14 +94,10 @@ __device__ __forceinline__ void compress(uint32_t cv[8], const uint32_t m[16],
 #pragma unroll
   for (int r = 0; r < 7; ++r) {
     const uint8_t *s = kSched.s[r];
-    B3_G(v0, v4, v8, v12, m[s[0]], m[s[1]]);
-    B3_G(v1, v5, v9, v13, m[s[2]], m[s[3]]);
-    B3_G(v2, v6, v10, v14, m[s[4]], m[s[5]]);
-    B3_G(v3, v7, v11, v15, m[s[6]], m[s[7]]);
-    B3_G(v0, v5, v10, v15, m[s[8]], m[s[9]]);
-    B3_G(v1, v6, v11, v12, m[s[10]], m[s[11]]);
-    B3_G(v2, v7, v8, v13, m[s[12]], m[s[13]]);
-    B3_G(v3, v4, v9, v14, m[s[14]], m[s[15]]);
+    B3_G4(v0, v4, v8, v12, v1, v5, v9, v13, v2, v6, v10, v14, v3, v7, v11, v15,
+          m[s[0]], m[s[2]], m[s[4]], m[s[6]], m[s[1]], m[s[3]], m[s[5]], m[s[7]]);
+    B3_G4(v0, v5, v10, v15, v1, v6, v11, v12, v2, v7, v8, v13, v3, v4, v9, v14,
+          m[s[8]], m[s[10]], m[s[12]], m[s[14]], m[s[9]], m[s[11]], m[s[13]], m[s[15]]);
   }
   cv[0] = v0 ^ v8;  cv[1] = v1 ^ v9;  cv[2] = v2 ^ v10; cv[3] = v3 ^ v11;
   cv[4] = v4 ^ v12; cv[5] = v5 ^ v13; cv[6] = v6 ^ v14; cv[7] = v7 ^ v15;
@@ -257,6 +279,34 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
 
   uint32_t stk[SD][8];
   uint32_t depth = 0;
+  // Leaf k's CV is in cur: merge the complete subtrees it closes (eagerly,
+  // through the D-deep stack), then push it unless it is the group's last.
+  auto finish = [&](uint32_t k) {
+    const bool last = (k + 1 == cnt);
+    const uint32_t nm = last ? depth : (uint32_t)__builtin_ctz(k + 1);
+    for (uint32_t q = 0; q < nm; ++q) {
+      uint32_t pm[16];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { pm[i] = stk[0][i]; pm[8 + i] = cur[i]; }
+      const uint32_t flags = PARENT | ((last && root_group && q + 1 == nm) ? ROOT : 0);
+      set_iv(cur);
+      compress(cur, pm, 0, 64, flags);
+#pragma unroll
+      for (int l = 0; l + 1 < SD; ++l)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) stk[l][i] = stk[l + 1][i];
+      --depth;
+    }
+    if (!last) {
+#pragma unroll
+      for (int l = SD - 1; l > 0; --l)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) stk[l][i] = stk[l - 1][i];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) stk[0][i] = cur[i];
+      ++depth;
+    }
+  };
   for (uint32_t k = 0; k < cnt; ++k) {
     const uint32_t leaf = first + k;
     const uint32_t off = leaf * kLeaf;
@@ -285,33 +335,7 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
         compress(cur, m, leaf, bl, flags);
       }
     }
-    if (D > 0) {
-      const bool last = (k + 1 == cnt);
-      const uint32_t nm = last ? depth : (uint32_t)__builtin_ctz(k + 1);
-      for (uint32_t q = 0; q < nm; ++q) {
-        uint32_t pm[16];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) { pm[i] = stk[0][i]; pm[8 + i] = cur[i]; }
-        const uint32_t flags =
-            PARENT | ((last && root_group && q + 1 == nm) ? ROOT : 0);
-        set_iv(cur);
-        compress(cur, pm, 0, 64, flags);
-#pragma unroll
-        for (int l = 0; l + 1 < SD; ++l)
-#pragma unroll
-          for (int i = 0; i < 8; ++i) stk[l][i] = stk[l + 1][i];
-        --depth;
-      }
-      if (!last) {
-#pragma unroll
-        for (int l = SD - 1; l > 0; --l)
-#pragma unroll
-          for (int i = 0; i < 8; ++i) stk[l][i] = stk[l - 1][i];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) stk[0][i] = cur[i];
-        ++depth;
-      }
-    }
+    if (D > 0) finish(k);
   }
   return root_group ? 1 : 2;
 }
