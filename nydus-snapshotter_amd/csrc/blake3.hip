@@ -248,7 +248,8 @@ __global__ void b3_fill_group_chunk(const uint64_t *__restrict__ gbase,
 
 // LM (load mode): bit0 = non-temporal loads, bit1 = prefetch the next 64-B
 // block of the lane's byte stream while the current one is compressed,
-// 4 = diagnostic: no global loads at all (wrong digests; VALU ceiling only).
+// 4 = diagnostic: no global loads at all (wrong digests; VALU ceiling only),
+// 5 = plain loads without the whole-leaf fast path (A/B reference).
 //
 // Hashes leaf group j of chunk c (ng groups).  Returns 0 (no work), 1 (cur =
 // root digest: the chunk fits this group) or 2 (cur = the group's subtree CV).
@@ -269,7 +270,8 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
   const uint32_t cnt = min(1u << D, nleaves - first);
   const bool root_group = (ng == 1);
   const uint8_t *src = data + ch.offset;
-  constexpr bool NT = (LM & 1) != 0, PF = (LM & 2) != 0, NOLOAD = LM == 4;
+  constexpr bool NT = LM < 4 && (LM & 1) != 0, PF = LM < 4 && (LM & 2) != 0;
+  constexpr bool NOLOAD = LM == 4, FAST = LM == 0;
   // The lane's bytes [pos, gend) are one contiguous stream of 64-B blocks.
   const uint32_t gend = min(len, (first + cnt) * kLeaf);
   uint32_t pos = first * kLeaf;
@@ -313,6 +315,27 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
     const uint32_t llen = min(kLeaf, len - off);
     const uint32_t nb = llen == 0 ? 1 : (llen + 63) >> 6;
     set_iv(cur);
+    if (FAST && __all(llen == kLeaf && (reinterpret_cast<uintptr_t>(src + off) & 15) == 0)) {
+      // Every active lane of the wave has a whole, aligned leaf: 16 blocks of
+      // plain 16-B loads, no per-block length / alignment / bounds checks.
+      // (Wave-uniform: a wave mixing whole and partial leaves would run both
+      // loops, each with its compression, one after the other.)
+      const u32x4 *q = reinterpret_cast<const u32x4 *>(src + off);
+      const uint32_t fl_end = CHUNK_END | ((root_group && nleaves == 1) ? ROOT : 0);
+      // unrolled by 2: keeps this loop's compressions a separate copy (the
+      // compiler otherwise merges them with the general loop's)
+#pragma unroll 2
+      for (uint32_t b = 0; b < 16; ++b, q += 4) {
+        const u32x4 x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+        m[0] = x0.x; m[1] = x0.y; m[2] = x0.z; m[3] = x0.w;
+        m[4] = x1.x; m[5] = x1.y; m[6] = x1.z; m[7] = x1.w;
+        m[8] = x2.x; m[9] = x2.y; m[10] = x2.z; m[11] = x2.w;
+        m[12] = x3.x; m[13] = x3.y; m[14] = x3.z; m[15] = x3.w;
+        compress(cur, m, leaf, 64, b == 0 ? CHUNK_START : b == 15 ? fl_end : 0u);
+      }
+      if (D > 0) finish(k);
+      continue;
+    }
     for (uint32_t b = 0; b < nb; ++b) {
       const uint32_t bl = min(64u, llen - (b << 6));
       uint32_t flags = (b == 0 ? CHUNK_START : 0) | (b + 1 == nb ? CHUNK_END : 0);
@@ -527,6 +550,7 @@ static void launch_groups(const uint8_t *data, uint64_t data_len,
     case 1: launch_groups_lm<D, 1>(data, data_len, chunks, n, ws, out, s); break;
     case 2: launch_groups_lm<D, 2>(data, data_len, chunks, n, ws, out, s); break;
     case 3: launch_groups_lm<D, 3>(data, data_len, chunks, n, ws, out, s); break;
+    case 5: launch_groups_lm<D, 5>(data, data_len, chunks, n, ws, out, s); break;
     default: launch_groups_lm<D, 4>(data, data_len, chunks, n, ws, out, s); break;
   }
 }

@@ -52,21 +52,33 @@ def main():
     res = {"files": len(sizes), "chunks": n, "file_bytes": fb, "chunk_size": chunk,
            "median_file": int(np.median(sizes)), "mean_file": int(sizes.mean()),
            "frac_bytes_in_files_lt_64k": round(float(sizes[sizes < 65536].sum() / sizes.sum()), 4)}
-    for lanes in (0, 1, 2, 4, 8):
-        eng = nydus_gpu.Engine(chunk_size=chunk, leaves_per_lane=lanes, timing=True)
-        ts = []
-        for r in range(6):
+    # argv[4]: comma list of b3_groups load modes to A/B (interleaved rounds,
+    # auto leaves-per-lane only); default: mode 0 over the leaves-per-lane sweep
+    modes = [int(x) for x in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0]
+    cases = [(lanes, 0) for lanes in (0, 1, 2, 4, 8)] if modes == [0] else [(0, m) for m in modes]
+    engines = {c: nydus_gpu.Engine(chunk_size=chunk, leaves_per_lane=c[0], timing=True,
+                                   flags=(1 + c[1]) << 8 if c[1] else 0) for c in cases}
+    ts = {c: [] for c in cases}
+    ref = None
+    for r in range(6):
+        for c, eng in engines.items():
             eng.process_device(buf.data_ptr(), nbytes, d_ch.data_ptr(), n, d_out.data_ptr())
-            t = eng.last_timing()
             if r:
-                ts.append(t)
-        torch.cuda.synchronize()
-        tot = float(np.median([t["total_ms"] for t in ts]))
-        dig = float(np.median([t["digest_ms"] for t in ts]))
-        res[f"lanes{lanes}"] = {"total_ms": round(tot, 3), "digest_ms": round(dig, 3),
-                                "tree_ms": round(float(np.median([t["tree_ms"] for t in ts])), 3),
-                                "dedup_ms": round(float(np.median([t["dedup_ms"] for t in ts])), 3),
-                                "GBps": round(fb / tot / 1e6, 1), "D": ts[-1]["group_log2"]}
+                ts[c].append(eng.last_timing())
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = d_out.clone()
+            else:
+                assert torch.equal(ref, d_out), f"case {c} differs"
+    for (lanes, mode), tl in ts.items():
+        tot = float(np.median([t["total_ms"] for t in tl]))
+        dig = float(np.median([t["digest_ms"] for t in tl]))
+        key = f"lanes{lanes}" + (f"_m{mode}" if mode else "")
+        res[key] = {"total_ms": round(tot, 3), "digest_ms": round(dig, 3),
+                    "tree_ms": round(float(np.median([t["tree_ms"] for t in tl])), 3),
+                    "dedup_ms": round(float(np.median([t["dedup_ms"] for t in tl])), 3),
+                    "GBps": round(fb / tot / 1e6, 1), "D": tl[-1]["group_log2"]}
+    for eng in engines.values():
         eng.close()
     print(json.dumps(res), flush=True)
 
