@@ -135,11 +135,20 @@ WORKLOADS = {
     "c3-blake3": dict(desc="C3 with blake3: 16 GiB layer, 1 MiB chunks, 200M-entry chunk dict",
                       n_files=4096, file_size=4 * MiB, chunk=MiB, digester="blake3", layers=1,
                       dict_entries=200_000_000, plant=0.3),
-    "c4": dict(desc="C4 per GPU: 16 x 1 GiB layers, 1 MiB chunks, blake3, 30% of chunks from a "
-                    "shared pool of 1024 contents; chunk dict (pool + 16M filler) partitioned by "
-                    "digest prefix over the GPUs, probes routed by all-to-all",
-               n_files=4096, file_size=4 * MiB, chunk=MiB, digester="blake3", layers=16,
-               pool=1024, dict_entries=16_000_000, sharded=True),
+    "c4": dict(desc="C4: 1 TiB registry corpus = 1024 layers x 1 GiB (256 x 4 MiB files), 1 MiB "
+                    "chunks, blake3, 30% of chunks drawn from a shared pool of 65536 contents "
+                    "(counter-hash PRNG keyed by content id); chunk dict = pool digests + 16M "
+                    "filler, partitioned by digest prefix over the GPUs, probes routed by "
+                    "all-to-all; layers round-robin over the GPUs (at most 128 per GPU: one "
+                    "GPU's share of the 8-GPU run)",
+               n_files=256, file_size=4 * MiB, chunk=MiB, digester="blake3",
+               layers_total=1024, max_layers_per_gpu=128, pool=65536,
+               dict_entries=16_000_000, sharded=True),
+    "c4-16": dict(desc="C4-shape per GPU: 16 x 1 GiB layers, 1 MiB chunks, blake3, 30% of chunks "
+                       "from a shared pool of 65536 contents; chunk dict (pool + 16M filler) "
+                       "partitioned by digest prefix over the GPUs, probes routed by all-to-all",
+                  n_files=4096, file_size=4 * MiB, chunk=MiB, digester="blake3", layers=16,
+                  pool=65536, dict_entries=16_000_000, sharded=True),
     "c5-1000": dict(desc="C5: 1000 layers x 64 MiB (16 x 4 MiB files), 64 KiB chunks, blake3, 30% of "
                          "chunks from a shared pool of 1024 contents; chunk dict (pool + 1M filler) "
                          "partitioned by digest prefix; layers split over the GPUs; one multi-layer "
@@ -153,25 +162,62 @@ WORKLOADS = {
 }
 
 
+def pool_content(torch, ids, S, device="cuda"):
+    """Pool contents for C4/C5: content i is a pure function of i (a splitmix64-
+    style counter hash of (i, word index)), so every rank regenerates the same
+    pool without holding it (65536 x 1 MiB would be 64 GiB)."""
+    w = torch.arange(S // 8, dtype=torch.int64, device=device)
+    z = (ids.to(torch.int64)[:, None] << 20) | w[None, :]
+    z = z * -7046029254386353131 + 0x632BE59BD9B4E019  # 0x9E3779B97F4A7C15 as int64
+    z = (z ^ ((z >> 30) & 0x3FFFFFFFF)) * -4658895280553007687  # 0xBF58476D1CE4E5B9
+    z = (z ^ ((z >> 27) & 0x1FFFFFFFFF)) * -7723592293110705685  # 0x94D049BB133111EB
+    z = z ^ ((z >> 31) & 0x1FFFFFFFF)
+    return z.view(torch.uint8).view(len(ids), S)
+
+
 def plant_pool(torch, buf, ch, stride, wl, seed):
-    """C4: copy pool contents (same seed on every rank) over ~30% of the chunks."""
+    """C4/C5: overwrite ~30% of the chunks with pool contents (rank-seeded
+    choice of chunks and of content ids)."""
     S = wl["chunk"]
     per_file = wl["file_size"] // S
-    g = torch.Generator(device="cuda").manual_seed(0x9001)
-    pool = torch.empty((wl["pool"], S), dtype=torch.uint8, device="cuda")
-    pool.random_(0, 256, generator=g)
     n = len(ch)
     rows = buf[: wl["n_files"] * stride].view(wl["n_files"], stride)[:, 512:].view(wl["n_files"], per_file, S)
     rng = np.random.default_rng(seed)
     sel = np.nonzero(rng.random(n) < 0.3)[0]
     src = rng.integers(0, wl["pool"], len(sel))
-    for a in range(0, len(sel), 256):
-        f = torch.from_numpy(sel[a:a + 256] // per_file).cuda()
-        k = torch.from_numpy(sel[a:a + 256] % per_file).cuda()
-        rows[f, k] = pool[torch.from_numpy(src[a:a + 256]).cuda()]
+    step = max(1, (256 * MiB) // S)
+    for a in range(0, len(sel), step):
+        f = torch.from_numpy(sel[a:a + step] // per_file).cuda()
+        k = torch.from_numpy(sel[a:a + step] % per_file).cuda()
+        rows[f, k] = pool_content(torch, torch.from_numpy(src[a:a + step]).cuda(), S)
     torch.cuda.synchronize()
-    del pool
     return None, len(sel)
+
+
+def pool_digests(torch, nydus_gpu, wl, device):
+    """Digests of all pool contents (they go into the chunk dict)."""
+    S, P = wl["chunk"], wl["pool"]
+    eng = nydus_gpu.Engine(device=device, digester=wl["digester"], chunk_size=S)
+    step = max(1, (512 * MiB) // S)
+    out = torch.empty((P, 32), dtype=torch.uint8, device="cuda")
+    pch = np.zeros(step, nydus_gpu.CHUNK_DTYPE)
+    pch["offset"] = np.arange(step, dtype=np.uint64) * S
+    pch["length"] = S
+    d_pch = torch.from_numpy(pch.view(np.uint8).copy()).cuda()
+    pout = torch.empty(step * 64, dtype=torch.uint8, device="cuda")
+    try:
+        for a in range(0, P, step):
+            b = min(P, a + step)
+            raw = pool_content(torch, torch.arange(a, b, device="cuda"), S).contiguous()
+            # stream-ordered after pool_content's kernels
+            eng.digest_device(raw.data_ptr(), raw.numel(), d_pch.data_ptr(), b - a, pout.data_ptr(),
+                              stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            out[a:b] = pout.view(-1, 64)[: b - a, :32]
+            del raw
+    finally:
+        eng.close()
+    return out
 
 
 def pmc_traffic(path, workload, kernel):
@@ -292,6 +338,8 @@ def main():
         wl["dict_entries"] = args.dict_entries
     if wl.get("layers_total"):  # split the layer set over the ranks
         mine = len(range(rank, wl["layers_total"], world))
+        if wl.get("max_layers_per_gpu") and mine > wl["max_layers_per_gpu"]:
+            mine = wl["max_layers_per_gpu"]  # HBM cap: one GPU's share of the 8-GPU run
         wl["layers"] = mine
         wl["n_files"] = wl["n_files"] * mine
     buf, ch = build_layer_on_gpu(torch, wl["n_files"], wl["file_size"], wl["chunk"], seed=0x6E79647573 + rank)
@@ -320,20 +368,8 @@ def main():
         dd = torch.empty((m, 32), dtype=torch.uint8, device="cuda")
         dd.random_(0, 256, generator=g)
         if wl.get("pool"):
-            pool_eng = nydus_gpu.Engine(device=local, digester=wl["digester"], chunk_size=wl["chunk"])
-            gpool = torch.Generator(device="cuda").manual_seed(0x9001)
-            praw = torch.empty((wl["pool"], wl["chunk"]), dtype=torch.uint8, device="cuda")
-            praw.random_(0, 256, generator=gpool)
-            pch = np.zeros(wl["pool"], nydus_gpu.CHUNK_DTYPE)
-            pch["offset"] = np.arange(wl["pool"], dtype=np.uint64) * wl["chunk"]
-            pch["length"] = wl["chunk"]
-            d_pch = torch.from_numpy(pch.view(np.uint8).copy()).cuda()
-            pout = torch.empty(wl["pool"] * 64, dtype=torch.uint8, device="cuda")
-            pool_eng.digest_device(praw.data_ptr(), praw.numel(), d_pch.data_ptr(), wl["pool"], pout.data_ptr())
-            torch.cuda.synchronize()
-            dd[: wl["pool"]] = pout.view(-1, 64)[:, :32]
-            del praw, pout
-            pool_eng.close()
+            assert m >= wl["pool"]
+            dd[: wl["pool"]] = pool_digests(torch, nydus_gpu, wl, local)
             expect_dict = planted
         else:
             eng.digest_device(buf.data_ptr(), buf.numel(), d_ch.data_ptr(), n, d_out.data_ptr())
@@ -491,7 +527,7 @@ def main():
         "data": "synthetic (random bytes generated on the GPU, real GNU tar headers)",
         "config": {"workload": wl["desc"], "name": args.workload,
                    "layer_bytes": int(buf.numel()), "file_bytes_per_gpu": file_bytes, "chunks": n,
-                   "chunk_size": wl["chunk"], "digester": wl["digester"],
+                   "chunk_size": wl["chunk"], "digester": wl["digester"], "layers_per_gpu": n_layers,
                    "leaves_per_lane": 1 << D, "parallelism": f"layer-sharded x{world}"},
         "stage_ms": {"digest": round(dig_ms, 3), "tree": round(tree_ms, 3), "dedup": round(dedup_ms, 3)},
         **extra,

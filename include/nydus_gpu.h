@@ -175,9 +175,13 @@ int ngpu_process(ngpu_engine *eng, const void *data, uint64_t len,
                  ngpu_layer_stats *stats);
 
 /* Device-resident variant: data, chunks and out are device pointers; work is
- * enqueued on `stream` (a hipStream_t, or NULL for the engine's stream) and
- * the call returns without synchronising.  stats may be NULL; if not NULL the
- * call synchronises the stream to fill it. */
+ * enqueued on `stream` (a hipStream_t; NULL = the null/default stream, as in
+ * HIP itself) and the call returns without synchronising, so it is stream-
+ * ordered after whatever the caller enqueued on the same stream to produce
+ * d_data / d_chunks.  stats may be NULL; if not NULL the call synchronises
+ * the stream to fill it.  The same holds for every *_device entry point
+ * below except ngpu_dict_load_device (synchronous: its inputs must be
+ * complete when it is called). */
 int ngpu_process_device(ngpu_engine *eng, const void *d_data, uint64_t len,
                         const ngpu_chunk *d_chunks, uint64_t n,
                         ngpu_result *d_out, void *stream,

@@ -391,6 +391,12 @@ int ngpu_dict_load_device(ngpu_engine *e, const uint8_t *d_digests, const uint32
   return 0;
 }
 
+// Device-pointer entry points run on the caller's stream.  NULL is the null
+// (default) stream, as everywhere in HIP — it used to mean the engine's own
+// non-blocking stream, which ran unordered with a caller (e.g. PyTorch on its
+// default stream, whose handle is 0) still producing the inputs.
+static inline hipStream_t dev_stream(void *s) { return (hipStream_t)s; }
+
 int ngpu_digest_device(ngpu_engine *e, const void *d_data, uint64_t len,
                        const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
                        void *stream) {
@@ -399,7 +405,7 @@ int ngpu_digest_device(ngpu_engine *e, const void *d_data, uint64_t len,
   std::lock_guard<std::mutex> g(e->mu);
   hipSetDevice(e->device);
   return enqueue_digest(e, (const uint8_t *)d_data, len, d_chunks, n, d_out,
-                        stream ? (hipStream_t)stream : e->stream);
+                        dev_stream(stream));
 }
 
 int ngpu_dict_probe_device(ngpu_engine *e, const uint8_t *d_digests, uint64_t stride,
@@ -409,7 +415,7 @@ int ngpu_dict_probe_device(ngpu_engine *e, const uint8_t *d_digests, uint64_t st
   std::lock_guard<std::mutex> g(e->mu);
   hipSetDevice(e->device);
   launch_dict_probe(d_digests, stride, n, e->dict, d_hits,
-                    stream ? (hipStream_t)stream : e->stream);
+                    dev_stream(stream));
   HIP_TRY(e, hipGetLastError());
   return 0;
 }
@@ -422,7 +428,7 @@ int ngpu_dedup_device(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n,
   if (d_hits && n_dict_blobs == 0) n_dict_blobs = e->dict.n_blobs ? e->dict.n_blobs : 1;
   std::lock_guard<std::mutex> g(e->mu);
   hipSetDevice(e->device);
-  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  hipStream_t s = dev_stream(stream);
   int rc = enqueue_dedup(e, d_chunks, n, d_out, d_hits, n_dict_blobs, s, nullptr, 1, nullptr);
   if (rc) return rc;
   if (stats) return read_stats(e, s, stats);
@@ -439,7 +445,7 @@ int ngpu_dedup_layers_device(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_
   std::lock_guard<std::mutex> g(e->mu);
   hipSetDevice(e->device);
   return enqueue_dedup(e, d_chunks, n, d_out, d_hits, n_dict_blobs,
-                       stream ? (hipStream_t)stream : e->stream, d_layer_first, n_layers,
+                       dev_stream(stream), d_layer_first, n_layers,
                        d_stats);
 }
 
@@ -452,7 +458,7 @@ int ngpu_process_layers_device(ngpu_engine *e, const void *d_data, uint64_t len,
   if (n >= 0xFFFFFFFFull || n_layers >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too large");
   std::lock_guard<std::mutex> g(e->mu);
   hipSetDevice(e->device);
-  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  hipStream_t s = dev_stream(stream);
   int rc = enqueue_digest(e, (const uint8_t *)d_data, len, d_chunks, n, d_out, s);
   if (rc) return rc;
   return enqueue_dedup(e, d_chunks, n, d_out, nullptr, 0, s, d_layer_first, n_layers, d_stats);
@@ -476,7 +482,7 @@ int ngpu_process_device(ngpu_engine *e, const void *d_data, uint64_t len,
   if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too many chunks in one call");
   std::lock_guard<std::mutex> g(e->mu);
   hipSetDevice(e->device);
-  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  hipStream_t s = dev_stream(stream);
   int rc = enqueue(e, (const uint8_t *)d_data, len, d_chunks, n, d_out, s);
   if (rc) return rc;
   if (stats) return read_stats(e, s, stats);

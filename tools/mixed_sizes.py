@@ -45,6 +45,7 @@ def main():
     nbytes, ch, sizes = layout(total, median, chunk)
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     buf.random_(0, 256)
+    torch.cuda.synchronize()
     n = len(ch)
     d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
     d_out = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
