@@ -222,12 +222,17 @@ def pool_digests(torch, nydus_gpu, wl, device):
 
 def pmc_traffic(path, workload, kernel):
     """HBM bytes per launch of the dominant kernel from a committed rocprofv3
-    PMC summary of the same bench command (scripts/gpu_pmc.sh ->
-    scripts/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected)."""
+    PMC summary of the same bench command.  Preferred: pmc_req_<workload>.json
+    (scripts/gpu_pmc_req.sh: L2->fabric read requests by size x bytes +
+    WRITE_SIZE, exact); else pmc_<workload>.json (scripts/gpu_pmc.sh:
+    FETCH_SIZE x2 + WRITE_SIZE, the gfx950 rule for 128-B requests)."""
     import glob
     if not path:
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{workload}.json")))
-        path = cands[-1] if cands else ""
+        for name in (f"pmc_req_{workload}.json", f"pmc_{workload}.json"):
+            cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)))
+            path = cands[-1] if cands else ""
+            if path:
+                break
     if not path or not os.path.exists(path):
         return None, None
     d = json.load(open(path))

@@ -85,14 +85,65 @@ constexpr Sched kSched = make_sched();
     B3_ROT(b0, 7); B3_ROT(b1, 7); B3_ROT(b2, 7); B3_ROT(b3, 7);                             \
   } while (0)
 
+// The first column step with the constant row folded in: v8..v11 = IV0..IV3
+// enter as VOP2 literals of the c += d adds, v12 / v14 / v15 (counter, block
+// length, flags) as sources of 3-operand xors, and v13 = 0 drops its xor.
+// Saves the 8 register copies and 1 xor per compression that initialising
+// v8..v15 in place costs.
+#define B3_XORTO(o, x, y) asm volatile("v_xor_b32 %0, %1, %2" : "=v"(o) : "v"(x), "v"(y))
+#define B3_ADDLIT(o, k, y) asm volatile("v_add_u32 %0, %1, %2" : "=v"(o) : "i"(k), "v"(y))
+#define B3_G4_FIRST(x0, x1, x2, x3, y0, y1, y2, y3)                                      \
+  do {                                                                                  \
+    B3_OP3("v_add3_u32", v0, v4, x0); B3_OP3("v_add3_u32", v1, v5, x1);                \
+    B3_OP3("v_add3_u32", v2, v6, x2); B3_OP3("v_add3_u32", v3, v7, x3);                \
+    B3_XORTO(v12, counter, v0); B3_XORTO(v14, blen, v2); B3_XORTO(v15, flags, v3);     \
+    B3_ROT(v12, 16);                                                                    \
+    asm volatile("v_alignbit_b32 %0, %1, %1, 16" : "=v"(v13) : "v"(v1));                \
+    B3_ROT(v14, 16); B3_ROT(v15, 16);                                                   \
+    B3_ADDLIT(v8, IV0, v12); B3_ADDLIT(v9, IV1, v13);                                   \
+    B3_ADDLIT(v10, IV2, v14); B3_ADDLIT(v11, IV3, v15);                                 \
+    B3_OP2("v_xor_b32", v4, v8); B3_OP2("v_xor_b32", v5, v9);                           \
+    B3_OP2("v_xor_b32", v6, v10); B3_OP2("v_xor_b32", v7, v11);                         \
+    B3_ROT(v4, 12); B3_ROT(v5, 12); B3_ROT(v6, 12); B3_ROT(v7, 12);                     \
+    B3_OP3("v_add3_u32", v0, v4, y0); B3_OP3("v_add3_u32", v1, v5, y1);                \
+    B3_OP3("v_add3_u32", v2, v6, y2); B3_OP3("v_add3_u32", v3, v7, y3);                \
+    B3_OP2("v_xor_b32", v12, v0); B3_OP2("v_xor_b32", v13, v1);                         \
+    B3_OP2("v_xor_b32", v14, v2); B3_OP2("v_xor_b32", v15, v3);                         \
+    B3_ROT(v12, 8); B3_ROT(v13, 8); B3_ROT(v14, 8); B3_ROT(v15, 8);                     \
+    B3_OP2("v_add_u32", v8, v12); B3_OP2("v_add_u32", v9, v13);                         \
+    B3_OP2("v_add_u32", v10, v14); B3_OP2("v_add_u32", v11, v15);                       \
+    B3_OP2("v_xor_b32", v4, v8); B3_OP2("v_xor_b32", v5, v9);                           \
+    B3_OP2("v_xor_b32", v6, v10); B3_OP2("v_xor_b32", v7, v11);                         \
+    B3_ROT(v4, 7); B3_ROT(v5, 7); B3_ROT(v6, 7); B3_ROT(v7, 7);                         \
+  } while (0)
+
+#ifndef B3_FOLD
+#define B3_FOLD 1
+#endif
+#ifndef B3_LOAD128
+#define B3_LOAD128 1
+#endif
+
 __device__ __forceinline__ void compress(uint32_t cv[8], const uint32_t m[16],
                                          uint32_t counter, uint32_t blen, uint32_t flags) {
   uint32_t v0 = cv[0], v1 = cv[1], v2 = cv[2], v3 = cv[3];
   uint32_t v4 = cv[4], v5 = cv[5], v6 = cv[6], v7 = cv[7];
+#if B3_FOLD
+  uint32_t v8, v9, v10, v11, v12, v13, v14, v15;
+  {
+    const uint8_t *s = kSched.s[0];
+    B3_G4_FIRST(m[s[0]], m[s[2]], m[s[4]], m[s[6]], m[s[1]], m[s[3]], m[s[5]], m[s[7]]);
+    B3_G4(v0, v5, v10, v15, v1, v6, v11, v12, v2, v7, v8, v13, v3, v4, v9, v14,
+          m[s[8]], m[s[10]], m[s[12]], m[s[14]], m[s[9]], m[s[11]], m[s[13]], m[s[15]]);
+  }
+#pragma unroll
+  for (int r = 1; r < 7; ++r) {
+#else
   uint32_t v8 = IV0, v9 = IV1, v10 = IV2, v11 = IV3;
   uint32_t v12 = counter, v13 = 0, v14 = blen, v15 = flags;
 #pragma unroll
   for (int r = 0; r < 7; ++r) {
+#endif
     const uint8_t *s = kSched.s[r];
     B3_G4(v0, v4, v8, v12, v1, v5, v9, v13, v2, v6, v10, v14, v3, v7, v11, v15,
           m[s[0]], m[s[2]], m[s[4]], m[s[6]], m[s[1]], m[s[3]], m[s[5]], m[s[7]]);
@@ -322,6 +373,28 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
       // loops, each with its compression, one after the other.)
       const u32x4 *q = reinterpret_cast<const u32x4 *>(src + off);
       const uint32_t fl_end = CHUNK_END | ((root_group && nleaves == 1) ? ROOT : 0);
+#if B3_LOAD128
+      // Both 64-B blocks of a 128-B line are loaded together (8 x 16-B loads
+      // per pair of compressions): a lane's line is requested from the fabric
+      // once.  Loading each block just before its compression left ~one
+      // compression between the two halves of the line, long enough for the
+      // L2 to evict it: 14 % of the lines were fetched twice (TCC_EA0_RDREQ_128B,
+      // profiles/r1/pmc_req_c2.json).
+      for (uint32_t b = 0; b < 16; b += 2, q += 8) {
+        const u32x4 x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
+        const u32x4 x4 = q[4], x5 = q[5], x6 = q[6], x7 = q[7];
+        m[0] = x0.x; m[1] = x0.y; m[2] = x0.z; m[3] = x0.w;
+        m[4] = x1.x; m[5] = x1.y; m[6] = x1.z; m[7] = x1.w;
+        m[8] = x2.x; m[9] = x2.y; m[10] = x2.z; m[11] = x2.w;
+        m[12] = x3.x; m[13] = x3.y; m[14] = x3.z; m[15] = x3.w;
+        compress(cur, m, leaf, 64, b == 0 ? CHUNK_START : 0u);
+        m[0] = x4.x; m[1] = x4.y; m[2] = x4.z; m[3] = x4.w;
+        m[4] = x5.x; m[5] = x5.y; m[6] = x5.z; m[7] = x5.w;
+        m[8] = x6.x; m[9] = x6.y; m[10] = x6.z; m[11] = x6.w;
+        m[12] = x7.x; m[13] = x7.y; m[14] = x7.z; m[15] = x7.w;
+        compress(cur, m, leaf, 64, b == 14 ? fl_end : 0u);
+      }
+#else
       // unrolled by 2: keeps this loop's compressions a separate copy (the
       // compiler otherwise merges them with the general loop's)
 #pragma unroll 2
@@ -333,6 +406,7 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
         m[12] = x3.x; m[13] = x3.y; m[14] = x3.z; m[15] = x3.w;
         compress(cur, m, leaf, 64, b == 0 ? CHUNK_START : b == 15 ? fl_end : 0u);
       }
+#endif
       if (D > 0) finish(k);
       continue;
     }
@@ -363,8 +437,17 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
   return root_group ? 1 : 2;
 }
 
+#ifndef B3_WAVES_PER_EU
+#define B3_WAVES_PER_EU 0
+#endif
+#if B3_WAVES_PER_EU
+#define B3_OCC __attribute__((amdgpu_waves_per_eu(B3_WAVES_PER_EU)))
+#else
+#define B3_OCC
+#endif
+
 template <int D, int LM>
-__global__ __launch_bounds__(256) void b3_groups(
+__global__ __launch_bounds__(256) B3_OCC void b3_groups(
     const uint8_t *__restrict__ data, uint64_t data_len,
     const ngpu_chunk *__restrict__ chunks, uint64_t n,
     const uint64_t *__restrict__ gbase, const uint32_t *__restrict__ gchunk,

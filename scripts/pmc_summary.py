@@ -34,6 +34,19 @@ def main():
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         res["traffic_bytes"] = int((2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024)
         res["correction"] = "FETCH_SIZE x2 (gfx950 half-count on wide streams), WRITE_SIZE as is, KiB -> B"
+    sized = ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
+    if all(k in avg for k in sized):
+        # read requests by size: the exact bytes the L2 asked of the fabric
+        # (Infinity Cache + HBM); no x2 rule needed (tools/fetch_calib.hip)
+        rb = 32 * avg[sized[0]] + 64 * avg[sized[1]] + 128 * avg[sized[2]]
+        res["read_request_bytes"] = int(rb)
+        wr = avg.get("WRITE_SIZE", 0) * 1024
+        res["traffic_bytes"] = int(rb + wr)
+        res["correction"] = ("TCC_EA0_RDREQ_{32,64,128}B_sum x size (+ WRITE_SIZE KiB if "
+                             "collected): exact request bytes, no x2 rule")
+    if "TCC_EA0_RDREQ_DRAM_sum" in avg and "TCC_EA0_RDREQ_sum" in avg:
+        res["dram_request_frac"] = round(avg["TCC_EA0_RDREQ_DRAM_sum"] /
+                                         max(1.0, avg["TCC_EA0_RDREQ_sum"]), 4)
     if "GRBM_GUI_ACTIVE" in avg and durs:
         res["clock_ghz"] = round(avg["GRBM_GUI_ACTIVE"] / 8 / (sum(durs) / len(durs) / 1e3) / 1e9, 3)
     if "SQ_INSTS_VALU" in avg:
