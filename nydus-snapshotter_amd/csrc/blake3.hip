@@ -224,76 +224,106 @@ __device__ __forceinline__ uint32_t small_key(const ngpu_chunk &ch, int D) {
   return len == 0 ? 1 : (len + 63) / 64;
 }
 
-// Leaf groups per multi-group chunk (0 for single-group chunks; exclusive-
-// scanned afterwards) and the histogram of single-group block counts.
-__global__ __launch_bounds__(256) void b3_count_groups(const ngpu_chunk *__restrict__ chunks,
-                                                       uint64_t n, int D,
-                                                       uint64_t *__restrict__ groups,
-                                                       uint32_t *__restrict__ hist) {
+// Leaf groups per chunk -> exclusive scan (groups[0..n], single pass with
+// decoupled look-back; multi-group chunks only, single-group chunks count 0)
+// and the histogram of single-group block counts.  4 consecutive chunks per
+// thread, so a workgroup issues its histogram atomics for 1024 chunks.
+constexpr int kPlanItems = 4;
+constexpr int kPlanTile = kTileThreads * kPlanItems;
+
+__global__ __launch_bounds__(kTileThreads) void b3_plan(const ngpu_chunk *__restrict__ chunks,
+                                                        uint64_t n, int D,
+                                                        uint64_t *__restrict__ groups,
+                                                        uint32_t *__restrict__ hist,
+                                                        uint64_t *__restrict__ ts) {
   __shared__ uint32_t h[kMaxKey + 1];
+  __shared__ uint64_t sh_tile, sh_pre;
   for (int i = threadIdx.x; i <= kMaxKey; i += blockDim.x) h[i] = 0;
+  if (threadIdx.x == 0)
+    sh_tile = __hip_atomic_fetch_add(ts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c < n) {
-    const uint32_t key = small_key(chunks[c], D);
-    if (key) {
-      groups[c] = 0;
-      atomicAdd(&h[key], 1u);
-    } else {
-      const uint32_t len = chunks[c].length;
-      groups[c] = (((len + kLeaf - 1) / kLeaf) + (1u << D) - 1) >> D;
+  const uint64_t tile = sh_tile;
+  const uint64_t c0 = tile * kPlanTile + threadIdx.x * kPlanItems;
+  uint64_t g[kPlanItems], sum = 0;
+#pragma unroll
+  for (int i = 0; i < kPlanItems; ++i) {
+    g[i] = 0;
+    const uint64_t c = c0 + i;
+    if (c < n) {
+      const uint32_t key = small_key(chunks[c], D);
+      if (key) {
+        atomicAdd(&h[key], 1u);
+      } else {
+        const uint32_t len = chunks[c].length;
+        g[i] = (((len + kLeaf - 1) / kLeaf) + (1u << D) - 1) >> D;
+      }
     }
-  } else if (c == n) {
-    groups[n] = 0;
+    sum += g[i];
   }
-  __syncthreads();
+  uint64_t tot;
+  uint64_t run = block_exclusive_scan(sum, &tot);  // (its barriers also publish h)
+  if (threadIdx.x < 64) {
+    const uint64_t pre = wave_lookback(ts + 1, tile, tot);
+    if (threadIdx.x == 0) sh_pre = pre;
+  }
   for (int i = threadIdx.x; i <= kMaxKey; i += blockDim.x)
     if (h[i]) atomicAdd(&hist[i], h[i]);
-}
-
-// Bucket start offsets, largest block count first; *nsmall = number of
-// single-group chunks.
-__global__ void b3_small_offsets(const uint32_t *__restrict__ hist,
-                                 uint32_t *__restrict__ cursor, uint64_t *__restrict__ nsmall) {
-  if (threadIdx.x != 0) return;
-  uint32_t acc = 0;
-  for (int k = kMaxKey; k >= 1; --k) {
-    cursor[k] = acc;
-    acc += hist[k];
+  __syncthreads();
+  run += sh_pre;
+#pragma unroll
+  for (int i = 0; i < kPlanItems; ++i) {
+    const uint64_t c = c0 + i;
+    if (c < n) groups[c] = run;
+    run += g[i];
+    if (c + 1 == n) groups[n] = run;
   }
-  *nsmall = acc;
 }
 
 // small[] = single-group chunk ids sorted by block count (descending; order
-// inside a bucket is arbitrary, results do not depend on it).
-__global__ __launch_bounds__(256) void b3_small_scatter(const ngpu_chunk *__restrict__ chunks,
-                                                        uint64_t n, int D,
-                                                        uint32_t *__restrict__ cursor,
-                                                        uint32_t *__restrict__ small) {
+// inside a bucket is arbitrary, results do not depend on it).  Every
+// workgroup derives the bucket starts from the finished histogram (256 keys,
+// one per thread); *nsmall = number of single-group chunks.
+__global__ __launch_bounds__(kTileThreads) void b3_small_scatter(
+    const ngpu_chunk *__restrict__ chunks, uint64_t n, int D, const uint32_t *__restrict__ hist,
+    uint32_t *__restrict__ cursor, uint32_t *__restrict__ small, uint64_t *__restrict__ nsmall) {
+  static_assert(kMaxKey == kTileThreads, "one bucket per thread");
   __shared__ uint32_t h[kMaxKey + 1], base[kMaxKey + 1];
-  for (int i = threadIdx.x; i <= kMaxKey; i += blockDim.x) h[i] = 0;
+  const int t = threadIdx.x;
+  const uint32_t bkey = kMaxKey - t;  // 256 .. 1: largest block count first
+  uint64_t tot;
+  const uint64_t start = block_exclusive_scan(hist[bkey], &tot);
+  if (blockIdx.x == 0 && t == 0) *nsmall = tot;
+  for (int i = t; i <= kMaxKey; i += blockDim.x) h[i] = 0;
   __syncthreads();
-  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  const uint32_t key = c < n ? small_key(chunks[c], D) : 0;
-  uint32_t rank = 0;
-  if (key) rank = atomicAdd(&h[key], 1u);
+  uint32_t key[kPlanItems], rank[kPlanItems];
+#pragma unroll
+  for (int i = 0; i < kPlanItems; ++i) {
+    const uint64_t c = blockIdx.x * (uint64_t)kPlanTile + i * kTileThreads + t;
+    key[i] = c < n ? small_key(chunks[c], D) : 0;
+    rank[i] = key[i] ? atomicAdd(&h[key[i]], 1u) : 0;
+  }
   __syncthreads();
-  for (int i = threadIdx.x; i <= kMaxKey; i += blockDim.x)
-    if (h[i]) base[i] = atomicAdd(&cursor[i], h[i]);
+  if (h[bkey]) base[bkey] = (uint32_t)start + atomicAdd(&cursor[bkey], h[bkey]);
   __syncthreads();
-  if (key) small[base[key] + rank] = (uint32_t)c;
+#pragma unroll
+  for (int i = 0; i < kPlanItems; ++i) {
+    const uint64_t c = blockIdx.x * (uint64_t)kPlanTile + i * kTileThreads + t;
+    if (key[i]) small[base[key[i]] + rank[i]] = (uint32_t)c;
+  }
 }
 
-// group -> chunk map; one wave per chunk, lanes stride over its groups.
+// group -> chunk map: W lanes per chunk (W = 64 / chunks per wave, a power
+// of two sized to the layer's groups per chunk), lanes stride over its groups.
 __global__ void b3_fill_group_chunk(const uint64_t *__restrict__ gbase,
                                     uint64_t n, uint32_t *__restrict__ gchunk,
-                                    uint64_t cap_g) {
-  const uint64_t waves = (gridDim.x * (uint64_t)blockDim.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t c = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6; c < n;
-       c += waves) {
-    uint64_t b = gbase[c], e = gbase[c + 1];
-    for (uint64_t g = b + lane; g < e && g < cap_g; g += 64) gchunk[g] = (uint32_t)c;
+                                    uint64_t cap_g, uint32_t W) {
+  const uint32_t per_wave = 64 / W;
+  const uint64_t slots = ((gridDim.x * (uint64_t)blockDim.x) >> 6) * per_wave;
+  const uint32_t lane = threadIdx.x & 63, sub = lane / W, sl = lane % W;
+  for (uint64_t c = ((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6) * per_wave + sub;
+       c < n; c += slots) {
+    const uint64_t b = gbase[c], e = gbase[c + 1];
+    for (uint64_t g = b + sl; g < e && g < cap_g; g += W) gchunk[g] = (uint32_t)c;
   }
 }
 
@@ -648,21 +678,26 @@ void launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
                    hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_end) {
   if (n == 0) return;
   {
-    const uint64_t blocks = (n + 1 + 255) / 256;
-    uint32_t *hist = ws.small_hist, *cursor = ws.small_hist + (kMaxKey + 1);
-    (void)hipMemsetAsync(hist, 0, (kMaxKey + 1) * sizeof(uint32_t), s);
-    hipLaunchKernelGGL(b3_count_groups, dim3((unsigned)blocks), dim3(256), 0, s,
-                       chunks, n, D, ws.groups, hist);
-    hipLaunchKernelGGL(b3_small_offsets, dim3(1), dim3(64), 0, s, hist, cursor, ws.stats + 10);
-    hipLaunchKernelGGL(b3_small_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                       chunks, n, D, cursor, ws.small);
+    // histogram + cursors + plan ticket + this call's tile words, one memset
+    const uint64_t nt = (n + kPlanTile - 1) / kPlanTile;
+    uint32_t *hist = reinterpret_cast<uint32_t *>(ws.tstat), *cursor = hist + (kMaxKey + 1);
+    uint64_t *ts = ws.tstat + kB3Ts;
+    (void)hipMemsetAsync(ws.tstat, 0, (kB3Ts + 1 + nt) * sizeof(uint64_t), s);
+    hipLaunchKernelGGL(b3_plan, dim3((unsigned)nt), dim3(kTileThreads), 0, s, chunks, n, D,
+                       ws.groups, hist, ts);
+    hipLaunchKernelGGL(b3_small_scatter, dim3((unsigned)nt), dim3(kTileThreads), 0, s, chunks, n,
+                       D, hist, cursor, ws.small, ws.stats + 10);
   }
-  launch_scan_u64(ws.groups, n, ws.scan_tmp, s);
   {
-    uint64_t waves = n < 16384 ? n : 16384;
-    uint64_t blocks = (waves * 64 + 255) / 256;
+    // lanes per chunk: the groups a chunk of the average size has, 1..64
+    const uint64_t per = data_len / (n * ((uint64_t)kLeaf << D)) + 1;
+    uint32_t W = 1;
+    while (W < 64 && W < per) W <<= 1;
+    const uint64_t waves_needed = (n * W + 63) / 64;
+    const uint64_t waves = waves_needed < 16384 ? waves_needed : 16384;
+    const uint64_t blocks = (waves * 64 + 255) / 256;
     hipLaunchKernelGGL(b3_fill_group_chunk, dim3((unsigned)blocks), dim3(256), 0,
-                       s, ws.groups, n, ws.group_chunk, ws.cap_g);
+                       s, ws.groups, n, ws.group_chunk, ws.cap_g, W);
   }
   if (ev_start) (void)hipEventRecord(ev_start, s);
   switch (D) {

@@ -34,6 +34,108 @@ __device__ __forceinline__ uint64_t digest_bucket(const uint32_t *w) {
   return ((uint64_t)w[1] << 32 | w[0]) * 0x9E3779B97F4A7C15ull;
 }
 
+// ---- single-pass scan across workgroups (decoupled look-back) -------------
+// A workgroup takes a ticket (its tile, in dispatch order), scans its 256
+// values in the block, publishes the tile aggregate, then walks back over
+// earlier tiles until it meets a published inclusive prefix.  Earlier tickets
+// belong to workgroups that are already resident and publish without waiting,
+// so the spin always ends.  One 64-bit word per tile carries flag + value, so
+// a single atomic load sees a consistent pair.
+constexpr int kTileThreads = 256;
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagPre = 2ull << 62, kValMask = kFlagAgg - 1;
+
+static __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *total) {
+  __shared__ uint64_t wsum[kTileThreads / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kTileThreads / 64; ++w) {
+    if (w < wid) pre += wsum[w];
+    tot += wsum[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+// Called by a whole wave: publish `agg` for `tile` and return the tile's
+// exclusive prefix.  Each round the wave reads 8 x 64 predecessors at once
+// (lane i, slot j: tile - 1 - i - 64 j; the 8 loads are in flight together),
+// waits until each has published, and adds aggregates up to the nearest
+// inclusive prefix; only a round without any prefix moves further back.
+// (Prefixes appear in dispatch order, so one round usually suffices: a
+// window of 64 took one L2 round trip per 64 tiles, 20 us at 1024 tiles.)
+static __device__ uint64_t wave_lookback(uint64_t *status, uint64_t tile, uint64_t agg) {
+  constexpr int K = 8;
+  const int lane = threadIdx.x & 63;
+  if (tile == 0) {
+    if (lane == 0)
+      __hip_atomic_store(status, kFlagPre | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0)
+    __hip_atomic_store(status + tile, kFlagAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t excl = 0;
+  for (int64_t end = (int64_t)tile;; end -= 64 * K) {
+    uint64_t s[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t t = end - 1 - lane - 64 * j;
+      s[j] = t >= 0 ? __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : kFlagPre;  // before tile 0: an inclusive prefix of 0
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t t = end - 1 - lane - 64 * j;
+      while (s[j] == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        s[j] = __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // nearest inclusive prefix: smallest (slot j, lane) in distance order
+    int jp = K, lp = 64;
+#pragma unroll
+    for (int j = K - 1; j >= 0; --j) {
+      const uint64_t pm = __ballot((s[j] & kFlagPre) != 0);
+      if (pm) { jp = j; lp = __builtin_ctzll(pm); }
+    }
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      if (j < jp || (j == jp && lane <= lp)) v += s[j] & kValMask;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+    excl += v;
+    if (jp < K) break;
+  }
+  if (lane == 0)
+    __hip_atomic_store(status + tile, kFlagPre | (excl + agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+// Workspace::tstat layout (u64 words), nt = tiles of cap_n chunks:
+//   [0, 257)            BLAKE3 small-chunk histogram + cursors (2 x 257 u32)
+//   [257]               BLAKE3 plan ticket, [258, 258 + nt) its tile status
+//   [kDedupTs(nt)]      dedup ticket, then nt words per dedup scan (kDedupScans)
+constexpr uint64_t kB3Ts = 257;
+__host__ __device__ constexpr uint64_t tstat_tiles(uint64_t cap_n) {
+  return cap_n / kTileThreads + 2;
+}
+__host__ __device__ constexpr uint64_t kDedupTs(uint64_t nt) { return kB3Ts + 1 + nt; }
+constexpr int kDedupScans = 4;  // NEW count, v6 offset, NEW bytes, DICT count
+__host__ __device__ constexpr uint64_t tstat_words(uint64_t nt) {
+  return kDedupTs(nt) + 1 + kDedupScans * nt;
+}
+
 // ---- launchers (defined in the .hip files) --------------------------------
 struct Workspace;
 
@@ -65,17 +167,14 @@ void launch_dict_build(const uint8_t *digests, uint64_t m, uint64_t *table,
                        uint64_t cap, hipStream_t s);
 // hits == nullptr: probe `dict`; otherwise use the given per-chunk hits.
 // n_blobs: inner blobs of the (global) dict.  L layers; layer l owns chunks
-// [lfirst[l], lfirst[l+1]) (device array); st: device ngpu_layer_stats[L].
+// [lfirst[l], lfirst[l+1]) (device array; nullptr = one layer, {0, n} is
+// written to ws.lfirst1); st: device ngpu_layer_stats[L].
 void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                   const ngpu_dict_hit *hits, uint32_t n_blobs, uint32_t align,
                   const uint64_t *lfirst, uint64_t L, Workspace &ws, ngpu_result *out,
                   ngpu_layer_stats *st, hipStream_t s);
-void launch_set_single_layer(uint64_t *lfirst, uint64_t n, hipStream_t s);
 void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
                        const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s);
-void launch_scan_u64(uint64_t *data, uint64_t n, uint64_t *tmp,
-                     hipStream_t s);  // exclusive, in place, n+1 entries used
-uint64_t scan_tmp_words(uint64_t n);
 
 // Device workspace, grown on demand and owned by the engine.
 struct Workspace {
@@ -83,11 +182,13 @@ struct Workspace {
   uint32_t *group_chunk = nullptr;// G_max: chunk id of each leaf group
   uint32_t *cv = nullptr;         // G_max x 8 words: subtree chaining values
   uint32_t *small = nullptr;      // n: single-group chunks sorted by work (blake3.hip)
-  uint32_t *small_hist = nullptr; // 2 x (16*16 + 1): block-count histogram + cursors
   uint32_t *tree_list = nullptr;  // n: chunks whose groups straddle a workgroup window
   uint64_t *newflag = nullptr;    // n+1: NEW flag -> scan = NEW index
   uint64_t *uoff = nullptr;       // n+1: aligned NEW size -> scan = offset
-  uint64_t *scan_tmp = nullptr;
+  uint64_t *nbytes = nullptr;     // n+1: scan of NEW chunk bytes (layer stats)
+  uint64_t *ndict = nullptr;      // n+1: scan of DICT flags (layer stats)
+  uint64_t *tstat = nullptr;      // tile tickets/status of the single-pass scans (+ histogram)
+  uint64_t tiles = 0;             // tiles the tstat layout is sized for
   uint64_t *intra = nullptr;      // intra-layer hash table
   uint64_t intra_cap = 0;
   uint32_t *blob_first = nullptr; // per layer: dict blobs + 1: first chunk hitting each

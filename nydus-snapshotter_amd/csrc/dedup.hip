@@ -116,79 +116,63 @@ __device__ __forceinline__ uint64_t layer_bucket(const uint32_t *d, uint32_t lay
   return digest_bucket(d) + (uint64_t)layer * 0xC2B2AE3D27D4EB4Full;
 }
 
-// chunk -> layer map: thread per chunk, binary search in lfirst[0..L]
-// (last layer whose first chunk <= c; empty layers are skipped naturally).
-__global__ void layer_fill(const uint64_t *__restrict__ first, uint64_t L, uint64_t n,
-                           uint32_t *__restrict__ chunk_layer) {
-  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  uint64_t lo = 0, hi = L;  // invariant: first[lo] <= c < first[hi]
-  while (hi - lo > 1) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (first[mid] <= c) lo = mid;
-    else hi = mid;
+// Stage 0 (one grid-stride launch instead of four memsets + a map kernel):
+// reset the per-layer blob first-hit slots, the layer stats, the intra table
+// and the scan tiles, and fill chunk -> layer (binary search in first[0..L]:
+// the last layer whose first chunk <= c, so empty layers are skipped).
+// single != nullptr: one layer; {0, n} is written there for the later stages.
+__global__ void dedup_init(const uint64_t *__restrict__ first, uint64_t L, uint64_t n,
+                           uint64_t *__restrict__ single, uint32_t *__restrict__ chunk_layer,
+                           uint32_t *__restrict__ blob_first, uint64_t nbf,
+                           uint64_t *__restrict__ st_words, uint64_t nst,
+                           uint64_t *__restrict__ intra, uint64_t icap,
+                           uint64_t *__restrict__ tiles, uint64_t ntw,
+                           uint64_t *__restrict__ newidx, uint64_t *__restrict__ uoff,
+                           uint64_t *__restrict__ nbytes, uint64_t *__restrict__ ndict,
+                           uint64_t total) {
+  const uint64_t stride = gridDim.x * (uint64_t)blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += stride) {
+    if (i < nbf) blob_first[i] = kNone;
+    if (i < nst) st_words[i] = 0;
+    if (i < icap) intra[i] = kEmpty;
+    if (i < ntw) tiles[i] = 0;
+    if (i < n) {
+      uint64_t lo = 0;
+      if (!single) {
+        uint64_t hi = L;  // invariant: first[lo] <= c < first[hi]
+        while (hi - lo > 1) {
+          const uint64_t mid = (lo + hi) >> 1;
+          if (first[mid] <= i) lo = mid;
+          else hi = mid;
+        }
+      }
+      chunk_layer[i] = (uint32_t)lo;
+    }
+    if (i == 0) {  // the scans' totals for n == 0 (the last tile writes them otherwise)
+      newidx[n] = 0;
+      uoff[n] = 0;
+      nbytes[n] = 0;
+      ndict[n] = 0;
+      if (single) { single[0] = 0; single[1] = n; }
+    }
   }
-  chunk_layer[c] = (uint32_t)lo;
 }
 
-// Stage 1: dict decision (from given hits, or by probing the local dict) +
-// reset of the per-chunk state.
-__global__ void dedup_probe(const ngpu_chunk *__restrict__ chunks, uint64_t n,
-                            DictDevice dict, const ngpu_dict_hit *__restrict__ hits,
-                            const uint32_t *__restrict__ chunk_layer,
-                            ngpu_result *__restrict__ out,
-                            uint64_t *__restrict__ newflag,
-                            uint32_t *__restrict__ blob_first, uint32_t n_blobs) {
-  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  ngpu_result &r = out[c];
-  uint32_t kind = NGPU_NEW;
-  ngpu_dict_hit h{kNone, 0, 0, 0};
-  if (hits) {
-    h = hits[c];
-  } else if (dict.m) {
-    uint32_t d[8];
-    load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
-    const uint32_t e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
-    if (e != kNone) h = ngpu_dict_hit{e, dict.index[e], dict.blob[e], dict.usize[e]};
-  }
-  if (h.entry != kNone && (h.usize == 0 || h.usize == chunks[c].length) && h.blob < n_blobs) {
-    kind = NGPU_DICT;
-    r.ref = h.entry;
-    r.index = h.index;
-    r.blob_index = h.blob;  // inner index; remapped in finalize
-    r.uncompressed_offset = 0;
-    atomicMin(blob_first + (uint64_t)chunk_layer[c] * (n_blobs + 1) + h.blob, (uint32_t)c);
-  }
-  r.kind = kind;
-  r.dict_blob = kind == NGPU_DICT ? h.blob : 0u;
-  newflag[c] = 0;
-}
-
-// Per-layer counters: lanes of a wave usually share one layer, so reduce in
-// the wave and issue ONE atomic (per-lane atomics on one address serialise:
-// 16K of them cost ~0.2 ms).  Every lane of the wave must call these.
-__device__ __forceinline__ void layer_add_u64(unsigned long long *base, size_t stride_words,
-                                              uint32_t layer, uint64_t v) {
-  const uint32_t l0 = __builtin_amdgcn_readfirstlane(layer);
-  if (__all(layer == l0)) {
+// atomicMin(base[key], v) for the lanes with act set.  Lanes of a wave
+// usually share one key (one layer, one dict blob): reduce in the wave and
+// issue ONE atomic (per-lane atomics on one address serialise).  Every lane
+// of the wave must call this.
+__device__ __forceinline__ void wave_min_u32(uint32_t *base, bool act, uint64_t key, uint32_t v) {
+  const uint64_t am = __ballot(act);
+  if (!am) return;
+  const uint64_t k0 = __shfl(key, __builtin_ctzll(am), 64);
+  if (__all(!act || key == k0)) {
+    uint32_t x = act ? v : kNone;
 #pragma unroll
-    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(base + (size_t)l0 * stride_words, (unsigned long long)v);
-  } else if (v) {
-    atomicAdd(base + (size_t)layer * stride_words, (unsigned long long)v);
-  }
-}
-
-__device__ __forceinline__ void layer_min_u32(uint32_t *base, size_t stride, uint32_t layer,
-                                              uint32_t v) {
-  const uint32_t l0 = __builtin_amdgcn_readfirstlane(layer);
-  if (__all(layer == l0)) {
-#pragma unroll
-    for (int o = 32; o; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    if ((threadIdx.x & 63) == 0 && v != kNone) atomicMin(base + (size_t)l0 * stride, v);
-  } else if (v != kNone) {
-    atomicMin(base + (size_t)layer * stride, v);
+    for (int o = 32; o; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMin(base + k0, x);
+  } else if (act) {
+    atomicMin(base + key, v);
   }
 }
 
@@ -198,14 +182,47 @@ __device__ __forceinline__ bool same_key(const ngpu_result *out, const uint32_t 
          digest_eq<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), id, d);
 }
 
-__global__ void dedup_insert(const ngpu_result *__restrict__ out, uint64_t n,
-                             const uint32_t *__restrict__ chunk_layer,
-                             uint64_t *__restrict__ table, uint64_t mask) {
+// Stage 1: dict decision (from given hits, or by probing the local dict);
+// a chunk the dict does not take goes into the intra-layer table (CAS into an
+// empty slot, or atomic MIN over the slot holding the same (layer, digest):
+// the first occurrence wins for any schedule).
+__global__ void dedup_probe_insert(const ngpu_chunk *__restrict__ chunks, uint64_t n,
+                                   DictDevice dict, const ngpu_dict_hit *__restrict__ hits,
+                                   const uint32_t *__restrict__ chunk_layer,
+                                   ngpu_result *__restrict__ out,
+                                   uint32_t *__restrict__ blob_first, uint32_t n_blobs,
+                                   uint64_t *__restrict__ table, uint64_t mask) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c >= n || out[c].kind == NGPU_DICT) return;
-  uint32_t d[8];
-  load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
-  const uint32_t layer = chunk_layer[c];
+  const bool live = c < n;
+  uint32_t d[8] = {};
+  uint32_t layer = 0;
+  ngpu_dict_hit h{kNone, 0, 0, 0};
+  if (live) {
+    load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
+    layer = chunk_layer[c];
+    if (hits) {
+      h = hits[c];
+    } else if (dict.m) {
+      const uint32_t e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
+      if (e != kNone) h = ngpu_dict_hit{e, dict.index[e], dict.blob[e], dict.usize[e]};
+    }
+  }
+  const bool is_dict = live && h.entry != kNone &&
+                       (h.usize == 0 || h.usize == chunks[c].length) && h.blob < n_blobs;
+  wave_min_u32(blob_first, is_dict, (uint64_t)layer * (n_blobs + 1) + h.blob, (uint32_t)c);
+  if (!live) return;
+  ngpu_result &r = out[c];
+  if (is_dict) {
+    r.kind = NGPU_DICT;
+    r.ref = h.entry;
+    r.index = h.index;
+    r.blob_index = h.blob;  // inner index; remapped in finalize
+    r.uncompressed_offset = 0;
+    r.dict_blob = h.blob;
+    return;
+  }
+  r.kind = NGPU_NEW;
+  r.dict_blob = 0;
   const uint32_t tag = digest_tag(d);
   const uint32_t id = (uint32_t)c;
   const uint64_t mine = ((uint64_t)tag << 32) | id;
@@ -224,212 +241,211 @@ __global__ void dedup_insert(const ngpu_result *__restrict__ out, uint64_t n,
   }
 }
 
+// Stage 2: INTRA / NEW per chunk.  Writes the four per-chunk quantities the
+// scan turns into prefixes: NEW flag, v6-aligned size, NEW bytes, DICT flag.
+// Per-layer figures are differences of these prefixes at layer boundaries,
+// so no per-layer atomics are needed anywhere.
 __global__ void dedup_resolve(const ngpu_chunk *__restrict__ chunks, uint64_t n,
                               const uint32_t *__restrict__ chunk_layer,
                               const uint64_t *__restrict__ table, uint64_t mask,
                               ngpu_result *__restrict__ out, uint32_t align,
-                              uint64_t *__restrict__ newflag,
-                              uint64_t *__restrict__ uoff,
-                              uint32_t *__restrict__ blob_first, uint32_t n_blobs) {
+                              uint64_t *__restrict__ newidx, uint64_t *__restrict__ uoff,
+                              uint64_t *__restrict__ nbytes, uint64_t *__restrict__ ndict) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  const bool live = c < n;
-  uint32_t layer = 0, first_new = kNone;
-  if (live) {
-    ngpu_result &r = out[c];
-    layer = chunk_layer[c];
-    uoff[c] = 0;
-    if (c == 0) { newflag[n] = 0; uoff[n] = 0; }
-    if (r.kind != NGPU_DICT) {
-      uint32_t d[8];
-      load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
-      const uint32_t tag = digest_tag(d);
-      uint32_t f = kNone;
-      for (uint64_t p = layer_bucket(d, layer) & mask;; p = (p + 1) & mask) {
-        const uint64_t s = table[p];
-        if (s == kEmpty) break;
-        if ((uint32_t)(s >> 32) == tag && same_key(out, chunk_layer, (uint32_t)s, d, layer)) {
-          f = (uint32_t)s;
-          break;
-        }
-      }
-      const uint32_t len = chunks[c].length;
-      if (f != (uint32_t)c && f != kNone && chunks[f].length == len) {
-        r.kind = NGPU_INTRA;
-        r.ref = f;
-      } else {
-        r.kind = NGPU_NEW;
-        r.ref = c;
-        newflag[c] = 1;
-        uoff[c] = ((uint64_t)len + align - 1) / align * align;
-        first_new = (uint32_t)c;
+  if (c >= n) return;
+  uint64_t v[kDedupScans] = {0, 0, 0, 0};  // NEW, aligned size, bytes, DICT
+  ngpu_result &r = out[c];
+  const uint32_t layer = chunk_layer[c];
+  if (r.kind == NGPU_DICT) {
+    v[3] = 1;
+  } else {
+    uint32_t d[8];
+    load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
+    const uint32_t tag = digest_tag(d);
+    uint32_t f = kNone;
+    for (uint64_t p = layer_bucket(d, layer) & mask;; p = (p + 1) & mask) {
+      const uint64_t s = table[p];
+      if (s == kEmpty) break;
+      if ((uint32_t)(s >> 32) == tag && same_key(out, chunk_layer, (uint32_t)s, d, layer)) {
+        f = (uint32_t)s;
+        break;
       }
     }
+    const uint32_t len = chunks[c].length;
+    if (f != (uint32_t)c && f != kNone && chunks[f].length == len) {
+      r.kind = NGPU_INTRA;
+      r.ref = f;
+    } else {
+      r.kind = NGPU_NEW;
+      r.ref = c;
+      v[0] = 1;
+      v[1] = ((uint64_t)len + align - 1) / align * align;
+      v[2] = len;
+    }
   }
-  layer_min_u32(blob_first + n_blobs, n_blobs + 1, layer, first_new);
+  newidx[c] = v[0];
+  uoff[c] = v[1];
+  nbytes[c] = v[2];
+  ndict[c] = v[3];
+}
+
+// Stage 3: the four arrays -> exclusive prefixes over the whole call, in
+// place, in one pass (decoupled look-back over tiles of 2048 chunks taken in
+// dispatch order; one wave looks back per array).  Large tiles keep the
+// tile tickets few: each is a device-scope atomic on one address.
+constexpr int kScanItems = 8;
+constexpr uint64_t kScanTile = kTileThreads * kScanItems;
+
+__global__ __launch_bounds__(kTileThreads) void dedup_scan(
+    uint64_t n, uint64_t *__restrict__ newidx, uint64_t *__restrict__ uoff,
+    uint64_t *__restrict__ nbytes, uint64_t *__restrict__ ndict, uint64_t *__restrict__ ts,
+    uint64_t nt) {
+  __shared__ uint64_t sh_tile, sh_pre[kDedupScans];
+  if (threadIdx.x == 0)
+    sh_tile = __hip_atomic_fetch_add(ts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint64_t tile = sh_tile;
+  const uint64_t c0 = tile * kScanTile + threadIdx.x * kScanItems;
+  uint64_t *arr[kDedupScans] = {newidx, uoff, nbytes, ndict};
+  uint64_t v[kDedupScans][kScanItems], run[kDedupScans];
+#pragma unroll
+  for (int k = 0; k < kDedupScans; ++k) {
+    uint64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+      v[k][i] = c0 + i < n ? arr[k][c0 + i] : 0;
+      sum += v[k][i];
+    }
+    uint64_t tot;
+    run[k] = block_exclusive_scan(sum, &tot);
+    if (threadIdx.x == 0) sh_pre[k] = tot;  // tile aggregate, replaced by the prefix below
+  }
+  __syncthreads();
+  static_assert(kTileThreads / 64 == kDedupScans, "one wave per array");
+  const int w = threadIdx.x >> 6;
+  const uint64_t pre = wave_lookback(ts + 1 + w * nt, tile, sh_pre[w]);
+  if ((threadIdx.x & 63) == 0) sh_pre[w] = pre;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kDedupScans; ++k) {
+    uint64_t x = run[k] + sh_pre[k];
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+      const uint64_t c = c0 + i;
+      if (c < n) arr[k][c] = x;
+      x += v[k][i];
+      if (c + 1 == n) arr[k][n] = x;
+    }
+  }
 }
 
 // Blob-table order per layer (one workgroup per layer): each dict blob gets a
 // real index at its first hit, the layer's own blob at its first NEW chunk
 // ([nydus v2.3.0] BlobManager alloc_index / get_or_create_current_blob).
-__global__ void blob_rank(const uint32_t *__restrict__ first_all, uint32_t nbo,
+// The first NEW chunk is found by binary search on the NEW-index scan (the
+// smallest c in the layer with newidx[c + 1] > newidx[first]); the layer
+// stats are differences of the scans at the layer's ends.
+__global__ void blob_rank(uint32_t *__restrict__ first_all, uint32_t nbo,
                           uint32_t *__restrict__ real_all, const uint64_t *__restrict__ lfirst,
                           const uint64_t *__restrict__ newidx, const uint64_t *__restrict__ uoff,
+                          const uint64_t *__restrict__ nbytes, const uint64_t *__restrict__ ndict,
                           ngpu_layer_stats *__restrict__ st) {
+  __shared__ uint32_t fl[1024];
   const uint64_t l = blockIdx.x;
-  const uint32_t *first = first_all + l * nbo;
+  uint32_t *first = first_all + l * nbo;
   uint32_t *real = real_all + l * nbo;
+  const uint64_t a = lfirst[l], e = lfirst[l + 1];
+  if (threadIdx.x < 64) {  // 64-ary search by wave 0 (one L2 round trip per 64x)
+    const int lane = threadIdx.x;
+    uint32_t own = kNone;
+    const uint64_t base_new = newidx[a];
+    if (newidx[e] > base_new) {
+      uint64_t lo = a, hi = e - 1;  // answer in [lo, hi]; pred(hi) holds
+      while (lo < hi) {
+        const uint64_t span = hi - lo + 1;
+        const uint64_t step = (span + 63) / 64;
+        const uint64_t p = lo + (uint64_t)lane * step;
+        const bool pred = p <= hi && newidx[(p < hi ? p : hi) + 1] > base_new;
+        const uint64_t m = __ballot(pred);  // monotone in lane; last lanes may be past hi
+        const int k = m ? __builtin_ctzll(m) : 64;
+        // k == 64: every probed position fails; x lies past the last one
+        const uint64_t kl = k < 64 ? (uint64_t)k : (hi - lo) / step + 1;
+        const uint64_t nhi = k < 64 ? lo + kl * step : hi;
+        const uint64_t nlo = kl > 0 ? lo + (kl - 1) * step + 1 : lo;
+        if (step == 1) { lo = hi = nhi; break; }
+        lo = nlo;
+        hi = nhi;
+      }
+      own = (uint32_t)lo;
+    }
+    if (lane == 0) first[nbo - 1] = own;
+  }
+  __syncthreads();
+  const bool lds = nbo <= 1024;
+  if (lds) {
+    for (uint32_t b = threadIdx.x; b < nbo; b += blockDim.x) fl[b] = first[b];
+    __syncthreads();
+  }
+  uint32_t used = 0;
   for (uint32_t b = threadIdx.x; b < nbo; b += blockDim.x) {
-    const uint32_t fb = first[b];
+    const uint32_t fb = lds ? fl[b] : first[b];
     uint32_t rank = kNone;
     if (fb != kNone) {
       rank = 0;
-      for (uint32_t o = 0; o < nbo; ++o) rank += first[o] < fb;
+      for (uint32_t o = 0; o < nbo; ++o) rank += (lds ? fl[o] : first[o]) < fb;
+      ++used;
     }
     real[b] = rank;
   }
+  __shared__ uint32_t used_all;
+  if (threadIdx.x == 0) used_all = 0;
+  __syncthreads();
+  if (used) atomicAdd(&used_all, used);
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t used = 0;
-    for (uint32_t b = 0; b < nbo; ++b) used += first[b] != kNone;
-    const uint64_t a = lfirst[l], e = lfirst[l + 1];
-    st[l].chunks = e - a;
-    st[l].new_chunks = newidx[e] - newidx[a];
-    st[l].own_blob_index = real[nbo - 1];  // kNone -> 0xFFFFFFFF
-    st[l].blobs = used;
-    st[l].uncompressed_size = uoff[e] - uoff[a];
+    const uint64_t chunks = e - a, nw = newidx[e] - newidx[a], nd = ndict[e] - ndict[a];
+    ngpu_layer_stats x{};
+    x.chunks = chunks;
+    x.new_chunks = nw;
+    x.dict_chunks = nd;
+    x.intra_chunks = chunks - nw - nd;
+    x.new_bytes = nbytes[e] - nbytes[a];
+    x.own_blob_index = real[nbo - 1];  // kNone -> 0xFFFFFFFF
+    x.blobs = used_all;
+    x.uncompressed_size = uoff[e] - uoff[a];
+    st[l] = x;
   }
 }
 
-__global__ void dedup_finalize(const ngpu_chunk *__restrict__ chunks, uint64_t n,
-                               const uint32_t *__restrict__ chunk_layer,
+__global__ void dedup_finalize(const uint64_t n, const uint32_t *__restrict__ chunk_layer,
                                const uint64_t *__restrict__ lfirst,
                                const uint64_t *__restrict__ newidx,
                                const uint64_t *__restrict__ uoff,
                                const uint32_t *__restrict__ real_all, uint32_t nbo,
-                               ngpu_result *__restrict__ out,
-                               ngpu_layer_stats *__restrict__ st) {
+                               ngpu_result *__restrict__ out) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  uint32_t layer = 0;
-  uint64_t new_bytes = 0, intra = 0, dict = 0;
-  if (c < n) {
-    ngpu_result &r = out[c];
-    layer = chunk_layer[c];
-    const uint32_t *real = real_all + (uint64_t)layer * nbo;
-    const uint64_t a = lfirst[layer];
-    const uint64_t ib = newidx[a], ob = uoff[a];
-    const uint32_t own = real[nbo - 1];
-    if (r.kind == NGPU_NEW) {
-      r.index = (uint32_t)(newidx[c] - ib);
-      r.uncompressed_offset = uoff[c] - ob;
-      r.blob_index = own;
-      new_bytes = chunks[c].length;
-    } else if (r.kind == NGPU_INTRA) {
-      const uint64_t f = r.ref;
-      r.index = (uint32_t)(newidx[f] - ib);
-      r.uncompressed_offset = uoff[f] - ob;
-      r.blob_index = own;
-      intra = 1;
-    } else {
-      r.blob_index = real[r.blob_index];
-      dict = 1;
-    }
+  if (c >= n) return;
+  ngpu_result &r = out[c];
+  const uint32_t layer = chunk_layer[c];
+  const uint32_t *real = real_all + (uint64_t)layer * nbo;
+  const uint64_t a = lfirst[layer];
+  const uint64_t ib = newidx[a], ob = uoff[a];
+  const uint32_t own = real[nbo - 1];
+  if (r.kind == NGPU_NEW) {
+    r.index = (uint32_t)(newidx[c] - ib);
+    r.uncompressed_offset = uoff[c] - ob;
+    r.blob_index = own;
+  } else if (r.kind == NGPU_INTRA) {
+    const uint64_t f = r.ref;
+    r.index = (uint32_t)(newidx[f] - ib);
+    r.uncompressed_offset = uoff[f] - ob;
+    r.blob_index = own;
+  } else {
+    r.blob_index = real[r.blob_index];
   }
-  constexpr size_t W = sizeof(ngpu_layer_stats) / 8;
-  unsigned long long *base = reinterpret_cast<unsigned long long *>(st);
-  layer_add_u64(base + offsetof(ngpu_layer_stats, new_bytes) / 8, W, layer, new_bytes);
-  layer_add_u64(base + offsetof(ngpu_layer_stats, intra_chunks) / 8, W, layer, intra);
-  layer_add_u64(base + offsetof(ngpu_layer_stats, dict_chunks) / 8, W, layer, dict);
-}
-
-// ---- exclusive scan over u64 (n+1 entries, in place) ----------------------
-constexpr int kScanThreads = 256;
-constexpr int kScanItems = 8;
-constexpr int kScanTile = kScanThreads * kScanItems;
-
-__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *total) {
-  __shared__ uint64_t wsum[kScanThreads / 64];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint64_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[wid] = x;
-  __syncthreads();
-  uint64_t pre = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < kScanThreads / 64; ++w) {
-    if (w < wid) pre += wsum[w];
-    tot += wsum[w];
-  }
-  __syncthreads();
-  *total = tot;
-  return pre + x - v;
-}
-
-__global__ __launch_bounds__(kScanThreads) void scan_reduce(const uint64_t *__restrict__ a,
-                                                            uint64_t m, uint64_t *__restrict__ tmp) {
-  const uint64_t base = blockIdx.x * (uint64_t)kScanTile + threadIdx.x * kScanItems;
-  uint64_t s = 0;
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i)
-    if (base + i < m) s += a[base + i];
-  uint64_t tot;
-  block_exclusive_scan(s, &tot);
-  if (threadIdx.x == 0) tmp[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(kScanThreads) void scan_top(uint64_t *__restrict__ tmp, uint64_t nb) {
-  uint64_t carry = 0;
-  for (uint64_t t0 = 0; t0 < nb; t0 += kScanThreads) {
-    const uint64_t i = t0 + threadIdx.x;
-    const uint64_t v = i < nb ? tmp[i] : 0;
-    uint64_t tot;
-    const uint64_t ex = block_exclusive_scan(v, &tot);
-    if (i < nb) tmp[i] = carry + ex;
-    carry += tot;
-  }
-}
-
-__global__ __launch_bounds__(kScanThreads) void scan_apply(uint64_t *__restrict__ a, uint64_t m,
-                                                           const uint64_t *__restrict__ tmp) {
-  const uint64_t base = blockIdx.x * (uint64_t)kScanTile + threadIdx.x * kScanItems;
-  uint64_t v[kScanItems], s = 0;
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    v[i] = base + i < m ? a[base + i] : 0;
-    s += v[i];
-  }
-  uint64_t tot;
-  uint64_t run = block_exclusive_scan(s, &tot) + tmp[blockIdx.x];
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    if (base + i < m) a[base + i] = run;
-    run += v[i];
-  }
-}
-
-__global__ void set_single_layer(uint64_t *lfirst, uint64_t n) {
-  lfirst[0] = 0;
-  lfirst[1] = n;
 }
 
 }  // namespace
-
-void launch_set_single_layer(uint64_t *lfirst, uint64_t n, hipStream_t s) {
-  hipLaunchKernelGGL(set_single_layer, dim3(1), dim3(1), 0, s, lfirst, n);
-}
-
-uint64_t scan_tmp_words(uint64_t n) { return (n + 1 + kScanTile - 1) / kScanTile + 1; }
-
-void launch_scan_u64(uint64_t *a, uint64_t n, uint64_t *tmp, hipStream_t s) {
-  const uint64_t m = n + 1;
-  const uint64_t nb = (m + kScanTile - 1) / kScanTile;
-  hipLaunchKernelGGL(scan_reduce, dim3((unsigned)nb), dim3(kScanThreads), 0, s, a, m, tmp);
-  hipLaunchKernelGGL(scan_top, dim3(1), dim3(kScanThreads), 0, s, tmp, nb);
-  hipLaunchKernelGGL(scan_apply, dim3((unsigned)nb), dim3(kScanThreads), 0, s, a, m, tmp);
-}
 
 void launch_dict_build(const uint8_t *digests, uint64_t m, uint64_t *table,
                        uint64_t cap, hipStream_t s) {
@@ -452,31 +468,38 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                   const uint64_t *lfirst, uint64_t L, Workspace &ws, ngpu_result *out,
                   ngpu_layer_stats *st, hipStream_t s) {
   const uint32_t nbo = n_blobs + 1;  // dict blobs + own blob (last slot), per layer
-  (void)hipMemsetAsync(ws.blob_first, 0xFF, sizeof(uint32_t) * nbo * L, s);
-  (void)hipMemsetAsync(st, 0, sizeof(ngpu_layer_stats) * L, s);
+  uint64_t *single = nullptr;
+  if (!lfirst) {
+    single = ws.lfirst1;
+    lfirst = ws.lfirst1;
+    L = 1;
+  }
+  const uint64_t nt = (n + kScanTile - 1) / kScanTile;
+  uint64_t *ts = ws.tstat + kDedupTs(ws.tiles);
+  const uint64_t nbf = (uint64_t)nbo * L, nst = L * (sizeof(ngpu_layer_stats) / 8);
+  const uint64_t icap = n ? ws.intra_cap : 0, ntw = 1 + kDedupScans * ws.tiles;
+  uint64_t total = n + 1;
+  for (uint64_t v : {nbf, nst, icap, ntw}) total = v > total ? v : total;
+  const uint64_t ib = (total + 255) / 256;
+  hipLaunchKernelGGL(dedup_init, dim3((unsigned)(ib < 4096 ? ib : 4096)), dim3(256), 0, s,
+                     lfirst, L, n, single, ws.chunk_layer, ws.blob_first, nbf,
+                     reinterpret_cast<uint64_t *>(st), nst, ws.intra, icap, ts, ntw,
+                     ws.newflag, ws.uoff, ws.nbytes, ws.ndict, total);
   if (n) {
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(layer_fill, dim3(blocks), dim3(256), 0, s, lfirst, L, n, ws.chunk_layer);
-    (void)hipMemsetAsync(ws.intra, 0xFF, ws.intra_cap * sizeof(uint64_t), s);
-    hipLaunchKernelGGL(dedup_probe, dim3(blocks), dim3(256), 0, s, chunks, n, dict, hits,
-                       ws.chunk_layer, out, ws.newflag, ws.blob_first, n_blobs);
-    hipLaunchKernelGGL(dedup_insert, dim3(blocks), dim3(256), 0, s, out, n, ws.chunk_layer,
-                       ws.intra, ws.intra_cap - 1);
+    hipLaunchKernelGGL(dedup_probe_insert, dim3(blocks), dim3(256), 0, s, chunks, n, dict, hits,
+                       ws.chunk_layer, out, ws.blob_first, n_blobs, ws.intra, ws.intra_cap - 1);
     hipLaunchKernelGGL(dedup_resolve, dim3(blocks), dim3(256), 0, s, chunks, n, ws.chunk_layer,
-                       ws.intra, ws.intra_cap - 1, out, align, ws.newflag, ws.uoff,
-                       ws.blob_first, n_blobs);
-  } else {
-    (void)hipMemsetAsync(ws.newflag, 0, sizeof(uint64_t), s);
-    (void)hipMemsetAsync(ws.uoff, 0, sizeof(uint64_t), s);
+                       ws.intra, ws.intra_cap - 1, out, align, ws.newflag, ws.uoff, ws.nbytes,
+                       ws.ndict);
+    hipLaunchKernelGGL(dedup_scan, dim3((unsigned)nt), dim3(kTileThreads), 0, s, n, ws.newflag,
+                       ws.uoff, ws.nbytes, ws.ndict, ts, ws.tiles);
   }
-  launch_scan_u64(ws.newflag, n, ws.scan_tmp, s);
-  launch_scan_u64(ws.uoff, n, ws.scan_tmp, s);
   hipLaunchKernelGGL(blob_rank, dim3((unsigned)L), dim3(256), 0, s, ws.blob_first, nbo,
-                     ws.blob_real, lfirst, ws.newflag, ws.uoff, st);
+                     ws.blob_real, lfirst, ws.newflag, ws.uoff, ws.nbytes, ws.ndict, st);
   if (n)
-    hipLaunchKernelGGL(dedup_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                       chunks, n, ws.chunk_layer, lfirst, ws.newflag, ws.uoff, ws.blob_real,
-                       nbo, out, st);
+    hipLaunchKernelGGL(dedup_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
+                       ws.chunk_layer, lfirst, ws.newflag, ws.uoff, ws.blob_real, nbo, out);
 }
 
 }  // namespace ngpu

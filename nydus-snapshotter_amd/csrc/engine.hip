@@ -75,15 +75,18 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
     uint64_t cn = n + 1 < 4096 ? 4096 : n + 1;
     uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
     if (grow(e, &ws.chunk_layer, c4, cn)) return NGPU_ENOMEM;
-    uint64_t c5 = 0, c6 = 0;
+    uint64_t c5 = 0;
     if (grow(e, &ws.small, c5, cn)) return NGPU_ENOMEM;
     uint64_t c7 = 0;
     if (grow(e, &ws.tree_list, c7, cn)) return NGPU_ENOMEM;
-    if (!ws.small_hist && grow(e, &ws.small_hist, c6, 1024)) return NGPU_ENOMEM;
     if (grow(e, &ws.groups, c0, cn)) return NGPU_ENOMEM;
     if (grow(e, &ws.newflag, c1, cn)) return NGPU_ENOMEM;
     if (grow(e, &ws.uoff, c2, cn)) return NGPU_ENOMEM;
-    if (grow(e, &ws.scan_tmp, c3, scan_tmp_words(cn))) return NGPU_ENOMEM;
+    uint64_t c8 = 0, c9 = 0;
+    if (grow(e, &ws.nbytes, c8, cn)) return NGPU_ENOMEM;
+    if (grow(e, &ws.ndict, c9, cn)) return NGPU_ENOMEM;
+    ws.tiles = tstat_tiles(cn);
+    if (grow(e, &ws.tstat, c3, tstat_words(ws.tiles))) return NGPU_ENOMEM;
     uint64_t icap = next_pow2(2 * cn);
     uint64_t ic = 0;
     if (ws.intra) (void)hipFree(ws.intra), ws.intra = nullptr;
@@ -177,13 +180,10 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_r
   if (!d_lfirst) L = 1;
   int rc = ensure_workspace(e, n, 0, 0, n_blobs, L);
   if (rc) return rc;
-  if (!d_lfirst) {
-    launch_set_single_layer(e->ws.lfirst1, n, s);
-    d_lfirst = e->ws.lfirst1;
-  }
   if (!d_stats) d_stats = e->ws.lstats;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   const uint32_t align = e->cfg.fs_version == 6 ? 4096u : 1u;
+  // d_lfirst == nullptr: the init kernel writes {0, n} into ws.lfirst1
   launch_dedup(d_chunks, n, e->dict, d_hits, n_blobs, align, d_lfirst, L, e->ws, d_out, d_stats, s);
   if (tm) HIP_TRY(e, hipEventRecord(e->ev[4], s));
   HIP_TRY(e, hipGetLastError());
@@ -282,9 +282,9 @@ void ngpu_destroy(ngpu_engine *e) {
   if (e->stream) hipStreamSynchronize(e->stream);
   free_dict(e);
   Workspace &ws = e->ws;
-  void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.scan_tmp,
+  void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.nbytes, ws.ndict, ws.tstat,
                   ws.intra, ws.blob_first, ws.blob_real, ws.stats, ws.chunk_layer,
-                  ws.lfirst1, ws.lstats, ws.small, ws.small_hist, ws.tree_list,
+                  ws.lfirst1, ws.lstats, ws.small, ws.tree_list,
                   e->d_data, e->d_chunks, e->d_results};
   for (void *p : bufs)
     if (p) (void)hipFree(p);
