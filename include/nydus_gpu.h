@@ -249,6 +249,10 @@ void ngpu_free_host(void *p);
  * engine (synchronises on the recorded events).  NGPU_EINVAL unless the
  * engine was created with NGPU_FLAG_TIMING. */
 int ngpu_last_timing(ngpu_engine *eng, ngpu_timing *out);
+/* The same for the call `back` calls before the last one (0 = the last).
+ * The engine keeps the events of its last 64 calls, so a caller can time a
+ * run of back-to-back calls without synchronising between them. */
+int ngpu_timing_at(ngpu_engine *eng, uint32_t back, ngpu_timing *out);
 
 /* ---- streaming Pack (converter.Pack, pkg/converter/convert_unix.go:325) ----
  * The reference returns an io.WriteCloser fed with the uncompressed layer tar

@@ -152,22 +152,28 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
   // tuning override: flags bits 8..10 = 1 + BLAKE3 load mode (0 = default)
   const uint32_t lm = (e->cfg.flags >> 8) & 7;
   e->ws.load_mode = lm ? (int)(lm - 1) : 0;
-  if (tm) HIP_TRY(e, hipEventRecord(e->ev[0], s));
+  hipEvent_t *ev = nullptr;
+  if (tm) {
+    e->tslot = (int)(e->tcalls++ % ngpu_engine::kTimingRing);
+    ev = e->ev[e->tslot];
+    e->timed[e->tslot] = false;
+    e->slot_D[e->tslot] = D;
+    HIP_TRY(e, hipEventRecord(ev[0], s));
+  }
   HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 16 * sizeof(uint64_t), s));
   if (e->cfg.digester == NGPU_DIGEST_SHA256) {
-    if (tm) HIP_TRY(e, hipEventRecord(e->ev[1], s));
+    if (tm) HIP_TRY(e, hipEventRecord(ev[1], s));
     // tuning override: flags bits 11..13 = 1 + SHA-256 variant (0 split,
     // 1 pair, 2/3 pair diagnostics)
     const uint32_t sv = (e->cfg.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7;
     launch_sha256(d_data, len, d_chunks, n, d_out, e->ws.stats + 7, sv ? (int)sv - 1 : -1, s);
-    if (tm) HIP_TRY(e, hipEventRecord(e->ev[2], s));
+    if (tm) HIP_TRY(e, hipEventRecord(ev[2], s));
   } else {
-    launch_blake3(d_data, d_chunks, n, len, D, e->ws, d_out, s, tm ? e->ev[1] : nullptr,
-                  tm ? e->ev[2] : nullptr);
+    launch_blake3(d_data, d_chunks, n, len, D, e->ws, d_out, s, tm ? ev[1] : nullptr,
+                  tm ? ev[2] : nullptr);
   }
-  if (tm) HIP_TRY(e, hipEventRecord(e->ev[3], s));
+  if (tm) HIP_TRY(e, hipEventRecord(ev[3], s));
   HIP_TRY(e, hipGetLastError());
-  e->last_D = D;
   return 0;
 }
 
@@ -185,9 +191,9 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_r
   const uint32_t align = e->cfg.fs_version == 6 ? 4096u : 1u;
   // d_lfirst == nullptr: the init kernel writes {0, n} into ws.lfirst1
   launch_dedup(d_chunks, n, e->dict, d_hits, n_blobs, align, d_lfirst, L, e->ws, d_out, d_stats, s);
-  if (tm) HIP_TRY(e, hipEventRecord(e->ev[4], s));
+  if (tm && e->tcalls) HIP_TRY(e, hipEventRecord(e->ev[e->tslot][4], s));
   HIP_TRY(e, hipGetLastError());
-  e->timed = tm && n > 0;
+  if (tm && e->tcalls) e->timed[e->tslot] = n > 0;
   return 0;
 }
 
@@ -260,11 +266,12 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
     return NGPU_EHIP;
   }
   if (c.flags & NGPU_FLAG_TIMING)
-    for (auto &ev : e->ev)
-      if (hipEventCreate(&ev) != hipSuccess) {
-        delete e;
-        return NGPU_EHIP;
-      }
+    for (auto &set : e->ev)
+      for (auto &ev : set)
+        if (hipEventCreate(&ev) != hipSuccess) {
+          ngpu_destroy(e);
+          return NGPU_EHIP;
+        }
   if (
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void **)&e->h_stats, 32 * sizeof(uint64_t), hipHostMallocDefault) !=
@@ -289,8 +296,9 @@ void ngpu_destroy(ngpu_engine *e) {
   for (void *p : bufs)
     if (p) (void)hipFree(p);
   if (e->h_stats) (void)hipHostFree(e->h_stats);
-  for (auto ev : e->ev)
-    if (ev) (void)hipEventDestroy(ev);
+  for (auto &set : e->ev)
+    for (auto ev : set)
+      if (ev) (void)hipEventDestroy(ev);
   if (e->stream) hipStreamDestroy(e->stream);
   delete e;
 }
@@ -523,20 +531,31 @@ int ngpu_process(ngpu_engine *e, const void *data, uint64_t len, const ngpu_chun
   return read_stats(e, s, stats);
 }
 
-int ngpu_last_timing(ngpu_engine *e, ngpu_timing *out) {
+int ngpu_timing_at(ngpu_engine *e, uint32_t back, ngpu_timing *out) {
   if (!e || !out) return NGPU_EINVAL;
   if (!(e->cfg.flags & NGPU_FLAG_TIMING))
     return fail(e, NGPU_EINVAL, "engine created without NGPU_FLAG_TIMING");
   std::lock_guard<std::mutex> g(e->mu);
   memset(out, 0, sizeof *out);
-  if (!e->timed) return 0;
-  HIP_TRY(e, hipEventSynchronize(e->ev[4]));
-  HIP_TRY(e, hipEventElapsedTime(&out->digest_ms, e->ev[1], e->ev[2]));
-  HIP_TRY(e, hipEventElapsedTime(&out->tree_ms, e->ev[2], e->ev[3]));
-  HIP_TRY(e, hipEventElapsedTime(&out->dedup_ms, e->ev[3], e->ev[4]));
-  HIP_TRY(e, hipEventElapsedTime(&out->total_ms, e->ev[0], e->ev[4]));
-  out->group_log2 = (uint32_t)e->last_D;
+  const uint64_t have = e->tcalls < (uint64_t)ngpu_engine::kTimingRing
+                            ? e->tcalls : (uint64_t)ngpu_engine::kTimingRing;
+  if (back >= have) {
+    if (back == 0) return 0;  // nothing recorded yet
+    return fail(e, NGPU_EINVAL, "timing %u calls back: only %llu kept", back,
+                (unsigned long long)have);
+  }
+  const int k = (int)((e->tcalls - 1 - back) % ngpu_engine::kTimingRing);
+  if (!e->timed[k]) return 0;
+  hipEvent_t *ev = e->ev[k];
+  HIP_TRY(e, hipEventSynchronize(ev[4]));
+  HIP_TRY(e, hipEventElapsedTime(&out->digest_ms, ev[1], ev[2]));
+  HIP_TRY(e, hipEventElapsedTime(&out->tree_ms, ev[2], ev[3]));
+  HIP_TRY(e, hipEventElapsedTime(&out->dedup_ms, ev[3], ev[4]));
+  HIP_TRY(e, hipEventElapsedTime(&out->total_ms, ev[0], ev[4]));
+  out->group_log2 = (uint32_t)e->slot_D[k];
   return 0;
 }
+
+int ngpu_last_timing(ngpu_engine *e, ngpu_timing *out) { return ngpu_timing_at(e, 0, out); }
 
 }  // extern "C"

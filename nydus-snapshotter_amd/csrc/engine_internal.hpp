@@ -28,10 +28,15 @@ struct ngpu_engine {
   ngpu_result *d_results = nullptr;
   uint64_t d_chunk_cap = 0;
   uint64_t *h_stats = nullptr;  // pinned
-  // NGPU_FLAG_TIMING: 0 start, 1 digest start, 2 digest end, 3 tree end, 4 end
-  hipEvent_t ev[5] = {};
-  bool timed = false;
-  int last_D = 0;
+  // NGPU_FLAG_TIMING: a ring of per-call event sets (0 start, 1 digest start,
+  // 2 digest end, 3 tree end, 4 end), so timing a call never makes the next
+  // one wait: ngpu_timing_at reads any of the last kTimingRing calls.
+  static constexpr int kTimingRing = 64;
+  hipEvent_t ev[kTimingRing][5] = {};
+  bool timed[kTimingRing] = {};
+  int slot_D[kTimingRing] = {};
+  uint64_t tcalls = 0;  // calls recorded so far; the current slot is (tcalls - 1) % ring
+  int tslot = 0;
   std::string err;
   std::mutex mu;
 };

@@ -50,7 +50,7 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_device_count", "ngpu_alloc_pinned", "ngpu_free_pinned", "ngpu_dict_load",
            "ngpu_dict_load_bootstrap", "ngpu_dict_clear", "ngpu_dict_size", "ngpu_tar_chunks",
            "ngpu_process", "ngpu_process_device", "ngpu_pack_tar", "ngpu_free_host",
-           "ngpu_chunk_table", "ngpu_last_timing", "ngpu_digest_device",
+           "ngpu_chunk_table", "ngpu_last_timing", "ngpu_timing_at", "ngpu_digest_device",
            "ngpu_dict_probe_device", "ngpu_dedup_device", "ngpu_dict_load_device",
            "ngpu_pack_open", "ngpu_pack_write", "ngpu_pack_reserve", "ngpu_pack_commit",
            "ngpu_pack_close", "ngpu_pack_abort", "ngpu_dedup_layers_device",
@@ -157,6 +157,7 @@ def lib():
     L.ngpu_free_host.restype = None
     L.ngpu_chunk_table.argtypes = [vp, vp, u64, vp, u64, pu64]
     L.ngpu_last_timing.argtypes = [vp, ctypes.POINTER(NgpuTiming)]
+    L.ngpu_timing_at.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(NgpuTiming)]
     L.ngpu_digest_device.argtypes = [vp, vp, u64, vp, u64, vp, vp]
     L.ngpu_dict_probe_device.argtypes = [vp, vp, u64, u64, vp, vp]
     L.ngpu_dedup_device.argtypes = [vp, vp, u64, vp, vp, u32, vp, ctypes.POINTER(NgpuLayerStats)]
@@ -477,6 +478,14 @@ class Engine:
     def last_timing(self) -> dict:
         t = NgpuTiming()
         self._check(lib().ngpu_last_timing(self._h, ctypes.byref(t)), "last_timing")
+        return t.as_dict()
+
+    def timing_at(self, back: int) -> dict:
+        """Stage timings of the call `back` calls before the last one (the
+        engine keeps its last 64); lets a caller time back-to-back calls
+        without synchronising between them."""
+        t = NgpuTiming()
+        self._check(lib().ngpu_timing_at(self._h, back, ctypes.byref(t)), "timing_at")
         return t.as_dict()
 
     def pack(self, retain: bool = False) -> "PackWriter":
