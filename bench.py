@@ -306,8 +306,9 @@ def end_to_end(torch, nydus_gpu, buf, wl, stride, device, sample_bytes=2 << 30):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20,
+                    help="untimed steps; the clock takes ~5 launches to settle (profiles/r1)")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--lanes", type=int, default=0, help="leaves per lane (0=auto)")
     ap.add_argument("--sha-mode", choices=["auto", "split", "pair"], default="auto",

@@ -22,16 +22,16 @@ ok $? pytest-gpu
 tail -5 "$OUT/pytest_gpu.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 ok $? smoke
-timeout -k 10 600 python bench.py --steps 10 --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 ok $? bench
 cat "$OUT/bench.json"
 for W in c3 c5; do
-  timeout -k 10 600 python bench.py --workload $W --steps 5 --warmup 2 > "$OUT/bench_$W.json" 2>> "$OUT/bench.err"
+  timeout -k 10 600 python bench.py --workload $W --steps 20 --warmup 20 > "$OUT/bench_$W.json" 2>> "$OUT/bench.err"
   ok $? bench-$W
   cat "$OUT/bench_$W.json"
 done
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-e2e > "$OUT/prof.log" 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 10 --warmup 10 --no-cpu-baseline --no-e2e > "$OUT/prof.log" 2>&1
 ok $? rocprof
 find "$OUT/prof" -name '*stats*' | head
 python3 "$ROOT/scripts/prof_agree.py" "$OUT/prof" 'b3_groups' "$OUT/prof.log" "$OUT/rocprof_agreement.json"
