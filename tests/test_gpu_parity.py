@@ -824,3 +824,63 @@ def test_small_file_mix_vs_oracle(engines, oracle, chunk_size, median, files):
         assert np.array_equal(out["digest"], dig), lanes
         for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
             assert np.array_equal(out[f], dec[f]), (lanes, f)
+
+
+def test_many_tiles_multi_layer_vs_oracle(oracle):
+    """600K small chunks in 53 layers (one empty) with duplicates and a chunk
+    dict: the BLAKE3 plan scan runs over > 512 tiles of 1024 chunks, so its
+    look-back needs more than one round, and the dedup scan over ~300 tiles;
+    every decision and every per-layer stat (derived from scan differences)
+    must equal the oracle's per-layer pack."""
+    import torch
+    rng = np.random.default_rng(600)
+    data = rng.integers(0, 256, 8 << 20, dtype=np.uint8).tobytes()
+    n = 600_000
+    ch = np.zeros(n, nydus_gpu.CHUNK_DTYPE)
+    ch["length"] = rng.integers(1, 3000, n)
+    ch["offset"] = rng.integers(0, len(data) - 3000, n)
+    dup = rng.choice(n, n // 4, replace=False)  # same bytes as an earlier-or-later chunk
+    src = rng.integers(0, n, len(dup))
+    ch["offset"][dup], ch["length"][dup] = ch["offset"][src], ch["length"][src]
+    ch["file_index"] = np.arange(n)
+    first = np.concatenate([[0], np.sort(rng.choice(np.arange(1, n), 52, replace=False)), [n]])
+    first[7] = first[6]  # an empty layer
+    first = first.astype(np.uint64)
+    L = len(first) - 1
+    dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    pick = rng.choice(n, n // 10, replace=False)
+    dd, ds = dig[pick], ch["length"][pick].astype(np.uint32)
+    ds[::7] = 0  # wildcard sizes
+    db = (np.arange(len(pick)) % 3).astype(np.uint32)
+    di = np.arange(len(pick), dtype=np.uint32)
+    eng = nydus_gpu.Engine(chunk_size=0x100000)
+    try:
+        eng.dict_load(dd, ds, db, di)
+        d_data, d_ch = _to_dev(np.frombuffer(data, np.uint8)), _to_dev(ch)
+        d_first = torch.from_numpy(first.view(np.int64).copy()).cuda()
+        out = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+        st = torch.zeros(L * nydus_gpu.LAYER_STATS_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        eng.process_layers_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), n,
+                                  out.data_ptr(), d_first.data_ptr(), L, st.data_ptr())
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+        stats = st.cpu().numpy().view(nydus_gpu.LAYER_STATS_DTYPE)
+    finally:
+        eng.close()
+    assert np.array_equal(got["digest"], dig)
+    for l in range(L):
+        a, b = int(first[l]), int(first[l + 1])
+        exp, own = oracle.dedup(dig[a:b], ch["length"][a:b], dd, ds, db, di)
+        g = got[a:b]
+        for f in ("kind", "index", "blob_index", "uncompressed_offset"):
+            assert np.array_equal(g[f], exp[f]), (l, f)
+        new = exp["kind"] == 0
+        assert stats[l]["chunks"] == b - a
+        assert stats[l]["new_chunks"] == new.sum()
+        assert stats[l]["intra_chunks"] == (exp["kind"] == 1).sum()
+        assert stats[l]["dict_chunks"] == (exp["kind"] == 2).sum()
+        assert stats[l]["new_bytes"] == ch["length"][a:b][new].astype(np.int64).sum()
+        ends = exp["uncompressed_offset"][new] + (ch["length"][a:b][new] + 4095) // 4096 * 4096
+        assert stats[l]["uncompressed_size"] == (ends.max() if new.any() else 0)
+        assert stats[l]["own_blob_index"] == (0xFFFFFFFF if own is None else own)
+        assert stats[l]["blobs"] == len(set(exp["blob_index"].tolist())), l
