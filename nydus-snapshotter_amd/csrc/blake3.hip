@@ -467,6 +467,23 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
   return root_group ? 1 : 2;
 }
 
+#ifndef B3_BALANCE
+#define B3_BALANCE 1
+#endif
+
+// Compressions of leaf group j of a chunk of len bytes (its 64-B blocks plus
+// the in-group parent merges): the lane's work.
+template <int D>
+__device__ __forceinline__ uint32_t group_work(uint32_t len, uint32_t j) {
+  const uint32_t nleaves = len == 0 ? 1 : (len + kLeaf - 1) / kLeaf;
+  const uint32_t first = j << D;
+  if (first >= nleaves) return 0;
+  const uint32_t cnt = min(1u << D, nleaves - first);
+  const uint32_t start = first * kLeaf, gend = min(len, (first + cnt) * kLeaf);
+  const uint32_t blocks = gend > start ? (gend - start + 63) / 64 : 1;
+  return blocks + cnt - 1;
+}
+
 #ifndef B3_WAVES_PER_EU
 #define B3_WAVES_PER_EU 0
 #endif
@@ -491,7 +508,55 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
   const uint64_t gm = gbase[n];
   const uint64_t total = gm + *nsmall;
   const uint64_t g0 = blockIdx.x * 256ull;
-  const uint64_t g = g0 + threadIdx.x;
+  uint32_t slot = threadIdx.x;  // the group of this workgroup window this lane hashes
+#if B3_BALANCE
+  // Lane balance inside the window: a wave runs as long as its longest lane,
+  // and the last group of a multi-group chunk is usually partial (real layers:
+  // 10 % of the lanes idle).  When the window's groups differ in work, lanes
+  // take them in descending work order (counting sort over 64 buckets), so
+  // each wave holds groups of near-equal work.  The window's tree reduction
+  // is slot-based, so it is unaffected; uniform windows (C2) skip the sort.
+  {
+    __shared__ uint32_t hb[64], perm[256], key0;
+    constexpr int KS = D > 1 ? D - 1 : 0;  // <= 34 buckets for D <= 4
+    const uint64_t gs = g0 + threadIdx.x;
+    uint32_t key = 0;
+    if (gs < total && gs < cap_g) {
+      uint32_t cc, jj;
+      if (gs < gm) {
+        cc = gchunk[gs];
+        jj = (uint32_t)(gs - gbase[cc]);
+      } else {
+        cc = small[gs - gm];
+        jj = 0;
+      }
+      key = group_work<D>(chunks[cc].length, jj);
+    }
+    if (threadIdx.x == 0) key0 = key;
+    if (threadIdx.x < 64) hb[threadIdx.x] = 0;
+    __syncthreads();
+    if (!__syncthreads_and(key == key0)) {
+      const uint32_t b = 63 - min(63u, key >> KS);  // descending work
+      const uint32_t r = atomicAdd(&hb[b], 1u);
+      __syncthreads();
+      if (threadIdx.x < 64) {  // exclusive scan of the 64 bucket counts (wave 0)
+        const uint32_t v = hb[threadIdx.x];
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o, 64);
+          if ((int)threadIdx.x >= o) x += y;
+        }
+        hb[threadIdx.x] = x - v;
+      }
+      __syncthreads();
+      perm[hb[b] + r] = threadIdx.x;
+      __syncthreads();
+      slot = perm[threadIdx.x];
+    }
+  }
+#endif
+  const uint64_t g = g0 + slot;
   uint32_t cur[8], c = 0, j = 0;
   uint64_t base = 0, ng = 0;
   int st = 0;
@@ -531,7 +596,7 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
   uint32_t k = inwg ? (uint32_t)ng : 1;
   if (inwg) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) lcv[8 * threadIdx.x + i] = cur[i];
+    for (int i = 0; i < 8; ++i) lcv[8 * slot + i] = cur[i];
   }
   for (;;) {
     const bool active = k > 1;
