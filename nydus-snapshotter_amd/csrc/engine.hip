@@ -141,6 +141,18 @@ void free_dict(ngpu_engine *e) {
   e->dict_blobs.clear();
 }
 
+int ws_acquire(ngpu_engine *e, hipStream_t s) {
+  if (e->ws_pending && e->ws_last != s) HIP_TRY(e, hipStreamWaitEvent(s, e->ws_done, 0));
+  return 0;
+}
+
+int ws_release(ngpu_engine *e, hipStream_t s) {
+  HIP_TRY(e, hipEventRecord(e->ws_done, s));
+  e->ws_last = s;
+  e->ws_pending = true;
+  return 0;
+}
+
 // Digest stage: resets the layer stats, runs the digest kernels.
 int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
                    const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
@@ -148,6 +160,7 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
   const int D = pick_group_log2(e, len);
   int rc = ensure_workspace(e, n, len, D, e->dict.n_blobs, 1);
   if (rc) return rc;
+  if ((rc = ws_acquire(e, s))) return rc;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   // tuning override: flags bits 8..10 = 1 + BLAKE3 load mode (0 = default)
   const uint32_t lm = (e->cfg.flags >> 8) & 7;
@@ -174,6 +187,7 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
   }
   if (tm) HIP_TRY(e, hipEventRecord(ev[3], s));
   HIP_TRY(e, hipGetLastError());
+  if ((rc = ws_release(e, s))) return rc;
   return 0;
 }
 
@@ -186,6 +200,7 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_r
   if (!d_lfirst) L = 1;
   int rc = ensure_workspace(e, n, 0, 0, n_blobs, L);
   if (rc) return rc;
+  if ((rc = ws_acquire(e, s))) return rc;
   if (!d_stats) d_stats = e->ws.lstats;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   const uint32_t align = e->cfg.fs_version == 6 ? 4096u : 1u;
@@ -194,6 +209,7 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_r
   if (tm && e->tcalls) HIP_TRY(e, hipEventRecord(e->ev[e->tslot][4], s));
   HIP_TRY(e, hipGetLastError());
   if (tm && e->tcalls) e->timed[e->tslot] = n > 0;
+  if ((rc = ws_release(e, s))) return rc;
   return 0;
 }
 
@@ -272,7 +288,7 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
           ngpu_destroy(e);
           return NGPU_EHIP;
         }
-  if (
+  if (hipEventCreateWithFlags(&e->ws_done, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void **)&e->h_stats, 32 * sizeof(uint64_t), hipHostMallocDefault) !=
           hipSuccess) {
@@ -299,6 +315,7 @@ void ngpu_destroy(ngpu_engine *e) {
   for (auto &set : e->ev)
     for (auto ev : set)
       if (ev) (void)hipEventDestroy(ev);
+  if (e->ws_done) (void)hipEventDestroy(e->ws_done);
   if (e->stream) hipStreamDestroy(e->stream);
   delete e;
 }

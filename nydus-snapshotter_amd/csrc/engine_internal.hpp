@@ -37,6 +37,12 @@ struct ngpu_engine {
   int slot_D[kTimingRing] = {};
   uint64_t tcalls = 0;  // calls recorded so far; the current slot is (tcalls - 1) % ring
   int tslot = 0;
+  // Workspace ordering across streams: every stage that uses `ws` records
+  // ws_done on its stream; a stage on another stream waits for it first, so
+  // calls on different streams never run over one workspace concurrently.
+  hipEvent_t ws_done = nullptr;
+  hipStream_t ws_last = nullptr;
+  bool ws_pending = false;
   std::string err;
   std::mutex mu;
 };
@@ -55,6 +61,9 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_r
                   const ngpu_dict_hit *d_hits, uint32_t n_blobs, hipStream_t s,
                   const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats);
 int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st);
+// Order a workspace stage on stream s after the previous one (any stream).
+int ws_acquire(ngpu_engine *e, hipStream_t s);
+int ws_release(ngpu_engine *e, hipStream_t s);
 
 }  // namespace ngpu
 

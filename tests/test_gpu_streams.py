@@ -64,3 +64,48 @@ def test_bench_pool_digests_match_planted_chunks():
     r1 = np.zeros(1, oracle_py.CHUNK_DTYPE)
     r1["length"] = S
     assert np.array_equal(oracle_py.digest_chunks(one, r1, "blake3")[0], pd[1099])
+
+
+def test_calls_on_different_streams_share_the_workspace_in_order():
+    """Back-to-back device-path calls on two different streams (no host sync
+    between them) use one engine workspace: the engine orders each stage
+    after the previous one, so every call's results equal the oracle's."""
+    import nydus_gpu
+    import oracle_py
+    S = 64 << 10
+    layers = []
+    for seed in range(2):
+        rng = np.random.default_rng(40 + seed)
+        P = 900 + 300 * seed  # different chunk counts -> different plans / tiles
+        ch = np.zeros(P, nydus_gpu.CHUNK_DTYPE)
+        ch["length"] = rng.integers(1, S + 1, P)
+        ch["offset"] = np.arange(P, dtype=np.uint64) * S
+        dup = rng.choice(P, P // 5, replace=False)
+        ch["length"][dup] = S
+        data = rng.integers(0, 256, P * S, dtype=np.uint8)
+        for d in dup[1:]:  # identical full chunks -> INTRA
+            data[int(ch["offset"][d]):int(ch["offset"][d]) + S] = data[int(ch["offset"][dup[0]]):int(ch["offset"][dup[0]]) + S]
+        dig = oracle_py.digest_chunks(data, ch.view(oracle_py.CHUNK_DTYPE), "blake3")
+        dec, _ = oracle_py.dedup(dig, ch["length"])
+        layers.append((torch.from_numpy(data).cuda(), torch.from_numpy(ch.view(np.uint8).copy()).cuda(),
+                       P, dig, dec))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    eng = nydus_gpu.Engine(device=0, digester="blake3", chunk_size=S)
+    try:
+        torch.cuda.synchronize()
+        outs = []
+        for k in range(6):
+            d_data, d_ch, P, _, _ = layers[k % 2]
+            out = torch.zeros(P * 64, dtype=torch.uint8, device="cuda")
+            eng.process_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), P, out.data_ptr(),
+                               stream=streams[k % 2].cuda_stream)
+            outs.append((k % 2, out))
+        torch.cuda.synchronize()
+        for k, (li, out) in enumerate(outs):
+            _, _, P, dig, dec = layers[li]
+            got = out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+            assert np.array_equal(got["digest"], dig), k
+            for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+                assert np.array_equal(got[f], dec[f]), (k, f)
+    finally:
+        eng.close()
