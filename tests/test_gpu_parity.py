@@ -884,3 +884,47 @@ def test_many_tiles_multi_layer_vs_oracle(oracle):
         assert stats[l]["uncompressed_size"] == (ends.max() if new.any() else 0)
         assert stats[l]["own_blob_index"] == (0xFFFFFFFF if own is None else own)
         assert stats[l]["blobs"] == len(set(exp["blob_index"].tolist())), l
+
+
+@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 1023, 1024, 1025, 2047, 2048, 2049, 4097,
+                               64 * 1024 + 1, 512 * 1024 + 3])
+def test_scan_tile_boundaries_vs_oracle(engines, oracle, n):
+    """Chunk counts at the single-pass scans' tile edges (256, 1024, 2048 and
+    the 512-tile look-back window): decisions, indices and offsets equal the
+    oracle's, for the single-layer path and a 3-layer call."""
+    import torch
+    rng = np.random.default_rng(n)
+    data = rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes()
+    ch = np.zeros(n, nydus_gpu.CHUNK_DTYPE)
+    ch["length"] = rng.integers(1, 2500, n)
+    ch["offset"] = rng.integers(0, len(data) - 2500, n)
+    dup = rng.random(n) < 0.3
+    src = rng.integers(0, n, n)
+    ch["offset"][dup], ch["length"][dup] = ch["offset"][src[dup]], ch["length"][src[dup]]
+    dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    dec, _ = oracle.dedup(dig, ch["length"])
+    out, st = engines("blake3", 0x100000).process(data, ch)
+    assert np.array_equal(out["digest"], dig)
+    for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+        assert np.array_equal(out[f], dec[f]), f
+    # three layers, the middle one empty when n allows a cut
+    cut = n // 2
+    first = np.array([0, cut, cut, n], dtype=np.int64)
+    eng = engines("blake3", 0x100000)
+    d_data, d_ch = _to_dev(np.frombuffer(data, np.uint8)), _to_dev(ch)
+    d_first = torch.from_numpy(first.copy()).cuda()
+    d_out = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    d_st = torch.zeros(3 * nydus_gpu.LAYER_STATS_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    eng.process_layers_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), n, d_out.data_ptr(),
+                              d_first.data_ptr(), 3, d_st.data_ptr())
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+    stats = d_st.cpu().numpy().view(nydus_gpu.LAYER_STATS_DTYPE)
+    for l in range(3):
+        a, b = int(first[l]), int(first[l + 1])
+        exp, _ = oracle.dedup(dig[a:b], ch["length"][a:b])
+        for f in ("kind", "index", "blob_index", "uncompressed_offset"):
+            assert np.array_equal(got[a:b][f], exp[f]), (l, f)
+        assert stats[l]["chunks"] == b - a
+        assert stats[l]["new_chunks"] == (exp["kind"] == 0).sum()
+        assert stats[l]["intra_chunks"] == (exp["kind"] == 1).sum()
