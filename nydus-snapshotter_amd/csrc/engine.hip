@@ -315,6 +315,14 @@ void ngpu_destroy(ngpu_engine *e) {
   for (auto &set : e->ev)
     for (auto ev : set)
       if (ev) (void)hipEventDestroy(ev);
+  for (auto &b : e->staging_pool) {
+    if (b.h) (void)hipHostFree(b.h);
+    if (b.h_ch) (void)hipHostFree(b.h_ch);
+    if (b.d) (void)hipFree(b.d);
+    if (b.d_ch) (void)hipFree(b.d_ch);
+    if (b.copied) (void)hipEventDestroy(b.copied);
+    if (b.done) (void)hipEventDestroy(b.done);
+  }
   if (e->ws_done) (void)hipEventDestroy(e->ws_done);
   if (e->stream) hipStreamDestroy(e->stream);
   delete e;

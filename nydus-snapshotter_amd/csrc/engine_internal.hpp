@@ -8,6 +8,15 @@
 
 #include "common.hpp"
 
+// Pinned staging + device buffers of one streaming-Pack slot, kept by the
+// engine between packs (pinning 64 MiB costs milliseconds: per-pack
+// allocation cost the streaming path a third of its rate).
+struct ngpu_staging_buf {
+  void *h = nullptr, *h_ch = nullptr, *d = nullptr, *d_ch = nullptr;
+  hipEvent_t copied = nullptr, done = nullptr;
+  uint64_t cap = 0;
+};
+
 struct ngpu_engine {
   ngpu_config cfg{};
   int device = 0;
@@ -43,6 +52,8 @@ struct ngpu_engine {
   hipEvent_t ws_done = nullptr;
   hipStream_t ws_last = nullptr;
   bool ws_pending = false;
+  std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu
+  std::mutex pool_mu;
   std::string err;
   std::mutex mu;
 };

@@ -171,6 +171,16 @@ void release(ngpu_pack *p) {
   }
   if (p->copy) (void)hipStreamSynchronize(p->copy);
   (void)hipStreamSynchronize(p->e->stream);
+  {
+    std::lock_guard<std::mutex> g(p->e->pool_mu);
+    for (Slot &s : p->slot) {
+      if (!s.h || !s.h_ch || !s.d_ch || !s.copied || !s.done ||
+          p->e->staging_pool.size() >= 4)
+        continue;
+      p->e->staging_pool.push_back({s.h, s.h_ch, s.d, s.d_ch, s.copied, s.done, p->cap});
+      s = Slot{};
+    }
+  }
   for (Slot &s : p->slot) {
     if (s.h) (void)hipHostFree(s.h);
     if (s.h_ch) (void)hipHostFree(s.h_ch);
@@ -399,7 +409,29 @@ int ngpu_pack_open_ex(ngpu_engine *e, uint32_t flags, ngpu_pack **out) {
   p->cap = cap;
   p->max_ch = cap / 1024 + 16;  // a chunk costs >= 1 KiB of tar stream unless it is a file's last
   bool ok = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking) == hipSuccess;
+  {
+    std::lock_guard<std::mutex> pg(e->pool_mu);
+    for (Slot &s : p->slot) {
+      auto &pool = e->staging_pool;
+      for (size_t i = 0; i < pool.size(); ++i) {
+        if (pool[i].cap != cap) continue;
+        const ngpu_staging_buf b = pool[i];
+        pool.erase(pool.begin() + (long)i);
+        s.h = (uint8_t *)b.h;
+        s.h_ch = (ngpu_chunk *)b.h_ch;
+        s.d = (uint8_t *)b.d;
+        s.d_ch = (ngpu_chunk *)b.d_ch;
+        s.copied = b.copied;
+        s.done = b.done;
+        break;
+      }
+    }
+  }
   for (Slot &s : p->slot) {
+    if (s.h) {  // from the engine's pool: only the device copy may be missing
+      if (!p->retain && !s.d) ok = ok && hipMalloc((void **)&s.d, cap) == hipSuccess;
+      continue;
+    }
     ok = ok && hipHostMalloc((void **)&s.h, cap, hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc((void **)&s.h_ch, p->max_ch * sizeof(ngpu_chunk), hipHostMallocDefault) ==
              hipSuccess &&
