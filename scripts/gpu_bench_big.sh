@@ -7,7 +7,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
-for W in c5-1000 c4 c3-64k; do
+for W in c5-1000 c4 c4-16 c3-64k; do
   timeout -k 10 400 python bench.py --workload $W --steps 10 --warmup 5 --no-e2e \
     > "$OUT/$W.json" 2>>"$OUT/err" || exit $?
   python3 -c "import json,sys; d=json.load(open('$OUT/$W.json')); print('$W', d['value'], d['ms_per_step'], d['stage_ms'], d['roofline']['frac'], d.get('decisions'))"
