@@ -522,6 +522,64 @@ def test_streaming_pack_errors(tars):
         eng.close()
 
 
+def test_staging_pool_reuse_across_packs(golden_layers, tars, oracle):
+    """The engine keeps streaming-Pack staging slots between packs (pack.hip
+    release / ngpu_pack_open_ex). Slots move between plain and retained packs
+    (a retained pack leaves no device copy behind), survive an aborted pack and
+    are shared by two packs open at once; every result still equals
+    pack_tar / the host writer fed with the oracle's decisions."""
+    import io as _io
+    from test_blob import cpu_stream
+    rng = np.random.default_rng(31)
+    cases = [c for c in golden_layers["cases"] if c["chunk_size"] == 0x10000]
+    assert cases
+    case = cases[0]
+    cs, dg = case["chunk_size"], case["digester"]
+    names = sorted(tars)
+    tb, tb2 = tars[case["layer"]], tars[names[0] if names[0] != case["layer"] else names[1]]
+    eng = nydus_gpu.Engine(digester=dg, chunk_size=cs, staging_bytes=4 * cs)
+    try:
+        ref, ref2 = eng.pack_tar(tb), eng.pack_tar(tb2)
+
+        def same(got, want):
+            assert got[0].tobytes() == want[0].tobytes()
+            assert got[1].tobytes() == want[1].tobytes()
+            assert got[2] == want[2]
+
+        def retained(t):
+            w = eng.pack(retain=True)
+            w.write(t)
+            out = _io.BytesIO()
+            ch, res, st, info = w.finish(out, compressor="none")
+            want = cpu_stream(oracle, t, cs, "none", dg)
+            assert ch.tobytes() == want[2].tobytes()
+            assert out.getvalue() == want[0]
+
+        for rnd in range(3):
+            same(_stream(eng, tb, rng, rnd % 2 == 1), ref)
+            retained(tb)
+            same(_stream(eng, tb, rng, False), ref)  # slots from the retained pack
+            w = eng.pack()
+            w.write(tb[: len(tb) // 2])
+            w.abort()
+            same(_stream(eng, tb2, rng, True), ref2)
+            # two packs open at once, writes interleaved
+            wa, wb = eng.pack(), eng.pack()
+            pa = pb = 0
+            while pa < len(tb) or pb < len(tb2):
+                k = int(rng.integers(1, 200_000))
+                if pa < len(tb):
+                    wa.write(tb[pa:pa + k])
+                    pa += k
+                if pb < len(tb2):
+                    wb.write(tb2[pb:pb + k])
+                    pb += k
+            same(wb.close(), ref2)
+            same(wa.close(), ref)
+    finally:
+        eng.close()
+
+
 def test_multi_layer_dedup_matches_per_layer(oracle):
     """One launch set over 40 layers == each layer packed alone (oracle per
     layer), with a shared chunk dict and cross-layer duplicate contents."""
