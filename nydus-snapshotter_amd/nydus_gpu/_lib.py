@@ -45,7 +45,7 @@ RESULT_DTYPE = np.dtype([("digest", "u1", (32,)), ("kind", "<u4"), ("index", "<u
                          ("uncompressed_offset", "<u8")])
 assert CHUNK_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 64
 
-# Every symbol include/nydus_gpu.h declares (checked by tests/test_abi.py).
+# Every symbol include/nydus_gpu.h declares (checked by tests/test_host.py).
 EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_device_count", "ngpu_alloc_pinned", "ngpu_free_pinned", "ngpu_dict_load",
            "ngpu_dict_load_bootstrap", "ngpu_dict_clear", "ngpu_dict_size", "ngpu_tar_chunks",
