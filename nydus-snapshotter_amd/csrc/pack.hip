@@ -488,7 +488,13 @@ int ngpu_pack_write(ngpu_pack *p, const void *buf, uint64_t len) {
     if (take >= (8ull << 20)) {
       if (!p->pool) {
         unsigned hw = std::thread::hardware_concurrency();
-        p->pool = new CopyPool(hw >= 16 ? 7 : (hw > 2 ? hw / 2 - 1 : 1));
+        unsigned nt = hw >= 16 ? 7 : (hw > 2 ? hw / 2 - 1 : 1);
+        // NGPU_COPY_THREADS: helper threads besides the caller (tuning knob)
+        if (const char *v = getenv("NGPU_COPY_THREADS")) {
+          const long x = strtol(v, nullptr, 10);
+          if (x >= 1 && x <= 63) nt = (unsigned)x;
+        }
+        p->pool = new CopyPool(nt);
       }
       p->pool->copy((uint8_t *)dst, b, take);
     } else {
