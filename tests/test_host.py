@@ -171,3 +171,24 @@ def test_tar_scanner_fuzz_agrees_with_oracle(tars, oracle):
             assert got.tobytes() == ref.tobytes(), it
             agree += 1
     assert agree > 50
+
+
+def test_product_never_reaches_the_oracle():
+    """The shipped path (Python mirror, C ABI sources, built libraries) neither
+    imports nor links anything under oracle/: the oracle is only the checker."""
+    pkg = os.path.join(ROOT, "nydus-snapshotter_amd")
+    bad = re.compile(r"import\s+oracle|oracle_py|liboracle|oracle/\S+\.so")
+    hits = []
+    for d, _, files in os.walk(pkg):
+        if "build" in d.split(os.sep) or "__pycache__" in d:
+            continue
+        for f in files:
+            p = os.path.join(d, f)
+            if f.endswith((".py", ".hip", ".cpp", ".hpp", ".h")) or f == "Makefile":
+                for i, line in enumerate(open(p, errors="replace"), 1):
+                    if bad.search(line) and not line.lstrip().startswith(("//", "#")):
+                        hits.append(f"{p}:{i}: {line.strip()}")
+            elif f.endswith(".so"):
+                if b"liboracle" in open(p, "rb").read():
+                    hits.append(p)
+    assert not hits, hits
