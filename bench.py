@@ -316,6 +316,7 @@ def main():
     ap.add_argument("--dict-entries", type=int, default=0, help="override dict size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--e2e-mib", type=int, default=2048, help="PCIe-inclusive sample size")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on a node; gloo to "
                     "rehearse several ranks on one GPU")
     ap.add_argument("--pmc-json", default="", help="PMC summary for roofline.traffic "
@@ -531,7 +532,7 @@ def main():
 
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e and not wl.get("dict_entries"):
-        e2e = end_to_end(torch, nydus_gpu, buf, wl, stride, local)
+        e2e = end_to_end(torch, nydus_gpu, buf, wl, stride, local, sample_bytes=args.e2e_mib << 20)
 
     roof["traffic"], roof["traffic_source"] = pmc_traffic(args.pmc_json, args.workload, roof["kernel"])
 
