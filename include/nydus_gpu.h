@@ -21,6 +21,11 @@
  *
  * Threading: an engine serialises its own calls internally; use one engine
  * per goroutine pool / per device for concurrency.
+ *
+ * Lifetimes: engines, chunk dicts and packs are reference counted.  A pack
+ * holds its engine and the dict it was opened with until it ends (close,
+ * finish or abort), so ngpu_destroy / ngpu_dict_release with packs still open
+ * only drop the caller's reference; the memory goes when the last pack ends.
  */
 #ifndef NYDUS_GPU_H
 #define NYDUS_GPU_H
@@ -32,7 +37,7 @@
 extern "C" {
 #endif
 
-#define NGPU_ABI_VERSION 1
+#define NGPU_ABI_VERSION 2
 
 /* PackOption.Digester (API extension; maps to nydus-image --digester). */
 enum ngpu_digester { NGPU_DIGEST_BLAKE3 = 0, NGPU_DIGEST_SHA256 = 1 };
@@ -54,8 +59,11 @@ enum ngpu_error {
   NGPU_ENODEV = -6,    /* no usable gfx950 device */
   NGPU_EIO = -7,       /* file I/O (chunk-dict bootstrap) */
   NGPU_EFORMAT = -8,   /* not a RAFS v6 bootstrap / bad chunk table */
-  NGPU_ENOTFOUND = -9  /* entry not found in a nydus blob (ErrNotFound,
+  NGPU_ENOTFOUND = -9, /* entry not found in a nydus blob (ErrNotFound,
                           pkg/converter/types.go:33-35) */
+  NGPU_ECANCELED = -10 /* cancelled through the pack's cancel flag (the
+                          reference's ctx.Done() / PackOption.Timeout kill of
+                          the builder, builder.go:153-174) */
 };
 
 typedef struct ngpu_engine ngpu_engine;
@@ -69,7 +77,8 @@ typedef struct {
                              [0x1000, 0x1000000] (types.go:76); 0 -> 0x100000 */
   uint32_t fs_version;    /* PackOption.FsVersion 5 or 6; 0 -> 6
                              (builder.go:79-81).  v6 aligns uncompressed
-                             offsets of NEW chunks to 4 KiB. */
+                             offsets of NEW chunks to 4 KiB (v5 with
+                             NGPU_FLAG_ALIGNED_CHUNK). */
   uint64_t staging_bytes; /* pinned staging slot size for host-buffer calls;
                              0 -> 256 MiB (two slots are allocated) */
   uint32_t leaves_per_lane; /* BLAKE3 tuning: 1 KiB leaves hashed per lane
@@ -79,12 +88,17 @@ typedef struct {
 
 /* ngpu_config.flags */
 #define NGPU_FLAG_TIMING 0x1u /* record HIP events around each stage */
+/* PackOption.AlignedChunk (types.go:73-74, `--aligned-chunk`, builder.go:131-133):
+ * 4 KiB-align the uncompressed offsets of NEW chunks for RAFS v5 too (v6
+ * always aligns). */
+#define NGPU_FLAG_ALIGNED_CHUNK 0x2u
 /* Tuning (benchmarks only): bits 8..10 = 1 + BLAKE3 load mode
  * (bit0 non-temporal loads, bit1 next-block prefetch); 0 = library default. */
 #define NGPU_FLAG_LOAD_MODE_SHIFT 8
 /* Tuning (benchmarks only): bits 11..13 = 1 + SHA-256 kernel (0: one lane per
- * chunk, 1: two lanes per chunk, 2/3: diagnostics with wrong digests);
- * 0 = library default (by chunk count). */
+ * chunk, 1: two lanes per chunk, 4: two lanes, one chunk group per
+ * workgroup, 5: two lanes, four groups per workgroup); 0 = library default
+ * (by chunk count); other values are rejected (NGPU_EINVAL). */
 #define NGPU_FLAG_SHA_MODE_SHIFT 11
 
 /* Per-stage device time of the last process call (NGPU_FLAG_TIMING). */
@@ -118,7 +132,9 @@ typedef struct {
   uint32_t blob_index;  /* real blob index, allocated in first-hit order */
   uint32_t dict_blob;   /* DICT: the entry's inner blob index in the chunk
                            dict (its blob table); otherwise 0 */
-  uint64_t uncompressed_offset; /* NEW/INTRA: offset in the layer blob */
+  uint64_t uncompressed_offset; /* NEW/INTRA: offset in the layer blob;
+                           DICT: the dict chunk's offset in ITS blob (nydus
+                           copies the cached chunk, chunk.copy_from) */
 } ngpu_result;
 
 /* Summary of one layer. */
@@ -144,16 +160,53 @@ int ngpu_device_count(void);
 int ngpu_alloc_pinned(ngpu_engine *eng, uint64_t bytes, void **out);
 int ngpu_free_pinned(ngpu_engine *eng, void *ptr);
 
-/* ---- chunk dict (PackOption.ChunkDictPath; builder.go:122-124) ---------- */
-/* Load n dict entries in chunk-table order into an HBM-resident hash table.
- * First entry wins for duplicate digests.  usize == 0 matches any size.
- * blob_index: the dict's inner blob index per entry; chunk_index: the
- * entry's RAFS chunk index (copied into DICT results). */
+/* ---- chunk dict handles (PackOption.ChunkDictPath; builder.go:122-124) ----
+ * The reference runs one nydus-image process per Pack, each loading its own
+ * `--chunk-dict bootstrap=P` ([nydus v2.3.0] HashChunkDict).  Here a dict is
+ * an HBM-resident, read-only, reference-counted object: a Pack captures the
+ * dict it is opened with, so packs with different dicts (or none) can be open
+ * on one engine at once, and 1000 Packs against one ChunkDictPath share one
+ * loaded table.  First table entry wins for duplicate digests; usize == 0
+ * matches any chunk size.
+ *
+ * ngpu_dict_open: load the chunk table (80-B records at the extended
+ * superblock's chunk_table_offset, pkg/layout/layout.go:25-27) and the blob
+ * table of a RAFS v6 bootstrap on the engine's device.  Rejected with
+ * NGPU_EINVAL, as nydus-image rejects an incompatible chunk-dict bootstrap
+ * ([nydus v2.3.0] RafsSuperConfig::check_compatibility, VERIFY): a digester
+ * flag (RafsSuperFlags HASH_BLAKE3 0x4 / HASH_SHA256 0x8) or chunk_size that
+ * differs from the engine's, or an engine with FsVersion 5.  The engine
+ * caches the dicts it opened by (path, device, inode, size, mtime): opening an
+ * unchanged file again returns the same dict with one more reference. */
+typedef struct ngpu_dict ngpu_dict;
+int ngpu_dict_open(ngpu_engine *eng, const char *path, ngpu_dict **out);
+/* From a chunk table in memory: n 80-B RAFS v6 chunk-info records (table
+ * order) and n_blobs 256-B RAFS v6 blob records (inner-index order; may be
+ * NULL / 0, the blob count is then max(blob_index) + 1). */
+int ngpu_dict_create(ngpu_engine *eng, const void *records, uint64_t n,
+                     const void *blob_table, uint32_t n_blobs, ngpu_dict **out);
+/* From device-resident arrays (entry order = table order), e.g. a 200M-entry
+ * dict built on the GPU.  d_uoff (u64 uncompressed offsets) may be NULL. */
+int ngpu_dict_create_device(ngpu_engine *eng, const uint8_t *d_digests, const uint32_t *d_usize,
+                            const uint32_t *d_blob_index, const uint32_t *d_chunk_index,
+                            const uint64_t *d_uoff, uint64_t n, uint32_t n_blobs,
+                            ngpu_dict **out);
+void ngpu_dict_retain(ngpu_dict *d);
+void ngpu_dict_release(ngpu_dict *d);
+uint64_t ngpu_dict_entries(const ngpu_dict *d);
+/* The engine's default dict, used by the calls without a dict argument
+ * (ngpu_process*, ngpu_pack_open*, ngpu_dict_probe_device) and captured by a
+ * pack when it opens.  NULL = no dict.  Takes a reference. */
+int ngpu_set_dict(ngpu_engine *eng, ngpu_dict *d);
+
+/* Legacy default-dict loaders (each = create + ngpu_set_dict + release).
+ * Replacing the default never changes the dict of a pack already open.
+ * ngpu_dict_load: n entries in chunk-table order; blob_index: inner blob index
+ * per entry; chunk_index: the entry's RAFS chunk index (copied into DICT
+ * results); compressed placement unknown (csize = usize, offsets 0). */
 int ngpu_dict_load(ngpu_engine *eng, const uint8_t *digests /* n x 32 */,
                    const uint32_t *usize, const uint32_t *blob_index,
                    const uint32_t *chunk_index, uint64_t n);
-/* Parse a RAFS v6 bootstrap's chunk table (80-B records at the extended
- * superblock's chunk_table_offset; pkg/layout/layout.go:25-27) and load it. */
 int ngpu_dict_load_bootstrap(ngpu_engine *eng, const char *path);
 int ngpu_dict_clear(ngpu_engine *eng);
 uint64_t ngpu_dict_size(const ngpu_engine *eng);
@@ -199,7 +252,8 @@ typedef struct {
   uint32_t index;  /* the entry's RAFS chunk index */
   uint32_t blob;   /* the entry's inner blob index */
   uint32_t usize;  /* the entry's uncompressed size (0 = any) */
-} ngpu_dict_hit;
+  uint64_t uncompressed_offset; /* the entry's offset in its blob */
+} ngpu_dict_hit;   /* 24 bytes */
 
 int ngpu_digest_device(ngpu_engine *eng, const void *d_data, uint64_t len,
                        const ngpu_chunk *d_chunks, uint64_t n,
@@ -231,11 +285,28 @@ int ngpu_process_layers_device(ngpu_engine *eng, const void *d_data, uint64_t le
                                const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
                                const uint64_t *d_layer_first, uint64_t n_layers,
                                ngpu_layer_stats *d_stats, void *stream);
-/* Build the dict from device-resident arrays (entry order = table order). */
+/* Build the default dict from device-resident arrays (entry order = table
+ * order); = ngpu_dict_create_device + ngpu_set_dict. */
 int ngpu_dict_load_device(ngpu_engine *eng, const uint8_t *d_digests,
                           const uint32_t *d_usize, const uint32_t *d_blob_index,
                           const uint32_t *d_chunk_index, uint64_t n,
                           uint32_t n_blobs);
+
+/* The same against an explicit dict (NULL = no chunk dict) instead of the
+ * engine's default.  ngpu_process_dict_device: d_layer_first NULL = one layer
+ * of n chunks (n_layers ignored); d_stats: device ngpu_layer_stats[n_layers]
+ * or NULL; stats: host, as in ngpu_process_device (synchronises), one-layer
+ * calls only. */
+int ngpu_dict_probe(const ngpu_dict *dict, const uint8_t *d_digests, uint64_t stride,
+                    uint64_t n, ngpu_dict_hit *d_hits, void *stream);
+int ngpu_process_dict(ngpu_engine *eng, ngpu_dict *dict, const void *data, uint64_t len,
+                      const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
+                      ngpu_layer_stats *stats);
+int ngpu_process_dict_device(ngpu_engine *eng, ngpu_dict *dict, const void *d_data,
+                             uint64_t len, const ngpu_chunk *d_chunks, uint64_t n,
+                             ngpu_result *d_out, const uint64_t *d_layer_first,
+                             uint64_t n_layers, ngpu_layer_stats *d_stats, void *stream,
+                             ngpu_layer_stats *stats);
 
 /* Whole tar layer in host memory -> chunk list + results (tar parse on the
  * host, digest/dedup on the GPU).  *chunks_out / *results_out are allocated
@@ -262,9 +333,21 @@ int ngpu_timing_at(ngpu_engine *eng, uint32_t back, ngpu_timing *out);
  * digested while the caller keeps writing; dedup runs at close in stream
  * order.  close (success or not) and abort release the pack; *chunks_out /
  * *results_out are malloc'd (ngpu_free_host).  A malformed or truncated tar
- * fails with NGPU_ETAR / NGPU_EUNSUPP at write/commit or close. */
+ * fails with NGPU_ETAR / NGPU_EUNSUPP at write/commit or close.
+ * A pack dedups against the dict it was opened with: ngpu_pack_open* take the
+ * engine's default dict at open time, ngpu_pack_open_dict an explicit one
+ * (NULL = none; its digester and chunk size must be the engine's). */
 typedef struct ngpu_pack ngpu_pack;
 int ngpu_pack_open(ngpu_engine *eng, ngpu_pack **out);
+int ngpu_pack_open_dict(ngpu_engine *eng, ngpu_dict *dict, uint32_t flags, ngpu_pack **out);
+/* Cancellation (ctx.Done() / PackOption.Timeout): `flag` is caller-owned
+ * memory that must outlive the pack; once another thread stores a non-zero
+ * value there, the pack's next write / commit / reserve, or the running
+ * close / finish at its next slot, blob window or compression batch, fails
+ * with NGPU_ECANCELED and releases the pack (the reference kills the
+ * builder process, builder.go:153-174, convert_unix.go:530-535).  NULL
+ * removes the flag. */
+int ngpu_pack_set_cancel(ngpu_pack *p, const volatile int32_t *flag);
 int ngpu_pack_write(ngpu_pack *p, const void *buf, uint64_t len);
 int ngpu_pack_reserve(ngpu_pack *p, void **ptr, uint64_t *avail);
 int ngpu_pack_commit(ngpu_pack *p, uint64_t n);
@@ -288,7 +371,9 @@ int ngpu_chunk_table(const ngpu_chunk *chunks, const ngpu_result *results,
  * (convert_unix.go:486-495): `data | tar_header | ... | toc | tar_header`
  * (convert_unix.go:296-300).  Entries: image.blob (the layer's NEW chunks in
  * index order, each compressed on its own, raw when compression does not
- * shrink it), image.boot (RAFS v6 bootstrap: blob table + chunk table),
+ * shrink it), image.boot (RAFS v6 bootstrap: blob table + chunk table: one
+ * record per distinct chunk the layer references -- its NEW chunks and the
+ * chunk-dict chunks it reuses, copied with their dict blob placement),
  * rafs.blob.toc (128-B TOCEntry records, types.go:147-163).  Compression and
  * SHA-256 run on the host (north star: compression stays on the host path). */
 
@@ -313,20 +398,28 @@ typedef struct {
   uint32_t n_dict_blobs; /* records in dict_blobs */
   const uint8_t *dict_blobs; /* the chunk dict's blob table (n x 256-B RAFS v6
                                 blob records, inner-index order), or NULL;
-                                ngpu_pack_finish defaults to the table
-                                ngpu_dict_load_bootstrap read */
+                                ngpu_pack_finish defaults to the blob table of
+                                the pack's dict */
+  const void *dict_chunks;   /* ngpu_blob_write: the chunk dict's chunk table
+                                (80-B RAFS v6 records, entry order) the DICT
+                                results' `ref` index, for the compressed
+                                placement their records copy; NULL: csize =
+                                usize, offset 0.  ngpu_pack_finish uses the
+                                pack's dict */
+  uint64_t n_dict_chunks;
 } ngpu_blob_options;
 
 typedef struct {
   uint64_t stream_bytes;      /* bytes written to dest */
   uint64_t blob_bytes;        /* image.blob: compressed chunk data */
   uint64_t bootstrap_bytes;   /* image.boot */
-  uint64_t blob_chunks;       /* chunk records in the bootstrap (NEW chunks) */
+  uint64_t blob_chunks;       /* chunk records of the layer's own blob (NEW) */
   uint64_t compressed_chunks; /* of which stored compressed */
   uint8_t stream_digest[32];  /* sha256 of the whole stream: the layer blob
                                  digest (LayerConvertFunc, convert_unix.go:870-914) */
   uint8_t blob_digest[32];    /* sha256 of image.blob (the own blob's id) */
   uint8_t toc_digest[32];     /* sha256 of the TOC (calcBlobTOCDigest :541-555) */
+  uint64_t dict_records;      /* chunk records copied from the chunk dict */
 } ngpu_blob_info;
 
 /* Thread-local message of the last failing engine-less call below. */

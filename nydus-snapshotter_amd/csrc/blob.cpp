@@ -35,11 +35,13 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <set>
 #include <thread>
 
 #include "blob.hpp"
@@ -61,11 +63,23 @@ int host_fail(int code, const char *fmt, ...) {
 }
 
 // ---- compressors ----------------------------------------------------------
+struct ZInBuf {  // ZSTD_inBuffer
+  const void *src;
+  size_t size, pos;
+};
+struct ZOutBuf {  // ZSTD_outBuffer
+  void *dst;
+  size_t size, pos;
+};
+
 struct Codecs {
   size_t (*zstd_compress)(void *, size_t, const void *, size_t, int) = nullptr;
   size_t (*zstd_decompress)(void *, size_t, const void *, size_t) = nullptr;
   size_t (*zstd_bound)(size_t) = nullptr;
   unsigned (*zstd_is_error)(size_t) = nullptr;
+  void *(*zstd_create_dstream)() = nullptr;
+  size_t (*zstd_free_dstream)(void *) = nullptr;
+  size_t (*zstd_decompress_stream)(void *, ZOutBuf *, ZInBuf *) = nullptr;
   int (*lz4_compress)(const char *, char *, int, int) = nullptr;
   int (*lz4_bound)(int) = nullptr;
 };
@@ -79,6 +93,10 @@ const Codecs &codecs() {
       c.zstd_decompress = (decltype(c.zstd_decompress))dlsym(z, "ZSTD_decompress");
       c.zstd_bound = (decltype(c.zstd_bound))dlsym(z, "ZSTD_compressBound");
       c.zstd_is_error = (decltype(c.zstd_is_error))dlsym(z, "ZSTD_isError");
+      c.zstd_create_dstream = (decltype(c.zstd_create_dstream))dlsym(z, "ZSTD_createDStream");
+      c.zstd_free_dstream = (decltype(c.zstd_free_dstream))dlsym(z, "ZSTD_freeDStream");
+      c.zstd_decompress_stream =
+          (decltype(c.zstd_decompress_stream))dlsym(z, "ZSTD_decompressStream");
     }
     if (void *l = dlopen("liblz4.so.1", RTLD_NOW | RTLD_LOCAL)) {
       c.lz4_compress = (decltype(c.lz4_compress))dlsym(l, "LZ4_compress_default");
@@ -333,6 +351,9 @@ struct BlobWriter::Impl {
   ngpu_write_fn w;
   void *ctx;
   std::vector<RafsV6BlobInfo> dict_blobs;
+  const DictPlace *dict_place = nullptr;
+  uint64_t n_place = 0;
+  const volatile int32_t *cancel = nullptr;
   std::unique_ptr<Pool> pool;
   Sha blob_sha;      // image.blob data
   Sha stream_sha;    // whole stream (continued from blob_sha)
@@ -420,14 +441,19 @@ struct BlobWriter::Impl {
 };
 
 BlobWriter::BlobWriter(const ngpu_blob_options &opt, ngpu_write_fn w, void *ctx,
-                       std::vector<RafsV6BlobInfo> dict_blobs)
+                       std::vector<RafsV6BlobInfo> dict_blobs, const DictPlace *dict_place,
+                       uint64_t n_place)
     : im_(new Impl) {
   im_->opt = opt;
   if (!im_->opt.compressor) im_->opt.compressor = NGPU_COMPRESSOR_ZSTD;
   im_->w = w;
   im_->ctx = ctx;
   im_->dict_blobs = std::move(dict_blobs);
+  im_->dict_place = dict_place;
+  im_->n_place = dict_place ? n_place : 0;
 }
+
+void BlobWriter::set_cancel(const volatile int32_t *flag) { im_->cancel = flag; }
 
 BlobWriter::~BlobWriter() = default;
 
@@ -458,6 +484,8 @@ int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) 
   // batches of <= 64 MiB of input keep the scratch bounded
   uint64_t a = 0;
   while (a < k) {
+    if (m.cancel && __atomic_load_n(m.cancel, __ATOMIC_RELAXED))
+      return m.rc = host_fail(NGPU_ECANCELED, "pack: cancelled");
     uint64_t b = a, bytes = 0;
     while (b < k && (b == a || bytes + len[b] <= (64ull << 20))) bytes += len[b++];
     const uint64_t nb = b - a;
@@ -545,6 +573,54 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
   if (k != m.csize.size()) return host_fail(NGPU_EINVAL, "pack: %llu chunk bodies for %llu NEW chunks",
                                             (unsigned long long)m.csize.size(),
                                             (unsigned long long)k);
+  // Chunk-dict chunks the layer reuses: one record per distinct (digest, real
+  // blob), a copy of the dict's record ([nydus v2.3.0] deduplicate_chunk:
+  // chunk.copy_from(cached_chunk) + set_file_offset + the real blob index;
+  // the v6 chunk table holds every distinct chunk a node references, keyed
+  // by digest and blob index -- VERIFY), first occurrence in stream order.
+  uint64_t ndict = 0;
+  {
+    std::vector<std::pair<std::array<uint8_t, 32>, uint32_t>> seen;
+    std::vector<uint64_t> order;
+    for (uint64_t i = 0; i < n; ++i)
+      if (res[i].kind == NGPU_DICT) order.push_back(i);
+    std::sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) {
+      const int c = memcmp(res[x].digest, res[y].digest, 32);
+      if (c) return c < 0;
+      if (res[x].blob_index != res[y].blob_index) return res[x].blob_index < res[y].blob_index;
+      return x < y;
+    });
+    std::vector<uint64_t> firsts;
+    for (size_t j = 0; j < order.size(); ++j) {
+      const uint64_t i = order[j];
+      if (j && memcmp(res[order[j - 1]].digest, res[i].digest, 32) == 0 &&
+          res[order[j - 1]].blob_index == res[i].blob_index)
+        continue;
+      firsts.push_back(i);
+    }
+    std::sort(firsts.begin(), firsts.end());
+    for (uint64_t i : firsts) {
+      const ngpu_result &r = res[i];
+      RafsV6ChunkInfo c;
+      memset(&c, 0, sizeof c);
+      memcpy(c.block_id, r.digest, 32);
+      c.blob_index = r.blob_index;
+      c.uncompressed_size = chunks[i].length;
+      if (r.ref < m.n_place) {
+        const DictPlace &pl = m.dict_place[r.ref];
+        c.flags = pl.flags;
+        c.compressed_size = pl.compressed_size;
+        c.compressed_offset = pl.compressed_offset;
+      } else {  // dict given without its chunk records: stored raw
+        c.compressed_size = chunks[i].length;
+      }
+      c.uncompressed_offset = r.uncompressed_offset;
+      c.file_offset = chunks[i].file_offset;
+      c.index = r.index;
+      b.chunks.push_back(c);
+      ++ndict;
+    }
+  }
   // blob table in real-index (first-hit) order
   b.blobs.assign(st.blobs, RafsV6BlobInfo{});
   std::vector<bool> set(st.blobs, false);
@@ -617,6 +693,7 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     info->bootstrap_bytes = boot.size();
     info->blob_chunks = k;
     info->compressed_chunks = m.compressed_chunks;
+    info->dict_records = ndict;
     memcpy(info->stream_digest, stream_dig, 32);
     memcpy(info->blob_digest, blob_dig, 32);
     memcpy(info->toc_digest, toc_dig, 32);
@@ -686,6 +763,47 @@ int copy_range(const Reader &r, uint64_t off, uint64_t len, ngpu_write_fn w, voi
   return 0;
 }
 
+// The zstd-compressed TOC entry at [off, off+len): decompressed as a stream
+// (the reference reads it through zstd.NewReader over a SectionReader,
+// convert_unix.go:255-270), so neither size field of an untrusted TOC sizes
+// an allocation.
+int copy_zstd(const Reader &r, uint64_t off, uint64_t len, const char *name, ngpu_write_fn w,
+              void *wctx) {
+  const Codecs &c = codecs();
+  if (!c.zstd_create_dstream || !c.zstd_decompress_stream || !c.zstd_free_dstream)
+    return host_fail(NGPU_EUNSUPP, "zstd unavailable");
+  if (off > r.size || len > r.size - off)
+    return host_fail(NGPU_EFORMAT, "entry %s runs past the end of the blob", name);
+  void *ds = c.zstd_create_dstream();
+  if (!ds) return host_fail(NGPU_ENOMEM, "zstd: no stream");
+  std::vector<uint8_t> in(std::min<uint64_t>(len, 1u << 20) + 1), out(1u << 20);
+  int rc = 0;
+  size_t last = 1;  // 0 once a frame is complete
+  while (len && !rc) {
+    const uint64_t k = std::min<uint64_t>(len, in.size());
+    if ((rc = r.read(in.data(), k, off))) break;
+    off += k;
+    len -= k;
+    ZInBuf ib{in.data(), (size_t)k, 0};
+    while (ib.pos < ib.size && !rc) {
+      ZOutBuf ob{out.data(), out.size(), 0};
+      last = c.zstd_decompress_stream(ds, &ob, &ib);
+      if (c.zstd_is_error(last)) rc = host_fail(NGPU_EFORMAT, "zstd: bad entry %s", name);
+      else if (w && ob.pos && w(wctx, out.data(), ob.pos) != 0) rc = host_fail(NGPU_EIO, "write failed");
+    }
+  }
+  while (!rc && last != 0) {  // flush what the decoder still holds
+    ZInBuf ib{in.data(), 0, 0};
+    ZOutBuf ob{out.data(), out.size(), 0};
+    last = c.zstd_decompress_stream(ds, &ob, &ib);
+    if (c.zstd_is_error(last)) rc = host_fail(NGPU_EFORMAT, "zstd: bad entry %s", name);
+    else if (ob.pos == 0 && last != 0) rc = host_fail(NGPU_EFORMAT, "zstd: truncated entry %s", name);
+    else if (w && ob.pos && w(wctx, out.data(), ob.pos) != 0) rc = host_fail(NGPU_EIO, "write failed");
+  }
+  c.zstd_free_dstream(ds);
+  return rc;
+}
+
 }  // namespace
 }  // namespace ngpu
 
@@ -714,140 +832,161 @@ int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
                     const ngpu_result *results, uint64_t n, const ngpu_layer_stats *stats,
                     const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx,
                     ngpu_blob_info *info) {
-  if ((n && (!data || !chunks || !results)) || !stats || !opt || !w)
-    return host_fail(NGPU_EINVAL, "ngpu_blob_write: bad argument");
-  std::vector<RafsV6BlobInfo> dict(opt->n_dict_blobs);
-  if (opt->n_dict_blobs) {
-    if (!opt->dict_blobs) return host_fail(NGPU_EINVAL, "ngpu_blob_write: dict_blobs is NULL");
-    memcpy(dict.data(), opt->dict_blobs, dict.size() * sizeof(RafsV6BlobInfo));
-  }
-  BlobWriter bw(*opt, w, ctx, std::move(dict));
-  int rc = bw.init();
-  if (rc) return rc;
-  std::vector<const uint8_t *> src;
-  std::vector<uint32_t> lens;
-  const uint8_t *base = (const uint8_t *)data;
-  for (uint64_t i = 0; i < n; ++i) {
-    if (results[i].kind != NGPU_NEW) continue;
-    if (chunks[i].offset > len || chunks[i].length > len - chunks[i].offset)
-      return host_fail(NGPU_EINVAL, "ngpu_blob_write: chunk %llu out of bounds",
-                       (unsigned long long)i);
-    src.push_back(base + chunks[i].offset);
-    lens.push_back(chunks[i].length);
-  }
-  rc = bw.add(src.data(), lens.data(), src.size());
-  if (!rc) rc = bw.finish(chunks, results, n, *stats, info);
+  const int rc = guarded([&]() -> int {
+    if ((n && (!data || !chunks || !results)) || !stats || !opt || !w)
+      return host_fail(NGPU_EINVAL, "ngpu_blob_write: bad argument");
+    std::vector<RafsV6BlobInfo> dict(opt->n_dict_blobs);
+    if (opt->n_dict_blobs) {
+      if (!opt->dict_blobs) return host_fail(NGPU_EINVAL, "ngpu_blob_write: dict_blobs is NULL");
+      memcpy(dict.data(), opt->dict_blobs, dict.size() * sizeof(RafsV6BlobInfo));
+    }
+    if (opt->n_dict_chunks && !opt->dict_chunks)
+      return host_fail(NGPU_EINVAL, "ngpu_blob_write: dict_chunks is NULL");
+    std::vector<DictPlace> place(opt->n_dict_chunks);
+    for (uint64_t i = 0; i < opt->n_dict_chunks; ++i) {
+      RafsV6ChunkInfo r;
+      memcpy(&r, (const uint8_t *)opt->dict_chunks + 80 * i, 80);
+      place[i] = DictPlace{r.compressed_offset, r.compressed_size, r.flags};
+    }
+    BlobWriter bw(*opt, w, ctx, std::move(dict), place.data(), place.size());
+    int rc = bw.init();
+    if (rc) return rc;
+    std::vector<const uint8_t *> src;
+    std::vector<uint32_t> lens;
+    const uint8_t *base = (const uint8_t *)data;
+    for (uint64_t i = 0; i < n; ++i) {
+      if (results[i].kind != NGPU_NEW) continue;
+      if (chunks[i].offset > len || chunks[i].length > len - chunks[i].offset)
+        return host_fail(NGPU_EINVAL, "ngpu_blob_write: chunk %llu out of bounds",
+                         (unsigned long long)i);
+      src.push_back(base + chunks[i].offset);
+      lens.push_back(chunks[i].length);
+    }
+    rc = bw.add(src.data(), lens.data(), src.size());
+    if (!rc) rc = bw.finish(chunks, results, n, *stats, info);
+    return rc;
+  });
+  if (rc == NGPU_ENOMEM) host_fail(rc, "ngpu_blob_write: out of memory");
   return rc;
 }
 
 int ngpu_unpack_entry(ngpu_read_at_fn ra, void *ctx, uint64_t size, const char *name,
                       ngpu_write_fn w, void *wctx, uint8_t *toc_entry_out) {
-  if (!ra || !name) return host_fail(NGPU_EINVAL, "ngpu_unpack_entry: bad argument");
-  Reader r{ra, ctx, size};
-  if (toc_entry_out) memset(toc_entry_out, 0, sizeof(TocEntry));
-  // seekFileByTOC (convert_unix.go:219-276)
-  uint64_t toff = 0, tlen = 0;
-  int rc = seek_by_tar_header(r, "rafs.blob.toc", 1 << 20, &toff, &tlen);
-  if (rc == 0) {
-    if (tlen % sizeof(TocEntry)) return host_fail(NGPU_EFORMAT, "invalid entries length %llu",
-                                                  (unsigned long long)tlen);
-    std::vector<TocEntry> toc(tlen / sizeof(TocEntry));
-    if ((rc = r.read(toc.data(), tlen, toff))) return rc;
-    for (const TocEntry &e : toc) {
-      if (std::string(e.name, strnlen(e.name, sizeof e.name)) != name) continue;
-      const uint32_t comp = e.flags & 0xf;
-      if (comp == NGPU_COMPRESSOR_NONE) {
-        rc = copy_range(r, e.compressed_offset, e.compressed_size, w, wctx);
-      } else if (comp == NGPU_COMPRESSOR_ZSTD) {
-        const Codecs &c = codecs();
-        if (!c.zstd_decompress) return host_fail(NGPU_EUNSUPP, "zstd unavailable");
-        std::vector<uint8_t> in(e.compressed_size), out(e.uncompressed_size + 1);
-        if ((rc = r.read(in.data(), in.size(), e.compressed_offset))) return rc;
-        const size_t z = c.zstd_decompress(out.data(), out.size(), in.data(), in.size());
-        if (c.zstd_is_error(z)) return host_fail(NGPU_EFORMAT, "zstd: bad entry %s", name);
-        if (w && z && w(wctx, out.data(), z) != 0) return host_fail(NGPU_EIO, "write failed");
-      } else {
-        return host_fail(NGPU_EUNSUPP, "unsupported compressor %x", comp);
+  const int rc = guarded([&]() -> int {
+    if (!ra || !name) return host_fail(NGPU_EINVAL, "ngpu_unpack_entry: bad argument");
+    Reader r{ra, ctx, size};
+    if (toc_entry_out) memset(toc_entry_out, 0, sizeof(TocEntry));
+    // seekFileByTOC (convert_unix.go:219-276)
+    uint64_t toff = 0, tlen = 0;
+    int rc = seek_by_tar_header(r, "rafs.blob.toc", 1 << 20, &toff, &tlen);
+    if (rc == 0) {
+      if (tlen % sizeof(TocEntry)) return host_fail(NGPU_EFORMAT, "invalid entries length %llu",
+                                                    (unsigned long long)tlen);
+      std::vector<TocEntry> toc(tlen / sizeof(TocEntry));
+      if ((rc = r.read(toc.data(), tlen, toff))) return rc;
+      for (const TocEntry &e : toc) {
+        if (std::string(e.name, strnlen(e.name, sizeof e.name)) != name) continue;
+        const uint32_t comp = e.flags & 0xf;
+        if (comp == NGPU_COMPRESSOR_NONE) {
+          rc = copy_range(r, e.compressed_offset, e.compressed_size, w, wctx);
+        } else if (comp == NGPU_COMPRESSOR_ZSTD) {
+          rc = copy_zstd(r, e.compressed_offset, e.compressed_size, name, w, wctx);
+        } else {
+          return host_fail(NGPU_EUNSUPP, "unsupported compressor %x", comp);
+        }
+        if (rc) return rc;
+        if (toc_entry_out) memcpy(toc_entry_out, &e, sizeof e);
+        return 0;
       }
-      if (rc) return rc;
-      if (toc_entry_out) memcpy(toc_entry_out, &e, sizeof e);
-      return 0;
+    } else if (rc != NGPU_ENOTFOUND) {
+      return rc;
     }
-  } else if (rc != NGPU_ENOTFOUND) {
-    return rc;
-  }
-  // seekFile fallback: old rafs blob format, by tar header (convert_unix.go:302-320)
-  uint64_t off = 0, len = 0;
-  if ((rc = seek_by_tar_header(r, name, -1, &off, &len))) return rc;
-  return copy_range(r, off, len, w, wctx);
+    // seekFile fallback: old rafs blob format, by tar header (convert_unix.go:302-320)
+    uint64_t off = 0, len = 0;
+    if ((rc = seek_by_tar_header(r, name, -1, &off, &len))) return rc;
+    return copy_range(r, off, len, w, wctx);
+  });
+  if (rc == NGPU_ENOMEM) host_fail(rc, "ngpu_unpack_entry: out of memory");
+  return rc;
 }
 
 int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
                const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
                uint64_t dict_size, ngpu_write_fn w, void *ctx, char **blob_ids_out) {
-  if ((n && (!bootstraps || !sizes)) || !blob_ids_out)
-    return host_fail(NGPU_EINVAL, "ngpu_merge: bad argument");
-  *blob_ids_out = nullptr;
-  std::vector<std::string> dict_ids;
-  if (dict_bootstrap) {
-    Bootstrap d;
-    int rc = parse_bootstrap((const uint8_t *)dict_bootstrap, dict_size, &d);
-    if (rc) return rc;
-    for (auto &b : d.blobs) dict_ids.push_back(blob_id_of(b));
-  }
-  Bootstrap out;
-  std::vector<std::string> ids;
-  for (uint64_t l = 0; l < n; ++l) {
-    Bootstrap b;
-    int rc = parse_bootstrap((const uint8_t *)bootstraps[l], sizes[l], &b);
-    if (rc) return rc;
-    if (!out.chunk_size) {
-      out.chunk_size = b.chunk_size;
-      out.flags = b.flags;
+  const int rc = guarded([&]() -> int {
+    if ((n && (!bootstraps || !sizes)) || !blob_ids_out)
+      return host_fail(NGPU_EINVAL, "ngpu_merge: bad argument");
+    *blob_ids_out = nullptr;
+    std::vector<std::string> dict_ids;
+    if (dict_bootstrap) {
+      Bootstrap d;
+      int rc = parse_bootstrap((const uint8_t *)dict_bootstrap, dict_size, &d);
+      if (rc) return rc;
+      for (auto &b : d.blobs) dict_ids.push_back(blob_id_of(b));
     }
-    std::vector<uint32_t> local(b.blobs.size());
-    int own = 0;
-    for (size_t i = 0; i < b.blobs.size(); ++i) {
-      std::string id = blob_id_of(b.blobs[i]);
-      // A layer's own (non-dict) blob is named after the layer: the digest of
-      // its whole nydus tar stream, which Merge receives as Layer.Digest and
-      // uses as the bootstrap file name (convert_unix.go:567-573, 595-599).
-      const bool is_dict = std::find(dict_ids.begin(), dict_ids.end(), id) != dict_ids.end();
-      if (!is_dict) {
-        if (++own > 1)
-          return host_fail(NGPU_EFORMAT, "layer %llu has more than one non-dict blob",
-                           (unsigned long long)l);
-        if (layer_digests && layer_digests[l] && layer_digests[l][0]) id = layer_digests[l];
+    Bootstrap out;
+    std::vector<std::string> ids;
+    std::set<std::array<uint8_t, 36>> seen;
+    for (uint64_t l = 0; l < n; ++l) {
+      Bootstrap b;
+      int rc = parse_bootstrap((const uint8_t *)bootstraps[l], sizes[l], &b);
+      if (rc) return rc;
+      if (!out.chunk_size) {
+        out.chunk_size = b.chunk_size;
+        out.flags = b.flags;
       }
-      auto it = std::find(ids.begin(), ids.end(), id);
-      if (it == ids.end()) {
-        ids.push_back(id);
-        RafsV6BlobInfo nb = b.blobs[i];
-        memset(nb.blob_id, 0, sizeof nb.blob_id);
-        memcpy(nb.blob_id, id.data(), std::min<size_t>(id.size(), 64));
-        nb.blob_index = (uint32_t)out.blobs.size();
-        out.blobs.push_back(nb);
-        local[i] = nb.blob_index;
-      } else {
-        local[i] = (uint32_t)(it - ids.begin());
+      std::vector<uint32_t> local(b.blobs.size());
+      int own = 0;
+      for (size_t i = 0; i < b.blobs.size(); ++i) {
+        std::string id = blob_id_of(b.blobs[i]);
+        // A layer's own (non-dict) blob is named after the layer: the digest of
+        // its whole nydus tar stream, which Merge receives as Layer.Digest and
+        // uses as the bootstrap file name (convert_unix.go:567-573, 595-599).
+        const bool is_dict = std::find(dict_ids.begin(), dict_ids.end(), id) != dict_ids.end();
+        if (!is_dict) {
+          if (++own > 1)
+            return host_fail(NGPU_EFORMAT, "layer %llu has more than one non-dict blob",
+                             (unsigned long long)l);
+          if (layer_digests && layer_digests[l] && layer_digests[l][0]) id = layer_digests[l];
+        }
+        auto it = std::find(ids.begin(), ids.end(), id);
+        if (it == ids.end()) {
+          ids.push_back(id);
+          RafsV6BlobInfo nb = b.blobs[i];
+          memset(nb.blob_id, 0, sizeof nb.blob_id);
+          memcpy(nb.blob_id, id.data(), std::min<size_t>(id.size(), 64));
+          nb.blob_index = (uint32_t)out.blobs.size();
+          out.blobs.push_back(nb);
+          local[i] = nb.blob_index;
+        } else {
+          local[i] = (uint32_t)(it - ids.begin());
+        }
+      }
+      for (RafsV6ChunkInfo c : b.chunks) {
+        if (c.blob_index >= local.size()) return host_fail(NGPU_EFORMAT, "chunk blob index out of range");
+        c.blob_index = local[c.blob_index];
+        // layers packed against one chunk dict each carry the dict chunks they
+        // reuse: the merged table keeps one record per (digest, blob)
+        std::array<uint8_t, 36> key;
+        memcpy(key.data(), c.block_id, 32);
+        memcpy(key.data() + 32, &c.blob_index, 4);
+        if (!seen.insert(key).second) continue;
+        out.chunks.push_back(c);
       }
     }
-    for (RafsV6ChunkInfo c : b.chunks) {
-      if (c.blob_index >= local.size()) return host_fail(NGPU_EFORMAT, "chunk blob index out of range");
-      c.blob_index = local[c.blob_index];
-      out.chunks.push_back(c);
-    }
-  }
-  if (!out.chunk_size) out.chunk_size = 0x100000;
-  const std::vector<uint8_t> boot = write_bootstrap(out);
-  if (w && w(ctx, boot.data(), boot.size()) != 0) return host_fail(NGPU_EIO, "write failed");
-  std::string s;
-  for (size_t i = 0; i < ids.size(); ++i) s += (i ? "," : "") + ids[i];
-  char *o = (char *)malloc(s.size() + 1);
-  if (!o) return NGPU_ENOMEM;
-  memcpy(o, s.c_str(), s.size() + 1);
-  *blob_ids_out = o;
-  return 0;
+    if (!out.chunk_size) out.chunk_size = 0x100000;
+    const std::vector<uint8_t> boot = write_bootstrap(out);
+    if (w && w(ctx, boot.data(), boot.size()) != 0) return host_fail(NGPU_EIO, "write failed");
+    std::string s;
+    for (size_t i = 0; i < ids.size(); ++i) s += (i ? "," : "") + ids[i];
+    char *o = (char *)malloc(s.size() + 1);
+    if (!o) return NGPU_ENOMEM;
+    memcpy(o, s.c_str(), s.size() + 1);
+    *blob_ids_out = o;
+    return 0;
+  });
+  if (rc == NGPU_ENOMEM) host_fail(rc, "ngpu_merge: out of memory");
+  return rc;
 }
 
 }  // extern "C"

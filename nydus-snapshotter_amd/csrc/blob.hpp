@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include <memory>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -58,10 +59,31 @@ static_assert(sizeof(RafsV6ChunkInfo) == 80, "RAFS v6 chunk info is 80 bytes");
 static_assert(sizeof(RafsV6BlobInfo) == 256, "RAFS v6 blob info is 256 bytes");
 static_assert(sizeof(TocEntry) == 128, "TOC entry is 128 bytes");
 
+// Compressed placement of a chunk-dict entry: what a DICT chunk record of a
+// layer bootstrap copies from the dict's record (nydus chunk.copy_from).
+struct DictPlace {
+  uint64_t compressed_offset;
+  uint32_t compressed_size;
+  uint32_t flags;
+};
+
 constexpr uint32_t kRafsV6Magic = 0xE0F5E1E2u;        // pkg/layout/layout.go:24
 constexpr uint64_t kRafsV6SuperBlockOffset = 1024;     // layout.go:26
 constexpr uint64_t kRafsV6ExtSuperBlockOffset = 1152;  // 1024 + 128
 constexpr uint64_t kBlobTableOffset = 4096;            // as in the reference fixture
+
+// C ABI entry points run their body through guarded(): no C++ exception
+// (bad_alloc from a hostile size, length_error, ...) crosses the boundary.
+template <class F>
+int guarded(F &&f) noexcept {
+  try {
+    return f();
+  } catch (const std::bad_alloc &) {
+    return NGPU_ENOMEM;
+  } catch (...) {
+    return NGPU_EINVAL;
+  }
+}
 
 // Parsed (minimal) RAFS v6 bootstrap: blob table + chunk table.
 struct Bootstrap {
@@ -77,9 +99,12 @@ std::string blob_id_of(const RafsV6BlobInfo &b);
 // Sequential writer of the nydus formatted stream for one layer.
 class BlobWriter {
  public:
-  // dict_blobs: the chunk dict's blob table (its inner-index order).
+  // dict_blobs: the chunk dict's blob table (its inner-index order);
+  // dict_place: compressed placement per dict entry (DICT results' `ref`),
+  // n_place entries (0: unknown, csize = usize and offset 0).
   BlobWriter(const ngpu_blob_options &opt, ngpu_write_fn w, void *ctx,
-             std::vector<RafsV6BlobInfo> dict_blobs);
+             std::vector<RafsV6BlobInfo> dict_blobs, const DictPlace *dict_place = nullptr,
+             uint64_t n_place = 0);
   ~BlobWriter();
   int init();  // loads the compressor; NGPU_EUNSUPP if unavailable
   // NEW chunks in index order (src[k] = host bytes of chunk with index
@@ -89,6 +114,8 @@ class BlobWriter {
   int finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_t n,
              const ngpu_layer_stats &st, ngpu_blob_info *info);
   const std::string &error() const { return err_; }
+  // Cancellation: checked before each compression batch (NGPU_ECANCELED).
+  void set_cancel(const volatile int32_t *flag);
 
  private:
   struct Impl;

@@ -14,6 +14,22 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Sets the calling thread's HIP device for a scope and restores it after, so
+// a library call never changes which device the caller (e.g. PyTorch) is on.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard &) = delete;
+  DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 // ---- device helpers --------------------------------------------------------
 // 16-B streaming load (read-once data: non-temporal).
 __device__ __forceinline__ u32x4 load_nt16(const void *p) {
@@ -156,6 +172,8 @@ struct DictDevice {
   const uint32_t *usize = nullptr;
   const uint32_t *blob = nullptr;    // inner blob index
   const uint32_t *index = nullptr;   // RAFS chunk index
+  const uint64_t *uoff = nullptr;    // uncompressed offset in its blob
+  const uint32_t *gid = nullptr;     // global entry id (node shards); null = identity
   const uint64_t *table = nullptr;   // hash slots
   uint64_t mask = 0;                 // table capacity - 1
   uint64_t m = 0;
@@ -175,6 +193,9 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                   ngpu_layer_stats *st, hipStream_t s);
 void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
                        const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s);
+// RAFS v6 chunk records (80 B, device) -> the dict's SoA arrays.
+void launch_dict_unpack(const uint8_t *recs, uint64_t n, uint8_t *digests, uint32_t *usize,
+                        uint32_t *blob, uint32_t *index, uint64_t *uoff, hipStream_t s);
 
 // Device workspace, grown on demand and owned by the engine.
 struct Workspace {

@@ -89,21 +89,47 @@ __global__ void dict_insert(const uint8_t *__restrict__ digests, uint64_t m,
   if (e < m) ht_insert_min<32>(table, mask, digests, (uint32_t)e);
 }
 
+// The hit record of local entry e (global id through gid for node shards).
+__device__ __forceinline__ ngpu_dict_hit dict_hit_of(const DictDevice &dict, uint32_t e) {
+  if (e == kNone) return ngpu_dict_hit{kNone, 0, 0, 0, 0};
+  return ngpu_dict_hit{dict.gid ? dict.gid[e] : e, dict.index[e], dict.blob[e], dict.usize[e],
+                       dict.uoff[e]};
+}
+
 // Look n digests (byte stride `stride`) up in the dict.
 __global__ void dict_probe_records(const uint8_t *__restrict__ digests, uint64_t stride,
                                    uint64_t n, DictDevice dict,
                                    ngpu_dict_hit *__restrict__ hits) {
   const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (q >= n) return;
-  ngpu_dict_hit h{kNone, 0, 0, 0};
+  uint32_t e = kNone;
   if (dict.m) {
     const uint4 *p = reinterpret_cast<const uint4 *>(digests + q * stride);
     const uint4 a = p[0], b = p[1];
     const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    const uint32_t e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
-    if (e != kNone) h = ngpu_dict_hit{e, dict.index[e], dict.blob[e], dict.usize[e]};
+    e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
   }
-  hits[q] = h;
+  hits[q] = dict_hit_of(dict, e);
+}
+
+// RAFS v6 chunk-info records (80 B: block_id[32], blob_index, flags,
+// compressed_size, uncompressed_size, compressed_offset, uncompressed_offset,
+// file_offset, index, reserved) -> SoA.  One thread per record.
+__global__ void dict_unpack(const uint8_t *__restrict__ recs, uint64_t n,
+                            uint8_t *__restrict__ digests, uint32_t *__restrict__ usize,
+                            uint32_t *__restrict__ blob, uint32_t *__restrict__ index,
+                            uint64_t *__restrict__ uoff) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4 *r = reinterpret_cast<const uint4 *>(recs + 80 * i);
+  const uint4 a = r[0], b = r[1], c = r[2], d = r[3], f = r[4];
+  uint4 *o = reinterpret_cast<uint4 *>(digests + 32 * i);
+  o[0] = a;
+  o[1] = b;
+  blob[i] = c.x;
+  usize[i] = c.w;
+  uoff[i] = (uint64_t)d.w << 32 | d.z;
+  index[i] = f.z;
 }
 
 // ---- layered dedup -----------------------------------------------------------
@@ -196,15 +222,14 @@ __global__ void dedup_probe_insert(const ngpu_chunk *__restrict__ chunks, uint64
   const bool live = c < n;
   uint32_t d[8] = {};
   uint32_t layer = 0;
-  ngpu_dict_hit h{kNone, 0, 0, 0};
+  ngpu_dict_hit h{kNone, 0, 0, 0, 0};
   if (live) {
     load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
     layer = chunk_layer[c];
     if (hits) {
       h = hits[c];
     } else if (dict.m) {
-      const uint32_t e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
-      if (e != kNone) h = ngpu_dict_hit{e, dict.index[e], dict.blob[e], dict.usize[e]};
+      h = dict_hit_of(dict, ht_lookup<32>(dict.table, dict.mask, dict.digests, d));
     }
   }
   const bool is_dict = live && h.entry != kNone &&
@@ -217,7 +242,7 @@ __global__ void dedup_probe_insert(const ngpu_chunk *__restrict__ chunks, uint64
     r.ref = h.entry;
     r.index = h.index;
     r.blob_index = h.blob;  // inner index; remapped in finalize
-    r.uncompressed_offset = 0;
+    r.uncompressed_offset = h.uncompressed_offset;  // chunk.copy_from(cached_chunk)
     r.dict_blob = h.blob;
     return;
   }
@@ -461,6 +486,13 @@ void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
   if (n == 0) return;
   hipLaunchKernelGGL(dict_probe_records, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                      digests, stride, n, dict, hits);
+}
+
+void launch_dict_unpack(const uint8_t *recs, uint64_t n, uint8_t *digests, uint32_t *usize,
+                        uint32_t *blob, uint32_t *index, uint64_t *uoff, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(dict_unpack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recs, n,
+                     digests, usize, blob, index, uoff);
 }
 
 void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,

@@ -128,19 +128,6 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
   return 0;
 }
 
-void free_dict(ngpu_engine *e) {
-  (void)hipFree(e->d_dict_digest);
-  (void)hipFree(e->d_dict_usize);
-  (void)hipFree(e->d_dict_blob);
-  (void)hipFree(e->d_dict_index);
-  (void)hipFree(e->d_dict_table);
-  e->d_dict_digest = nullptr;
-  e->d_dict_usize = e->d_dict_blob = e->d_dict_index = nullptr;
-  e->d_dict_table = nullptr;
-  e->dict = DictDevice{};
-  e->dict_blobs.clear();
-}
-
 int ws_acquire(ngpu_engine *e, hipStream_t s) {
   if (e->ws_pending && e->ws_last != s) HIP_TRY(e, hipStreamWaitEvent(s, e->ws_done, 0));
   return 0;
@@ -158,7 +145,7 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
                    const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
                    hipStream_t s) {
   const int D = pick_group_log2(e, len);
-  int rc = ensure_workspace(e, n, len, D, e->dict.n_blobs, 1);
+  int rc = ensure_workspace(e, n, len, D, 0, 1);
   if (rc) return rc;
   if ((rc = ws_acquire(e, s))) return rc;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
@@ -193,19 +180,21 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
 
 // Dedup stage: dict decisions (given hits or the engine's dict), intra-layer
 // dedup, NEW indices / offsets, blob order, stats.
-int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
-                  const ngpu_dict_hit *d_hits, uint32_t n_blobs, hipStream_t s,
-                  const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats) {
-  if (!d_hits) n_blobs = e->dict.n_blobs;
+int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chunks, uint64_t n,
+                  ngpu_result *d_out, const ngpu_dict_hit *d_hits, uint32_t n_blobs,
+                  hipStream_t s, const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats) {
+  if (!d_hits) n_blobs = dict_blobs(dict);
   if (!d_lfirst) L = 1;
   int rc = ensure_workspace(e, n, 0, 0, n_blobs, L);
   if (rc) return rc;
   if ((rc = ws_acquire(e, s))) return rc;
   if (!d_stats) d_stats = e->ws.lstats;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
-  const uint32_t align = e->cfg.fs_version == 6 ? 4096u : 1u;
+  const uint32_t align =
+      (e->cfg.fs_version == 6 || (e->cfg.flags & NGPU_FLAG_ALIGNED_CHUNK)) ? 4096u : 1u;
   // d_lfirst == nullptr: the init kernel writes {0, n} into ws.lfirst1
-  launch_dedup(d_chunks, n, e->dict, d_hits, n_blobs, align, d_lfirst, L, e->ws, d_out, d_stats, s);
+  launch_dedup(d_chunks, n, dict ? dict->dev : DictDevice{}, d_hits, n_blobs, align, d_lfirst, L,
+               e->ws, d_out, d_stats, s);
   if (tm && e->tcalls) HIP_TRY(e, hipEventRecord(e->ev[e->tslot][4], s));
   HIP_TRY(e, hipGetLastError());
   if (tm && e->tcalls) e->timed[e->tslot] = n > 0;
@@ -213,12 +202,41 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_r
   return 0;
 }
 
-int enqueue(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
-            const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
-            hipStream_t s) {
+int enqueue(ngpu_engine *e, const ngpu_dict *dict, const uint8_t *d_data, uint64_t len,
+            const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out, hipStream_t s) {
   int rc = enqueue_digest(e, d_data, len, d_chunks, n, d_out, s);
   if (rc) return rc;
-  return enqueue_dedup(e, d_chunks, n, d_out, nullptr, 0, s, nullptr, 1, nullptr);
+  return enqueue_dedup(e, dict, d_chunks, n, d_out, nullptr, 0, s, nullptr, 1, nullptr);
+}
+
+void engine_ref(ngpu_engine *e) { e->refs.fetch_add(1, std::memory_order_relaxed); }
+
+void engine_unref(ngpu_engine *e) {
+  if (!e || e->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+  DeviceGuard g(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  Workspace &ws = e->ws;
+  void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.nbytes, ws.ndict, ws.tstat,
+                  ws.intra, ws.blob_first, ws.blob_real, ws.stats, ws.chunk_layer,
+                  ws.lfirst1, ws.lstats, ws.small, ws.tree_list,
+                  e->d_data, e->d_chunks, e->d_results};
+  for (void *p : bufs)
+    if (p) (void)hipFree(p);
+  if (e->h_stats) (void)hipHostFree(e->h_stats);
+  for (auto &set : e->ev)
+    for (auto ev : set)
+      if (ev) (void)hipEventDestroy(ev);
+  for (auto &b : e->staging_pool) {
+    if (b.h) (void)hipHostFree(b.h);
+    if (b.h_ch) (void)hipHostFree(b.h_ch);
+    if (b.d) (void)hipFree(b.d);
+    if (b.d_ch) (void)hipFree(b.d_ch);
+    if (b.copied) (void)hipEventDestroy(b.copied);
+    if (b.done) (void)hipEventDestroy(b.done);
+  }
+  if (e->ws_done) (void)hipEventDestroy(e->ws_done);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
 }
 
 // Layer stats of a single-layer call (internal lstats[0]) + the digest
@@ -244,10 +262,6 @@ int ngpu_abi_version(void) { return NGPU_ABI_VERSION; }
 
 // internal (host.cpp), not part of nydus_gpu.h
 uint32_t ngpu_engine_chunk_size(const ngpu_engine *e) { return e->cfg.chunk_size; }
-void ngpu_engine_set_dict_blobs(ngpu_engine *e, const uint8_t *rec, uint64_t bytes) {
-  std::lock_guard<std::mutex> g(e->mu);
-  e->dict_blobs.assign(rec, rec + bytes);
-}
 
 int ngpu_device_count(void) {
   int n = 0;
@@ -268,6 +282,12 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   if (c.fs_version != 5 && c.fs_version != 6) return NGPU_EINVAL;
   if (c.digester != NGPU_DIGEST_BLAKE3 && c.digester != NGPU_DIGEST_SHA256) return NGPU_EINVAL;
   if (c.leaves_per_lane & (c.leaves_per_lane - 1) || c.leaves_per_lane > 16) return NGPU_EINVAL;
+  // SHA-256 kernel override (benchmarks): 1 + {0 split, 1 pair, 4 pair one
+  // group per workgroup, 5 pair four groups}; anything else is rejected
+  switch ((c.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7) {
+    case 0: case 1: case 2: case 5: case 6: break;
+    default: return NGPU_EINVAL;
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return NGPU_ENODEV;
   if (c.device < 0 || c.device >= ndev) return NGPU_ENODEV;
@@ -277,10 +297,7 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   ngpu_engine *e = new ngpu_engine();
   e->cfg = c;
   e->device = c.device;
-  if (hipSetDevice(c.device) != hipSuccess) {
-    delete e;
-    return NGPU_EHIP;
-  }
+  DeviceGuard dg(c.device);
   if (c.flags & NGPU_FLAG_TIMING)
     for (auto &set : e->ev)
       for (auto &ev : set)
@@ -301,31 +318,17 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
 
 void ngpu_destroy(ngpu_engine *e) {
   if (!e) return;
-  hipSetDevice(e->device);
-  if (e->stream) hipStreamSynchronize(e->stream);
-  free_dict(e);
-  Workspace &ws = e->ws;
-  void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.nbytes, ws.ndict, ws.tstat,
-                  ws.intra, ws.blob_first, ws.blob_real, ws.stats, ws.chunk_layer,
-                  ws.lfirst1, ws.lstats, ws.small, ws.tree_list,
-                  e->d_data, e->d_chunks, e->d_results};
-  for (void *p : bufs)
-    if (p) (void)hipFree(p);
-  if (e->h_stats) (void)hipHostFree(e->h_stats);
-  for (auto &set : e->ev)
-    for (auto ev : set)
-      if (ev) (void)hipEventDestroy(ev);
-  for (auto &b : e->staging_pool) {
-    if (b.h) (void)hipHostFree(b.h);
-    if (b.h_ch) (void)hipHostFree(b.h_ch);
-    if (b.d) (void)hipFree(b.d);
-    if (b.d_ch) (void)hipFree(b.d_ch);
-    if (b.copied) (void)hipEventDestroy(b.copied);
-    if (b.done) (void)hipEventDestroy(b.done);
+  ngpu_dict *d;
+  std::vector<ngpu_dict *> cache;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    d = e->dict;
+    e->dict = nullptr;
+    cache.swap(e->dict_cache);
   }
-  if (e->ws_done) (void)hipEventDestroy(e->ws_done);
-  if (e->stream) hipStreamDestroy(e->stream);
-  delete e;
+  dict_unref(d);
+  for (ngpu_dict *c : cache) dict_unref(c);
+  engine_unref(e);  // open packs keep the engine until they end
 }
 
 const char *ngpu_last_error(const ngpu_engine *e) { return e ? e->err.c_str() : "null engine"; }
@@ -333,7 +336,7 @@ const char *ngpu_last_error(const ngpu_engine *e) { return e ? e->err.c_str() : 
 int ngpu_alloc_pinned(ngpu_engine *e, uint64_t bytes, void **out) {
   if (!e || !out) return NGPU_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
+  DeviceGuard dg(e->device);
   HIP_TRY(e, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
   return 0;
 }
@@ -341,86 +344,6 @@ int ngpu_alloc_pinned(ngpu_engine *e, uint64_t bytes, void **out) {
 int ngpu_free_pinned(ngpu_engine *e, void *p) {
   if (!e) return NGPU_EINVAL;
   HIP_TRY(e, hipHostFree(p));
-  return 0;
-}
-
-int ngpu_dict_load(ngpu_engine *e, const uint8_t *digests, const uint32_t *usize,
-                   const uint32_t *blob_index, const uint32_t *chunk_index, uint64_t n) {
-  if (!e || (n && (!digests || !usize || !blob_index))) return NGPU_EINVAL;
-  if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "dict too large (%llu entries)",
-                                      (unsigned long long)n);
-  std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
-  HIP_TRY(e, hipStreamSynchronize(e->stream));
-  free_dict(e);
-  if (n == 0) return 0;
-  uint32_t nb = 0;
-  for (uint64_t i = 0; i < n; ++i)
-    if (blob_index[i] + 1 > nb) nb = blob_index[i] + 1;
-  if (nb > (1u << 20)) return fail(e, NGPU_EINVAL, "dict blob index %u too large", nb - 1);
-  const uint64_t cap = next_pow2(2 * n + 16);
-  HIP_TRY(e, hipMalloc((void **)&e->d_dict_digest, n * 32));
-  HIP_TRY(e, hipMalloc((void **)&e->d_dict_usize, n * 4));
-  HIP_TRY(e, hipMalloc((void **)&e->d_dict_blob, n * 4));
-  HIP_TRY(e, hipMalloc((void **)&e->d_dict_index, n * 4));
-  HIP_TRY(e, hipMalloc((void **)&e->d_dict_table, cap * 8));
-  HIP_TRY(e, hipMemcpyAsync(e->d_dict_digest, digests, n * 32, hipMemcpyHostToDevice, e->stream));
-  HIP_TRY(e, hipMemcpyAsync(e->d_dict_usize, usize, n * 4, hipMemcpyHostToDevice, e->stream));
-  HIP_TRY(e, hipMemcpyAsync(e->d_dict_blob, blob_index, n * 4, hipMemcpyHostToDevice, e->stream));
-  if (chunk_index)
-    HIP_TRY(e, hipMemcpyAsync(e->d_dict_index, chunk_index, n * 4, hipMemcpyHostToDevice, e->stream));
-  else
-    HIP_TRY(e, hipMemsetAsync(e->d_dict_index, 0, n * 4, e->stream));
-  launch_dict_build(e->d_dict_digest, n, e->d_dict_table, cap, e->stream);
-  HIP_TRY(e, hipGetLastError());
-  HIP_TRY(e, hipStreamSynchronize(e->stream));
-  e->dict.digests = e->d_dict_digest;
-  e->dict.usize = e->d_dict_usize;
-  e->dict.blob = e->d_dict_blob;
-  e->dict.index = e->d_dict_index;
-  e->dict.table = e->d_dict_table;
-  e->dict.mask = cap - 1;
-  e->dict.m = n;
-  e->dict.n_blobs = nb;
-  return 0;
-}
-
-int ngpu_dict_load_device(ngpu_engine *e, const uint8_t *d_digests, const uint32_t *d_usize,
-                          const uint32_t *d_blob_index, const uint32_t *d_chunk_index,
-                          uint64_t n, uint32_t n_blobs) {
-  if (!e || (n && (!d_digests || !d_usize || !d_blob_index))) return NGPU_EINVAL;
-  if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "dict too large");
-  if (n_blobs == 0 || n_blobs > (1u << 20)) return fail(e, NGPU_EINVAL, "bad n_blobs %u", n_blobs);
-  std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
-  HIP_TRY(e, hipStreamSynchronize(e->stream));
-  free_dict(e);
-  if (n == 0) return 0;
-  const uint64_t cap = next_pow2(2 * n + 16);
-  HIP_TRY(e, hipMalloc((void **)&e->d_dict_digest, n * 32));
-  HIP_TRY(e, hipMalloc((void **)&e->d_dict_usize, n * 4));
-  HIP_TRY(e, hipMalloc((void **)&e->d_dict_blob, n * 4));
-  HIP_TRY(e, hipMalloc((void **)&e->d_dict_index, n * 4));
-  HIP_TRY(e, hipMalloc((void **)&e->d_dict_table, cap * 8));
-  const hipMemcpyKind k = hipMemcpyDeviceToDevice;
-  HIP_TRY(e, hipMemcpyAsync(e->d_dict_digest, d_digests, n * 32, k, e->stream));
-  HIP_TRY(e, hipMemcpyAsync(e->d_dict_usize, d_usize, n * 4, k, e->stream));
-  HIP_TRY(e, hipMemcpyAsync(e->d_dict_blob, d_blob_index, n * 4, k, e->stream));
-  if (d_chunk_index)
-    HIP_TRY(e, hipMemcpyAsync(e->d_dict_index, d_chunk_index, n * 4, k, e->stream));
-  else
-    HIP_TRY(e, hipMemsetAsync(e->d_dict_index, 0, n * 4, e->stream));
-  launch_dict_build(e->d_dict_digest, n, e->d_dict_table, cap, e->stream);
-  HIP_TRY(e, hipGetLastError());
-  HIP_TRY(e, hipStreamSynchronize(e->stream));
-  e->dict.digests = e->d_dict_digest;
-  e->dict.usize = e->d_dict_usize;
-  e->dict.blob = e->d_dict_blob;
-  e->dict.index = e->d_dict_index;
-  e->dict.table = e->d_dict_table;
-  e->dict.mask = cap - 1;
-  e->dict.m = n;
-  e->dict.n_blobs = n_blobs;
   return 0;
 }
 
@@ -436,21 +359,9 @@ int ngpu_digest_device(ngpu_engine *e, const void *d_data, uint64_t len,
   if (!e || (n && (!d_data || !d_chunks || !d_out))) return NGPU_EINVAL;
   if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too many chunks in one call");
   std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
+  DeviceGuard dg(e->device);
   return enqueue_digest(e, (const uint8_t *)d_data, len, d_chunks, n, d_out,
                         dev_stream(stream));
-}
-
-int ngpu_dict_probe_device(ngpu_engine *e, const uint8_t *d_digests, uint64_t stride,
-                           uint64_t n, ngpu_dict_hit *d_hits, void *stream) {
-  if (!e || (n && (!d_digests || !d_hits)) || stride < 32 || (stride & 15))
-    return NGPU_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
-  launch_dict_probe(d_digests, stride, n, e->dict, d_hits,
-                    dev_stream(stream));
-  HIP_TRY(e, hipGetLastError());
-  return 0;
 }
 
 int ngpu_dedup_device(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n,
@@ -458,11 +369,12 @@ int ngpu_dedup_device(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n,
                       void *stream, ngpu_layer_stats *stats) {
   if (!e || (n && (!d_chunks || !d_out))) return NGPU_EINVAL;
   if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too many chunks in one call");
-  if (d_hits && n_dict_blobs == 0) n_dict_blobs = e->dict.n_blobs ? e->dict.n_blobs : 1;
   std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
+  DeviceGuard dg(e->device);
+  if (d_hits && n_dict_blobs == 0) n_dict_blobs = dict_blobs(e->dict) ? dict_blobs(e->dict) : 1;
   hipStream_t s = dev_stream(stream);
-  int rc = enqueue_dedup(e, d_chunks, n, d_out, d_hits, n_dict_blobs, s, nullptr, 1, nullptr);
+  int rc = enqueue_dedup(e, e->dict, d_chunks, n, d_out, d_hits, n_dict_blobs, s, nullptr, 1,
+                         nullptr);
   if (rc) return rc;
   if (stats) return read_stats(e, s, stats);
   return 0;
@@ -474,56 +386,66 @@ int ngpu_dedup_layers_device(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_
                              uint64_t n_layers, ngpu_layer_stats *d_stats, void *stream) {
   if (!e || !d_layer_first || n_layers == 0 || (n && (!d_chunks || !d_out))) return NGPU_EINVAL;
   if (n >= 0xFFFFFFFFull || n_layers >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too large");
-  if (d_hits && n_dict_blobs == 0) n_dict_blobs = e->dict.n_blobs ? e->dict.n_blobs : 1;
   std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
-  return enqueue_dedup(e, d_chunks, n, d_out, d_hits, n_dict_blobs,
-                       dev_stream(stream), d_layer_first, n_layers,
-                       d_stats);
+  DeviceGuard dg(e->device);
+  if (d_hits && n_dict_blobs == 0) n_dict_blobs = dict_blobs(e->dict) ? dict_blobs(e->dict) : 1;
+  return enqueue_dedup(e, e->dict, d_chunks, n, d_out, d_hits, n_dict_blobs, dev_stream(stream),
+                       d_layer_first, n_layers, d_stats);
+}
+
+// dict == kDefault: the engine's default dict (read under e->mu).
+static ngpu_dict *const kDefault = reinterpret_cast<ngpu_dict *>(1);
+
+static int process_device(ngpu_engine *e, ngpu_dict *dict, const void *d_data, uint64_t len,
+                          const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+                          const uint64_t *d_layer_first, uint64_t n_layers,
+                          ngpu_layer_stats *d_stats, void *stream, ngpu_layer_stats *stats) {
+  if (!e || (d_layer_first && n_layers == 0) || (n && (!d_data || !d_chunks || !d_out)))
+    return NGPU_EINVAL;
+  if (n >= 0xFFFFFFFFull || n_layers >= 0xFFFFFFFFull)
+    return fail(e, NGPU_EINVAL, "too many chunks in one call");
+  if (stats && d_layer_first) return fail(e, NGPU_EINVAL, "host stats are for one-layer calls");
+  std::lock_guard<std::mutex> g(e->mu);
+  DeviceGuard dg(e->device);
+  if (dict == kDefault) dict = e->dict;
+  if (int rc = dict_check(e, dict)) return rc;
+  hipStream_t s = dev_stream(stream);
+  int rc = enqueue_digest(e, (const uint8_t *)d_data, len, d_chunks, n, d_out, s);
+  if (rc) return rc;
+  rc = enqueue_dedup(e, dict, d_chunks, n, d_out, nullptr, 0, s, d_layer_first,
+                     d_layer_first ? n_layers : 1, d_stats);
+  if (rc) return rc;
+  if (stats) return read_stats(e, s, stats);
+  return 0;
 }
 
 int ngpu_process_layers_device(ngpu_engine *e, const void *d_data, uint64_t len,
                                const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
                                const uint64_t *d_layer_first, uint64_t n_layers,
                                ngpu_layer_stats *d_stats, void *stream) {
-  if (!e || !d_layer_first || n_layers == 0 || (n && (!d_data || !d_chunks || !d_out)))
-    return NGPU_EINVAL;
-  if (n >= 0xFFFFFFFFull || n_layers >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too large");
-  std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
-  hipStream_t s = dev_stream(stream);
-  int rc = enqueue_digest(e, (const uint8_t *)d_data, len, d_chunks, n, d_out, s);
-  if (rc) return rc;
-  return enqueue_dedup(e, d_chunks, n, d_out, nullptr, 0, s, d_layer_first, n_layers, d_stats);
+  if (!d_layer_first) return NGPU_EINVAL;
+  return process_device(e, kDefault, d_data, len, d_chunks, n, d_out, d_layer_first, n_layers,
+                        d_stats, stream, nullptr);
 }
-
-int ngpu_dict_clear(ngpu_engine *e) {
-  if (!e) return NGPU_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
-  HIP_TRY(e, hipStreamSynchronize(e->stream));
-  free_dict(e);
-  return 0;
-}
-
-uint64_t ngpu_dict_size(const ngpu_engine *e) { return e ? e->dict.m : 0; }
 
 int ngpu_process_device(ngpu_engine *e, const void *d_data, uint64_t len,
                         const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
                         void *stream, ngpu_layer_stats *stats) {
-  if (!e || (n && (!d_data || !d_chunks || !d_out))) return NGPU_EINVAL;
-  if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too many chunks in one call");
-  std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
-  hipStream_t s = dev_stream(stream);
-  int rc = enqueue(e, (const uint8_t *)d_data, len, d_chunks, n, d_out, s);
-  if (rc) return rc;
-  if (stats) return read_stats(e, s, stats);
-  return 0;
+  return process_device(e, kDefault, d_data, len, d_chunks, n, d_out, nullptr, 1, nullptr, stream,
+                        stats);
 }
 
-int ngpu_process(ngpu_engine *e, const void *data, uint64_t len, const ngpu_chunk *chunks,
-                 uint64_t n, ngpu_result *out, ngpu_layer_stats *stats) {
+int ngpu_process_dict_device(ngpu_engine *e, ngpu_dict *dict, const void *d_data, uint64_t len,
+                             const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
+                             const uint64_t *d_layer_first, uint64_t n_layers,
+                             ngpu_layer_stats *d_stats, void *stream, ngpu_layer_stats *stats) {
+  return process_device(e, dict, d_data, len, d_chunks, n, d_out, d_layer_first, n_layers, d_stats,
+                        stream, stats);
+}
+
+static int process_host(ngpu_engine *e, ngpu_dict *dict, const void *data, uint64_t len,
+                        const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
+                        ngpu_layer_stats *stats) {
   if (!e || (n && (!data || !chunks || !out))) return NGPU_EINVAL;
   if (n >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "too many chunks in one call");
   for (uint64_t i = 0; i < n; ++i) {
@@ -533,7 +455,9 @@ int ngpu_process(ngpu_engine *e, const void *data, uint64_t len, const ngpu_chun
       return fail(e, NGPU_EINVAL, "chunk %llu longer than chunk_size", (unsigned long long)i);
   }
   std::lock_guard<std::mutex> g(e->mu);
-  hipSetDevice(e->device);
+  DeviceGuard dg(e->device);
+  if (dict == kDefault) dict = e->dict;
+  if (int rc = dict_check(e, dict)) return rc;
   hipStream_t s = e->stream;
   uint64_t c0 = e->d_data_cap;
   if (grow(e, &e->d_data, c0, len + 64)) return NGPU_ENOMEM;
@@ -549,11 +473,22 @@ int ngpu_process(ngpu_engine *e, const void *data, uint64_t len, const ngpu_chun
   if (len) HIP_TRY(e, hipMemcpyAsync(e->d_data, data, len, hipMemcpyHostToDevice, s));
   if (n) HIP_TRY(e, hipMemcpyAsync(e->d_chunks, chunks, n * sizeof(ngpu_chunk),
                                    hipMemcpyHostToDevice, s));
-  int rc = enqueue(e, e->d_data, len, e->d_chunks, n, e->d_results, s);
+  int rc = enqueue(e, dict, e->d_data, len, e->d_chunks, n, e->d_results, s);
   if (rc) return rc;
   if (n) HIP_TRY(e, hipMemcpyAsync(out, e->d_results, n * sizeof(ngpu_result),
                                    hipMemcpyDeviceToHost, s));
   return read_stats(e, s, stats);
+}
+
+int ngpu_process(ngpu_engine *e, const void *data, uint64_t len, const ngpu_chunk *chunks,
+                 uint64_t n, ngpu_result *out, ngpu_layer_stats *stats) {
+  return process_host(e, kDefault, data, len, chunks, n, out, stats);
+}
+
+int ngpu_process_dict(ngpu_engine *e, ngpu_dict *dict, const void *data, uint64_t len,
+                      const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
+                      ngpu_layer_stats *stats) {
+  return process_host(e, dict, data, len, chunks, n, out, stats);
 }
 
 int ngpu_timing_at(ngpu_engine *e, uint32_t back, ngpu_timing *out) {

@@ -1,11 +1,14 @@
-// engine_internal.hpp — engine state and stage helpers shared by
-// engine.hip (C ABI) and pack.hip (streaming Pack writer).  Not installed.
+// engine_internal.hpp — engine / chunk-dict state and stage helpers shared by
+// engine.hip (C ABI), dict.hip (chunk dicts), pack.hip (streaming Pack
+// writer) and node.hip (multi-GPU node).  Not installed.
 #pragma once
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
 
+#include "blob.hpp"
 #include "common.hpp"
 
 // Pinned staging + device buffers of one streaming-Pack slot, kept by the
@@ -17,19 +20,31 @@ struct ngpu_staging_buf {
   uint64_t cap = 0;
 };
 
+// A chunk dict ([nydus v2.3.0] HashChunkDict): HBM-resident, read-only once
+// built, reference counted (the engine's default slot, its open cache, every
+// pack using it and the caller each hold one).
+struct ngpu_dict {
+  std::atomic<int> refs{1};
+  int device = 0;
+  uint32_t digester = 0, chunk_size = 0;
+  ngpu::DictDevice dev;                // device arrays + hash table
+  std::vector<void *> allocs;          // device allocations owned
+  std::vector<uint8_t> blob_table;     // 256-B RAFS v6 blob records (inner-index order)
+  std::vector<ngpu::DictPlace> place;  // per entry: compressed placement (empty: unknown)
+  // identity of the bootstrap file it was opened from (ngpu_dict_open cache)
+  std::string path;
+  uint64_t st_dev = 0, st_ino = 0, st_size = 0;
+  int64_t st_mtime_ns = 0;
+};
+
 struct ngpu_engine {
+  std::atomic<int> refs{1};  // the creator + every open pack
   ngpu_config cfg{};
   int device = 0;
   hipStream_t stream = nullptr;
   ngpu::Workspace ws;
-  // chunk dict, HBM resident
-  uint8_t *d_dict_digest = nullptr;
-  uint32_t *d_dict_usize = nullptr, *d_dict_blob = nullptr, *d_dict_index = nullptr;
-  uint64_t *d_dict_table = nullptr;
-  ngpu::DictDevice dict;
-  // blob table (256-B RAFS v6 records) of a bootstrap-loaded dict, for the
-  // blob writer's DICT blob entries (host copy; empty for array-loaded dicts)
-  std::vector<uint8_t> dict_blobs;
+  ngpu_dict *dict = nullptr;              // default dict (one reference), may be null
+  std::vector<ngpu_dict *> dict_cache;    // dicts opened by path (one reference each)
   // host-path device buffers
   uint8_t *d_data = nullptr;
   uint64_t d_data_cap = 0;
@@ -67,14 +82,28 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D, uint3
                      uint64_t L);
 int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
                    const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out, hipStream_t s);
+// d_hits == nullptr: probe `dict` (may be null: no chunk dict).
 // d_lfirst == nullptr: one layer of n chunks (stats -> internal lstats[0]).
-int enqueue_dedup(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
-                  const ngpu_dict_hit *d_hits, uint32_t n_blobs, hipStream_t s,
-                  const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats);
+int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chunks, uint64_t n,
+                  ngpu_result *d_out, const ngpu_dict_hit *d_hits, uint32_t n_blobs,
+                  hipStream_t s, const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats);
 int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st);
 // Order a workspace stage on stream s after the previous one (any stream).
 int ws_acquire(ngpu_engine *e, hipStream_t s);
 int ws_release(ngpu_engine *e, hipStream_t s);
+
+// Reference counts.  engine_unref frees the engine when the last holder (the
+// creator's ngpu_destroy or the last open pack) lets go.
+void engine_ref(ngpu_engine *e);
+void engine_unref(ngpu_engine *e);
+void dict_ref(ngpu_dict *d);
+void dict_unref(ngpu_dict *d);
+// A dict usable by engine e (same device, digester and chunk size), or an
+// error message.
+int dict_check(ngpu_engine *e, const ngpu_dict *d);
+// The engine's default dict with one more reference (null if none).
+ngpu_dict *default_dict(ngpu_engine *e);
+inline uint32_t dict_blobs(const ngpu_dict *d) { return d ? d->dev.n_blobs : 0; }
 
 }  // namespace ngpu
 

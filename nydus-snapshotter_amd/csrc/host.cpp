@@ -31,149 +31,100 @@ using ngpu::kRafsV6SuperBlockOffset;
 extern "C" {
 
 uint32_t ngpu_engine_chunk_size(const ngpu_engine *);  // engine.hip (internal)
-void ngpu_engine_set_dict_blobs(ngpu_engine *, const uint8_t *, uint64_t);
 
 int ngpu_tar_chunks(const void *tar_v, uint64_t len, uint32_t chunk_size, ngpu_chunk *out,
                     uint64_t cap, uint64_t *n_chunks, uint64_t *n_files) {
-  if ((!tar_v && len) || chunk_size == 0) return NGPU_EINVAL;
-  struct Rec : ngpu::TarSink {
-    ngpu_chunk *out;
-    uint64_t cap, n = 0;
-    int chunk(uint64_t off, uint32_t l, uint32_t fi, uint64_t fo) override {
-      if (n < cap && out) out[n] = ngpu_chunk{off, l, fi, fo};
-      ++n;
-      return 0;
-    }
-    int data(const uint8_t *, uint64_t) override { return 0; }
-  } rec;
-  rec.out = out;
-  rec.cap = cap;
-  ngpu::TarScanner sc(chunk_size);
-  int rc = sc.feed((const uint8_t *)tar_v, len, rec);
-  if (!rc) rc = sc.finish();
-  if (rc) return rc;
-  if (n_chunks) *n_chunks = rec.n;
-  if (n_files) *n_files = sc.files();
-  return NGPU_OK;
+  return ngpu::guarded([&]() -> int {
+    if ((!tar_v && len) || chunk_size == 0) return NGPU_EINVAL;
+    struct Rec : ngpu::TarSink {
+      ngpu_chunk *out;
+      uint64_t cap, n = 0;
+      int chunk(uint64_t off, uint32_t l, uint32_t fi, uint64_t fo) override {
+        if (n < cap && out) out[n] = ngpu_chunk{off, l, fi, fo};
+        ++n;
+        return 0;
+      }
+      int data(const uint8_t *, uint64_t) override { return 0; }
+    } rec;
+    rec.out = out;
+    rec.cap = cap;
+    ngpu::TarScanner sc(chunk_size);
+    int rc = sc.feed((const uint8_t *)tar_v, len, rec);
+    if (!rc) rc = sc.finish();
+    if (rc) return rc;
+    if (n_chunks) *n_chunks = rec.n;
+    if (n_files) *n_files = sc.files();
+    return NGPU_OK;
+  });
 }
 
 void ngpu_free_host(void *p) { free(p); }
 
 int ngpu_pack_tar(ngpu_engine *eng, const void *tar, uint64_t len, ngpu_chunk **chunks_out,
                   ngpu_result **results_out, uint64_t *n_out, ngpu_layer_stats *stats) {
-  if (!eng || !chunks_out || !results_out || !n_out) return NGPU_EINVAL;
-  *chunks_out = nullptr;
-  *results_out = nullptr;
-  *n_out = 0;
-  const uint32_t cs = ngpu_engine_chunk_size(eng);
-  uint64_t n = 0, files = 0;
-  int rc = ngpu_tar_chunks(tar, len, cs, nullptr, 0, &n, &files);
-  if (rc) return rc;
-  ngpu_chunk *ch = (ngpu_chunk *)malloc(sizeof(ngpu_chunk) * (n ? n : 1));
-  ngpu_result *res = (ngpu_result *)malloc(sizeof(ngpu_result) * (n ? n : 1));
-  if (!ch || !res) {
-    free(ch);
-    free(res);
-    return NGPU_ENOMEM;
-  }
-  rc = ngpu_tar_chunks(tar, len, cs, ch, n, &n, &files);
-  if (!rc) rc = ngpu_process(eng, tar, len, ch, n, res, stats);
-  if (rc) {
-    free(ch);
-    free(res);
-    return rc;
-  }
-  *chunks_out = ch;
-  *results_out = res;
-  *n_out = n;
-  return NGPU_OK;
+  return ngpu::guarded([&]() -> int {
+    if (!eng || !chunks_out || !results_out || !n_out) return NGPU_EINVAL;
+    *chunks_out = nullptr;
+    *results_out = nullptr;
+    *n_out = 0;
+    const uint32_t cs = ngpu_engine_chunk_size(eng);
+    uint64_t n = 0, files = 0;
+    int rc = ngpu_tar_chunks(tar, len, cs, nullptr, 0, &n, &files);
+    if (rc) return rc;
+    ngpu_chunk *ch = (ngpu_chunk *)malloc(sizeof(ngpu_chunk) * (n ? n : 1));
+    ngpu_result *res = (ngpu_result *)malloc(sizeof(ngpu_result) * (n ? n : 1));
+    if (!ch || !res) {
+      free(ch);
+      free(res);
+      return NGPU_ENOMEM;
+    }
+    rc = ngpu_tar_chunks(tar, len, cs, ch, n, &n, &files);
+    if (!rc) rc = ngpu_process(eng, tar, len, ch, n, res, stats);
+    if (rc) {
+      free(ch);
+      free(res);
+      return rc;
+    }
+    *chunks_out = ch;
+    *results_out = res;
+    *n_out = n;
+    return NGPU_OK;
+  });
 }
 
 int ngpu_chunk_table(const ngpu_chunk *chunks, const ngpu_result *results, uint64_t n,
                      uint8_t *out, uint64_t cap, uint64_t *n_records) {
-  if ((n && (!chunks || !results)) || !n_records) return NGPU_EINVAL;
-  // NEW chunks in index order; compressor "none": csize = usize, compressed
-  // offsets packed back to back (the fixture's coff rule with csize = usize).
-  std::vector<uint64_t> order;
-  for (uint64_t i = 0; i < n; ++i)
-    if (results[i].kind == NGPU_NEW) order.push_back(i);
-  // NEW indices are assigned in stream order, so order is already sorted by
-  // index; verify rather than assume.
-  for (uint64_t k = 0; k < order.size(); ++k)
-    if (results[order[k]].index != k) return NGPU_EINVAL;
-  uint64_t coff = 0;
-  for (uint64_t k = 0; k < order.size() && k < cap && out; ++k) {
-    const uint64_t i = order[k];
-    RafsV6ChunkInfo r;
-    memset(&r, 0, sizeof r);
-    memcpy(r.block_id, results[i].digest, 32);
-    r.blob_index = results[i].blob_index;
-    r.flags = 0;  // not compressed
-    r.compressed_size = chunks[i].length;
-    r.uncompressed_size = chunks[i].length;
-    r.compressed_offset = coff;
-    r.uncompressed_offset = results[i].uncompressed_offset;
-    r.file_offset = chunks[i].file_offset;
-    r.index = results[i].index;
-    memcpy(out + 80 * k, &r, 80);
-    coff += chunks[i].length;
-  }
-  *n_records = order.size();
-  return NGPU_OK;
-}
-
-// Reads the chunk table of a RAFS v6 bootstrap (ChunkDictPath) and loads it
-// as the chunk dict, table order preserved (first entry wins).
-int ngpu_dict_load_bootstrap(ngpu_engine *eng, const char *path) {
-  if (!eng || !path) return NGPU_EINVAL;
-  FILE *f = fopen(path, "rb");
-  if (!f) return NGPU_EIO;
-  uint8_t sb[kRafsV6ExtSuperBlockOffset + 256];
-  if (fread(sb, 1, sizeof sb, f) != sizeof sb) {
-    fclose(f);
-    return NGPU_EFORMAT;
-  }
-  uint32_t magic;
-  memcpy(&magic, sb + kRafsV6SuperBlockOffset, 4);
-  if (magic != kRafsV6Magic) {
-    fclose(f);
-    return NGPU_EFORMAT;
-  }
-  const uint8_t *ext = sb + kRafsV6ExtSuperBlockOffset;
-  uint64_t bto, cto, cts;
-  uint32_t bts;
-  memcpy(&bto, ext + 8, 8);
-  memcpy(&bts, ext + 16, 4);
-  memcpy(&cto, ext + 24, 8);  // RafsV6ChunkInfoOffset = 1024+128+24 (layout.go:27)
-  memcpy(&cts, ext + 32, 8);
-  if (cts % 80 || bts % 256) {
-    fclose(f);
-    return NGPU_EFORMAT;
-  }
-  const uint64_t m = cts / 80;
-  std::vector<RafsV6ChunkInfo> recs(m);
-  if (m && (fseeko(f, (off_t)cto, SEEK_SET) != 0 ||
-            fread(recs.data(), 80, m, f) != m)) {
-    fclose(f);
-    return NGPU_EFORMAT;
-  }
-  std::vector<uint8_t> blobs(bts);
-  if (bts && (fseeko(f, (off_t)bto, SEEK_SET) != 0 || fread(blobs.data(), 1, bts, f) != bts)) {
-    fclose(f);
-    return NGPU_EFORMAT;
-  }
-  fclose(f);
-  std::vector<uint8_t> dig(m * 32);
-  std::vector<uint32_t> us(m), blob(m), idx(m);
-  for (uint64_t i = 0; i < m; ++i) {
-    memcpy(&dig[i * 32], recs[i].block_id, 32);
-    us[i] = recs[i].uncompressed_size;
-    blob[i] = recs[i].blob_index;
-    idx[i] = recs[i].index;
-  }
-  const int rc = ngpu_dict_load(eng, dig.data(), us.data(), blob.data(), idx.data(), m);
-  if (rc == 0) ngpu_engine_set_dict_blobs(eng, blobs.data(), blobs.size());
-  return rc;
+  return ngpu::guarded([&]() -> int {
+    if ((n && (!chunks || !results)) || !n_records) return NGPU_EINVAL;
+    // NEW chunks in index order; compressor "none": csize = usize, compressed
+    // offsets packed back to back (the fixture's coff rule with csize = usize).
+    std::vector<uint64_t> order;
+    for (uint64_t i = 0; i < n; ++i)
+      if (results[i].kind == NGPU_NEW) order.push_back(i);
+    // NEW indices are assigned in stream order, so order is already sorted by
+    // index; verify rather than assume.
+    for (uint64_t k = 0; k < order.size(); ++k)
+      if (results[order[k]].index != k) return NGPU_EINVAL;
+    uint64_t coff = 0;
+    for (uint64_t k = 0; k < order.size() && k < cap && out; ++k) {
+      const uint64_t i = order[k];
+      RafsV6ChunkInfo r;
+      memset(&r, 0, sizeof r);
+      memcpy(r.block_id, results[i].digest, 32);
+      r.blob_index = results[i].blob_index;
+      r.flags = 0;  // not compressed
+      r.compressed_size = chunks[i].length;
+      r.uncompressed_size = chunks[i].length;
+      r.compressed_offset = coff;
+      r.uncompressed_offset = results[i].uncompressed_offset;
+      r.file_offset = chunks[i].file_offset;
+      r.index = results[i].index;
+      memcpy(out + 80 * k, &r, 80);
+      coff += chunks[i].length;
+    }
+    *n_records = order.size();
+    return NGPU_OK;
+  });
 }
 
 }  // extern "C"

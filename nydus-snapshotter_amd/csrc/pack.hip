@@ -136,7 +136,9 @@ class CopyPool {
 }  // namespace
 
 struct ngpu_pack : TarSink {
-  ngpu_engine *e = nullptr;
+  ngpu_engine *e = nullptr;    // one reference, dropped when the pack ends
+  ngpu_dict *dict = nullptr;   // the chunk dict it dedups against (one reference)
+  const volatile int32_t *cancel = nullptr;  // caller-owned cancel flag
   TarScanner sc;
   Slot slot[2];
   int cur = 0;
@@ -163,9 +165,15 @@ struct ngpu_pack : TarSink {
 
 namespace {
 
+bool cancelled(const ngpu_pack *p) {
+  return p->cancel && __atomic_load_n(p->cancel, __ATOMIC_RELAXED) != 0;
+}
+
 void release(ngpu_pack *p) {
   if (!p) return;
-  (void)hipSetDevice(p->e->device);
+  ngpu_engine *e = p->e;
+  ngpu_dict *dict = p->dict;
+  DeviceGuard dg(e->device);
   for (Slot &s : p->slot) {
     if (s.done) (void)hipEventSynchronize(s.done);
   }
@@ -195,6 +203,8 @@ void release(ngpu_pack *p) {
   if (p->copy) (void)hipStreamDestroy(p->copy);
   delete p->pool;
   delete p;
+  dict_unref(dict);
+  engine_unref(e);  // may free the engine if its creator already destroyed it
 }
 
 int grow_results(ngpu_pack *p, uint64_t want) {
@@ -287,13 +297,20 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
   std::vector<RafsV6BlobInfo> dict;
   const uint8_t *rec = opt.dict_blobs;
   uint64_t nrec = opt.n_dict_blobs;
-  if (!rec || !nrec) {
-    rec = e->dict_blobs.data();
-    nrec = e->dict_blobs.size() / sizeof(RafsV6BlobInfo);
+  if ((!rec || !nrec) && p->dict) {
+    rec = p->dict->blob_table.data();
+    nrec = p->dict->blob_table.size() / sizeof(RafsV6BlobInfo);
   }
   dict.resize(nrec);
   if (nrec) memcpy(dict.data(), rec, nrec * sizeof(RafsV6BlobInfo));
-  BlobWriter bw(o, w, ctx, std::move(dict));
+  const DictPlace *place = nullptr;
+  uint64_t nplace = 0;
+  if (p->dict && !p->dict->place.empty()) {
+    place = p->dict->place.data();
+    nplace = p->dict->place.size();
+  }
+  BlobWriter bw(o, w, ctx, std::move(dict), place, nplace);
+  bw.set_cancel(p->cancel);
   int rc = bw.init();
   if (rc) return fail(e, rc, "pack: %s", ngpu_host_error());
 
@@ -374,6 +391,10 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
   std::vector<const uint8_t *> hp;
   if (nw) rc = enqueue(0);
   for (uint64_t wi = 0; wi < nw && !rc; ++wi) {
+    if (cancelled(p)) {
+      rc = fail(e, NGPU_ECANCELED, "pack: cancelled");
+      break;
+    }
     if (wi + 1 < nw && (rc = enqueue(wi + 1))) break;
     const int b = wi & 1;
     if (hipEventSynchronize(ev[b]) != hipSuccess) {
@@ -397,12 +418,19 @@ extern "C" {
 
 int ngpu_pack_open(ngpu_engine *e, ngpu_pack **out) { return ngpu_pack_open_ex(e, 0, out); }
 
-int ngpu_pack_open_ex(ngpu_engine *e, uint32_t flags, ngpu_pack **out) {
+static ngpu_dict *const kDefaultDict = reinterpret_cast<ngpu_dict *>(1);
+
+static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack **out) {
   if (!e || !out || (flags & ~NGPU_PACK_RETAIN)) return NGPU_EINVAL;
   *out = nullptr;
   std::lock_guard<std::mutex> g(e->mu);
-  HIP_TRY(e, hipSetDevice(e->device));
+  DeviceGuard dg(e->device);
+  if (dict == kDefaultDict) dict = e->dict;
+  if (int rc = dict_check(e, dict)) return rc;
   ngpu_pack *p = new ngpu_pack(e);
+  engine_ref(e);
+  dict_ref(dict);
+  p->dict = dict;
   p->retain = flags & NGPU_PACK_RETAIN;
   uint64_t cap = e->cfg.staging_bytes;
   if (cap < 4ull * e->cfg.chunk_size) cap = 4ull * e->cfg.chunk_size;
@@ -441,8 +469,9 @@ int ngpu_pack_open_ex(ngpu_engine *e, uint32_t flags, ngpu_pack **out) {
          hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
   }
   // size the digest workspace once so no slot dispatch reallocates it
-  if (ok) ok = ensure_workspace(e, p->max_ch, cap, pick_group_log2(e, cap), e->dict.n_blobs, 1) == 0;
+  if (ok) ok = ensure_workspace(e, p->max_ch, cap, pick_group_log2(e, cap), dict_blobs(dict), 1) == 0;
   if (!ok) {
+    (void)hipGetLastError();
     release(p);
     return fail(e, NGPU_ENOMEM, "pack: staging allocation failed");
   }
@@ -450,13 +479,28 @@ int ngpu_pack_open_ex(ngpu_engine *e, uint32_t flags, ngpu_pack **out) {
   return 0;
 }
 
+int ngpu_pack_open_ex(ngpu_engine *e, uint32_t flags, ngpu_pack **out) {
+  return pack_open(e, kDefaultDict, flags, out);
+}
+
+int ngpu_pack_open_dict(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack **out) {
+  return pack_open(e, dict, flags, out);
+}
+
+int ngpu_pack_set_cancel(ngpu_pack *p, const volatile int32_t *flag) {
+  if (!p) return NGPU_EINVAL;
+  p->cancel = flag;
+  return 0;
+}
+
 int ngpu_pack_reserve(ngpu_pack *p, void **ptr, uint64_t *avail) {
   if (!p || !ptr || !avail) return NGPU_EINVAL;
   if (p->err) return p->err;
+  if (cancelled(p)) return p->err = fail(p->e, NGPU_ECANCELED, "pack: cancelled");
   Slot &s = p->slot[p->cur];
   if (s.fill == p->cap) {
     std::lock_guard<std::mutex> g(p->e->mu);
-    (void)hipSetDevice(p->e->device);
+    DeviceGuard dg(p->e->device);
     int rc = switch_slot(p);
     if (rc) return p->err = rc;
   }
@@ -469,9 +513,10 @@ int ngpu_pack_reserve(ngpu_pack *p, void **ptr, uint64_t *avail) {
 int ngpu_pack_commit(ngpu_pack *p, uint64_t n) {
   if (!p) return NGPU_EINVAL;
   if (p->err) return p->err;
+  if (cancelled(p)) return p->err = fail(p->e, NGPU_ECANCELED, "pack: cancelled");
   Slot &s = p->slot[p->cur];
   if (n > p->cap - s.fill) return p->err = NGPU_EINVAL;
-  const int rc = p->sc.feed(s.h + s.fill, n, *p);
+  const int rc = guarded([&] { return p->sc.feed(s.h + s.fill, n, *p); });
   s.fill += n;
   if (rc) return p->err = rc;
   return 0;
@@ -516,9 +561,9 @@ int ngpu_pack_close(ngpu_pack *p, ngpu_chunk **chunks_out, ngpu_result **results
                           nullptr);
 }
 
-int ngpu_pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx,
-                     ngpu_chunk **chunks_out, ngpu_result **results_out, uint64_t *n_out,
-                     ngpu_layer_stats *stats, ngpu_blob_info *info) {
+static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx,
+                       ngpu_chunk **chunks_out, ngpu_result **results_out, uint64_t *n_out,
+                       ngpu_layer_stats *stats, ngpu_blob_info *info) {
   if (!p || !chunks_out || !results_out || !n_out || (w && !opt)) {
     release(p);
     return NGPU_EINVAL;
@@ -528,6 +573,7 @@ int ngpu_pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w
   *n_out = 0;
   ngpu_engine *e = p->e;
   int rc = p->err ? p->err : p->sc.finish();
+  if (!rc && cancelled(p)) rc = fail(e, NGPU_ECANCELED, "pack: cancelled");
   if (!rc && w && !p->retain)
     rc = fail(e, NGPU_EINVAL, "pack: writing the blob stream needs ngpu_pack_open_ex(NGPU_PACK_RETAIN)");
   const uint64_t n = p->chunks.size();
@@ -536,7 +582,7 @@ int ngpu_pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w
   ngpu_layer_stats st{};
   if (!rc) {
     std::lock_guard<std::mutex> g(e->mu);
-    (void)hipSetDevice(e->device);
+    DeviceGuard dg(e->device);
     rc = dispatch(p, p->slot[p->cur], p->dispatched, n);
     if (!rc) rc = grow_results(p, n + 1);
     if (!rc && hipMalloc((void **)&p->d_all, (n + 1) * sizeof(ngpu_chunk)) != hipSuccess)
@@ -550,7 +596,8 @@ int ngpu_pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w
                          e->stream) != hipSuccess)
         rc = fail(e, NGPU_EHIP, "pack: chunk table copy failed");
     }
-    if (!rc) rc = enqueue_dedup(e, p->d_all, n, p->d_res, nullptr, 0, e->stream, nullptr, 1, nullptr);
+    if (!rc) rc = enqueue_dedup(e, p->dict, p->d_all, n, p->d_res, nullptr, 0, e->stream, nullptr, 1,
+                                nullptr);
     if (!rc && n &&
         hipMemcpyAsync(res, p->d_res, n * sizeof(ngpu_result), hipMemcpyDeviceToHost,
                        e->stream) != hipSuccess)
@@ -569,6 +616,12 @@ int ngpu_pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w
   *results_out = res;
   *n_out = n;
   return 0;
+}
+
+int ngpu_pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx,
+                     ngpu_chunk **chunks_out, ngpu_result **results_out, uint64_t *n_out,
+                     ngpu_layer_stats *stats, ngpu_blob_info *info) {
+  return guarded([&] { return pack_finish(p, opt, w, ctx, chunks_out, results_out, n_out, stats, info); });
 }
 
 }  // extern "C"

@@ -243,9 +243,7 @@ __device__ __forceinline__ uint32_t bswap_words(u32x4 v, int i) {
 
 // R round waves + R schedule waves per workgroup (R groups of 32 chunks), so
 // one workgroup per CU puts every wave on its own SIMD.
-// DIAG (benchmarks only, wrong digests): 1 = no cross-lane exchange,
-// 2 = the schedule waves do no work (round waves alone).
-template <int R, int DIAG>
+template <int R>
 __global__ __launch_bounds__(128 * R) void sha256_pair(
     const uint8_t *__restrict__ data, uint64_t data_len,
     const ngpu_chunk *__restrict__ chunks, uint64_t n,
@@ -369,8 +367,7 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
             uint32_t Y = (P3 ^ M) + kwv;
             asm("" : "+v"(Y));  // keep the DPP add a separate VOP2 op
             uint32_t Z =
-                Y + (DIAG == 1 ? P1 : (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P1, kDppRowRor8,
-                                                                            0xf, 0xf, false));
+                Y + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P1, kDppRowRor8, 0xf, 0xf, false);
             asm("" : "+v"(Z));
             const uint32_t S = xor3(rotr32(P0, r1), rotr32(P0, r2), rotr32(P0, r3));
             // bitop3 truth-table index is S0<<2 | S1<<1 | S2: 0x78 = a ^ (b & c)
@@ -384,7 +381,7 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
           H2 += side ? P2 : F2; H3 += side ? P3 : F3;
         }
       }
-    } else if (DIAG != 2) {
+    } else {
       produce(2 * ph + 2 + half, set ^ 1);
     }
     __syncthreads();
@@ -409,21 +406,15 @@ void launch_sha256(const uint8_t *data, uint64_t data_len,
   if (variant >= 1) {
     const dim3 g2((unsigned)((n + 63) / 64)), g1((unsigned)((n + 31) / 32));
     switch (variant) {
-      case 2:  // diagnostics
-        hipLaunchKernelGGL((sha256_pair<2, 1>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
-        break;
-      case 3:
-        hipLaunchKernelGGL((sha256_pair<2, 2>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
-        break;
       case 4:  // one group per workgroup
-        hipLaunchKernelGGL((sha256_pair<1, 0>), g1, dim3(128), 0, s, data, data_len, chunks, n, out, err);
+        hipLaunchKernelGGL((sha256_pair<1>), g1, dim3(128), 0, s, data, data_len, chunks, n, out, err);
         break;
       case 5:  // four groups per workgroup: a round and a schedule wave share each SIMD
-        hipLaunchKernelGGL((sha256_pair<4, 0>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0, s,
+        hipLaunchKernelGGL((sha256_pair<4>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0, s,
                            data, data_len, chunks, n, out, err);
         break;
       default:
-        hipLaunchKernelGGL((sha256_pair<2, 0>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
+        hipLaunchKernelGGL((sha256_pair<2>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
     }
     return;
   }

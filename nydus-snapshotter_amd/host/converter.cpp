@@ -4,8 +4,11 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <tuple>
 
 #include "nydus_gpu.h"
@@ -62,10 +65,11 @@ Error compressor_of(const std::string &s, uint32_t *out) {
   return {};
 }
 
-// One engine per (device, digester, chunk size, fs version), like the Python
-// mirror; an engine serialises its own calls.
+// One engine per (device, digester, chunk size, fs version, aligned chunk),
+// like the Python mirror; an engine serialises its own calls, and every Pack
+// holds its own chunk dict handle, so Packs share engines safely.
 std::mutex g_mu;
-std::map<std::tuple<int, uint32_t, uint32_t, uint32_t>, ngpu_engine *> g_engines;
+std::map<std::tuple<int, uint32_t, uint32_t, uint32_t, bool>, ngpu_engine *> g_engines;
 
 Error engine_for(const PackOption &opt, ngpu_engine **out) {
   uint32_t cs = 0;
@@ -76,7 +80,9 @@ Error engine_for(const PackOption &opt, ngpu_engine **out) {
   if (opt.Digester.empty() || opt.Digester == "blake3") dg = NGPU_DIGEST_BLAKE3;
   else if (opt.Digester == "sha256") dg = NGPU_DIGEST_SHA256;
   else return err(NGPU_EINVAL, "unsupported digester " + opt.Digester);
-  const auto key = std::make_tuple(opt.Device, dg, cs, (uint32_t)(fv[0] - '0'));
+  // AlignedChunk only matters for RAFS v5 (types.go:73-74; builder.go:131-133)
+  const bool aligned = opt.AlignedChunk && fv == "5";
+  const auto key = std::make_tuple(opt.Device, dg, cs, (uint32_t)(fv[0] - '0'), aligned);
   std::lock_guard<std::mutex> g(g_mu);
   auto it = g_engines.find(key);
   if (it == g_engines.end()) {
@@ -86,6 +92,7 @@ Error engine_for(const PackOption &opt, ngpu_engine **out) {
     cfg.digester = dg;
     cfg.chunk_size = cs;
     cfg.fs_version = std::get<3>(key);
+    if (aligned) cfg.flags |= NGPU_FLAG_ALIGNED_CHUNK;
     ngpu_engine *e = nullptr;
     if (int rc = ngpu_create(&cfg, &e)) return err(rc, "gpu engine: create failed");
     it = g_engines.emplace(key, e).first;
@@ -96,17 +103,30 @@ Error engine_for(const PackOption &opt, ngpu_engine **out) {
 
 class GpuPackWriteCloser : public PackWriteCloser {
  public:
-  GpuPackWriteCloser(ngpu_engine *e, ngpu_pack *p, Writer &dest, uint32_t comp)
-      : e_(e), p_(p), dest_(dest), comp_(comp) {}
+  GpuPackWriteCloser(ngpu_engine *e, ngpu_pack *p, Writer &dest, uint32_t comp, double timeout)
+      : e_(e), p_(p), dest_(dest), comp_(comp), timeout_(timeout) {
+    ngpu_pack_set_cancel(p_, &cancel_);
+    if (timeout_ > 0)  // builder.go:153-158: the builder runs under ctx.WithTimeout
+      timer_ = std::thread([this] {
+        std::unique_lock<std::mutex> g(tm_);
+        if (!tcv_.wait_for(g, std::chrono::duration<double>(timeout_), [this] { return done_; }))
+          Cancel();
+      });
+  }
   ~GpuPackWriteCloser() override {
+    StopTimer();
     if (p_) ngpu_pack_abort(p_);
   }
+  void Cancel() override { __atomic_store_n(&cancel_, 1, __ATOMIC_RELAXED); }
   Error Write(const void *p, size_t n) override {
     if (!p_) return err(NGPU_EINVAL, "write to a closed pack");
     if (!n) return {};
     if (int rc = ngpu_pack_write(p_, p, n)) {
-      p_ = nullptr;  // released by the library
-      return err(rc, std::string("pack write: ") + ngpu_last_error(e_));
+      Error e = Killed(rc, std::string("pack write: ") + ngpu_last_error(e_));
+      ngpu_pack_abort(p_);  // a failed write leaves the pack open
+      p_ = nullptr;
+      StopTimer();
+      return e;
     }
     return {};
   }
@@ -123,7 +143,8 @@ class GpuPackWriteCloser : public PackWriteCloser {
     ngpu_pack *p = p_;
     p_ = nullptr;
     const int rc = ngpu_pack_finish(p, &o, write_trampoline, &dest_, &ch, &res, &n, &st, &info);
-    if (rc) return err(rc, std::string("convert nydus ref: ") + ngpu_last_error(e_));
+    StopTimer();
+    if (rc) return Killed(rc, std::string("convert nydus ref: ") + ngpu_last_error(e_));
     ngpu_free_host(ch);
     ngpu_free_host(res);
     stats_.Digest = "sha256:" + hex(info.stream_digest, 32);
@@ -138,10 +159,32 @@ class GpuPackWriteCloser : public PackWriteCloser {
   const PackStats &Stats() const override { return stats_; }
 
  private:
+  // builder.go:169-171: a timed-out builder fails with "signal: killed"
+  Error Killed(int rc, const std::string &msg) const {
+    if (rc != NGPU_ECANCELED) return err(rc, msg);
+    char b[96] = "";
+    if (timeout_ > 0) snprintf(b, sizeof b, ", possibly due to timeout %gs", timeout_);
+    return err(rc, std::string("signal: killed") + b + ": " + msg);
+  }
+  void StopTimer() {
+    if (!timer_.joinable()) return;
+    {
+      std::lock_guard<std::mutex> g(tm_);
+      done_ = true;
+    }
+    tcv_.notify_all();
+    timer_.join();
+  }
   ngpu_engine *e_;
   ngpu_pack *p_;
   Writer &dest_;
   uint32_t comp_;
+  double timeout_;
+  alignas(4) volatile int32_t cancel_ = 0;
+  std::thread timer_;
+  std::mutex tm_;
+  std::condition_variable tcv_;
+  bool done_ = false;
   PackStats stats_;
 };
 
@@ -210,13 +253,17 @@ Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser>
   if (Error e = compressor_of(opt.Compressor, &comp)) return e;
   ngpu_engine *e = nullptr;
   if (Error x = engine_for(opt, &e)) return x;
-  int rc = opt.ChunkDictPath.empty() ? ngpu_dict_clear(e)
-                                     : ngpu_dict_load_bootstrap(e, opt.ChunkDictPath.c_str());
-  if (rc) return err(rc, "load chunk dict " + opt.ChunkDictPath + ": " + ngpu_last_error(e));
+  // the Pack's own dict handle (loaded once per unchanged ChunkDictPath and
+  // shared by every Pack naming it; builder.go:122-124 passes it per process)
+  ngpu_dict *d = nullptr;
+  int rc = 0;
+  if (!opt.ChunkDictPath.empty() && (rc = ngpu_dict_open(e, opt.ChunkDictPath.c_str(), &d)))
+    return err(rc, "load chunk dict " + opt.ChunkDictPath + ": " + ngpu_last_error(e));
   ngpu_pack *p = nullptr;
-  if ((rc = ngpu_pack_open_ex(e, NGPU_PACK_RETAIN, &p)))
-    return err(rc, std::string("pack open: ") + ngpu_last_error(e));
-  out->reset(new GpuPackWriteCloser(e, p, dest, comp));
+  rc = ngpu_pack_open_dict(e, d, NGPU_PACK_RETAIN, &p);
+  ngpu_dict_release(d);  // the pack holds its own reference
+  if (rc) return err(rc, std::string("pack open: ") + ngpu_last_error(e));
+  out->reset(new GpuPackWriteCloser(e, p, dest, comp, opt.Timeout));
   return {};
 }
 

@@ -96,7 +96,7 @@ struct PackOption {  // types.go:58-90
   bool OCIRef = false, AlignedChunk = false;
   std::string ChunkSize;       // power of two in [0x1000, 0x1000000] (types.go:76)
   std::string BatchSize;
-  double Timeout = 0;
+  double Timeout = 0;           // seconds; 0 = none (the builder's ctx.WithTimeout)
   bool Encrypt = false;
   std::string Digester;        // API extension: "blake3" (default) | "sha256"
   int Device = 0;              // GPU ordinal
@@ -124,6 +124,9 @@ struct PackStats {
 class PackWriteCloser : public WriteCloser {
  public:
   virtual const PackStats &Stats() const = 0;  // valid after a nil Close()
+  // ctx.Done(): the running or next Write / Close fails ("signal: killed",
+  // code NGPU_ECANCELED).  Safe from any thread.
+  virtual void Cancel() = 0;
 };
 
 Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser> *out);

@@ -20,8 +20,8 @@ KIND_NAMES = {0: "NEW", 1: "INTRA", 2: "DICT"}
 NEW, INTRA, DICT = 0, 1, 2
 
 ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ETAR", -5: "EUNSUPP",
-          -6: "ENODEV", -7: "EIO", -8: "EFORMAT", -9: "ENOTFOUND"}
-ENOTFOUND = -9
+          -6: "ENODEV", -7: "EIO", -8: "EFORMAT", -9: "ENOTFOUND", -10: "ECANCELED"}
+EINVAL, ENOTFOUND, ECANCELED = -1, -9, -10
 
 # PackOption.Compressor -> TOCEntry flag values (pkg/converter/types.go:22-31);
 # "" is nydus-image's default (zstd).
@@ -56,13 +56,18 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_pack_close", "ngpu_pack_abort", "ngpu_dedup_layers_device",
            "ngpu_process_layers_device", "ngpu_host_error", "ngpu_blob_write",
            "ngpu_pack_open_ex", "ngpu_pack_finish", "ngpu_unpack_entry", "ngpu_merge",
-           "ngpu_write_fd"]
+           "ngpu_write_fd", "ngpu_dict_open", "ngpu_dict_create", "ngpu_dict_create_device",
+           "ngpu_dict_retain", "ngpu_dict_release", "ngpu_dict_entries", "ngpu_set_dict",
+           "ngpu_dict_probe", "ngpu_process_dict", "ngpu_process_dict_device",
+           "ngpu_pack_open_dict", "ngpu_pack_set_cancel"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
                               ("blobs", "<u4"), ("uncompressed_size", "<u8")])
 
-HIT_DTYPE = np.dtype([("entry", "<u4"), ("index", "<u4"), ("blob", "<u4"), ("usize", "<u4")])
+HIT_DTYPE = np.dtype([("entry", "<u4"), ("index", "<u4"), ("blob", "<u4"), ("usize", "<u4"),
+                      ("uncompressed_offset", "<u8")])
+assert HIT_DTYPE.itemsize == 24
 MISS = 0xFFFFFFFF
 
 
@@ -74,6 +79,7 @@ class NgpuConfig(ctypes.Structure):
 
 
 FLAG_TIMING = 0x1
+FLAG_ALIGNED_CHUNK = 0x2
 
 
 class NgpuTiming(ctypes.Structure):
@@ -99,17 +105,20 @@ class NgpuBlobOptions(ctypes.Structure):
     _fields_ = [("compressor", ctypes.c_uint32), ("level", ctypes.c_int32),
                 ("threads", ctypes.c_uint32), ("digester", ctypes.c_uint32),
                 ("chunk_size", ctypes.c_uint32), ("n_dict_blobs", ctypes.c_uint32),
-                ("dict_blobs", ctypes.c_void_p)]
+                ("dict_blobs", ctypes.c_void_p), ("dict_chunks", ctypes.c_void_p),
+                ("n_dict_chunks", ctypes.c_uint64)]
 
 
 class NgpuBlobInfo(ctypes.Structure):
     _fields_ = [("stream_bytes", ctypes.c_uint64), ("blob_bytes", ctypes.c_uint64),
                 ("bootstrap_bytes", ctypes.c_uint64), ("blob_chunks", ctypes.c_uint64),
                 ("compressed_chunks", ctypes.c_uint64), ("stream_digest", ctypes.c_uint8 * 32),
-                ("blob_digest", ctypes.c_uint8 * 32), ("toc_digest", ctypes.c_uint8 * 32)]
+                ("blob_digest", ctypes.c_uint8 * 32), ("toc_digest", ctypes.c_uint8 * 32),
+                ("dict_records", ctypes.c_uint64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_[:5]}
+        d["dict_records"] = self.dict_records
         for k in ("stream_digest", "blob_digest", "toc_digest"):
             d[k] = bytes(getattr(self, k)).hex()
         return d
@@ -183,6 +192,22 @@ def lib():
     L.ngpu_unpack_entry.argtypes = [READ_AT_FN, vp, u64, ctypes.c_char_p, WRITE_FN, vp, vp]
     L.ngpu_merge.argtypes = [ctypes.POINTER(vp), pu64, ctypes.POINTER(ctypes.c_char_p), u64, vp,
                              u64, WRITE_FN, vp, ctypes.POINTER(vp)]
+    L.ngpu_dict_open.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
+    L.ngpu_dict_create.argtypes = [vp, vp, u64, vp, u32, ctypes.POINTER(vp)]
+    L.ngpu_dict_create_device.argtypes = [vp, vp, vp, vp, vp, vp, u64, u32, ctypes.POINTER(vp)]
+    L.ngpu_dict_retain.argtypes = [vp]
+    L.ngpu_dict_retain.restype = None
+    L.ngpu_dict_release.argtypes = [vp]
+    L.ngpu_dict_release.restype = None
+    L.ngpu_dict_entries.argtypes = [vp]
+    L.ngpu_dict_entries.restype = u64
+    L.ngpu_set_dict.argtypes = [vp, vp]
+    L.ngpu_dict_probe.argtypes = [vp, vp, u64, u64, vp, vp]
+    L.ngpu_process_dict.argtypes = [vp, vp, vp, u64, vp, u64, vp, ctypes.POINTER(NgpuLayerStats)]
+    L.ngpu_process_dict_device.argtypes = [vp, vp, vp, u64, vp, u64, vp, vp, u64, vp, vp,
+                                           ctypes.POINTER(NgpuLayerStats)]
+    L.ngpu_pack_open_dict.argtypes = [vp, vp, u32, ctypes.POINTER(vp)]
+    L.ngpu_pack_set_cancel.argtypes = [vp, vp]
     _lib = L
     return L
 
@@ -269,22 +294,29 @@ class _Sink:
 
 
 def blob_options(compressor: str = "", level: int = 0, threads: int = 0, digester: str = "blake3",
-                 chunk_size: int = 0x100000, dict_blobs: np.ndarray = None):
+                 chunk_size: int = 0x100000, dict_blobs: np.ndarray = None,
+                 dict_chunks: np.ndarray = None):
     if compressor not in COMPRESSORS:
         raise ValueError(f"unsupported compressor {compressor!r}")
     o = NgpuBlobOptions(compressor=COMPRESSORS[compressor], level=level, threads=threads,
                         digester=DIGESTERS[digester], chunk_size=chunk_size)
-    keep = None
+    keep = []
     if dict_blobs is not None and len(dict_blobs):
-        keep = np.ascontiguousarray(dict_blobs).view(np.uint8).reshape(-1)
-        o.n_dict_blobs = keep.size // 256
-        o.dict_blobs = keep.ctypes.data
+        b = np.ascontiguousarray(dict_blobs).view(np.uint8).reshape(-1)
+        o.n_dict_blobs = b.size // 256
+        o.dict_blobs = b.ctypes.data
+        keep.append(b)
+    if dict_chunks is not None and len(dict_chunks):
+        c = np.ascontiguousarray(dict_chunks).view(np.uint8).reshape(-1)
+        o.n_dict_chunks = c.size // 80
+        o.dict_chunks = c.ctypes.data
+        keep.append(c)
     return o, keep
 
 
 def blob_write(data, chunks, results, stats: dict, dest, compressor: str = "", level: int = 0,
                threads: int = 0, digester: str = "blake3", chunk_size: int = 0x100000,
-               dict_blobs: np.ndarray = None) -> dict:
+               dict_blobs: np.ndarray = None, dict_chunks: np.ndarray = None) -> dict:
     """Host: write the nydus blob stream of a packed layer to `dest` (a
     writable file-like); returns the ngpu_blob_info as a dict."""
     L = lib()
@@ -292,7 +324,7 @@ def blob_write(data, chunks, results, stats: dict, dest, compressor: str = "", l
     ch = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
     rs = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
     st = NgpuLayerStats(**{k: stats[k] for k, _ in NgpuLayerStats._fields_})
-    o, keep = blob_options(compressor, level, threads, digester, chunk_size, dict_blobs)
+    o, keep = blob_options(compressor, level, threads, digester, chunk_size, dict_blobs, dict_chunks)
     sink = _Sink(dest)
     info = NgpuBlobInfo()
     rc = L.ngpu_blob_write(_ptr(buf), buf.size, _ptr(ch), _ptr(rs), len(ch), ctypes.byref(st),
@@ -350,20 +382,64 @@ def merge(bootstraps, layer_digests, dict_bootstrap: bytes = None):
     return b"".join(out), (s.split(",") if s else [])
 
 
+DEFAULT_DICT = object()  # "the engine's default dict" (the calls without a dict argument)
+
+
+class ChunkDict:
+    """A chunk dict handle (ngpu_dict*): the HBM-resident HashChunkDict of one
+    ChunkDictPath (or of arrays), reference counted.  A pack opened with it
+    keeps its own reference, so releasing the handle never disturbs a pack."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @property
+    def handle(self) -> int:
+        return self._h.value if self._h else 0
+
+    @property
+    def entries(self) -> int:
+        return lib().ngpu_dict_entries(self._h)
+
+    def release(self):
+        if getattr(self, "_h", None):
+            lib().ngpu_dict_release(self._h)
+            self._h = None
+
+    __del__ = release
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.release()
+
+    def probe_device(self, d_digests: int, stride: int, n: int, d_hits: int, stream: int = 0):
+        rc = lib().ngpu_dict_probe(self._h, ctypes.c_void_p(d_digests), stride, n,
+                                   ctypes.c_void_p(d_hits), ctypes.c_void_p(stream) if stream else None)
+        if rc:
+            raise NgpuError(rc, "dict_probe")
+
+
+def _dict_arg(d):
+    return None if d is None else d._h
+
+
 class Engine:
     """One GPU engine (ngpu_engine*).  Mirrors the PackOption fields the
     digest/dedup stage consumes (pkg/converter/types.go:58-90)."""
 
     def __init__(self, device: int = 0, digester: str = "blake3", chunk_size: int = 0x100000,
                  fs_version: int = 6, leaves_per_lane: int = 0, staging_bytes: int = 0,
-                 timing: bool = False, flags: int = 0):
+                 timing: bool = False, flags: int = 0, aligned_chunk: bool = False):
         L = lib()
         if digester not in DIGESTERS:
             raise ValueError(f"unsupported digester {digester!r}")
         cfg = NgpuConfig(device=device, digester=DIGESTERS[digester], chunk_size=chunk_size,
                          fs_version=fs_version, staging_bytes=staging_bytes,
                          leaves_per_lane=leaves_per_lane,
-                         flags=flags | (FLAG_TIMING if timing else 0))
+                         flags=flags | (FLAG_TIMING if timing else 0) |
+                         (FLAG_ALIGNED_CHUNK if aligned_chunk else 0))
         h = ctypes.c_void_p()
         rc = L.ngpu_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc:
@@ -405,19 +481,62 @@ class Engine:
     def dict_clear(self):
         self._check(lib().ngpu_dict_clear(self._h), "dict_clear")
 
+    def dict_open(self, path: str) -> ChunkDict:
+        """ngpu_dict_open: load (or reuse, if unchanged) a RAFS v6 chunk-dict bootstrap."""
+        h = ctypes.c_void_p()
+        self._check(lib().ngpu_dict_open(self._h, path.encode(), ctypes.byref(h)), "dict_open")
+        return ChunkDict(h)
+
+    def dict_create(self, records, blobs=None) -> ChunkDict:
+        """From 80-B RAFS v6 chunk records (table order) + 256-B blob records."""
+        r = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
+        b = None if blobs is None or not len(blobs) else np.ascontiguousarray(blobs).view(np.uint8).reshape(-1)
+        h = ctypes.c_void_p()
+        self._check(lib().ngpu_dict_create(self._h, _ptr(r), r.size // 80, _ptr(b),
+                                           0 if b is None else b.size // 256, ctypes.byref(h)),
+                    "dict_create")
+        return ChunkDict(h)
+
+    def dict_create_device(self, d_digests: int, d_usize: int, d_blob: int, d_index: int, n: int,
+                           n_blobs: int, d_uoff: int = 0) -> ChunkDict:
+        h = ctypes.c_void_p()
+        self._check(lib().ngpu_dict_create_device(self._h, self._vp(d_digests), self._vp(d_usize),
+                                                  self._vp(d_blob), self._vp(d_index), self._vp(d_uoff),
+                                                  n, n_blobs, ctypes.byref(h)), "dict_create_device")
+        return ChunkDict(h)
+
+    def set_dict(self, d):
+        self._check(lib().ngpu_set_dict(self._h, _dict_arg(d)), "set_dict")
+
     @property
     def dict_size(self) -> int:
         return lib().ngpu_dict_size(self._h)
 
-    def process(self, data, chunks):
-        """Host data + chunk descriptors -> (RESULT_DTYPE array, stats dict)."""
+    def process(self, data, chunks, dict=DEFAULT_DICT):
+        """Host data + chunk descriptors -> (RESULT_DTYPE array, stats dict).
+        dict: a ChunkDict, None (no dict) or the engine's default."""
         buf = _buf(data)
         ch = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
         out = np.zeros(len(ch), dtype=RESULT_DTYPE)
         st = NgpuLayerStats()
-        self._check(lib().ngpu_process(self._h, _ptr(buf), buf.size, _ptr(ch), len(ch), _ptr(out),
-                                       ctypes.byref(st)), "process")
+        if dict is DEFAULT_DICT:
+            rc = lib().ngpu_process(self._h, _ptr(buf), buf.size, _ptr(ch), len(ch), _ptr(out),
+                                    ctypes.byref(st))
+        else:
+            rc = lib().ngpu_process_dict(self._h, _dict_arg(dict), _ptr(buf), buf.size, _ptr(ch),
+                                         len(ch), _ptr(out), ctypes.byref(st))
+        self._check(rc, "process")
         return out, st.as_dict()
+
+    def process_dict_device(self, dict, d_data: int, length: int, d_chunks: int, n: int, d_out: int,
+                            d_layer_first: int = 0, n_layers: int = 1, d_stats: int = 0,
+                            stream: int = 0, want_stats: bool = False):
+        st = NgpuLayerStats()
+        self._check(lib().ngpu_process_dict_device(
+            self._h, _dict_arg(dict), self._vp(d_data), length, self._vp(d_chunks), n, self._vp(d_out),
+            self._vp(d_layer_first), n_layers, self._vp(d_stats), self._vp(stream),
+            ctypes.byref(st) if want_stats else None), "process_dict_device")
+        return st.as_dict() if want_stats else None
 
     def process_device(self, d_data: int, length: int, d_chunks: int, n: int, d_out: int,
                        stream: int = 0, want_stats: bool = False):
@@ -488,10 +607,11 @@ class Engine:
         self._check(lib().ngpu_timing_at(self._h, back, ctypes.byref(t)), "timing_at")
         return t.as_dict()
 
-    def pack(self, retain: bool = False) -> "PackWriter":
+    def pack(self, retain: bool = False, dict=DEFAULT_DICT) -> "PackWriter":
         """Streaming Pack (converter.Pack mirror): returns a writer.  retain=True
-        keeps the layer in HBM so finish() can write the nydus blob stream."""
-        return PackWriter(self, retain)
+        keeps the layer in HBM so finish() can write the nydus blob stream.
+        dict: a ChunkDict, None, or the engine's default at open time."""
+        return PackWriter(self, retain, dict)
 
     def pack_tar(self, tar):
         """Whole tar layer -> (chunks, results, stats)."""
@@ -521,12 +641,24 @@ class PackWriter:
     any split, close() -> (chunks, results, stats).  Errors raise NgpuError;
     a failed writer is released (like Close() reporting the builder error)."""
 
-    def __init__(self, engine: Engine, retain: bool = False):
+    def __init__(self, engine: Engine, retain: bool = False, dict=DEFAULT_DICT):
         self._eng = engine
         h = ctypes.c_void_p()
-        engine._check(lib().ngpu_pack_open_ex(engine._h, PACK_RETAIN if retain else 0,
-                                              ctypes.byref(h)), "pack_open")
+        fl = PACK_RETAIN if retain else 0
+        if dict is DEFAULT_DICT:
+            rc = lib().ngpu_pack_open_ex(engine._h, fl, ctypes.byref(h))
+        else:
+            rc = lib().ngpu_pack_open_dict(engine._h, _dict_arg(dict), fl, ctypes.byref(h))
+        engine._check(rc, "pack_open")
         self._p = h
+        # cancel flag (ngpu_pack_set_cancel): caller-owned, outlives the pack
+        self._cancel = ctypes.c_int32(0)
+        lib().ngpu_pack_set_cancel(self._p, ctypes.byref(self._cancel))
+
+    def cancel(self):
+        """ctx.Done(): the running or next write / close fails with ECANCELED.
+        Safe to call from another thread."""
+        self._cancel.value = 1
 
     def write(self, data) -> int:
         buf = _buf(data)

@@ -32,7 +32,9 @@ import numpy as np
 import io
 import tarfile
 
-from ._lib import COMPRESSORS, DICT, ENOTFOUND, NEW, Engine, NgpuError, merge, unpack_entry
+import threading
+
+from ._lib import COMPRESSORS, DICT, ECANCELED, ENOTFOUND, NEW, Engine, NgpuError, merge, unpack_entry
 
 EntryBlob = "image.blob"            # convert_unix.go:45
 EntryBootstrap = "image.boot"       # :46
@@ -104,35 +106,84 @@ def parse_chunk_size(s: str) -> int:
     return v
 
 
+_ENGINES_MU = threading.Lock()
+
+
 def _engine(opt: PackOption) -> Engine:
     fs = int(opt.FsVersion or "6")
     if fs not in (5, 6):
         raise ConverterError(f"invalid fs version {opt.FsVersion}")
     dg = opt.Digester or "blake3"
-    key = (opt.Device, dg, parse_chunk_size(opt.ChunkSize), fs)
-    if key not in _ENGINES:
-        _ENGINES[key] = Engine(device=opt.Device, digester=dg, chunk_size=key[2], fs_version=fs)
-    return _ENGINES[key]
+    # AlignedChunk only matters for RAFS v5 (types.go:73-74): v6 always aligns
+    aligned = bool(opt.AlignedChunk) and fs == 5
+    key = (opt.Device, dg, parse_chunk_size(opt.ChunkSize), fs, aligned)
+    with _ENGINES_MU:
+        if key not in _ENGINES:
+            _ENGINES[key] = Engine(device=opt.Device, digester=dg, chunk_size=key[2], fs_version=fs,
+                                   aligned_chunk=aligned)
+        return _ENGINES[key]
 
 
 class _PackWriteCloser:
+    """One Pack: its own chunk dict handle (ngpu_dict_open: loaded once per
+    unchanged ChunkDictPath, shared by every Pack that names it) and its own
+    cancel flag, so concurrent Packs on one cached engine never see each
+    other's dict (the reference runs one nydus-image per Pack)."""
+
     def __init__(self, dest: BinaryIO, opt: PackOption):
         self._dest, self._opt = dest, opt
         if (opt.Compressor or "") not in COMPRESSORS:
             raise ConverterError(f"unsupported compressor {opt.Compressor!r}")
         self._eng = _engine(opt)
+        cd = None
         if opt.ChunkDictPath:
-            self._eng.dict_load_bootstrap(opt.ChunkDictPath)
-        else:
-            self._eng.dict_clear()
-        self._w = self._eng.pack(retain=True)
+            try:
+                cd = self._eng.dict_open(opt.ChunkDictPath)
+            except NgpuError as e:
+                raise ConverterError(f"load chunk dict {opt.ChunkDictPath}: {e}") from e
+        try:
+            self._w = self._eng.pack(retain=True, dict=cd)
+        finally:
+            if cd is not None:
+                cd.release()  # the pack holds its own reference
+        self._timer = None
+        if opt.Timeout:
+            # builder.go:153-158: exec.CommandContext(ctx with Timeout) kills the
+            # builder; here the pack's cancel flag stops it
+            self._timer = threading.Timer(opt.Timeout, self._w.cancel)
+            self._timer.daemon = True
+            self._timer.start()
         self.result = None
 
+    def _killed(self, e: NgpuError):
+        if e.code == ECANCELED:
+            why = f", possibly due to timeout {self._opt.Timeout}s" if self._opt.Timeout else ""
+            return ConverterError(f"signal: killed{why}: {e}")
+        return e
+
+    def cancel(self):
+        """ctx.Done(): the running write/close fails (safe from any thread)."""
+        self._w.cancel()
+
     def write(self, data) -> int:
-        return self._w.write(data)
+        try:
+            return self._w.write(data)
+        except NgpuError as e:
+            self._stop_timer()
+            raise self._killed(e) from e
+
+    def _stop_timer(self):
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
 
     def close(self):
-        ch, res, st, info = self._w.finish(self._dest, compressor=self._opt.Compressor or "")
+        try:
+            ch, res, st, info = self._w.finish(self._dest, compressor=self._opt.Compressor or "")
+        except NgpuError as e:
+            raise self._killed(e) from e
+        finally:
+            self._stop_timer()
         self.result = {"chunks": ch, "results": res, "stats": st, "info": info,
                        "digest": "sha256:" + info["stream_digest"]}
         return self.result

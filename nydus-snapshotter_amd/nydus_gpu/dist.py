@@ -28,6 +28,7 @@ from typing import Callable, Optional
 import torch
 
 MISS = 0xFFFFFFFF
+HIT_WORDS = 6  # ngpu_dict_hit as int32 words: entry, index, blob, usize, uoff lo, uoff hi
 
 
 def owner_of(digests: torch.Tensor, world: int) -> torch.Tensor:
@@ -39,9 +40,10 @@ def owner_of(digests: torch.Tensor, world: int) -> torch.Tensor:
 class ShardedChunkDict:
     """Digest-prefix partition of a chunk dict across ranks.
 
-    probe_fn(local_digests (m, 32) uint8) -> (m, 4) int32 hits in LOCAL entry
-    ids ([entry, index, blob, usize], entry == -1 for a miss).  On the GPU
-    path this is ``engine_probe_fn(engine)``.
+    probe_fn(local_digests (m, 32) uint8) -> (m, HIT_WORDS) int32 hits in
+    LOCAL entry ids (ngpu_dict_hit words: entry, index, blob, usize,
+    uncompressed offset lo/hi; entry == -1 for a miss).  On the GPU path this
+    is ``engine_probe_fn(engine)``.
     """
 
     def __init__(self, rank: int, world: int, group=None, comm_device=None):
@@ -59,14 +61,15 @@ class ShardedChunkDict:
         own = owner_of(digests, self.world) == self.rank
         return torch.nonzero(own, as_tuple=False).flatten()
 
-    def load(self, digests, usize, blob, index, n_blobs: int, load_fn):
-        """Keep this rank's partition.  load_fn(d, us, bl, ix) builds the local
-        table from the owned rows (engine.dict_load_device on the GPU)."""
+    def load(self, digests, usize, blob, index, n_blobs: int, load_fn, uoff=None):
+        """Keep this rank's partition.  load_fn(d, us, bl, ix, uo) builds the
+        local table from the owned rows (engine.dict_create_device on the GPU);
+        uoff (int64 uncompressed offsets) may be None."""
         ids = self.partition(digests)
         self.local_to_global = ids.to(torch.int64)
         self.n_blobs = n_blobs
         load_fn(digests[ids].contiguous(), usize[ids].contiguous(), blob[ids].contiguous(),
-                index[ids].contiguous())
+                index[ids].contiguous(), None if uoff is None else uoff[ids].contiguous())
         return int(ids.numel())
 
     def _a2a(self, out, inp, out_splits, in_splits):
@@ -74,7 +77,7 @@ class ShardedChunkDict:
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
     def probe(self, digests: torch.Tensor) -> torch.Tensor:
-        """digests (n, 32) uint8 -> hits (n, 4) int32 with global entry ids."""
+        """digests (n, 32) uint8 -> hits (n, HIT_WORDS) int32 with global entry ids."""
         n = digests.shape[0]
         dev = digests.device
         if self.world == 1:
@@ -90,16 +93,16 @@ class ShardedChunkDict:
         out_splits = rcounts.tolist()
         recv = torch.empty((sum(out_splits), 32), dtype=torch.uint8, device=cdev)
         self._a2a(recv, send, out_splits, in_splits)
-        hits = self._local(recv.to(dev)).to(cdev)  # (sum(out_splits), 4)
-        back = torch.empty((n, 4), dtype=torch.int32, device=cdev)
+        hits = self._local(recv.to(dev)).to(cdev)  # (sum(out_splits), HIT_WORDS)
+        back = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=cdev)
         self._a2a(back, hits.contiguous(), in_splits, out_splits)
-        res = torch.empty((n, 4), dtype=torch.int32, device=dev)
+        res = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=dev)
         res[order] = back.to(dev)
         return res
 
     def _local(self, digests: torch.Tensor) -> torch.Tensor:
         if digests.shape[0] == 0 or self.local_to_global is None or self.local_to_global.numel() == 0:
-            h = torch.zeros((digests.shape[0], 4), dtype=torch.int32, device=digests.device)
+            h = torch.zeros((digests.shape[0], HIT_WORDS), dtype=torch.int32, device=digests.device)
             h[:, 0] = -1
             return h
         h = self.probe_fn(digests).clone()
@@ -116,7 +119,7 @@ def engine_probe_fn(engine, stream_fn=None):
 
     def probe(d: torch.Tensor) -> torch.Tensor:
         d = d.contiguous()
-        hits = torch.empty((d.shape[0], 4), dtype=torch.int32, device=d.device)
+        hits = torch.empty((d.shape[0], HIT_WORDS), dtype=torch.int32, device=d.device)
         s = stream_fn() if stream_fn else torch.cuda.current_stream().cuda_stream
         engine.dict_probe_device(d.data_ptr(), 32, d.shape[0], hits.data_ptr(), stream=s)
         return hits
@@ -124,10 +127,12 @@ def engine_probe_fn(engine, stream_fn=None):
 
 
 def engine_load_fn(engine, n_blobs: int):
-    def load(d, us, bl, ix):
+    def load(d, us, bl, ix, uo=None):
         torch.cuda.current_stream().synchronize()
-        engine.dict_load_device(d.data_ptr(), us.data_ptr(), bl.data_ptr(), ix.data_ptr(),
-                                d.shape[0], n_blobs)
+        cd = engine.dict_create_device(d.data_ptr(), us.data_ptr(), bl.data_ptr(), ix.data_ptr(),
+                                       d.shape[0], n_blobs, d_uoff=uo.data_ptr() if uo is not None else 0)
+        engine.set_dict(cd if d.shape[0] else None)
+        cd.release()
     return load
 
 

@@ -106,6 +106,6 @@ uint64_t oracle_cpu_digest_dedup(const uint8_t *data, const oracle_chunk *chunks
   free(th);
   free(jobs);
   uint32_t own;
-  return oracle_dedup(digests, sizes, n, NULL, NULL, NULL, NULL, 0, 4096,
+  return oracle_dedup(digests, sizes, n, NULL, NULL, NULL, NULL, NULL, 0, 4096,
                       decisions, &own);
 }

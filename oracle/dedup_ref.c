@@ -69,8 +69,8 @@ static void map_add(map_t *m, uint64_t id) {
 uint64_t oracle_dedup(const uint8_t *digests, const uint32_t *sizes, uint64_t n,
                       const uint8_t *dict_digests, const uint32_t *dict_sizes,
                       const uint32_t *dict_blob, const uint32_t *dict_index,
-                      uint64_t m, uint32_t align, oracle_decision *out,
-                      uint32_t *own_blob) {
+                      const uint64_t *dict_uoff, uint64_t m, uint32_t align,
+                      oracle_decision *out, uint32_t *own_blob) {
   map_t gdict = {0}, layered = {0};
   uint32_t max_inner = 0;
   for (uint64_t j = 0; j < m; j++)
@@ -93,10 +93,13 @@ uint64_t oracle_dedup(const uint8_t *digests, const uint32_t *sizes, uint64_t n,
     if (e != UINT64_MAX && (dict_sizes[e] == 0 || dict_sizes[e] == sizes[i])) {
       uint32_t inner = dict_blob[e];
       if (real[inner] == UINT32_MAX) real[inner] = next_blob++;
+      /* chunk.copy_from(cached_chunk): index and uncompressed offset are the
+       * dict chunk's (its place in the dict's blob) */
       o->kind = ORACLE_DICT;
       o->ref = e;
       o->index = dict_index ? dict_index[e] : 0;
       o->blob_index = real[inner];
+      o->uncompressed_offset = dict_uoff ? dict_uoff[e] : 0;
       continue;
     }
     uint64_t l = map_get(&layered, d);

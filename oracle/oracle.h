@@ -83,8 +83,8 @@ typedef struct {
 uint64_t oracle_dedup(const uint8_t *digests, const uint32_t *sizes, uint64_t n,
                       const uint8_t *dict_digests, const uint32_t *dict_sizes,
                       const uint32_t *dict_blob, const uint32_t *dict_index,
-                      uint64_t m, uint32_t align, oracle_decision *out,
-                      uint32_t *own_blob);
+                      const uint64_t *dict_uoff, uint64_t m, uint32_t align,
+                      oracle_decision *out, uint32_t *own_blob);
 
 /* Digest every chunk of `data` (one call per chunk) into out (n x 32 B). */
 void oracle_digest_chunks(const uint8_t *data, const oracle_chunk *chunks,

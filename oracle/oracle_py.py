@@ -38,7 +38,7 @@ def lib():
         L.oracle_sha256.argtypes = [vp, ctypes.c_size_t, vp]
         L.oracle_tar_chunks.argtypes = [vp, u64, u32, vp, u64, ctypes.POINTER(u64)]
         L.oracle_tar_chunks.restype = ctypes.c_int64
-        L.oracle_dedup.argtypes = [vp, vp, u64, vp, vp, vp, vp, u64, u32, vp, ctypes.POINTER(u32)]
+        L.oracle_dedup.argtypes = [vp, vp, u64, vp, vp, vp, vp, vp, u64, u32, vp, ctypes.POINTER(u32)]
         L.oracle_dedup.restype = u64
         L.oracle_digest_chunks.argtypes = [vp, vp, u64, ctypes.c_int, vp]
         L.oracle_cpu_digest_dedup.argtypes = [vp, vp, u64, ctypes.c_int, ctypes.c_int, vp, vp, vp]
@@ -89,7 +89,9 @@ def digest_chunks(data, chunks, digester: str) -> np.ndarray:
 
 
 def dedup(digests, sizes, dict_digests=None, dict_sizes=None, dict_blob=None, dict_index=None,
-          align=4096):
+          align=4096, dict_uoff=None):
+    """Restated dedup decisions.  DICT decisions copy the dict entry's chunk
+    index and uncompressed offset (dict_uoff; 0 when not given)."""
     digests = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1, 32)
     sizes = np.ascontiguousarray(sizes, dtype=np.uint32)
     n = len(sizes)
@@ -99,11 +101,15 @@ def dedup(digests, sizes, dict_digests=None, dict_sizes=None, dict_blob=None, di
         dict_sizes = np.ascontiguousarray(dict_sizes, dtype=np.uint32)
         dict_blob = np.ascontiguousarray(dict_blob, dtype=np.uint32)
         dict_index = np.ascontiguousarray(dict_index, dtype=np.uint32)
+        if dict_uoff is not None:
+            dict_uoff = np.ascontiguousarray(dict_uoff, dtype=np.uint64)
     out = np.zeros(n, dtype=DECISION_DTYPE)
     own = ctypes.c_uint32(0)
     lib().oracle_dedup(_ptr(digests), _ptr(sizes), n, _ptr(dict_digests) if m else None,
                        _ptr(dict_sizes) if m else None, _ptr(dict_blob) if m else None,
-                       _ptr(dict_index) if m else None, m, align, _ptr(out), ctypes.byref(own))
+                       _ptr(dict_index) if m else None,
+                       _ptr(dict_uoff) if m and dict_uoff is not None else None, m, align,
+                       _ptr(out), ctypes.byref(own))
     return out, (None if own.value == 0xFFFFFFFF else own.value)
 
 

@@ -43,7 +43,8 @@ def cpu_results(oracle, tar, chunk, digester="blake3", dict_boot=None):
     if dict_boot is not None:
         d = rafs.read_v6(dict_boot)["chunks"]
         kw = dict(dict_digests=d["block_id"], dict_sizes=d["uncompressed_size"],
-                  dict_blob=d["blob_index"], dict_index=d["index"])
+                  dict_blob=d["blob_index"], dict_index=d["index"],
+                  dict_uoff=d["uncompressed_offset"])
     dec, own = oracle.dedup(dig, ch["length"], **kw)
     res = np.zeros(len(ch), nydus_gpu.RESULT_DTYPE)
     res["digest"] = dig
@@ -66,16 +67,41 @@ def cpu_results(oracle, tar, chunk, digester="blake3", dict_boot=None):
 
 def cpu_stream(oracle, tar, chunk, compressor, digester="blake3", dict_boot=None):
     ch, res, st = cpu_results(oracle, tar, chunk, digester, dict_boot)
-    dict_blobs = rafs.read_v6(dict_boot)["blobs"] if dict_boot is not None else None
+    dict_blobs = dict_chunks = None
+    if dict_boot is not None:
+        d = rafs.read_v6(dict_boot)
+        dict_blobs, dict_chunks = d["blobs"], d["chunks"]
     out = io.BytesIO()
     info = nydus_gpu.blob_write(tar, ch, res, st, out, compressor=compressor, digester=digester,
-                                chunk_size=chunk, dict_blobs=dict_blobs)
+                                chunk_size=chunk, dict_blobs=dict_blobs, dict_chunks=dict_chunks)
     return out.getvalue(), info, ch, res, st
 
 
-def check_stream(oracle, stream, info, tar, ch, res, compressor, digester="blake3"):
+def expected_dict_records(ch, res, dict_chunks):
+    """The chunk-dict records a layer bootstrap must carry (restated
+    [nydus v2.3.0] deduplicate_chunk: chunk.copy_from(dict chunk) +
+    set_file_offset + real blob index; one record per distinct (digest, real
+    blob), VERIFY): a copy of the dict record with the layer's blob index and
+    the first occurrence's file offset."""
+    out, seen = [], set()
+    for i in np.nonzero(res["kind"] == nydus_gpu.DICT)[0]:
+        key = (bytes(res["digest"][i]), int(res["blob_index"][i]))
+        if key in seen:
+            continue
+        seen.add(key)
+        r = dict_chunks[int(res["ref"][i])].copy()
+        assert bytes(r["block_id"]) == key[0]
+        r["blob_index"] = key[1]
+        r["file_offset"] = ch["file_offset"][i]
+        r["uncompressed_size"] = ch["length"][i]
+        out.append(r)
+    return np.array(out, dtype=rafs.CHUNK_INFO_DTYPE)
+
+
+def check_stream(oracle, stream, info, tar, ch, res, compressor, digester="blake3", dict_boot=None):
     """Everything the reference reader and the fixture rules say about a Pack
-    output, plus round trip of every chunk record."""
+    output, plus round trip of every own-blob chunk record and the exact
+    chunk-dict records (dict_boot: the ChunkDictPath bootstrap)."""
     assert info["stream_bytes"] == len(stream)
     assert info["stream_digest"] == hashlib.sha256(stream).hexdigest()       # a9
     assert info["toc_digest"] == blob_ref.calc_blob_toc_digest(stream)
@@ -94,10 +120,18 @@ def check_stream(oracle, stream, info, tar, ch, res, compressor, digester="blake
         assert toc is not None and toc["name"].decode() == name
     b = rafs.read_v6(boot)
     assert b["flags"] & (0x8 if digester == "sha256" else 0x4)
-    recs = b["chunks"]
-    new = np.nonzero(res["kind"] == nydus_gpu.NEW)[0]
-    assert len(recs) == len(new) == info["blob_chunks"]
     own = [i for i, bb in enumerate(b["blobs"]) if bb["blob_id"].decode() == info["blob_digest"]]
+    new = np.nonzero(res["kind"] == nydus_gpu.NEW)[0]
+    allrecs = b["chunks"]
+    recs = allrecs[allrecs["blob_index"] == own[0]] if own else allrecs[:0]
+    drecs = allrecs[allrecs["blob_index"] != own[0]] if own else allrecs
+    assert len(recs) == len(new) == info["blob_chunks"]
+    assert len(drecs) == info["dict_records"]
+    if dict_boot is not None:
+        exp = expected_dict_records(ch, res, rafs.read_v6(dict_boot)["chunks"])
+        assert rafs.canonical(drecs) == rafs.canonical(exp)
+    else:
+        assert len(drecs) == 0
     if len(new):
         assert len(own) == 1
         ob = b["blobs"][own[0]]
@@ -219,7 +253,10 @@ def test_testpack_flow_cpu_decisions(oracle, tars, tmp_path):
                                                 dict_boot=dict_boot)
     assert (lres["kind"] == nydus_gpu.DICT).all() and lst["own_blob_index"] == 0xFFFFFFFF
     assert linfo["blob_bytes"] == 0
-    check_stream(oracle, ustream, uinfo, tars["oci_upper"], uch, ures, "zstd")
+    # the lower layer's bootstrap lists the dict chunks under the dict blob
+    check_stream(oracle, lstream, linfo, tars["oci_lower"], lch, lres, "zstd", dict_boot=dict_boot)
+    assert linfo["dict_records"] == len({bytes(d) for d in lres["digest"]}) > 0
+    check_stream(oracle, ustream, uinfo, tars["oci_upper"], uch, ures, "zstd", dict_boot=dict_boot)
     ldig = "sha256:" + hashlib.sha256(lstream).hexdigest()
     udig = "sha256:" + hashlib.sha256(ustream).hexdigest()
     out = io.BytesIO()
@@ -228,9 +265,16 @@ def test_testpack_flow_cpu_decisions(oracle, tars, tmp_path):
     assert blobs == [ddig, udig]
     m = rafs.read_v6(out.getvalue())
     assert m["blob_ids"] == [ddig[7:], udig[7:]]
-    # every merged chunk record points at the blob that holds its data
-    nu = int((ures["kind"] == nydus_gpu.NEW).sum())
-    assert (m["chunks"]["blob_index"][-nu:] == 1).all()
+    # every merged chunk record points at the blob that holds its data: the
+    # upper layer's NEW chunks at its own blob, the lower's dict chunks at the dict's
+    new_ids = {bytes(d) for d in ures["digest"][ures["kind"] == nydus_gpu.NEW]}
+    dict_ids = {bytes(d) for d in lres["digest"]}
+    for r in m["chunks"]:
+        k = bytes(r["block_id"])
+        assert r["blob_index"] == (1 if k in new_ids else 0), k.hex()
+        assert k in new_ids or k in dict_ids
+    assert len(m["chunks"]) == len(new_ids | dict_ids) + int(
+        sum(1 for k in {bytes(d) for d in ures["digest"][ures["kind"] == nydus_gpu.DICT]} if k not in dict_ids))
     # WithTar: image/ + image/image.boot (utils.go:92-160)
     out2 = io.BytesIO()
     cv.Merge([cv.Layer(ldig, lstream), cv.Layer(udig, ustream)], out2,

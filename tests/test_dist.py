@@ -45,10 +45,10 @@ def _expected(d, us, bl, ix, q):
     first = {}
     for i, row in enumerate(d):
         first.setdefault(row.tobytes(), i)
-    out = np.zeros((len(q), 4), np.int64)
+    out = np.zeros((len(q), 6), np.int64)
     for i, row in enumerate(q):
         e = first.get(row.tobytes(), -1)
-        out[i] = (e, ix[e], bl[e], us[e]) if e >= 0 else (-1, 0, 0, 0)
+        out[i] = (e, ix[e], bl[e], us[e], 4096 * e, 0) if e >= 0 else (-1, 0, 0, 0, 0, 0)
     return out
 
 
@@ -61,15 +61,18 @@ def _worker(rank, world, port, ret):
         sd = ShardedChunkDict(rank, world)
         local = {}
 
-        def load(dd, uu, bb, ii):
+        def load(dd, uu, bb, ii, uo):
             for k in range(dd.shape[0]):
-                local.setdefault(dd[k].numpy().tobytes(), (k, int(ii[k]), int(bb[k]), int(uu[k])))
+                local.setdefault(dd[k].numpy().tobytes(),
+                                 (k, int(ii[k]), int(bb[k]), int(uu[k]), int(uo[k]) & 0xFFFFFFFF,
+                                  int(uo[k]) >> 32))
 
+        uoff = torch.arange(len(d), dtype=torch.int64) * 4096
         n_local = sd.load(torch.from_numpy(d), torch.from_numpy(us), torch.from_numpy(bl),
-                          torch.from_numpy(ix), 5, load)
+                          torch.from_numpy(ix), 5, load, uoff=uoff)
 
         def probe(q):
-            out = torch.zeros((q.shape[0], 4), dtype=torch.int32)
+            out = torch.zeros((q.shape[0], 6), dtype=torch.int32)
             out[:, 0] = -1
             for k in range(q.shape[0]):
                 h = local.get(q[k].numpy().tobytes())

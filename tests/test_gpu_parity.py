@@ -356,7 +356,7 @@ def test_split_stages_equal_process(oracle):
                                  want_stats=True)
         o2 = torch.zeros_like(o1)
         eng.digest_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), n, o2.data_ptr())
-        hits = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+        hits = torch.empty((n, 6), dtype=torch.int32, device="cuda")  # ngpu_dict_hit, 24 B
         eng.dict_probe_device(o2.data_ptr(), 64, n, hits.data_ptr())
         st2 = eng.dedup_device(d_ch.data_ptr(), n, o2.data_ptr(), hits.data_ptr(), 3, want_stats=True)
         torch.cuda.synchronize()
@@ -662,10 +662,20 @@ def test_converter_testpack_flow(tars, oracle, tmp_path):
     lstream, lres = pack(tars["oci_lower"], dict_path)
     ustream, ures = pack(tars["oci_upper"], dict_path)
     assert (lres["results"]["kind"] == nydus_gpu.DICT).all()
+    from nydus_gpu import inspect as ni
     for tar, stream, res in ((tars["oci_lower"], lstream, lres), (tars["oci_upper"], ustream, ures)):
         ref = cpu_stream(oracle, tar, 0x100000, "zstd", dict_boot=merged.getvalue())
         assert stream == ref[0]
-        check_stream(oracle, stream, res["info"], tar, res["chunks"], res["results"], "zstd")
+        # the layer bootstrap lists its dict chunks under the dict blob, copied
+        # from the dict's records (check_stream compares them to the expectation)
+        check_stream(oracle, stream, res["info"], tar, res["chunks"], res["results"], "zstd",
+                     dict_boot=merged.getvalue())
+        a, b = tmp_path / "gpu.stream", tmp_path / "oracle.stream"
+        a.write_bytes(stream)
+        b.write_bytes(ref[0])
+        assert ni.main(["--diff", str(a), str(b)]) == 0
+        assert ni.canonical(ni.load_bootstrap(stream)) == ni.canonical(ni.load_bootstrap(ref[0]))
+    assert lres["info"]["dict_records"] == len({bytes(d) for d in lres["results"]["digest"]}) > 0
     out = _io.BytesIO()
     blobs = cv.Merge([cv.Layer(lres["digest"], lstream), cv.Layer(ures["digest"], ustream)], out,
                      cv.MergeOption(ChunkDictPath=dict_path))

@@ -23,7 +23,7 @@ def test_header_symbols_exported():
     L = nydus_gpu.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.ngpu_abi_version() == 1
+    assert L.ngpu_abi_version() == 2
 
 
 def test_struct_sizes():
@@ -120,8 +120,10 @@ def test_merge_blob_bookkeeping():
     layer's non-dict blob takes the layer digest (convert_unix.go:567-573)."""
     recs = np.zeros(3, rafs.CHUNK_INFO_DTYPE)
     recs["blob_index"] = [0, 1, 1]
+    recs["block_id"][:, 0] = [1, 2, 3]
     a = rafs.write_v6_bootstrap(recs, 0x100000, blobs=rafs.make_blob_table(["aa" * 32, "bb" * 32], 0x100000))
     recs2 = np.zeros(1, rafs.CHUNK_INFO_DTYPE)
+    recs2["block_id"][:, 0] = 9
     b = rafs.write_v6_bootstrap(recs2, 0x100000, blobs=rafs.make_blob_table(["cc" * 32], 0x100000))
     c = rafs.write_v6_bootstrap(recs2, 0x100000, blobs=rafs.make_blob_table(["bb" * 32], 0x100000))
     d = rafs.write_v6_bootstrap(np.zeros(0, rafs.CHUNK_INFO_DTYPE), 0x100000,
@@ -134,6 +136,9 @@ def test_merge_blob_bookkeeping():
     # without digests the ids are kept
     merged, ids = nydus_gpu.merge([b], [""])
     assert ids == ["cc" * 32]
+    # two layers carrying the same dict chunk record: one record per (digest, blob)
+    merged, ids = nydus_gpu.merge([c, c], ["11" * 32, "22" * 32], d)
+    assert ids == ["bb" * 32] and len(rafs.read_v6(merged)["chunks"]) == 1
 
 
 def test_tar_scanner_fuzz_agrees_with_oracle(tars, oracle):
