@@ -355,6 +355,43 @@ int ngpu_pack_close(ngpu_pack *p, ngpu_chunk **chunks_out, ngpu_result **results
                     uint64_t *n_out, ngpu_layer_stats *stats);
 void ngpu_pack_abort(ngpu_pack *p);
 
+/* ---- multi-GPU node ------------------------------------
+ * One process drives the GPUs of a node: one engine per listed device (a
+ * device may be listed twice, e.g. to rehearse a 2-GPU node on one GPU).
+ * Layers are independent units: ngpu_node_pack_open spreads streaming Packs
+ * over the engines round robin, ngpu_node_process_device runs device-resident
+ * layers on a chosen engine.  A node chunk dict is either partitioned by
+ * digest prefix -- entry with digest d lives on device
+ * ((d[0] << 8 | d[1]) * n) >> 16, keeping table order, so "first entry wins"
+ * holds per digest -- or replicated on every device.  Probing a partitioned
+ * dict is the node's exchange step: the requester's digests go to every
+ * owner over xGMI (hipMemcpyPeerAsync), each owner probes the entries it owns
+ * and the hits come back the same way, ordered by cross-device events, with
+ * GLOBAL entry ids -- the in-process form of the north star's digest-prefix
+ * all-to-all (nydus_gpu/dist.py keeps the one-process-per-GPU RCCL form).
+ * Peer access between the listed devices is enabled at creation. */
+typedef struct ngpu_node ngpu_node;
+int ngpu_node_create(const int32_t *devices, uint32_t n, const ngpu_config *cfg, ngpu_node **out);
+void ngpu_node_destroy(ngpu_node *node);
+uint32_t ngpu_node_size(const ngpu_node *node);
+/* The node's engine i (borrowed: valid until ngpu_node_destroy). */
+ngpu_engine *ngpu_node_engine(ngpu_node *node, uint32_t i);
+#define NGPU_NODE_DICT_PARTITION 0u /* shard by digest prefix (default) */
+#define NGPU_NODE_DICT_REPLICATE 1u /* a full copy on every device */
+/* Node chunk dicts, usable by any engine of the node (ngpu_pack_open_dict,
+ * ngpu_process_dict*, ngpu_node_*); checks as ngpu_dict_open. */
+int ngpu_node_dict_open(ngpu_node *node, const char *path, uint32_t mode, ngpu_dict **out);
+int ngpu_node_dict_create(ngpu_node *node, const void *records, uint64_t n,
+                          const void *blob_table, uint32_t n_blobs, uint32_t mode,
+                          ngpu_dict **out);
+/* Device index of the node device that owns digests[32] (partitioned dicts). */
+uint32_t ngpu_node_owner(const ngpu_node *node, const uint8_t *digest);
+int ngpu_node_pack_open(ngpu_node *node, ngpu_dict *dict, uint32_t flags, ngpu_pack **out);
+int ngpu_node_process_device(ngpu_node *node, uint32_t i, ngpu_dict *dict, const void *d_data,
+                             uint64_t len, const ngpu_chunk *d_chunks, uint64_t n,
+                             ngpu_result *d_out, const uint64_t *d_layer_first,
+                             uint64_t n_layers, ngpu_layer_stats *d_stats, void *stream);
+
 /* ---- RAFS v6 chunk table ---------------------------- */
 /* Serialise the layer's unique chunk records (NEW chunks in index order) as
  * 80-byte RAFS v6 chunk-info entries.  compressor "none": compressed size =

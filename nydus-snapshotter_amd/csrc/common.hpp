@@ -193,6 +193,15 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                   ngpu_layer_stats *st, hipStream_t s);
 void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
                        const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s);
+// Node dict exchange (node.hip): pack n digests (byte stride) to 32-B rows;
+// probe the rows a part owns (owner = ((d0 << 8 | d1) * W) >> 16); merge the
+// W parts' hit arrays (W x n) by owner.
+void launch_pack_digests(const uint8_t *src, uint64_t stride, uint64_t n, uint8_t *dst,
+                         hipStream_t s);
+void launch_dict_probe_owned(const uint8_t *q, uint64_t n, uint32_t owner, uint32_t W,
+                             const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s);
+void launch_hits_merge(const uint8_t *q, uint64_t n, uint32_t W, const ngpu_dict_hit *parts,
+                       ngpu_dict_hit *hits, hipStream_t s);
 // RAFS v6 chunk records (80 B, device) -> the dict's SoA arrays.
 void launch_dict_unpack(const uint8_t *recs, uint64_t n, uint8_t *digests, uint32_t *usize,
                         uint32_t *blob, uint32_t *index, uint64_t *uoff, hipStream_t s);
@@ -220,6 +229,10 @@ struct Workspace {
   uint64_t cap_layers = 0;
   uint64_t *stats = nullptr;      // device-side counters (ngpu_layer_stats)
   uint64_t cap_n = 0, cap_g = 0, cap_blobs = 0;
+  // node dict exchange: packed digests (n x 32), per-part hits (W x n), hits (n)
+  uint8_t *xq = nullptr;
+  ngpu_dict_hit *xparts = nullptr, *xhits = nullptr;
+  uint64_t cap_x = 0, cap_xparts = 0;
   int load_mode = 0;              // b3_groups load mode (see blake3.hip)
 };
 

@@ -488,6 +488,72 @@ void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
                      digests, stride, n, dict, hits);
 }
 
+// ---- node dict exchange (node.hip) -------------------------------------------
+namespace {
+
+__device__ __forceinline__ uint32_t owner_of(uint32_t w0, uint32_t W) {
+  const uint32_t hi = (w0 & 0xFF) << 8 | ((w0 >> 8) & 0xFF);  // digest bytes 0, 1
+  return (uint32_t)(((uint64_t)hi * W) >> 16);
+}
+
+__global__ void pack_digests(const uint8_t *__restrict__ src, uint64_t stride, uint64_t n,
+                             uint8_t *__restrict__ dst) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4 *p = reinterpret_cast<const uint4 *>(src + i * stride);
+  uint4 *o = reinterpret_cast<uint4 *>(dst + 32 * i);
+  o[0] = p[0];
+  o[1] = p[1];
+}
+
+__global__ void dict_probe_owned(const uint8_t *__restrict__ q, uint64_t n, uint32_t owner,
+                                 uint32_t W, DictDevice dict, ngpu_dict_hit *__restrict__ hits) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4 *p = reinterpret_cast<const uint4 *>(q + 32 * i);
+  const uint4 a = p[0];
+  if (owner_of(a.x, W) != owner) return;  // another part answers this one
+  uint32_t e = kNone;
+  if (dict.m) {
+    const uint4 b = p[1];
+    const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
+  }
+  hits[i] = dict_hit_of(dict, e);
+}
+
+__global__ void hits_merge(const uint8_t *__restrict__ q, uint64_t n, uint32_t W,
+                           const ngpu_dict_hit *__restrict__ parts,
+                           ngpu_dict_hit *__restrict__ hits) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t w0 = reinterpret_cast<const uint32_t *>(q + 32 * i)[0];
+  hits[i] = parts[(uint64_t)owner_of(w0, W) * n + i];
+}
+
+}  // namespace
+
+void launch_pack_digests(const uint8_t *src, uint64_t stride, uint64_t n, uint8_t *dst,
+                         hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(pack_digests, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, stride,
+                     n, dst);
+}
+
+void launch_dict_probe_owned(const uint8_t *q, uint64_t n, uint32_t owner, uint32_t W,
+                             const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(dict_probe_owned, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, n,
+                     owner, W, dict, hits);
+}
+
+void launch_hits_merge(const uint8_t *q, uint64_t n, uint32_t W, const ngpu_dict_hit *parts,
+                       ngpu_dict_hit *hits, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(hits_merge, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, n, W, parts,
+                     hits);
+}
+
 void launch_dict_unpack(const uint8_t *recs, uint64_t n, uint8_t *digests, uint32_t *usize,
                         uint32_t *blob, uint32_t *index, uint64_t *uoff, hipStream_t s) {
   if (n == 0) return;

@@ -25,7 +25,7 @@ using namespace ngpu;
 
 namespace ngpu {
 
-uint64_t next_pow2(uint64_t x);
+void node_dict_free(ngpu_dict *d);  // node.hip
 
 void dict_ref(ngpu_dict *d) {
   if (d) d->refs.fetch_add(1, std::memory_order_relaxed);
@@ -33,6 +33,7 @@ void dict_ref(ngpu_dict *d) {
 
 void dict_unref(ngpu_dict *d) {
   if (!d || d->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+  if (!d->io.empty() || !d->parts.empty()) node_dict_free(d);
   DeviceGuard g(d->device);
   // hipFree waits for the device, so no queued probe still reads the table
   for (void *p : d->allocs) (void)hipFree(p);
@@ -41,7 +42,9 @@ void dict_unref(ngpu_dict *d) {
 
 int dict_check(ngpu_engine *e, const ngpu_dict *d) {
   if (!d) return 0;
-  if (d->device != e->device)
+  bool here = d->device == e->device;
+  for (const ngpu_dict *p : d->parts) here = here || p->device == e->device;  // node dicts
+  if (!here)
     return fail(e, NGPU_EINVAL, "chunk dict lives on device %d, engine on %d", d->device, e->device);
   if (d->digester != e->cfg.digester)
     return fail(e, NGPU_EINVAL, "inconsistent digester: chunk dict %s vs engine %s",
@@ -413,6 +416,7 @@ uint64_t ngpu_dict_size(const ngpu_engine *e) {
 int ngpu_dict_probe(const ngpu_dict *d, const uint8_t *d_digests, uint64_t stride, uint64_t n,
                     ngpu_dict_hit *d_hits, void *stream) {
   if (!d || (n && (!d_digests || !d_hits)) || stride < 32 || (stride & 15)) return NGPU_EINVAL;
+  if (!d->parts.empty()) return NGPU_EINVAL;  // node dicts are probed through an engine
   DeviceGuard dg(d->device);
   launch_dict_probe(d_digests, stride, n, d->dev, d_hits, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? 0 : NGPU_EHIP;

@@ -188,6 +188,13 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chu
   int rc = ensure_workspace(e, n, 0, 0, n_blobs, L);
   if (rc) return rc;
   if ((rc = ws_acquire(e, s))) return rc;
+  if (!d_hits && dict && !dict->parts.empty()) {  // node dict (node.hip)
+    ngpu_dict *replica = nullptr;
+    rc = node_dict_hits(e, const_cast<ngpu_dict *>(dict), reinterpret_cast<const uint8_t *>(d_out),
+                        sizeof(ngpu_result), n, s, &d_hits, &replica);
+    if (rc) return rc;
+    if (replica) dict = replica;
+  }
   if (!d_stats) d_stats = e->ws.lstats;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   const uint32_t align =
@@ -218,7 +225,7 @@ void engine_unref(ngpu_engine *e) {
   Workspace &ws = e->ws;
   void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.nbytes, ws.ndict, ws.tstat,
                   ws.intra, ws.blob_first, ws.blob_real, ws.stats, ws.chunk_layer,
-                  ws.lfirst1, ws.lstats, ws.small, ws.tree_list,
+                  ws.lfirst1, ws.lstats, ws.small, ws.tree_list, ws.xq, ws.xparts, ws.xhits,
                   e->d_data, e->d_chunks, e->d_results};
   for (void *p : bufs)
     if (p) (void)hipFree(p);

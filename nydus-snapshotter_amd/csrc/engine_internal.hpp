@@ -35,6 +35,20 @@ struct ngpu_dict {
   std::string path;
   uint64_t st_dev = 0, st_ino = 0, st_size = 0;
   int64_t st_mtime_ns = 0;
+  // node dicts (node.hip): one part per node device -- a digest-prefix shard
+  // (its DictDevice::gid maps local to global entry ids) or a full replica --
+  // and per part a probe stream plus the exchange buffers on its device.
+  // dev.m / dev.n_blobs are the global counts; dev's arrays stay null.
+  struct PartIO {
+    hipStream_t stream = nullptr;
+    uint8_t *q = nullptr;        // requester digests (n x 32), copied in
+    ngpu_dict_hit *h = nullptr;  // this part's hits (n), copied back
+    uint64_t cap = 0;
+  };
+  std::vector<ngpu_dict *> parts;
+  std::vector<PartIO> io;
+  bool replicated = false;
+  std::mutex io_mu;
 };
 
 struct ngpu_engine {
@@ -104,6 +118,17 @@ int dict_check(ngpu_engine *e, const ngpu_dict *d);
 // The engine's default dict with one more reference (null if none).
 ngpu_dict *default_dict(ngpu_engine *e);
 inline uint32_t dict_blobs(const ngpu_dict *d) { return d ? d->dev.n_blobs : 0; }
+uint64_t next_pow2(uint64_t x);
+// From 80-B RAFS v6 records in host memory on engine e's device (e->mu held).
+int dict_from_records(ngpu_engine *e, const uint8_t *recs, uint64_t m, const uint8_t *blobs,
+                      uint32_t n_blobs, ngpu_dict **out);
+int read_dict_bootstrap(ngpu_engine *e, const char *path, uint64_t file_size,
+                        std::vector<uint8_t> *recs, std::vector<uint8_t> *blobs);
+// Node dicts: the replica on e's device, or (partitioned) route the probe of
+// n digests (byte stride) over the parts into e's workspace hits, ordered on
+// stream s.  *hits = the per-chunk hits with global entry ids.
+int node_dict_hits(ngpu_engine *e, ngpu_dict *d, const uint8_t *digests, uint64_t stride,
+                   uint64_t n, hipStream_t s, const ngpu_dict_hit **hits, ngpu_dict **replica);
 
 }  // namespace ngpu
 

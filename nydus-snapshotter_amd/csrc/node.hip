@@ -1,0 +1,329 @@
+// node.hip — one process driving the GPUs of a node, and
+// node chunk dicts: partitioned by digest prefix, or replicated.
+//
+// The reference converts layers concurrently in one process (goroutines,
+// pkg/converter/convert_unix.go:467-538) and hands each to its own
+// nydus-image; the chunk dict is loaded by every one of them.  Here a node
+// keeps one engine per GPU and one dict for all of them.  A partitioned dict
+// keeps the entries whose digest prefix maps to device o on device o
+// (owner = ((d[0] << 8 | d[1]) * n) >> 16, nydus_gpu/dist.py's rule), in
+// global table order, with their global entry ids, so "first entry wins" and
+// the DICT results are the same as with the whole dict on one GPU.
+//
+// The exchange (the north star's digest-prefix all-to-all, in-process): the
+// requester packs its chunk digests (n x 32 B), every owner receives them over
+// xGMI with hipMemcpyPeerAsync on its own probe stream, probes the rows it
+// owns, and its hit array (n x 24 B) goes back the same way; the requester
+// merges the W arrays by owner.  Copies, not peer loads/stores from kernels:
+// the DMA engines keep coarse-grained HBM coherent across the GPUs, and the
+// payload is tiny (16K chunks of a 16 GiB layer = 512 KiB out, 384 KiB back
+// per owner), so the exchange is latency-bound, not link-bound.
+#include <stdio.h>
+#include <string.h>
+#include <sys/stat.h>
+
+#include <algorithm>
+
+#include "engine_internal.hpp"
+
+using namespace ngpu;
+
+struct ngpu_node {
+  std::vector<ngpu_engine *> eng;  // one per listed device (a reference each)
+  std::vector<int> dev;
+  std::atomic<uint64_t> rr{0};     // round robin over the engines for Packs
+};
+
+namespace ngpu {
+
+static uint32_t owner_of(const uint8_t *d, uint32_t W) {
+  return (uint32_t)((((uint64_t)d[0] << 8 | d[1]) * W) >> 16);
+}
+
+static void free_io(ngpu_dict::PartIO &io, int device) {
+  DeviceGuard g(device);
+  if (io.stream) (void)hipStreamSynchronize(io.stream);
+  if (io.q) (void)hipFree(io.q);
+  if (io.h) (void)hipFree(io.h);
+  io.q = nullptr;
+  io.h = nullptr;
+  io.cap = 0;
+}
+
+int node_dict_hits(ngpu_engine *e, ngpu_dict *d, const uint8_t *digests, uint64_t stride,
+                   uint64_t n, hipStream_t s, const ngpu_dict_hit **hits, ngpu_dict **replica) {
+  *hits = nullptr;
+  *replica = nullptr;
+  if (d->replicated) {  // no exchange: the copy on this engine's device
+    for (ngpu_dict *p : d->parts)
+      if (p->device == e->device) {
+        *replica = p;
+        return 0;
+      }
+    return fail(e, NGPU_EINVAL, "node chunk dict has no replica on device %d", e->device);
+  }
+  const uint32_t W = (uint32_t)d->parts.size();
+  Workspace &ws = e->ws;
+  if (n > ws.cap_x || !ws.xq) {
+    if (ws.xq) (void)hipFree(ws.xq), ws.xq = nullptr;
+    if (ws.xhits) (void)hipFree(ws.xhits), ws.xhits = nullptr;
+    const uint64_t c = next_pow2(n < 1024 ? 1024 : n);
+    HIP_TRY(e, hipMalloc((void **)&ws.xq, c * 32));
+    HIP_TRY(e, hipMalloc((void **)&ws.xhits, c * sizeof(ngpu_dict_hit)));
+    ws.cap_x = c;
+  }
+  if ((uint64_t)W * n > ws.cap_xparts || !ws.xparts) {
+    if (ws.xparts) (void)hipFree(ws.xparts), ws.xparts = nullptr;
+    const uint64_t c = (uint64_t)W * ws.cap_x;
+    HIP_TRY(e, hipMalloc((void **)&ws.xparts, c * sizeof(ngpu_dict_hit)));
+    ws.cap_xparts = c;
+  }
+  *hits = ws.xhits;
+  if (n == 0) return 0;
+  launch_pack_digests(digests, stride, n, ws.xq, s);
+  hipEvent_t ready = nullptr;
+  HIP_TRY(e, hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  HIP_TRY(e, hipEventRecord(ready, s));
+  std::vector<hipEvent_t> done(W, nullptr);
+  int rc = 0;
+  {
+    std::lock_guard<std::mutex> g(d->io_mu);  // the parts' buffers are shared by requesters
+    for (uint32_t o = 0; o < W && !rc; ++o) {
+      ngpu_dict *p = d->parts[o];
+      ngpu_dict::PartIO &io = d->io[o];
+      DeviceGuard dg(p->device);
+      if (n > io.cap) {
+        free_io(io, p->device);
+        const uint64_t c = ws.cap_x;
+        if (hipMalloc((void **)&io.q, c * 32) != hipSuccess ||
+            hipMalloc((void **)&io.h, c * sizeof(ngpu_dict_hit)) != hipSuccess) {
+          free_io(io, p->device);
+          rc = fail(e, NGPU_ENOMEM, "node dict: exchange buffers on device %d", p->device);
+          break;
+        }
+        io.cap = c;
+      }
+      const bool ok =
+          hipStreamWaitEvent(io.stream, ready, 0) == hipSuccess &&
+          hipMemcpyPeerAsync(io.q, p->device, ws.xq, e->device, n * 32, io.stream) == hipSuccess;
+      if (ok) launch_dict_probe_owned(io.q, n, o, W, p->dev, io.h, io.stream);
+      if (!ok || hipGetLastError() != hipSuccess ||
+          hipMemcpyPeerAsync(ws.xparts + (uint64_t)o * n, e->device, io.h, p->device,
+                             n * sizeof(ngpu_dict_hit), io.stream) != hipSuccess ||
+          hipEventCreateWithFlags(&done[o], hipEventDisableTiming) != hipSuccess ||
+          hipEventRecord(done[o], io.stream) != hipSuccess)
+        rc = fail(e, NGPU_EHIP, "node dict: exchange with device %d failed", p->device);
+    }
+  }
+  for (uint32_t o = 0; o < W; ++o) {
+    if (!done[o]) continue;
+    if (!rc && hipStreamWaitEvent(s, done[o], 0) != hipSuccess)
+      rc = fail(e, NGPU_EHIP, "node dict: cross-device wait failed");
+    DeviceGuard dg(d->parts[o]->device);
+    (void)hipEventDestroy(done[o]);
+  }
+  (void)hipEventDestroy(ready);
+  if (rc) return rc;
+  launch_hits_merge(ws.xq, n, W, ws.xparts, ws.xhits, s);
+  HIP_TRY(e, hipGetLastError());
+  return 0;
+}
+
+namespace {
+
+// A node dict over records in host memory (each engine's mu taken in turn).
+int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint8_t *blobs,
+                    uint32_t n_blobs, uint32_t mode, ngpu_dict **out) {
+  ngpu_engine *e0 = node->eng[0];
+  if (mode != NGPU_NODE_DICT_PARTITION && mode != NGPU_NODE_DICT_REPLICATE)
+    return fail(e0, NGPU_EINVAL, "bad node dict mode %u", mode);
+  if (m >= 0xFFFFFFFFull) return fail(e0, NGPU_EINVAL, "chunk dict too large");
+  uint32_t nb = 0;
+  for (uint64_t i = 0; i < m; ++i) {
+    const RafsV6ChunkInfo *r = reinterpret_cast<const RafsV6ChunkInfo *>(recs + 80 * i);
+    nb = std::max(nb, r->blob_index + 1);
+  }
+  if (n_blobs) {
+    if (nb > n_blobs) return fail(e0, NGPU_EFORMAT, "chunk dict record points at blob %u of %u",
+                                  nb - 1, n_blobs);
+    nb = n_blobs;
+  }
+  ngpu_dict *d = new ngpu_dict();
+  d->device = node->dev[0];
+  d->digester = e0->cfg.digester;
+  d->chunk_size = e0->cfg.chunk_size;
+  d->replicated = mode == NGPU_NODE_DICT_REPLICATE;
+  d->dev.m = m;
+  d->dev.n_blobs = nb;
+  d->place.resize(m);
+  for (uint64_t i = 0; i < m; ++i) {
+    const RafsV6ChunkInfo *r = reinterpret_cast<const RafsV6ChunkInfo *>(recs + 80 * i);
+    d->place[i] = DictPlace{r->compressed_offset, r->compressed_size, r->flags};
+  }
+  if (blobs && n_blobs) d->blob_table.assign(blobs, blobs + 256ull * n_blobs);
+  const uint32_t W = (uint32_t)node->eng.size();
+  // partition: rows per owner in global table order, with their global ids
+  std::vector<std::vector<uint8_t>> part_recs(W);
+  std::vector<std::vector<uint32_t>> gid(W);
+  if (!d->replicated) {
+    for (uint64_t i = 0; i < m; ++i) {
+      const uint32_t o = owner_of(recs + 80 * i, W);
+      part_recs[o].insert(part_recs[o].end(), recs + 80 * i, recs + 80 * (i + 1));
+      gid[o].push_back((uint32_t)i);
+    }
+  }
+  int rc = 0;
+  d->io.resize(W);
+  for (uint32_t o = 0; o < W && !rc; ++o) {
+    ngpu_engine *e = node->eng[o];
+    std::lock_guard<std::mutex> g(e->mu);
+    DeviceGuard dg(e->device);
+    ngpu_dict *p = nullptr;
+    const uint8_t *pr = d->replicated ? recs : part_recs[o].data();
+    const uint64_t pm = d->replicated ? m : gid[o].size();
+    if ((rc = dict_from_records(e, pr, pm, blobs, nb, &p))) break;
+    p->dev.n_blobs = nb;
+    p->place.clear();  // the global table (d->place) answers the writer
+    d->parts.push_back(p);
+    if (!d->replicated && pm) {
+      uint32_t *g32 = nullptr;
+      if (hipMalloc((void **)&g32, pm * 4) != hipSuccess) {
+        rc = fail(e, NGPU_ENOMEM, "node dict: gid allocation failed");
+        break;
+      }
+      p->allocs.push_back(g32);
+      if (hipMemcpy(g32, gid[o].data(), pm * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        rc = fail(e, NGPU_EHIP, "node dict: gid upload failed");
+        break;
+      }
+      p->dev.gid = g32;
+    }
+    if (hipStreamCreateWithFlags(&d->io[o].stream, hipStreamNonBlocking) != hipSuccess)
+      rc = fail(e, NGPU_EHIP, "node dict: probe stream");
+  }
+  if (rc) {
+    dict_unref(d);
+    return rc;
+  }
+  *out = d;
+  return 0;
+}
+
+}  // namespace
+
+// Called by dict_unref for a node dict.
+void node_dict_free(ngpu_dict *d) {
+  for (size_t o = 0; o < d->io.size(); ++o) {
+    const int dev = o < d->parts.size() ? d->parts[o]->device : d->device;
+    free_io(d->io[o], dev);
+    if (d->io[o].stream) {
+      DeviceGuard g(dev);
+      (void)hipStreamDestroy(d->io[o].stream);
+    }
+  }
+  for (ngpu_dict *p : d->parts) dict_unref(p);
+  d->parts.clear();
+}
+
+}  // namespace ngpu
+
+extern "C" {
+
+int ngpu_node_create(const int32_t *devices, uint32_t n, const ngpu_config *cfg, ngpu_node **out) {
+  if (!devices || !n || n > 64 || !out) return NGPU_EINVAL;
+  *out = nullptr;
+  ngpu_node *node = new ngpu_node();
+  for (uint32_t i = 0; i < n; ++i) {
+    ngpu_config c{};
+    if (cfg) c = *cfg;
+    c.device = devices[i];
+    ngpu_engine *e = nullptr;
+    const int rc = ngpu_create(&c, &e);
+    if (rc) {
+      ngpu_node_destroy(node);
+      return rc;
+    }
+    node->eng.push_back(e);
+    node->dev.push_back(devices[i]);
+  }
+  // xGMI peer access between every pair of distinct devices (the exchange
+  // copies go device to device)
+  for (uint32_t a = 0; a < n; ++a)
+    for (uint32_t b = 0; b < n; ++b) {
+      if (node->dev[a] == node->dev[b]) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, node->dev[a], node->dev[b]) != hipSuccess || !can) continue;
+      DeviceGuard g(node->dev[a]);
+      const hipError_t st = hipDeviceEnablePeerAccess(node->dev[b], 0);
+      if (st != hipSuccess && st != hipErrorPeerAccessAlreadyEnabled) {
+        ngpu_node_destroy(node);
+        return NGPU_EHIP;
+      }
+      (void)hipGetLastError();
+    }
+  *out = node;
+  return 0;
+}
+
+void ngpu_node_destroy(ngpu_node *node) {
+  if (!node) return;
+  for (ngpu_engine *e : node->eng) ngpu_destroy(e);
+  delete node;
+}
+
+uint32_t ngpu_node_size(const ngpu_node *node) { return node ? (uint32_t)node->eng.size() : 0; }
+
+ngpu_engine *ngpu_node_engine(ngpu_node *node, uint32_t i) {
+  return node && i < node->eng.size() ? node->eng[i] : nullptr;
+}
+
+uint32_t ngpu_node_owner(const ngpu_node *node, const uint8_t *digest) {
+  return node && digest ? owner_of(digest, (uint32_t)node->eng.size()) : 0;
+}
+
+int ngpu_node_dict_create(ngpu_node *node, const void *records, uint64_t n,
+                          const void *blob_table, uint32_t n_blobs, uint32_t mode,
+                          ngpu_dict **out) {
+  if (!node || !out || (n && !records) || (n_blobs && !blob_table)) return NGPU_EINVAL;
+  *out = nullptr;
+  return guarded([&] {
+    return node_dict_build(node, (const uint8_t *)records, n, (const uint8_t *)blob_table, n_blobs,
+                           mode, out);
+  });
+}
+
+int ngpu_node_dict_open(ngpu_node *node, const char *path, uint32_t mode, ngpu_dict **out) {
+  if (!node || !path || !out) return NGPU_EINVAL;
+  *out = nullptr;
+  return guarded([&] {
+    struct stat st;
+    ngpu_engine *e0 = node->eng[0];
+    if (stat(path, &st) != 0) return fail(e0, NGPU_EIO, "stat chunk dict %s", path);
+    std::vector<uint8_t> recs, blobs;
+    int rc;
+    {
+      std::lock_guard<std::mutex> g(e0->mu);
+      rc = read_dict_bootstrap(e0, path, (uint64_t)st.st_size, &recs, &blobs);
+    }
+    if (rc) return rc;
+    return node_dict_build(node, recs.data(), recs.size() / 80, blobs.data(),
+                           (uint32_t)(blobs.size() / 256), mode, out);
+  });
+}
+
+int ngpu_node_pack_open(ngpu_node *node, ngpu_dict *dict, uint32_t flags, ngpu_pack **out) {
+  if (!node || !out) return NGPU_EINVAL;
+  const uint64_t i = node->rr.fetch_add(1, std::memory_order_relaxed) % node->eng.size();
+  return ngpu_pack_open_dict(node->eng[i], dict, flags, out);
+}
+
+int ngpu_node_process_device(ngpu_node *node, uint32_t i, ngpu_dict *dict, const void *d_data,
+                             uint64_t len, const ngpu_chunk *d_chunks, uint64_t n,
+                             ngpu_result *d_out, const uint64_t *d_layer_first,
+                             uint64_t n_layers, ngpu_layer_stats *d_stats, void *stream) {
+  if (!node || i >= node->eng.size()) return NGPU_EINVAL;
+  return ngpu_process_dict_device(node->eng[i], dict, d_data, len, d_chunks, n, d_out,
+                                  d_layer_first, n_layers, d_stats, stream, nullptr);
+}
+
+}  // extern "C"

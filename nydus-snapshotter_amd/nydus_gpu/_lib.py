@@ -59,7 +59,9 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_write_fd", "ngpu_dict_open", "ngpu_dict_create", "ngpu_dict_create_device",
            "ngpu_dict_retain", "ngpu_dict_release", "ngpu_dict_entries", "ngpu_set_dict",
            "ngpu_dict_probe", "ngpu_process_dict", "ngpu_process_dict_device",
-           "ngpu_pack_open_dict", "ngpu_pack_set_cancel"]
+           "ngpu_pack_open_dict", "ngpu_pack_set_cancel", "ngpu_node_create", "ngpu_node_destroy",
+           "ngpu_node_size", "ngpu_node_engine", "ngpu_node_dict_open", "ngpu_node_dict_create",
+           "ngpu_node_owner", "ngpu_node_pack_open", "ngpu_node_process_device"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
@@ -208,6 +210,19 @@ def lib():
                                            ctypes.POINTER(NgpuLayerStats)]
     L.ngpu_pack_open_dict.argtypes = [vp, vp, u32, ctypes.POINTER(vp)]
     L.ngpu_pack_set_cancel.argtypes = [vp, vp]
+    L.ngpu_node_create.argtypes = [vp, u32, ctypes.POINTER(NgpuConfig), ctypes.POINTER(vp)]
+    L.ngpu_node_destroy.argtypes = [vp]
+    L.ngpu_node_destroy.restype = None
+    L.ngpu_node_size.argtypes = [vp]
+    L.ngpu_node_size.restype = u32
+    L.ngpu_node_engine.argtypes = [vp, u32]
+    L.ngpu_node_engine.restype = vp
+    L.ngpu_node_dict_open.argtypes = [vp, ctypes.c_char_p, u32, ctypes.POINTER(vp)]
+    L.ngpu_node_dict_create.argtypes = [vp, vp, u64, vp, u32, u32, ctypes.POINTER(vp)]
+    L.ngpu_node_owner.argtypes = [vp, vp]
+    L.ngpu_node_owner.restype = u32
+    L.ngpu_node_pack_open.argtypes = [vp, vp, u32, ctypes.POINTER(vp)]
+    L.ngpu_node_process_device.argtypes = [vp, u32, vp, vp, u64, vp, u64, vp, vp, u64, vp, vp]
     _lib = L
     return L
 
@@ -429,9 +444,18 @@ class Engine:
     """One GPU engine (ngpu_engine*).  Mirrors the PackOption fields the
     digest/dedup stage consumes (pkg/converter/types.go:58-90)."""
 
+    @classmethod
+    def _borrow(cls, handle, owner, digester, chunk_size, fs_version):
+        """A view of an engine owned by something else (a Node): close() is a no-op."""
+        e = cls.__new__(cls)
+        e._h, e._owner = handle, owner
+        e.digester, e.chunk_size, e.fs_version = digester, chunk_size, fs_version
+        return e
+
     def __init__(self, device: int = 0, digester: str = "blake3", chunk_size: int = 0x100000,
                  fs_version: int = 6, leaves_per_lane: int = 0, staging_bytes: int = 0,
                  timing: bool = False, flags: int = 0, aligned_chunk: bool = False):
+        self._owner = None
         L = lib()
         if digester not in DIGESTERS:
             raise ValueError(f"unsupported digester {digester!r}")
@@ -450,9 +474,9 @@ class Engine:
         self.fs_version = fs_version
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and getattr(self, "_owner", None) is None:
             lib().ngpu_destroy(self._h)
-            self._h = None
+        self._h = None
 
     __del__ = close
 
@@ -734,3 +758,93 @@ class PackWriter:
             L.ngpu_free_host(pc)
             L.ngpu_free_host(pr)
         return ch, rs, st.as_dict(), (info.as_dict() if dest is not None else None)
+
+
+NODE_DICT_PARTITION, NODE_DICT_REPLICATE = 0, 1
+
+
+class Node:
+    """One process driving several GPUs (ngpu_node*): one
+    engine per listed device (a device may repeat, to rehearse a multi-GPU
+    node on one GPU); node chunk dicts are partitioned by digest prefix (the
+    probe exchange runs over xGMI) or replicated."""
+
+    def __init__(self, devices, digester: str = "blake3", chunk_size: int = 0x100000,
+                 fs_version: int = 6, staging_bytes: int = 0, timing: bool = False, flags: int = 0):
+        L = lib()
+        cfg = NgpuConfig(device=0, digester=DIGESTERS[digester], chunk_size=chunk_size,
+                         fs_version=fs_version, staging_bytes=staging_bytes,
+                         flags=flags | (FLAG_TIMING if timing else 0))
+        devs = (ctypes.c_int32 * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        rc = L.ngpu_node_create(devs, len(devices), ctypes.byref(cfg), ctypes.byref(h))
+        if rc:
+            raise NgpuError(rc, "ngpu_node_create")
+        self._h = h
+        self.devices = list(devices)
+        self.digester, self.chunk_size = digester, chunk_size
+        self.engines = [Engine._borrow(ctypes.c_void_p(L.ngpu_node_engine(h, i)), self, digester,
+                                       chunk_size, fs_version) for i in range(len(devices))]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            for e in self.engines:
+                e._h = None
+            lib().ngpu_node_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __len__(self):
+        return lib().ngpu_node_size(self._h)
+
+    def owner(self, digest: bytes) -> int:
+        b = np.frombuffer(bytes(digest), np.uint8)
+        return lib().ngpu_node_owner(self._h, _ptr(b))
+
+    def _err(self, rc, what):
+        if rc:
+            msg = lib().ngpu_last_error(self.engines[0]._h)
+            raise NgpuError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def dict_open(self, path: str, mode: int = NODE_DICT_PARTITION) -> ChunkDict:
+        h = ctypes.c_void_p()
+        self._err(lib().ngpu_node_dict_open(self._h, path.encode(), mode, ctypes.byref(h)),
+                  "node_dict_open")
+        return ChunkDict(h)
+
+    def dict_create(self, records, blobs=None, mode: int = NODE_DICT_PARTITION) -> ChunkDict:
+        r = np.ascontiguousarray(records).view(np.uint8).reshape(-1)
+        b = None if blobs is None or not len(blobs) else np.ascontiguousarray(blobs).view(np.uint8).reshape(-1)
+        h = ctypes.c_void_p()
+        self._err(lib().ngpu_node_dict_create(self._h, _ptr(r), r.size // 80, _ptr(b),
+                                              0 if b is None else b.size // 256, mode, ctypes.byref(h)),
+                  "node_dict_create")
+        return ChunkDict(h)
+
+    def pack(self, dict=None, retain: bool = False) -> "PackWriter":
+        """A streaming Pack on the next engine (round robin)."""
+        h = ctypes.c_void_p()
+        self._err(lib().ngpu_node_pack_open(self._h, _dict_arg(dict), PACK_RETAIN if retain else 0,
+                                            ctypes.byref(h)), "node_pack_open")
+        w = PackWriter.__new__(PackWriter)
+        # the pack's engine, for error messages and finish() options
+        w._eng = self.engines[0]
+        w._p = h
+        w._cancel = ctypes.c_int32(0)
+        lib().ngpu_pack_set_cancel(w._p, ctypes.byref(w._cancel))
+        return w
+
+    def process_device(self, i: int, dict, d_data: int, length: int, d_chunks: int, n: int,
+                       d_out: int, d_layer_first: int = 0, n_layers: int = 1, d_stats: int = 0,
+                       stream: int = 0):
+        vp = Engine._vp
+        self.engines[i]._check(lib().ngpu_node_process_device(
+            self._h, i, _dict_arg(dict), vp(d_data), length, vp(d_chunks), n, vp(d_out),
+            vp(d_layer_first), n_layers, vp(d_stats), vp(stream)), "node_process_device")

@@ -1,0 +1,142 @@
+"""GPU: the multi-GPU node behind the C ABI (ngpu_node_*).
+
+On this one-GPU box a node lists device 0 several times: W engines, W dict
+parts and the full exchange (digest packing, hipMemcpyPeerAsync to every
+owner, owned-row probes, hits back, merge by owner) run exactly as on an
+8-GPU node, only the copies stay inside one HBM.  Every decision must equal
+the oracle's with the WHOLE dict (global entry ids, first-entry-wins)."""
+import io
+
+import numpy as np
+import pytest
+
+import nydus_gpu
+from nydus_gpu import rafs
+
+pytestmark = pytest.mark.gpu
+
+
+def _layer(rng, total, chunk_size, dup_frac=0.3):
+    data = bytearray(rng.integers(0, 256, total, dtype=np.uint8).tobytes())
+    chunks, off = [], 0
+    while True:
+        ln = int(rng.integers(1, chunk_size + 1)) if rng.random() < 0.5 else chunk_size
+        if off + ln > total:
+            break
+        chunks.append([off, ln, len(chunks), 0])
+        off = (off + ln + 511) // 512 * 512
+    n = len(chunks)
+    for _ in range(int(n * dup_frac)):
+        a, b = sorted(rng.integers(0, n, 2))
+        la = chunks[a][1]
+        if a != b and la <= chunks[b][1]:
+            chunks[b][1] = la
+            data[chunks[b][0]:chunks[b][0] + la] = data[chunks[a][0]:chunks[a][0] + la]
+    return bytes(data), np.array([tuple(c) for c in chunks], dtype=nydus_gpu.CHUNK_DTYPE)
+
+
+def _dict_records(rng, dig, sizes, extra=5000, blobs=7):
+    """Dict records: half the layer's digests, random filler, later duplicate
+    keys (first wins), usize 0 wildcards, size mismatches, several blobs."""
+    n = len(dig)
+    pick = rng.choice(n, n // 2, replace=False)
+    m = len(pick) + extra + 50
+    r = np.zeros(m, rafs.CHUNK_INFO_DTYPE)
+    r["block_id"] = np.concatenate([dig[pick], rng.integers(0, 256, (extra, 32), dtype=np.uint8),
+                                    dig[pick[:50]]])
+    r["uncompressed_size"] = np.concatenate([sizes[pick], rng.integers(1, 1 << 16, extra),
+                                             sizes[pick[:50]]])
+    r["uncompressed_size"][: n // 20] = 0
+    r["uncompressed_size"][n // 20: n // 10] += 1
+    r["blob_index"] = rng.integers(0, blobs, m)
+    r["index"] = rng.integers(0, 1 << 20, m)
+    r["uncompressed_offset"] = rng.integers(0, 1 << 40, m) // 4096 * 4096
+    r["compressed_offset"] = rng.integers(0, 1 << 40, m)
+    r["compressed_size"] = rng.integers(1, 1 << 16, m)
+    r["flags"] = rng.integers(0, 2, m)
+    return r
+
+
+def _expect(oracle, dig, ch, recs):
+    dec, own = oracle.dedup(dig, ch["length"], recs["block_id"], recs["uncompressed_size"],
+                            recs["blob_index"], recs["index"], dict_uoff=recs["uncompressed_offset"])
+    return dec
+
+
+def _to_dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()
+
+
+@pytest.mark.parametrize("W,mode", [(2, nydus_gpu.NODE_DICT_PARTITION), (4, nydus_gpu.NODE_DICT_PARTITION),
+                                    (2, nydus_gpu.NODE_DICT_REPLICATE)])
+def test_node_dict_device_layers_vs_oracle(oracle, W, mode):
+    """Device-resident layers on every engine of a W-device node against a
+    partitioned / replicated node dict == the oracle with the whole dict."""
+    import torch
+    from nydus_gpu.dist import owner_of
+    rng = np.random.default_rng(40 + W + mode)
+    cs = 0x10000
+    layers = [_layer(rng, 12 << 20, cs) for _ in range(W)]
+    digs = [oracle.digest_chunks(d, c.view(oracle.CHUNK_DTYPE), "blake3") for d, c in layers]
+    recs = _dict_records(rng, np.concatenate(digs), np.concatenate([c["length"] for _, c in layers]))
+    blobs = rafs.make_blob_table([f"{i:064x}" for i in range(7)], cs)
+    node = nydus_gpu.Node([0] * W, chunk_size=cs)
+    try:
+        # the partition rule is dist.py's
+        o = owner_of(__import__("torch").from_numpy(recs["block_id"][:200].copy()), W).tolist()
+        assert [node.owner(bytes(b)) for b in recs["block_id"][:200]] == o
+        d = node.dict_create(recs, blobs, mode=mode)
+        assert d.entries == len(recs)
+        for i, (data, ch) in enumerate(layers):
+            n = len(ch)
+            d_data, d_ch = _to_dev(np.frombuffer(data, np.uint8)), _to_dev(ch)
+            out = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+            node.process_device(i, d, d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), n,
+                                out.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+            exp = _expect(oracle, digs[i], ch, recs)
+            assert np.array_equal(got["digest"], digs[i])
+            for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+                assert np.array_equal(got[f], exp[f]), (i, f)
+            assert (exp["kind"] == 2).sum() > 0
+        d.release()
+    finally:
+        node.close()
+
+
+def test_node_packs_round_robin_write_dict_records(oracle, tars, tmp_path):
+    """Streaming Packs spread over a 2-device node against a partitioned dict
+    opened from a RAFS v6 bootstrap: each Pack output stream is byte-equal to
+    the host writer fed with the oracle's decisions (global entry ids, so the
+    DICT records copy the right dict records)."""
+    from test_blob import check_stream, cpu_stream
+    cs = 0x100000
+    eng = nydus_gpu.Engine(chunk_size=cs)
+    try:
+        ch, out, _ = eng.pack_tar(tars["chunk_dict"])
+        tab = nydus_gpu.chunk_table(ch, out).view(rafs.CHUNK_INFO_DTYPE).reshape(-1)
+    finally:
+        eng.close()
+    boot = rafs.write_v6_bootstrap(tab, cs, flags=0x5,
+                                   blobs=rafs.make_blob_table(["ab" * 32], cs, counts=[len(tab)]))
+    path = tmp_path / "dict-bootstrap"
+    path.write_bytes(boot)
+    node = nydus_gpu.Node([0, 0], chunk_size=cs)
+    try:
+        d = node.dict_open(str(path))
+        ws = [node.pack(d, retain=True) for _ in range(4)]
+        d.release()
+        names = ["oci_lower", "oci_upper", "oci_lower", "alpine_like"]
+        for w, name in zip(ws, names):
+            w.write(tars[name])
+        for w, name in zip(ws, names):
+            o = io.BytesIO()
+            ch, res, st, info = w.finish(o, compressor="none")
+            ref = cpu_stream(oracle, tars[name], cs, "none", dict_boot=boot)
+            assert o.getvalue() == ref[0], name
+            check_stream(oracle, o.getvalue(), info, tars[name], ch, res, "none", dict_boot=boot)
+        assert info is not None
+    finally:
+        node.close()

@@ -18,7 +18,7 @@ from conftest import GOLDEN, ROOT
 def test_header_symbols_exported():
     hdr = open(os.path.join(ROOT, "include", "nydus_gpu.h")).read()
     declared = sorted(set(re.findall(
-        r"^(?:int|void|uint64_t|uint32_t|const char)\s*\*?\s*(ngpu_\w+)\s*\(", hdr, re.M)))
+        r"^(?:int|void|uint64_t|uint32_t|const char|ngpu_engine)\s*\*?\s*(ngpu_\w+)\s*\(", hdr, re.M)))
     assert declared == sorted(nydus_gpu.EXPORTS)
     L = nydus_gpu.lib()
     for name in declared:
