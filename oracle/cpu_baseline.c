@@ -12,8 +12,9 @@
  *     falls back to the scalar oracle_blake3 if absent;
  *   - SHA-256: OpenSSL's SHA256() (SHA-NI) via dlopen of libcrypto; falls back
  *     to the scalar oracle_sha256;
- * spread over T pthreads (chunk i -> thread i % T), followed by the
- * single-stream oracle_dedup pass (what nydus-image does in stream order).
+ * spread over T pthreads (each takes the next chunk from a shared counter,
+ * so ragged layers balance), followed by the single-stream oracle_dedup pass
+ * (what nydus-image does in stream order).
  */
 #include <dlfcn.h>
 #include <pthread.h>
@@ -66,12 +67,13 @@ typedef struct {
   uint64_t n;
   int digester, tid, nthreads;
   uint8_t *out;
+  uint64_t *next;  /* shared chunk counter */
 } job_t;
 
 static void *worker(void *arg) {
   job_t *j = (job_t *)arg;
   _Alignas(64) uint8_t state[8192];
-  for (uint64_t i = (uint64_t)j->tid; i < j->n; i += (uint64_t)j->nthreads) {
+  for (uint64_t i; (i = __atomic_fetch_add(j->next, 1, __ATOMIC_RELAXED)) < j->n;) {
     const uint8_t *p = j->data + j->chunks[i].offset;
     size_t l = j->chunks[i].length;
     uint8_t *o = j->out + 32 * i;
@@ -98,8 +100,9 @@ uint64_t oracle_cpu_digest_dedup(const uint8_t *data, const oracle_chunk *chunks
   if (threads < 1) threads = 1;
   pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
   job_t *jobs = (job_t *)malloc(sizeof(job_t) * (size_t)threads);
+  uint64_t next = 0;
   for (int t = 0; t < threads; t++) {
-    jobs[t] = (job_t){data, chunks, n, digester, t, threads, digests};
+    jobs[t] = (job_t){data, chunks, n, digester, t, threads, digests, &next};
     pthread_create(&th[t], NULL, worker, &jobs[t]);
   }
   for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
