@@ -996,3 +996,82 @@ def test_scan_tile_boundaries_vs_oracle(engines, oracle, n):
         assert stats[l]["chunks"] == b - a
         assert stats[l]["new_chunks"] == (exp["kind"] == 0).sum()
         assert stats[l]["intra_chunks"] == (exp["kind"] == 1).sum()
+
+
+@pytest.mark.parametrize("fs", [5, 6])
+def test_fixture_replay_through_gpu_dedup(fs):
+    """The reference's real nydus-image bootstraps
+    (pkg/filesystem/testdata/v5-bootstrap-file-size-736032.tar.gz,
+    v6-bootstrap-chunk-pos-438272.tar.gz): their chunk streams (digests +
+    sizes, file by file in inode order) through the GPU dedup stage
+    (ngpu_dedup_device, FsVersion 5 / 6) give nydus-image's own index and
+    uncompressed offset for every one of the 2,624 chunk references."""
+    import torch
+    import rafs_fixtures
+    from test_oracle import V5_FIXTURE, V6_FIXTURE
+    if fs == 5:
+        d = rafs_fixtures.read_v5(rafs_fixtures.boot_from_targz(V5_FIXTURE))
+        fx = np.concatenate([f[4] for f in d["files"]])
+        count, usize, _ = d["ext_blobs"][0]
+    else:
+        files = rafs_fixtures.read_v6_files(rafs_fixtures.boot_from_targz(V6_FIXTURE))
+        fx = np.concatenate([f[3] for f in files])
+        b = rafs.read_v6_from_targz(V6_FIXTURE)["blobs"][0]
+        count, usize = int(b["chunk_count"]), int(b["uncompressed_size"])
+    n = len(fx)
+    res = np.zeros(n, nydus_gpu.RESULT_DTYPE)
+    res["digest"] = fx["block_id"]
+    ch = np.zeros(n, nydus_gpu.CHUNK_DTYPE)
+    ch["length"] = fx["uncompressed_size"]
+    ch["file_offset"] = fx["file_offset"]
+    eng = nydus_gpu.Engine(chunk_size=0x100000, fs_version=fs)
+    try:
+        d_out, d_ch = _to_dev(res), _to_dev(ch)
+        st = eng.dedup_device(d_ch.data_ptr(), n, d_out.data_ptr(), want_stats=True)
+        got = d_out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+    finally:
+        eng.close()
+    assert np.array_equal(got["index"], fx["index"])
+    assert np.array_equal(got["uncompressed_offset"], fx["uncompressed_offset"])
+    assert np.array_equal(got["blob_index"], fx["blob_index"])
+    assert st["new_chunks"] == count == 2515 and st["intra_chunks"] == n - count
+    if fs == 5:
+        assert st["uncompressed_size"] == usize
+    else:  # v6: the blob's uncompressed size is 4K-rounded
+        assert (st["uncompressed_size"] + 4095) // 4096 * 4096 == usize
+
+
+def test_reference_v6_bootstrap_as_chunk_dict(tmp_path):
+    """The reference's v6 fixture as PackOption.ChunkDictPath: the dict loads
+    from a real nydus-image bootstrap (blake3, 1 MiB, its blob table), and the
+    fixture's own chunk stream replayed against it is all DICT, each result
+    carrying the dict record's entry, index and uncompressed offset."""
+    import rafs_fixtures
+    from test_oracle import V6_FIXTURE
+    boot = rafs_fixtures.boot_from_targz(V6_FIXTURE)
+    path = tmp_path / "image.boot"
+    path.write_bytes(boot)
+    table = rafs.read_v6(boot)["chunks"]
+    fx = np.concatenate([f[3] for f in rafs_fixtures.read_v6_files(boot)])
+    n = len(fx)
+    res = np.zeros(n, nydus_gpu.RESULT_DTYPE)
+    res["digest"] = fx["block_id"]
+    ch = np.zeros(n, nydus_gpu.CHUNK_DTYPE)
+    ch["length"] = fx["uncompressed_size"]
+    eng = nydus_gpu.Engine(chunk_size=0x100000)
+    try:
+        d = eng.dict_open(str(path))
+        assert d.entries == len(table) == 2515
+        eng.set_dict(d)
+        d.release()
+        d_out, d_ch = _to_dev(res), _to_dev(ch)
+        st = eng.dedup_device(d_ch.data_ptr(), n, d_out.data_ptr(), want_stats=True)
+        got = d_out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+    finally:
+        eng.close()
+    assert (got["kind"] == nydus_gpu.DICT).all() and st["dict_chunks"] == n
+    pos = {bytes(r["block_id"]): i for i, r in enumerate(table)}
+    assert np.array_equal(got["ref"], [pos[bytes(b)] for b in fx["block_id"]])
+    assert np.array_equal(got["index"], fx["index"])
+    assert np.array_equal(got["uncompressed_offset"], fx["uncompressed_offset"])
+    assert st["own_blob_index"] == 0xFFFFFFFF and st["blobs"] == 1

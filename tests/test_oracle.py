@@ -4,6 +4,8 @@ The fixtures come from implementations independent of oracle/ (ROCm LLVM's
 official BLAKE3 C v1.8.2, OpenSSL SHA-256, Python tarfile, an independent
 Python dedup restatement): tests/golden/make_golden.py.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -114,3 +116,104 @@ def test_tar_malformed(oracle, bad):
     else:
         with pytest.raises(ValueError):
             oracle.tar_chunks(bad, 4096)
+
+
+# ---- pinned on the reference's own nydus-image output ------------------------
+# pkg/filesystem/testdata/v5-bootstrap-file-size-736032.tar.gz is a real
+# nydus-image RAFS v5 bootstrap (2,602 regular files, 2,624 chunk references,
+# 2,515 distinct chunks).  Its per-file chunk arrays pin the tar-rafs chunking
+# rule and, replayed through the oracle's dedup, the
+# dedup semantics (a5): first occurrence gets the next index, a repeat copies
+# the first occurrence's record, v5 offsets are packed (no --aligned-chunk).
+
+V5_FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                          "v5-bootstrap-file-size-736032.tar.gz")
+
+
+def _v5():
+    import rafs_fixtures
+    return rafs_fixtures.read_v5(rafs_fixtures.boot_from_targz(V5_FIXTURE))
+
+
+def test_v5_fixture_chunking_rule():
+    """chunks per file = ceil(size / S); chunk k covers [k*S, min((k+1)*S, size))."""
+    d = _v5()
+    S = d["block_size"]
+    assert S == 0x100000 and d["flags"] & 0x4  # 1 MiB chunks, HASH_BLAKE3
+    assert len(d["files"]) == 2602
+    for name, ino, size, nlink, ch in d["files"]:
+        assert len(ch) == (size + S - 1) // S, name
+        k = np.arange(len(ch), dtype=np.uint64)
+        assert np.array_equal(ch["file_offset"], k * S), name
+        assert np.array_equal(ch["uncompressed_size"].astype(np.uint64),
+                              np.minimum(S, size - k * S)), name
+
+
+def test_v5_fixture_records_pin_the_dedup_replay(oracle):
+    """Replay the fixture's chunk stream (digest + size, file by file in
+    inode-table order) through the oracle's dedup: every chunk's index,
+    uncompressed offset (align 1: v5 without AlignedChunk) and kind agree with
+    what nydus-image wrote, and the blob's chunk count / sizes too."""
+    d = _v5()
+    ch = np.concatenate([f[4] for f in d["files"]])
+    dig = np.ascontiguousarray(ch["block_id"])
+    dec, own = oracle.dedup(dig, ch["uncompressed_size"], align=1)
+    assert own == 0
+    assert np.array_equal(dec["index"], ch["index"])
+    assert np.array_equal(dec["uncompressed_offset"], ch["uncompressed_offset"])
+    assert np.array_equal(dec["blob_index"], ch["blob_index"])
+    new = dec["kind"] == 0
+    count, usize, csize = d["ext_blobs"][0]
+    assert new.sum() == count == 2515 and (dec["kind"] == 1).sum() == len(ch) - 2515
+    # a repeated digest carries the first occurrence's whole record (chunk.copy_from)
+    ref = dec["ref"].astype(np.int64)
+    for f in ("flags", "compressed_size", "compressed_offset", "uncompressed_offset", "index"):
+        assert np.array_equal(ch[f], ch[f][ref]), f
+    # in index order: uncompressed offsets packed by size, compressed by csize;
+    # a chunk stored raw (flag bit 0 clear) has csize == usize
+    r = ch[new][np.argsort(ch["index"][new])]
+    assert np.array_equal(r["uncompressed_offset"][1:], np.cumsum(r["uncompressed_size"].astype(np.uint64))[:-1])
+    assert np.array_equal(r["compressed_offset"][1:], np.cumsum(r["compressed_size"].astype(np.uint64))[:-1])
+    raw = (r["flags"] & 1) == 0
+    assert raw.sum() == 178 and np.array_equal(r["compressed_size"][raw], r["uncompressed_size"][raw])
+    assert int(r["uncompressed_offset"][-1]) + int(r["uncompressed_size"][-1]) == usize
+    assert int(r["compressed_offset"][-1]) + int(r["compressed_size"][-1]) == csize
+
+
+V6_FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                          "v6-bootstrap-chunk-pos-438272.tar.gz")
+
+
+def _v6():
+    import rafs_fixtures
+    return rafs_fixtures.read_v6_files(rafs_fixtures.boot_from_targz(V6_FIXTURE))
+
+
+def test_v6_fixture_chunking_rule():
+    """RAFS v6 fixture: each regular file's chunk indexes resolve to records
+    whose sizes follow ceil(size / S) chunks of S (the last one short), and
+    whose file_offset is k * S."""
+    files = _v6()
+    S = 0x100000
+    assert len(files) == 2602
+    for path, ino, size, ch in files:
+        k = np.arange(len(ch), dtype=np.uint64)
+        assert len(ch) == (size + S - 1) // S, path
+        assert np.array_equal(ch["uncompressed_size"].astype(np.uint64), np.minimum(S, size - k * S)), path
+        assert np.array_equal(ch["file_offset"], k * S), path
+
+
+def test_v6_fixture_records_pin_the_dedup_replay(oracle):
+    """The v6 fixture's chunk stream replayed through the oracle's dedup with
+    v6's 4 KiB alignment: nydus-image's index and uncompressed offset for all
+    2,624 chunk references; repeats share the first occurrence's record."""
+    files = _v6()
+    ch = np.concatenate([f[3] for f in files])
+    dec, own = oracle.dedup(np.ascontiguousarray(ch["block_id"]), ch["uncompressed_size"], align=4096)
+    assert own == 0
+    assert np.array_equal(dec["index"], ch["index"])
+    assert np.array_equal(dec["uncompressed_offset"], ch["uncompressed_offset"])
+    assert (dec["kind"] == 0).sum() == 2515
+    ref = dec["ref"].astype(np.int64)
+    for f in ("flags", "compressed_size", "compressed_offset", "index"):
+        assert np.array_equal(ch[f], ch[f][ref]), f
