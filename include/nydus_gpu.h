@@ -411,6 +411,9 @@ int ngpu_chunk_table(const ngpu_chunk *chunks, const ngpu_result *results,
  * shrink it), image.boot (RAFS v6 bootstrap: blob table + chunk table: one
  * record per distinct chunk the layer references -- its NEW chunks and the
  * chunk-dict chunks it reuses, copied with their dict blob placement),
+ * blob.meta + blob.meta.header (convert_unix.go:47-48: the chunk-info array
+ * of the layer's blob and its 4 KiB header) and blob.digest (the chunks'
+ * digests, index order) when the blob has chunks, and
  * rafs.blob.toc (128-B TOCEntry records, types.go:147-163).  Compression and
  * SHA-256 run on the host (north star: compression stays on the host path). */
 
@@ -457,6 +460,7 @@ typedef struct {
   uint8_t blob_digest[32];    /* sha256 of image.blob (the own blob's id) */
   uint8_t toc_digest[32];     /* sha256 of the TOC (calcBlobTOCDigest :541-555) */
   uint64_t dict_records;      /* chunk records copied from the chunk dict */
+  uint64_t meta_entries;      /* entries of the blob.meta chunk-info array (0: none) */
 } ngpu_blob_info;
 
 /* Thread-local message of the last failing engine-less call below. */

@@ -116,11 +116,12 @@ class NgpuBlobInfo(ctypes.Structure):
                 ("bootstrap_bytes", ctypes.c_uint64), ("blob_chunks", ctypes.c_uint64),
                 ("compressed_chunks", ctypes.c_uint64), ("stream_digest", ctypes.c_uint8 * 32),
                 ("blob_digest", ctypes.c_uint8 * 32), ("toc_digest", ctypes.c_uint8 * 32),
-                ("dict_records", ctypes.c_uint64)]
+                ("dict_records", ctypes.c_uint64), ("meta_entries", ctypes.c_uint64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_[:5]}
         d["dict_records"] = self.dict_records
+        d["meta_entries"] = self.meta_entries
         for k in ("stream_digest", "blob_digest", "toc_digest"):
             d[k] = bytes(getattr(self, k)).hex()
         return d

@@ -133,8 +133,14 @@ int main(int argc, char **argv) {
   REQUIRE_NOERR(UnpackEntry(ra, EntryBootstrap, boot, &e));
   Compressor c = 0;
   REQUIRE(e.GetName() == EntryBootstrap && !e.GetCompressor(&c) && c == CompressorNone, "toc");
+  BufferWriter meta;  // the blob's chunk-info array (convert_unix.go:47)
+  TOCEntry me;
+  REQUIRE_NOERR(UnpackEntry(ra, EntryBlobMeta, meta, &me));
+  REQUIRE(me.GetName() == EntryBlobMeta && meta.data.size() % 24 == 0 &&
+              meta.data.size() / 24 == upper.stats.NewChunks,
+          "blob.meta: one 24-B chunk-info entry per own chunk");
   BufferWriter none;
-  Error nf = UnpackEntry(ra, EntryBlobMeta, none, nullptr);
+  Error nf = UnpackEntry(ra, "no.such.entry", none, nullptr);
   REQUIRE(IsNotFound(nf), "ErrNotFound for a missing entry (got %d)", nf.code);
 
   // option errors come back as errors, like the Go API

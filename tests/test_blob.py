@@ -149,7 +149,49 @@ def check_stream(oracle, stream, info, tar, ch, res, compressor, digester="blake
         assert body == src
         assert oracle.digest(body, digester) == bytes(r["block_id"])
     assert int((recs["flags"] & 1).sum()) == info["compressed_chunks"]
+    check_blob_meta(stream, info, recs)
     return b
+
+
+BLOB_CCT_MAGIC = 0xB10BB10B
+
+
+def check_blob_meta(stream, info, recs):
+    """blob.meta / blob.meta.header / blob.digest (convert_unix.go:47-48;
+    layout restated from [nydus v2.3.0] Blob::dump_meta_data, VERIFY): the
+    reference reader finds each through the TOC; the header describes the
+    chunk-info array, whose BlobChunkInfoV2 entries (index order) decode to
+    the own blob's chunk records, and blob.digest holds their digests."""
+    import struct
+    r = recs[np.argsort(recs["index"], kind="stable")]
+    if len(r) == 0 or (r["uncompressed_offset"] % 4096).any():
+        assert info["meta_entries"] == 0
+        for name in ("blob.meta", "blob.meta.header", "blob.digest"):
+            with pytest.raises(blob_ref.NotFound):
+                blob_ref.unpack_entry(stream, name)
+        return
+    assert info["meta_entries"] == len(r)
+    meta, e_meta = blob_ref.unpack_entry(stream, "blob.meta")
+    hdr, e_hdr = blob_ref.unpack_entry(stream, "blob.meta.header")
+    dig, e_dig = blob_ref.unpack_entry(stream, "blob.digest")
+    assert meta == nydus_gpu.unpack_entry(stream, "blob.meta")[0]
+    assert len(hdr) == 4096 and e_hdr["compressed_offset"] == e_meta["compressed_offset"] + e_meta["compressed_size"]
+    magic, feat, ci_algo, n, ci_off, ci_csize, ci_usize = struct.unpack_from("<IIIIQQQ", hdr, 0)
+    assert magic == BLOB_CCT_MAGIC == struct.unpack_from("<I", hdr, 4088)[0]
+    assert feat & 0x4 and feat & 0x20  # CHUNK_INFO_V2, INLINED_CHUNK_DIGEST
+    assert n == len(r) and ci_usize == len(meta) == 24 * len(r)
+    assert ci_off == e_meta["compressed_offset"] and ci_csize == e_meta["compressed_size"]
+    assert ci_algo == (3 if e_meta["flags"] & 0xF == 0x2 else 0)
+    ci = np.frombuffer(meta, "<u8").reshape(-1, 3)
+    u, c = ci[:, 0], ci[:, 1]
+    assert np.array_equal((u & 0xFFFFFFFF) << 12, r["uncompressed_offset"])
+    assert np.array_equal(((u >> 32) & 0xFFFFFF) + 1, r["uncompressed_size"])
+    assert np.array_equal((u >> 56) & 1, r["flags"] & 1)
+    assert np.array_equal(c & 0xFFFFFFFFFF, r["compressed_offset"])
+    assert np.array_equal((c >> 40) + 1, r["compressed_size"])
+    assert (ci[:, 2] == 0).all()
+    assert dig == np.ascontiguousarray(r["block_id"]).tobytes()
+    assert e_dig["uncompressed_digest"] == hashlib.sha256(dig).hexdigest()
 
 
 @pytest.mark.parametrize("compressor", ["none", "zstd", "lz4_block", ""])
@@ -199,10 +241,13 @@ def test_blob_stream_deterministic(oracle, tars):
 def test_unpack_entry_not_found_and_corrupt(oracle, tars):
     stream, *_ = cpu_stream(oracle, tars["oci_lower"], 0x100000, "zstd")
     with pytest.raises(nydus_gpu.NgpuError) as e:
-        nydus_gpu.unpack_entry(stream, "blob.meta")
+        nydus_gpu.unpack_entry(stream, "no.such.entry")
     assert e.value.code == nydus_gpu.ENOTFOUND
     with pytest.raises(blob_ref.NotFound):
-        blob_ref.unpack_entry(stream, "blob.meta")
+        blob_ref.unpack_entry(stream, "no.such.entry")
+    # the lower layer (packed without a dict) has chunks of its own: blob.meta is there;
+    # an empty blob writes none (nydus-image skips it, blob.rs dump_meta_data)
+    assert nydus_gpu.unpack_entry(stream, "blob.meta")[0] == blob_ref.unpack_entry(stream, "blob.meta")[0]
     bad = bytearray(stream)
     bad[-512 + 148] ^= 0x1  # checksum of the last header
     with pytest.raises(nydus_gpu.NgpuError):
