@@ -243,6 +243,50 @@ def pool_digests(torch, nydus_gpu, wl, device):
     return out
 
 
+def probe_bench(torch, nydus_gpu, eng, dd, Q, build_s, reps=5):
+    """The chunk-dict probe alone (dict_probe_records through
+    ngpu_dict_probe_device) over Q queries against the HBM-resident dict,
+    30% of them planted dict digests: HIP-event time per launch on the
+    launching stream, against the HBM roofline.  Algorithmic bytes per probe
+    (for this layout): 32 B query + 8 B hash slot + 24 B hit
+    record written, + 64 B dict record (key verify + hit fields) on a hit."""
+    m = dd.shape[0]
+    g = torch.Generator(device="cuda").manual_seed(0x9B0B)
+    q = torch.empty((Q, 32), dtype=torch.uint8, device="cuda")
+    q.random_(0, 256, generator=g)
+    k = int(Q * 0.3)
+    q[:k] = dd[torch.randint(0, m, (k,), device="cuda", generator=g)]
+    q = q[torch.randperm(Q, device="cuda", generator=g)].contiguous()
+    hits = torch.empty((Q, 6), dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    eng.dict_probe_device(q.data_ptr(), 32, Q, hits.data_ptr(), stream=s.cuda_stream)  # warm
+    ev[0].record(s)
+    for r in range(reps):
+        eng.dict_probe_device(q.data_ptr(), 32, Q, hits.data_ptr(), stream=s.cuda_stream)
+        ev[r + 1].record(s)
+    torch.cuda.synchronize()
+    ms = [ev[r].elapsed_time(ev[r + 1]) for r in range(reps)]
+    t = float(np.median(ms)) / 1e3
+    nhit = int((hits[:, 0] != -1).sum())
+    assert nhit >= k * 0.99, (nhit, k)
+    alg = Q * (32 + 8 + 24) + nhit * 64
+    del q, hits
+    traffic, src = pmc_traffic("", "probe", "dict_probe_records")
+    tr = {}
+    if traffic:  # PMC request bytes of the same launches (scripts/gpu_pmc_probe.sh)
+        tr = {"traffic": traffic, "traffic_source": src,
+              "traffic_gbs": round(traffic / t / 1e9, 1),
+              "traffic_frac": round(traffic / t / PEAK_HBM, 4),
+              "lines_per_probe": round(traffic / 128 / Q, 2)}
+    return {"kernel": "dict_probe_records", "queries": Q, "hits": nhit, "dict_entries": m, **tr,
+            "ms": round(t * 1e3, 4), "gprobes_s": round(Q / t / 1e9, 2),
+            "bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": round(PEAK_HBM / 1e9, 1),
+            "unit": "GB/s", "frac": round(alg / t / PEAK_HBM, 4), "algorithmic_bytes": alg,
+            "build": {"kernel": "dict_insert", "entries": m, "s": round(build_s, 4),
+                      "gentries_s": round(m / build_s / 1e9, 2)}}
+
+
 def pmc_traffic(path, workload, kernel):
     """HBM bytes per launch of the dominant kernel from a committed rocprofv3
     PMC summary of the same bench command.  Preferred: pmc_req_<workload>.json
@@ -347,6 +391,8 @@ def main():
                     "(default: newest profiles/r*/pmc_<workload>.json)")
     ap.add_argument("--cpu-sample-mib", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--probe-queries", type=int, default=16 << 20,
+                    help="dict workloads: queries of the probe-only roofline measurement (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -436,11 +482,16 @@ def main():
             local_m = m
         torch.cuda.synchronize()
         build_s = time.perf_counter() - t0
+        probe = None
+        if not wl.get("sharded") and args.probe_queries:
+            probe = probe_bench(torch, nydus_gpu, eng, dd, args.probe_queries, build_s)
         del dd, us, bl, ix
         torch.cuda.empty_cache()
         extra["dict"] = {"entries": m, "entries_this_gpu": local_m, "build_s": round(build_s, 3),
                          "build_Mentries_s": round(local_m / build_s / 1e6, 1),
                          "expected_dict_hits": expect_dict}
+        if probe:
+            extra["probe_roofline"] = probe
 
     layer_first = (np.arange(n_layers + 1, dtype=np.int64) * per_layer)
     d_first = torch.from_numpy(layer_first).cuda()

@@ -167,22 +167,31 @@ void launch_sha256(const uint8_t *data, uint64_t data_len,
                    const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
                    uint64_t *err, int variant, hipStream_t s);
 
+// One chunk-dict entry in HBM (64 B, 64-B aligned): the key and every field
+// a hit returns, so a probe that hits reads one hash-slot line and one record
+// line (SoA arrays cost a line per field: six random lines per hit).
+struct alignas(64) DictRec {
+  uint32_t digest[8];
+  uint32_t usize;  // uncompressed size (0 = any)
+  uint32_t blob;   // inner blob index
+  uint32_t index;  // RAFS chunk index
+  uint32_t gid;    // global entry id (table order; differs from the slot in node shards)
+  uint64_t uoff;   // uncompressed offset in its blob
+  uint64_t pad;
+};
+static_assert(sizeof(DictRec) == 64, "DictRec is 64 bytes");
+
 struct DictDevice {
-  const uint8_t *digests = nullptr;  // m x 32
-  const uint32_t *usize = nullptr;
-  const uint32_t *blob = nullptr;    // inner blob index
-  const uint32_t *index = nullptr;   // RAFS chunk index
-  const uint64_t *uoff = nullptr;    // uncompressed offset in its blob
-  const uint32_t *gid = nullptr;     // global entry id (node shards); null = identity
-  const uint64_t *table = nullptr;   // hash slots
+  const DictRec *rec = nullptr;      // m records, table order
+  const uint64_t *table = nullptr;   // hash slots {tag : local id}
   uint64_t mask = 0;                 // table capacity - 1
   uint64_t m = 0;
   uint32_t n_blobs = 0;
 };
 
 // dedup.hip
-void launch_dict_build(const uint8_t *digests, uint64_t m, uint64_t *table,
-                       uint64_t cap, hipStream_t s);
+void launch_dict_build(const DictRec *rec, uint64_t m, uint64_t *table, uint64_t cap,
+                       hipStream_t s);
 // hits == nullptr: probe `dict`; otherwise use the given per-chunk hits.
 // n_blobs: inner blobs of the (global) dict.  L layers; layer l owns chunks
 // [lfirst[l], lfirst[l+1]) (device array; nullptr = one layer, {0, n} is
@@ -202,9 +211,14 @@ void launch_dict_probe_owned(const uint8_t *q, uint64_t n, uint32_t owner, uint3
                              const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s);
 void launch_hits_merge(const uint8_t *q, uint64_t n, uint32_t W, const ngpu_dict_hit *parts,
                        ngpu_dict_hit *hits, hipStream_t s);
-// RAFS v6 chunk records (80 B, device) -> the dict's SoA arrays.
-void launch_dict_unpack(const uint8_t *recs, uint64_t n, uint8_t *digests, uint32_t *usize,
-                        uint32_t *blob, uint32_t *index, uint64_t *uoff, hipStream_t s);
+// RAFS v6 chunk records (80 B, device) -> dict records; gid = gids[i] (device
+// array) or gid0 + i.
+void launch_dict_unpack(const uint8_t *recs, uint64_t n, const uint32_t *gids, uint32_t gid0,
+                        DictRec *out, hipStream_t s);
+// Device SoA arrays -> dict records (index / uoff may be null: 0), gid = i.
+void launch_dict_pack(const uint8_t *digests, const uint32_t *usize, const uint32_t *blob,
+                      const uint32_t *index, const uint64_t *uoff, uint64_t n, DictRec *out,
+                      hipStream_t s);
 
 // Device workspace, grown on demand and owned by the engine.
 struct Workspace {

@@ -83,17 +83,25 @@ __device__ uint32_t ht_lookup(const uint64_t *table, uint64_t mask,
   }
 }
 
-__global__ void dict_insert(const uint8_t *__restrict__ digests, uint64_t m,
+__global__ void dict_insert(const DictRec *__restrict__ rec, uint64_t m,
                             uint64_t *__restrict__ table, uint64_t mask) {
   const uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (e < m) ht_insert_min<32>(table, mask, digests, (uint32_t)e);
+  if (e < m)
+    ht_insert_min<sizeof(DictRec)>(table, mask, reinterpret_cast<const uint8_t *>(rec), (uint32_t)e);
+}
+
+__device__ __forceinline__ uint32_t dict_lookup(const DictDevice &dict, const uint32_t d[8]) {
+  return ht_lookup<sizeof(DictRec)>(dict.table, dict.mask,
+                                    reinterpret_cast<const uint8_t *>(dict.rec), d);
 }
 
 // The hit record of local entry e (global id through gid for node shards).
 __device__ __forceinline__ ngpu_dict_hit dict_hit_of(const DictDevice &dict, uint32_t e) {
   if (e == kNone) return ngpu_dict_hit{kNone, 0, 0, 0, 0};
-  return ngpu_dict_hit{dict.gid ? dict.gid[e] : e, dict.index[e], dict.blob[e], dict.usize[e],
-                       dict.uoff[e]};
+  // the record's second half: the line the digest compare just brought in
+  const uint4 f = reinterpret_cast<const uint4 *>(dict.rec + e)[2];  // usize, blob, index, gid
+  const uint64_t uo = dict.rec[e].uoff;
+  return ngpu_dict_hit{f.w, f.z, f.y, f.x, uo};
 }
 
 // Look n digests (byte stride `stride`) up in the dict.
@@ -107,29 +115,40 @@ __global__ void dict_probe_records(const uint8_t *__restrict__ digests, uint64_t
     const uint4 *p = reinterpret_cast<const uint4 *>(digests + q * stride);
     const uint4 a = p[0], b = p[1];
     const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
+    e = dict_lookup(dict, d);
   }
   hits[q] = dict_hit_of(dict, e);
 }
 
 // RAFS v6 chunk-info records (80 B: block_id[32], blob_index, flags,
 // compressed_size, uncompressed_size, compressed_offset, uncompressed_offset,
-// file_offset, index, reserved) -> SoA.  One thread per record.
+// file_offset, index, reserved) -> dict records.  One thread per record.
 __global__ void dict_unpack(const uint8_t *__restrict__ recs, uint64_t n,
-                            uint8_t *__restrict__ digests, uint32_t *__restrict__ usize,
-                            uint32_t *__restrict__ blob, uint32_t *__restrict__ index,
-                            uint64_t *__restrict__ uoff) {
+                            const uint32_t *__restrict__ gids, uint32_t gid0,
+                            DictRec *__restrict__ out) {
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint4 *r = reinterpret_cast<const uint4 *>(recs + 80 * i);
   const uint4 a = r[0], b = r[1], c = r[2], d = r[3], f = r[4];
-  uint4 *o = reinterpret_cast<uint4 *>(digests + 32 * i);
+  uint4 *o = reinterpret_cast<uint4 *>(out + i);
   o[0] = a;
   o[1] = b;
-  blob[i] = c.x;
-  usize[i] = c.w;
-  uoff[i] = (uint64_t)d.w << 32 | d.z;
-  index[i] = f.z;
+  o[2] = make_uint4(c.w, c.x, f.z, gids ? gids[i] : gid0 + (uint32_t)i);
+  o[3] = make_uint4(d.z, d.w, 0, 0);
+}
+
+__global__ void dict_pack(const uint8_t *__restrict__ digests, const uint32_t *__restrict__ usize,
+                          const uint32_t *__restrict__ blob, const uint32_t *__restrict__ index,
+                          const uint64_t *__restrict__ uoff, uint64_t n, DictRec *__restrict__ out) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4 *dg = reinterpret_cast<const uint4 *>(digests + 32 * i);
+  uint4 *o = reinterpret_cast<uint4 *>(out + i);
+  o[0] = dg[0];
+  o[1] = dg[1];
+  o[2] = make_uint4(usize[i], blob[i], index ? index[i] : 0, (uint32_t)i);
+  const uint64_t u = uoff ? uoff[i] : 0;
+  o[3] = make_uint4((uint32_t)u, (uint32_t)(u >> 32), 0, 0);
 }
 
 // ---- layered dedup -----------------------------------------------------------
@@ -229,7 +248,7 @@ __global__ void dedup_probe_insert(const ngpu_chunk *__restrict__ chunks, uint64
     if (hits) {
       h = hits[c];
     } else if (dict.m) {
-      h = dict_hit_of(dict, ht_lookup<32>(dict.table, dict.mask, dict.digests, d));
+      h = dict_hit_of(dict, dict_lookup(dict, d));
     }
   }
   const bool is_dict = live && h.entry != kNone &&
@@ -472,13 +491,12 @@ __global__ void dedup_finalize(const uint64_t n, const uint32_t *__restrict__ ch
 
 }  // namespace
 
-void launch_dict_build(const uint8_t *digests, uint64_t m, uint64_t *table,
-                       uint64_t cap, hipStream_t s) {
+void launch_dict_build(const DictRec *rec, uint64_t m, uint64_t *table, uint64_t cap,
+                       hipStream_t s) {
   hipMemsetAsync(table, 0xFF, cap * sizeof(uint64_t), s);
   if (m == 0) return;
   const uint64_t blocks = (m + 255) / 256;
-  hipLaunchKernelGGL(dict_insert, dim3((unsigned)blocks), dim3(256), 0, s, digests, m,
-                     table, cap - 1);
+  hipLaunchKernelGGL(dict_insert, dim3((unsigned)blocks), dim3(256), 0, s, rec, m, table, cap - 1);
 }
 
 void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
@@ -517,7 +535,7 @@ __global__ void dict_probe_owned(const uint8_t *__restrict__ q, uint64_t n, uint
   if (dict.m) {
     const uint4 b = p[1];
     const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    e = ht_lookup<32>(dict.table, dict.mask, dict.digests, d);
+    e = dict_lookup(dict, d);
   }
   hits[i] = dict_hit_of(dict, e);
 }
@@ -554,11 +572,19 @@ void launch_hits_merge(const uint8_t *q, uint64_t n, uint32_t W, const ngpu_dict
                      hits);
 }
 
-void launch_dict_unpack(const uint8_t *recs, uint64_t n, uint8_t *digests, uint32_t *usize,
-                        uint32_t *blob, uint32_t *index, uint64_t *uoff, hipStream_t s) {
+void launch_dict_unpack(const uint8_t *recs, uint64_t n, const uint32_t *gids, uint32_t gid0,
+                        DictRec *out, hipStream_t s) {
   if (n == 0) return;
-  hipLaunchKernelGGL(dict_unpack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recs, n,
-                     digests, usize, blob, index, uoff);
+  hipLaunchKernelGGL(dict_unpack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recs, n, gids,
+                     gid0, out);
+}
+
+void launch_dict_pack(const uint8_t *digests, const uint32_t *usize, const uint32_t *blob,
+                      const uint32_t *index, const uint64_t *uoff, uint64_t n, DictRec *out,
+                      hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(dict_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, digests, usize,
+                     blob, index, uoff, n, out);
 }
 
 void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,

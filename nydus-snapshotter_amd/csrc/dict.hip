@@ -60,13 +60,13 @@ ngpu_dict *default_dict(ngpu_engine *e) {  // e->mu held
   return e->dict;
 }
 
-// Allocate the device arrays of an m-entry dict.
+// Allocate the records and hash table of an m-entry dict.
 int dict_alloc(ngpu_engine *e, ngpu_dict *d, uint64_t m, uint32_t n_blobs) {
   const uint64_t cap = next_pow2(2 * m + 16);
-  void *p[6] = {};
-  const uint64_t bytes[6] = {m * 32, m * 4, m * 4, m * 4, m * 8, cap * 8};
-  for (int i = 0; i < 6; ++i) {
-    if (hipMalloc(&p[i], bytes[i] ? bytes[i] : 8) != hipSuccess) {
+  void *p[2] = {};
+  const uint64_t bytes[2] = {m * sizeof(DictRec), cap * 8};
+  for (int i = 0; i < 2; ++i) {
+    if (hipMalloc(&p[i], bytes[i] ? bytes[i] : 64) != hipSuccess) {
       (void)hipGetLastError();  // the caller's dict_unref frees p[0..i)
       return fail(e, NGPU_ENOMEM, "chunk dict: %llu entries do not fit in HBM",
                   (unsigned long long)m);
@@ -74,12 +74,8 @@ int dict_alloc(ngpu_engine *e, ngpu_dict *d, uint64_t m, uint32_t n_blobs) {
     d->allocs.push_back(p[i]);
   }
   DictDevice &v = d->dev;
-  v.digests = (const uint8_t *)p[0];
-  v.usize = (const uint32_t *)p[1];
-  v.blob = (const uint32_t *)p[2];
-  v.index = (const uint32_t *)p[3];
-  v.uoff = (const uint64_t *)p[4];
-  v.table = (const uint64_t *)p[5];
+  v.rec = (const DictRec *)p[0];
+  v.table = (const uint64_t *)p[1];
   v.mask = cap - 1;
   v.m = m;
   v.n_blobs = n_blobs;
@@ -96,16 +92,17 @@ ngpu_dict *dict_new(ngpu_engine *e) {
 
 // Build the hash table over the uploaded digests (first table entry wins).
 int dict_build(ngpu_engine *e, ngpu_dict *d) {
-  launch_dict_build(d->dev.digests, d->dev.m, const_cast<uint64_t *>(d->dev.table),
-                    d->dev.mask + 1, e->stream);
+  launch_dict_build(d->dev.rec, d->dev.m, const_cast<uint64_t *>(d->dev.table), d->dev.mask + 1,
+                    e->stream);
   HIP_TRY(e, hipGetLastError());
   HIP_TRY(e, hipStreamSynchronize(e->stream));
   return 0;
 }
 
-// From 80-B RAFS v6 chunk records in host memory (e->mu held).
+// From 80-B RAFS v6 chunk records in host memory (e->mu held); gids: the
+// records' global entry ids (node shards), null = their positions.
 int dict_from_records(ngpu_engine *e, const uint8_t *recs, uint64_t m, const uint8_t *blobs,
-                      uint32_t n_blobs, ngpu_dict **out) {
+                      uint32_t n_blobs, ngpu_dict **out, const uint32_t *gids) {
   if (m >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "chunk dict too large (%llu entries)",
                                       (unsigned long long)m);
   uint32_t nb = 0;
@@ -131,27 +128,30 @@ int dict_from_records(ngpu_engine *e, const uint8_t *recs, uint64_t m, const uin
     d->place[i] = DictPlace{r->compressed_offset, r->compressed_size, r->flags};
   }
   if (blobs && n_blobs) d->blob_table.assign(blobs, blobs + 256ull * n_blobs);
-  // upload in batches of <= 1M records, unpack to SoA on the GPU
+  // upload in batches of <= 1M records, unpack to dict records on the GPU
   const uint64_t batch = std::min<uint64_t>(m, 1u << 20);
   uint8_t *tmp = nullptr;
-  if (m && hipMalloc((void **)&tmp, batch * 80) != hipSuccess) {
+  uint32_t *tmp_gid = nullptr;
+  if (m && (hipMalloc((void **)&tmp, batch * 80) != hipSuccess ||
+            (gids && hipMalloc((void **)&tmp_gid, batch * 4) != hipSuccess))) {
+    if (tmp) (void)hipFree(tmp);
     dict_unref(d);
     return fail(e, NGPU_ENOMEM, "chunk dict: staging allocation failed");
   }
-  DictDevice &v = d->dev;
+  DictRec *rec = const_cast<DictRec *>(d->dev.rec);
   for (uint64_t a = 0; a < m && !rc; a += batch) {
     const uint64_t k = std::min(batch, m - a);
-    if (hipMemcpyAsync(tmp, recs + 80 * a, k * 80, hipMemcpyHostToDevice, e->stream) != hipSuccess) {
+    if (hipMemcpyAsync(tmp, recs + 80 * a, k * 80, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        (gids && hipMemcpyAsync(tmp_gid, gids + a, k * 4, hipMemcpyHostToDevice, e->stream) !=
+                     hipSuccess)) {
       rc = fail(e, NGPU_EHIP, "chunk dict: upload failed");
       break;
     }
-    launch_dict_unpack(tmp, k, const_cast<uint8_t *>(v.digests) + 32 * a,
-                       const_cast<uint32_t *>(v.usize) + a, const_cast<uint32_t *>(v.blob) + a,
-                       const_cast<uint32_t *>(v.index) + a, const_cast<uint64_t *>(v.uoff) + a,
-                       e->stream);
+    launch_dict_unpack(tmp, k, gids ? tmp_gid : nullptr, (uint32_t)a, rec + a, e->stream);
     // the next batch overwrites tmp
     if (hipStreamSynchronize(e->stream) != hipSuccess) rc = fail(e, NGPU_EHIP, "chunk dict: unpack failed");
   }
+  if (tmp_gid) (void)hipFree(tmp_gid);
   if (tmp) (void)hipFree(tmp);
   if (!rc) rc = dict_build(e, d);
   if (rc) {
@@ -176,19 +176,26 @@ int dict_from_arrays(ngpu_engine *e, const uint8_t *dg, const uint32_t *us, cons
     dict_unref(d);
     return rc;
   }
-  DictDevice &v = d->dev;
-  hipStream_t s = e->stream;
-  bool ok = true;
-  if (m) {
-    ok = hipMemcpyAsync((void *)v.digests, dg, m * 32, kind, s) == hipSuccess &&
-         hipMemcpyAsync((void *)v.usize, us, m * 4, kind, s) == hipSuccess &&
-         hipMemcpyAsync((void *)v.blob, bl, m * 4, kind, s) == hipSuccess &&
-         (ix ? hipMemcpyAsync((void *)v.index, ix, m * 4, kind, s)
-             : hipMemsetAsync((void *)v.index, 0, m * 4, s)) == hipSuccess &&
-         (uo ? hipMemcpyAsync((void *)v.uoff, uo, m * 8, kind, s)
-             : hipMemsetAsync((void *)v.uoff, 0, m * 8, s)) == hipSuccess;
+  DictRec *rec = const_cast<DictRec *>(d->dev.rec);
+  if (m && kind == hipMemcpyHostToDevice) {  // pack on the host, one upload
+    std::vector<DictRec> h(m);
+    for (uint64_t i = 0; i < m; ++i) {
+      DictRec &r = h[i];
+      memset(&r, 0, sizeof r);
+      memcpy(r.digest, dg + 32 * i, 32);
+      r.usize = us[i];
+      r.blob = bl[i];
+      r.index = ix ? ix[i] : 0;
+      r.gid = (uint32_t)i;
+      r.uoff = uo ? uo[i] : 0;
+    }
+    if (hipMemcpyAsync(rec, h.data(), m * sizeof(DictRec), kind, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+      rc = fail(e, NGPU_EHIP, "chunk dict: upload failed");
+  } else if (m) {
+    launch_dict_pack(dg, us, bl, ix, uo, m, rec, e->stream);
+    if (hipGetLastError() != hipSuccess) rc = fail(e, NGPU_EHIP, "chunk dict: pack failed");
   }
-  if (!ok) rc = fail(e, NGPU_EHIP, "chunk dict: upload failed");
   if (!rc) rc = dict_build(e, d);
   if (rc) {
     dict_unref(d);
@@ -267,7 +274,8 @@ int dict_load_file(ngpu_engine *e, const char *path, const struct stat &st, ngpu
   int rc = read_dict_bootstrap(e, path, (uint64_t)st.st_size, &recs, &blobs);
   if (rc) return rc;
   ngpu_dict *d = nullptr;
-  if ((rc = dict_from_records(e, recs.data(), recs.size() / 80, blobs.data(), blobs.size() / 256, &d)))
+  if ((rc = dict_from_records(e, recs.data(), recs.size() / 80, blobs.data(), blobs.size() / 256, &d,
+                              nullptr)))
     return rc;
   d->path = path;
   d->st_dev = st.st_dev;
@@ -334,7 +342,7 @@ int ngpu_dict_create(ngpu_engine *e, const void *records, uint64_t n, const void
   DeviceGuard dg(e->device);
   return guarded([&] {
     return dict_from_records(e, (const uint8_t *)records, n, (const uint8_t *)blob_table, n_blobs,
-                             out);
+                             out, nullptr);
   });
 }
 

@@ -36,9 +36,9 @@ struct ngpu_dict {
   uint64_t st_dev = 0, st_ino = 0, st_size = 0;
   int64_t st_mtime_ns = 0;
   // node dicts (node.hip): one part per node device -- a digest-prefix shard
-  // (its DictDevice::gid maps local to global entry ids) or a full replica --
+  // (its records carry their global entry ids) or a full replica --
   // and per part a probe stream plus the exchange buffers on its device.
-  // dev.m / dev.n_blobs are the global counts; dev's arrays stay null.
+  // dev.m / dev.n_blobs are the global counts; dev.rec / dev.table stay null.
   struct PartIO {
     hipStream_t stream = nullptr;
     uint8_t *q = nullptr;        // requester digests (n x 32), copied in
@@ -121,7 +121,7 @@ inline uint32_t dict_blobs(const ngpu_dict *d) { return d ? d->dev.n_blobs : 0; 
 uint64_t next_pow2(uint64_t x);
 // From 80-B RAFS v6 records in host memory on engine e's device (e->mu held).
 int dict_from_records(ngpu_engine *e, const uint8_t *recs, uint64_t m, const uint8_t *blobs,
-                      uint32_t n_blobs, ngpu_dict **out);
+                      uint32_t n_blobs, ngpu_dict **out, const uint32_t *gids);
 int read_dict_bootstrap(ngpu_engine *e, const char *path, uint64_t file_size,
                         std::vector<uint8_t> *recs, std::vector<uint8_t> *blobs);
 // Node dicts: the replica on e's device, or (partitioned) route the probe of

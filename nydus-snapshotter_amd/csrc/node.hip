@@ -181,23 +181,11 @@ int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint
     ngpu_dict *p = nullptr;
     const uint8_t *pr = d->replicated ? recs : part_recs[o].data();
     const uint64_t pm = d->replicated ? m : gid[o].size();
-    if ((rc = dict_from_records(e, pr, pm, blobs, nb, &p))) break;
+    if ((rc = dict_from_records(e, pr, pm, blobs, nb, &p, d->replicated ? nullptr : gid[o].data())))
+      break;
     p->dev.n_blobs = nb;
     p->place.clear();  // the global table (d->place) answers the writer
     d->parts.push_back(p);
-    if (!d->replicated && pm) {
-      uint32_t *g32 = nullptr;
-      if (hipMalloc((void **)&g32, pm * 4) != hipSuccess) {
-        rc = fail(e, NGPU_ENOMEM, "node dict: gid allocation failed");
-        break;
-      }
-      p->allocs.push_back(g32);
-      if (hipMemcpy(g32, gid[o].data(), pm * 4, hipMemcpyHostToDevice) != hipSuccess) {
-        rc = fail(e, NGPU_EHIP, "node dict: gid upload failed");
-        break;
-      }
-      p->dev.gid = g32;
-    }
     if (hipStreamCreateWithFlags(&d->io[o].stream, hipStreamNonBlocking) != hipSuccess)
       rc = fail(e, NGPU_EHIP, "node dict: probe stream");
   }
