@@ -867,7 +867,8 @@ int copy_zstd(const Reader &r, uint64_t off, uint64_t len, const char *name, ngp
   if (!ds) return host_fail(NGPU_ENOMEM, "zstd: no stream");
   std::vector<uint8_t> in(std::min<uint64_t>(len, 1u << 20) + 1), out(1u << 20);
   int rc = 0;
-  size_t last = 1;  // 0 once a frame is complete
+  // 0 between frames: an empty section is a clean EOF, as for the Go decoder
+  size_t last = 0;
   while (len && !rc) {
     const uint64_t k = std::min<uint64_t>(len, in.size());
     if ((rc = r.read(in.data(), k, off))) break;

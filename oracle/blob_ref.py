@@ -97,7 +97,9 @@ def seek_file_by_toc(ra: bytes, target: str):
         # that exist (EOF ends the copy without an error)
         raw = ra[e["compressed_offset"]:e["compressed_offset"] + e["compressed_size"]]
         if comp == COMPRESSOR_ZSTD:
-            data = zstd_decompress(raw, e["uncompressed_size"])
+            # zstd.NewReader(sr) + io.Copy: the frame(s) decide the length;
+            # the entry's uncompressed_size is never read
+            data = zstd_stream_decompress(raw)
         elif comp == COMPRESSOR_NONE:
             data = raw
         else:
@@ -126,19 +128,63 @@ def calc_blob_toc_digest(ra: bytes) -> str:
 _zstd = _lz4 = None
 
 
-def zstd_decompress(src: bytes, usize: int) -> bytes:
+def _load_zstd():
     global _zstd
     if _zstd is None:
-        _zstd = ctypes.CDLL("libzstd.so.1")
-        _zstd.ZSTD_decompress.restype = ctypes.c_size_t
-        _zstd.ZSTD_decompress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
-                                          ctypes.c_size_t]
-        _zstd.ZSTD_isError.argtypes = [ctypes.c_size_t]
+        z = ctypes.CDLL("libzstd.so.1")
+        z.ZSTD_decompress.restype = ctypes.c_size_t
+        z.ZSTD_decompress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                      ctypes.c_size_t]
+        z.ZSTD_isError.argtypes = [ctypes.c_size_t]
+        z.ZSTD_createDStream.restype = ctypes.c_void_p
+        z.ZSTD_freeDStream.argtypes = [ctypes.c_void_p]
+        z.ZSTD_decompressStream.restype = ctypes.c_size_t
+        z.ZSTD_decompressStream.argtypes = [ctypes.c_void_p, ctypes.POINTER(_ZBuf),
+                                            ctypes.POINTER(_ZBuf)]
+        _zstd = z
+    return _zstd
+
+
+class _ZBuf(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("size", ctypes.c_size_t), ("pos", ctypes.c_size_t)]
+
+
+def zstd_decompress(src: bytes, usize: int) -> bytes:
+    """One frame of exactly usize bytes (chunk data: the record's size)."""
+    _load_zstd()
     dst = ctypes.create_string_buffer(max(1, usize))
     r = _zstd.ZSTD_decompress(dst, usize, src, len(src))
     if _zstd.ZSTD_isError(r) or r != usize:
         raise ValueError("zstd decompression failed")
     return dst.raw[:usize]
+
+
+def zstd_stream_decompress(src: bytes) -> bytes:
+    """What klauspost/compress v1.17.11 zstd.Decoder yields through io.Copy
+    (the reader at convert_unix.go:252-265): back-to-back frames decoded
+    until the input ends; empty input is a clean EOF (no bytes, no error);
+    input that ends inside a frame, or a bad frame, is an error."""
+    z = _load_zstd()
+    ds = z.ZSTD_createDStream()
+    out, chunk = [], ctypes.create_string_buffer(1 << 20)
+    src_buf = ctypes.create_string_buffer(src, max(1, len(src)))
+    ib = _ZBuf(ctypes.cast(src_buf, ctypes.c_void_p), len(src), 0)
+    last = 0  # 0: between frames
+    try:
+        while True:
+            ob = _ZBuf(ctypes.cast(chunk, ctypes.c_void_p), len(chunk), 0)
+            if ib.pos == ib.size and last == 0:
+                break
+            before = ib.pos
+            last = z.ZSTD_decompressStream(ds, ctypes.byref(ob), ctypes.byref(ib))
+            if z.ZSTD_isError(last):
+                raise ValueError("zstd: bad frame")
+            out.append(chunk.raw[:ob.pos])
+            if ib.pos == ib.size and ob.pos == 0 and before == ib.pos and last != 0:
+                raise ValueError("zstd: unexpected EOF")
+    finally:
+        z.ZSTD_freeDStream(ds)
+    return b"".join(out)
 
 
 def lz4_block_decompress(src: bytes, usize: int) -> bytes:

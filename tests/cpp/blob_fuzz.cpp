@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <random>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -61,7 +62,7 @@ int main(int argc, char **argv) {
       s[pos] = val;
       edits.emplace_back(pos, val);
     };
-    const int kind = (int)(rng() % 4);
+    const int kind = (int)(rng() % 5);
     const uint64_t tail = s.size() < 20000 ? s.size() : 20000;  // headers, TOC, bootstrap
     if (kind == 0) {  // flip a few bytes in the tail
       const int k = 1 + (int)(rng() % 4);
@@ -74,15 +75,30 @@ int main(int argc, char **argv) {
     } else if (kind == 2) {  // rewrite an octal size digit of one of the last headers
       const uint64_t h = s.size() - 512 * (1 + rng() % 3);
       set(h + 124 + rng() % 11, (uint8_t)('0' + rng() % 8));
-    } else {  // random byte over the TOC entries
+    } else if (kind == 3) {  // random byte over the TOC entries
       set(s.size() - 512 - 1 - rng() % 256, (uint8_t)rng());
+    } else {  // one field of one TOC entry: flags -> zstd, or a huge size / offset
+      const uint64_t toc_len = strtoull(std::string((const char *)&s[s.size() - 512 + 124], 11).c_str(),
+                                        nullptr, 8);
+      const uint64_t n = toc_len / 128;
+      if (n && toc_len <= s.size() - 512) {
+        const uint64_t e = s.size() - 512 - toc_len + 128 * (rng() % n);
+        const int field = (int)(rng() % 4);
+        if (field == 0) {
+          set(e, 0x2);  // compressor zstd on whatever the entry holds
+        } else {      // 1 compressed_offset, 2 compressed_size, 3 uncompressed_size
+          const uint64_t at = e + 56 + 8 * (field - 1);
+          const uint64_t v = field == 3 ? rng() : rng() >> (rng() % 64);
+          for (int b = 0; b < 8; ++b) set(at + b, (uint8_t)(v >> (8 * b)));
+        }
+      }
     }
     printf("%zu ", s.size());
     for (size_t i = 0; i < edits.size(); ++i)
       printf("%s%llu:%u", i ? "," : "", (unsigned long long)edits[i].first, edits[i].second);
     printf("|");
     Src src{&s};
-    for (const char *name : {"image.boot", "image.blob"}) {
+    for (const char *name : {"image.boot", "image.blob", "blob.meta"}) {
       Out o;
       uint8_t toc[128];
       const int rc = ngpu_unpack_entry(ra, &src, s.size(), name, wr, &o, toc);

@@ -390,7 +390,10 @@ def test_fd_writer_matches_python_writer(oracle, tars, tmp_path):
 
 def test_reader_mutation_fuzz_asan(oracle, tars, tmp_path):
     """Mutated Pack streams (tail byte flips, truncations, header size digits,
-    TOC fields) through the product reader + merge built with ASan/UBSan
+    TOC bytes, and whole TOC fields: flags -> zstd, huge compressed offsets /
+    sizes, huge uncompressed sizes the zstd reader must ignore) through the
+    product reader + merge built with ASan/UBSan, for image.boot, image.blob
+    and the zstd-compressed blob.meta
     (tests/cpp/blob_fuzz.cpp, host only): no memory error, and every outcome
     agrees with the reference reader (oracle/blob_ref.py) — same bytes when
     both succeed.  One documented deviation: a TOC entry whose range runs past
@@ -418,7 +421,9 @@ def test_reader_mutation_fuzz_asan(oracle, tars, tmp_path):
         for x in b:
             h = ((h ^ x) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
         return h
-    seen = {"ok": 0, "both_fail": 0, "past_end": 0}
+    seen = {"ok": 0, "both_fail": 0, "past_end": 0, "zstd_ok": 0}
+    meta = blob_ref.unpack_entry(stream, "blob.meta")[1]
+    assert meta["flags"] & 0xF == blob_ref.COMPRESSOR_ZSTD  # the fuzz reaches the zstd path
     for line in out.stdout.splitlines():
         head, res = line.split("|")
         size, _, ed = head.partition(" ")
@@ -427,7 +432,8 @@ def test_reader_mutation_fuzz_asan(oracle, tars, tmp_path):
             p, v = e.split(":")
             s[int(p)] = int(v)
         s = bytes(s)
-        for name, r in zip((blob_ref.ENTRY_BOOTSTRAP, blob_ref.ENTRY_BLOB), res.split(";")):
+        for name, r in zip((blob_ref.ENTRY_BOOTSTRAP, blob_ref.ENTRY_BLOB, "blob.meta"),
+                           res.split(";")):
             rc, ln, h = map(int, r.split(","))
             try:
                 data, toc = blob_ref.unpack_entry(s, name)
@@ -438,13 +444,59 @@ def test_reader_mutation_fuzz_asan(oracle, tars, tmp_path):
                 assert ok, (line, name)
                 assert len(data) == ln and (ln > 100_000 or fnv(data) == h), (line, name)
                 seen["ok"] += 1
+                seen["zstd_ok"] += bool(toc and toc["flags"] & 0xF == blob_ref.COMPRESSOR_ZSTD)
             elif ok:
                 assert rc == -8 and toc is not None and \
                     toc["compressed_offset"] + toc["compressed_size"] > len(s), (line, name)
                 seen["past_end"] += 1
             else:
                 seen["both_fail"] += 1
-    assert seen["ok"] > 500 and seen["both_fail"] > 100, seen
+    assert seen["ok"] > 500 and seen["both_fail"] > 100 and seen["zstd_ok"] > 100, seen
+
+
+def test_blob_writer_threads_tsan(oracle, tars, tmp_path):
+    """The host blob writer's compression pool + ordered sink (ngpu_blob_write
+    with 8 threads, tests/cpp/blob_tsan.cpp) built under ThreadSanitizer:
+    no data race reported, and the stream is byte-equal to the regular
+    build's for every compressor, with chunk-dict records in the bootstrap."""
+    import subprocess
+    from conftest import ROOT
+    from nydus_gpu._lib import NgpuLayerStats
+    exe = str(tmp_path / "blob_tsan")
+    csrc = os.path.join(ROOT, "nydus-snapshotter_amd", "csrc")
+    subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=thread",
+                           "-I", os.path.join(ROOT, "include"), "-I", csrc,
+                           os.path.join(ROOT, "tests", "cpp", "blob_tsan.cpp"),
+                           os.path.join(csrc, "blob.cpp"), "-o", exe, "-lcrypto", "-ldl",
+                           "-lpthread"])
+    cs, tar = 0x10000, tars["alpine_like"]
+    ch, res, st = cpu_results(oracle, tar, cs)
+    tab = nydus_gpu.chunk_table(ch, res).view(rafs.CHUNK_INFO_DTYPE).reshape(-1)[::3].copy()
+    dict_boot = rafs.write_v6_bootstrap(tab, cs, flags=0x5,
+                                        blobs=rafs.make_blob_table(["ab" * 32], cs, counts=[len(tab)]))
+    d = rafs.read_v6(dict_boot)
+    ch, res, st = cpu_results(oracle, tar, cs, "blake3", dict_boot)
+    assert (res["kind"] == nydus_gpu.DICT).sum() > 10 and (res["kind"] == nydus_gpu.NEW).sum() > 50
+    files = {"data": tar, "ch": np.ascontiguousarray(ch).tobytes(),
+             "res": np.ascontiguousarray(res).tobytes(),
+             "st": bytes(NgpuLayerStats(**{k: st[k] for k, _ in NgpuLayerStats._fields_})),
+             "db": np.ascontiguousarray(d["blobs"]).tobytes(),
+             "dc": np.ascontiguousarray(d["chunks"]).tobytes()}
+    for k, v in files.items():
+        (tmp_path / k).write_bytes(v)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66")
+    for name, code in (("zstd", 2), ("lz4_block", 4), ("none", 1)):
+        p = tmp_path / f"out-{name}"
+        r = subprocess.run([exe] + [str(tmp_path / k) for k in ("data", "ch", "res", "st")] +
+                           [str(p), str(code), "8", str(cs), "0",
+                            str(tmp_path / "db"), str(tmp_path / "dc")],
+                           capture_output=True, text=True, env=env, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
+        ref = io.BytesIO()
+        nydus_gpu.blob_write(tar, ch, res, st, ref, compressor=name, threads=8, chunk_size=cs,
+                             dict_blobs=d["blobs"], dict_chunks=d["chunks"])
+        assert p.read_bytes() == ref.getvalue(), name
 
 
 def test_inspect_canonical_dump(oracle, tars, tmp_path):
