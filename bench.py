@@ -371,12 +371,136 @@ def end_to_end(torch, nydus_gpu, buf, wl, stride, device, sample_bytes=2 << 30):
     return res
 
 
+def node_bench(args):
+    """`--node 0,1,..`: ONE process drives the listed GPUs through the C ABI's
+    multi-GPU node (ngpu_node_*, csrc/node.hip) -- the form a cgo
+    caller uses.  Each device holds its own layer set of the workload; one node
+    dict (pool digests + filler, 80-B RAFS v6 records) is built partitioned by
+    digest prefix, then replicated, and every step runs
+    ngpu_node_process_device on every device (digest + the dedup stage, whose
+    probe goes over the exchange when partitioned).  The two modes' dedup
+    times give the exchange cost.  Listing one device several times rehearses
+    the node on one GPU (the copies then stay inside one HBM).  Not the
+    driver's line (that is the one-process-per-GPU launch in main())."""
+    import torch
+    import nydus_gpu
+    from nydus_gpu import rafs
+    devs = [int(x) for x in args.node.split(",")]
+    W = len(devs)
+    wl = dict(WORKLOADS[args.workload])
+    if not wl.get("pool") or wl.get("tar"):
+        raise SystemExit("--node takes a layered dict workload (c4-16, c5-1000)")
+    if wl.get("layers_total"):
+        wl["layers"] = -(-wl["layers_total"] // W)
+        wl["n_files"] *= wl["layers"]
+    if args.dict_entries:
+        wl["dict_entries"] = args.dict_entries
+    S, m, L = wl["chunk"], wl["dict_entries"], wl["layers"]
+    node = nydus_gpu.Node(devs, digester=wl["digester"], chunk_size=S, timing=True)
+    per = []
+    try:
+        _, stride, _, _ = synthetic_layout(1, wl["file_size"], S)
+        for i, dev in enumerate(devs):
+            with torch.cuda.device(dev):
+                buf, ch = build_layer_on_gpu(torch, wl["n_files"], wl["file_size"], S,
+                                             seed=0x6E79647573 + i)
+                _, planted = plant_pool(torch, buf, ch, stride, wl, seed=i)
+                n = len(ch)
+                first = np.arange(L + 1, dtype=np.int64) * (n // L)
+                per.append(dict(
+                    dev=dev, buf=buf, n=n, planted=planted, bytes=int(ch["length"].sum()),
+                    d_ch=torch.from_numpy(ch.view(np.uint8).copy()).cuda(),
+                    out=torch.empty(n * 64, dtype=torch.uint8, device="cuda"),
+                    first=torch.from_numpy(first).cuda(),
+                    st=torch.zeros(L * nydus_gpu.LAYER_STATS_DTYPE.itemsize, dtype=torch.uint8,
+                                   device="cuda"),
+                    stream=torch.cuda.Stream()))
+        with torch.cuda.device(devs[0]):
+            pool = pool_digests(torch, nydus_gpu, wl, devs[0]).cpu().numpy()
+        rng = np.random.default_rng(0xD1C7)
+        recs = np.zeros(m, rafs.CHUNK_INFO_DTYPE)
+        recs["block_id"][: len(pool)] = pool
+        recs["block_id"][len(pool):] = rng.integers(0, 256, (m - len(pool), 32), dtype=np.uint8)
+        recs["uncompressed_size"] = S
+        recs["compressed_size"] = S
+        recs["blob_index"] = rng.integers(0, 8, m)
+        recs["index"] = np.arange(m)
+        recs["uncompressed_offset"] = np.arange(m, dtype=np.uint64) * S
+        blobs = rafs.make_blob_table([f"{b:064x}" for b in range(8)], S)
+        del pool
+        torch.cuda.synchronize()
+
+        def step(d):
+            for i, p in enumerate(per):
+                node.process_device(i, d, p["buf"].data_ptr(), p["buf"].numel(), p["d_ch"].data_ptr(),
+                                    p["n"], p["out"].data_ptr(), p["first"].data_ptr(), L,
+                                    p["st"].data_ptr(), stream=p["stream"].cuda_stream)
+
+        def sync():
+            for p in per:
+                p["stream"].synchronize()
+
+        modes = {}
+        for name, mode in (("partition", nydus_gpu.NODE_DICT_PARTITION),
+                           ("replicate", nydus_gpu.NODE_DICT_REPLICATE)):
+            t0 = time.perf_counter()
+            d = node.dict_create(recs, blobs, mode=mode)
+            build_s = time.perf_counter() - t0
+            for _ in range(args.warmup):
+                step(d)
+            sync()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step(d)
+            sync()
+            elapsed = time.perf_counter() - t0
+            hits = []
+            for i, p in enumerate(per):
+                res = p["out"].cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+                hits.append(int((res["kind"] == nydus_gpu.DICT).sum()))
+                assert hits[-1] >= p["planted"] * 0.99, (name, i, hits[-1], p["planted"])
+            tm = [e.timing_at(b) for e in node.engines for b in range(min(args.steps, 64))]
+            total = sum(p["bytes"] for p in per) * args.steps
+            modes[name] = {"dict_build_s": round(build_s, 2), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+                           "value_gbs": round(total / elapsed / 1e9, 1),
+                           "digest_ms": round(float(np.mean([t["digest_ms"] for t in tm])), 3),
+                           "dedup_ms": round(float(np.mean([t["dedup_ms"] for t in tm])), 3),
+                           "dict_hits": hits}
+            d.release()
+        ex = modes["partition"]["dedup_ms"] - modes["replicate"]["dedup_ms"]
+        n_all = sum(p["n"] for p in per)
+        line = {
+            "metric": "GB/s of layer data chunk-hashed+deduped (node, one process)",
+            "value": modes["partition"]["value_gbs"], "unit": "GB/s", "n_gpus": len(set(devs)),
+            "node_devices": devs, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": modes["partition"]["ms_per_step"], "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (random bytes generated on the GPU, real GNU tar headers; pool "
+                    "contents planted)",
+            "config": {"workload": wl["desc"], "name": args.workload, "layers_per_device": L,
+                       "chunks_per_device": per[0]["n"], "dict_entries": m,
+                       "parallelism": f"node x{W} (ngpu_node_*, one process)"},
+            "modes": modes,
+            "exchange": {"dedup_ms_partition_minus_replicate": round(ex, 3),
+                         "bytes_per_step": n_all * (32 + 24) * (W - 1) // W,
+                         "note": "per step every device sends its digests (32 B/chunk) to each owner "
+                                 "and gets 24-B hits back; on a one-GPU rehearsal the peer copies "
+                                 "stay in one HBM and the W engines share the GPU"},
+        }
+        print(json.dumps(line), flush=True)
+    finally:
+        per.clear()
+        node.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=20,
-                    help="untimed steps; the clock takes ~5 launches to settle (profiles/r1)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps (default 20; 80 for the pool/dict workloads, whose setup -- "
+                         "64 GiB of pool hashed, a 16M-200M entry dict built, GBs freed -- leaves "
+                         "the GPU ~30%% slow for ~150 ms after it: profiles/r2/c4-16_warmup_r2u.json)")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--lanes", type=int, default=0, help="leaves per lane (0=auto)")
     ap.add_argument("--sha-mode", choices=["auto", "split", "pair"], default="auto",
@@ -393,7 +517,16 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--probe-queries", type=int, default=16 << 20,
                     help="dict workloads: queries of the probe-only roofline measurement (0 = skip)")
+    ap.add_argument("--dump-timings", action="store_true",
+                    help="add every timed call's stage times (oldest first) to the line")
+    ap.add_argument("--node", default="", help="comma list of devices: one process drives them "
+                    "through ngpu_node_* (a device may repeat: one-GPU rehearsal); see node_bench")
     args = ap.parse_args()
+    if args.warmup is None:
+        w = WORKLOADS[args.workload]
+        args.warmup = 80 if (w.get("pool") or w.get("dict_entries")) else 20
+    if args.node:
+        return node_bench(args)
 
     import torch
     import nydus_gpu
@@ -570,7 +703,8 @@ def main():
     timings = [eng.timing_at(b) for b in range(min(args.steps, 64))]
     total_bytes = file_bytes * args.steps * world
     value = total_bytes / elapsed / 1e9
-    dig_ms = float(np.mean([t["digest_ms"] for t in timings]))
+    dig_all = [t["digest_ms"] for t in timings]
+    dig_ms = float(np.mean(dig_all))
     tree_ms = float(np.mean([t["tree_ms"] for t in timings]))
     dedup_ms = float(np.mean([t["dedup_ms"] for t in timings]))
     D = timings[-1]["group_log2"]
@@ -648,12 +782,17 @@ def main():
                    "layer_bytes": int(buf.numel()), "file_bytes_per_gpu": file_bytes, "chunks": n,
                    "chunk_size": wl["chunk"], "digester": wl["digester"], "layers_per_gpu": n_layers,
                    "leaves_per_lane": 1 << D, "parallelism": f"layer-sharded x{world}"},
-        "stage_ms": {"digest": round(dig_ms, 3), "tree": round(tree_ms, 3), "dedup": round(dedup_ms, 3)},
+        "stage_ms": {"digest": round(dig_ms, 3), "tree": round(tree_ms, 3), "dedup": round(dedup_ms, 3),
+                     "digest_min_med_max": [round(float(f(dig_all)), 3)
+                                            for f in (np.min, np.median, np.max)]},
         **extra,
         "roofline": roof,
         "cpu_baseline": cpu,
         "e2e_pcie": e2e,
     }
+    if args.dump_timings:
+        line["timings"] = [{k: round(t[k], 3) for k in ("digest_ms", "tree_ms", "dedup_ms", "total_ms")}
+                           for t in timings[::-1]]
     if cpu:
         # device-resident GPU rate (the layer already in HBM) over the all-core CPU rate
         line["speedup_vs_cpu"] = round(value / cpu["value"], 2)
