@@ -461,13 +461,34 @@ def node_bench(args):
                 assert hits[-1] >= p["planted"] * 0.99, (name, i, hits[-1], p["planted"])
             tm = [e.timing_at(b) for e in node.engines for b in range(min(args.steps, 64))]
             total = sum(p["bytes"] for p in per) * args.steps
+            # the dedup stage alone (dict routing + exchange + dedup kernels),
+            # one engine at a time so no other engine's digest shares the GPU:
+            # ngpu_dedup_layers_device with the node dict as the engine default
+            alone = []
+            for i, p in enumerate(per):
+                e = node.engines[i]
+                e.set_dict(d)
+                with torch.cuda.device(p["dev"]):
+                    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                    for r in range(25):
+                        if r == 5:
+                            ev[0].record(p["stream"])
+                        e.dedup_layers_device(p["d_ch"].data_ptr(), p["n"], p["out"].data_ptr(),
+                                              p["first"].data_ptr(), L, p["st"].data_ptr(),
+                                              stream=p["stream"].cuda_stream)
+                    ev[1].record(p["stream"])
+                    p["stream"].synchronize()
+                    alone.append(ev[0].elapsed_time(ev[1]) / 20)
+                e.set_dict(None)
             modes[name] = {"dict_build_s": round(build_s, 2), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
                            "value_gbs": round(total / elapsed / 1e9, 1),
                            "digest_ms": round(float(np.mean([t["digest_ms"] for t in tm])), 3),
                            "dedup_ms": round(float(np.mean([t["dedup_ms"] for t in tm])), 3),
+                           "dedup_alone_ms": [round(a, 4) for a in alone],
                            "dict_hits": hits}
             d.release()
-        ex = modes["partition"]["dedup_ms"] - modes["replicate"]["dedup_ms"]
+        ex = float(np.mean(modes["partition"]["dedup_alone_ms"])) - \
+            float(np.mean(modes["replicate"]["dedup_alone_ms"]))
         n_all = sum(p["n"] for p in per)
         line = {
             "metric": "GB/s of layer data chunk-hashed+deduped (node, one process)",
@@ -481,7 +502,7 @@ def node_bench(args):
                        "chunks_per_device": per[0]["n"], "dict_entries": m,
                        "parallelism": f"node x{W} (ngpu_node_*, one process)"},
             "modes": modes,
-            "exchange": {"dedup_ms_partition_minus_replicate": round(ex, 3),
+            "exchange": {"dedup_alone_ms_partition_minus_replicate": round(ex, 4),
                          "bytes_per_step": n_all * (32 + 24) * (W - 1) // W,
                          "note": "per step every device sends its digests (32 B/chunk) to each owner "
                                  "and gets 24-B hits back; on a one-GPU rehearsal the peer copies "

@@ -92,6 +92,10 @@ typedef struct {
  * 4 KiB-align the uncompressed offsets of NEW chunks for RAFS v5 too (v6
  * always aligns). */
 #define NGPU_FLAG_ALIGNED_CHUNK 0x2u
+/* Tuning / tests: never take the one-workgroup path for small calls (chunk
+ * planning and the dedup stage of calls with <= 4096 chunks run in one fused
+ * workgroup each by default; this flag keeps the multi-kernel grid path). */
+#define NGPU_FLAG_GRID_STAGES 0x4u
 /* Tuning (benchmarks only): bits 8..10 = 1 + BLAKE3 load mode
  * (bit0 non-temporal loads, bit1 next-block prefetch); 0 = library default. */
 #define NGPU_FLAG_LOAD_MODE_SHIFT 8

@@ -19,6 +19,8 @@
 //     level by level in LDS (pairwise with the odd tail promoted == BLAKE3's
 //     left-complete tree), 1024 CVs per LDS tile; the last compression gets
 //     ROOT.  This carries 1/2^D of the parent work only.
+#include <hip/hip_ext.h>
+
 #include "common.hpp"
 
 namespace ngpu {
@@ -324,6 +326,94 @@ __global__ void b3_fill_group_chunk(const uint64_t *__restrict__ gbase,
        c < n; c += slots) {
     const uint64_t b = gbase[c], e = gbase[c + 1];
     for (uint64_t g = b + sl; g < e && g < cap_g; g += W) gchunk[g] = (uint32_t)c;
+  }
+}
+
+// Small calls (<= kSmallPlanChunks chunks): the stats reset, the tile memset,
+// b3_plan, b3_small_scatter and b3_fill_group_chunk in ONE workgroup -- the
+// scan, the histogram, the bucket starts and the group -> chunk map all live
+// in LDS, so five dispatches (~5 us each, mostly empty) become one.  Same
+// outputs as the grid path: groups[0..n], small[] (bucket order), *nsmall,
+// gchunk[0..min(groups[n], cap_g)).
+constexpr int kSmallPlanThreads = 1024;
+static_assert(kSmallPlanChunks == (uint64_t)kSmallPlanThreads * kPlanItems, "one item set");
+
+__device__ __forceinline__ uint64_t block1024_exclusive_scan(uint64_t v, uint64_t *wsum,
+                                                             uint64_t *total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kSmallPlanThreads / 64; ++w) {
+    if (w < wid) pre += wsum[w];
+    tot += wsum[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+__global__ __launch_bounds__(kSmallPlanThreads) void b3_plan_small(
+    const ngpu_chunk *__restrict__ chunks, uint64_t n, int D, uint64_t *__restrict__ groups,
+    uint32_t *__restrict__ small, uint32_t *__restrict__ gchunk, uint64_t cap_g,
+    uint64_t *__restrict__ stats) {
+  __shared__ uint32_t h[kMaxKey + 1], cur[kMaxKey + 1], base[kMaxKey + 1];
+  __shared__ uint64_t gpre[kSmallPlanChunks + 1], wsum[kSmallPlanThreads / 64];
+  const int t = threadIdx.x;
+  if (t < 16) stats[t] = 0;  // the call's device counters (nsmall rewritten below)
+  for (int i = t; i <= kMaxKey; i += kSmallPlanThreads) h[i] = cur[i] = 0;
+  __syncthreads();
+  const uint64_t c0 = (uint64_t)t * kPlanItems;
+  uint64_t g[kPlanItems], sum = 0;
+  uint32_t key[kPlanItems];
+#pragma unroll
+  for (int i = 0; i < kPlanItems; ++i) {
+    const uint64_t c = c0 + i;
+    g[i] = 0;
+    key[i] = 0;
+    if (c < n) {
+      const uint32_t len = chunks[c].length;
+      key[i] = small_key(chunks[c], D);
+      if (key[i]) atomicAdd(&h[key[i]], 1u);
+      else g[i] = (((len + kLeaf - 1) / kLeaf) + (1u << D) - 1) >> D;
+    }
+    sum += g[i];
+  }
+  uint64_t tot;
+  uint64_t run = block1024_exclusive_scan(sum, wsum, &tot);  // its barriers publish h
+#pragma unroll
+  for (int i = 0; i < kPlanItems; ++i) {
+    const uint64_t c = c0 + i;
+    if (c < n) groups[c] = gpre[c] = run;
+    run += g[i];
+    if (c + 1 == n) groups[n] = gpre[n] = run;
+  }
+  // bucket starts, largest block count first (keys kMaxKey .. 1 on threads 0 ..)
+  const uint32_t bkey = kMaxKey - t;
+  const uint64_t start = block1024_exclusive_scan(t < kMaxKey ? h[bkey] : 0, wsum, &tot);
+  if (t < kMaxKey) base[bkey] = (uint32_t)start;
+  if (t == 0) stats[10] = tot;  // nsmall
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kPlanItems; ++i)
+    if (key[i]) small[base[key[i]] + atomicAdd(&cur[key[i]], 1u)] = (uint32_t)(c0 + i);
+  // group -> chunk: the chunk c with gpre[c] <= g < gpre[c + 1]
+  const uint64_t G = gpre[n] < cap_g ? gpre[n] : cap_g;
+  for (uint64_t gg = t; gg < G; gg += kSmallPlanThreads) {
+    uint64_t lo = 0, hi = n;  // gpre[lo] <= gg < gpre[hi]
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (gpre[mid] <= gg) lo = mid;
+      else hi = mid;
+    }
+    gchunk[gg] = (uint32_t)lo;
   }
 }
 
@@ -712,24 +802,26 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
 template <int D, int LM>
 static void launch_groups_lm(const uint8_t *data, uint64_t data_len,
                              const ngpu_chunk *chunks, uint64_t n, Workspace &ws,
-                             ngpu_result *out, hipStream_t s) {
+                             ngpu_result *out, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const uint64_t blocks = (ws.cap_g + 255) / 256;
-  hipLaunchKernelGGL((b3_groups<D, LM>), dim3((unsigned)blocks), dim3(256), 0, s, data,
-                     data_len, chunks, n, ws.groups, ws.group_chunk, ws.cap_g,
-                     ws.cv, out, ws.stats + 7, ws.small, ws.stats + 10, ws.tree_list);
+  hipExtLaunchKernelGGL((b3_groups<D, LM>), dim3((unsigned)blocks), dim3(256), 0, s, e0, e1, 0,
+                        data, data_len, chunks, n, (const uint64_t *)ws.groups,
+                        (const uint32_t *)ws.group_chunk, ws.cap_g, ws.cv, out, ws.stats + 7,
+                        (const uint32_t *)ws.small, (const uint64_t *)(ws.stats + 10),
+                        ws.tree_list);
 }
 
 template <int D>
 static void launch_groups(const uint8_t *data, uint64_t data_len,
                           const ngpu_chunk *chunks, uint64_t n, Workspace &ws,
-                          ngpu_result *out, hipStream_t s) {
+                          ngpu_result *out, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   switch (ws.load_mode) {
-    case 0: launch_groups_lm<D, 0>(data, data_len, chunks, n, ws, out, s); break;
-    case 1: launch_groups_lm<D, 1>(data, data_len, chunks, n, ws, out, s); break;
-    case 2: launch_groups_lm<D, 2>(data, data_len, chunks, n, ws, out, s); break;
-    case 3: launch_groups_lm<D, 3>(data, data_len, chunks, n, ws, out, s); break;
-    case 5: launch_groups_lm<D, 5>(data, data_len, chunks, n, ws, out, s); break;
-    default: launch_groups_lm<D, 4>(data, data_len, chunks, n, ws, out, s); break;
+    case 0: launch_groups_lm<D, 0>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
+    case 1: launch_groups_lm<D, 1>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
+    case 2: launch_groups_lm<D, 2>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
+    case 3: launch_groups_lm<D, 3>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
+    case 5: launch_groups_lm<D, 5>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
+    default: launch_groups_lm<D, 4>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
   }
 }
 
@@ -738,22 +830,29 @@ uint64_t blake3_max_groups(uint64_t n, uint64_t data_len, int D) {
   return n + ((data_len / kLeaf + n) >> D) + 1;
 }
 
-void launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
+bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
                    uint64_t data_len, int D, Workspace &ws, ngpu_result *out,
-                   hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_end) {
-  if (n == 0) return;
-  {
-    // histogram + cursors + plan ticket + this call's tile words, one memset
+                   hipStream_t s, hipEvent_t ev_first, hipEvent_t ev_start, hipEvent_t ev_end_groups,
+                   hipEvent_t ev_end) {
+  if (n == 0) {
+    (void)hipMemsetAsync(ws.stats, 0, 16 * sizeof(uint64_t), s);
+    return false;
+  }
+  if (!ws.grid_stages && n <= kSmallPlanChunks) {
+    hipExtLaunchKernelGGL(b3_plan_small, dim3(1), dim3(kSmallPlanThreads), 0, s, ev_first, nullptr,
+                          0, chunks, n, D, ws.groups, ws.small, ws.group_chunk, ws.cap_g, ws.stats);
+  } else {
+    // the call's device counters; histogram + cursors + plan ticket + this
+    // call's tile words, one memset
+    (void)hipMemsetAsync(ws.stats, 0, 16 * sizeof(uint64_t), s);
     const uint64_t nt = (n + kPlanTile - 1) / kPlanTile;
     uint32_t *hist = reinterpret_cast<uint32_t *>(ws.tstat), *cursor = hist + (kMaxKey + 1);
     uint64_t *ts = ws.tstat + kB3Ts;
     (void)hipMemsetAsync(ws.tstat, 0, (kB3Ts + 1 + nt) * sizeof(uint64_t), s);
-    hipLaunchKernelGGL(b3_plan, dim3((unsigned)nt), dim3(kTileThreads), 0, s, chunks, n, D,
-                       ws.groups, hist, ts);
+    hipExtLaunchKernelGGL(b3_plan, dim3((unsigned)nt), dim3(kTileThreads), 0, s, ev_first, nullptr,
+                          0, chunks, n, D, ws.groups, hist, ts);
     hipLaunchKernelGGL(b3_small_scatter, dim3((unsigned)nt), dim3(kTileThreads), 0, s, chunks, n,
-                       D, hist, cursor, ws.small, ws.stats + 10);
-  }
-  {
+                       D, (const uint32_t *)hist, cursor, ws.small, ws.stats + 10);
     // lanes per chunk: the groups a chunk of the average size has, 1..64
     const uint64_t per = data_len / (n * ((uint64_t)kLeaf << D)) + 1;
     uint32_t W = 1;
@@ -762,22 +861,20 @@ void launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
     const uint64_t waves = waves_needed < 16384 ? waves_needed : 16384;
     const uint64_t blocks = (waves * 64 + 255) / 256;
     hipLaunchKernelGGL(b3_fill_group_chunk, dim3((unsigned)blocks), dim3(256), 0,
-                       s, ws.groups, n, ws.group_chunk, ws.cap_g, W);
+                       s, (const uint64_t *)ws.groups, n, ws.group_chunk, ws.cap_g, W);
   }
-  if (ev_start) (void)hipEventRecord(ev_start, s);
   switch (D) {
-    case 0: launch_groups<0>(data, data_len, chunks, n, ws, out, s); break;
-    case 1: launch_groups<1>(data, data_len, chunks, n, ws, out, s); break;
-    case 2: launch_groups<2>(data, data_len, chunks, n, ws, out, s); break;
-    case 3: launch_groups<3>(data, data_len, chunks, n, ws, out, s); break;
-    default: launch_groups<4>(data, data_len, chunks, n, ws, out, s); break;
+    case 0: launch_groups<0>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
+    case 1: launch_groups<1>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
+    case 2: launch_groups<2>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
+    case 3: launch_groups<3>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
+    default: launch_groups<4>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
   }
-  if (ev_end) (void)hipEventRecord(ev_end, s);
-  {
-    uint64_t blocks = n < 2048 ? n : 2048;
-    hipLaunchKernelGGL(b3_tree, dim3((unsigned)blocks), dim3(kTreeThreads), 0, s,
-                       ws.groups, ws.tree_list, ws.stats + 9, ws.cap_g, ws.cv, out);
-  }
+  const uint64_t blocks = n < 2048 ? n : 2048;
+  hipExtLaunchKernelGGL(b3_tree, dim3((unsigned)blocks), dim3(kTreeThreads), 0, s, nullptr, ev_end,
+                        0, (const uint64_t *)ws.groups, (const uint32_t *)ws.tree_list,
+                        (const uint64_t *)(ws.stats + 9), ws.cap_g, ws.cv, out);
+  return true;
 }
 
 }  // namespace ngpu

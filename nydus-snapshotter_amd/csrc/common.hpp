@@ -155,12 +155,22 @@ __host__ __device__ constexpr uint64_t tstat_words(uint64_t nt) {
 // ---- launchers (defined in the .hip files) --------------------------------
 struct Workspace;
 
-// blake3.hip
-// ev_groups (may be null): recorded right after the leaf-group kernel.
-void launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
+// Calls with at most this many chunks (and layers) plan their BLAKE3 groups
+// and run their dedup stage in one fused workgroup each (dispatch cost: one
+// launch instead of four and six); Workspace::grid_stages turns this off.
+constexpr uint64_t kSmallPlanChunks = 4096;
+constexpr uint64_t kSmallDedupChunks = 4096;
+constexpr uint64_t kSmallDedupLayers = 64;
+
+// blake3.hip.  Events (each may be null) ride on the kernels themselves
+// (hipExtLaunchKernelGGL start/stop), so timing and stream ordering add no
+// marker packets: ev_first = start of the first kernel, ev_groups_* = the
+// leaf-group kernel, ev_end = end of the stage.  Returns false when nothing
+// was launched (n == 0: ev_end was not recorded).
+bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
                    uint64_t data_len, int group_log2, Workspace &ws,
-                   ngpu_result *out, hipStream_t s, hipEvent_t ev_groups_start,
-                   hipEvent_t ev_groups_end);
+                   ngpu_result *out, hipStream_t s, hipEvent_t ev_first,
+                   hipEvent_t ev_groups_start, hipEvent_t ev_groups_end, hipEvent_t ev_end);
 uint64_t blake3_max_groups(uint64_t n, uint64_t data_len, int group_log2);
 // sha256.hip
 void launch_sha256(const uint8_t *data, uint64_t data_len,
@@ -196,10 +206,11 @@ void launch_dict_build(const DictRec *rec, uint64_t m, uint64_t *table, uint64_t
 // n_blobs: inner blobs of the (global) dict.  L layers; layer l owns chunks
 // [lfirst[l], lfirst[l+1]) (device array; nullptr = one layer, {0, n} is
 // written to ws.lfirst1); st: device ngpu_layer_stats[L].
+// ev_end (may be null): recorded by the stage's last kernel.
 void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                   const ngpu_dict_hit *hits, uint32_t n_blobs, uint32_t align,
                   const uint64_t *lfirst, uint64_t L, Workspace &ws, ngpu_result *out,
-                  ngpu_layer_stats *st, hipStream_t s);
+                  ngpu_layer_stats *st, hipStream_t s, hipEvent_t ev_end);
 void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
                        const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s);
 // Node dict exchange (node.hip): pack n digests (byte stride) to 32-B rows;
@@ -248,6 +259,7 @@ struct Workspace {
   ngpu_dict_hit *xparts = nullptr, *xhits = nullptr;
   uint64_t cap_x = 0, cap_xparts = 0;
   int load_mode = 0;              // b3_groups load mode (see blake3.hip)
+  bool grid_stages = false;       // NGPU_FLAG_GRID_STAGES: no fused small-call path
 };
 
 }  // namespace ngpu

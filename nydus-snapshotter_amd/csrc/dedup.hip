@@ -21,6 +21,8 @@
 // Roofline: HBM-bound probes.
 #include <stddef.h>
 
+#include <hip/hip_ext.h>
+
 #include "common.hpp"
 
 namespace ngpu {
@@ -166,17 +168,27 @@ __device__ __forceinline__ uint64_t layer_bucket(const uint32_t *d, uint32_t lay
 // and the scan tiles, and fill chunk -> layer (binary search in first[0..L]:
 // the last layer whose first chunk <= c, so empty layers are skipped).
 // single != nullptr: one layer; {0, n} is written there for the later stages.
-__global__ void dedup_init(const uint64_t *__restrict__ first, uint64_t L, uint64_t n,
-                           uint64_t *__restrict__ single, uint32_t *__restrict__ chunk_layer,
-                           uint32_t *__restrict__ blob_first, uint64_t nbf,
-                           uint64_t *__restrict__ st_words, uint64_t nst,
-                           uint64_t *__restrict__ intra, uint64_t icap,
-                           uint64_t *__restrict__ tiles, uint64_t ntw,
-                           uint64_t *__restrict__ newidx, uint64_t *__restrict__ uoff,
-                           uint64_t *__restrict__ nbytes, uint64_t *__restrict__ ndict,
-                           uint64_t total) {
-  const uint64_t stride = gridDim.x * (uint64_t)blockDim.x;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += stride) {
+struct DedupInit {
+  const uint64_t *first;
+  uint64_t L, n;
+  uint64_t *single;
+  uint32_t *chunk_layer, *blob_first;
+  uint64_t nbf;
+  uint64_t *st_words;
+  uint64_t nst;
+  uint64_t *intra, icap, *tiles, ntw;
+  uint64_t *newidx, *uoff, *nbytes, *ndict;
+  uint64_t total;
+};
+
+__device__ __forceinline__ void init_item(const DedupInit &a, uint64_t i) {
+  const uint64_t *first = a.first;
+  const uint64_t L = a.L, n = a.n, nbf = a.nbf, nst = a.nst, icap = a.icap, ntw = a.ntw;
+  uint64_t *single = a.single;
+  uint32_t *chunk_layer = a.chunk_layer, *blob_first = a.blob_first;
+  uint64_t *st_words = a.st_words, *intra = a.intra, *tiles = a.tiles;
+  uint64_t *newidx = a.newidx, *uoff = a.uoff, *nbytes = a.nbytes, *ndict = a.ndict;
+  {
     if (i < nbf) blob_first[i] = kNone;
     if (i < nst) st_words[i] = 0;
     if (i < icap) intra[i] = kEmpty;
@@ -201,6 +213,12 @@ __global__ void dedup_init(const uint64_t *__restrict__ first, uint64_t L, uint6
       if (single) { single[0] = 0; single[1] = n; }
     }
   }
+}
+
+__global__ void dedup_init(DedupInit a) {
+  const uint64_t stride = gridDim.x * (uint64_t)blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.total; i += stride)
+    init_item(a, i);
 }
 
 // atomicMin(base[key], v) for the lanes with act set.  Lanes of a wave
@@ -231,13 +249,12 @@ __device__ __forceinline__ bool same_key(const ngpu_result *out, const uint32_t 
 // a chunk the dict does not take goes into the intra-layer table (CAS into an
 // empty slot, or atomic MIN over the slot holding the same (layer, digest):
 // the first occurrence wins for any schedule).
-__global__ void dedup_probe_insert(const ngpu_chunk *__restrict__ chunks, uint64_t n,
-                                   DictDevice dict, const ngpu_dict_hit *__restrict__ hits,
-                                   const uint32_t *__restrict__ chunk_layer,
-                                   ngpu_result *__restrict__ out,
-                                   uint32_t *__restrict__ blob_first, uint32_t n_blobs,
-                                   uint64_t *__restrict__ table, uint64_t mask) {
-  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+// Every lane of the wave must call this (wave_min_u32); c >= n: no chunk.
+__device__ __forceinline__ void probe_insert_item(
+    uint64_t c, const ngpu_chunk *__restrict__ chunks, uint64_t n, const DictDevice &dict,
+    const ngpu_dict_hit *__restrict__ hits, const uint32_t *__restrict__ chunk_layer,
+    ngpu_result *__restrict__ out, uint32_t *__restrict__ blob_first, uint32_t n_blobs,
+    uint64_t *__restrict__ table, uint64_t mask) {
   const bool live = c < n;
   uint32_t d[8] = {};
   uint32_t layer = 0;
@@ -285,18 +302,25 @@ __global__ void dedup_probe_insert(const ngpu_chunk *__restrict__ chunks, uint64
   }
 }
 
+__global__ void dedup_probe_insert(const ngpu_chunk *__restrict__ chunks, uint64_t n,
+                                   DictDevice dict, const ngpu_dict_hit *__restrict__ hits,
+                                   const uint32_t *__restrict__ chunk_layer,
+                                   ngpu_result *__restrict__ out,
+                                   uint32_t *__restrict__ blob_first, uint32_t n_blobs,
+                                   uint64_t *__restrict__ table, uint64_t mask) {
+  probe_insert_item(blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, chunks, n, dict, hits,
+                    chunk_layer, out, blob_first, n_blobs, table, mask);
+}
+
 // Stage 2: INTRA / NEW per chunk.  Writes the four per-chunk quantities the
 // scan turns into prefixes: NEW flag, v6-aligned size, NEW bytes, DICT flag.
 // Per-layer figures are differences of these prefixes at layer boundaries,
 // so no per-layer atomics are needed anywhere.
-__global__ void dedup_resolve(const ngpu_chunk *__restrict__ chunks, uint64_t n,
-                              const uint32_t *__restrict__ chunk_layer,
-                              const uint64_t *__restrict__ table, uint64_t mask,
-                              ngpu_result *__restrict__ out, uint32_t align,
-                              uint64_t *__restrict__ newidx, uint64_t *__restrict__ uoff,
-                              uint64_t *__restrict__ nbytes, uint64_t *__restrict__ ndict) {
-  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c >= n) return;
+__device__ __forceinline__ void resolve_item(
+    uint64_t c, const ngpu_chunk *__restrict__ chunks, const uint32_t *__restrict__ chunk_layer,
+    const uint64_t *__restrict__ table, uint64_t mask, ngpu_result *__restrict__ out,
+    uint32_t align, uint64_t *__restrict__ newidx, uint64_t *__restrict__ uoff,
+    uint64_t *__restrict__ nbytes, uint64_t *__restrict__ ndict) {
   uint64_t v[kDedupScans] = {0, 0, 0, 0};  // NEW, aligned size, bytes, DICT
   ngpu_result &r = out[c];
   const uint32_t layer = chunk_layer[c];
@@ -331,6 +355,17 @@ __global__ void dedup_resolve(const ngpu_chunk *__restrict__ chunks, uint64_t n,
   uoff[c] = v[1];
   nbytes[c] = v[2];
   ndict[c] = v[3];
+}
+
+__global__ void dedup_resolve(const ngpu_chunk *__restrict__ chunks, uint64_t n,
+                              const uint32_t *__restrict__ chunk_layer,
+                              const uint64_t *__restrict__ table, uint64_t mask,
+                              ngpu_result *__restrict__ out, uint32_t align,
+                              uint64_t *__restrict__ newidx, uint64_t *__restrict__ uoff,
+                              uint64_t *__restrict__ nbytes, uint64_t *__restrict__ ndict) {
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (c < n)
+    resolve_item(c, chunks, chunk_layer, table, mask, out, align, newidx, uoff, nbytes, ndict);
 }
 
 // Stage 3: the four arrays -> exclusive prefixes over the whole call, in
@@ -389,13 +424,18 @@ __global__ __launch_bounds__(kTileThreads) void dedup_scan(
 // The first NEW chunk is found by binary search on the NEW-index scan (the
 // smallest c in the layer with newidx[c + 1] > newidx[first]); the layer
 // stats are differences of the scans at the layer's ends.
-__global__ void blob_rank(uint32_t *__restrict__ first_all, uint32_t nbo,
-                          uint32_t *__restrict__ real_all, const uint64_t *__restrict__ lfirst,
-                          const uint64_t *__restrict__ newidx, const uint64_t *__restrict__ uoff,
-                          const uint64_t *__restrict__ nbytes, const uint64_t *__restrict__ ndict,
-                          ngpu_layer_stats *__restrict__ st) {
-  __shared__ uint32_t fl[1024];
-  const uint64_t l = blockIdx.x;
+// One workgroup (any multiple of 64 threads) ranks layer l; fl: 1024 words
+// of LDS, used_all: one LDS word.
+__device__ void blob_rank_layer(uint64_t l, uint32_t *__restrict__ first_all, uint32_t nbo,
+                                uint32_t *__restrict__ real_all,
+                                const uint64_t *__restrict__ lfirst,
+                                const uint64_t *__restrict__ newidx,
+                                const uint64_t *__restrict__ uoff,
+                                const uint64_t *__restrict__ nbytes,
+                                const uint64_t *__restrict__ ndict,
+                                ngpu_layer_stats *__restrict__ st, uint32_t *fl,
+                                uint32_t *used_all_p) {
+  uint32_t &used_all = *used_all_p;
   uint32_t *first = first_all + l * nbo;
   uint32_t *real = real_all + l * nbo;
   const uint64_t a = lfirst[l], e = lfirst[l + 1];
@@ -441,7 +481,6 @@ __global__ void blob_rank(uint32_t *__restrict__ first_all, uint32_t nbo,
     }
     real[b] = rank;
   }
-  __shared__ uint32_t used_all;
   if (threadIdx.x == 0) used_all = 0;
   __syncthreads();
   if (used) atomicAdd(&used_all, used);
@@ -461,14 +500,22 @@ __global__ void blob_rank(uint32_t *__restrict__ first_all, uint32_t nbo,
   }
 }
 
-__global__ void dedup_finalize(const uint64_t n, const uint32_t *__restrict__ chunk_layer,
-                               const uint64_t *__restrict__ lfirst,
-                               const uint64_t *__restrict__ newidx,
-                               const uint64_t *__restrict__ uoff,
-                               const uint32_t *__restrict__ real_all, uint32_t nbo,
-                               ngpu_result *__restrict__ out) {
-  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c >= n) return;
+__global__ void blob_rank(uint32_t *__restrict__ first_all, uint32_t nbo,
+                          uint32_t *__restrict__ real_all, const uint64_t *__restrict__ lfirst,
+                          const uint64_t *__restrict__ newidx, const uint64_t *__restrict__ uoff,
+                          const uint64_t *__restrict__ nbytes, const uint64_t *__restrict__ ndict,
+                          ngpu_layer_stats *__restrict__ st) {
+  __shared__ uint32_t fl[1024], used_all;
+  blob_rank_layer(blockIdx.x, first_all, nbo, real_all, lfirst, newidx, uoff, nbytes, ndict, st,
+                  fl, &used_all);
+}
+
+__device__ __forceinline__ void finalize_item(uint64_t c, const uint32_t *__restrict__ chunk_layer,
+                                              const uint64_t *__restrict__ lfirst,
+                                              const uint64_t *__restrict__ newidx,
+                                              const uint64_t *__restrict__ uoff,
+                                              const uint32_t *__restrict__ real_all, uint32_t nbo,
+                                              ngpu_result *__restrict__ out) {
   ngpu_result &r = out[c];
   const uint32_t layer = chunk_layer[c];
   const uint32_t *real = real_all + (uint64_t)layer * nbo;
@@ -487,6 +534,94 @@ __global__ void dedup_finalize(const uint64_t n, const uint32_t *__restrict__ ch
   } else {
     r.blob_index = real[r.blob_index];
   }
+}
+
+__global__ void dedup_finalize(const uint64_t n, const uint32_t *__restrict__ chunk_layer,
+                               const uint64_t *__restrict__ lfirst,
+                               const uint64_t *__restrict__ newidx,
+                               const uint64_t *__restrict__ uoff,
+                               const uint32_t *__restrict__ real_all, uint32_t nbo,
+                               ngpu_result *__restrict__ out) {
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (c < n) finalize_item(c, chunk_layer, lfirst, newidx, uoff, real_all, nbo, out);
+}
+
+// ---- small calls: the whole dedup stage in ONE workgroup -----------------------
+// A layer of a few thousand chunks (C1: 108) spends ~5 us per launch of the
+// six stage kernels above on nothing but dispatch; here the stages run back
+// to back inside one 1024-thread workgroup, with barriers between them and
+// plain block scans instead of the tile look-back.  The per-chunk work is the
+// same device code, so decisions are identical by construction (and by the
+// parity tests, which force both paths).  Phases hand data over through
+// global memory within ONE workgroup, so the barrier's workgroup-scope
+// acquire/release is the whole synchronisation (all waves share the CU's
+// vector L1; the hash-table atomics run at L2).  An agent-scope fence here
+// would write back and invalidate the L2 at every phase (buffer_wbl2 /
+// buffer_inv sc1): measured 29 us per call instead of ~10.
+constexpr uint32_t kSmallThreads = 1024;
+constexpr uint32_t kSmallItems = 4;
+
+__device__ __forceinline__ void small_phase_end() { __syncthreads(); }
+
+__global__ __launch_bounds__(kSmallThreads) void dedup_small(
+    DedupInit a, const ngpu_chunk *__restrict__ chunks, DictDevice dict,
+    const ngpu_dict_hit *__restrict__ hits, uint32_t n_blobs, uint32_t align,
+    const uint64_t *__restrict__ lfirst, uint32_t *__restrict__ blob_real,
+    ngpu_layer_stats *__restrict__ st, ngpu_result *__restrict__ out) {
+  __shared__ uint32_t fl[1024], used_all;
+  __shared__ uint64_t wsum[kSmallThreads / 64];
+  const uint64_t n = a.n, mask = a.icap - 1;
+  const uint32_t nbo = n_blobs + 1;
+  for (uint64_t i = threadIdx.x; i < a.total; i += kSmallThreads) init_item(a, i);
+  small_phase_end();
+  const uint64_t n_up = (n + kSmallThreads - 1) / kSmallThreads * kSmallThreads;
+  for (uint64_t c = threadIdx.x; c < n_up; c += kSmallThreads)  // whole waves: wave_min_u32
+    probe_insert_item(c, chunks, n, dict, hits, a.chunk_layer, out, a.blob_first, n_blobs, a.intra,
+                      mask);
+  small_phase_end();
+  for (uint64_t c = threadIdx.x; c < n; c += kSmallThreads)
+    resolve_item(c, chunks, a.chunk_layer, a.intra, mask, out, align, a.newidx, a.uoff, a.nbytes,
+                 a.ndict);
+  small_phase_end();
+  // exclusive scans of the four arrays (n <= kSmallThreads * kSmallItems)
+  uint64_t *arr[kDedupScans] = {a.newidx, a.uoff, a.nbytes, a.ndict};
+  const uint64_t c0 = (uint64_t)threadIdx.x * kSmallItems;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int k = 0; k < kDedupScans; ++k) {
+    uint64_t v[kSmallItems], sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kSmallItems; ++i) {
+      v[i] = c0 + i < n ? arr[k][c0 + i] : 0;
+      sum += v[i];
+    }
+    uint64_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint64_t run = x - sum;
+    for (int w = 0; w < wid; ++w) run += wsum[w];
+#pragma unroll
+    for (uint32_t i = 0; i < kSmallItems; ++i) {
+      const uint64_t c = c0 + i;
+      if (c < n) arr[k][c] = run;
+      run += v[i];
+      if (c + 1 == n) arr[k][n] = run;
+    }
+    __syncthreads();  // wsum reused by the next array
+  }
+  small_phase_end();
+  for (uint64_t l = 0; l < a.L; ++l) {
+    blob_rank_layer(l, a.blob_first, nbo, blob_real, lfirst, a.newidx, a.uoff, a.nbytes, a.ndict,
+                    st, fl, &used_all);
+    __syncthreads();  // fl / used_all reused by the next layer
+  }
+  small_phase_end();
+  for (uint64_t c = threadIdx.x; c < n; c += kSmallThreads)
+    finalize_item(c, a.chunk_layer, lfirst, a.newidx, a.uoff, blob_real, nbo, out);
 }
 
 }  // namespace
@@ -590,7 +725,7 @@ void launch_dict_pack(const uint8_t *digests, const uint32_t *usize, const uint3
 void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                   const ngpu_dict_hit *hits, uint32_t n_blobs, uint32_t align,
                   const uint64_t *lfirst, uint64_t L, Workspace &ws, ngpu_result *out,
-                  ngpu_layer_stats *st, hipStream_t s) {
+                  ngpu_layer_stats *st, hipStream_t s, hipEvent_t ev_end) {
   const uint32_t nbo = n_blobs + 1;  // dict blobs + own blob (last slot), per layer
   uint64_t *single = nullptr;
   if (!lfirst) {
@@ -598,17 +733,25 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
     lfirst = ws.lfirst1;
     L = 1;
   }
+  const bool small = !ws.grid_stages && n <= kSmallDedupChunks && L <= kSmallDedupLayers;
   const uint64_t nt = (n + kScanTile - 1) / kScanTile;
   uint64_t *ts = ws.tstat + kDedupTs(ws.tiles);
   const uint64_t nbf = (uint64_t)nbo * L, nst = L * (sizeof(ngpu_layer_stats) / 8);
-  const uint64_t icap = n ? ws.intra_cap : 0, ntw = 1 + kDedupScans * ws.tiles;
+  // the small path scans in LDS: no tile words to reset
+  const uint64_t icap = n ? ws.intra_cap : 0, ntw = small ? 0 : 1 + kDedupScans * ws.tiles;
   uint64_t total = n + 1;
   for (uint64_t v : {nbf, nst, icap, ntw}) total = v > total ? v : total;
+  const DedupInit a{lfirst, L, n, single, ws.chunk_layer, ws.blob_first, nbf,
+                    reinterpret_cast<uint64_t *>(st), nst, ws.intra, icap, ts, ntw,
+                    ws.newflag, ws.uoff, ws.nbytes, ws.ndict, total};
+  if (small) {
+    static_assert(kSmallDedupChunks <= kSmallThreads * kSmallItems, "one scan pass");
+    hipExtLaunchKernelGGL(dedup_small, dim3(1), dim3(kSmallThreads), 0, s, nullptr, ev_end, 0, a,
+                          chunks, dict, hits, n_blobs, align, lfirst, ws.blob_real, st, out);
+    return;
+  }
   const uint64_t ib = (total + 255) / 256;
-  hipLaunchKernelGGL(dedup_init, dim3((unsigned)(ib < 4096 ? ib : 4096)), dim3(256), 0, s,
-                     lfirst, L, n, single, ws.chunk_layer, ws.blob_first, nbf,
-                     reinterpret_cast<uint64_t *>(st), nst, ws.intra, icap, ts, ntw,
-                     ws.newflag, ws.uoff, ws.nbytes, ws.ndict, total);
+  hipLaunchKernelGGL(dedup_init, dim3((unsigned)(ib < 4096 ? ib : 4096)), dim3(256), 0, s, a);
   if (n) {
     const unsigned blocks = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(dedup_probe_insert, dim3(blocks), dim3(256), 0, s, chunks, n, dict, hits,
@@ -619,11 +762,16 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
     hipLaunchKernelGGL(dedup_scan, dim3((unsigned)nt), dim3(kTileThreads), 0, s, n, ws.newflag,
                        ws.uoff, ws.nbytes, ws.ndict, ts, ws.tiles);
   }
-  hipLaunchKernelGGL(blob_rank, dim3((unsigned)L), dim3(256), 0, s, ws.blob_first, nbo,
-                     ws.blob_real, lfirst, ws.newflag, ws.uoff, ws.nbytes, ws.ndict, st);
+  // the stage's last kernel carries the end event (no separate marker packet)
+  hipExtLaunchKernelGGL(blob_rank, dim3((unsigned)L), dim3(256), 0, s, nullptr,
+                        n ? nullptr : ev_end, 0, ws.blob_first, nbo, ws.blob_real, lfirst,
+                        (const uint64_t *)ws.newflag, (const uint64_t *)ws.uoff,
+                        (const uint64_t *)ws.nbytes, (const uint64_t *)ws.ndict, st);
   if (n)
-    hipLaunchKernelGGL(dedup_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
-                       ws.chunk_layer, lfirst, ws.newflag, ws.uoff, ws.blob_real, nbo, out);
+    hipExtLaunchKernelGGL(dedup_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                          nullptr, ev_end, 0, n, (const uint32_t *)ws.chunk_layer, lfirst,
+                          (const uint64_t *)ws.newflag, (const uint64_t *)ws.uoff,
+                          (const uint32_t *)ws.blob_real, nbo, out);
 }
 
 }  // namespace ngpu

@@ -129,12 +129,18 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
 }
 
 int ws_acquire(ngpu_engine *e, hipStream_t s) {
-  if (e->ws_pending && e->ws_last != s) HIP_TRY(e, hipStreamWaitEvent(s, e->ws_done, 0));
+  if (e->ws_pending && e->ws_last != s) HIP_TRY(e, hipStreamWaitEvent(s, e->ws_last_ev, 0));
   return 0;
 }
 
-int ws_release(ngpu_engine *e, hipStream_t s) {
-  HIP_TRY(e, hipEventRecord(e->ws_done, s));
+// bound: an event the stage's last kernel already records at its end (a
+// stop event of hipExtLaunchKernelGGL), or null to record ws_done now.
+int ws_release(ngpu_engine *e, hipStream_t s, hipEvent_t bound) {
+  if (!bound) {
+    HIP_TRY(e, hipEventRecord(e->ws_done, s));
+    bound = e->ws_done;
+  }
+  e->ws_last_ev = bound;
   e->ws_last = s;
   e->ws_pending = true;
   return 0;
@@ -158,23 +164,30 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
     ev = e->ev[e->tslot];
     e->timed[e->tslot] = false;
     e->slot_D[e->tslot] = D;
-    HIP_TRY(e, hipEventRecord(ev[0], s));
   }
-  HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 16 * sizeof(uint64_t), s));
+  hipEvent_t bound = nullptr;  // the stage-end event a kernel records
   if (e->cfg.digester == NGPU_DIGEST_SHA256) {
+    if (tm) HIP_TRY(e, hipEventRecord(ev[0], s));
+    HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 16 * sizeof(uint64_t), s));
     if (tm) HIP_TRY(e, hipEventRecord(ev[1], s));
     // tuning override: flags bits 11..13 = 1 + SHA-256 variant (0 split,
-    // 1 pair, 2/3 pair diagnostics)
+    // 1 pair, 4/5 pair layouts)
     const uint32_t sv = (e->cfg.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7;
     launch_sha256(d_data, len, d_chunks, n, d_out, e->ws.stats + 7, sv ? (int)sv - 1 : -1, s);
-    if (tm) HIP_TRY(e, hipEventRecord(ev[2], s));
+    if (tm) {
+      HIP_TRY(e, hipEventRecord(ev[2], s));
+      HIP_TRY(e, hipEventRecord(ev[3], s));
+      bound = ev[3];
+    }
   } else {
-    launch_blake3(d_data, d_chunks, n, len, D, e->ws, d_out, s, tm ? ev[1] : nullptr,
-                  tm ? ev[2] : nullptr);
+    // events ride on the kernels: no marker packets between the launches
+    hipEvent_t end = tm ? ev[3] : e->ws_done;
+    if (launch_blake3(d_data, d_chunks, n, len, D, e->ws, d_out, s, tm ? ev[0] : nullptr,
+                      tm ? ev[1] : nullptr, tm ? ev[2] : nullptr, end))
+      bound = end;
   }
-  if (tm) HIP_TRY(e, hipEventRecord(ev[3], s));
   HIP_TRY(e, hipGetLastError());
-  if ((rc = ws_release(e, s))) return rc;
+  if ((rc = ws_release(e, s, bound))) return rc;
   return 0;
 }
 
@@ -200,12 +213,13 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chu
   const uint32_t align =
       (e->cfg.fs_version == 6 || (e->cfg.flags & NGPU_FLAG_ALIGNED_CHUNK)) ? 4096u : 1u;
   // d_lfirst == nullptr: the init kernel writes {0, n} into ws.lfirst1
+  // the last dedup kernel records the stage end (timing slot or ws_done)
+  hipEvent_t end = tm && e->tcalls ? e->ev[e->tslot][4] : e->ws_done;
   launch_dedup(d_chunks, n, dict ? dict->dev : DictDevice{}, d_hits, n_blobs, align, d_lfirst, L,
-               e->ws, d_out, d_stats, s);
-  if (tm && e->tcalls) HIP_TRY(e, hipEventRecord(e->ev[e->tslot][4], s));
+               e->ws, d_out, d_stats, s, end);
   HIP_TRY(e, hipGetLastError());
   if (tm && e->tcalls) e->timed[e->tslot] = n > 0;
-  if ((rc = ws_release(e, s))) return rc;
+  if ((rc = ws_release(e, s, end))) return rc;
   return 0;
 }
 
@@ -303,6 +317,7 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NGPU_ENODEV;
   ngpu_engine *e = new ngpu_engine();
   e->cfg = c;
+  e->ws.grid_stages = (c.flags & NGPU_FLAG_GRID_STAGES) != 0;
   e->device = c.device;
   DeviceGuard dg(c.device);
   if (c.flags & NGPU_FLAG_TIMING)

@@ -79,6 +79,7 @@ struct ngpu_engine {
   // ws_done on its stream; a stage on another stream waits for it first, so
   // calls on different streams never run over one workspace concurrently.
   hipEvent_t ws_done = nullptr;
+  hipEvent_t ws_last_ev = nullptr;  // the event that ended the last stage
   hipStream_t ws_last = nullptr;
   bool ws_pending = false;
   std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu
@@ -104,7 +105,8 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chu
 int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st);
 // Order a workspace stage on stream s after the previous one (any stream).
 int ws_acquire(ngpu_engine *e, hipStream_t s);
-int ws_release(ngpu_engine *e, hipStream_t s);
+// bound: the stage-end event its last kernel records (null: record ws_done).
+int ws_release(ngpu_engine *e, hipStream_t s, hipEvent_t bound);
 
 // Reference counts.  engine_unref frees the engine when the last holder (the
 // creator's ngpu_destroy or the last open pack) lets go.

@@ -5,11 +5,12 @@ replaces the digest/dedup stage that pkg/converter hands to
 `nydus-image create` (pkg/converter/tool/builder.go:148-178).
 """
 from ._lib import (CHUNK_DTYPE, COMPRESSORS, DEFAULT_DICT, DICT, DIGESTERS, ECANCELED, EINVAL,  # noqa: F401
-                   ENOTFOUND, EXPORTS, HIT_DTYPE, FdWriter, INTRA, KIND_NAMES, LAYER_STATS_DTYPE, MISS, NEW,
+                   ENOTFOUND, EXPORTS, FLAG_GRID_STAGES, HIT_DTYPE, FdWriter, INTRA, KIND_NAMES, LAYER_STATS_DTYPE, MISS, NEW,
                    RESULT_DTYPE, TOC_ENTRY_DTYPE, ChunkDict, Engine, Node, NODE_DICT_PARTITION,
                    NODE_DICT_REPLICATE, NgpuError, blob_write, chunk_table,
                    lib, merge, tar_chunks, unpack_entry)
 
 __all__ = ["Engine", "Node", "NODE_DICT_PARTITION", "NODE_DICT_REPLICATE", "ChunkDict", "DEFAULT_DICT", "NgpuError", "tar_chunks", "chunk_table", "lib", "CHUNK_DTYPE",
            "RESULT_DTYPE", "HIT_DTYPE", "MISS", "NEW", "INTRA", "DICT", "KIND_NAMES", "DIGESTERS", "EXPORTS",
-           "COMPRESSORS", "TOC_ENTRY_DTYPE", "FdWriter", "blob_write", "unpack_entry", "merge"]
+           "COMPRESSORS", "TOC_ENTRY_DTYPE", "FdWriter", "blob_write", "unpack_entry", "merge",
+           "FLAG_GRID_STAGES"]

@@ -82,6 +82,7 @@ class NgpuConfig(ctypes.Structure):
 
 FLAG_TIMING = 0x1
 FLAG_ALIGNED_CHUNK = 0x2
+FLAG_GRID_STAGES = 0x4  # no fused one-workgroup path for small calls (tests / tuning)
 
 
 class NgpuTiming(ctypes.Structure):

@@ -19,6 +19,9 @@ LANES = [1, 2, 4, 8, 16]
 # "pair" runs two chunk groups per workgroup; 5 forces one group per workgroup.
 SHA_SPLIT, SHA_PAIR, SHA_PAIR_R1 = 1 << 11, 2 << 11, 5 << 11
 SHA_FLAGS = [0, SHA_SPLIT, SHA_PAIR, SHA_PAIR_R1]
+# Calls with <= 4096 chunks plan and dedup in one fused workgroup; this flag
+# forces the multi-kernel grid path, so both are checked on the same inputs.
+GRID = nydus_gpu.FLAG_GRID_STAGES
 
 
 @pytest.fixture(scope="module")
@@ -71,7 +74,7 @@ def test_kat_batched_all_lengths(engines, kat):
     ch = np.array(chunks, dtype=nydus_gpu.CHUNK_DTYPE)
     for digester in ("blake3", "sha256"):
         for lanes, fl in ([(l, 0) for l in LANES] if digester == "blake3" else
-                          [(0, f) for f in SHA_FLAGS]):
+                          [(0, f) for f in SHA_FLAGS]) + [(0, GRID)]:
             out, _ = engines(digester, 0x1000000, lanes, flags=fl).process(data, ch)
             got = [o.tobytes().hex() for o in out["digest"]]
             assert got == [v[digester] for v in vecs], (digester, lanes, fl)
@@ -188,7 +191,7 @@ def test_random_vs_oracle(engines, oracle, seed, chunk_size, unaligned):
         exp_d = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), digester)
         exp, own = oracle.dedup(exp_d, ch["length"])
         for lanes, fl in ([(0, 0), (1, 0), (16, 0)] if digester == "blake3" else
-                          [(0, f) for f in SHA_FLAGS]):
+                          [(0, f) for f in SHA_FLAGS]) + [(0, GRID)]:
             out, st = engines(digester, chunk_size, lanes, flags=fl).process(data, ch)
             assert np.array_equal(out["digest"], exp_d), (digester, lanes, fl)
             for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
@@ -226,7 +229,8 @@ def test_sha256_ragged_wave(engines, oracle, fl):
         eng.process(data, bad)
 
 
-def test_random_dict_vs_oracle(oracle):
+@pytest.mark.parametrize("fl", [0, GRID])
+def test_random_dict_vs_oracle(oracle, fl):
     """Dict with duplicates (first wins), usize 0 wildcard, size mismatches and
     several inner blobs: decisions and blob allocation order match the oracle."""
     rng = np.random.default_rng(11)
@@ -242,7 +246,7 @@ def test_random_dict_vs_oracle(oracle):
     db = rng.integers(0, 7, len(dd)).astype(np.uint32)
     di = rng.integers(0, 1 << 20, len(dd)).astype(np.uint32)
     exp, own = oracle.dedup(dig, ch["length"], dd, ds, db, di)
-    eng = nydus_gpu.Engine(chunk_size=0x10000)
+    eng = nydus_gpu.Engine(chunk_size=0x10000, flags=fl)
     try:
         eng.dict_load(dd, ds, db, di)
         out, st = eng.process(data, ch)
@@ -580,14 +584,18 @@ def test_staging_pool_reuse_across_packs(golden_layers, tars, oracle):
         eng.close()
 
 
-def test_multi_layer_dedup_matches_per_layer(oracle):
-    """One launch set over 40 layers == each layer packed alone (oracle per
-    layer), with a shared chunk dict and cross-layer duplicate contents."""
+@pytest.mark.parametrize("L,fl", [(40, 0), (40, GRID), (64, 0), (80, 0)])
+def test_multi_layer_dedup_matches_per_layer(oracle, L, fl):
+    """One launch set over L layers == each layer packed alone (oracle per
+    layer), with a shared chunk dict and cross-layer duplicate contents (<= 64
+    layers of a small call: the fused one-workgroup dedup; 80 layers and
+    GRID: the multi-kernel path)."""
     import torch
     rng = np.random.default_rng(31)
     data, ch = _random_layer(rng, 40 << 20, 0x10000, dup_frac=0.4)
     n = len(ch)
-    cuts = np.sort(rng.choice(np.arange(1, n), 39, replace=False))
+    assert n <= 4096
+    cuts = np.sort(rng.choice(np.arange(1, n), L - 1, replace=False))
     first = np.concatenate([[0], cuts, [n]]).astype(np.uint64)
     first[5] = first[4]  # an empty layer
     dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
@@ -595,22 +603,22 @@ def test_multi_layer_dedup_matches_per_layer(oracle):
     dd, ds = dig[pick], ch["length"][pick].astype(np.uint32)
     db = (np.arange(len(pick)) % 5).astype(np.uint32)
     di = np.arange(len(pick), dtype=np.uint32)
-    eng = nydus_gpu.Engine(chunk_size=0x10000)
+    eng = nydus_gpu.Engine(chunk_size=0x10000, flags=fl)
     try:
         eng.dict_load(dd, ds, db, di)
         d_data, d_ch = _to_dev(np.frombuffer(data, np.uint8)), _to_dev(ch)
         d_first = torch.from_numpy(first.view(np.int64).copy()).cuda()
         out = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
-        st = torch.zeros(40 * nydus_gpu.LAYER_STATS_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        st = torch.zeros(L * nydus_gpu.LAYER_STATS_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
         eng.process_layers_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), n, out.data_ptr(),
-                                  d_first.data_ptr(), 40, st.data_ptr())
+                                  d_first.data_ptr(), L, st.data_ptr())
         torch.cuda.synchronize()
         got = out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
         stats = st.cpu().numpy().view(nydus_gpu.LAYER_STATS_DTYPE)
     finally:
         eng.close()
     assert np.array_equal(got["digest"], dig)
-    for l in range(40):
+    for l in range(L):
         a, b = int(first[l]), int(first[l + 1])
         exp, own = oracle.dedup(dig[a:b], ch["length"][a:b], dd, ds, db, di)
         g = got[a:b]
@@ -887,11 +895,11 @@ def test_small_file_mix_vs_oracle(engines, oracle, chunk_size, median, files):
     dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
     dec, _ = oracle.dedup(dig, ch["length"])
     assert (dec["kind"] == 1).sum() > 0
-    for lanes in LANES:
-        out, st = engines("blake3", chunk_size, lanes).process(data, ch)
-        assert np.array_equal(out["digest"], dig), lanes
+    for lanes, fl in [(l, 0) for l in LANES] + [(0, GRID)]:
+        out, st = engines("blake3", chunk_size, lanes, flags=fl).process(data, ch)
+        assert np.array_equal(out["digest"], dig), (lanes, fl)
         for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
-            assert np.array_equal(out[f], dec[f]), (lanes, f)
+            assert np.array_equal(out[f], dec[f]), (lanes, fl, f)
 
 
 def test_many_tiles_multi_layer_vs_oracle(oracle):
@@ -954,12 +962,16 @@ def test_many_tiles_multi_layer_vs_oracle(oracle):
         assert stats[l]["blobs"] == len(set(exp["blob_index"].tolist())), l
 
 
-@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 1023, 1024, 1025, 2047, 2048, 2049, 4097,
-                               64 * 1024 + 1, 512 * 1024 + 3])
-def test_scan_tile_boundaries_vs_oracle(engines, oracle, n):
+_SCAN_N = [1, 2, 255, 256, 257, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4096, 4097,
+           64 * 1024 + 1, 512 * 1024 + 3]
+
+
+@pytest.mark.parametrize("n,fl", [(n, 0) for n in _SCAN_N] + [(n, GRID) for n in _SCAN_N if n <= 4097])
+def test_scan_tile_boundaries_vs_oracle(engines, oracle, n, fl):
     """Chunk counts at the single-pass scans' tile edges (256, 1024, 2048 and
-    the 512-tile look-back window): decisions, indices and offsets equal the
-    oracle's, for the single-layer path and a 3-layer call."""
+    the 512-tile look-back window) and at the fused small-call limit (4096):
+    decisions, indices and offsets equal the oracle's, for the single-layer
+    path and a 3-layer call, on the fused and the grid path."""
     import torch
     rng = np.random.default_rng(n)
     data = rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes()
@@ -971,14 +983,14 @@ def test_scan_tile_boundaries_vs_oracle(engines, oracle, n):
     ch["offset"][dup], ch["length"][dup] = ch["offset"][src[dup]], ch["length"][src[dup]]
     dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
     dec, _ = oracle.dedup(dig, ch["length"])
-    out, st = engines("blake3", 0x100000).process(data, ch)
+    out, st = engines("blake3", 0x100000, flags=fl).process(data, ch)
     assert np.array_equal(out["digest"], dig)
     for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
         assert np.array_equal(out[f], dec[f]), f
     # three layers, the middle one empty when n allows a cut
     cut = n // 2
     first = np.array([0, cut, cut, n], dtype=np.int64)
-    eng = engines("blake3", 0x100000)
+    eng = engines("blake3", 0x100000, flags=fl)
     d_data, d_ch = _to_dev(np.frombuffer(data, np.uint8)), _to_dev(ch)
     d_first = torch.from_numpy(first.copy()).cuda()
     d_out = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
