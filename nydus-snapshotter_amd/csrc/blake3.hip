@@ -721,21 +721,199 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
 }
 
 // Upper levels: one workgroup per chunk with more than one leaf group.
+// ---- small layers: one compression per lane QUAD (latency path) ---------------
+// A small layer has far fewer 1-KiB leaves than the chip has lanes (C1: ~10K
+// leaves, 157 waves for 1,024 SIMDs), so b3_groups runs one wave per SIMD and
+// each lane's 16 chained compressions (680 VALU ops each, one op per ~5
+// cycles for a lone wave) ARE the kernel time.  Here four lanes share each
+// compression, one column of the 4 x 4 state per lane: a G step is the
+// lane's own G, and the row rotation between column and diagonal steps rides
+// on the first use of b, c and d as DPP quad_perm operands of v_add / v_xor
+// (gfx950 has no DPP on VOP3, so b costs one v_mov_dpp): ~190 VALU ops per
+// lane per compression instead of 680.  The message block is staged in LDS
+// (each lane stores its 16 B, then reads its 28 schedule words at per-lane
+// offsets fixed for the kernel) -- the "message words staged in LDS" of the
+// north star.  Chunk trees above the leaves go to b3_tree.
+constexpr int kQuadThreads = 256;           // 64 quads = 64 leaves per workgroup
+constexpr uint64_t kQuadMaxLeaves = 16384;  // <= 1,024 waves: at most one per SIMD
+constexpr int kQP1 = 0x39, kQP2 = 0x4E, kQP3 = 0x93;  // quad_perm: lane i reads lane i+1/+2/+3
+
+template <int P>
+__device__ __forceinline__ uint32_t qperm(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, P, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) {
+  return __builtin_amdgcn_alignbit(x, x, n);
+}
+// G on the lane's column, registers aligned.
+__device__ __forceinline__ void gq(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d,
+                                   uint32_t mx, uint32_t my) {
+  a = a + b + mx; d = rotr32(d ^ a, 16); c = c + d; b = rotr32(b ^ c, 12);
+  a = a + b + my; d = rotr32(d ^ a, 8);  c = c + d; b = rotr32(b ^ c, 7);
+}
+// G whose b, c, d are first read from quad lanes +PB, +PC, +PD (the row
+// rotation folded into each word's first use); leaves them rotated.
+template <int PB, int PC, int PD>
+__device__ __forceinline__ void gq_rot(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d,
+                                       uint32_t mx, uint32_t my) {
+  const uint32_t br = qperm<PB>(b);
+  a = a + br + mx; d = rotr32(qperm<PD>(d) ^ a, 16); c = qperm<PC>(c) + d;
+  b = rotr32(br ^ c, 12);
+  a = a + b + my; d = rotr32(d ^ a, 8); c = c + d; b = rotr32(b ^ c, 7);
+}
+// Lane q of a quad holds cv[q], cv[4 + q] in (x, y); m: the lane's schedule
+// words, round r = {column x, column y, diagonal x, diagonal y}; dq = v[12 + q]
+// (counter lo, counter hi, block length, flags).
+__device__ __forceinline__ void compress_quad(uint32_t &x, uint32_t &y, const uint32_t m[28],
+                                              uint32_t ivq, uint32_t dq) {
+  uint32_t a = x, b = y, c = ivq, d = dq;
+  gq(a, b, c, d, m[0], m[1]);
+  gq_rot<kQP1, kQP2, kQP3>(a, b, c, d, m[2], m[3]);  // column -> diagonal
+#pragma unroll
+  for (int r = 1; r < 7; ++r) {
+    gq_rot<kQP3, kQP2, kQP1>(a, b, c, d, m[4 * r], m[4 * r + 1]);      // diagonal -> column
+    gq_rot<kQP1, kQP2, kQP3>(a, b, c, d, m[4 * r + 2], m[4 * r + 3]);  // column -> diagonal
+  }
+  // diagonal alignment: v[8 + q] is on lane q + 2, v[4 + q] on q - 1, v[12 + q] on q + 1
+  x = a ^ qperm<kQP2>(c);
+  y = qperm<kQP3>(b) ^ qperm<kQP1>(d);
+}
+
+// The schedule word of round r, slot s (column x/y, diagonal x/y) for the 4
+// lanes of a quad, one nibble per lane.
+struct QuadSched { uint16_t w[7][4]; };
+constexpr QuadSched make_quad_sched() {
+  QuadSched t{};
+  for (int r = 0; r < 7; ++r)
+    for (int sl = 0; sl < 4; ++sl) {
+      uint16_t v = 0;
+      for (int q = 0; q < 4; ++q) {
+        const int pos = (sl < 2 ? 0 : 8) + 2 * q + (sl & 1);
+        v |= (uint16_t)(kSched.s[r][pos] << (4 * q));
+      }
+      t.w[r][sl] = v;
+    }
+  return t;
+}
+constexpr QuadSched kQuadSched = make_quad_sched();
+
+// The lane's 16 bytes of a block: valid (0..16) bytes, zero padded; byte
+// loads when partial or unaligned (never past the chunk).
+__device__ __forceinline__ u32x4 load16(const uint8_t *p, int valid) {
+  if (valid >= 16 && (reinterpret_cast<uintptr_t>(p) & 15) == 0)
+    return *reinterpret_cast<const u32x4 *>(p);
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < valid) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+  return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+// One leaf per quad: leaves [0, gm) of multi-leaf chunks (CV to cv_out, the
+// chunk queued for b3_tree by its leaf 0), then the single-leaf chunks
+// (digest, ROOT).  Group == leaf (D = 0).
+__global__ __launch_bounds__(kQuadThreads) void b3_quad_leaves(
+    const uint8_t *__restrict__ data, uint64_t data_len, const ngpu_chunk *__restrict__ chunks,
+    uint64_t n, const uint64_t *__restrict__ gbase, const uint32_t *__restrict__ gchunk,
+    uint64_t cap_g, uint32_t *__restrict__ cv_out, ngpu_result *__restrict__ out,
+    uint64_t *__restrict__ err, const uint32_t *__restrict__ small,
+    const uint64_t *__restrict__ nsmall, uint32_t *__restrict__ tree_list) {
+  __shared__ __attribute__((aligned(16))) uint32_t qmsg[kQuadThreads / 4 * 16];
+  const uint32_t q = threadIdx.x & 3, quad = threadIdx.x >> 2;
+  const uint64_t gm = gbase[n], total = gm + *nsmall;
+  const uint64_t g = blockIdx.x * (uint64_t)(kQuadThreads / 4) + quad;
+  if (g >= total || g >= cap_g) return;  // per quad: its four lanes leave together
+  uint32_t c, j;
+  bool root_group;
+  if (g < gm) {
+    c = gchunk[g];
+    j = (uint32_t)(g - gbase[c]);
+    root_group = false;
+  } else {
+    c = small[g - gm];
+    j = 0;
+    root_group = true;
+  }
+  const ngpu_chunk ch = chunks[c];
+  const uint32_t len = ch.length;
+  if (ch.offset > data_len || len > data_len - ch.offset) {  // bad descriptor
+    if (j == 0 && q == 0) atomicAdd((unsigned long long *)err, 1ull);
+    return;
+  }
+  uint32_t *blk = qmsg + quad * 16;
+  uint32_t wo[28];  // this lane's schedule words: LDS word offsets in the quad's block
+#pragma unroll
+  for (int r = 0; r < 7; ++r)
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) wo[4 * r + sl] = (kQuadSched.w[r][sl] >> (4 * q)) & 15u;
+  const uint32_t off = j * kLeaf;
+  const uint32_t llen = min(kLeaf, len - off);
+  const uint32_t nb = llen == 0 ? 1 : (llen + 63) >> 6;
+  const uint8_t *src = data + ch.offset + off + 16 * q;
+  const uint32_t iv_lo[4] = {IV0, IV1, IV2, IV3}, iv_hi[4] = {IV4, IV5, IV6, IV7};
+  const uint32_t ivq = q == 0 ? iv_lo[0] : q == 1 ? iv_lo[1] : q == 2 ? iv_lo[2] : iv_lo[3];
+  uint32_t x = ivq, y = q == 0 ? iv_hi[0] : q == 1 ? iv_hi[1] : q == 2 ? iv_hi[2] : iv_hi[3];
+  auto valid = [&](uint32_t b) { return (int)min(16u, (uint32_t)max(0, (int)llen - (int)(64 * b + 16 * q))); };
+  u32x4 w = load16(src, valid(0));
+  for (uint32_t b = 0; b < nb; ++b) {
+    u32x4 nx = w;
+    if (b + 1 < nb) nx = load16(src + 64 * (b + 1), valid(b + 1));  // next block in flight
+    *reinterpret_cast<u32x4 *>(blk + 4 * q) = w;
+    // the quad's four stores are in this wave's LDS queue ahead of its loads
+    asm volatile("" ::: "memory");
+    uint32_t m[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) m[k] = blk[wo[k]];
+    asm volatile("" ::: "memory");
+    const uint32_t bl = min(64u, llen - 64 * b);
+    const uint32_t flags = (b == 0 ? CHUNK_START : 0u) |
+                           (b + 1 == nb ? (CHUNK_END | (root_group ? ROOT : 0u)) : 0u);
+    const uint32_t dq = q == 0 ? j : q == 1 ? 0u : q == 2 ? bl : flags;
+    compress_quad(x, y, m, ivq, dq);
+    w = nx;
+  }
+  if (root_group) {
+    uint32_t *d = reinterpret_cast<uint32_t *>(out[c].digest);
+    d[q] = x;
+    d[4 + q] = y;
+  } else {
+    cv_out[g * 8 + q] = x;
+    cv_out[g * 8 + 4 + q] = y;
+    if (j == 0 && q == 0) {  // err + 2 == stats[9]: chunks queued for b3_tree
+      const uint64_t t = atomicAdd(reinterpret_cast<unsigned long long *>(err + 2), 1ull);
+      tree_list[t] = c;
+    }
+  }
+}
+
 constexpr int kTreeThreads = 256;
+constexpr uint32_t kTreeQuads = kTreeThreads / 4;
 constexpr int kTile = 1024;  // CVs per LDS tile (32 KiB)
 
+// all_queued: every multi-group chunk was queued (b3_quad_leaves), none was
+// finished inside a b3_groups workgroup.
 __global__ __launch_bounds__(kTreeThreads) void b3_tree(
     const uint64_t *__restrict__ gbase, const uint32_t *__restrict__ tree_list,
     const uint64_t *__restrict__ queued, uint64_t cap_g,
-    uint32_t *__restrict__ cv, ngpu_result *__restrict__ out) {
+    uint32_t *__restrict__ cv, ngpu_result *__restrict__ out, bool all_queued) {
   __shared__ uint32_t t[kTile * 8];
   const int tid = threadIdx.x;
+  // quad lanes for the narrow levels (<= 2 parents per quad): this lane's
+  // column and schedule word offsets in a parent's 16-word message
+  const uint32_t qlane = tid & 3, qid = tid >> 2;
+  uint32_t wo[28];
+#pragma unroll
+  for (int r = 0; r < 7; ++r)
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) wo[4 * r + sl] = (kQuadSched.w[r][sl] >> (4 * qlane)) & 15u;
+  const uint32_t ivq = qlane == 0 ? IV0 : qlane == 1 ? IV1 : qlane == 2 ? IV2 : IV3;
+  const uint32_t ivh = qlane == 0 ? IV4 : qlane == 1 ? IV5 : qlane == 2 ? IV6 : IV7;
   const uint64_t nq = *queued;  // 0: every chunk was finished inside b3_groups
   for (uint64_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
     const uint32_t c = tree_list[qi];
     const uint64_t base = gbase[c];
     uint64_t k = gbase[c + 1] - base;
-    if (k <= 1 || base + k > cap_g || tree_in_workgroup(base, k)) continue;
+    if (k <= 1 || base + k > cap_g || (!all_queued && tree_in_workgroup(base, k))) continue;
     uint32_t *a = cv + base * 8;
     for (;;) {
       const bool final_pass = k <= kTile;
@@ -747,6 +925,47 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
         __syncthreads();
         while (cnt > 1) {
           const uint32_t p = cnt >> 1;
+          const uint32_t pflags = PARENT | ((final_pass && cnt == 2) ? ROOT : 0);
+          if (p <= 2 * kTreeQuads) {
+            // Narrow level: a quad of lanes per parent (compress_quad), its
+            // message being the two child CVs already adjacent in t.
+            uint32_t rx[2], ry[2];
+            const uint32_t dq = qlane == 2 ? 64u : qlane == 3 ? pflags : 0u;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const uint32_t pi = qid + s * kTreeQuads;
+              if (pi < p) {
+                uint32_t m[28];
+#pragma unroll
+                for (int k2 = 0; k2 < 28; ++k2) m[k2] = t[16 * pi + wo[k2]];
+                rx[s] = ivq;
+                ry[s] = ivh;
+                compress_quad(rx[s], ry[s], m, ivq, dq);
+              }
+            }
+            uint32_t odd[8];
+            const bool has_odd = (cnt & 1) && tid == 0;
+            if (has_odd) {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) odd[i] = t[8 * (cnt - 1) + i];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const uint32_t pi = qid + s * kTreeQuads;
+              if (pi < p) {
+                t[8 * pi + qlane] = rx[s];
+                t[8 * pi + 4 + qlane] = ry[s];
+              }
+            }
+            if (has_odd) {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) t[8 * p + i] = odd[i];
+            }
+            __syncthreads();
+            cnt = p + (cnt & 1);
+            continue;
+          }
           uint32_t r[2][8];
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
@@ -756,8 +975,7 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
 #pragma unroll
               for (int i = 0; i < 16; ++i) m[i] = t[16 * q + i];
               set_iv(r[s]);
-              compress(r[s], m, 0, 64,
-                       PARENT | ((final_pass && cnt == 2) ? ROOT : 0));
+              compress(r[s], m, 0, 64, pflags);
             }
           }
           uint32_t odd[8];
@@ -863,7 +1081,16 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
     hipLaunchKernelGGL(b3_fill_group_chunk, dim3((unsigned)blocks), dim3(256), 0,
                        s, (const uint64_t *)ws.groups, n, ws.group_chunk, ws.cap_g, W);
   }
-  switch (D) {
+  // small layers at one leaf per lane: a quad of lanes per compression instead
+  const bool quad = D == 0 && !ws.grid_stages && data_len / kLeaf + n <= kQuadMaxLeaves;
+  if (quad) {
+    const uint64_t blocks = (ws.cap_g + kQuadThreads / 4 - 1) / (kQuadThreads / 4);
+    hipExtLaunchKernelGGL(b3_quad_leaves, dim3((unsigned)blocks), dim3(kQuadThreads), 0, s,
+                          ev_start, ev_end_groups, 0, data, data_len, chunks, n,
+                          (const uint64_t *)ws.groups, (const uint32_t *)ws.group_chunk, ws.cap_g,
+                          ws.cv, out, ws.stats + 7, (const uint32_t *)ws.small,
+                          (const uint64_t *)(ws.stats + 10), ws.tree_list);
+  } else switch (D) {
     case 0: launch_groups<0>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
     case 1: launch_groups<1>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
     case 2: launch_groups<2>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
@@ -873,7 +1100,7 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
   const uint64_t blocks = n < 2048 ? n : 2048;
   hipExtLaunchKernelGGL(b3_tree, dim3((unsigned)blocks), dim3(kTreeThreads), 0, s, nullptr, ev_end,
                         0, (const uint64_t *)ws.groups, (const uint32_t *)ws.tree_list,
-                        (const uint64_t *)(ws.stats + 9), ws.cap_g, ws.cv, out);
+                        (const uint64_t *)(ws.stats + 9), ws.cap_g, ws.cv, out, quad);
   return true;
 }
 
