@@ -107,7 +107,9 @@ typedef struct {
 
 /* Per-stage device time of the last process call (NGPU_FLAG_TIMING). */
 typedef struct {
-  float digest_ms;   /* leaf/group digest kernel (b3_groups / sha256_chunks) */
+  float digest_ms;   /* leaf/group digest kernel (b3_groups / b3_quad_leaves /
+                        sha256_*); BLAKE3: from the end of chunk planning, i.e.
+                        the kernel plus its dispatch */
   float tree_ms;     /* BLAKE3 upper-tree kernel (0 for sha256) */
   float dedup_ms;    /* dict probe + intra-layer dedup + scans + finalize */
   float total_ms;    /* whole enqueue, first to last kernel */

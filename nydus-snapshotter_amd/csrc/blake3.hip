@@ -1057,7 +1057,9 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
     return false;
   }
   if (!ws.grid_stages && n <= kSmallPlanChunks) {
-    hipExtLaunchKernelGGL(b3_plan_small, dim3(1), dim3(kSmallPlanThreads), 0, s, ev_first, nullptr,
+    // ev_start = END of planning: a start event of hipExtLaunchKernel is a
+    // marker packet (~5-10 us on a small layer), a stop event binds to the kernel
+    hipExtLaunchKernelGGL(b3_plan_small, dim3(1), dim3(kSmallPlanThreads), 0, s, ev_first, ev_start,
                           0, chunks, n, D, ws.groups, ws.small, ws.group_chunk, ws.cap_g, ws.stats);
   } else {
     // the call's device counters; histogram + cursors + plan ticket + this
@@ -1078,24 +1080,24 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
     const uint64_t waves_needed = (n * W + 63) / 64;
     const uint64_t waves = waves_needed < 16384 ? waves_needed : 16384;
     const uint64_t blocks = (waves * 64 + 255) / 256;
-    hipLaunchKernelGGL(b3_fill_group_chunk, dim3((unsigned)blocks), dim3(256), 0,
-                       s, (const uint64_t *)ws.groups, n, ws.group_chunk, ws.cap_g, W);
+    hipExtLaunchKernelGGL(b3_fill_group_chunk, dim3((unsigned)blocks), dim3(256), 0, s, nullptr,
+                          ev_start, 0, (const uint64_t *)ws.groups, n, ws.group_chunk, ws.cap_g, W);
   }
   // small layers at one leaf per lane: a quad of lanes per compression instead
   const bool quad = D == 0 && !ws.grid_stages && data_len / kLeaf + n <= kQuadMaxLeaves;
   if (quad) {
     const uint64_t blocks = (ws.cap_g + kQuadThreads / 4 - 1) / (kQuadThreads / 4);
     hipExtLaunchKernelGGL(b3_quad_leaves, dim3((unsigned)blocks), dim3(kQuadThreads), 0, s,
-                          ev_start, ev_end_groups, 0, data, data_len, chunks, n,
+                          nullptr, ev_end_groups, 0, data, data_len, chunks, n,
                           (const uint64_t *)ws.groups, (const uint32_t *)ws.group_chunk, ws.cap_g,
                           ws.cv, out, ws.stats + 7, (const uint32_t *)ws.small,
                           (const uint64_t *)(ws.stats + 10), ws.tree_list);
   } else switch (D) {
-    case 0: launch_groups<0>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
-    case 1: launch_groups<1>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
-    case 2: launch_groups<2>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
-    case 3: launch_groups<3>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
-    default: launch_groups<4>(data, data_len, chunks, n, ws, out, s, ev_start, ev_end_groups); break;
+    case 0: launch_groups<0>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
+    case 1: launch_groups<1>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
+    case 2: launch_groups<2>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
+    case 3: launch_groups<3>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
+    default: launch_groups<4>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
   }
   const uint64_t blocks = n < 2048 ? n : 2048;
   hipExtLaunchKernelGGL(b3_tree, dim3((unsigned)blocks), dim3(kTreeThreads), 0, s, nullptr, ev_end,

@@ -164,8 +164,10 @@ constexpr uint64_t kSmallDedupLayers = 64;
 
 // blake3.hip.  Events (each may be null) ride on the kernels themselves
 // (hipExtLaunchKernelGGL start/stop), so timing and stream ordering add no
-// marker packets: ev_first = start of the first kernel, ev_groups_* = the
-// leaf-group kernel, ev_end = end of the stage.  Returns false when nothing
+// marker packets: ev_first = start of the first kernel (the one start event:
+// it IS a marker), ev_groups_start = end of chunk planning (so the digest
+// time is the leaf kernel plus its dispatch), ev_groups_end = end of the
+// leaf kernel, ev_end = end of the stage.  Returns false when nothing
 // was launched (n == 0: ev_end was not recorded).
 bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
                    uint64_t data_len, int group_log2, Workspace &ws,
