@@ -736,7 +736,10 @@ def main():
         # compressions done by b3_groups: all leaf blocks + in-group parents
         comp = blocks + (leaves - groups)
         achieved = comp * OPS_PER_COMPRESSION / (dig_ms / 1e3)
-        roof = {"bound": "valu", "kernel": f"b3_groups<{D}>", "achieved": round(achieved / 1e12, 3),
+        # launch_blake3's rule: one leaf per lane quad for <= 16K leaves at D = 0
+        quad = D == 0 and int(buf.numel()) // 1024 + n <= 16384
+        kname = "b3_quad_leaves" if quad else f"b3_groups<{D}>"
+        roof = {"bound": "valu", "kernel": kname, "achieved": round(achieved / 1e12, 3),
                 "peak": round(PEAK_INT_OPS / 1e12, 3), "unit": "Tops/s",
                 "frac": round(achieved / PEAK_INT_OPS, 4), "traffic": None,
                 "hbm_gbs": round(file_bytes / (dig_ms / 1e3) / 1e9, 1),
