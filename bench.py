@@ -182,6 +182,10 @@ WORKLOADS = {
                n_files=1024, file_size=16 * MiB, chunk=64 * 1024, digester="blake3", layers=1),
     "small": dict(desc="1 GiB layer, 1 MiB chunks, blake3", n_files=256, file_size=4 * MiB,
                   chunk=MiB, digester="blake3", layers=1),
+    # mid-size layers (the auto rule hashes them one leaf per lane or per lane quad)
+    **{f"l{m}m": dict(desc=f"{m} MiB layer, 4 MiB files, 1 MiB chunks, blake3", n_files=m // 4,
+                      file_size=4 * MiB, chunk=MiB, digester="blake3", layers=1)
+       for m in (8, 16, 24, 32, 48, 64, 128)},
 }
 
 

@@ -735,7 +735,10 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
 // offsets fixed for the kernel) -- the "message words staged in LDS" of the
 // north star.  Chunk trees above the leaves go to b3_tree.
 constexpr int kQuadThreads = 256;           // 64 quads = 64 leaves per workgroup
-constexpr uint64_t kQuadMaxLeaves = 16384;  // <= 1,024 waves: at most one per SIMD
+#ifndef B3_QUAD_MAX_LEAVES
+#define B3_QUAD_MAX_LEAVES 16384
+#endif
+constexpr uint64_t kQuadMaxLeaves = B3_QUAD_MAX_LEAVES;  // <= 1,024 waves: at most one per SIMD
 constexpr int kQP1 = 0x39, kQP2 = 0x4E, kQP3 = 0x93;  // quad_perm: lane i reads lane i+1/+2/+3
 
 template <int P>
