@@ -740,8 +740,8 @@ def main():
         # compressions done by b3_groups: all leaf blocks + in-group parents
         comp = blocks + (leaves - groups)
         achieved = comp * OPS_PER_COMPRESSION / (dig_ms / 1e3)
-        # launch_blake3's rule: one leaf per lane quad for <= 16K leaves at D = 0
-        quad = D == 0 and int(buf.numel()) // 1024 + n <= 16384
+        # launch_blake3's rule: one leaf per lane quad for <= 32K leaves at D = 0
+        quad = D == 0 and int(buf.numel()) // 1024 + n <= 32768
         kname = "b3_quad_leaves" if quad else f"b3_groups<{D}>"
         roof = {"bound": "valu", "kernel": kname, "achieved": round(achieved / 1e12, 3),
                 "peak": round(PEAK_INT_OPS / 1e12, 3), "unit": "Tops/s",

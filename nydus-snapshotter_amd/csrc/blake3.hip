@@ -735,10 +735,14 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
 // offsets fixed for the kernel) -- the "message words staged in LDS" of the
 // north star.  Chunk trees above the leaves go to b3_tree.
 constexpr int kQuadThreads = 256;           // 64 quads = 64 leaves per workgroup
+// Up to 32K leaves (<= 2 quad waves per SIMD).  Measured crossover with the
+// lane-per-leaf path (profiles/r2/quad_threshold_r2qt.json, digest ms, lane vs
+// quad): 8 MiB 0.030 / 0.018, 16 MiB 0.030 / 0.020, 32 MiB 0.033 / 0.026,
+// 48 MiB 0.033 / 0.032, 64 MiB equal.
 #ifndef B3_QUAD_MAX_LEAVES
-#define B3_QUAD_MAX_LEAVES 16384
+#define B3_QUAD_MAX_LEAVES 32768
 #endif
-constexpr uint64_t kQuadMaxLeaves = B3_QUAD_MAX_LEAVES;  // <= 1,024 waves: at most one per SIMD
+constexpr uint64_t kQuadMaxLeaves = B3_QUAD_MAX_LEAVES;
 constexpr int kQP1 = 0x39, kQP2 = 0x4E, kQP3 = 0x93;  // quad_perm: lane i reads lane i+1/+2/+3
 
 template <int P>
