@@ -737,8 +737,15 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
   const uint64_t nt = (n + kScanTile - 1) / kScanTile;
   uint64_t *ts = ws.tstat + kDedupTs(ws.tiles);
   const uint64_t nbf = (uint64_t)nbo * L, nst = L * (sizeof(ngpu_layer_stats) / 8);
-  // the small path scans in LDS: no tile words to reset
-  const uint64_t icap = n ? ws.intra_cap : 0, ntw = small ? 0 : 1 + kDedupScans * ws.tiles;
+  // the small path scans in LDS (no tile words to reset) and uses the first
+  // 2n (pow2) slots of the intra table: its init pass zeroes only those
+  uint64_t icap = n ? ws.intra_cap : 0;
+  if (small && n) {
+    uint64_t c = 64;
+    while (c < 2 * n) c <<= 1;
+    icap = c < icap ? c : icap;
+  }
+  const uint64_t ntw = small ? 0 : 1 + kDedupScans * ws.tiles;
   uint64_t total = n + 1;
   for (uint64_t v : {nbf, nst, icap, ntw}) total = v > total ? v : total;
   const DedupInit a{lfirst, L, n, single, ws.chunk_layer, ws.blob_first, nbf,
