@@ -92,9 +92,11 @@ typedef struct {
  * 4 KiB-align the uncompressed offsets of NEW chunks for RAFS v5 too (v6
  * always aligns). */
 #define NGPU_FLAG_ALIGNED_CHUNK 0x2u
-/* Tuning / tests: never take the one-workgroup path for small calls (chunk
- * planning and the dedup stage of calls with <= 4096 chunks run in one fused
- * workgroup each by default; this flag keeps the multi-kernel grid path). */
+/* Tuning / tests: never take the small-call paths.  By default chunk planning
+ * and the dedup stage of calls with <= 4096 chunks run in one fused workgroup
+ * each, and BLAKE3 layers of <= 32K leaves (one leaf per lane) hash each
+ * compression on a quad of lanes; this flag keeps the multi-kernel grid path
+ * and one lane per leaf (same results). */
 #define NGPU_FLAG_GRID_STAGES 0x4u
 /* Tuning (benchmarks only): bits 8..10 = 1 + BLAKE3 load mode
  * (bit0 non-temporal loads, bit1 next-block prefetch); 0 = library default. */
