@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "engine_internal.hpp"
+#include "tarstream.hpp"
 
 using namespace ngpu;
 
@@ -505,6 +506,82 @@ static int process_host(ngpu_engine *e, ngpu_dict *dict, const void *data, uint6
 int ngpu_process(ngpu_engine *e, const void *data, uint64_t len, const ngpu_chunk *chunks,
                  uint64_t n, ngpu_result *out, ngpu_layer_stats *stats) {
   return process_host(e, kDefault, data, len, chunks, n, out, stats);
+}
+
+// A whole layer tar in host memory.  Its bytes start crossing PCIe before the
+// host walks the headers, so with a pinned buffer the walk (tarstream.hpp)
+// overlaps the H2D DMA; then the chunk table follows, the stages run and the
+// results come back.  Single walk (one pass collects the chunks).
+int ngpu_pack_tar(ngpu_engine *e, const void *tar, uint64_t len, ngpu_chunk **chunks_out,
+                  ngpu_result **results_out, uint64_t *n_out, ngpu_layer_stats *stats) {
+  return guarded([&]() -> int {
+    if (!e || !chunks_out || !results_out || !n_out || (!tar && len)) return NGPU_EINVAL;
+    *chunks_out = nullptr;
+    *results_out = nullptr;
+    *n_out = 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    DeviceGuard dg(e->device);
+    ngpu_dict *dict = e->dict;
+    if (int rc = dict_check(e, dict)) return rc;
+    hipStream_t s = e->stream;
+    uint64_t c0 = e->d_data_cap;
+    if (grow(e, &e->d_data, c0, len + 64)) return NGPU_ENOMEM;
+    e->d_data_cap = c0;
+    if (len) HIP_TRY(e, hipMemcpyAsync(e->d_data, tar, len, hipMemcpyHostToDevice, s));
+    struct Vec : TarSink {
+      std::vector<ngpu_chunk> v;
+      int chunk(uint64_t off, uint32_t l, uint32_t fi, uint64_t fo) override {
+        v.push_back(ngpu_chunk{off, l, fi, fo});
+        return 0;
+      }
+      int data(const uint8_t *, uint64_t) override { return 0; }
+    } vec;
+    TarScanner sc(e->cfg.chunk_size);
+    int rc = sc.feed(static_cast<const uint8_t *>(tar), len, vec);
+    if (!rc) rc = sc.finish();
+    const uint64_t n = vec.v.size();
+    if (!rc && n >= 0xFFFFFFFFull) rc = fail(e, NGPU_EINVAL, "too many chunks in one call");
+    if (rc) {
+      (void)hipStreamSynchronize(s);  // the DMA may still read the caller's buffer
+      return rc;
+    }
+    if (n + 1 > e->d_chunk_cap || !e->d_chunks) {
+      uint64_t a = 0, b = 0;
+      (void)hipStreamSynchronize(s);  // buffers about to be replaced may be in use
+      if (e->d_chunks) hipFree(e->d_chunks), e->d_chunks = nullptr;
+      if (e->d_results) hipFree(e->d_results), e->d_results = nullptr;
+      if (grow(e, &e->d_chunks, a, n + 1)) return NGPU_ENOMEM;
+      if (grow(e, &e->d_results, b, n + 1)) return NGPU_ENOMEM;
+      e->d_chunk_cap = a < b ? a : b;
+    }
+    ngpu_chunk *ch = (ngpu_chunk *)malloc(sizeof(ngpu_chunk) * (n ? n : 1));
+    ngpu_result *res = (ngpu_result *)malloc(sizeof(ngpu_result) * (n ? n : 1));
+    if (!ch || !res) {
+      (void)hipStreamSynchronize(s);
+      free(ch);
+      free(res);
+      return NGPU_ENOMEM;
+    }
+    if (n) memcpy(ch, vec.v.data(), n * sizeof(ngpu_chunk));
+    auto bail = [&](int code) {
+      (void)hipStreamSynchronize(s);
+      free(ch);
+      free(res);
+      return code;
+    };
+    if (n && hipMemcpyAsync(e->d_chunks, ch, n * sizeof(ngpu_chunk), hipMemcpyHostToDevice, s) !=
+                 hipSuccess)
+      return bail(fail(e, NGPU_EHIP, "chunk table H2D failed"));
+    if ((rc = enqueue(e, dict, e->d_data, len, e->d_chunks, n, e->d_results, s))) return bail(rc);
+    if (n && hipMemcpyAsync(res, e->d_results, n * sizeof(ngpu_result), hipMemcpyDeviceToHost, s) !=
+                 hipSuccess)
+      return bail(fail(e, NGPU_EHIP, "results D2H failed"));
+    if ((rc = read_stats(e, s, stats))) return bail(rc);
+    *chunks_out = ch;
+    *results_out = res;
+    *n_out = n;
+    return NGPU_OK;
+  });
 }
 
 int ngpu_process_dict(ngpu_engine *e, ngpu_dict *dict, const void *data, uint64_t len,

@@ -60,38 +60,6 @@ int ngpu_tar_chunks(const void *tar_v, uint64_t len, uint32_t chunk_size, ngpu_c
 
 void ngpu_free_host(void *p) { free(p); }
 
-int ngpu_pack_tar(ngpu_engine *eng, const void *tar, uint64_t len, ngpu_chunk **chunks_out,
-                  ngpu_result **results_out, uint64_t *n_out, ngpu_layer_stats *stats) {
-  return ngpu::guarded([&]() -> int {
-    if (!eng || !chunks_out || !results_out || !n_out) return NGPU_EINVAL;
-    *chunks_out = nullptr;
-    *results_out = nullptr;
-    *n_out = 0;
-    const uint32_t cs = ngpu_engine_chunk_size(eng);
-    uint64_t n = 0, files = 0;
-    int rc = ngpu_tar_chunks(tar, len, cs, nullptr, 0, &n, &files);
-    if (rc) return rc;
-    ngpu_chunk *ch = (ngpu_chunk *)malloc(sizeof(ngpu_chunk) * (n ? n : 1));
-    ngpu_result *res = (ngpu_result *)malloc(sizeof(ngpu_result) * (n ? n : 1));
-    if (!ch || !res) {
-      free(ch);
-      free(res);
-      return NGPU_ENOMEM;
-    }
-    rc = ngpu_tar_chunks(tar, len, cs, ch, n, &n, &files);
-    if (!rc) rc = ngpu_process(eng, tar, len, ch, n, res, stats);
-    if (rc) {
-      free(ch);
-      free(res);
-      return rc;
-    }
-    *chunks_out = ch;
-    *results_out = res;
-    *n_out = n;
-    return NGPU_OK;
-  });
-}
-
 int ngpu_chunk_table(const ngpu_chunk *chunks, const ngpu_result *results, uint64_t n,
                      uint8_t *out, uint64_t cap, uint64_t *n_records) {
   return ngpu::guarded([&]() -> int {

