@@ -256,6 +256,11 @@ void engine_unref(ngpu_engine *e) {
     if (b.copied) (void)hipEventDestroy(b.copied);
     if (b.done) (void)hipEventDestroy(b.done);
   }
+  for (auto &b : e->pack_pool) {
+    if (b.d_res) (void)hipFree(b.d_res);
+    if (b.d_all) (void)hipFree(b.d_all);
+    if (b.copy) (void)hipStreamDestroy(b.copy);
+  }
   if (e->ws_done) (void)hipEventDestroy(e->ws_done);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;

@@ -20,6 +20,17 @@ struct ngpu_staging_buf {
   uint64_t cap = 0;
 };
 
+// Per-pack device buffers and copy stream, kept by the engine between packs
+// (a stream create/destroy and two hipMalloc/hipFree pairs per pack were most
+// of a small layer's streaming Pack: 0.9 ms for C1's 10 MB).
+struct ngpu_pack_bufs {
+  hipStream_t copy = nullptr;
+  ngpu_result *d_res = nullptr;
+  uint64_t res_cap = 0;
+  ngpu_chunk *d_all = nullptr;
+  uint64_t all_cap = 0;
+};
+
 // A chunk dict ([nydus v2.3.0] HashChunkDict): HBM-resident, read-only once
 // built, reference counted (the engine's default slot, its open cache, every
 // pack using it and the caller each hold one).
@@ -83,6 +94,7 @@ struct ngpu_engine {
   hipStream_t ws_last = nullptr;
   bool ws_pending = false;
   std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu
+  std::vector<ngpu_pack_bufs> pack_pool;        // guarded by pool_mu
   std::mutex pool_mu;
   std::string err;
   std::mutex mu;

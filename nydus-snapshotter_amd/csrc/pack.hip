@@ -148,6 +148,7 @@ struct ngpu_pack : TarSink {
   ngpu_result *d_res = nullptr;
   uint64_t res_cap = 0;
   ngpu_chunk *d_all = nullptr;
+  uint64_t all_cap = 0;
   hipStream_t copy = nullptr;
   CopyPool *pool = nullptr;  // created on the first large write
   bool retain = false;       // NGPU_PACK_RETAIN: device segments kept to the end
@@ -198,6 +199,15 @@ void release(ngpu_pack *p) {
     if (s.done) (void)hipEventDestroy(s.done);
   }
   for (Seg &g : p->segs) (void)hipFree(g.d);
+  {
+    std::lock_guard<std::mutex> g(p->e->pool_mu);
+    if (p->copy && p->e->pack_pool.size() < 4) {  // the streams are idle (synchronised above)
+      p->e->pack_pool.push_back({p->copy, p->d_res, p->res_cap, p->d_all, p->all_cap});
+      p->copy = nullptr;
+      p->d_res = nullptr;
+      p->d_all = nullptr;
+    }
+  }
   if (p->d_res) (void)hipFree(p->d_res);
   if (p->d_all) (void)hipFree(p->d_all);
   if (p->copy) (void)hipStreamDestroy(p->copy);
@@ -436,9 +446,18 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
   if (cap < 4ull * e->cfg.chunk_size) cap = 4ull * e->cfg.chunk_size;
   p->cap = cap;
   p->max_ch = cap / 1024 + 16;  // a chunk costs >= 1 KiB of tar stream unless it is a file's last
-  bool ok = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking) == hipSuccess;
+  bool ok = true;
   {
     std::lock_guard<std::mutex> pg(e->pool_mu);
+    if (!e->pack_pool.empty()) {
+      const ngpu_pack_bufs b = e->pack_pool.back();
+      e->pack_pool.pop_back();
+      p->copy = b.copy;
+      p->d_res = b.d_res;
+      p->res_cap = b.res_cap;
+      p->d_all = b.d_all;
+      p->all_cap = b.all_cap;
+    }
     for (Slot &s : p->slot) {
       auto &pool = e->staging_pool;
       for (size_t i = 0; i < pool.size(); ++i) {
@@ -455,6 +474,7 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
       }
     }
   }
+  if (!p->copy) ok = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking) == hipSuccess;
   for (Slot &s : p->slot) {
     if (s.h) {  // from the engine's pool: only the device copy may be missing
       if (!p->retain && !s.d) ok = ok && hipMalloc((void **)&s.d, cap) == hipSuccess;
@@ -585,8 +605,15 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
     DeviceGuard dg(e->device);
     rc = dispatch(p, p->slot[p->cur], p->dispatched, n);
     if (!rc) rc = grow_results(p, n + 1);
-    if (!rc && hipMalloc((void **)&p->d_all, (n + 1) * sizeof(ngpu_chunk)) != hipSuccess)
-      rc = fail(e, NGPU_ENOMEM, "pack: chunk table allocation failed");
+    if (!rc && p->all_cap < n + 1) {  // kept between packs (engine pack_pool)
+      if (p->d_all) (void)hipFree(p->d_all), p->d_all = nullptr, p->all_cap = 0;
+      uint64_t c = 4096;
+      while (c < n + 1) c *= 2;
+      if (hipMalloc((void **)&p->d_all, c * sizeof(ngpu_chunk)) != hipSuccess)
+        rc = fail(e, NGPU_ENOMEM, "pack: chunk table allocation failed");
+      else
+        p->all_cap = c;
+    }
     ch = (ngpu_chunk *)malloc(sizeof(ngpu_chunk) * (n ? n : 1));
     res = (ngpu_result *)malloc(sizeof(ngpu_result) * (n ? n : 1));
     if (!rc && (!ch || !res)) rc = NGPU_ENOMEM;
