@@ -57,7 +57,11 @@ constexpr Sched kSched = make_sched();
 // is 6 % slower on the box (5.89 -> 5.52 ms per 16 GiB C2 launch,
 // profiles/r1/ab_issue_order.jsonl); SDWA rotr16 and split v_add3 were
 // measured there too and lose, and two leaves per lane in lockstep (runs of
-// 8, 108 VGPRs) gain nothing over runs of 4.
+// 8, 108 VGPRs) gain nothing over runs of 4.  Round 2 (same-box A/B): the
+// same order in plain C++ behind sched_barriers -- no conservative s_nop
+// hazard pads around the asm, 1006 -> 66 s_nops -- is 2.5 % SLOWER
+// (profiles/r2/ab_g4_noasm_r2nop.json); all-8-byte encodings with every
+// step 8-byte aligned change nothing (ab_g4_e64_r2e64.json).
 #define B3_OP3(op, a, b, x) asm volatile(op " %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(x))
 #define B3_OP2(op, a, b) asm volatile(op " %0, %0, %1" : "+v"(a) : "v"(b))
 #define B3_ROT(a, n) asm volatile("v_alignbit_b32 %0, %0, %0, " #n : "+v"(a))
