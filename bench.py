@@ -41,8 +41,8 @@ MiB = 1 << 20
 # 39.3 T int32 ops/s.  Measured, not assumed: a wave64 v_add3/v_xor/v_alignbit
 # takes 4 SIMD cycles (rocprofv3: SQ_INSTS_VALU x 4 / 1024 SIMDs = the whole
 # b3_groups duration at the GRBM clock; DESIGN.md §Roofline, profiles/).
-SHA_MODES = {"auto": 0, "split": 1, "pair": 2}
-SHA_PAIR_MAX_CHUNKS = 256 * 4 * 32  # launch_sha256's auto rule (sha256.hip)
+SHA_MODES = {"auto": 0, "split": 1, "pair": 2, "lane": 3}
+SHA_PAIR_MAX_CHUNKS = 256 * 128  # launch_sha256's auto rule (sha256.hip)
 CLOCK_HZ = 2.4e9
 PEAK_INT_OPS = 256 * 4 * 16 * 2.4e9
 PEAK_HBM = 8.0e12
@@ -572,8 +572,9 @@ def main():
                          "the GPU ~30%% slow for ~150 ms after it: profiles/r2/c4-16_warmup_r2u.json)")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--lanes", type=int, default=0, help="leaves per lane (0=auto)")
-    ap.add_argument("--sha-mode", choices=["auto", "split", "pair"], default="auto",
-                    help="SHA-256 kernel: one lane per chunk (split) or two (pair)")
+    ap.add_argument("--sha-mode", choices=["auto", "split", "pair", "lane"], default="auto",
+                    help="SHA-256 kernel: one lane per chunk (lane; split = schedule/round "
+                         "waves) or two (pair)")
     ap.add_argument("--dict-entries", type=int, default=0, help="override dict size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -796,11 +797,16 @@ def main():
         blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).sum())
         ops = blocks * 1384  # SURVEY.md §8(d) SHA-256 op count
         achieved = ops / (dig_ms / 1e3)
-        pair = args.sha_mode == "pair" or (args.sha_mode == "auto" and n <= SHA_PAIR_MAX_CHUNKS)
+        mode = args.sha_mode
+        if mode == "auto":  # launch_sha256's rule
+            mode = "pair" if n <= SHA_PAIR_MAX_CHUNKS else "lane"
+        pair = mode == "pair"
         # SHA-256 is serial within a chunk: with fewer chunks than the chip has
         # lanes, a chunk's round chain (VALU ops on its critical wave, 4 cycles
         # per wave64 op) bounds the kernel, not chip-wide VALU throughput.
-        chain_ops = 66 * 9 if pair else 64 * 14  # VALU ops per block on the round wave
+        # VALU ops per block on the critical wave: pair/split round waves; the
+        # lane kernel's wave does the whole block (schedule + rounds)
+        chain_ops = {"pair": 66 * 9, "split": 64 * 14, "lane": 1384}[mode]
         lanes_used = n * (2 if pair else 1)
         max_blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).max())
         chain_s = max_blocks * chain_ops * 4 / CLOCK_HZ
@@ -808,7 +814,7 @@ def main():
         # (tools/valu_ops.hip, profiles/r1/valu_ops_issue_rates.jsonl); the
         # round wave is alone on its SIMD by design
         lone_s = max_blocks * chain_ops * 5 / CLOCK_HZ
-        roof = {"bound": "valu", "kernel": "sha256_pair" if pair else "sha256_split",
+        roof = {"bound": "valu", "kernel": "sha256_" + mode,
                 "achieved": round(achieved / 1e12, 3),
                 "peak": round(PEAK_INT_OPS / 1e12, 3), "unit": "Tops/s",
                 "frac": round(achieved / PEAK_INT_OPS, 4), "traffic": None,

@@ -102,7 +102,8 @@ typedef struct {
  * (bit0 non-temporal loads, bit1 next-block prefetch); 0 = library default. */
 #define NGPU_FLAG_LOAD_MODE_SHIFT 8
 /* Tuning (benchmarks only): bits 11..13 = 1 + SHA-256 kernel (0: one lane per
- * chunk, 1: two lanes per chunk, 4: two lanes, one chunk group per
+ * chunk with schedule/round waves, 1: two lanes per chunk, 2: one lane per
+ * chunk, each wave schedules its own blocks, 4: two lanes, one chunk group per
  * workgroup, 5: two lanes, four groups per workgroup); 0 = library default
  * (by chunk count); other values are rejected (NGPU_EINVAL). */
 #define NGPU_FLAG_SHA_MODE_SHIFT 11

@@ -172,7 +172,7 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
     HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 16 * sizeof(uint64_t), s));
     if (tm) HIP_TRY(e, hipEventRecord(ev[1], s));
     // tuning override: flags bits 11..13 = 1 + SHA-256 variant (0 split,
-    // 1 pair, 4/5 pair layouts)
+    // 1 pair, 2 lane, 4/5 pair layouts)
     const uint32_t sv = (e->cfg.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7;
     launch_sha256(d_data, len, d_chunks, n, d_out, e->ws.stats + 7, sv ? (int)sv - 1 : -1, s);
     if (tm) {
@@ -309,10 +309,10 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   if (c.fs_version != 5 && c.fs_version != 6) return NGPU_EINVAL;
   if (c.digester != NGPU_DIGEST_BLAKE3 && c.digester != NGPU_DIGEST_SHA256) return NGPU_EINVAL;
   if (c.leaves_per_lane & (c.leaves_per_lane - 1) || c.leaves_per_lane > 16) return NGPU_EINVAL;
-  // SHA-256 kernel override (benchmarks): 1 + {0 split, 1 pair, 4 pair one
-  // group per workgroup, 5 pair four groups}; anything else is rejected
+  // SHA-256 kernel override (benchmarks): 1 + {0 split, 1 pair, 2 lane, 4 pair
+  // one group per workgroup, 5 pair four groups}; anything else is rejected
   switch ((c.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7) {
-    case 0: case 1: case 2: case 5: case 6: break;
+    case 0: case 1: case 2: case 3: case 5: case 6: break;
     default: return NGPU_EINVAL;
   }
   int ndev = 0;

@@ -32,6 +32,10 @@ __device__ __forceinline__ uint32_t bswap(uint32_t x) {
   return __builtin_amdgcn_perm(x, x, 0x00010203u);
 }
 
+__device__ __forceinline__ uint32_t bswap_words(u32x4 v, int i) {
+  return bswap(i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
+}
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // symmetric truth table
 }
@@ -208,6 +212,58 @@ __global__ __launch_bounds__(128) void sha256_split(
   }
 }
 
+// One lane per chunk and no wave specialisation: each lane expands its own
+// message schedule and runs the rounds (sha_block), with the next block
+// prefetched into registers.  No LDS and no barrier, so occupancy is set by
+// registers alone (8 waves per SIMD), and with >= 4 chunk waves per SIMD
+// (many-chunk layers, e.g. 64 KiB chunks) the SIMD issues at its full rate
+// instead of leaving a schedule wave's SIMD half idle.
+__global__ __launch_bounds__(256) void sha256_lane(
+    const uint8_t *__restrict__ data, uint64_t data_len,
+    const ngpu_chunk *__restrict__ chunks, uint64_t n,
+    ngpu_result *__restrict__ out, uint64_t *__restrict__ err) {
+  const uint64_t c = blockIdx.x * 256ull + threadIdx.x;
+  if (c >= n) return;
+  const ngpu_chunk ch = chunks[c];
+  if (ch.offset > data_len || ch.length > data_len - ch.offset) {
+    atomicAdd((unsigned long long *)err, 1ull);
+    return;
+  }
+  const uint32_t len = ch.length;
+  const uint8_t *p = data + ch.offset;
+  const uint32_t nb = (len + 8) / 64 + 1, full = len >> 6;
+  const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  u32x4 pf0 = {}, pf1 = {}, pf2 = {}, pf3 = {};
+  bool have_pf = false;
+  auto prefetch = [&](uint32_t b) {
+    have_pf = aligned && b < full;
+    if (have_pf) {
+      const u32x4 *q = reinterpret_cast<const u32x4 *>(p + 64ull * b);
+      pf0 = q[0]; pf1 = q[1]; pf2 = q[2]; pf3 = q[3];
+    }
+  };
+  prefetch(0);
+  for (uint32_t b = 0; b < nb; ++b) {
+    uint32_t w[16];
+    if (have_pf) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        w[i] = bswap_words(pf0, i); w[4 + i] = bswap_words(pf1, i);
+        w[8 + i] = bswap_words(pf2, i); w[12 + i] = bswap_words(pf3, i);
+      }
+    } else {
+      sha_load_block(p, len, b, w);
+    }
+    prefetch(b + 1);
+    sha_block(h, w);
+  }
+  uint4 *dd = reinterpret_cast<uint4 *>(out[c].digest);
+  dd[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
+  dd[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
+}
+
 // Two lanes per chunk for the rounds (few, long chunks: the per-chunk round
 // chain is the whole critical path, so shortening it is the only lever once
 // every chunk has a lane).
@@ -236,10 +292,6 @@ __global__ __launch_bounds__(128) void sha256_split(
 // with the next pair of blocks prefetched into registers.  KW[set][half][chunk][t]
 // in LDS; chunk row 32 holds the constant 1 the A lanes add (~x + 1 = -x).
 constexpr uint32_t kDppRowRor8 = 0x128;
-
-__device__ __forceinline__ uint32_t bswap_words(u32x4 v, int i) {
-  return bswap(i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
-}
 
 // R round waves + R schedule waves per workgroup (R groups of 32 chunks), so
 // one workgroup per CU puts every wave on its own SIMD.
@@ -398,11 +450,20 @@ void launch_sha256(const uint8_t *data, uint64_t data_len,
                    const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
                    uint64_t *err, int variant, hipStream_t s) {
   if (n == 0) return;
-  // Auto: two lanes per chunk while one lane per chunk leaves SIMDs idle
-  // (<= one round wave per SIMD: 256 CUs x 4 SIMDs x 32 chunks).  Measured
-  // (profiles/r1/sha_variants.jsonl): 16384 x 1 MiB chunks 785 vs 538 GB/s,
-  // 65536 x 256 KiB chunks 989 vs 1111 GB/s.
-  if (variant < 0) variant = n <= 256ull * 4 * 32 ? 1 : 0;
+  // Auto (same-box sweep, profiles/r2/sha_variants_lane_r2sl.jsonl, GB/s):
+  //  * <= 16384 chunks (one 64-chunk workgroup per CU): two lanes per chunk,
+  //    each round wave alone on its SIMD; 16384 x 1 MiB: pair 786, lane 385.
+  //  * <= 32768 chunks: two lanes per chunk, four groups per workgroup (one
+  //    workgroup per CU, a round and a schedule wave on each SIMD); 32768 x
+  //    512 KiB: 1343, against 950 for two 2-group workgroups per CU.
+  //  * more: one lane per chunk, every wave doing its own schedule;
+  //    65536 x 256 KiB lane 1512 / pair-4 1342, 262144 x 64 KiB 1657 / split 1190.
+  if (variant < 0) variant = n <= 256ull * 64 ? 1 : n <= 256ull * 128 ? 5 : 2;
+  if (variant == 2) {
+    hipLaunchKernelGGL(sha256_lane, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, data,
+                       data_len, chunks, n, out, err);
+    return;
+  }
   if (variant >= 1) {
     const dim3 g2((unsigned)((n + 63) / 64)), g1((unsigned)((n + 31) / 32));
     switch (variant) {

@@ -15,10 +15,12 @@ pytestmark = pytest.mark.gpu
 
 LANES = [1, 2, 4, 8, 16]
 # SHA-256 kernels, forced through ngpu_config.flags bits 11..12 (1 + variant):
-# 0 = auto, one lane per chunk ("split"), two lanes per chunk ("pair").
-# "pair" runs two chunk groups per workgroup; 5 forces one group per workgroup.
-SHA_SPLIT, SHA_PAIR, SHA_PAIR_R1 = 1 << 11, 2 << 11, 5 << 11
-SHA_FLAGS = [0, SHA_SPLIT, SHA_PAIR, SHA_PAIR_R1]
+# 0 = auto, one lane per chunk ("split": schedule/round waves; "lane": one wave
+# does both), two lanes per chunk ("pair").
+# "pair" runs two chunk groups per workgroup; 5 forces one group, 6 four groups.
+SHA_SPLIT, SHA_PAIR, SHA_LANE = 1 << 11, 2 << 11, 3 << 11
+SHA_PAIR_R1, SHA_PAIR_R4 = 5 << 11, 6 << 11
+SHA_FLAGS = [0, SHA_SPLIT, SHA_PAIR, SHA_LANE, SHA_PAIR_R1, SHA_PAIR_R4]
 # Calls with <= 4096 chunks plan and dedup in one fused workgroup; this flag
 # forces the multi-kernel grid path, so both are checked on the same inputs.
 GRID = nydus_gpu.FLAG_GRID_STAGES
@@ -201,7 +203,7 @@ def test_random_vs_oracle(engines, oracle, seed, chunk_size, unaligned, total):
             assert st["new_chunks"] == int((exp["kind"] == 0).sum())
 
 
-@pytest.mark.parametrize("fl", [SHA_SPLIT, SHA_PAIR, SHA_PAIR_R1])
+@pytest.mark.parametrize("fl", [SHA_SPLIT, SHA_PAIR, SHA_LANE, SHA_PAIR_R1, SHA_PAIR_R4])
 def test_sha256_ragged_wave(engines, oracle, fl):
     """Chunks of very different block counts in one wave (lanes finish at
     different blocks), lengths around the 55/56/64-byte padding edges, odd

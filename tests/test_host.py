@@ -72,6 +72,12 @@ def test_engine_option_validation():
         with pytest.raises(nydus_gpu.NgpuError) as e:
             nydus_gpu.Engine(chunk_size=bad)
         assert e.value.code == -1
+    # SHA-256 kernel override: field = 1 + {0, 1, 2, 4, 5}; fields 4 and 7
+    # (no such kernel) are rejected before any device call
+    for bad in (4 << 11, 7 << 11):
+        with pytest.raises(nydus_gpu.NgpuError) as e:
+            nydus_gpu.Engine(digester="sha256", flags=bad)
+        assert e.value.code == -1
 
 
 def test_v6_fixture_layout():

@@ -1,5 +1,4 @@
-"""SHA-256 kernel timing by variant (diagnostics: variants 2/3 give wrong
-digests).  python tools/sha_diag.py [chunk_size]"""
+"""SHA-256 kernel timing by variant.  python tools/sha_diag.py [chunk_size]"""
 import json
 import sys
 
@@ -20,7 +19,7 @@ ch["length"] = S
 d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
 d_out = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
 ref = None
-for v, name in [(1, "split"), (2, "pair"), (5, "pair-r1"), (6, "pair-r4"), (3, "pair-nodpp"), (4, "pair-nosched")]:
+for v, name in [(1, "split"), (2, "pair"), (3, "lane"), (5, "pair-r1"), (6, "pair-r4")]:
     eng = nydus_gpu.Engine(digester="sha256", chunk_size=S, flags=v << 11)
     s = torch.cuda.Stream()
     for _ in range(2):
