@@ -578,6 +578,9 @@ def main():
     ap.add_argument("--dict-entries", type=int, default=0, help="override dict size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--d2h", choices=["auto", "same", "copy"], default="auto",
+                    help="result-table D2H: on the call's stream (same) or on a copy stream "
+                         "overlapping the next step (copy); auto = same below 1 MiB of results")
     ap.add_argument("--e2e-mib", type=int, default=2048, help="PCIe-inclusive sample size")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on a node; gloo to "
                     "rehearse several ranks on one GPU")
@@ -704,7 +707,10 @@ def main():
     # Results go back to the host on a copy stream, double-buffered: the D2H of
     # step k's result table overlaps step k+1's kernels, as in a pipeline over
     # many layers (C5-shape: a 16 MiB table, ~0.3 ms of PCIe per step).
-    d_outs = [d_out, torch.empty_like(d_out)]
+    # A small table (C1: 7 KB) goes back on the call's own stream: the copy
+    # stream's two cross-stream waits and event markers cost more than the copy.
+    same_d2h = args.d2h == "same" or (args.d2h == "auto" and d_out.numel() < (1 << 20))
+    d_outs = [d_out, d_out if same_d2h else torch.empty_like(d_out)]
     h_outs = [h_out, torch.empty_like(h_out).pin_memory()]
     copy_stream = torch.cuda.Stream()
     copy_done = [None, None]
@@ -730,6 +736,9 @@ def main():
                                         n_layers, d_lstats.data_ptr(),
                                         d_hits=hits.data_ptr() if hits is not None else 0,
                                         n_dict_blobs=8 if hits is not None else 0, stream=s)
+            if same_d2h:
+                h_outs[k].copy_(dout, non_blocking=True)
+                return
             done = torch.cuda.Event()
             done.record(stream)
         with torch.cuda.stream(copy_stream):
@@ -861,7 +870,8 @@ def main():
         "config": {"workload": wl["desc"], "name": args.workload,
                    "layer_bytes": int(buf.numel()), "file_bytes_per_gpu": file_bytes, "chunks": n,
                    "chunk_size": wl["chunk"], "digester": wl["digester"], "layers_per_gpu": n_layers,
-                   "leaves_per_lane": 1 << D, "parallelism": f"layer-sharded x{world}"},
+                   "leaves_per_lane": 1 << D, "parallelism": f"layer-sharded x{world}",
+                   "result_d2h": "call stream" if same_d2h else "copy stream, overlapped"},
         "stage_ms": {"digest": round(dig_ms, 3), "tree": round(tree_ms, 3), "dedup": round(dedup_ms, 3),
                      "digest_min_med_max": [round(float(f(dig_all)), 3)
                                             for f in (np.min, np.median, np.max)]},

@@ -893,9 +893,16 @@ __global__ __launch_bounds__(kQuadThreads) void b3_quad_leaves(
   }
 }
 
-constexpr int kTreeThreads = 256;
+// 1024 threads = 256 quads: every level of a 1024-CV tile (<= 512 parents)
+// runs as compress_quad in at most two passes.  A chain of ~10 levels is the
+// kernel's whole time on small layers (a 1 MiB chunk = 1024 leaves): with 256
+// threads the two widest levels ran one 680-op compression per lane (2 and 1
+// per lane), ~6.8 K issued ops against 2 x 190 here (C1 tree 18.8 -> see
+// DESIGN.md §b3_quad_leaves).
+constexpr int kTreeThreads = 1024;
 constexpr uint32_t kTreeQuads = kTreeThreads / 4;
 constexpr int kTile = 1024;  // CVs per LDS tile (32 KiB)
+static_assert(kTile / 2 <= 2 * kTreeQuads, "a tile level is at most two quad passes");
 
 // all_queued: every multi-group chunk was queued (b3_quad_leaves), none was
 // finished inside a b3_groups workgroup.
@@ -905,8 +912,8 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
     uint32_t *__restrict__ cv, ngpu_result *__restrict__ out, bool all_queued) {
   __shared__ uint32_t t[kTile * 8];
   const int tid = threadIdx.x;
-  // quad lanes for the narrow levels (<= 2 parents per quad): this lane's
-  // column and schedule word offsets in a parent's 16-word message
+  // a quad of lanes per parent: this lane's column and schedule word offsets
+  // in a parent's 16-word message (the two child CVs, adjacent in t)
   const uint32_t qlane = tid & 3, qid = tid >> 2;
   uint32_t wo[28];
 #pragma unroll
@@ -933,56 +940,18 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
         while (cnt > 1) {
           const uint32_t p = cnt >> 1;
           const uint32_t pflags = PARENT | ((final_pass && cnt == 2) ? ROOT : 0);
-          if (p <= 2 * kTreeQuads) {
-            // Narrow level: a quad of lanes per parent (compress_quad), its
-            // message being the two child CVs already adjacent in t.
-            uint32_t rx[2], ry[2];
-            const uint32_t dq = qlane == 2 ? 64u : qlane == 3 ? pflags : 0u;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const uint32_t pi = qid + s * kTreeQuads;
-              if (pi < p) {
-                uint32_t m[28];
-#pragma unroll
-                for (int k2 = 0; k2 < 28; ++k2) m[k2] = t[16 * pi + wo[k2]];
-                rx[s] = ivq;
-                ry[s] = ivh;
-                compress_quad(rx[s], ry[s], m, ivq, dq);
-              }
-            }
-            uint32_t odd[8];
-            const bool has_odd = (cnt & 1) && tid == 0;
-            if (has_odd) {
-#pragma unroll
-              for (int i = 0; i < 8; ++i) odd[i] = t[8 * (cnt - 1) + i];
-            }
-            __syncthreads();
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const uint32_t pi = qid + s * kTreeQuads;
-              if (pi < p) {
-                t[8 * pi + qlane] = rx[s];
-                t[8 * pi + 4 + qlane] = ry[s];
-              }
-            }
-            if (has_odd) {
-#pragma unroll
-              for (int i = 0; i < 8; ++i) t[8 * p + i] = odd[i];
-            }
-            __syncthreads();
-            cnt = p + (cnt & 1);
-            continue;
-          }
-          uint32_t r[2][8];
+          const uint32_t dq = qlane == 2 ? 64u : qlane == 3 ? pflags : 0u;
+          uint32_t rx[2], ry[2];
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const uint32_t q = tid + s * kTreeThreads;
-            if (q < p) {
-              uint32_t m[16];
+            const uint32_t pi = qid + s * kTreeQuads;
+            if (pi < p) {
+              uint32_t m[28];
 #pragma unroll
-              for (int i = 0; i < 16; ++i) m[i] = t[16 * q + i];
-              set_iv(r[s]);
-              compress(r[s], m, 0, 64, pflags);
+              for (int k2 = 0; k2 < 28; ++k2) m[k2] = t[16 * pi + wo[k2]];
+              rx[s] = ivq;
+              ry[s] = ivh;
+              compress_quad(rx[s], ry[s], m, ivq, dq);
             }
           }
           uint32_t odd[8];
@@ -994,10 +963,10 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
           __syncthreads();
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const uint32_t q = tid + s * kTreeThreads;
-            if (q < p) {
-#pragma unroll
-              for (int i = 0; i < 8; ++i) t[8 * q + i] = r[s][i];
+            const uint32_t pi = qid + s * kTreeQuads;
+            if (pi < p) {
+              t[8 * pi + qlane] = rx[s];
+              t[8 * pi + 4 + qlane] = ry[s];
             }
           }
           if (has_odd) {

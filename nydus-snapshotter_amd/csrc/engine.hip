@@ -129,15 +129,37 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
   return 0;
 }
 
+#ifndef NGPU_EVENT_FENCE
+#define NGPU_EVENT_FENCE hipEventDisableSystemFence
+#endif
+
 int ws_acquire(ngpu_engine *e, hipStream_t s) {
-  if (e->ws_pending && e->ws_last != s) HIP_TRY(e, hipStreamWaitEvent(s, e->ws_last_ev, 0));
+  if (!e->ws_pending || e->ws_last == s) return 0;
+  if (!e->ws_last_ev) {  // a lazy stage end (ws_lazy_end): record it now
+    HIP_TRY(e, hipEventRecord(e->ws_done, e->ws_last));
+    e->ws_last_ev = e->ws_done;
+  }
+  HIP_TRY(e, hipStreamWaitEvent(s, e->ws_last_ev, 0));
   return 0;
 }
 
+// A kernel that carries an event (a stop event of hipExtLaunchKernelGGL, or a
+// marker after it) holds the next kernel on its stream back by ~4.4 us
+// (rocprofv3 trace of back-to-back C1 calls), so a stage binds no end event
+// when none is needed yet:
+//  * chained: the next stage of the same call follows on the same stream;
+//  * s is the engine's own stream, which lives as long as the engine, so the
+//    event can be recorded later, by the ws_acquire of a stage on another
+//    stream (recorded then, it also covers later work on s: safe, not tight).
+bool ws_lazy_end(const ngpu_engine *e, hipStream_t s, bool chained) {
+  return chained || (s && s == e->stream);
+}
+
 // bound: an event the stage's last kernel already records at its end (a
-// stop event of hipExtLaunchKernelGGL), or null to record ws_done now.
-int ws_release(ngpu_engine *e, hipStream_t s, hipEvent_t bound) {
-  if (!bound) {
+// stop event of hipExtLaunchKernelGGL), or null to record ws_done now --
+// unless the end may be lazy (ws_lazy_end), then ws_acquire records it.
+int ws_release(ngpu_engine *e, hipStream_t s, hipEvent_t bound, bool chained) {
+  if (!bound && !ws_lazy_end(e, s, chained)) {
     HIP_TRY(e, hipEventRecord(e->ws_done, s));
     bound = e->ws_done;
   }
@@ -150,7 +172,7 @@ int ws_release(ngpu_engine *e, hipStream_t s, hipEvent_t bound) {
 // Digest stage: resets the layer stats, runs the digest kernels.
 int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
                    const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
-                   hipStream_t s) {
+                   hipStream_t s, bool chained) {
   const int D = pick_group_log2(e, len);
   int rc = ensure_workspace(e, n, len, D, 0, 1);
   if (rc) return rc;
@@ -182,13 +204,13 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
     }
   } else {
     // events ride on the kernels: no marker packets between the launches
-    hipEvent_t end = tm ? ev[3] : e->ws_done;
+    hipEvent_t end = tm ? ev[3] : ws_lazy_end(e, s, chained) ? nullptr : e->ws_done;
     if (launch_blake3(d_data, d_chunks, n, len, D, e->ws, d_out, s, tm ? ev[0] : nullptr,
                       tm ? ev[1] : nullptr, tm ? ev[2] : nullptr, end))
       bound = end;
   }
   HIP_TRY(e, hipGetLastError());
-  if ((rc = ws_release(e, s, bound))) return rc;
+  if ((rc = ws_release(e, s, bound, chained))) return rc;
   return 0;
 }
 
@@ -215,20 +237,31 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chu
       (e->cfg.fs_version == 6 || (e->cfg.flags & NGPU_FLAG_ALIGNED_CHUNK)) ? 4096u : 1u;
   // d_lfirst == nullptr: the init kernel writes {0, n} into ws.lfirst1
   // the last dedup kernel records the stage end (timing slot or ws_done)
-  hipEvent_t end = tm && e->tcalls ? e->ev[e->tslot][4] : e->ws_done;
+  hipEvent_t end = tm && e->tcalls      ? e->ev[e->tslot][4]
+                   : ws_lazy_end(e, s, false) ? nullptr
+                                              : e->ws_done;
   launch_dedup(d_chunks, n, dict ? dict->dev : DictDevice{}, d_hits, n_blobs, align, d_lfirst, L,
                e->ws, d_out, d_stats, s, end);
   HIP_TRY(e, hipGetLastError());
   if (tm && e->tcalls) e->timed[e->tslot] = n > 0;
-  if ((rc = ws_release(e, s, end))) return rc;
+  if ((rc = ws_release(e, s, end, false))) return rc;
   return 0;
+}
+
+int enqueue_chain(ngpu_engine *e, const ngpu_dict *dict, const uint8_t *d_data, uint64_t len,
+                  const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out, hipStream_t s,
+                  const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats) {
+  int rc = enqueue_digest(e, d_data, len, d_chunks, n, d_out, s, true);
+  if (rc) return rc;
+  rc = enqueue_dedup(e, dict, d_chunks, n, d_out, nullptr, 0, s, d_lfirst, L, d_stats);
+  // the chained digest left its end unrecorded: s may be gone after the call
+  if (rc) (void)ws_release(e, s, nullptr, false);
+  return rc;
 }
 
 int enqueue(ngpu_engine *e, const ngpu_dict *dict, const uint8_t *d_data, uint64_t len,
             const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out, hipStream_t s) {
-  int rc = enqueue_digest(e, d_data, len, d_chunks, n, d_out, s);
-  if (rc) return rc;
-  return enqueue_dedup(e, dict, d_chunks, n, d_out, nullptr, 0, s, nullptr, 1, nullptr);
+  return enqueue_chain(e, dict, d_data, len, d_chunks, n, d_out, s, nullptr, 1, nullptr);
 }
 
 void engine_ref(ngpu_engine *e) { e->refs.fetch_add(1, std::memory_order_relaxed); }
@@ -326,14 +359,19 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   e->ws.grid_stages = (c.flags & NGPU_FLAG_GRID_STAGES) != 0;
   e->device = c.device;
   DeviceGuard dg(c.device);
+  // The engine's events order work on this device only (stage ends, timing):
+  // no system-scope fence, which writes back the caches when a kernel that
+  // carries the event ends and holds the next kernel back by ~4.4 us.  Host
+  // reads of results go through stream-ordered copies + stream syncs.
   if (c.flags & NGPU_FLAG_TIMING)
     for (auto &set : e->ev)
       for (auto &ev : set)
-        if (hipEventCreate(&ev) != hipSuccess) {
+        if (hipEventCreateWithFlags(&ev, NGPU_EVENT_FENCE) != hipSuccess) {
           ngpu_destroy(e);
           return NGPU_EHIP;
         }
-  if (hipEventCreateWithFlags(&e->ws_done, hipEventDisableTiming) != hipSuccess ||
+  if (hipEventCreateWithFlags(&e->ws_done, hipEventDisableTiming | NGPU_EVENT_FENCE) !=
+          hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void **)&e->h_stats, 32 * sizeof(uint64_t), hipHostMallocDefault) !=
           hipSuccess) {
@@ -438,10 +476,8 @@ static int process_device(ngpu_engine *e, ngpu_dict *dict, const void *d_data, u
   if (dict == kDefault) dict = e->dict;
   if (int rc = dict_check(e, dict)) return rc;
   hipStream_t s = dev_stream(stream);
-  int rc = enqueue_digest(e, (const uint8_t *)d_data, len, d_chunks, n, d_out, s);
-  if (rc) return rc;
-  rc = enqueue_dedup(e, dict, d_chunks, n, d_out, nullptr, 0, s, d_layer_first,
-                     d_layer_first ? n_layers : 1, d_stats);
+  int rc = enqueue_chain(e, dict, (const uint8_t *)d_data, len, d_chunks, n, d_out, s,
+                         d_layer_first, d_layer_first ? n_layers : 1, d_stats);
   if (rc) return rc;
   if (stats) return read_stats(e, s, stats);
   return 0;

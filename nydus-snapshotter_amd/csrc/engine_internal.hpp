@@ -86,9 +86,11 @@ struct ngpu_engine {
   int slot_D[kTimingRing] = {};
   uint64_t tcalls = 0;  // calls recorded so far; the current slot is (tcalls - 1) % ring
   int tslot = 0;
-  // Workspace ordering across streams: every stage that uses `ws` records
-  // ws_done on its stream; a stage on another stream waits for it first, so
-  // calls on different streams never run over one workspace concurrently.
+  // Workspace ordering across streams: every stage that uses `ws` ends with
+  // an event on its stream (ws_last_ev; null = not recorded yet, only while
+  // ws_last is the engine's own stream); a stage on another stream waits for
+  // it first, so calls on different streams never run over one workspace
+  // concurrently.
   hipEvent_t ws_done = nullptr;
   hipEvent_t ws_last_ev = nullptr;  // the event that ended the last stage
   hipStream_t ws_last = nullptr;
@@ -107,8 +109,11 @@ int fail(ngpu_engine *e, int code, const char *fmt, ...);
 int pick_group_log2(const ngpu_engine *e, uint64_t data_len);
 int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D, uint32_t n_blobs,
                      uint64_t L);
+// chained: the caller enqueues the dedup stage next on the same stream (under
+// the same lock), so the digest stage binds no end event (ws_lazy_end).
 int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
-                   const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out, hipStream_t s);
+                   const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out, hipStream_t s,
+                   bool chained = false);
 // d_hits == nullptr: probe `dict` (may be null: no chunk dict).
 // d_lfirst == nullptr: one layer of n chunks (stats -> internal lstats[0]).
 int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chunks, uint64_t n,
@@ -117,8 +122,16 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chu
 int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st);
 // Order a workspace stage on stream s after the previous one (any stream).
 int ws_acquire(ngpu_engine *e, hipStream_t s);
-// bound: the stage-end event its last kernel records (null: record ws_done).
-int ws_release(ngpu_engine *e, hipStream_t s, hipEvent_t bound);
+// Digest then dedup on one stream (digest chained).
+int enqueue_chain(ngpu_engine *e, const ngpu_dict *dict, const uint8_t *d_data, uint64_t len,
+                  const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out, hipStream_t s,
+                  const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats);
+// May the stage on s leave its end event unrecorded (chained, or s is the
+// engine's own stream)?  ws_acquire records it when another stream needs it.
+bool ws_lazy_end(const ngpu_engine *e, hipStream_t s, bool chained);
+// bound: the stage-end event its last kernel records (null: record ws_done,
+// or nothing when ws_lazy_end).
+int ws_release(ngpu_engine *e, hipStream_t s, hipEvent_t bound, bool chained);
 
 // Reference counts.  engine_unref frees the engine when the last holder (the
 // creator's ngpu_destroy or the last open pack) lets go.

@@ -109,3 +109,61 @@ def test_calls_on_different_streams_share_the_workspace_in_order():
                 assert np.array_equal(got[f], dec[f]), (k, f)
     finally:
         eng.close()
+
+
+def test_pack_on_engine_stream_interleaved_with_device_calls(oracle):
+    """Streaming Pack runs on the engine's own stream, whose stage ends are
+    recorded lazily (only when a stage on another stream needs the
+    workspace).  Pack writes and device-path calls on a caller stream,
+    alternated with no host sync: both results equal the oracle's."""
+    import io
+    import tarfile
+    import nydus_gpu
+    S = 64 << 10
+    rng = np.random.default_rng(5)
+    bio = io.BytesIO()
+    tf = tarfile.open(fileobj=bio, mode="w", format=tarfile.GNU_FORMAT)
+    for i in range(40):
+        n = int(rng.choice([0, 700, 70000, 1 << 20]) + rng.integers(0, 5000))
+        ti = tarfile.TarInfo(f"f{i}")
+        ti.size = n
+        tf.addfile(ti, io.BytesIO(rng.integers(0, 256, n, dtype=np.uint8).tobytes()))
+    tf.close()
+    tb = bio.getvalue()
+    P = 700
+    ch = np.zeros(P, nydus_gpu.CHUNK_DTYPE)
+    ch["length"] = rng.integers(1, S + 1, P)
+    ch["offset"] = np.arange(P, dtype=np.uint64) * S
+    data = rng.integers(0, 256, P * S, dtype=np.uint8)
+    dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    dec, _ = oracle.dedup(dig, ch["length"])
+    d_data = torch.from_numpy(data).cuda()
+    d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+    s = torch.cuda.Stream()
+    eng = nydus_gpu.Engine(device=0, digester="blake3", chunk_size=S, staging_bytes=1 << 20)
+    try:
+        torch.cuda.synchronize()
+        w = eng.pack()
+        outs = []
+        for pos in range(0, len(tb), 300 << 10):
+            w.write(tb[pos:pos + (300 << 10)])
+            out = torch.zeros(P * 64, dtype=torch.uint8, device="cuda")
+            eng.process_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), P,
+                               out.data_ptr(), stream=s.cuda_stream)
+            outs.append(out)
+        pch, pout, _ = w.close()
+        torch.cuda.synchronize()
+    finally:
+        eng.close()
+    for k, out in enumerate(outs):
+        got = out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+        assert np.array_equal(got["digest"], dig), k
+        for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+            assert np.array_equal(got[f], dec[f]), (k, f)
+    ref_ch = oracle.tar_chunks(tb, S)
+    assert pch.tobytes() == ref_ch.tobytes()
+    pdig = oracle.digest_chunks(tb, ref_ch, "blake3")
+    assert np.array_equal(pout["digest"], pdig)
+    pdec, _ = oracle.dedup(pdig, ref_ch["length"])
+    for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+        assert np.array_equal(pout[f], pdec[f]), f
