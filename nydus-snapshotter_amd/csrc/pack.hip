@@ -47,6 +47,7 @@ struct Slot {
   ngpu_chunk *h_ch = nullptr; // pinned slot-relative descriptors
   ngpu_chunk *d_ch = nullptr;
   uint64_t base = 0, fill = 0;
+  uint64_t sent = 0;          // bytes [0, sent) already queued H2D (eager copies)
   hipEvent_t copied = nullptr, done = nullptr;
   bool busy = false;
 };
@@ -256,7 +257,12 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
     p->segs.push_back(g);
     dev = g.d;
   }
-  HIP_TRY(e, hipMemcpyAsync(dev, s.h, s.fill, hipMemcpyHostToDevice, p->copy));
+  // bytes [0, sent) went H2D as they were committed (eager_copy); the copy
+  // stream is in order, so s.copied covers them too
+  const uint64_t from = p->retain ? 0 : s.sent;
+  if (s.fill > from)
+    HIP_TRY(e, hipMemcpyAsync(dev + from, s.h + from, s.fill - from, hipMemcpyHostToDevice, p->copy));
+  s.sent = s.fill;
   HIP_TRY(e, hipMemcpyAsync(s.d_ch, s.h_ch, nch * sizeof(ngpu_chunk), hipMemcpyHostToDevice,
                             p->copy));
   HIP_TRY(e, hipEventRecord(s.copied, p->copy));
@@ -289,7 +295,24 @@ int switch_slot(ngpu_pack *p) {
   memcpy(t.h, s.h + (carry_from - s.base), carry);
   t.base = carry_from;
   t.fill = carry;
+  t.sent = 0;
   p->cur ^= 1;
+  return 0;
+}
+
+// Queue the slot's newly committed bytes H2D once kEagerCopy of them have
+// gathered, so the layer's copy runs while the caller is still writing and
+// only the tail is left for the dispatch (C1 through 1 MiB writes: the whole
+// 10 MB copy used to start at close).  Not with NGPU_PACK_RETAIN, whose
+// device segment is sized and allocated at dispatch.
+constexpr uint64_t kEagerCopy = 1ull << 20;
+
+int eager_copy(ngpu_pack *p, Slot &s) {
+  if (p->retain || s.fill - s.sent < kEagerCopy) return 0;
+  DeviceGuard dg(p->e->device);
+  HIP_TRY(p->e, hipMemcpyAsync(s.d + s.sent, s.h + s.sent, s.fill - s.sent, hipMemcpyHostToDevice,
+                               p->copy));
+  s.sent = s.fill;
   return 0;
 }
 
@@ -536,8 +559,9 @@ int ngpu_pack_commit(ngpu_pack *p, uint64_t n) {
   if (cancelled(p)) return p->err = fail(p->e, NGPU_ECANCELED, "pack: cancelled");
   Slot &s = p->slot[p->cur];
   if (n > p->cap - s.fill) return p->err = NGPU_EINVAL;
-  const int rc = guarded([&] { return p->sc.feed(s.h + s.fill, n, *p); });
+  int rc = guarded([&] { return p->sc.feed(s.h + s.fill, n, *p); });
   s.fill += n;
+  if (!rc) rc = eager_copy(p, s);
   if (rc) return p->err = rc;
   return 0;
 }
