@@ -739,6 +739,9 @@ constexpr int kQuadThreads = 256;           // 64 quads = 64 leaves per workgrou
 // lane-per-leaf path (profiles/r2/quad_threshold_r2qt.json, digest ms, lane vs
 // quad): 8 MiB 0.030 / 0.018, 16 MiB 0.030 / 0.020, 32 MiB 0.033 / 0.026,
 // 48 MiB 0.033 / 0.032, 64 MiB equal.
+#ifndef B3_QUAD_PF
+#define B3_QUAD_PF 1
+#endif
 #ifndef B3_QUAD_MAX_LEAVES
 #define B3_QUAD_MAX_LEAVES 32768
 #endif
@@ -861,10 +864,27 @@ __global__ __launch_bounds__(kQuadThreads) void b3_quad_leaves(
   const uint32_t ivq = q == 0 ? iv_lo[0] : q == 1 ? iv_lo[1] : q == 2 ? iv_lo[2] : iv_lo[3];
   uint32_t x = ivq, y = q == 0 ? iv_hi[0] : q == 1 ? iv_hi[1] : q == 2 ? iv_hi[2] : iv_hi[3];
   auto valid = [&](uint32_t b) { return (int)min(16u, (uint32_t)max(0, (int)llen - (int)(64 * b + 16 * q))); };
+#if B3_QUAD_PF
+  // the whole leaf in flight at once (16 x 16 B per lane): one memory latency
+  // per leaf instead of one per block behind a one-block prefetch
+  u32x4 wb[16];
+  if (llen == kLeaf && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+#pragma unroll
+    for (int b = 0; b < 16; ++b) wb[b] = *reinterpret_cast<const u32x4 *>(src + 64 * b);
+  } else {
+#pragma unroll
+    for (int b = 0; b < 16; ++b) wb[b] = (uint32_t)b < nb ? load16(src + 64 * b, valid(b)) : u32x4{};
+  }
+#pragma unroll
+  for (uint32_t b = 0; b < 16; ++b) {
+    if (b >= nb) continue;  // (not break: keeps the loop unrolled, wb in registers)
+    const u32x4 w = wb[b];
+#else
   u32x4 w = load16(src, valid(0));
   for (uint32_t b = 0; b < nb; ++b) {
     u32x4 nx = w;
     if (b + 1 < nb) nx = load16(src + 64 * (b + 1), valid(b + 1));  // next block in flight
+#endif
     *reinterpret_cast<u32x4 *>(blk + 4 * q) = w;
     // the quad's four stores are in this wave's LDS queue ahead of its loads
     asm volatile("" ::: "memory");
@@ -877,7 +897,9 @@ __global__ __launch_bounds__(kQuadThreads) void b3_quad_leaves(
                            (b + 1 == nb ? (CHUNK_END | (root_group ? ROOT : 0u)) : 0u);
     const uint32_t dq = q == 0 ? j : q == 1 ? 0u : q == 2 ? bl : flags;
     compress_quad(x, y, m, ivq, dq);
+#if !B3_QUAD_PF
     w = nx;
+#endif
   }
   if (root_group) {
     uint32_t *d = reinterpret_cast<uint32_t *>(out[c].digest);

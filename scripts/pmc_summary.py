@@ -24,7 +24,7 @@ def main():
             for r in csv.DictReader(open(f)):
                 if not pat.search(r["Kernel_Name"]):
                     continue
-                m = re.search(r"(b3_groups<[^>]*>|sha256_\w+)", r["Kernel_Name"])
+                m = re.search(r"(b3_groups<[^>]*>|b3_quad_leaves|sha256_\w+)", r["Kernel_Name"])
                 name = m.group(1) if m else r["Kernel_Name"]
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
                 durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
