@@ -316,12 +316,11 @@ __global__ void dedup_probe_insert(const ngpu_chunk *__restrict__ chunks, uint64
 // scan turns into prefixes: NEW flag, v6-aligned size, NEW bytes, DICT flag.
 // Per-layer figures are differences of these prefixes at layer boundaries,
 // so no per-layer atomics are needed anywhere.
-__device__ __forceinline__ void resolve_item(
+__device__ __forceinline__ void resolve_values(
     uint64_t c, const ngpu_chunk *__restrict__ chunks, const uint32_t *__restrict__ chunk_layer,
     const uint64_t *__restrict__ table, uint64_t mask, ngpu_result *__restrict__ out,
-    uint32_t align, uint64_t *__restrict__ newidx, uint64_t *__restrict__ uoff,
-    uint64_t *__restrict__ nbytes, uint64_t *__restrict__ ndict) {
-  uint64_t v[kDedupScans] = {0, 0, 0, 0};  // NEW, aligned size, bytes, DICT
+    uint32_t align, uint64_t v[kDedupScans]) {
+  v[0] = v[1] = v[2] = v[3] = 0;  // NEW, aligned size, bytes, DICT
   ngpu_result &r = out[c];
   const uint32_t layer = chunk_layer[c];
   if (r.kind == NGPU_DICT) {
@@ -351,6 +350,15 @@ __device__ __forceinline__ void resolve_item(
       v[2] = len;
     }
   }
+}
+
+__device__ __forceinline__ void resolve_item(
+    uint64_t c, const ngpu_chunk *__restrict__ chunks, const uint32_t *__restrict__ chunk_layer,
+    const uint64_t *__restrict__ table, uint64_t mask, ngpu_result *__restrict__ out,
+    uint32_t align, uint64_t *__restrict__ newidx, uint64_t *__restrict__ uoff,
+    uint64_t *__restrict__ nbytes, uint64_t *__restrict__ ndict) {
+  uint64_t v[kDedupScans];
+  resolve_values(c, chunks, chunk_layer, table, mask, out, align, v);
   newidx[c] = v[0];
   uoff[c] = v[1];
   nbytes[c] = v[2];
@@ -563,13 +571,18 @@ constexpr uint32_t kSmallItems = 4;
 
 __device__ __forceinline__ void small_phase_end() { __syncthreads(); }
 
+// lfirst and st are NOT __restrict__: for a single-layer call lfirst is
+// a.single, and st is a.st_words, both written by the init phase of this same
+// kernel.  (With __restrict__ the compiler may hoist the lfirst loads above
+// the init writes: an empty layer then reported the previous call's chunk
+// count -- tests/test_gpu_parity.py::test_host_reads_see_fresh_results_on_recycled_memory.)
 __global__ __launch_bounds__(kSmallThreads) void dedup_small(
     DedupInit a, const ngpu_chunk *__restrict__ chunks, DictDevice dict,
     const ngpu_dict_hit *__restrict__ hits, uint32_t n_blobs, uint32_t align,
-    const uint64_t *__restrict__ lfirst, uint32_t *__restrict__ blob_real,
-    ngpu_layer_stats *__restrict__ st, ngpu_result *__restrict__ out) {
+    const uint64_t *lfirst, uint32_t *__restrict__ blob_real, ngpu_layer_stats *st,
+    ngpu_result *__restrict__ out) {
   __shared__ uint32_t fl[1024], used_all;
-  __shared__ uint64_t wsum[kSmallThreads / 64];
+  __shared__ uint64_t wsum[2][kDedupScans][kSmallThreads / 64];
   const uint64_t n = a.n, mask = a.icap - 1;
   const uint32_t nbo = n_blobs + 1;
   for (uint64_t i = threadIdx.x; i < a.total; i += kSmallThreads) init_item(a, i);
@@ -579,39 +592,47 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small(
     probe_insert_item(c, chunks, n, dict, hits, a.chunk_layer, out, a.blob_first, n_blobs, a.intra,
                       mask);
   small_phase_end();
-  for (uint64_t c = threadIdx.x; c < n; c += kSmallThreads)
-    resolve_item(c, chunks, a.chunk_layer, a.intra, mask, out, align, a.newidx, a.uoff, a.nbytes,
-                 a.ndict);
-  small_phase_end();
-  // exclusive scans of the four arrays (n <= kSmallThreads * kSmallItems)
+  // Resolve into registers and scan the four arrays together, one row of
+  // kSmallThreads chunks at a time (chunk r * kSmallThreads + thread): one
+  // barrier per row (C1: one), each array written once, where resolve wrote
+  // the arrays and four separate scans re-read them.
   uint64_t *arr[kDedupScans] = {a.newidx, a.uoff, a.nbytes, a.ndict};
-  const uint64_t c0 = (uint64_t)threadIdx.x * kSmallItems;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int k = 0; k < kDedupScans; ++k) {
-    uint64_t v[kSmallItems], sum = 0;
+  uint64_t carry[kDedupScans] = {0, 0, 0, 0};
+  for (uint64_t r = 0; r * kSmallThreads < n; ++r) {
+    const uint64_t c = r * kSmallThreads + threadIdx.x;
+    uint64_t v[kDedupScans] = {0, 0, 0, 0}, x[kDedupScans];
+    if (c < n) resolve_values(c, chunks, a.chunk_layer, a.intra, mask, out, align, v);
 #pragma unroll
-    for (uint32_t i = 0; i < kSmallItems; ++i) {
-      v[i] = c0 + i < n ? arr[k][c0 + i] : 0;
-      sum += v[i];
-    }
-    uint64_t x = sum;
+    for (int k = 0; k < kDedupScans; ++k) x[k] = v[k];
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    uint64_t run = x - sum;
-    for (int w = 0; w < wid; ++w) run += wsum[w];
 #pragma unroll
-    for (uint32_t i = 0; i < kSmallItems; ++i) {
-      const uint64_t c = c0 + i;
-      if (c < n) arr[k][c] = run;
-      run += v[i];
-      if (c + 1 == n) arr[k][n] = run;
+      for (int k = 0; k < kDedupScans; ++k) {
+        const uint64_t y = __shfl_up(x[k], o, 64);
+        if (lane >= o) x[k] += y;
+      }
     }
-    __syncthreads();  // wsum reused by the next array
+    const uint32_t b = r & 1;  // double-buffered: one barrier per row
+    if (lane == 63) {
+#pragma unroll
+      for (int k = 0; k < kDedupScans; ++k) wsum[b][k][wid] = x[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kDedupScans; ++k) {
+      uint64_t pre = 0, tot = 0;
+#pragma unroll 4
+      for (int w = 0; w < (int)(kSmallThreads / 64); ++w) {
+        const uint64_t t = wsum[b][k][w];
+        if (w < wid) pre += t;
+        tot += t;
+      }
+      const uint64_t run = carry[k] + pre + x[k] - v[k];
+      if (c < n) arr[k][c] = run;
+      if (c + 1 == n) arr[k][n] = run + v[k];
+      carry[k] += tot;
+    }
   }
   small_phase_end();
   for (uint64_t l = 0; l < a.L; ++l) {

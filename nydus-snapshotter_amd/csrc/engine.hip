@@ -129,10 +129,6 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
   return 0;
 }
 
-#ifndef NGPU_EVENT_FENCE
-#define NGPU_EVENT_FENCE hipEventDisableSystemFence
-#endif
-
 int ws_acquire(ngpu_engine *e, hipStream_t s) {
   if (!e->ws_pending || e->ws_last == s) return 0;
   if (!e->ws_last_ev) {  // a lazy stage end (ws_lazy_end): record it now
@@ -295,18 +291,45 @@ void engine_unref(ngpu_engine *e) {
     if (b.copy) (void)hipStreamDestroy(b.copy);
   }
   if (e->ws_done) (void)hipEventDestroy(e->ws_done);
+  if (e->host_ev) (void)hipEventDestroy(e->host_ev);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
 
 // Layer stats of a single-layer call (internal lstats[0]) + the digest
 // stage's bad-descriptor counter.
-int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st) {
+// Before the host reads what the stream's kernels wrote: a system-scope
+// release on the stream.  A stage with a lazy end (ws_lazy_end) leaves its
+// last kernel with the default device-scope release, and a small D2H copy
+// then read stale device memory (an empty pack's layer stats came back as a
+// previous engine's: test_streaming_pack_errors).
+int host_fence(ngpu_engine *e, hipStream_t s) {
+  HIP_TRY(e, hipEventRecord(e->host_ev, s));
+  return 0;
+}
+
+int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st, bool fenced) {
+  if (!fenced) {
+    if (int rc = host_fence(e, s)) return rc;
+  }
+#ifdef NGPU_DIAG_STATS
+  memset(e->h_stats, 0xEE, 32 * sizeof(uint64_t));
+#endif
   HIP_TRY(e, hipMemcpyAsync(e->h_stats, e->ws.stats, 16 * sizeof(uint64_t),
                             hipMemcpyDeviceToHost, s));
   HIP_TRY(e, hipMemcpyAsync(e->h_stats + 16, e->ws.lstats, sizeof(ngpu_layer_stats),
                             hipMemcpyDeviceToHost, s));
   HIP_TRY(e, hipStreamSynchronize(s));
+#ifdef NGPU_DIAG_STATS
+  {
+    uint64_t again[6] = {};
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(again, e->ws.lstats, sizeof(again), hipMemcpyDeviceToHost);
+    fprintf(stderr, "diag read_stats: lstats=%p h=%llu again=%llu stats[7]=%llu\n",
+            (void *)e->ws.lstats, (unsigned long long)e->h_stats[16],
+            (unsigned long long)again[0], (unsigned long long)e->h_stats[7]);
+  }
+#endif
   if (e->h_stats[7])
     return fail(e, NGPU_EINVAL, "%llu chunk descriptor(s) outside the data buffer",
                 (unsigned long long)e->h_stats[7]);
@@ -359,19 +382,19 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   e->ws.grid_stages = (c.flags & NGPU_FLAG_GRID_STAGES) != 0;
   e->device = c.device;
   DeviceGuard dg(c.device);
-  // The engine's events order work on this device only (stage ends, timing):
-  // no system-scope fence, which writes back the caches when a kernel that
-  // carries the event ends and holds the next kernel back by ~4.4 us.  Host
-  // reads of results go through stream-ordered copies + stream syncs.
+  // Events keep the default system-scope fence: the end event of a call on a
+  // caller's stream is also what makes its results visible to the host's
+  // copies.  (hipEventDisableSystemFence measured +2 % on C1 and is not
+  // worth that: profiles/r2/ab_event_fence_r2ef.json.)
   if (c.flags & NGPU_FLAG_TIMING)
     for (auto &set : e->ev)
       for (auto &ev : set)
-        if (hipEventCreateWithFlags(&ev, NGPU_EVENT_FENCE) != hipSuccess) {
+        if (hipEventCreate(&ev) != hipSuccess) {
           ngpu_destroy(e);
           return NGPU_EHIP;
         }
-  if (hipEventCreateWithFlags(&e->ws_done, hipEventDisableTiming | NGPU_EVENT_FENCE) !=
-          hipSuccess ||
+  if (hipEventCreateWithFlags(&e->ws_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->host_ev, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void **)&e->h_stats, 32 * sizeof(uint64_t), hipHostMallocDefault) !=
           hipSuccess) {
@@ -442,7 +465,7 @@ int ngpu_dedup_device(ngpu_engine *e, const ngpu_chunk *d_chunks, uint64_t n,
   int rc = enqueue_dedup(e, e->dict, d_chunks, n, d_out, d_hits, n_dict_blobs, s, nullptr, 1,
                          nullptr);
   if (rc) return rc;
-  if (stats) return read_stats(e, s, stats);
+  if (stats) return read_stats(e, s, stats, false);
   return 0;
 }
 
@@ -479,7 +502,7 @@ static int process_device(ngpu_engine *e, ngpu_dict *dict, const void *d_data, u
   int rc = enqueue_chain(e, dict, (const uint8_t *)d_data, len, d_chunks, n, d_out, s,
                          d_layer_first, d_layer_first ? n_layers : 1, d_stats);
   if (rc) return rc;
-  if (stats) return read_stats(e, s, stats);
+  if (stats) return read_stats(e, s, stats, false);
   return 0;
 }
 
@@ -539,9 +562,10 @@ static int process_host(ngpu_engine *e, ngpu_dict *dict, const void *data, uint6
                                    hipMemcpyHostToDevice, s));
   int rc = enqueue(e, dict, e->d_data, len, e->d_chunks, n, e->d_results, s);
   if (rc) return rc;
+  if ((rc = host_fence(e, s))) return rc;
   if (n) HIP_TRY(e, hipMemcpyAsync(out, e->d_results, n * sizeof(ngpu_result),
                                    hipMemcpyDeviceToHost, s));
-  return read_stats(e, s, stats);
+  return read_stats(e, s, stats, true);
 }
 
 int ngpu_process(ngpu_engine *e, const void *data, uint64_t len, const ngpu_chunk *chunks,
@@ -614,10 +638,11 @@ int ngpu_pack_tar(ngpu_engine *e, const void *tar, uint64_t len, ngpu_chunk **ch
                  hipSuccess)
       return bail(fail(e, NGPU_EHIP, "chunk table H2D failed"));
     if ((rc = enqueue(e, dict, e->d_data, len, e->d_chunks, n, e->d_results, s))) return bail(rc);
+    if ((rc = host_fence(e, s))) return bail(rc);
     if (n && hipMemcpyAsync(res, e->d_results, n * sizeof(ngpu_result), hipMemcpyDeviceToHost, s) !=
                  hipSuccess)
       return bail(fail(e, NGPU_EHIP, "results D2H failed"));
-    if ((rc = read_stats(e, s, stats))) return bail(rc);
+    if ((rc = read_stats(e, s, stats, true))) return bail(rc);
     *chunks_out = ch;
     *results_out = res;
     *n_out = n;

@@ -92,6 +92,7 @@ struct ngpu_engine {
   // it first, so calls on different streams never run over one workspace
   // concurrently.
   hipEvent_t ws_done = nullptr;
+  hipEvent_t host_ev = nullptr;  // host_fence marker (system scope)
   hipEvent_t ws_last_ev = nullptr;  // the event that ended the last stage
   hipStream_t ws_last = nullptr;
   bool ws_pending = false;
@@ -119,7 +120,10 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
 int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chunks, uint64_t n,
                   ngpu_result *d_out, const ngpu_dict_hit *d_hits, uint32_t n_blobs,
                   hipStream_t s, const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats);
-int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st);
+// A system-scope release on s before the host reads device results.
+int host_fence(ngpu_engine *e, hipStream_t s);
+// fenced: host_fence already recorded after the last kernel.
+int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st, bool fenced);
 // Order a workspace stage on stream s after the previous one (any stream).
 int ws_acquire(ngpu_engine *e, hipStream_t s);
 // Digest then dedup on one stream (digest chained).

@@ -417,6 +417,7 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
                        ds + maxk, c, dwin[b]);
     HIP_TRY(e, hipGetLastError());
     const uint64_t bytes = doff[a + c - 1] + len[a + c - 1];
+    if (int rc = host_fence(e, e->stream)) return rc;
     HIP_TRY(e, hipMemcpyAsync(p->slot[b].h, dwin[b], bytes, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipEventRecord(ev[b], e->stream));
     return 0;
@@ -649,11 +650,12 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
     }
     if (!rc) rc = enqueue_dedup(e, p->dict, p->d_all, n, p->d_res, nullptr, 0, e->stream, nullptr, 1,
                                 nullptr);
+    if (!rc) rc = host_fence(e, e->stream);
     if (!rc && n &&
         hipMemcpyAsync(res, p->d_res, n * sizeof(ngpu_result), hipMemcpyDeviceToHost,
                        e->stream) != hipSuccess)
       rc = fail(e, NGPU_EHIP, "pack: result copy failed");
-    if (!rc) rc = read_stats(e, e->stream, &st);
+    if (!rc) rc = read_stats(e, e->stream, &st, true);
     if (!rc && w) rc = write_stream(p, *opt, w, ctx, ch, res, n, st, info);
   }
   release(p);

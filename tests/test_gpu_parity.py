@@ -529,6 +529,31 @@ def test_streaming_pack_errors(tars):
         eng.close()
 
 
+def test_host_reads_see_fresh_results_on_recycled_memory(tars):
+    """Device memory recycled from a previous engine holds stale stats and
+    results; a pack on a fresh engine (engine stream, no stage-end events)
+    must still hand the host its own (host_fence before every D2H)."""
+    import torch
+    tb = tars["oci_lower"]
+    for it in range(12):
+        junk = torch.full((64 << 20,), 0x5A, dtype=torch.uint8, device="cuda")
+        del junk
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        eng = nydus_gpu.Engine(chunk_size=0x10000)
+        try:
+            ch, out, st = eng.pack().close()  # empty layer first: all-zero stats
+            assert len(ch) == 0 and st["chunks"] == 0 and st["new_chunks"] == 0, it
+            ref = eng.pack_tar(tb)
+            w = eng.pack()
+            w.write(tb)
+            ch2, out2, st2 = w.close()
+            assert ch2.tobytes() == ref[0].tobytes() and out2.tobytes() == ref[1].tobytes(), it
+            assert st2 == ref[2] and st2["chunks"] == len(ch2), it
+        finally:
+            eng.close()
+
+
 def test_staging_pool_reuse_across_packs(golden_layers, tars, oracle):
     """The engine keeps streaming-Pack staging slots between packs (pack.hip
     release / ngpu_pack_open_ex). Slots move between plain and retained packs
