@@ -299,10 +299,10 @@ void engine_unref(ngpu_engine *e) {
 // Layer stats of a single-layer call (internal lstats[0]) + the digest
 // stage's bad-descriptor counter.
 // Before the host reads what the stream's kernels wrote: a system-scope
-// release on the stream.  A stage with a lazy end (ws_lazy_end) leaves its
-// last kernel with the default device-scope release, and a small D2H copy
-// then read stale device memory (an empty pack's layer stats came back as a
-// previous engine's: test_streaming_pack_errors).
+// release on the stream.  A stage with a lazy end (ws_lazy_end) leaves no
+// event after its last kernel, so nothing else on the stream is guaranteed to
+// be system-scoped before the copy; one marker per host read is cheap next to
+// the PCIe transfer around it.
 int host_fence(ngpu_engine *e, hipStream_t s) {
   HIP_TRY(e, hipEventRecord(e->host_ev, s));
   return 0;
