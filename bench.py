@@ -294,6 +294,99 @@ def probe_bench(torch, nydus_gpu, eng, dd, Q, build_s, reps=5):
                       "gentries_s": round(m / build_s / 1e9, 2)}}
 
 
+def sharded_dict_extra(torch, dist, eng, buf, d_ch, n, stream, rank, world, backend,
+                       entries=4 << 20, plant=0.3, steps=10, warmup=3):
+    """N > 1 only: the C4 exchange on this run's layers, so the driver's
+    multi-GPU run puts RCCL on xGMI under the product's dict path
+    (nydus_gpu/dist.py).  Every rank plants 30 % of its own
+    layer's chunk digests; one all_gather_into_tensor assembles the global
+    dict (planted rows of every rank + random filler, same table on every
+    rank), each rank keeps its digest-prefix partition
+    (ShardedChunkDict.load -> ngpu_dict_create_device), and a step is
+    digest -> all_to_all_single probe routing (counts, queries, hits back) ->
+    dedup with the returned hits.  Checked: every rank's DICT count equals
+    its planted count, summed over ranks.  Reported beside the headline
+    line, never as `value`."""
+    from nydus_gpu.dist import ShardedChunkDict, engine_load_fn, engine_probe_fn
+    cdev = None if backend == "nccl" else "cpu"
+    d_out = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    eng.digest_device(buf.data_ptr(), buf.numel(), d_ch.data_ptr(), n, d_out.data_ptr())
+    torch.cuda.synchronize()
+    k = int(n * plant)
+    g = torch.Generator(device="cuda").manual_seed(0xC4 + rank)
+    sel = torch.randperm(n, device="cuda", generator=g)[:k]
+    mine = d_out.view(n, 64)[sel, :32].contiguous()
+    every = torch.empty((world * k, 32), dtype=torch.uint8, device="cuda")
+    if cdev:
+        parts = [torch.empty((k, 32), dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, mine.cpu())
+        every.copy_(torch.cat(parts))
+    else:
+        dist.all_gather_into_tensor(every, mine)
+    m = max(entries, world * k)
+    gd = torch.Generator(device="cuda").manual_seed(0xD1C7)  # same filler on every rank
+    dd = torch.empty((m, 32), dtype=torch.uint8, device="cuda")
+    dd.random_(0, 256, generator=gd)
+    dd[: world * k] = every
+    us = torch.zeros((m,), dtype=torch.int32, device="cuda")  # usize 0: wildcard, any size hits
+    bl = torch.randint(0, 8, (m,), dtype=torch.int32, device="cuda", generator=gd)
+    ix = torch.arange(m, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    sdict = ShardedChunkDict(rank, world, comm_device=cdev)
+    local_m = sdict.load(dd, us, bl, ix, 8, engine_load_fn(eng, 8))
+    sdict.probe_fn = engine_probe_fn(eng, stream_fn=lambda: stream.cuda_stream)
+    del dd, us, bl, ix, every
+    d_first = torch.tensor([0, n], dtype=torch.int64, device="cuda")
+    d_lst = torch.zeros(256, dtype=torch.uint8, device="cuda")
+    probe_s = []
+
+    def step():
+        with torch.cuda.stream(stream):
+            s = stream.cuda_stream
+            eng.digest_device(buf.data_ptr(), buf.numel(), d_ch.data_ptr(), n, d_out.data_ptr(),
+                              stream=s)
+            t0 = time.perf_counter()
+            hits = sdict.probe(d_out.view(n, 64)[:, :32])  # host sync on the split sizes
+            probe_s.append(time.perf_counter() - t0)
+            eng.dedup_layers_device(d_ch.data_ptr(), n, d_out.data_ptr(), d_first.data_ptr(), 1,
+                                    d_lst.data_ptr(), d_hits=hits.data_ptr(), n_dict_blobs=8,
+                                    stream=s)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    probe_s.clear()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    kinds = torch.bincount(d_out.view(n, 64)[:, 32].to(torch.int64), minlength=3).cpu()  # kind u32 @32
+    agg = torch.tensor([el, float(kinds[2]), float(k), float(np.median(probe_s))],
+                       dtype=torch.float64)
+    red = [agg.clone() for _ in range(world)]
+    if cdev:
+        dist.all_gather(red, agg)
+    else:
+        redc = [r.cuda() for r in red]
+        dist.all_gather(redc, agg.cuda())
+        red = [r.cpu() for r in redc]
+    red = torch.stack(red)
+    el_max = float(red[:, 0].max())
+    hits_all, planted_all = int(red[:, 1].sum()), int(red[:, 2].sum())
+    return {"what": "C4 exchange on this run's layers: digest -> all_to_all_single dict probe "
+                    "(digest-prefix partition; RCCL over xGMI when backend is nccl) -> dedup",
+            "backend": backend, "collectives": ["all_gather_into_tensor (dict build)",
+                                                "all_to_all_single x3 per step (counts, queries, hits)"],
+            "dict_entries": m, "entries_this_gpu": local_m, "steps": steps,
+            "ms_per_step": round(el_max / steps * 1e3, 3),
+            "probe_exchange_ms_median_max_rank": round(float(red[:, 3].max()) * 1e3, 3),
+            "dict_hits_all_ranks": hits_all, "planted_all_ranks": planted_all,
+            "hits_ok": hits_all == planted_all, "_elapsed": el_max}
+
+
 def pmc_traffic(path, workload, kernel):
     """HBM bytes per launch of the dominant kernel from a committed rocprofv3
     PMC summary of the same bench command.  Preferred: pmc_req_<workload>.json
@@ -587,6 +680,9 @@ def main():
     ap.add_argument("--pmc-json", default="", help="PMC summary for roofline.traffic "
                     "(default: newest profiles/r*/pmc_<workload>.json)")
     ap.add_argument("--cpu-sample-mib", type=int, default=2048)
+    ap.add_argument("--no-sharded-extra", action="store_true",
+                    help="N > 1: skip the RCCL-routed partitioned-dict step run after the "
+                         "headline measurement")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--probe-queries", type=int, default=16 << 20,
                     help="dict workloads: queries of the probe-only roofline measurement (0 = skip)")
@@ -891,6 +987,28 @@ def main():
             line["speedup_vs_cpu_pcie_inclusive"] = {
                 k: round(e2e[k] / cpu["value"], 2) for k in ("host_path_gbs", "streaming_gbs")
                 if k in e2e}
+    if dist and sdict is None and n_layers == 1 and not args.no_sharded_extra:
+        # the headline is already measured; a watchdog keeps a stuck collective
+        # from costing the line (rank 0 prints it without this entry)
+        import threading
+
+        def stuck():
+            if rank == 0:
+                print(json.dumps(dict(pending_line[0], sharded_dict={"error": "timeout"})),
+                      flush=True)
+            os._exit(0)
+        pending_line = [line]
+        dog = threading.Timer(120.0, stuck)
+        dog.daemon = True
+        dog.start()
+        try:
+            sx = sharded_dict_extra(torch, dist, eng, buf, d_ch, n, stream, rank, world,
+                                    args.dist_backend)
+            sx["gbs"] = round(file_bytes * sx["steps"] * world / sx.pop("_elapsed") / 1e9, 2)
+            line["sharded_dict"] = sx
+        except Exception as ex:  # reported, never fatal to the headline line
+            line["sharded_dict"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
+        dog.cancel()
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()
