@@ -512,6 +512,106 @@ def end_to_end(torch, nydus_gpu, buf, wl, stride, device, sample_bytes=2 << 30):
     return res
 
 
+def concurrent_bench(args):
+    """`--streams K` (tar workloads, e.g. c1): ONE engine converts K copies of
+    the layer side by side, one caller stream each -- the shape of containerd
+    converting an image's layers concurrently (one LayerConvertFunc per
+    layer, convert_unix.go:822) through one cached engine.  The engine gives
+    calls on distinct streams distinct workspace slots (NGPU_WS_SLOTS), so a
+    small layer, which leaves most of the chip idle (C1: <= one wave per SIMD,
+    four launches), overlaps the others on the GPU's hardware queues.
+    `--engines K`: K engines on device 0 instead (one stream each).  A step =
+    one ngpu_process_device + the result table back, per stream.  value =
+    the layers' file bytes of all streams / time."""
+    import torch
+    import nydus_gpu
+    wl = dict(WORKLOADS[args.workload])
+    if not wl.get("tar"):
+        raise SystemExit("--engines takes a tar workload (c1)")
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import layers
+    tar = layers.LAYERS[wl["tar"]]()
+    ch = nydus_gpu.tar_chunks(tar, wl["chunk"])
+    n, file_bytes = len(ch), int(ch["length"].sum())
+    K = max(args.engines, args.streams)
+    one = nydus_gpu.Engine(device=0, digester=wl["digester"], chunk_size=wl["chunk"]) \
+        if args.engines <= 1 else None
+    per = []
+    for i in range(K):
+        per.append(dict(
+            eng=one or nydus_gpu.Engine(device=0, digester=wl["digester"], chunk_size=wl["chunk"]),
+            buf=torch.from_numpy(np.frombuffer(tar, np.uint8).copy()).cuda(),
+            d_ch=torch.from_numpy(ch.view(np.uint8).copy()).cuda(),
+            d_out=torch.empty(n * 64, dtype=torch.uint8, device="cuda"),
+            h_out=torch.empty(n * 64, dtype=torch.uint8, pin_memory=True),
+            stream=torch.cuda.Stream()))
+    torch.cuda.synchronize()
+
+    def one(p):
+        s = p["stream"]
+        p["eng"].process_device(p["buf"].data_ptr(), p["buf"].numel(), p["d_ch"].data_ptr(), n,
+                                p["d_out"].data_ptr(), stream=s.cuda_stream)
+        with torch.cuda.stream(s):
+            p["h_out"].copy_(p["d_out"], non_blocking=True)
+
+    def step():
+        for p in per:
+            one(p)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if args.threads:
+        # one submitting thread per stream (goroutines calling Pack); ctypes
+        # drops the GIL inside the engine, the engine serialises only its
+        # enqueue section
+        import threading
+        go = threading.Barrier(K + 1)
+
+        def run(p):
+            go.wait()
+            for _ in range(args.steps):
+                one(p)
+            p["stream"].synchronize()
+        th = [threading.Thread(target=run, args=(p,)) for p in per]
+        for t in th:
+            t.start()
+        go.wait()
+        t0 = time.perf_counter()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        t_submit = elapsed
+    else:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        t_submit = time.perf_counter() - t0  # host time spent enqueueing
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    ref = per[0]["h_out"].numpy().view(nydus_gpu.RESULT_DTYPE)
+    for p in per[1:]:  # every engine's decisions equal
+        assert (p["h_out"].numpy() == per[0]["h_out"].numpy()).all()
+    kinds = np.bincount(ref["kind"], minlength=3)
+    for e in {id(p["eng"]): p["eng"] for p in per}.values():
+        e.close()
+    value = file_bytes * K * args.steps / elapsed / 1e9
+    line = {"metric": "GB/s of layer data chunk-hashed+deduped (node)", "value": round(value, 2),
+            "unit": "GB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "dtype": "u32", "data": "synthetic alpine-like layer tar (tests/golden/layers.py)",
+            "config": {"workload": wl["desc"], "name": args.workload,
+                       "engines": 1 if one else K, "streams": K,
+                       "submit": f"{K} threads" if args.threads else "one thread",
+                       "ws_slots": int(os.environ.get("NGPU_WS_SLOTS", 4)),
+                       "chunks": n, "file_bytes_per_layer": file_bytes},
+            "us_per_layer": round(elapsed / args.steps / K * 1e6, 2),
+            "host_submit_us_per_layer": round(t_submit / args.steps / K * 1e6, 2),
+            "decisions": {"NEW": int(kinds[0]), "INTRA": int(kinds[1]), "DICT": int(kinds[2])}}
+    print(json.dumps(line), flush=True)
+
+
 def node_bench(args):
     """`--node 0,1,..`: ONE process drives the listed GPUs through the C ABI's
     multi-GPU node (ngpu_node_*, csrc/node.hip) -- the form a cgo
@@ -688,6 +788,12 @@ def main():
                     help="dict workloads: queries of the probe-only roofline measurement (0 = skip)")
     ap.add_argument("--dump-timings", action="store_true",
                     help="add every timed call's stage times (oldest first) to the line")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="tar workloads: one engine converts K layers at once, one stream each")
+    ap.add_argument("--threads", action="store_true",
+                    help="--streams/--engines: one submitting host thread per stream")
+    ap.add_argument("--engines", type=int, default=1,
+                    help="tar workloads: K engines on device 0 convert layers concurrently")
     ap.add_argument("--node", default="", help="comma list of devices: one process drives them "
                     "through ngpu_node_* (a device may repeat: one-GPU rehearsal); see node_bench")
     args = ap.parse_args()
@@ -696,6 +802,8 @@ def main():
         args.warmup = 80 if (w.get("pool") or w.get("dict_entries")) else 20
     if args.node:
         return node_bench(args)
+    if args.engines > 1 or args.streams > 1:
+        return concurrent_bench(args)
 
     import torch
     import nydus_gpu

@@ -8,6 +8,7 @@
 // two in [0x1000, 0x1000000], FsVersion "5"/"6", default "6").
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -28,6 +29,7 @@ int fail(ngpu_engine *e, int code, const char *fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
+    std::lock_guard<std::mutex> g(e->err_mu);
     e->err = buf;
   }
   return code;
@@ -69,9 +71,31 @@ int pick_group_log2(const ngpu_engine *e, uint64_t data_len) {
   return D;
 }
 
+// Before a slot's buffers are freed: its last stage has finished.  (The
+// stage is on another stream; a buffer freed under it could be handed to
+// another slot's allocation and written by a stage unordered with it.)
+int slot_quiesce(ngpu_engine *e) {
+  ngpu_ws_slot &sl = *e->cur;
+  if (!sl.pending) return 0;
+  if (!sl.last_ev) {  // lazy end: record it on the stage's stream now
+    HIP_TRY(e, hipEventRecord(sl.done, sl.last));
+    sl.last_ev = sl.done;
+  }
+  HIP_TRY(e, hipEventSynchronize(sl.last_ev));
+  return 0;
+}
+
 int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
                      uint32_t n_blobs, uint64_t L) {
-  Workspace &ws = e->ws;
+  Workspace &ws = e->cur->ws;
+  {
+    const uint64_t nb = ((uint64_t)n_blobs + 1) * (L ? L : 1);
+    const bool regrow =
+        n + 1 > ws.cap_n || L > ws.cap_layers || nb > ws.cap_blobs ||
+        (e->cfg.digester == NGPU_DIGEST_BLAKE3 && blake3_max_groups(n, data_len, D) > ws.cap_g);
+    if (regrow && ws.groups)
+      if (int rc = slot_quiesce(e)) return rc;
+  }
   if (n + 1 > ws.cap_n || !ws.groups) {
     uint64_t cn = n + 1 < 4096 ? 4096 : n + 1;
     uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
@@ -129,13 +153,39 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
   return 0;
 }
 
+ngpu_ws_slot *use_slot(ngpu_engine *e, hipStream_t s) {
+  ngpu_ws_slot *pick = nullptr;
+  for (auto &sl : e->slots)  // the slot this stream used last: stream order
+    if (sl.pending && sl.last == s) {
+      pick = &sl;
+      break;
+    }
+  if (!pick)  // an idle slot: never used, or its last stage has ended
+    for (auto &sl : e->slots) {
+      if (!sl.pending) {
+        pick = &sl;
+        break;
+      }
+      if (sl.last_ev && hipEventQuery(sl.last_ev) == hipSuccess &&
+          (!pick || sl.tick < pick->tick))
+        pick = &sl;
+    }
+  if (!pick)  // all busy: the least recently used (ws_acquire waits for it)
+    for (auto &sl : e->slots)
+      if (!pick || sl.tick < pick->tick) pick = &sl;
+  pick->tick = ++e->tick;
+  e->cur = pick;
+  return pick;
+}
+
 int ws_acquire(ngpu_engine *e, hipStream_t s) {
-  if (!e->ws_pending || e->ws_last == s) return 0;
-  if (!e->ws_last_ev) {  // a lazy stage end (ws_lazy_end): record it now
-    HIP_TRY(e, hipEventRecord(e->ws_done, e->ws_last));
-    e->ws_last_ev = e->ws_done;
+  ngpu_ws_slot &sl = *e->cur;
+  if (!sl.pending || sl.last == s) return 0;
+  if (!sl.last_ev) {  // a lazy stage end (ws_lazy_end): record it now
+    HIP_TRY(e, hipEventRecord(sl.done, sl.last));
+    sl.last_ev = sl.done;
   }
-  HIP_TRY(e, hipStreamWaitEvent(s, e->ws_last_ev, 0));
+  HIP_TRY(e, hipStreamWaitEvent(s, sl.last_ev, 0));
   return 0;
 }
 
@@ -144,24 +194,30 @@ int ws_acquire(ngpu_engine *e, hipStream_t s) {
 // (rocprofv3 trace of back-to-back C1 calls), so a stage binds no end event
 // when none is needed yet:
 //  * chained: the next stage of the same call follows on the same stream;
-//  * s is the engine's own stream, which lives as long as the engine, so the
-//    event can be recorded later, by the ws_acquire of a stage on another
-//    stream (recorded then, it also covers later work on s: safe, not tight).
+//  * s lives as long as the engine (its own stream, a pack compute stream),
+//    so the event can be recorded later, by the ws_acquire of a stage on
+//    another stream (recorded then, it also covers later work on s: safe,
+//    not tight).
 bool ws_lazy_end(const ngpu_engine *e, hipStream_t s, bool chained) {
-  return chained || (s && s == e->stream);
+  if (chained) return true;
+  if (!s) return false;
+  for (hipStream_t x : e->streams)
+    if (x == s) return true;
+  return false;
 }
 
 // bound: an event the stage's last kernel already records at its end (a
-// stop event of hipExtLaunchKernelGGL), or null to record ws_done now --
+// stop event of hipExtLaunchKernelGGL), or null to record the slot's done event now --
 // unless the end may be lazy (ws_lazy_end), then ws_acquire records it.
 int ws_release(ngpu_engine *e, hipStream_t s, hipEvent_t bound, bool chained) {
+  ngpu_ws_slot &sl = *e->cur;
   if (!bound && !ws_lazy_end(e, s, chained)) {
-    HIP_TRY(e, hipEventRecord(e->ws_done, s));
-    bound = e->ws_done;
+    HIP_TRY(e, hipEventRecord(sl.done, s));
+    bound = sl.done;
   }
-  e->ws_last_ev = bound;
-  e->ws_last = s;
-  e->ws_pending = true;
+  sl.last_ev = bound;
+  sl.last = s;
+  sl.pending = true;
   return 0;
 }
 
@@ -170,13 +226,15 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
                    const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
                    hipStream_t s, bool chained) {
   const int D = pick_group_log2(e, len);
+  use_slot(e, s);
+  Workspace &ws = e->cur->ws;
   int rc = ensure_workspace(e, n, len, D, 0, 1);
   if (rc) return rc;
   if ((rc = ws_acquire(e, s))) return rc;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   // tuning override: flags bits 8..10 = 1 + BLAKE3 load mode (0 = default)
   const uint32_t lm = (e->cfg.flags >> 8) & 7;
-  e->ws.load_mode = lm ? (int)(lm - 1) : 0;
+  ws.load_mode = lm ? (int)(lm - 1) : 0;
   hipEvent_t *ev = nullptr;
   if (tm) {
     e->tslot = (int)(e->tcalls++ % ngpu_engine::kTimingRing);
@@ -187,12 +245,12 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
   hipEvent_t bound = nullptr;  // the stage-end event a kernel records
   if (e->cfg.digester == NGPU_DIGEST_SHA256) {
     if (tm) HIP_TRY(e, hipEventRecord(ev[0], s));
-    HIP_TRY(e, hipMemsetAsync(e->ws.stats, 0, 16 * sizeof(uint64_t), s));
+    HIP_TRY(e, hipMemsetAsync(ws.stats, 0, 16 * sizeof(uint64_t), s));
     if (tm) HIP_TRY(e, hipEventRecord(ev[1], s));
     // tuning override: flags bits 11..13 = 1 + SHA-256 variant (0 split,
     // 1 pair, 2 lane, 4/5 pair layouts)
     const uint32_t sv = (e->cfg.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7;
-    launch_sha256(d_data, len, d_chunks, n, d_out, e->ws.stats + 7, sv ? (int)sv - 1 : -1, s);
+    launch_sha256(d_data, len, d_chunks, n, d_out, ws.stats + 7, sv ? (int)sv - 1 : -1, s);
     if (tm) {
       HIP_TRY(e, hipEventRecord(ev[2], s));
       HIP_TRY(e, hipEventRecord(ev[3], s));
@@ -200,8 +258,8 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
     }
   } else {
     // events ride on the kernels: no marker packets between the launches
-    hipEvent_t end = tm ? ev[3] : ws_lazy_end(e, s, chained) ? nullptr : e->ws_done;
-    if (launch_blake3(d_data, d_chunks, n, len, D, e->ws, d_out, s, tm ? ev[0] : nullptr,
+    hipEvent_t end = tm ? ev[3] : ws_lazy_end(e, s, chained) ? nullptr : e->cur->done;
+    if (launch_blake3(d_data, d_chunks, n, len, D, ws, d_out, s, tm ? ev[0] : nullptr,
                       tm ? ev[1] : nullptr, tm ? ev[2] : nullptr, end))
       bound = end;
   }
@@ -217,6 +275,7 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chu
                   hipStream_t s, const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats) {
   if (!d_hits) n_blobs = dict_blobs(dict);
   if (!d_lfirst) L = 1;
+  use_slot(e, s);
   int rc = ensure_workspace(e, n, 0, 0, n_blobs, L);
   if (rc) return rc;
   if ((rc = ws_acquire(e, s))) return rc;
@@ -227,17 +286,17 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chu
     if (rc) return rc;
     if (replica) dict = replica;
   }
-  if (!d_stats) d_stats = e->ws.lstats;
+  if (!d_stats) d_stats = e->cur->ws.lstats;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
   const uint32_t align =
       (e->cfg.fs_version == 6 || (e->cfg.flags & NGPU_FLAG_ALIGNED_CHUNK)) ? 4096u : 1u;
   // d_lfirst == nullptr: the init kernel writes {0, n} into ws.lfirst1
-  // the last dedup kernel records the stage end (timing slot or ws_done)
+  // the last dedup kernel records the stage end (timing slot or the slot's done event)
   hipEvent_t end = tm && e->tcalls      ? e->ev[e->tslot][4]
                    : ws_lazy_end(e, s, false) ? nullptr
-                                              : e->ws_done;
+                                              : e->cur->done;
   launch_dedup(d_chunks, n, dict ? dict->dev : DictDevice{}, d_hits, n_blobs, align, d_lfirst, L,
-               e->ws, d_out, d_stats, s, end);
+               e->cur->ws, d_out, d_stats, s, end);
   HIP_TRY(e, hipGetLastError());
   if (tm && e->tcalls) e->timed[e->tslot] = n > 0;
   if ((rc = ws_release(e, s, end, false))) return rc;
@@ -266,14 +325,20 @@ void engine_unref(ngpu_engine *e) {
   if (!e || e->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
   DeviceGuard g(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  Workspace &ws = e->ws;
-  void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.nbytes, ws.ndict, ws.tstat,
-                  ws.intra, ws.blob_first, ws.blob_real, ws.stats, ws.chunk_layer,
-                  ws.lfirst1, ws.lstats, ws.small, ws.tree_list, ws.xq, ws.xparts, ws.xhits,
-                  e->d_data, e->d_chunks, e->d_results};
-  for (void *p : bufs)
+  for (hipStream_t x : e->streams)
+    if (x != e->stream) (void)hipStreamSynchronize(x);
+  for (auto &sl : e->slots) {
+    Workspace &ws = sl.ws;
+    void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.nbytes, ws.ndict,
+                    ws.tstat, ws.intra, ws.blob_first, ws.blob_real, ws.stats, ws.chunk_layer,
+                    ws.lfirst1, ws.lstats, ws.small, ws.tree_list, ws.xq, ws.xparts, ws.xhits};
+    for (void *p : bufs)
+      if (p) (void)hipFree(p);
+    if (sl.h_stats) (void)hipHostFree(sl.h_stats);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
+  for (void *p : {(void *)e->d_data, (void *)e->d_chunks, (void *)e->d_results})
     if (p) (void)hipFree(p);
-  if (e->h_stats) (void)hipHostFree(e->h_stats);
   for (auto &set : e->ev)
     for (auto ev : set)
       if (ev) (void)hipEventDestroy(ev);
@@ -289,8 +354,10 @@ void engine_unref(ngpu_engine *e) {
     if (b.d_res) (void)hipFree(b.d_res);
     if (b.d_all) (void)hipFree(b.d_all);
     if (b.copy) (void)hipStreamDestroy(b.copy);
+    if (b.fence) (void)hipEventDestroy(b.fence);
   }
-  if (e->ws_done) (void)hipEventDestroy(e->ws_done);
+  for (hipStream_t x : e->streams)  // every pack compute stream (+ the engine's)
+    if (x != e->stream) (void)hipStreamDestroy(x);
   if (e->host_ev) (void)hipEventDestroy(e->host_ev);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -303,8 +370,8 @@ void engine_unref(ngpu_engine *e) {
 // event after its last kernel, so nothing else on the stream is guaranteed to
 // be system-scoped before the copy; one marker per host read is cheap next to
 // the PCIe transfer around it.
-int host_fence(ngpu_engine *e, hipStream_t s) {
-  HIP_TRY(e, hipEventRecord(e->host_ev, s));
+int host_fence(ngpu_engine *e, hipStream_t s, hipEvent_t ev) {
+  HIP_TRY(e, hipEventRecord(ev ? ev : e->host_ev, s));
   return 0;
 }
 
@@ -312,28 +379,16 @@ int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st, bool fenced)
   if (!fenced) {
     if (int rc = host_fence(e, s)) return rc;
   }
-#ifdef NGPU_DIAG_STATS
-  memset(e->h_stats, 0xEE, 32 * sizeof(uint64_t));
-#endif
-  HIP_TRY(e, hipMemcpyAsync(e->h_stats, e->ws.stats, 16 * sizeof(uint64_t),
-                            hipMemcpyDeviceToHost, s));
-  HIP_TRY(e, hipMemcpyAsync(e->h_stats + 16, e->ws.lstats, sizeof(ngpu_layer_stats),
-                            hipMemcpyDeviceToHost, s));
+  ngpu_ws_slot &sl = *e->cur;  // the slot the call's stages used (e->mu held)
+  uint64_t *h = sl.h_stats;
+  HIP_TRY(e, hipMemcpyAsync(h, sl.ws.stats, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(e, hipMemcpyAsync(h + 16, sl.ws.lstats, sizeof(ngpu_layer_stats), hipMemcpyDeviceToHost,
+                            s));
   HIP_TRY(e, hipStreamSynchronize(s));
-#ifdef NGPU_DIAG_STATS
-  {
-    uint64_t again[6] = {};
-    (void)hipDeviceSynchronize();
-    (void)hipMemcpy(again, e->ws.lstats, sizeof(again), hipMemcpyDeviceToHost);
-    fprintf(stderr, "diag read_stats: lstats=%p h=%llu again=%llu stats[7]=%llu\n",
-            (void *)e->ws.lstats, (unsigned long long)e->h_stats[16],
-            (unsigned long long)again[0], (unsigned long long)e->h_stats[7]);
-  }
-#endif
-  if (e->h_stats[7])
+  if (h[7])
     return fail(e, NGPU_EINVAL, "%llu chunk descriptor(s) outside the data buffer",
-                (unsigned long long)e->h_stats[7]);
-  if (st) memcpy(st, e->h_stats + 16, sizeof(ngpu_layer_stats));
+                (unsigned long long)h[7]);
+  if (st) memcpy(st, h + 16, sizeof(ngpu_layer_stats));
   return 0;
 }
 
@@ -379,7 +434,16 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NGPU_ENODEV;
   ngpu_engine *e = new ngpu_engine();
   e->cfg = c;
-  e->ws.grid_stages = (c.flags & NGPU_FLAG_GRID_STAGES) != 0;
+  // NGPU_WS_SLOTS: workspace slots = calls on distinct streams that may run
+  // at once (default 4, the hardware queues HIP gives a process)
+  int nslots = 4;
+  if (const char *v = getenv("NGPU_WS_SLOTS")) {
+    const long x = strtol(v, nullptr, 10);
+    if (x >= 1 && x <= 64) nslots = (int)x;
+  }
+  e->slots.resize((size_t)nslots);
+  for (auto &sl : e->slots) sl.ws.grid_stages = (c.flags & NGPU_FLAG_GRID_STAGES) != 0;
+  e->cur = &e->slots[0];
   e->device = c.device;
   DeviceGuard dg(c.device);
   // Events keep the default system-scope fence: the end event of a call on a
@@ -393,12 +457,15 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
           ngpu_destroy(e);
           return NGPU_EHIP;
         }
-  if (hipEventCreateWithFlags(&e->ws_done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->host_ev, hipEventDisableTiming) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc((void **)&e->h_stats, 32 * sizeof(uint64_t), hipHostMallocDefault) !=
-          hipSuccess) {
-    delete e;
+  bool ok = hipEventCreateWithFlags(&e->host_ev, hipEventDisableTiming) == hipSuccess &&
+            hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess;
+  if (ok) e->streams.push_back(e->stream);
+  for (auto &sl : e->slots)
+    ok = ok && hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess &&
+         hipHostMalloc((void **)&sl.h_stats, 32 * sizeof(uint64_t), hipHostMallocDefault) ==
+             hipSuccess;
+  if (!ok) {
+    ngpu_destroy(e);
     return NGPU_EHIP;
   }
   *out = e;

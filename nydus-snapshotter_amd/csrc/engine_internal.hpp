@@ -20,11 +20,15 @@ struct ngpu_staging_buf {
   uint64_t cap = 0;
 };
 
-// Per-pack device buffers and copy stream, kept by the engine between packs
+// Per-pack device buffers and streams, kept by the engine between packs
 // (a stream create/destroy and two hipMalloc/hipFree pairs per pack were most
-// of a small layer's streaming Pack: 0.9 ms for C1's 10 MB).
+// of a small layer's streaming Pack: 0.9 ms for C1's 10 MB).  `stream` is the
+// pack's compute stream: packs open at once run side by side on the GPU.
+// Compute streams live until the engine is destroyed (ngpu_engine::streams).
 struct ngpu_pack_bufs {
   hipStream_t copy = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t fence = nullptr;  // the pack's host_fence marker
   ngpu_result *d_res = nullptr;
   uint64_t res_cap = 0;
   ngpu_chunk *d_all = nullptr;
@@ -62,12 +66,37 @@ struct ngpu_dict {
   std::mutex io_mu;
 };
 
+// One HBM workspace and its cross-stream ordering state.  Every stage that
+// uses the workspace ends with an event on its stream (last_ev; null = not
+// recorded yet, only while `last` is a stream that lives as long as the
+// engine); a stage on another stream waits for it first, so calls on
+// different streams never run over one workspace concurrently.  An engine
+// keeps several (NGPU_WS_SLOTS, default 4): a call on a stream keeps the slot
+// its stream used last (stream order is the ordering), a call on another
+// stream takes an idle slot, so independent layers on different streams --
+// containerd converting an image's layers concurrently -- run side by side
+// on the GPU instead of queueing behind one workspace.
+struct ngpu_ws_slot {
+  ngpu::Workspace ws;
+  hipEvent_t done = nullptr;     // stage-end event when no kernel carries one
+  hipEvent_t last_ev = nullptr;  // the event that ended the last stage
+  hipStream_t last = nullptr;    // stream of the last stage
+  bool pending = false;          // a stage has been enqueued on this slot
+  uint64_t *h_stats = nullptr;   // pinned: counters + layer stats read back
+  uint64_t tick = 0;             // last use (LRU)
+};
+
 struct ngpu_engine {
   std::atomic<int> refs{1};  // the creator + every open pack
   ngpu_config cfg{};
   int device = 0;
   hipStream_t stream = nullptr;
-  ngpu::Workspace ws;
+  std::vector<ngpu_ws_slot> slots;  // fixed at create
+  ngpu_ws_slot *cur = nullptr;      // the slot of the call being enqueued (e->mu held)
+  uint64_t tick = 0;
+  // streams that live as long as the engine (its own + every pack compute
+  // stream): a stage on one of them may leave its end event unrecorded
+  std::vector<hipStream_t> streams;  // guarded by mu
   ngpu_dict *dict = nullptr;              // default dict (one reference), may be null
   std::vector<ngpu_dict *> dict_cache;    // dicts opened by path (one reference each)
   // host-path device buffers
@@ -76,7 +105,6 @@ struct ngpu_engine {
   ngpu_chunk *d_chunks = nullptr;
   ngpu_result *d_results = nullptr;
   uint64_t d_chunk_cap = 0;
-  uint64_t *h_stats = nullptr;  // pinned
   // NGPU_FLAG_TIMING: a ring of per-call event sets (0 start, 1 digest start,
   // 2 digest end, 3 tree end, 4 end), so timing a call never makes the next
   // one wait: ngpu_timing_at reads any of the last kTimingRing calls.
@@ -86,20 +114,12 @@ struct ngpu_engine {
   int slot_D[kTimingRing] = {};
   uint64_t tcalls = 0;  // calls recorded so far; the current slot is (tcalls - 1) % ring
   int tslot = 0;
-  // Workspace ordering across streams: every stage that uses `ws` ends with
-  // an event on its stream (ws_last_ev; null = not recorded yet, only while
-  // ws_last is the engine's own stream); a stage on another stream waits for
-  // it first, so calls on different streams never run over one workspace
-  // concurrently.
-  hipEvent_t ws_done = nullptr;
   hipEvent_t host_ev = nullptr;  // host_fence marker (system scope)
-  hipEvent_t ws_last_ev = nullptr;  // the event that ended the last stage
-  hipStream_t ws_last = nullptr;
-  bool ws_pending = false;
   std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu
   std::vector<ngpu_pack_bufs> pack_pool;        // guarded by pool_mu
   std::mutex pool_mu;
   std::string err;
+  std::mutex err_mu;  // fail() may run outside mu (a pack's blob stream)
   std::mutex mu;
 };
 
@@ -107,9 +127,16 @@ struct ngpu_engine {
 namespace ngpu {
 
 int fail(ngpu_engine *e, int code, const char *fmt, ...);
+// Pick the workspace slot for a stage on stream s and make it e->cur (e->mu
+// held): the slot s used last, else an idle slot, else the least recently
+// used one (ws_acquire then orders s after its last stage).
+ngpu_ws_slot *use_slot(ngpu_engine *e, hipStream_t s);
 int pick_group_log2(const ngpu_engine *e, uint64_t data_len);
 int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D, uint32_t n_blobs,
                      uint64_t L);
+// Host-wait until the current slot's last stage has finished (before any of
+// its buffers is freed).
+int slot_quiesce(ngpu_engine *e);
 // chained: the caller enqueues the dedup stage next on the same stream (under
 // the same lock), so the digest stage binds no end event (ws_lazy_end).
 int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
@@ -120,8 +147,9 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
 int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chunks, uint64_t n,
                   ngpu_result *d_out, const ngpu_dict_hit *d_hits, uint32_t n_blobs,
                   hipStream_t s, const uint64_t *d_lfirst, uint64_t L, ngpu_layer_stats *d_stats);
-// A system-scope release on s before the host reads device results.
-int host_fence(ngpu_engine *e, hipStream_t s);
+// A system-scope release on s before the host reads device results (ev: a
+// marker event of the caller's; null = the engine's, e->mu held).
+int host_fence(ngpu_engine *e, hipStream_t s, hipEvent_t ev = nullptr);
 // fenced: host_fence already recorded after the last kernel.
 int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st, bool fenced);
 // Order a workspace stage on stream s after the previous one (any stream).

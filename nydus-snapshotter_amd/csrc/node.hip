@@ -63,7 +63,9 @@ int node_dict_hits(ngpu_engine *e, ngpu_dict *d, const uint8_t *digests, uint64_
     return fail(e, NGPU_EINVAL, "node chunk dict has no replica on device %d", e->device);
   }
   const uint32_t W = (uint32_t)d->parts.size();
-  Workspace &ws = e->ws;
+  Workspace &ws = e->cur->ws;  // the dedup stage's slot (use_slot)
+  if (((n > ws.cap_x && ws.xq) || ((uint64_t)W * n > ws.cap_xparts && ws.xparts)))
+    if (int rc = slot_quiesce(e)) return rc;  // no buffer freed under a running stage
   if (n > ws.cap_x || !ws.xq) {
     if (ws.xq) (void)hipFree(ws.xq), ws.xq = nullptr;
     if (ws.xhits) (void)hipFree(ws.xhits), ws.xhits = nullptr;

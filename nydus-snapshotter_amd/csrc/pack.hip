@@ -151,6 +151,8 @@ struct ngpu_pack : TarSink {
   ngpu_chunk *d_all = nullptr;
   uint64_t all_cap = 0;
   hipStream_t copy = nullptr;
+  hipStream_t stream = nullptr;  // compute: digest, dedup, gather (lives as long as the engine)
+  hipEvent_t fence = nullptr;    // host_fence marker of this pack
   CopyPool *pool = nullptr;  // created on the first large write
   bool retain = false;       // NGPU_PACK_RETAIN: device segments kept to the end
   std::vector<Seg> segs;
@@ -180,7 +182,7 @@ void release(ngpu_pack *p) {
     if (s.done) (void)hipEventSynchronize(s.done);
   }
   if (p->copy) (void)hipStreamSynchronize(p->copy);
-  (void)hipStreamSynchronize(p->e->stream);
+  if (p->stream) (void)hipStreamSynchronize(p->stream);
   {
     std::lock_guard<std::mutex> g(p->e->pool_mu);
     for (Slot &s : p->slot) {
@@ -201,10 +203,17 @@ void release(ngpu_pack *p) {
   }
   for (Seg &g : p->segs) (void)hipFree(g.d);
   {
+    // the streams are idle (synchronised above).  Every compute stream goes
+    // back to the pool: the engine's workspace slots may still name it as
+    // the stream of their last stage (ws_lazy_end), so it lives until the
+    // engine does.  The pool holds as many as packs were ever open at once.
     std::lock_guard<std::mutex> g(p->e->pool_mu);
-    if (p->copy && p->e->pack_pool.size() < 4) {  // the streams are idle (synchronised above)
-      p->e->pack_pool.push_back({p->copy, p->d_res, p->res_cap, p->d_all, p->all_cap});
+    if (p->stream) {
+      p->e->pack_pool.push_back({p->copy, p->stream, p->fence, p->d_res, p->res_cap, p->d_all,
+                                 p->all_cap});
       p->copy = nullptr;
+      p->stream = nullptr;
+      p->fence = nullptr;
       p->d_res = nullptr;
       p->d_all = nullptr;
     }
@@ -212,6 +221,7 @@ void release(ngpu_pack *p) {
   if (p->d_res) (void)hipFree(p->d_res);
   if (p->d_all) (void)hipFree(p->d_all);
   if (p->copy) (void)hipStreamDestroy(p->copy);
+  if (p->fence) (void)hipEventDestroy(p->fence);
   delete p->pool;
   delete p;
   dict_unref(dict);
@@ -226,8 +236,8 @@ int grow_results(ngpu_pack *p, uint64_t want) {
   HIP_TRY(p->e, hipMalloc((void **)&n, c * sizeof(ngpu_result)));
   if (p->d_res) {
     HIP_TRY(p->e, hipMemcpyAsync(n, p->d_res, p->dispatched * sizeof(ngpu_result),
-                                 hipMemcpyDeviceToDevice, p->e->stream));
-    HIP_TRY(p->e, hipStreamSynchronize(p->e->stream));
+                                 hipMemcpyDeviceToDevice, p->stream));
+    HIP_TRY(p->e, hipStreamSynchronize(p->stream));
     (void)hipFree(p->d_res);
   }
   p->d_res = n;
@@ -266,10 +276,10 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
   HIP_TRY(e, hipMemcpyAsync(s.d_ch, s.h_ch, nch * sizeof(ngpu_chunk), hipMemcpyHostToDevice,
                             p->copy));
   HIP_TRY(e, hipEventRecord(s.copied, p->copy));
-  HIP_TRY(e, hipStreamWaitEvent(e->stream, s.copied, 0));
-  rc = enqueue_digest(e, dev, s.fill, s.d_ch, nch, p->d_res + a, e->stream);
+  HIP_TRY(e, hipStreamWaitEvent(p->stream, s.copied, 0));
+  rc = enqueue_digest(e, dev, s.fill, s.d_ch, nch, p->d_res + a, p->stream);
   if (rc) return rc;
-  HIP_TRY(e, hipEventRecord(s.done, e->stream));
+  HIP_TRY(e, hipEventRecord(s.done, p->stream));
   s.busy = true;
   p->dispatched = b;
   return 0;
@@ -381,7 +391,7 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
   hipEvent_t ev[2] = {};
   const uint64_t desc_bytes = maxk * (8 + 8 + 4);
   auto cleanup = [&] {
-    (void)hipStreamSynchronize(e->stream);
+    (void)hipStreamSynchronize(p->stream);
     for (int i = 0; i < 2; ++i) {
       if (dwin[i]) (void)hipFree(dwin[i]);
       if (ddesc[i]) (void)hipFree(ddesc[i]);
@@ -409,17 +419,18 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
     for (uint64_t i = 0; i < c; ++i) ho[i] = doff[a + i];
     memcpy(hl, &len[a], c * 4);
     uint64_t *ds = (uint64_t *)ddesc[b];
-    HIP_TRY(e, hipMemcpyAsync(ds, hs, c * 8, hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(e, hipMemcpyAsync(ds + maxk, ho, c * 8, hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(e, hipMemcpyAsync(ds + 2 * maxk, hl, c * 4, hipMemcpyHostToDevice, e->stream));
+    hipStream_t ps = p->stream;
+    HIP_TRY(e, hipMemcpyAsync(ds, hs, c * 8, hipMemcpyHostToDevice, ps));
+    HIP_TRY(e, hipMemcpyAsync(ds + maxk, ho, c * 8, hipMemcpyHostToDevice, ps));
+    HIP_TRY(e, hipMemcpyAsync(ds + 2 * maxk, hl, c * 4, hipMemcpyHostToDevice, ps));
     const unsigned grid = (unsigned)(c < 2048 ? c : 2048);
-    hipLaunchKernelGGL(gather_chunks, dim3(grid), dim3(256), 0, e->stream, ds, (uint32_t *)(ds + 2 * maxk),
+    hipLaunchKernelGGL(gather_chunks, dim3(grid), dim3(256), 0, ps, ds, (uint32_t *)(ds + 2 * maxk),
                        ds + maxk, c, dwin[b]);
     HIP_TRY(e, hipGetLastError());
     const uint64_t bytes = doff[a + c - 1] + len[a + c - 1];
-    if (int rc = host_fence(e, e->stream)) return rc;
-    HIP_TRY(e, hipMemcpyAsync(p->slot[b].h, dwin[b], bytes, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipEventRecord(ev[b], e->stream));
+    if (int rc = host_fence(e, ps, p->fence)) return rc;
+    HIP_TRY(e, hipMemcpyAsync(p->slot[b].h, dwin[b], bytes, hipMemcpyDeviceToHost, ps));
+    HIP_TRY(e, hipEventRecord(ev[b], ps));
     return 0;
   };
   std::vector<const uint8_t *> hp;
@@ -477,6 +488,8 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
       const ngpu_pack_bufs b = e->pack_pool.back();
       e->pack_pool.pop_back();
       p->copy = b.copy;
+      p->stream = b.stream;
+      p->fence = b.fence;
       p->d_res = b.d_res;
       p->res_cap = b.res_cap;
       p->d_all = b.d_all;
@@ -499,6 +512,11 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
     }
   }
   if (!p->copy) ok = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking) == hipSuccess;
+  if (ok && !p->fence) ok = hipEventCreateWithFlags(&p->fence, hipEventDisableTiming) == hipSuccess;
+  if (ok && !p->stream) {
+    ok = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) == hipSuccess;
+    if (ok) e->streams.push_back(p->stream);  // lives until the engine does (e->mu held)
+  }
   for (Slot &s : p->slot) {
     if (s.h) {  // from the engine's pool: only the device copy may be missing
       if (!p->retain && !s.d) ok = ok && hipMalloc((void **)&s.d, cap) == hipSuccess;
@@ -512,8 +530,13 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
          hipEventCreateWithFlags(&s.copied, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
   }
-  // size the digest workspace once so no slot dispatch reallocates it
-  if (ok) ok = ensure_workspace(e, p->max_ch, cap, pick_group_log2(e, cap), dict_blobs(dict), 1) == 0;
+  // take a workspace slot for the pack's stream and size it once, so no
+  // staging-slot dispatch reallocates it
+  if (ok) {
+    use_slot(e, p->stream);
+    ok = ensure_workspace(e, p->max_ch, cap, pick_group_log2(e, cap), dict_blobs(dict), 1) == 0 &&
+         ws_acquire(e, p->stream) == 0 && ws_release(e, p->stream, nullptr, true) == 0;
+  }
   if (!ok) {
     (void)hipGetLastError();
     release(p);
@@ -626,36 +649,40 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
   ngpu_result *res = nullptr;
   ngpu_layer_stats st{};
   if (!rc) {
-    std::lock_guard<std::mutex> g(e->mu);
     DeviceGuard dg(e->device);
-    rc = dispatch(p, p->slot[p->cur], p->dispatched, n);
-    if (!rc) rc = grow_results(p, n + 1);
-    if (!rc && p->all_cap < n + 1) {  // kept between packs (engine pack_pool)
-      if (p->d_all) (void)hipFree(p->d_all), p->d_all = nullptr, p->all_cap = 0;
-      uint64_t c = 4096;
-      while (c < n + 1) c *= 2;
-      if (hipMalloc((void **)&p->d_all, c * sizeof(ngpu_chunk)) != hipSuccess)
-        rc = fail(e, NGPU_ENOMEM, "pack: chunk table allocation failed");
-      else
-        p->all_cap = c;
+    {
+      std::lock_guard<std::mutex> g(e->mu);
+      hipStream_t ps = p->stream;
+      rc = dispatch(p, p->slot[p->cur], p->dispatched, n);
+      if (!rc) rc = grow_results(p, n + 1);
+      if (!rc && p->all_cap < n + 1) {  // kept between packs (engine pack_pool)
+        if (p->d_all) (void)hipFree(p->d_all), p->d_all = nullptr, p->all_cap = 0;
+        uint64_t c = 4096;
+        while (c < n + 1) c *= 2;
+        if (hipMalloc((void **)&p->d_all, c * sizeof(ngpu_chunk)) != hipSuccess)
+          rc = fail(e, NGPU_ENOMEM, "pack: chunk table allocation failed");
+        else
+          p->all_cap = c;
+      }
+      ch = (ngpu_chunk *)malloc(sizeof(ngpu_chunk) * (n ? n : 1));
+      res = (ngpu_result *)malloc(sizeof(ngpu_result) * (n ? n : 1));
+      if (!rc && (!ch || !res)) rc = NGPU_ENOMEM;
+      if (!rc && n) {
+        memcpy(ch, p->chunks.data(), n * sizeof(ngpu_chunk));
+        if (hipMemcpyAsync(p->d_all, ch, n * sizeof(ngpu_chunk), hipMemcpyHostToDevice, ps) !=
+            hipSuccess)
+          rc = fail(e, NGPU_EHIP, "pack: chunk table copy failed");
+      }
+      if (!rc)
+        rc = enqueue_dedup(e, p->dict, p->d_all, n, p->d_res, nullptr, 0, ps, nullptr, 1, nullptr);
+      if (!rc) rc = host_fence(e, ps, p->fence);
+      if (!rc && n &&
+          hipMemcpyAsync(res, p->d_res, n * sizeof(ngpu_result), hipMemcpyDeviceToHost, ps) !=
+              hipSuccess)
+        rc = fail(e, NGPU_EHIP, "pack: result copy failed");
+      if (!rc) rc = read_stats(e, ps, &st, true);
     }
-    ch = (ngpu_chunk *)malloc(sizeof(ngpu_chunk) * (n ? n : 1));
-    res = (ngpu_result *)malloc(sizeof(ngpu_result) * (n ? n : 1));
-    if (!rc && (!ch || !res)) rc = NGPU_ENOMEM;
-    if (!rc && n) {
-      memcpy(ch, p->chunks.data(), n * sizeof(ngpu_chunk));
-      if (hipMemcpyAsync(p->d_all, ch, n * sizeof(ngpu_chunk), hipMemcpyHostToDevice,
-                         e->stream) != hipSuccess)
-        rc = fail(e, NGPU_EHIP, "pack: chunk table copy failed");
-    }
-    if (!rc) rc = enqueue_dedup(e, p->dict, p->d_all, n, p->d_res, nullptr, 0, e->stream, nullptr, 1,
-                                nullptr);
-    if (!rc) rc = host_fence(e, e->stream);
-    if (!rc && n &&
-        hipMemcpyAsync(res, p->d_res, n * sizeof(ngpu_result), hipMemcpyDeviceToHost,
-                       e->stream) != hipSuccess)
-      rc = fail(e, NGPU_EHIP, "pack: result copy failed");
-    if (!rc) rc = read_stats(e, e->stream, &st, true);
+    // the blob stream is host work on the pack's own buffers: no engine lock
     if (!rc && w) rc = write_stream(p, *opt, w, ctx, ch, res, n, st, info);
   }
   release(p);
