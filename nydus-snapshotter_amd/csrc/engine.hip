@@ -355,6 +355,8 @@ void engine_unref(ngpu_engine *e) {
     if (b.d_all) (void)hipFree(b.d_all);
     if (b.copy) (void)hipStreamDestroy(b.copy);
     if (b.fence) (void)hipEventDestroy(b.fence);
+    if (b.h_stats) (void)hipHostFree(b.h_stats);
+    if (b.h_io) (void)hipHostFree(b.h_io);
   }
   for (hipStream_t x : e->streams)  // every pack compute stream (+ the engine's)
     if (x != e->stream) (void)hipStreamDestroy(x);
@@ -379,12 +381,21 @@ int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st, bool fenced)
   if (!fenced) {
     if (int rc = host_fence(e, s)) return rc;
   }
-  ngpu_ws_slot &sl = *e->cur;  // the slot the call's stages used (e->mu held)
-  uint64_t *h = sl.h_stats;
+  uint64_t *h = e->cur->h_stats;  // the slot the call's stages used (e->mu held)
+  if (int rc = read_stats_enqueue(e, s, h)) return rc;
+  HIP_TRY(e, hipStreamSynchronize(s));
+  return read_stats_parse(e, h, st);
+}
+
+int read_stats_enqueue(ngpu_engine *e, hipStream_t s, uint64_t *h) {
+  const ngpu_ws_slot &sl = *e->cur;
   HIP_TRY(e, hipMemcpyAsync(h, sl.ws.stats, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(e, hipMemcpyAsync(h + 16, sl.ws.lstats, sizeof(ngpu_layer_stats), hipMemcpyDeviceToHost,
                             s));
-  HIP_TRY(e, hipStreamSynchronize(s));
+  return 0;
+}
+
+int read_stats_parse(ngpu_engine *e, const uint64_t *h, ngpu_layer_stats *st) {
   if (h[7])
     return fail(e, NGPU_EINVAL, "%llu chunk descriptor(s) outside the data buffer",
                 (unsigned long long)h[7]);

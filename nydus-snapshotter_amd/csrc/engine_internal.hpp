@@ -29,6 +29,9 @@ struct ngpu_pack_bufs {
   hipStream_t copy = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t fence = nullptr;  // the pack's host_fence marker
+  uint64_t *h_stats = nullptr;  // pinned, 32 words: the pack's stats read back
+  uint8_t *h_io = nullptr;      // pinned: chunk table out, results back (no pageable copies
+  uint64_t io_cap = 0;          // under the engine lock)
   ngpu_result *d_res = nullptr;
   uint64_t res_cap = 0;
   ngpu_chunk *d_all = nullptr;
@@ -115,7 +118,8 @@ struct ngpu_engine {
   uint64_t tcalls = 0;  // calls recorded so far; the current slot is (tcalls - 1) % ring
   int tslot = 0;
   hipEvent_t host_ev = nullptr;  // host_fence marker (system scope)
-  std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu
+  std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu, <= kStagingPool
+  static constexpr size_t kStagingPool = 32;   // 16 packs open at once keep theirs
   std::vector<ngpu_pack_bufs> pack_pool;        // guarded by pool_mu
   std::mutex pool_mu;
   std::string err;
@@ -152,6 +156,11 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chu
 int host_fence(ngpu_engine *e, hipStream_t s, hipEvent_t ev = nullptr);
 // fenced: host_fence already recorded after the last kernel.
 int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st, bool fenced);
+// The same in two halves, for callers that wait outside e->mu: enqueue the
+// copies of the current slot's counters + layer stats into pinned h (32
+// words) on s (e->mu held); after s is synchronised, check and unpack them.
+int read_stats_enqueue(ngpu_engine *e, hipStream_t s, uint64_t *h);
+int read_stats_parse(ngpu_engine *e, const uint64_t *h, ngpu_layer_stats *st);
 // Order a workspace stage on stream s after the previous one (any stream).
 int ws_acquire(ngpu_engine *e, hipStream_t s);
 // Digest then dedup on one stream (digest chained).

@@ -153,6 +153,9 @@ struct ngpu_pack : TarSink {
   hipStream_t copy = nullptr;
   hipStream_t stream = nullptr;  // compute: digest, dedup, gather (lives as long as the engine)
   hipEvent_t fence = nullptr;    // host_fence marker of this pack
+  uint64_t *h_stats = nullptr;   // pinned: its stats, read after the engine lock is let go
+  uint8_t *h_io = nullptr;       // pinned staging of the chunk table / results at close
+  uint64_t io_cap = 0;
   CopyPool *pool = nullptr;  // created on the first large write
   bool retain = false;       // NGPU_PACK_RETAIN: device segments kept to the end
   std::vector<Seg> segs;
@@ -187,7 +190,7 @@ void release(ngpu_pack *p) {
     std::lock_guard<std::mutex> g(p->e->pool_mu);
     for (Slot &s : p->slot) {
       if (!s.h || !s.h_ch || !s.d_ch || !s.copied || !s.done ||
-          p->e->staging_pool.size() >= 4)
+          p->e->staging_pool.size() >= ngpu_engine::kStagingPool)
         continue;
       p->e->staging_pool.push_back({s.h, s.h_ch, s.d, s.d_ch, s.copied, s.done, p->cap});
       s = Slot{};
@@ -209,11 +212,13 @@ void release(ngpu_pack *p) {
     // engine does.  The pool holds as many as packs were ever open at once.
     std::lock_guard<std::mutex> g(p->e->pool_mu);
     if (p->stream) {
-      p->e->pack_pool.push_back({p->copy, p->stream, p->fence, p->d_res, p->res_cap, p->d_all,
-                                 p->all_cap});
+      p->e->pack_pool.push_back({p->copy, p->stream, p->fence, p->h_stats, p->h_io, p->io_cap,
+                                 p->d_res, p->res_cap, p->d_all, p->all_cap});
+      p->h_io = nullptr;
       p->copy = nullptr;
       p->stream = nullptr;
       p->fence = nullptr;
+      p->h_stats = nullptr;
       p->d_res = nullptr;
       p->d_all = nullptr;
     }
@@ -222,6 +227,8 @@ void release(ngpu_pack *p) {
   if (p->d_all) (void)hipFree(p->d_all);
   if (p->copy) (void)hipStreamDestroy(p->copy);
   if (p->fence) (void)hipEventDestroy(p->fence);
+  if (p->h_stats) (void)hipHostFree(p->h_stats);
+  if (p->h_io) (void)hipHostFree(p->h_io);
   delete p->pool;
   delete p;
   dict_unref(dict);
@@ -285,8 +292,8 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
   return 0;
 }
 
-// Current slot is full: dispatch its complete chunks, carry the chunk in
-// progress to the other slot and make that one current.
+// Current slot is full: dispatch its complete chunks (under the engine lock),
+// carry the chunk in progress to the other slot and make that one current.
 int switch_slot(ngpu_pack *p) {
   Slot &s = p->slot[p->cur];
   Slot &t = p->slot[p->cur ^ 1];
@@ -296,9 +303,12 @@ int switch_slot(ngpu_pack *p) {
   const uint64_t carry_from = k < p->chunks.size() ? p->chunks[k].offset : end;
   const uint64_t carry = end - carry_from;
   if (carry >= p->cap) return fail(p->e, NGPU_EINVAL, "chunk larger than a staging slot");
-  int rc = dispatch(p, s, p->dispatched, k);
-  if (rc) return rc;
-  if (t.busy) {
+  {
+    std::lock_guard<std::mutex> g(p->e->mu);  // the engine lock covers the enqueue only
+    int rc = dispatch(p, s, p->dispatched, k);
+    if (rc) return rc;
+  }
+  if (t.busy) {  // the other slot's copy + digest, waited for without the lock
     HIP_TRY(p->e, hipEventSynchronize(t.done));
     t.busy = false;
   }
@@ -317,8 +327,20 @@ int switch_slot(ngpu_pack *p) {
 // device segment is sized and allocated at dispatch.
 constexpr uint64_t kEagerCopy = 1ull << 20;
 
+// NGPU_EAGER_COPY (bytes, tuning knob): the eager copy granule.
+uint64_t eager_granule() {
+  static const uint64_t g = [] {
+    if (const char *v = getenv("NGPU_EAGER_COPY")) {
+      const unsigned long long x = strtoull(v, nullptr, 0);
+      if (x >= 4096) return (uint64_t)x;
+    }
+    return kEagerCopy;
+  }();
+  return g;
+}
+
 int eager_copy(ngpu_pack *p, Slot &s) {
-  if (p->retain || s.fill - s.sent < kEagerCopy) return 0;
+  if (p->retain || s.fill - s.sent < eager_granule()) return 0;
   DeviceGuard dg(p->e->device);
   HIP_TRY(p->e, hipMemcpyAsync(s.d + s.sent, s.h + s.sent, s.fill - s.sent, hipMemcpyHostToDevice,
                                p->copy));
@@ -490,6 +512,9 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
       p->copy = b.copy;
       p->stream = b.stream;
       p->fence = b.fence;
+      p->h_stats = b.h_stats;
+      p->h_io = b.h_io;
+      p->io_cap = b.io_cap;
       p->d_res = b.d_res;
       p->res_cap = b.res_cap;
       p->d_all = b.d_all;
@@ -513,6 +538,9 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
   }
   if (!p->copy) ok = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking) == hipSuccess;
   if (ok && !p->fence) ok = hipEventCreateWithFlags(&p->fence, hipEventDisableTiming) == hipSuccess;
+  if (ok && !p->h_stats)
+    ok = hipHostMalloc((void **)&p->h_stats, 32 * sizeof(uint64_t), hipHostMallocDefault) ==
+         hipSuccess;
   if (ok && !p->stream) {
     ok = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) == hipSuccess;
     if (ok) e->streams.push_back(p->stream);  // lives until the engine does (e->mu held)
@@ -566,7 +594,6 @@ int ngpu_pack_reserve(ngpu_pack *p, void **ptr, uint64_t *avail) {
   if (cancelled(p)) return p->err = fail(p->e, NGPU_ECANCELED, "pack: cancelled");
   Slot &s = p->slot[p->cur];
   if (s.fill == p->cap) {
-    std::lock_guard<std::mutex> g(p->e->mu);
     DeviceGuard dg(p->e->device);
     int rc = switch_slot(p);
     if (rc) return p->err = rc;
@@ -667,21 +694,42 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
       ch = (ngpu_chunk *)malloc(sizeof(ngpu_chunk) * (n ? n : 1));
       res = (ngpu_result *)malloc(sizeof(ngpu_result) * (n ? n : 1));
       if (!rc && (!ch || !res)) rc = NGPU_ENOMEM;
+      // the chunk table goes out and the results come back through pinned
+      // memory: a pageable copy would block this thread under the lock
+      const uint64_t io = n * (sizeof(ngpu_chunk) > sizeof(ngpu_result) ? sizeof(ngpu_chunk)
+                                                                         : sizeof(ngpu_result));
+      if (!rc && io > p->io_cap) {
+        if (p->h_io) (void)hipHostFree(p->h_io), p->h_io = nullptr, p->io_cap = 0;
+        uint64_t c = 64 << 10;
+        while (c < io) c *= 2;
+        if (hipHostMalloc((void **)&p->h_io, c, hipHostMallocDefault) != hipSuccess)
+          rc = fail(e, NGPU_ENOMEM, "pack: pinned result buffer allocation failed");
+        else
+          p->io_cap = c;
+      }
       if (!rc && n) {
         memcpy(ch, p->chunks.data(), n * sizeof(ngpu_chunk));
-        if (hipMemcpyAsync(p->d_all, ch, n * sizeof(ngpu_chunk), hipMemcpyHostToDevice, ps) !=
-            hipSuccess)
+        memcpy(p->h_io, ch, n * sizeof(ngpu_chunk));
+        if (hipMemcpyAsync(p->d_all, p->h_io, n * sizeof(ngpu_chunk), hipMemcpyHostToDevice,
+                           ps) != hipSuccess)
           rc = fail(e, NGPU_EHIP, "pack: chunk table copy failed");
       }
       if (!rc)
         rc = enqueue_dedup(e, p->dict, p->d_all, n, p->d_res, nullptr, 0, ps, nullptr, 1, nullptr);
       if (!rc) rc = host_fence(e, ps, p->fence);
+      // (stream order: the results overwrite h_io after the chunk table left it)
       if (!rc && n &&
-          hipMemcpyAsync(res, p->d_res, n * sizeof(ngpu_result), hipMemcpyDeviceToHost, ps) !=
+          hipMemcpyAsync(p->h_io, p->d_res, n * sizeof(ngpu_result), hipMemcpyDeviceToHost, ps) !=
               hipSuccess)
         rc = fail(e, NGPU_EHIP, "pack: result copy failed");
-      if (!rc) rc = read_stats(e, ps, &st, true);
+      if (!rc) rc = read_stats_enqueue(e, ps, p->h_stats);
     }
+    // wait for the pack's own stream without the engine lock (other packs
+    // and calls keep enqueueing meanwhile), then check its stats
+    if (!rc && hipStreamSynchronize(p->stream) != hipSuccess)
+      rc = fail(e, NGPU_EHIP, "pack: stream failed");
+    if (!rc) rc = read_stats_parse(e, p->h_stats, &st);
+    if (!rc && n) memcpy(res, p->h_io, n * sizeof(ngpu_result));
     // the blob stream is host work on the pack's own buffers: no engine lock
     if (!rc && w) rc = write_stream(p, *opt, w, ctx, ch, res, n, st, info);
   }

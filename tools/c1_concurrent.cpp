@@ -5,7 +5,11 @@
 // submitting (T = 1: one thread round-robins the streams).  Prints one JSON
 // line: GB/s of file data, us per layer, host enqueue us per layer.
 //
-// usage: c1_concurrent TAR K T STEPS WARMUP [CHUNK_SIZE]
+// Mode "pack": T threads each loop the converter.Pack drop-in over the layer
+// (ngpu_pack_open, ngpu_pack_write in 1 MiB pieces from pageable memory,
+// ngpu_pack_close) on the same engine -- PCIe included.
+//
+// usage: c1_concurrent TAR K T STEPS WARMUP [CHUNK_SIZE] [device|pack]
 // build: hipcc --offload-arch=gfx950 -O2 -std=c++17 -I../include tools/c1_concurrent.cpp \
 //          -o tools/c1_concurrent -L nydus-snapshotter_amd -lnydusgpu -Wl,-rpath,<lib dir>
 #include <hip/hip_runtime.h>
@@ -46,6 +50,7 @@ int main(int argc, char **argv) {
   fclose(f);
   const int K = atoi(argv[2]), T = atoi(argv[3]), steps = atoi(argv[4]), warm = atoi(argv[5]);
   const uint32_t S = argc > 6 ? (uint32_t)strtoul(argv[6], nullptr, 0) : 0x100000;
+  const bool pack = argc > 7 && strcmp(argv[7], "pack") == 0;
   uint64_t n = 0, nf = 0;
   ngpu_tar_chunks(tar.data(), tar.size(), S, nullptr, 0, &n, &nf);
   std::vector<ngpu_chunk> ch(n);
@@ -57,6 +62,60 @@ int main(int argc, char **argv) {
   cfg.chunk_size = S;
   ngpu_engine *eng = nullptr;
   if (ngpu_create(&cfg, &eng)) return 1;
+  if (pack) {
+    auto layer = [&](std::vector<ngpu_result> &keep) {
+      ngpu_pack *p = nullptr;
+      if (ngpu_pack_open(eng, &p)) exit(1);
+      for (size_t a = 0; a < tar.size(); a += 1 << 20) {
+        const size_t take = tar.size() - a < (1u << 20) ? tar.size() - a : (1u << 20);
+        if (ngpu_pack_write(p, tar.data() + a, take)) {
+          fprintf(stderr, "write: %s\n", ngpu_last_error(eng));
+          exit(1);
+        }
+      }
+      ngpu_chunk *c = nullptr;
+      ngpu_result *res = nullptr;
+      uint64_t m = 0;
+      if (ngpu_pack_close(p, &c, &res, &m, nullptr)) {
+        fprintf(stderr, "close: %s\n", ngpu_last_error(eng));
+        exit(1);
+      }
+      keep.assign(res, res + m);
+      ngpu_free_host(c);
+      ngpu_free_host(res);
+    };
+    std::vector<std::vector<ngpu_result>> last(T);
+    for (int i = 0; i < warm; ++i) layer(last[0]);
+    std::atomic<int> ready{0};
+    std::atomic<bool> go{false};
+    std::vector<std::thread> th;
+    using clk = std::chrono::steady_clock;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        ready++;
+        while (!go.load()) {
+        }
+        for (int i = 0; i < steps; ++i) layer(last[t]);
+      });
+    while (ready.load() < T) {
+    }
+    const auto t0 = clk::now();
+    go = true;
+    for (auto &x : th) x.join();
+    const double el = std::chrono::duration<double>(clk::now() - t0).count();
+    int same = 1;
+    for (auto &v : last)
+      same &= v.size() == last[0].size() &&
+              memcmp(v.data(), last[0].data(), v.size() * sizeof(ngpu_result)) == 0;
+    const double layers = (double)T * steps;
+    printf("{\"tool\": \"c1_concurrent\", \"mode\": \"pack\", \"threads\": %d, \"steps\": %d, "
+           "\"chunks\": %llu, \"file_bytes_per_layer\": %llu, \"gbs\": %.2f, "
+           "\"us_per_layer\": %.2f, \"results_equal\": %s}\n",
+           T, steps, (unsigned long long)n, (unsigned long long)bytes, bytes * layers / el / 1e9,
+           el / layers * 1e6, same ? "true" : "false");
+    ngpu_destroy(eng);
+    return same ? 0 : 1;
+  }
   std::vector<Lane> lanes(K);
   for (auto &l : lanes) {
     CK(hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking));
@@ -109,7 +168,7 @@ int main(int argc, char **argv) {
   uint64_t nw = 0;
   for (uint64_t i = 0; i < n; ++i) nw += lanes[0].h_out[i].kind == NGPU_NEW;
   const double layers = (double)K * steps;
-  printf("{\"tool\": \"c1_concurrent\", \"streams\": %d, \"threads\": %d, \"steps\": %d, "
+  printf("{\"tool\": \"c1_concurrent\", \"mode\": \"device\", \"streams\": %d, \"threads\": %d, \"steps\": %d, "
          "\"chunks\": %llu, \"file_bytes_per_layer\": %llu, \"gbs\": %.2f, \"us_per_layer\": %.2f, "
          "\"host_enqueue_us_per_layer\": %.2f, \"results_equal\": %s, \"new_chunks\": %llu}\n",
          K, T, steps, (unsigned long long)n, (unsigned long long)bytes, bytes * layers / el / 1e9,
