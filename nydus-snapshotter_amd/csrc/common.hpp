@@ -174,6 +174,10 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
                    ngpu_result *out, hipStream_t s, hipEvent_t ev_first,
                    hipEvent_t ev_groups_start, hipEvent_t ev_groups_end, hipEvent_t ev_end);
 uint64_t blake3_max_groups(uint64_t n, uint64_t data_len, int group_log2);
+// True when the call's chunk planning runs inside its leaf kernel
+// (b3_quad_planned: small layers on the quad path) -- there is no planning
+// kernel, so ev_groups_start is not recorded.
+bool blake3_planned_in_leaves(uint64_t n, uint64_t data_len, int group_log2, const Workspace &ws);
 // sha256.hip
 void launch_sha256(const uint8_t *data, uint64_t data_len,
                    const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,

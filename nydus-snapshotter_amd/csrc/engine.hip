@@ -241,6 +241,8 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
     ev = e->ev[e->tslot];
     e->timed[e->tslot] = false;
     e->slot_D[e->tslot] = D;
+    e->slot_fused[e->tslot] =
+        e->cfg.digester == NGPU_DIGEST_BLAKE3 && blake3_planned_in_leaves(n, len, D, ws);
   }
   hipEvent_t bound = nullptr;  // the stage-end event a kernel records
   if (e->cfg.digester == NGPU_DIGEST_SHA256) {
@@ -751,7 +753,7 @@ int ngpu_timing_at(ngpu_engine *e, uint32_t back, ngpu_timing *out) {
   if (!e->timed[k]) return 0;
   hipEvent_t *ev = e->ev[k];
   HIP_TRY(e, hipEventSynchronize(ev[4]));
-  HIP_TRY(e, hipEventElapsedTime(&out->digest_ms, ev[1], ev[2]));
+  HIP_TRY(e, hipEventElapsedTime(&out->digest_ms, e->slot_fused[k] ? ev[0] : ev[1], ev[2]));
   HIP_TRY(e, hipEventElapsedTime(&out->tree_ms, ev[2], ev[3]));
   HIP_TRY(e, hipEventElapsedTime(&out->dedup_ms, ev[3], ev[4]));
   HIP_TRY(e, hipEventElapsedTime(&out->total_ms, ev[0], ev[4]));

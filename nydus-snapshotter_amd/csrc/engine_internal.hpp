@@ -115,6 +115,7 @@ struct ngpu_engine {
   hipEvent_t ev[kTimingRing][5] = {};
   bool timed[kTimingRing] = {};
   int slot_D[kTimingRing] = {};
+  bool slot_fused[kTimingRing] = {};  // planning inside the leaf kernel: digest from ev[0]
   uint64_t tcalls = 0;  // calls recorded so far; the current slot is (tcalls - 1) % ring
   int tslot = 0;
   hipEvent_t host_ev = nullptr;  // host_fence marker (system scope)
