@@ -10,10 +10,12 @@ is the dict probe:
   2. owner(d) = top bits of the digest's first two bytes
      ((d0 << 8 | d1) * world >> 16; for power-of-two worlds the top
      log2(world) bits of byte 0);
-  3. records are sorted by owner and exchanged with one all_to_all_single
-     (32 B per query out, 16 B per hit back) — payload is tiny
-     (1 MiB chunks: 16384 x 48 B per 16 GiB layer), so the exchange is
-     latency-bound, not link-bound;
+  3. records are sorted by owner and exchanged with all_to_all_single
+     (32 B per query out, 24 B per hit back) — payload is tiny
+     (1 MiB chunks: 16384 x 56 B per 16 GiB layer), so the exchange is
+     latency-bound, not link-bound.  Variable splits (sized on the host,
+     one sync per probe) or, with `cap`, equal padded splits that keep the
+     whole probe on the device stream;
   4. the owner probes its partition (engine.dict_probe_device) and returns
      ngpu_dict_hit records with GLOBAL entry ids (chunk-table order);
   5. each rank runs its own layer dedup with those hits (engine.dedup_device).
@@ -46,11 +48,21 @@ class ShardedChunkDict:
     is ``engine_probe_fn(engine)``.
     """
 
-    def __init__(self, rank: int, world: int, group=None, comm_device=None):
+    def __init__(self, rank: int, world: int, group=None, comm_device=None, cap: int = 0):
         """comm_device: device the all-to-all runs on (None = the tensors' own;
-        "cpu" when the process group is gloo and the data lives on a GPU)."""
+        "cpu" when the process group is gloo and the data lives on a GPU).
+
+        cap > 0 (the same on every rank): at most cap queries per probe, and
+        the exchange uses EQUAL splits -- every rank sends each owner a
+        cap-row slot, padded -- so no split size ever goes to the host: the
+        probe is stream-ordered end to end (no device->host sync between a
+        layer's digest and its dedup).  It moves world x the query bytes and
+        probes world x cap rows (padding included) in exchange.  cap == 0:
+        variable splits, sized on the host from an all-to-all of the counts
+        (one sync per probe, minimal bytes)."""
         self.rank, self.world, self.group = rank, world, group
         self.comm_device = comm_device
+        self.cap = int(cap)
         self.local_to_global: Optional[torch.Tensor] = None
         self.n_blobs = 0
         self.probe_fn: Optional[Callable[[torch.Tensor], torch.Tensor]] = None
@@ -82,6 +94,8 @@ class ShardedChunkDict:
         dev = digests.device
         if self.world == 1:
             return self._local(digests)
+        if self.cap:
+            return self._probe_equal(digests)
         cdev = torch.device(self.comm_device) if self.comm_device else dev
         own = owner_of(digests, self.world)
         order = torch.argsort(own, stable=True)
@@ -98,6 +112,34 @@ class ShardedChunkDict:
         self._a2a(back, hits.contiguous(), in_splits, out_splits)
         res = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=dev)
         res[order] = back.to(dev)
+        return res
+
+    def _probe_equal(self, digests: torch.Tensor) -> torch.Tensor:
+        """Equal-split exchange (cap rows per owner, see __init__): each query
+        goes to row `pos` of its owner's slot, pos = its rank among this
+        rank's queries for that owner (stable), all computed on the device."""
+        n, W, cap = digests.shape[0], self.world, self.cap
+        if n > cap:
+            raise ValueError(f"{n} queries > cap {cap}")
+        dev = digests.device
+        cdev = torch.device(self.comm_device) if self.comm_device else dev
+        own = owner_of(digests, W)
+        order = torch.argsort(own, stable=True)
+        own_s = own[order]
+        counts = torch.bincount(own, minlength=W)
+        start = torch.cumsum(counts, 0) - counts
+        pos = torch.arange(n, device=dev) - start[own_s]
+        send = torch.zeros((W, cap, 32), dtype=torch.uint8, device=dev)
+        send[own_s, pos] = digests[order]
+        send = send.view(W * cap, 32).to(cdev)
+        recv = torch.empty_like(send)
+        self._a2a(recv, send, None, None)
+        hits = self._local(recv.to(dev)).to(cdev)  # (W * cap, HIT_WORDS): padding rows ignored
+        back = torch.empty_like(hits)
+        self._a2a(back, hits.contiguous(), None, None)
+        back = back.to(dev).view(W, cap, HIT_WORDS)
+        res = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=dev)
+        res[order] = back[own_s, pos]
         return res
 
     def _local(self, digests: torch.Tensor) -> torch.Tensor:

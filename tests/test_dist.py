@@ -52,13 +52,13 @@ def _expected(d, us, bl, ix, q):
     return out
 
 
-def _worker(rank, world, port, ret):
+def _worker(rank, world, port, ret, cap=0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         d, us, bl, ix = _global_dict()
-        sd = ShardedChunkDict(rank, world)
+        sd = ShardedChunkDict(rank, world, cap=cap)
         local = {}
 
         def load(dd, uu, bb, ii, uo):
@@ -97,10 +97,25 @@ def test_owner_is_prefix():
 
 
 @pytest.mark.timeout(180)
-def test_sharded_dict_two_ranks():
+@pytest.mark.parametrize("cap", [0, 700, 1024])
+def test_sharded_dict_two_ranks(cap):
+    """cap 0: variable splits sized on the host; cap >= queries: equal padded
+    splits, no host sync (ShardedChunkDict._probe_equal)."""
     world = 2
     mgr = mp.Manager()
     ret = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), ret), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), ret, cap), nprocs=world, join=True)
     assert ret[0][0] and ret[1][0]
     assert ret[0][1] + ret[1][1] == 5000  # the partition covers the dict exactly once
+
+
+@pytest.mark.timeout(180)
+def test_sharded_dict_four_ranks_equal_splits():
+    """Four owners, equal padded splits: every rank's hits equal the whole
+    dict's first-occurrence answers."""
+    world = 4
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), ret, 700), nprocs=world, join=True)
+    assert all(ret[r][0] for r in range(world))
+    assert sum(ret[r][1] for r in range(world)) == 5000

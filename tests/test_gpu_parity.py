@@ -384,7 +384,7 @@ def test_split_stages_equal_process(oracle):
         eng.close()
 
 
-def _sharded_worker(rank, world, port, ret):
+def _sharded_worker(rank, world, port, ret, equal=False):
     import os
     import torch
     import torch.distributed as dist
@@ -405,7 +405,8 @@ def _sharded_worker(rank, world, port, ret):
         db = (np.arange(len(dd)) % 4).astype(np.uint32)
         di = np.arange(len(dd), dtype=np.uint32)
         eng = nydus_gpu.Engine(chunk_size=0x10000)
-        sd = ShardedChunkDict(rank, world, comm_device="cpu")
+        cap = max(len(c) for _, c in layers) if equal else 0  # equal padded splits
+        sd = ShardedChunkDict(rank, world, comm_device="cpu", cap=cap)
         sd.load(torch.from_numpy(dd).cuda(), torch.from_numpy(ds.view(np.int32)).cuda(),
                 torch.from_numpy(db.view(np.int32)).cuda(), torch.from_numpy(di.view(np.int32)).cuda(),
                 4, engine_load_fn(eng, 4))
@@ -427,10 +428,12 @@ def _sharded_worker(rank, world, port, ret):
         dist.destroy_process_group()
 
 
-def test_sharded_dict_two_ranks_one_gpu():
+@pytest.mark.parametrize("equal", [False, True])
+def test_sharded_dict_two_ranks_one_gpu(equal):
     """Two ranks (processes) on the one GPU: dict partitioned by digest prefix,
     probes routed by all-to-all (gloo carries the exchange here; RCCL on a
-    multi-GPU node), decisions identical to the oracle with the whole dict."""
+    multi-GPU node), decisions identical to the oracle with the whole dict.
+    equal: equal padded splits (no host sync in the probe)."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -439,7 +442,7 @@ def test_sharded_dict_two_ranks_one_gpu():
     s.close()
     mgr = mp.Manager()
     ret = mgr.dict()
-    mp.spawn(_sharded_worker, args=(2, port, ret), nprocs=2, join=True)
+    mp.spawn(_sharded_worker, args=(2, port, ret, equal), nprocs=2, join=True)
     assert ret[0][0] and ret[1][0]
     assert ret[0][1] > 0 and ret[1][1] > 0
 
