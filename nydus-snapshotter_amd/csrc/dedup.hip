@@ -645,6 +645,231 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small(
     finalize_item(c, a.chunk_layer, lfirst, a.newidx, a.uoff, blob_real, nbo, out);
 }
 
+// ---- small single-layer calls: the whole stage in LDS --------------------------
+// Every Pack and most device calls are one layer of at most a few thousand
+// chunks (C1: 108).  dedup_small hands its phases over through global memory:
+// each phase waits on several dependent L2 / HBM round trips (digest loads,
+// device-scope table atomics, scan arrays, the 64-ary search), ~14 us for C1.
+// Here the intra-layer table, the lengths, the NEW-index / offset prefixes
+// and the blob ranks live in LDS; global memory is read once per chunk
+// (descriptor, digest, dict hit) plus the rare full-digest compare of a tag
+// match, and written once per chunk.  Same decisions by construction: the
+// same first-occurrence table (LDS CAS / atomic MIN instead of device
+// atomics), the same size rule, the same scans in chunk order, the same
+// first-hit blob ranking.
+constexpr uint32_t kLdsChunks = 4096;   // == kSmallDedupChunks
+constexpr uint32_t kLdsSlots = 8192;    // next_pow2(2n) for n <= 4096
+constexpr uint32_t kLdsBlobs = 1024;    // dict blobs + own
+constexpr int kLdsItems = (int)(kLdsChunks / kSmallThreads);
+static_assert(kLdsChunks == kSmallDedupChunks, "one LDS slot per chunk");
+
+__global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
+    const ngpu_chunk *__restrict__ chunks, uint64_t n, DictDevice dict,
+    const ngpu_dict_hit *__restrict__ hits, uint32_t n_blobs, uint32_t align,
+    ngpu_layer_stats *__restrict__ st, ngpu_result *__restrict__ out) {
+  __shared__ uint64_t table[kLdsSlots];
+  __shared__ uint64_t off[kLdsChunks];   // exclusive prefix of aligned NEW sizes
+  __shared__ uint32_t len_s[kLdsChunks];
+  __shared__ uint32_t nidx[kLdsChunks];  // exclusive prefix of NEW flags
+  __shared__ uint32_t bf[kLdsBlobs], real[kLdsBlobs];
+  __shared__ uint64_t wsum[2][4][kSmallThreads / 64];
+  __shared__ uint32_t used_all;
+  const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const uint32_t nbo = n_blobs + 1;
+  uint32_t mask = 63;
+  while (mask + 1 < 2 * n) mask = mask * 2 + 1;
+  for (uint32_t i = t; i <= mask; i += kSmallThreads) table[i] = kEmpty;
+  for (uint32_t i = t; i < nbo; i += kSmallThreads) bf[i] = kNone;
+  if (t == 0) used_all = 0;
+  __syncthreads();
+  // A: dict decisions (DICT results written now) and the intra-layer table.
+  // Item k of thread t is chunk k * kSmallThreads + t (rows, for the scans).
+  // Per chunk, for phase B: len_s = length | DICT flag (bit 31), off = the
+  // digest's tag : bucket (overwritten by the chunk's offset prefix in B).
+  constexpr uint32_t kDictBit = 0x80000000u;
+#pragma unroll 1
+  for (int k = 0; k < kLdsItems; ++k) {
+    const uint64_t c = (uint64_t)k * kSmallThreads + t;
+    if (c >= n) break;
+    uint32_t dg[8];
+    load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, dg);
+    const uint32_t len = chunks[c].length;
+    ngpu_dict_hit h{kNone, 0, 0, 0, 0};
+    if (hits) h = hits[c];
+    else if (dict.m) h = dict_hit_of(dict, dict_lookup(dict, dg));
+    ngpu_result &r = out[c];
+    if (h.entry != kNone && (h.usize == 0 || h.usize == len) && h.blob < n_blobs) {
+      len_s[c] = len | kDictBit;
+      r.kind = NGPU_DICT;
+      r.ref = h.entry;
+      r.index = h.index;
+      r.blob_index = h.blob;  // inner index; remapped below
+      r.uncompressed_offset = h.uncompressed_offset;  // chunk.copy_from(cached_chunk)
+      r.dict_blob = h.blob;
+      atomicMin(&bf[h.blob], (uint32_t)c);
+      continue;
+    }
+    len_s[c] = len;
+    r.dict_blob = 0;
+    const uint32_t tag = digest_tag(dg), bucket = (uint32_t)digest_bucket(dg);
+    off[c] = ((uint64_t)tag << 32) | bucket;
+    const uint64_t mine = ((uint64_t)tag << 32) | c;
+    for (uint32_t p = bucket & mask;; p = (p + 1) & mask) {
+      uint64_t sv = table[p];
+      if (sv == kEmpty) {
+        const uint64_t old = atomicCAS((unsigned long long *)&table[p], (unsigned long long)kEmpty,
+                                       (unsigned long long)mine);
+        if (old == kEmpty) break;
+        sv = old;
+      }
+      if ((uint32_t)(sv >> 32) == tag &&
+          digest_eq<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), (uint32_t)sv, dg)) {
+        if ((uint32_t)sv > c) atomicMin((unsigned long long *)&table[p], (unsigned long long)mine);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  // B: resolve INTRA / NEW and scan the four per-chunk quantities in chunk
+  // order, one row of kSmallThreads chunks at a time (one barrier per row).
+  // an INTRA chunk's len_s becomes kIntraBit | its first occurrence once
+  // resolved: no later chunk reads it (a first occurrence is always the
+  // smallest id of its digest, never an INTRA chunk)
+  constexpr uint32_t kIntraBit = 0x40000000u;
+  uint64_t carry[4] = {0, 0, 0, 0};
+  __shared__ uint32_t own_first;
+  if (t == 0) own_first = kNone;
+#pragma unroll 1
+  for (int k = 0; k < kLdsItems; ++k) {
+    const uint64_t c = (uint64_t)k * kSmallThreads + t;
+    uint64_t v[4] = {0, 0, 0, 0};  // NEW, aligned size, bytes, DICT
+    if (c < n) {
+      const uint32_t lv = len_s[c];
+      if (lv & kDictBit) {
+        v[3] = 1;
+      } else {
+        const uint64_t tb = off[c];
+        const uint32_t tag = (uint32_t)(tb >> 32);
+        uint32_t f = kNone;
+        for (uint32_t p = (uint32_t)tb & mask;; p = (p + 1) & mask) {
+          const uint64_t sv = table[p];
+          if (sv == kEmpty) break;
+          const uint32_t id = (uint32_t)sv;
+          if ((uint32_t)(sv >> 32) != tag) continue;
+          if (id == c) {
+            f = id;
+            break;
+          }
+          uint32_t dg[8];  // a tag match with another chunk: compare the digests
+          load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, dg);
+          if (digest_eq<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), id, dg)) {
+            f = id;
+            break;
+          }
+        }
+        const uint32_t len = lv;
+        if (f != (uint32_t)c && f != kNone && (len_s[f] & ~kDictBit) == len) {
+          len_s[c] = kIntraBit | f;  // INTRA
+        } else {
+          v[0] = 1;
+          v[1] = ((uint64_t)len + align - 1) / align * align;
+          v[2] = len;
+        }
+      }
+    }
+    if ((uint64_t)k * kSmallThreads >= n) break;  // uniform: the row is empty
+    uint64_t x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = v[q];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t y = __shfl_up(x[q], o, 64);
+        if (lane >= o) x[q] += y;
+      }
+    }
+    const uint32_t b = k & 1;  // double-buffered: one barrier per row
+    if (lane == 63) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wsum[b][q][wid] = x[q];
+    }
+    __syncthreads();
+    uint64_t pre[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll 4
+      for (int w = 0; w < (int)(kSmallThreads / 64); ++w) {
+        const uint64_t y = wsum[b][q][w];
+        if (w < (int)wid) pre[q] += y;
+        tot[q] += y;
+      }
+    }
+    if (c < n) {
+      nidx[c] = (uint32_t)(carry[0] + pre[0] + x[0] - v[0]);
+      off[c] = carry[1] + pre[1] + x[1] - v[1];
+      if (v[0]) atomicMin(&own_first, (uint32_t)c);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) carry[q] += tot[q];
+  }
+  __syncthreads();
+  // C: blob order of the layer: dict blobs at their first hit, the own blob
+  // at its first NEW chunk ([nydus v2.3.0] alloc_index / get_or_create_current_blob)
+  if (t == 0) bf[nbo - 1] = own_first;
+  __syncthreads();
+  uint32_t used = 0;
+  for (uint32_t b = t; b < nbo; b += kSmallThreads) {
+    const uint32_t fb = bf[b];
+    uint32_t rank = kNone;
+    if (fb != kNone) {
+      rank = 0;
+      for (uint32_t o = 0; o < nbo; ++o) rank += bf[o] < fb;
+      ++used;
+    }
+    real[b] = rank;
+  }
+  if (used) atomicAdd(&used_all, used);
+  __syncthreads();
+  // D: final per-chunk fields and the layer stats
+  const uint32_t own = real[nbo - 1];
+#pragma unroll 1
+  for (int k = 0; k < kLdsItems; ++k) {
+    const uint64_t c = (uint64_t)k * kSmallThreads + t;
+    if (c >= n) break;
+    ngpu_result &r = out[c];
+    const uint32_t lv = len_s[c];
+    if (lv & kDictBit) {
+      r.blob_index = real[r.dict_blob];
+    } else if (lv & kIntraBit) {
+      const uint32_t f = lv & ~kIntraBit;
+      r.kind = NGPU_INTRA;
+      r.ref = f;
+      r.index = nidx[f];
+      r.uncompressed_offset = off[f];
+      r.blob_index = own;
+    } else {
+      r.kind = NGPU_NEW;
+      r.ref = c;
+      r.index = nidx[c];
+      r.uncompressed_offset = off[c];
+      r.blob_index = own;
+    }
+  }
+  if (t == 0) {
+    ngpu_layer_stats x{};
+    x.chunks = n;
+    x.new_chunks = carry[0];
+    x.dict_chunks = carry[3];
+    x.intra_chunks = n - carry[0] - carry[3];
+    x.new_bytes = carry[2];
+    x.own_blob_index = own;  // kNone -> 0xFFFFFFFF
+    x.blobs = used_all;
+    x.uncompressed_size = carry[1];
+    st[0] = x;
+  }
+}
+
 }  // namespace
 
 void launch_dict_build(const DictRec *rec, uint64_t m, uint64_t *table, uint64_t cap,
@@ -772,6 +997,11 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
   const DedupInit a{lfirst, L, n, single, ws.chunk_layer, ws.blob_first, nbf,
                     reinterpret_cast<uint64_t *>(st), nst, ws.intra, icap, ts, ntw,
                     ws.newflag, ws.uoff, ws.nbytes, ws.ndict, total};
+  if (small && single && nbo <= kLdsBlobs) {  // one layer: the whole stage in LDS
+    hipExtLaunchKernelGGL(dedup_small_lds, dim3(1), dim3(kSmallThreads), 0, s, nullptr, ev_end, 0,
+                          chunks, n, dict, hits, n_blobs, align, st, out);
+    return;
+  }
   if (small) {
     static_assert(kSmallDedupChunks <= kSmallThreads * kSmallItems, "one scan pass");
     hipExtLaunchKernelGGL(dedup_small, dim3(1), dim3(kSmallThreads), 0, s, nullptr, ev_end, 0, a,
