@@ -1034,7 +1034,10 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
     const uint64_t *__restrict__ gbase, const uint32_t *__restrict__ tree_list,
     const uint64_t *__restrict__ queued, uint64_t cap_g,
     uint32_t *__restrict__ cv, ngpu_result *__restrict__ out, bool all_queued) {
-  __shared__ uint32_t t[kTile * 8];
+  // two tiles, ping-pong: a level reads one and writes the other, so it needs
+  // one barrier (the chain of ~10 narrow levels is the kernel's time on a
+  // small layer; with one tile each level read, barriered, wrote, barriered)
+  __shared__ uint32_t tt[2][kTile * 8];
   const int tid = threadIdx.x;
   // a quad of lanes per parent: this lane's column and schedule word offsets
   // in a parent's 16-word message (the two child CVs, adjacent in t)
@@ -1059,13 +1062,15 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
       for (uint64_t tile = 0; tile < ntiles; ++tile) {
         uint32_t cnt = (uint32_t)min<uint64_t>(kTile, k - tile * kTile);
         const uint32_t *src = a + tile * kTile * 8;
-        for (uint32_t w = tid; w < cnt * 8; w += kTreeThreads) t[w] = src[w];
+        for (uint32_t w = tid; w < cnt * 8; w += kTreeThreads) tt[0][w] = src[w];
         __syncthreads();
+        int cur = 0;
         while (cnt > 1) {
+          const uint32_t *t = tt[cur];
+          uint32_t *o = tt[cur ^ 1];
           const uint32_t p = cnt >> 1;
           const uint32_t pflags = PARENT | ((final_pass && cnt == 2) ? ROOT : 0);
           const uint32_t dq = qlane == 2 ? 64u : qlane == 3 ? pflags : 0u;
-          uint32_t rx[2], ry[2];
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
             const uint32_t pi = qid + s * kTreeQuads;
@@ -1073,38 +1078,22 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
               uint32_t m[28];
 #pragma unroll
               for (int k2 = 0; k2 < 28; ++k2) m[k2] = t[16 * pi + wo[k2]];
-              rx[s] = ivq;
-              ry[s] = ivh;
-              compress_quad(rx[s], ry[s], m, ivq, dq);
+              uint32_t rx = ivq, ry = ivh;
+              compress_quad(rx, ry, m, ivq, dq);
+              o[8 * pi + qlane] = rx;
+              o[8 * pi + 4 + qlane] = ry;
             }
           }
-          uint32_t odd[8];
-          const bool has_odd = (cnt & 1) && tid == 0;
-          if (has_odd) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) odd[i] = t[8 * (cnt - 1) + i];
-          }
+          if ((cnt & 1) && tid < 8) o[8 * p + tid] = t[8 * (cnt - 1) + tid];  // odd tail promoted
           __syncthreads();
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const uint32_t pi = qid + s * kTreeQuads;
-            if (pi < p) {
-              t[8 * pi + qlane] = rx[s];
-              t[8 * pi + 4 + qlane] = ry[s];
-            }
-          }
-          if (has_odd) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) t[8 * p + i] = odd[i];
-          }
-          __syncthreads();
+          cur ^= 1;
           cnt = p + (cnt & 1);
         }
         if (tid < 8) {
           if (final_pass)
-            reinterpret_cast<uint32_t *>(out[c].digest)[tid] = t[tid];
+            reinterpret_cast<uint32_t *>(out[c].digest)[tid] = tt[cur][tid];
           else
-            a[tile * 8 + tid] = t[tid];
+            a[tile * 8 + tid] = tt[cur][tid];
         }
         __syncthreads();
       }
