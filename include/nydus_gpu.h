@@ -19,8 +19,15 @@
  * exceptions cross the ABI.  A missing or unusable GPU is an error
  * (NGPU_ENODEV): there is no CPU fallback in this library.
  *
- * Threading: an engine serialises its own calls internally; use one engine
- * per goroutine pool / per device for concurrency.
+ * Threading: one engine per device serves any number of goroutines.  Calls
+ * take the engine's lock only while they enqueue work.  Calls on distinct
+ * streams use distinct HBM workspaces (NGPU_WS_SLOTS, default 4) and run side
+ * by side on the GPU; calls on one stream are ordered by it.  Every pack has
+ * its own compute stream and waits for it, and writes its blob stream,
+ * outside the lock, so Packs of an image's layers proceed concurrently.  A
+ * split-stage caller (ngpu_digest_device, then ngpu_dedup_device) keeps both
+ * stages of a layer on one stream: the dedup stage reports the bad-descriptor
+ * count of the digest stage that ran last on its workspace.
  *
  * Lifetimes: engines, chunk dicts and packs are reference counted.  A pack
  * holds its engine and the dict it was opened with until it ends (close,
