@@ -175,11 +175,11 @@ int main(int argc, char **argv) {
          el / layers * 1e6, enq_max / (layers / T) * 1e6, same ? "true" : "false",
          (unsigned long long)nw);
   for (auto &l : lanes) {
-    hipFree(l.d_data);
-    hipFree(l.d_ch);
-    hipFree(l.d_out);
-    hipHostFree(l.h_out);
-    hipStreamDestroy(l.s);
+    (void)hipFree(l.d_data);
+    (void)hipFree(l.d_ch);
+    (void)hipFree(l.d_out);
+    (void)hipHostFree(l.h_out);
+    (void)hipStreamDestroy(l.s);
   }
   ngpu_destroy(eng);
   return same ? 0 : 1;
