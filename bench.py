@@ -178,9 +178,9 @@ WORKLOADS = {
     "c5-1000": dict(desc="C5: 1000 layers x 64 MiB (16 x 4 MiB files), 64 KiB chunks, blake3, 30% of "
                          "chunks from a shared pool of 1024 contents; chunk dict (pool + 1M filler) "
                          "partitioned by digest prefix; layers split over the GPUs; one multi-layer "
-                         "dedup launch set per step",
+                         "dedup launch set per step; then one host Merge of the layers' bootstraps",
                     n_files=16, file_size=4 * MiB, chunk=64 * 1024, digester="blake3",
-                    layers_total=1000, pool=1024, dict_entries=1_000_000, sharded=True),
+                    layers_total=1000, pool=1024, dict_entries=1_000_000, sharded=True, merge=True),
     "c5": dict(desc="C5-shape: 16 GiB layer, 64 KiB chunks, blake3, no dict",
                n_files=1024, file_size=16 * MiB, chunk=64 * 1024, digester="blake3", layers=1),
     "small": dict(desc="1 GiB layer, 1 MiB chunks, blake3", n_files=256, file_size=4 * MiB,
@@ -388,6 +388,65 @@ def sharded_dict_extra(torch, dist, eng, buf, d_ch, n, stream, rank, world, back
             "probe_enqueue_ms_median_max_rank": round(float(red[:, 3].max()) * 1e3, 3),
             "dict_hits_all_ranks": hits_all, "planted_all_ranks": planted_all,
             "hits_ok": hits_all == planted_all, "_elapsed": el_max}
+
+
+def merge_extra(nydus_gpu, ch, res, n_layers, per_layer, S, dict_host):
+    """C5's last step ("chunk-dict Merge of 1000 layers", BASELINE configs[4]):
+    after the timed digest + dedup steps, each layer's bootstrap is built from
+    its decisions (RAFS v6: its NEW chunks -- ngpu_chunk_table -- and one
+    record per (digest, blob) it reuses from the dict; blob table = the dict
+    blobs it hit + its own blob, in real-index order), then ONE host
+    ngpu_merge of all of them against the chunk dict bootstrap
+    (convert_unix.go:560-666 -> nydus-image merge, builder.go:220-294).
+    Merge is host bookkeeping: timed and reported here,
+    never part of `value`."""
+    from nydus_gpu import rafs
+    dict_ids = [f"{b:064x}" for b in range(8)]
+    t0 = time.perf_counter()
+    boots, digs = [], []
+    for l in range(n_layers):
+        a, b = l * per_layer, (l + 1) * per_layer
+        cl, rl = ch[a:b], res[a:b]
+        new = nydus_gpu.chunk_table(cl, rl).view(rafs.CHUNK_INFO_DTYPE).reshape(-1)
+        dm = rl["kind"] == nydus_gpu.DICT
+        key = np.concatenate([rl["digest"][dm], rl["blob_index"][dm, None].view(np.uint8)], 1)
+        _, first = np.unique(key, axis=0, return_index=True)
+        sel = np.nonzero(dm)[0][np.sort(first)]
+        dr = np.zeros(len(sel), rafs.CHUNK_INFO_DTYPE)
+        dr["block_id"] = rl["digest"][sel]
+        dr["blob_index"] = rl["blob_index"][sel]
+        dr["compressed_size"] = dr["uncompressed_size"] = cl["length"][sel]
+        dr["uncompressed_offset"] = rl["uncompressed_offset"][sel]
+        dr["file_offset"] = cl["file_offset"][sel]
+        dr["index"] = rl["index"][sel]
+        nb = int(rl["blob_index"].max()) + 1 if len(rl) else 0
+        ids = [""] * nb
+        for r_, i_ in zip(rl["blob_index"][dm], rl["dict_blob"][dm]):
+            ids[r_] = dict_ids[i_]
+        own = f"{0xB10B0000 + l:064x}"
+        ids = [x or own for x in ids]
+        recs = np.concatenate([new, dr])
+        boots.append(rafs.write_v6_bootstrap(recs, S, blobs=rafs.make_blob_table(ids, S)))
+        digs.append(f"{0x1A7E0000 + l:064x}")
+    dg, us, bl, ix = dict_host
+    drec = np.zeros(len(dg), rafs.CHUNK_INFO_DTYPE)
+    drec["block_id"] = dg
+    drec["blob_index"] = bl
+    drec["compressed_size"] = drec["uncompressed_size"] = us
+    drec["index"] = ix
+    drec["uncompressed_offset"] = ix.astype(np.uint64) * S
+    dboot = rafs.write_v6_bootstrap(drec, S, blobs=rafs.make_blob_table(dict_ids, S))
+    build_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    merged, blob_ids = nydus_gpu.merge(boots, digs, dboot)
+    merge_s = time.perf_counter() - t0
+    own_used = sum(1 for x in blob_ids if x not in dict_ids)
+    return {"what": "one host Merge (ngpu_merge) of the step's per-layer bootstraps against the "
+                    "chunk dict bootstrap", "layers": n_layers,
+            "bootstraps_bytes": int(sum(len(b) for b in boots)), "dict_bootstrap_bytes": len(dboot),
+            "bootstrap_build_s": round(build_s, 3), "merge_ms": round(merge_s * 1e3, 2),
+            "merged_bytes": len(merged), "blobs": len(blob_ids), "own_blobs": own_used,
+            "dict_blobs": len(blob_ids) - own_used}
 
 
 def pmc_traffic(path, workload, kernel):
@@ -898,6 +957,9 @@ def main():
         probe = None
         if not wl.get("sharded") and args.probe_queries:
             probe = probe_bench(torch, nydus_gpu, eng, dd, args.probe_queries, build_s)
+        dict_host = None
+        if wl.get("merge") and world == 1:  # the C5 Merge needs the dict bootstrap
+            dict_host = (dd.cpu().numpy(), us.cpu().numpy(), bl.cpu().numpy(), ix.cpu().numpy())
         del dd, us, bl, ix
         torch.cuda.empty_cache()
         extra["dict"] = {"entries": m, "entries_this_gpu": local_m, "build_s": round(build_s, 3),
@@ -985,6 +1047,8 @@ def main():
         extra["dict"]["dict_hits"] = int(kinds[2])
         assert kinds[2] >= extra["dict"]["expected_dict_hits"] * 0.99, (kinds, extra)
     extra["decisions"] = {"NEW": int(kinds[0]), "INTRA": int(kinds[1]), "DICT": int(kinds[2])}
+    if wl.get("merge") and world == 1 and rank == 0:
+        extra["merge"] = merge_extra(nydus_gpu, ch, res, n_layers, per_layer, wl["chunk"], dict_host)
 
     timings = [eng.timing_at(b) for b in range(min(args.steps, 64))]
     total_bytes = file_bytes * args.steps * world

@@ -36,3 +36,43 @@ def test_pool_content_is_a_function_of_the_id():
     # bytes look uniform (no constant high bytes from the shifts)
     counts = np.bincount(a.numpy().ravel(), minlength=256)
     assert counts.min() > 0.5 * counts.mean()
+
+
+def test_merge_extra_on_oracle_decisions():
+    """bench.merge_extra (C5's host Merge): per-layer bootstraps built from
+    dedup decisions, merged against the dict bootstrap -> every layer's own
+    blob plus exactly the dict blobs the layers hit.  Decisions come from the
+    CPU oracle (no GPU), three layers of 12 chunks."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(bench.__file__), "oracle"))
+    import oracle_py
+    S, P, L = 4096, 12, 3
+    rng = np.random.default_rng(4)
+    m = 50
+    dg = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+    us = np.full(m, S, np.int32)
+    bl = (np.arange(m) % 3).astype(np.int32)  # dict blobs 0..2
+    ix = np.arange(m, dtype=np.int32)
+    ch = np.zeros(P * L, nydus_gpu.CHUNK_DTYPE)
+    ch["length"] = S
+    ch["offset"] = np.arange(P * L, dtype=np.uint64) * S
+    ch["file_offset"] = (np.arange(P * L) % P) * S
+    res = np.zeros(P * L, nydus_gpu.RESULT_DTYPE)
+    for l in range(L):
+        dig = rng.integers(0, 256, (P, 32), dtype=np.uint8)
+        dig[0] = dg[l]          # a dict hit on blob l % 3
+        dig[5] = dg[3 + l]      # another one
+        dig[7] = dig[6]         # INTRA
+        dec, _ = oracle_py.dedup(dig, ch["length"][:P], dg, us.view(np.uint32), bl.view(np.uint32),
+                                 ix.view(np.uint32))
+        sl = slice(l * P, (l + 1) * P)
+        for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+            res[f][sl] = dec[f]
+        res["digest"][sl] = dig
+        res["dict_blob"][sl] = np.where(dec["kind"] == nydus_gpu.DICT, bl[np.minimum(dec["ref"], m - 1)], 0)
+    out = bench.merge_extra(nydus_gpu, ch, res, L, P, S, (dg, us, bl, ix))
+    hit_blobs = {int(bl[l]) for l in range(L)} | {int(bl[3 + l]) for l in range(L)}
+    assert out["own_blobs"] == L
+    assert out["dict_blobs"] == len(hit_blobs)
+    assert out["layers"] == L and out["merged_bytes"] > 0
