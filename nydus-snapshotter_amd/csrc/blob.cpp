@@ -42,6 +42,7 @@
 #include <functional>
 #include <mutex>
 #include <set>
+#include <unordered_map>
 #include <thread>
 
 #include "blob.hpp"
@@ -301,7 +302,7 @@ std::string blob_id_of(const RafsV6BlobInfo &b) {
   return std::string(b.blob_id, strnlen(b.blob_id, sizeof b.blob_id));
 }
 
-int parse_bootstrap(const uint8_t *p, uint64_t n, Bootstrap *out) {
+int parse_bootstrap(const uint8_t *p, uint64_t n, Bootstrap *out, bool with_chunks) {
   if (n < kRafsV6ExtSuperBlockOffset + 64) return host_fail(NGPU_EFORMAT, "bootstrap too small");
   uint32_t magic;
   memcpy(&magic, p + kRafsV6SuperBlockOffset, 4);
@@ -320,6 +321,7 @@ int parse_bootstrap(const uint8_t *p, uint64_t n, Bootstrap *out) {
     return host_fail(NGPU_EFORMAT, "bad blob/chunk table bounds");
   out->blobs.resize(bts / sizeof(RafsV6BlobInfo));
   if (bts) memcpy(out->blobs.data(), p + bto, bts);
+  if (!with_chunks) return 0;
   out->chunks.resize(cts / sizeof(RafsV6ChunkInfo));
   if (cts) memcpy(out->chunks.data(), p + cto, cts);
   return 0;
@@ -1010,13 +1012,30 @@ int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
     std::vector<std::string> dict_ids;
     if (dict_bootstrap) {
       Bootstrap d;
-      int rc = parse_bootstrap((const uint8_t *)dict_bootstrap, dict_size, &d);
+      int rc = parse_bootstrap((const uint8_t *)dict_bootstrap, dict_size, &d, false);
       if (rc) return rc;
       for (auto &b : d.blobs) dict_ids.push_back(blob_id_of(b));
     }
     Bootstrap out;
     std::vector<std::string> ids;
-    std::set<std::array<uint8_t, 36>> seen;
+    std::unordered_map<std::string, uint32_t> id_index;  // ids[] position of a blob id
+    // (digest, merged blob index) keys already in the merged table: a flat
+    // open-addressing table of positions in out.chunks (digests are uniform,
+    // so their first 8 bytes mixed with the blob index hash well).  A std::set
+    // of 36-B keys -- a node allocation and a tree walk per record -- took
+    // 0.6 s of C5's 1000-layer, 1M-record Merge.
+    uint64_t total = 0;
+    for (uint64_t l = 0; l < n; ++l) total += sizes[l] / sizeof(RafsV6ChunkInfo);
+    uint64_t cap = 1024;
+    while (cap < 2 * total) cap <<= 1;
+    std::vector<uint32_t> slot(cap, 0xFFFFFFFFu);
+    out.chunks.reserve((size_t)total);
+    auto key_hash = [](const RafsV6ChunkInfo &c) {
+      uint64_t a, b;
+      memcpy(&a, c.block_id, 8);
+      memcpy(&b, c.block_id + 8, 8);
+      return (a ^ (b * 0x9E3779B97F4A7C15ull)) + c.blob_index * 0xC2B2AE3D27D4EB4Full;
+    };
     for (uint64_t l = 0; l < n; ++l) {
       Bootstrap b;
       int rc = parse_bootstrap((const uint8_t *)bootstraps[l], sizes[l], &b);
@@ -1039,8 +1058,9 @@ int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
                              (unsigned long long)l);
           if (layer_digests && layer_digests[l] && layer_digests[l][0]) id = layer_digests[l];
         }
-        auto it = std::find(ids.begin(), ids.end(), id);
-        if (it == ids.end()) {
+        auto it = id_index.find(id);
+        if (it == id_index.end()) {
+          id_index.emplace(id, (uint32_t)ids.size());
           ids.push_back(id);
           RafsV6BlobInfo nb = b.blobs[i];
           memset(nb.blob_id, 0, sizeof nb.blob_id);
@@ -1049,7 +1069,7 @@ int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
           out.blobs.push_back(nb);
           local[i] = nb.blob_index;
         } else {
-          local[i] = (uint32_t)(it - ids.begin());
+          local[i] = it->second;
         }
       }
       for (RafsV6ChunkInfo c : b.chunks) {
@@ -1057,10 +1077,17 @@ int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
         c.blob_index = local[c.blob_index];
         // layers packed against one chunk dict each carry the dict chunks they
         // reuse: the merged table keeps one record per (digest, blob)
-        std::array<uint8_t, 36> key;
-        memcpy(key.data(), c.block_id, 32);
-        memcpy(key.data() + 32, &c.blob_index, 4);
-        if (!seen.insert(key).second) continue;
+        uint64_t h = key_hash(c) & (cap - 1);
+        bool dup = false;
+        for (; slot[h] != 0xFFFFFFFFu; h = (h + 1) & (cap - 1)) {
+          const RafsV6ChunkInfo &o = out.chunks[slot[h]];
+          if (o.blob_index == c.blob_index && memcmp(o.block_id, c.block_id, 32) == 0) {
+            dup = true;
+            break;
+          }
+        }
+        if (dup) continue;
+        slot[h] = (uint32_t)out.chunks.size();
         out.chunks.push_back(c);
       }
     }

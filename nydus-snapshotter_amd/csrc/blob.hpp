@@ -92,7 +92,8 @@ struct Bootstrap {
   std::vector<RafsV6BlobInfo> blobs;
   std::vector<RafsV6ChunkInfo> chunks;
 };
-int parse_bootstrap(const uint8_t *p, uint64_t n, Bootstrap *out);
+// with_chunks = false: the blob table only (the chunk table is still bounds-checked)
+int parse_bootstrap(const uint8_t *p, uint64_t n, Bootstrap *out, bool with_chunks = true);
 std::vector<uint8_t> write_bootstrap(const Bootstrap &b);
 std::string blob_id_of(const RafsV6BlobInfo &b);
 
