@@ -1118,3 +1118,55 @@ def test_reference_v6_bootstrap_as_chunk_dict(tmp_path):
     assert np.array_equal(got["index"], fx["index"])
     assert np.array_equal(got["uncompressed_offset"], fx["uncompressed_offset"])
     assert st["own_blob_index"] == 0xFFFFFFFF and st["blobs"] == 1
+
+
+def test_reference_v5_bootstrap_as_chunk_dict(tmp_path, oracle):
+    """FsVersion "5" with ChunkDictPath = the reference's real v5 nydus-image
+    bootstrap (RAFS v5 keeps each file's chunk infos after its inode; the dict
+    is every file's chunks in inode-table order, first insertion wins).  The
+    fixture's chunk stream replayed against it (plus random chunks) equals
+    the oracle dedup against the same records; a v5 dict on a FsVersion 6
+    engine and a v6 dict on a FsVersion 5 engine are rejected."""
+    import rafs_fixtures
+    from test_oracle import V5_FIXTURE, V6_FIXTURE
+    boot = rafs_fixtures.boot_from_targz(V5_FIXTURE)
+    path = tmp_path / "v5.boot"
+    path.write_bytes(boot)
+    v5 = rafs_fixtures.read_v5(boot)
+    recs = np.concatenate([f[4] for f in v5["files"]])
+    rng = np.random.default_rng(55)
+    n = 3000
+    pick = rng.integers(0, len(recs), n)
+    res = np.zeros(n, nydus_gpu.RESULT_DTYPE)
+    res["digest"] = recs["block_id"][pick]
+    res["digest"][::7] = rng.integers(0, 256, (len(res["digest"][::7]), 32), dtype=np.uint8)
+    ch = np.zeros(n, nydus_gpu.CHUNK_DTYPE)
+    ch["length"] = recs["uncompressed_size"][pick]
+    ch["length"][::7] = rng.integers(1, 0x100000, len(ch["length"][::7]))
+    eng = nydus_gpu.Engine(chunk_size=v5["block_size"], fs_version=5)
+    try:
+        d = eng.dict_open(str(path))
+        assert d.entries == len(recs)
+        eng.set_dict(d)
+        d.release()
+        d_out, d_ch = _to_dev(res), _to_dev(ch)
+        st = eng.dedup_device(d_ch.data_ptr(), n, d_out.data_ptr(), want_stats=True)
+        got = d_out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+    finally:
+        eng.close()
+    exp, _ = oracle.dedup(res["digest"], ch["length"], recs["block_id"], recs["uncompressed_size"],
+                          recs["blob_index"], recs["index"], align=1,
+                          dict_uoff=recs["uncompressed_offset"])
+    for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+        assert np.array_equal(got[f], exp[f]), f
+    assert st["dict_chunks"] == int((exp["kind"] == nydus_gpu.DICT).sum()) > n // 2
+    # version pairing
+    v6path = tmp_path / "v6.boot"
+    v6path.write_bytes(rafs_fixtures.boot_from_targz(V6_FIXTURE))
+    for fs, pth in ((6, path), (5, v6path)):
+        e2 = nydus_gpu.Engine(chunk_size=0x100000, fs_version=fs)
+        try:
+            with pytest.raises(nydus_gpu.NgpuError, match="inconsistent version"):
+                e2.dict_open(str(pth))
+        finally:
+            e2.close()
