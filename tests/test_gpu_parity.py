@@ -1170,3 +1170,31 @@ def test_reference_v5_bootstrap_as_chunk_dict(tmp_path, oracle):
                 e2.dict_open(str(pth))
         finally:
             e2.close()
+
+
+@pytest.mark.parametrize("blobs", [1000, 1500])
+def test_small_layer_dict_with_many_blobs(oracle, blobs):
+    """A small single-layer call against a dict of many inner blobs: up to
+    1023 the whole dedup stage stays in LDS (dedup_small_lds ranks the blobs
+    there), beyond it the global small path takes over; both equal the oracle,
+    blob allocation order included."""
+    rng = np.random.default_rng(21 + blobs)
+    data, ch = _random_layer(rng, 6 << 20, 0x10000, dup_frac=0.3)
+    dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    n = len(ch)
+    pick = rng.choice(n, n // 2, replace=False)
+    dd = np.concatenate([rng.integers(0, 256, (3000, 32), dtype=np.uint8), dig[pick]])
+    ds = np.concatenate([rng.integers(1, 1 << 16, 3000), ch["length"][pick]]).astype(np.uint32)
+    db = (np.arange(len(dd)) * 7919 % blobs).astype(np.uint32)
+    di = np.arange(len(dd), dtype=np.uint32)
+    exp, _ = oracle.dedup(dig, ch["length"], dd, ds, db, di)
+    eng = nydus_gpu.Engine(chunk_size=0x10000)
+    try:
+        eng.dict_load(dd, ds, db, di)
+        out, st = eng.process(data, ch)
+    finally:
+        eng.close()
+    for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+        assert np.array_equal(out[f], exp[f]), f
+    assert st["dict_chunks"] == int((exp["kind"] == 2).sum()) > 0
+    assert st["blobs"] == len(set(out["blob_index"].tolist()))
