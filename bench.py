@@ -1067,7 +1067,9 @@ def main():
         achieved = comp * OPS_PER_COMPRESSION / (dig_ms / 1e3)
         # launch_blake3's rule: one leaf per lane quad for <= 32K leaves at D = 0
         quad = D == 0 and int(buf.numel()) // 1024 + n <= 32768
-        kname = "b3_quad_leaves" if quad else f"b3_groups<{D}>"
+        # <= 4096 chunks: planning inside the leaf kernel (b3_quad_planned)
+        kname = (("b3_quad_planned" if n <= 4096 else "b3_quad_leaves") if quad
+                 else f"b3_groups<{D}>")
         roof = {"bound": "valu", "kernel": kname, "achieved": round(achieved / 1e12, 3),
                 "peak": round(PEAK_INT_OPS / 1e12, 3), "unit": "Tops/s",
                 "frac": round(achieved / PEAK_INT_OPS, 4), "traffic": None,
