@@ -1164,17 +1164,19 @@ def main():
             line["speedup_vs_cpu_pcie_inclusive"] = {
                 k: round(e2e[k] / cpu["value"], 2) for k in ("host_path_gbs", "streaming_gbs")
                 if k in e2e}
+    dog = None
+    printed = [False]
     if dist and sdict is None and n_layers == 1 and not args.no_sharded_extra:
         # the headline is already measured; a watchdog keeps a stuck collective
-        # from costing the line (rank 0 prints it without this entry)
+        # (here, or in the closing barrier after a rank failed in here) from
+        # costing the line: on expiry rank 0 prints it if it has not yet, and
+        # every rank exits
         import threading
 
         def stuck():
-            if rank == 0:
-                print(json.dumps(dict(pending_line[0], sharded_dict={"error": "timeout"})),
-                      flush=True)
+            if rank == 0 and not printed[0]:
+                print(json.dumps(dict(line, sharded_dict={"error": "timeout"})), flush=True)
             os._exit(0)
-        pending_line = [line]
         dog = threading.Timer(120.0, stuck)
         dog.daemon = True
         dog.start()
@@ -1185,13 +1187,15 @@ def main():
             line["sharded_dict"] = sx
         except Exception as ex:  # reported, never fatal to the headline line
             line["sharded_dict"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
-        dog.cancel()
     if rank == 0:
         print(json.dumps(line), flush=True)
+        printed[0] = True
     eng.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+    if dog:
+        dog.cancel()
 
 
 if __name__ == "__main__":
