@@ -1198,3 +1198,37 @@ def test_small_layer_dict_with_many_blobs(oracle, blobs):
         assert np.array_equal(out[f], exp[f]), f
     assert st["dict_chunks"] == int((exp["kind"] == 2).sum()) > 0
     assert st["blobs"] == len(set(out["blob_index"].tolist()))
+
+
+def test_v5_dict_bootstrap_fuzz(tmp_path):
+    """Corrupted RAFS v5 chunk-dict bootstraps (the file is untrusted input):
+    every mutation either loads or fails with an NgpuError -- never a crash
+    or a hang.  Mutations: truncation at random points, random bytes over the
+    super block, the inode table, inodes and their chunk arrays."""
+    import rafs_fixtures
+    from test_oracle import V5_FIXTURE
+    boot = bytearray(rafs_fixtures.boot_from_targz(V5_FIXTURE))
+    rng = np.random.default_rng(77)
+    eng = nydus_gpu.Engine(chunk_size=0x100000, fs_version=5)
+    loaded = failed = 0
+    try:
+        for k in range(150):
+            b = bytearray(boot)
+            if k % 3 == 0:
+                b = b[: int(rng.integers(0, len(b)))]
+            else:
+                lo = 0 if k % 3 == 1 else 8192
+                for _ in range(int(rng.integers(1, 8))):
+                    p = int(rng.integers(lo, len(b) - 8))
+                    b[p:p + 8] = rng.integers(0, 256, 8, dtype=np.uint8).tobytes()
+            path = tmp_path / f"f{k}.boot"
+            path.write_bytes(bytes(b))
+            try:
+                d = eng.dict_open(str(path))
+                d.release()
+                loaded += 1
+            except nydus_gpu.NgpuError:
+                failed += 1
+    finally:
+        eng.close()
+    assert loaded + failed == 150 and failed > 0
