@@ -160,17 +160,17 @@ ngpu_ws_slot *use_slot(ngpu_engine *e, hipStream_t s) {
       pick = &sl;
       break;
     }
-  if (!pick)  // an idle slot: never used, or its last stage has ended
-    for (auto &sl : e->slots) {
+  if (!pick)  // a slot never used yet
+    for (auto &sl : e->slots)
       if (!sl.pending) {
         pick = &sl;
         break;
       }
-      if (sl.last_ev && hipEventQuery(sl.last_ev) == hipSuccess &&
-          (!pick || sl.tick < pick->tick))
-        pick = &sl;
-    }
-  if (!pick)  // all busy: the least recently used (ws_acquire waits for it)
+  // else the least recently used: with streams taking turns it is the one
+  // most likely finished, and ws_acquire's GPU-side wait costs nothing then.
+  // (Querying every slot's event first cost ~1-2 us of host time per slot
+  // and call, on a path the host enqueue already bounds.)
+  if (!pick)
     for (auto &sl : e->slots)
       if (!pick || sl.tick < pick->tick) pick = &sl;
   pick->tick = ++e->tick;

@@ -68,8 +68,9 @@ def test_bench_pool_digests_match_planted_chunks():
 
 def test_calls_on_different_streams_share_the_workspace_in_order():
     """Back-to-back device-path calls on two different streams (no host sync
-    between them) use one engine workspace: the engine orders each stage
-    after the previous one, so every call's results equal the oracle's."""
+    between them) on one engine: whether they share a workspace (ordered on
+    the GPU) or take one each (NGPU_WS_SLOTS), every call's results equal
+    the oracle's."""
     import nydus_gpu
     import oracle_py
     S = 64 << 10
@@ -92,14 +93,15 @@ def test_calls_on_different_streams_share_the_workspace_in_order():
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     eng = nydus_gpu.Engine(device=0, digester="blake3", chunk_size=S)
     try:
+        # outputs zero-filled on torch's stream and complete before any call
+        # (the calls run on other streams, unordered with that fill)
+        outs = [(k % 2, torch.zeros(layers[k % 2][2] * 64, dtype=torch.uint8, device="cuda"))
+                for k in range(6)]
         torch.cuda.synchronize()
-        outs = []
-        for k in range(6):
-            d_data, d_ch, P, _, _ = layers[k % 2]
-            out = torch.zeros(P * 64, dtype=torch.uint8, device="cuda")
+        for k, (li, out) in enumerate(outs):
+            d_data, d_ch, P, _, _ = layers[li]
             eng.process_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), P, out.data_ptr(),
-                               stream=streams[k % 2].cuda_stream)
-            outs.append((k % 2, out))
+                               stream=streams[li].cuda_stream)
         torch.cuda.synchronize()
         for k, (li, out) in enumerate(outs):
             _, _, P, dig, dec = layers[li]
@@ -144,13 +146,15 @@ def test_pack_on_engine_stream_interleaved_with_device_calls(oracle):
     try:
         torch.cuda.synchronize()
         w = eng.pack()
-        outs = []
-        for pos in range(0, len(tb), 300 << 10):
+        # outputs zero-filled on torch's stream and complete before the calls
+        # on `s` (unordered with that fill)
+        outs = [torch.zeros(P * 64, dtype=torch.uint8, device="cuda")
+                for _ in range(0, len(tb), 300 << 10)]
+        torch.cuda.synchronize()
+        for pos, out in zip(range(0, len(tb), 300 << 10), outs):
             w.write(tb[pos:pos + (300 << 10)])
-            out = torch.zeros(P * 64, dtype=torch.uint8, device="cuda")
             eng.process_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), P,
                                out.data_ptr(), stream=s.cuda_stream)
-            outs.append(out)
         pch, pout, _ = w.close()
         torch.cuda.synchronize()
     finally:
