@@ -92,6 +92,14 @@ struct Bootstrap {
   std::vector<RafsV6BlobInfo> blobs;
   std::vector<RafsV6ChunkInfo> chunks;
 };
+constexpr uint32_t kRafsV5Magic = 0x52414653u;  // "RAFS"
+constexpr uint32_t kRafsV5Version = 0x500;
+// A RAFS v5 bootstrap as a chunk dict: every regular file's 80-B chunk infos
+// in inode-table order (recs) and its blobs as 256-B v6 blob records (blobs);
+// *digester / *chunk_size from its flags / block size.  Untrusted input:
+// every offset is bounds-checked (NGPU_EFORMAT + ngpu_host_error()).
+int parse_v5_bootstrap(const uint8_t *p, uint64_t n, uint32_t *digester, uint32_t *chunk_size,
+                       std::vector<uint8_t> *recs, std::vector<uint8_t> *blobs);
 // with_chunks = false: the blob table only (the chunk table is still bounds-checked)
 int parse_bootstrap(const uint8_t *p, uint64_t n, Bootstrap *out, bool with_chunks = true);
 std::vector<uint8_t> write_bootstrap(const Bootstrap &b);
