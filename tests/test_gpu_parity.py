@@ -1200,16 +1200,17 @@ def test_small_layer_dict_with_many_blobs(oracle, blobs):
     assert st["blobs"] == len(set(out["blob_index"].tolist()))
 
 
-def test_v5_dict_bootstrap_fuzz(tmp_path):
-    """Corrupted RAFS v5 chunk-dict bootstraps (the file is untrusted input):
-    every mutation either loads or fails with an NgpuError -- never a crash
-    or a hang.  Mutations: truncation at random points, random bytes over the
-    super block, the inode table, inodes and their chunk arrays."""
+@pytest.mark.parametrize("fs", [5, 6])
+def test_dict_bootstrap_fuzz(tmp_path, fs):
+    """Corrupted RAFS v5 / v6 chunk-dict bootstraps (the file is untrusted
+    input): every mutation either loads or fails with an NgpuError -- never a
+    crash or a hang.  Mutations: truncation at random points, random bytes
+    over the super blocks, the inode / blob / chunk tables."""
     import rafs_fixtures
-    from test_oracle import V5_FIXTURE
-    boot = bytearray(rafs_fixtures.boot_from_targz(V5_FIXTURE))
-    rng = np.random.default_rng(77)
-    eng = nydus_gpu.Engine(chunk_size=0x100000, fs_version=5)
+    from test_oracle import V5_FIXTURE, V6_FIXTURE
+    boot = bytearray(rafs_fixtures.boot_from_targz(V5_FIXTURE if fs == 5 else V6_FIXTURE))
+    rng = np.random.default_rng(77 + fs)
+    eng = nydus_gpu.Engine(chunk_size=0x100000, fs_version=fs)
     loaded = failed = 0
     try:
         for k in range(150):
@@ -1217,7 +1218,7 @@ def test_v5_dict_bootstrap_fuzz(tmp_path):
             if k % 3 == 0:
                 b = b[: int(rng.integers(0, len(b)))]
             else:
-                lo = 0 if k % 3 == 1 else 8192
+                lo = 0 if k % 3 == 1 else (8192 if fs == 5 else 1024)
                 for _ in range(int(rng.integers(1, 8))):
                     p = int(rng.integers(lo, len(b) - 8))
                     b[p:p + 8] = rng.integers(0, 256, 8, dtype=np.uint8).tobytes()
