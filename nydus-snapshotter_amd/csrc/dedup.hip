@@ -20,6 +20,7 @@
 // {tag = digest word 2 : id}; bucket = (digest words 0,1) * golden ratio.
 // Roofline: HBM-bound probes.
 #include <stddef.h>
+#include <stdlib.h>
 
 #include <hip/hip_ext.h>
 
@@ -120,6 +121,55 @@ __global__ void dict_probe_records(const uint8_t *__restrict__ digests, uint64_t
     e = dict_lookup(dict, d);
   }
   hits[q] = dict_hit_of(dict, e);
+}
+
+// The wavefront-cooperative form of the same lookup (the north star's
+// "chunk-dict hash table ... probed with wavefront-cooperative open
+// addressing"; A/B against dict_probe_records, NGPU_PROBE_COOP=1): 16 lanes
+// per query read 16 consecutive slots from the query's bucket in one
+// coalesced access, ballot for the first empty slot and the tag matches
+// before it, and verify those in probe order -- the decisions of sequential
+// linear probing, with the slot reads of a probe run side by side instead of
+// one dependent load per slot.
+__global__ __launch_bounds__(256) void dict_probe_coop(const uint8_t *__restrict__ digests,
+                                                       uint64_t stride, uint64_t n,
+                                                       DictDevice dict,
+                                                       ngpu_dict_hit *__restrict__ hits) {
+  const uint64_t q = (blockIdx.x * 256ull + threadIdx.x) >> 4;
+  const uint32_t sub = threadIdx.x & 15, grp = (threadIdx.x & 63) >> 4;
+  const bool live = q < n;
+  uint32_t e = kNone;
+  if (live && dict.m) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(digests + q * stride);
+    const uint4 a = p[0], b = p[1];
+    const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const uint32_t tag = digest_tag(d);
+    uint64_t pos = digest_bucket(d) & dict.mask;
+    for (;;) {
+      const uint64_t sv = dict.table[(pos + sub) & dict.mask];
+      const bool empty = sv == kEmpty, match = !empty && (uint32_t)(sv >> 32) == tag;
+      // this group's 16 bits of the wave's ballots (a wave holds 4 groups;
+      // groups of one wave may run different numbers of rounds)
+      const uint32_t me = (uint32_t)(__ballot(empty) >> (16 * grp)) & 0xFFFFu;
+      uint32_t mm = (uint32_t)(__ballot(match) >> (16 * grp)) & 0xFFFFu;
+      const uint32_t fe = me ? (uint32_t)__builtin_ctz(me) : 16u;
+      mm &= (1u << fe) - 1u;
+      bool found = false;
+      while (mm) {
+        const uint32_t i = (uint32_t)__builtin_ctz(mm);
+        const uint32_t id = (uint32_t)__shfl(sv, (int)(16 * grp + i), 64);
+        if (digest_eq<sizeof(DictRec)>(reinterpret_cast<const uint8_t *>(dict.rec), id, d)) {
+          e = id;
+          found = true;
+          break;
+        }
+        mm &= mm - 1;
+      }
+      if (found || fe < 16) break;
+      pos += 16;
+    }
+  }
+  if (live && sub == 0) hits[q] = dict_hit_of(dict, e);
 }
 
 // RAFS v6 chunk-info records (80 B: block_id[32], blob_index, flags,
@@ -883,6 +933,15 @@ void launch_dict_build(const DictRec *rec, uint64_t m, uint64_t *table, uint64_t
 void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
                        const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s) {
   if (n == 0) return;
+  static const bool coop = [] {  // A/B knob (bench.py probe_roofline)
+    const char *v = getenv("NGPU_PROBE_COOP");
+    return v && v[0] == '1';
+  }();
+  if (coop) {
+    hipLaunchKernelGGL(dict_probe_coop, dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), 0, s,
+                       digests, stride, n, dict, hits);
+    return;
+  }
   hipLaunchKernelGGL(dict_probe_records, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                      digests, stride, n, dict, hits);
 }
