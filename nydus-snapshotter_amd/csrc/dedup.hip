@@ -933,11 +933,9 @@ void launch_dict_build(const DictRec *rec, uint64_t m, uint64_t *table, uint64_t
 void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
                        const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s) {
   if (n == 0) return;
-  static const bool coop = [] {  // A/B knob (bench.py probe_roofline)
-    const char *v = getenv("NGPU_PROBE_COOP");
-    return v && v[0] == '1';
-  }();
-  if (coop) {
+  // A/B knob, read per call (bench.py probe_roofline; 2.6x slower)
+  const char *coop = getenv("NGPU_PROBE_COOP");
+  if (coop && coop[0] == '1') {
     hipLaunchKernelGGL(dict_probe_coop, dim3((unsigned)((n * 16 + 255) / 256)), dim3(256), 0, s,
                        digests, stride, n, dict, hits);
     return;
