@@ -680,9 +680,16 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
     {
       std::lock_guard<std::mutex> g(e->mu);
       hipStream_t ps = p->stream;
-      rc = dispatch(p, p->slot[p->cur], p->dispatched, n);
+      // a layer that fit one staging slot goes out in this one dispatch, so
+      // the slot's device chunk table already lists every chunk: the dedup
+      // reads only lengths from it (the offsets are slot-relative), and the
+      // second copy of the table is skipped
+      Slot &cs = p->slot[p->cur];
+      const bool one_slot = p->dispatched == 0 && n > 0;
+      rc = dispatch(p, cs, p->dispatched, n);
+      const ngpu_chunk *d_dedup = one_slot ? cs.d_ch : p->d_all;
       if (!rc) rc = grow_results(p, n + 1);
-      if (!rc && p->all_cap < n + 1) {  // kept between packs (engine pack_pool)
+      if (!rc && !one_slot && p->all_cap < n + 1) {  // kept between packs (engine pack_pool)
         if (p->d_all) (void)hipFree(p->d_all), p->d_all = nullptr, p->all_cap = 0;
         uint64_t c = 4096;
         while (c < n + 1) c *= 2;
@@ -707,15 +714,16 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
         else
           p->io_cap = c;
       }
-      if (!rc && n) {
-        memcpy(ch, p->chunks.data(), n * sizeof(ngpu_chunk));
+      if (!rc && n) memcpy(ch, p->chunks.data(), n * sizeof(ngpu_chunk));
+      if (!rc && n && !one_slot) {
         memcpy(p->h_io, ch, n * sizeof(ngpu_chunk));
         if (hipMemcpyAsync(p->d_all, p->h_io, n * sizeof(ngpu_chunk), hipMemcpyHostToDevice,
                            ps) != hipSuccess)
           rc = fail(e, NGPU_EHIP, "pack: chunk table copy failed");
+        d_dedup = p->d_all;
       }
       if (!rc)
-        rc = enqueue_dedup(e, p->dict, p->d_all, n, p->d_res, nullptr, 0, ps, nullptr, 1, nullptr);
+        rc = enqueue_dedup(e, p->dict, d_dedup, n, p->d_res, nullptr, 0, ps, nullptr, 1, nullptr);
       if (!rc) rc = host_fence(e, ps, p->fence);
       // (stream order: the results overwrite h_io after the chunk table left it)
       if (!rc && n &&
