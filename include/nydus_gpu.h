@@ -127,7 +127,11 @@ typedef struct {
   uint32_t reserved;
 } ngpu_timing;
 
-/* One chunk of layer file data. 24 bytes. */
+/* One chunk of layer file data. 24 bytes.  Chunks lie
+ * inside the data buffer and do not overlap (a tar's file extents never do):
+ * a descriptor past the buffer, or overlaps adding up to more BLAKE3 leaves
+ * than the buffer holds, fail the call with NGPU_EINVAL once its stats are
+ * read. */
 typedef struct {
   uint64_t offset;      /* byte offset of the chunk in the data buffer */
   uint32_t length;      /* 1 .. chunk_size bytes */

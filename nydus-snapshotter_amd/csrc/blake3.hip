@@ -598,6 +598,10 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
   const uint64_t gm = gbase[n];
   const uint64_t total = gm + *nsmall;
   const uint64_t g0 = blockIdx.x * 256ull;
+  // err[1] (stats[8]): more groups than the launch covers (overlapping
+  // descriptors); the call fails instead of leaving groups unhashed
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (total > gridDim.x * 256ull || total > cap_g))
+    err[1] = total;
   uint32_t slot = threadIdx.x;  // the group of this workgroup window this lane hashes
 #if B3_BALANCE
   // Lane balance inside the window: a wave runs as long as its longest lane,
@@ -901,6 +905,9 @@ __global__ __launch_bounds__(kQuadThreads) void b3_quad_leaves(
   const uint32_t q = threadIdx.x & 3, quad = threadIdx.x >> 2;
   const uint64_t gm = gbase[n], total = gm + *nsmall;
   const uint64_t g = blockIdx.x * (uint64_t)(kQuadThreads / 4) + quad;
+  if (blockIdx.x == 0 && threadIdx.x == 0 &&
+      (total > gridDim.x * (uint64_t)(kQuadThreads / 4) || total > cap_g))
+    err[1] = total;  // stats[8]: overlapping descriptors (b3_groups)
   if (g >= total || g >= cap_g) return;  // per quad: its four lanes leave together
   uint32_t c, j;
   bool root_group;
@@ -999,7 +1006,12 @@ __global__ __launch_bounds__(kQuadThreads) void b3_quad_planned(
     gpre[n] = ts;
     if (writer) groups[n] = ts;
   }
-  if (writer && t < 16) stats[t] = t == 7 ? tb : t == 9 ? tm : 0;
+  // stats[8]: more leaves than the launch covers -- descriptors that overlap
+  // (a tar's file extents never do); the call then fails instead of leaving
+  // leaves unhashed
+  const uint64_t span = (uint64_t)gridDim.x * (kQuadThreads / 4);
+  if (writer && t < 16)
+    stats[t] = t == 7 ? tb : t == 9 ? tm : t == 8 ? (ts > span || ts > cap_g ? ts : 0) : 0;
   __syncthreads();
   const uint32_t q = t & 3, quad = t >> 2;
   const uint64_t g = blockIdx.x * (uint64_t)(kQuadThreads / 4) + quad;
@@ -1106,11 +1118,20 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
 
 }  // namespace
 
+// Groups this call can have: its own bound, not the workspace's capacity (a
+// workspace sized for a 64 MiB staging slot would otherwise launch ~6x the
+// workgroups a 10 MB layer needs -- and every b3_quad_planned workgroup scans
+// all descriptors before it finds it has no leaf: 22 -> 67 us per C1 Pack).
+static uint64_t call_groups(uint64_t n, uint64_t data_len, int D, const Workspace &ws) {
+  const uint64_t g = blake3_max_groups(n, data_len, D);
+  return g < ws.cap_g ? g : ws.cap_g;
+}
+
 template <int D, int LM>
 static void launch_groups_lm(const uint8_t *data, uint64_t data_len,
                              const ngpu_chunk *chunks, uint64_t n, Workspace &ws,
                              ngpu_result *out, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  const uint64_t blocks = (ws.cap_g + 255) / 256;
+  const uint64_t blocks = (call_groups(n, data_len, D, ws) + 255) / 256;
   hipExtLaunchKernelGGL((b3_groups<D, LM>), dim3((unsigned)blocks), dim3(256), 0, s, e0, e1, 0,
                         data, data_len, chunks, n, (const uint64_t *)ws.groups,
                         (const uint32_t *)ws.group_chunk, ws.cap_g, ws.cv, out, ws.stats + 7,
@@ -1157,7 +1178,7 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
     // with the call's first kernel (ev_first; ev_start is left unrecorded,
     // ngpu_timing_at reads ev_first instead)
     (void)ev_start;
-    const uint64_t blocks = (ws.cap_g + kQuadThreads / 4 - 1) / (kQuadThreads / 4);
+    const uint64_t blocks = (call_groups(n, data_len, D, ws) + kQuadThreads / 4 - 1) / (kQuadThreads / 4);
     hipExtLaunchKernelGGL(b3_quad_planned, dim3((unsigned)blocks), dim3(kQuadThreads), 0, s,
                           ev_first, ev_end_groups, 0, data, data_len, chunks, n, ws.cap_g, ws.cv,
                           out, ws.groups, ws.stats, ws.tree_list);
@@ -1191,7 +1212,7 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
   if (blake3_planned_in_leaves(n, data_len, D, ws)) {
     // (leaves done above)
   } else if (quad) {
-    const uint64_t blocks = (ws.cap_g + kQuadThreads / 4 - 1) / (kQuadThreads / 4);
+    const uint64_t blocks = (call_groups(n, data_len, D, ws) + kQuadThreads / 4 - 1) / (kQuadThreads / 4);
     hipExtLaunchKernelGGL(b3_quad_leaves, dim3((unsigned)blocks), dim3(kQuadThreads), 0, s,
                           nullptr, ev_end_groups, 0, data, data_len, chunks, n,
                           (const uint64_t *)ws.groups, (const uint32_t *)ws.group_chunk, ws.cap_g,

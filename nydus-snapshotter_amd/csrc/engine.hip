@@ -401,6 +401,9 @@ int read_stats_parse(ngpu_engine *e, const uint64_t *h, ngpu_layer_stats *st) {
   if (h[7])
     return fail(e, NGPU_EINVAL, "%llu chunk descriptor(s) outside the data buffer",
                 (unsigned long long)h[7]);
+  if (h[8])
+    return fail(e, NGPU_EINVAL, "chunk descriptors overlap (%llu leaves, more than the buffer holds)",
+                (unsigned long long)h[8]);
   if (st) memcpy(st, h + 16, sizeof(ngpu_layer_stats));
   return 0;
 }

@@ -291,6 +291,26 @@ def test_bad_descriptor_device_path(engines):
         eng.process(bytes(4096), ch)
 
 
+@pytest.mark.parametrize("fl", [0, GRID])
+def test_overlapping_descriptors(engines, oracle, fl):
+    """Chunks that overlap (a tar's file extents never do) can hold more leaves
+    than the buffer bounds a launch by: the call fails (NGPU_EINVAL) instead
+    of leaving leaves unhashed.  A mild overlap inside the bound still hashes
+    every chunk exactly."""
+    S = 0x10000
+    data = np.random.default_rng(3).integers(0, 256, S, dtype=np.uint8).tobytes()
+    eng = engines("blake3", S, fl)
+    many = np.zeros(2000, nydus_gpu.CHUNK_DTYPE)
+    many["length"] = S  # 2000 x the whole buffer: 128,000 leaves
+    with pytest.raises(nydus_gpu.NgpuError, match="overlap"):
+        eng.process(data, many)
+    mild = np.zeros(40, nydus_gpu.CHUNK_DTYPE)
+    mild["offset"] = np.arange(40, dtype=np.uint64) * 1024
+    mild["length"] = 2048  # each chunk shares 1 KiB with the next
+    out, _ = eng.process(data, mild)
+    assert np.array_equal(out["digest"], oracle.digest_chunks(data, mild.view(oracle.CHUNK_DTYPE), "blake3"))
+
+
 def test_empty_layer(engines):
     out, st = engines().process(b"", np.zeros(0, nydus_gpu.CHUNK_DTYPE))
     assert len(out) == 0 and st["chunks"] == 0 and st["own_blob_index"] == 0xFFFFFFFF
