@@ -1040,12 +1040,15 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
   const uint64_t nt = (n + kScanTile - 1) / kScanTile;
   uint64_t *ts = ws.tstat + kDedupTs(ws.tiles);
   const uint64_t nbf = (uint64_t)nbo * L, nst = L * (sizeof(ngpu_layer_stats) / 8);
-  // the small path scans in LDS (no tile words to reset) and uses the first
-  // 2n (pow2) slots of the intra table: its init pass zeroes only those
+  // the intra table of this call: its first next_pow2(2(n + 1)) slots (the
+  // load the workspace is sized for, <= 0.5), not the
+  // workspace's whole table (sized by the largest call the slot has served:
+  // after a 16M-chunk layer, zeroing all of it cost a small layer ~0.1 ms).
+  // The small path scans in LDS (no tile words to reset).
   uint64_t icap = n ? ws.intra_cap : 0;
-  if (small && n) {
+  if (n) {
     uint64_t c = 64;
-    while (c < 2 * n) c <<= 1;
+    while (c < 2 * (n + 1)) c <<= 1;
     icap = c < icap ? c : icap;
   }
   const uint64_t ntw = small ? 0 : 1 + kDedupScans * ws.tiles;
@@ -1070,9 +1073,9 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
   if (n) {
     const unsigned blocks = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(dedup_probe_insert, dim3(blocks), dim3(256), 0, s, chunks, n, dict, hits,
-                       ws.chunk_layer, out, ws.blob_first, n_blobs, ws.intra, ws.intra_cap - 1);
+                       ws.chunk_layer, out, ws.blob_first, n_blobs, ws.intra, icap - 1);
     hipLaunchKernelGGL(dedup_resolve, dim3(blocks), dim3(256), 0, s, chunks, n, ws.chunk_layer,
-                       ws.intra, ws.intra_cap - 1, out, align, ws.newflag, ws.uoff, ws.nbytes,
+                       ws.intra, icap - 1, out, align, ws.newflag, ws.uoff, ws.nbytes,
                        ws.ndict);
     hipLaunchKernelGGL(dedup_scan, dim3((unsigned)nt), dim3(kTileThreads), 0, s, n, ws.newflag,
                        ws.uoff, ws.nbytes, ws.ndict, ts, ws.tiles);
