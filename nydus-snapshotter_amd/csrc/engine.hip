@@ -362,6 +362,7 @@ void engine_unref(ngpu_engine *e) {
   }
   for (hipStream_t x : e->streams)  // every pack compute stream (+ the engine's)
     if (x != e->stream) (void)hipStreamDestroy(x);
+  if (e->h_results) (void)hipHostFree(e->h_results);
   if (e->host_ev) (void)hipEventDestroy(e->host_ev);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -613,6 +614,18 @@ int ngpu_process_dict_device(ngpu_engine *e, ngpu_dict *dict, const void *d_data
                         stream, stats);
 }
 
+// Results of a host-buffer call come back through pinned memory: a D2H
+// hipMemcpyAsync into pageable memory takes the runtime's staging path.
+static int pinned_results(ngpu_engine *e, uint64_t n) {
+  if (n <= e->h_results_cap) return 0;
+  uint64_t c = 4096;
+  while (c < n) c *= 2;
+  if (e->h_results) (void)hipHostFree(e->h_results), e->h_results = nullptr, e->h_results_cap = 0;
+  HIP_TRY(e, hipHostMalloc((void **)&e->h_results, c * sizeof(ngpu_result), hipHostMallocDefault));
+  e->h_results_cap = c;
+  return 0;
+}
+
 static int process_host(ngpu_engine *e, ngpu_dict *dict, const void *data, uint64_t len,
                         const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
                         ngpu_layer_stats *stats) {
@@ -643,12 +656,16 @@ static int process_host(ngpu_engine *e, ngpu_dict *dict, const void *data, uint6
   if (len) HIP_TRY(e, hipMemcpyAsync(e->d_data, data, len, hipMemcpyHostToDevice, s));
   if (n) HIP_TRY(e, hipMemcpyAsync(e->d_chunks, chunks, n * sizeof(ngpu_chunk),
                                    hipMemcpyHostToDevice, s));
-  int rc = enqueue(e, dict, e->d_data, len, e->d_chunks, n, e->d_results, s);
+  int rc = pinned_results(e, n);
+  if (rc) return rc;
+  rc = enqueue(e, dict, e->d_data, len, e->d_chunks, n, e->d_results, s);
   if (rc) return rc;
   if ((rc = host_fence(e, s))) return rc;
-  if (n) HIP_TRY(e, hipMemcpyAsync(out, e->d_results, n * sizeof(ngpu_result),
+  if (n) HIP_TRY(e, hipMemcpyAsync(e->h_results, e->d_results, n * sizeof(ngpu_result),
                                    hipMemcpyDeviceToHost, s));
-  return read_stats(e, s, stats, true);
+  if ((rc = read_stats(e, s, stats, true))) return rc;  // synchronises s
+  if (n) memcpy(out, e->h_results, n * sizeof(ngpu_result));
+  return 0;
 }
 
 int ngpu_process(ngpu_engine *e, const void *data, uint64_t len, const ngpu_chunk *chunks,
@@ -720,12 +737,14 @@ int ngpu_pack_tar(ngpu_engine *e, const void *tar, uint64_t len, ngpu_chunk **ch
     if (n && hipMemcpyAsync(e->d_chunks, ch, n * sizeof(ngpu_chunk), hipMemcpyHostToDevice, s) !=
                  hipSuccess)
       return bail(fail(e, NGPU_EHIP, "chunk table H2D failed"));
+    if ((rc = pinned_results(e, n))) return bail(rc);
     if ((rc = enqueue(e, dict, e->d_data, len, e->d_chunks, n, e->d_results, s))) return bail(rc);
     if ((rc = host_fence(e, s))) return bail(rc);
-    if (n && hipMemcpyAsync(res, e->d_results, n * sizeof(ngpu_result), hipMemcpyDeviceToHost, s) !=
-                 hipSuccess)
+    if (n && hipMemcpyAsync(e->h_results, e->d_results, n * sizeof(ngpu_result),
+                            hipMemcpyDeviceToHost, s) != hipSuccess)
       return bail(fail(e, NGPU_EHIP, "results D2H failed"));
-    if ((rc = read_stats(e, s, stats, true))) return bail(rc);
+    if ((rc = read_stats(e, s, stats, true))) return bail(rc);  // synchronises s
+    if (n) memcpy(res, e->h_results, n * sizeof(ngpu_result));
     *chunks_out = ch;
     *results_out = res;
     *n_out = n;

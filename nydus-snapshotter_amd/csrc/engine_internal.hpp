@@ -108,6 +108,10 @@ struct ngpu_engine {
   ngpu_chunk *d_chunks = nullptr;
   ngpu_result *d_results = nullptr;
   uint64_t d_chunk_cap = 0;
+  // pinned landing buffer of the host-buffer calls' result tables (copied to
+  // the caller's pageable memory after the stream sync, as packs do with h_io)
+  ngpu_result *h_results = nullptr;
+  uint64_t h_results_cap = 0;
   // NGPU_FLAG_TIMING: a ring of per-call event sets (0 start, 1 digest start,
   // 2 digest end, 3 tree end, 4 end), so timing a call never makes the next
   // one wait: ngpu_timing_at reads any of the last kTimingRing calls.
