@@ -772,16 +772,22 @@ def node_bench(args):
                 e = node.engines[i]
                 e.set_dict(d)
                 with torch.cuda.device(p["dev"]):
-                    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-                    for r in range(25):
-                        if r == 5:
-                            ev[0].record(p["stream"])
-                        e.dedup_layers_device(p["d_ch"].data_ptr(), p["n"], p["out"].data_ptr(),
-                                              p["first"].data_ptr(), L, p["st"].data_ptr(),
-                                              stream=p["stream"].cuda_stream)
-                    ev[1].record(p["stream"])
+                    # every rerun starts from digest-stage records (kind =
+                    # NGPU_DIGESTED: the dedup stage takes only those), so the
+                    # mark is restored before each timed dedup, outside its events
+                    kind = p["out"].view(torch.int32).view(p["n"], 16)[:, 8]
+                    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(25)]
+                    with torch.cuda.stream(p["stream"]):
+                        for r in range(25):
+                            kind.fill_(nydus_gpu.DIGESTED)
+                            ev[r][0].record(p["stream"])
+                            e.dedup_layers_device(p["d_ch"].data_ptr(), p["n"], p["out"].data_ptr(),
+                                                  p["first"].data_ptr(), L, p["st"].data_ptr(),
+                                                  stream=p["stream"].cuda_stream)
+                            ev[r][1].record(p["stream"])
                     p["stream"].synchronize()
-                    alone.append(ev[0].elapsed_time(ev[1]) / 20)
+                    e.device_status()
+                    alone.append(float(np.mean([a.elapsed_time(b) for a, b in ev[5:]])))
                 e.set_dict(None)
             modes[name] = {"dict_build_s": round(build_s, 2), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
                            "value_gbs": round(total / elapsed / 1e9, 1),
@@ -1166,17 +1172,22 @@ def main():
                 if k in e2e}
     dog = None
     printed = [False]
+    print_mu = __import__("threading").Lock()  # the line is printed once: here or by the watchdog
     if dist and sdict is None and n_layers == 1 and not args.no_sharded_extra:
         # the headline is already measured; a watchdog keeps a stuck collective
         # (here, or in the closing barrier after a rank failed in here) from
         # costing the line: on expiry rank 0 prints it if it has not yet, and
-        # every rank exits
+        # every rank exits NON-ZERO, so a driver can tell a hang from a clean run
         import threading
 
         def stuck():
-            if rank == 0 and not printed[0]:
+            with print_mu:
+                first = rank == 0 and not printed[0]
+                printed[0] = True
+            if first:
                 print(json.dumps(dict(line, sharded_dict={"error": "timeout"})), flush=True)
-            os._exit(0)
+            sys.stdout.flush()
+            os._exit(3)
         dog = threading.Timer(120.0, stuck)
         dog.daemon = True
         dog.start()
@@ -1188,8 +1199,11 @@ def main():
         except Exception as ex:  # reported, never fatal to the headline line
             line["sharded_dict"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
     if rank == 0:
-        print(json.dumps(line), flush=True)
-        printed[0] = True
+        with print_mu:
+            first = not printed[0]
+            printed[0] = True
+        if first:
+            print(json.dumps(line), flush=True)
     eng.close()
     if dist:
         dist.barrier()

@@ -44,16 +44,26 @@
 extern "C" {
 #endif
 
-#define NGPU_ABI_VERSION 2
+#define NGPU_ABI_VERSION 3
 
 /* PackOption.Digester (API extension; maps to nydus-image --digester). */
 enum ngpu_digester { NGPU_DIGEST_BLAKE3 = 0, NGPU_DIGEST_SHA256 = 1 };
 
-/* Per-chunk dedup outcome ([nydus v2.3.0] Node::deduplicate_chunk). */
+/* Per-chunk dedup outcome ([nydus v2.3.0] Node::deduplicate_chunk), and the
+ * two states a record has around it. */
 enum ngpu_kind {
   NGPU_NEW = 0,   /* first occurrence: new data in this layer's blob */
   NGPU_INTRA = 1, /* duplicate of an earlier NEW chunk of this layer */
-  NGPU_DICT = 2   /* found in the chunk dict (PackOption.ChunkDictPath) */
+  NGPU_DICT = 2,  /* found in the chunk dict (PackOption.ChunkDictPath) */
+  /* Written by the digest stage next to each digest (ngpu_digest_device).  The
+   * dedup stage takes only records marked so: a caller that supplies its own
+   * digests to ngpu_dedup_* sets kind = NGPU_DIGESTED. */
+  NGPU_DIGESTED = 3,
+  /* Set by the dedup stage on a record that reached it without a digest (kind
+   * not NGPU_DIGESTED, or an all-zero digest): the record takes no part in
+   * dedup, and the call fails with NGPU_EDEVICE when its stats are read
+   * (ngpu_device_status for calls that read none). */
+  NGPU_UNHASHED = 4
 };
 
 enum ngpu_error {
@@ -68,9 +78,11 @@ enum ngpu_error {
   NGPU_EFORMAT = -8,   /* not a RAFS v6 bootstrap / bad chunk table */
   NGPU_ENOTFOUND = -9, /* entry not found in a nydus blob (ErrNotFound,
                           pkg/converter/types.go:33-35) */
-  NGPU_ECANCELED = -10 /* cancelled through the pack's cancel flag (the
+  NGPU_ECANCELED = -10, /* cancelled through the pack's cancel flag (the
                           reference's ctx.Done() / PackOption.Timeout kill of
                           the builder, builder.go:153-174) */
+  NGPU_EDEVICE = -11   /* a device-side check failed: a chunk reached the
+                          dedup stage without its digest (NGPU_UNHASHED) */
 };
 
 typedef struct ngpu_engine ngpu_engine;
@@ -105,8 +117,11 @@ typedef struct {
  * compression on a quad of lanes; this flag keeps the multi-kernel grid path
  * and one lane per leaf (same results). */
 #define NGPU_FLAG_GRID_STAGES 0x4u
-/* Tuning (benchmarks only): bits 8..10 = 1 + BLAKE3 load mode
- * (bit0 non-temporal loads, bit1 next-block prefetch); 0 = library default. */
+/* Tuning (benchmarks only): bits 8..10 = 1 + BLAKE3 load mode (0 plain loads
+ * with the whole-leaf fast path, 1 non-temporal loads, 2 next-block prefetch,
+ * 3 both, 5 plain loads without the fast path); 0 = library default.  Every
+ * mode computes the same digests; other values (5, 7) are rejected with
+ * NGPU_EINVAL. */
 #define NGPU_FLAG_LOAD_MODE_SHIFT 8
 /* Tuning (benchmarks only): bits 11..13 = 1 + SHA-256 kernel (0: one lane per
  * chunk with schedule/round waves, 1: two lanes per chunk, 2: one lane per
@@ -114,6 +129,14 @@ typedef struct {
  * workgroup, 5: two lanes, four groups per workgroup); 0 = library default
  * (by chunk count); other values are rejected (NGPU_EINVAL). */
 #define NGPU_FLAG_SHA_MODE_SHIFT 11
+
+/* Errors of device-pointer calls that read no stats (stats == NULL,
+ * ngpu_digest_device, the *_layers_device calls): synchronises every stream
+ * the engine's workspaces were last used on, returns the first error any
+ * stage recorded since the previous ngpu_device_status (NGPU_EINVAL for bad or
+ * overlapping descriptors, NGPU_EDEVICE for unhashed chunks; message in
+ * ngpu_last_error) and clears them.  0: no stage recorded an error. */
+int ngpu_device_status(ngpu_engine *eng);
 
 /* Per-stage device time of the last process call (NGPU_FLAG_TIMING). */
 typedef struct {

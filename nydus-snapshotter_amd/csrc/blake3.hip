@@ -419,8 +419,11 @@ __global__ __launch_bounds__(kSmallPlanThreads) void b3_plan_small(
 
 // LM (load mode): bit0 = non-temporal loads, bit1 = prefetch the next 64-B
 // block of the lane's byte stream while the current one is compressed,
-// 4 = diagnostic: no global loads at all (wrong digests; VALU ceiling only),
 // 5 = plain loads without the whole-leaf fast path (A/B reference).
+// 4 = diagnostic: no global loads at all (wrong digests; VALU ceiling only).
+// It exists only in a diagnostic build (-DNGPU_DIAG_NOLOAD=1, never the
+// library the ABI ships): no ngpu_config value reaches it (ngpu_create
+// rejects the load-mode values that would).
 //
 // Hashes leaf group j of chunk c (ng groups).  Returns 0 (no work), 1 (cur =
 // root digest: the chunk fits this group) or 2 (cur = the group's subtree CV).
@@ -433,7 +436,7 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
   const ngpu_chunk ch = chunks[c];
   const uint32_t len = ch.length;
   if (ch.offset > data_len || len > data_len - ch.offset) {  // bad descriptor
-    if (j == 0) atomicAdd((unsigned long long *)err, 1ull);
+    if (j == 0) note_bad_desc(err, 1);
     return 0;
   }
   const uint32_t nleaves = len == 0 ? 1 : (len + kLeaf - 1) / kLeaf;
@@ -601,7 +604,7 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
   // err[1] (stats[8]): more groups than the launch covers (overlapping
   // descriptors); the call fails instead of leaving groups unhashed
   if (blockIdx.x == 0 && threadIdx.x == 0 && (total > gridDim.x * 256ull || total > cap_g))
-    err[1] = total;
+    note_overlap(err, total);
   uint32_t slot = threadIdx.x;  // the group of this workgroup window this lane hashes
 #if B3_BALANCE
   // Lane balance inside the window: a wave runs as long as its longest lane,
@@ -671,6 +674,7 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
     uint4 *d = reinterpret_cast<uint4 *>(out[c].digest);
     d[0] = make_uint4(cur[0], cur[1], cur[2], cur[3]);
     d[1] = make_uint4(cur[4], cur[5], cur[6], cur[7]);
+    out[c].kind = NGPU_DIGESTED;  // the dedup stage takes only marked records
   }
   // Chunks whose groups all sit in this workgroup finish here: the upper
   // levels of their tree are reduced in LDS (pairwise, odd tail promoted).
@@ -719,6 +723,7 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
       uint4 *d = reinterpret_cast<uint4 *>(out[c].digest);
       d[0] = make_uint4(r[0], r[1], r[2], r[3]);
       d[1] = make_uint4(r[4], r[5], r[6], r[7]);
+      out[c].kind = NGPU_DIGESTED;
     }
     k = active ? p + (k & 1) : 1;
   }
@@ -886,6 +891,7 @@ __device__ __forceinline__ void quad_leaf(const uint8_t *__restrict__ data, cons
     uint32_t *d = reinterpret_cast<uint32_t *>(out[c].digest);
     d[q] = x;
     d[4 + q] = y;
+    if (q == 0) out[c].kind = NGPU_DIGESTED;
   } else {
     cv_out[g * 8 + q] = x;
     cv_out[g * 8 + 4 + q] = y;
@@ -907,7 +913,7 @@ __global__ __launch_bounds__(kQuadThreads) void b3_quad_leaves(
   const uint64_t g = blockIdx.x * (uint64_t)(kQuadThreads / 4) + quad;
   if (blockIdx.x == 0 && threadIdx.x == 0 &&
       (total > gridDim.x * (uint64_t)(kQuadThreads / 4) || total > cap_g))
-    err[1] = total;  // stats[8]: overlapping descriptors (b3_groups)
+    note_overlap(err, total);  // stats[8]: overlapping descriptors (b3_groups)
   if (g >= total || g >= cap_g) return;  // per quad: its four lanes leave together
   uint32_t c, j;
   bool root_group;
@@ -922,7 +928,7 @@ __global__ __launch_bounds__(kQuadThreads) void b3_quad_leaves(
   }
   const ngpu_chunk ch = chunks[c];
   if (ch.offset > data_len || ch.length > data_len - ch.offset) {  // bad descriptor
-    if (j == 0 && q == 0) atomicAdd((unsigned long long *)err, 1ull);
+    if (j == 0 && q == 0) note_bad_desc(err, 1);
     return;
   }
   quad_leaf(data, ch, c, j, root_group, g, q, qmsg + quad * 16, cv_out, out);
@@ -1010,8 +1016,13 @@ __global__ __launch_bounds__(kQuadThreads) void b3_quad_planned(
   // (a tar's file extents never do); the call then fails instead of leaving
   // leaves unhashed
   const uint64_t span = (uint64_t)gridDim.x * (kQuadThreads / 4);
+  const uint64_t over = ts > span || ts > cap_g ? ts : 0;
   if (writer && t < 16)
-    stats[t] = t == 7 ? tb : t == 9 ? tm : t == 8 ? (ts > span || ts > cap_g ? ts : 0) : 0;
+    stats[t] = t == kStBadDesc ? tb : t == kStTreeQueued ? tm : t == kStOverlap ? over : 0;
+  if (writer && t == 0 && tb)
+    atomicAdd((unsigned long long *)(stats + kStSticky), (unsigned long long)tb);
+  if (writer && t == 0 && over)
+    atomicMax((unsigned long long *)(stats + kStSticky + 1), (unsigned long long)over);
   __syncthreads();
   const uint32_t q = t & 3, quad = t >> 2;
   const uint64_t g = blockIdx.x * (uint64_t)(kQuadThreads / 4) + quad;
@@ -1106,6 +1117,8 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
             reinterpret_cast<uint32_t *>(out[c].digest)[tid] = tt[cur][tid];
           else
             a[tile * 8 + tid] = tt[cur][tid];
+        } else if (tid == 8 && final_pass) {
+          out[c].kind = NGPU_DIGESTED;  // (tt is read-only here: same wave as the digest)
         }
         __syncthreads();
       }
@@ -1139,18 +1152,30 @@ static void launch_groups_lm(const uint8_t *data, uint64_t data_len,
                         ws.tree_list);
 }
 
+#ifndef NGPU_DIAG_NOLOAD
+#define NGPU_DIAG_NOLOAD 0
+#endif
+
+// false: a load mode this build has no kernel for (nothing launched).
 template <int D>
-static void launch_groups(const uint8_t *data, uint64_t data_len,
+static bool launch_groups(const uint8_t *data, uint64_t data_len,
                           const ngpu_chunk *chunks, uint64_t n, Workspace &ws,
                           ngpu_result *out, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   switch (ws.load_mode) {
-    case 0: launch_groups_lm<D, 0>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
-    case 1: launch_groups_lm<D, 1>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
-    case 2: launch_groups_lm<D, 2>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
-    case 3: launch_groups_lm<D, 3>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
-    case 5: launch_groups_lm<D, 5>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
-    default: launch_groups_lm<D, 4>(data, data_len, chunks, n, ws, out, s, e0, e1); break;
+    case 0: launch_groups_lm<D, 0>(data, data_len, chunks, n, ws, out, s, e0, e1); return true;
+    case 1: launch_groups_lm<D, 1>(data, data_len, chunks, n, ws, out, s, e0, e1); return true;
+    case 2: launch_groups_lm<D, 2>(data, data_len, chunks, n, ws, out, s, e0, e1); return true;
+    case 3: launch_groups_lm<D, 3>(data, data_len, chunks, n, ws, out, s, e0, e1); return true;
+    case 5: launch_groups_lm<D, 5>(data, data_len, chunks, n, ws, out, s, e0, e1); return true;
+#if NGPU_DIAG_NOLOAD
+    case 4: launch_groups_lm<D, 4>(data, data_len, chunks, n, ws, out, s, e0, e1); return true;
+#endif
+    default: return false;
   }
+}
+
+bool blake3_load_mode_ok(int lm) {
+  return lm == 0 || lm == 1 || lm == 2 || lm == 3 || lm == 5 || (NGPU_DIAG_NOLOAD && lm == 4);
 }
 
 bool blake3_planned_in_leaves(uint64_t n, uint64_t data_len, int D, const Workspace &ws) {
@@ -1218,12 +1243,16 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
                           (const uint64_t *)ws.groups, (const uint32_t *)ws.group_chunk, ws.cap_g,
                           ws.cv, out, ws.stats + 7, (const uint32_t *)ws.small,
                           (const uint64_t *)(ws.stats + 10), ws.tree_list);
-  } else switch (D) {
-    case 0: launch_groups<0>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
-    case 1: launch_groups<1>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
-    case 2: launch_groups<2>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
-    case 3: launch_groups<3>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
-    default: launch_groups<4>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
+  } else {
+    bool ok;
+    switch (D) {
+      case 0: ok = launch_groups<0>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
+      case 1: ok = launch_groups<1>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
+      case 2: ok = launch_groups<2>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
+      case 3: ok = launch_groups<3>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
+      default: ok = launch_groups<4>(data, data_len, chunks, n, ws, out, s, nullptr, ev_end_groups); break;
+    }
+    if (!ok) return false;  // (ngpu_create validates the mode; never taken)
   }
   const uint64_t blocks = n < 2048 ? n : 2048;
   hipExtLaunchKernelGGL(b3_tree, dim3((unsigned)blocks), dim3(kTreeThreads), 0, s, nullptr, ev_end,

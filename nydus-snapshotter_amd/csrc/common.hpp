@@ -12,6 +12,31 @@ constexpr uint32_t kLeaf = 1024;        // BLAKE3 chunk ("leaf" here) bytes
 constexpr uint64_t kEmpty = ~0ull;      // empty hash-table slot
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
+// Workspace::stats words (u64).  The digest stage resets [0, 16) per call;
+// the dedup stage resets its own [kStUnhashed, kStUnhashedFirst].  The sticky
+// words [16, 20) are never reset by a stage: every error branch adds to them
+// too, so a device-pointer call that nobody reads stats for still leaves its
+// error for ngpu_device_status (and the next host read of the slot).
+constexpr int kStBadDesc = 7;          // descriptors outside the data buffer
+constexpr int kStOverlap = 8;          // leaves past the launch (overlapping descriptors)
+constexpr int kStTreeQueued = 9;       // chunks queued for b3_tree
+constexpr int kStSmall = 10;           // single-group chunks (b3 planning)
+constexpr int kStUnhashed = 11;        // chunks that reached dedup without a digest
+constexpr int kStUnhashedFirst = 12;   // ~(smallest such chunk id) (atomic max), 0 = none
+constexpr int kStSticky = 16;          // + {0 bad desc, 1 overlap, 2 unhashed, 3 ~first unhashed}
+constexpr int kStWords = 20;           // words read back per stats read
+
+// Error branch of a kernel: bump the per-call word k and its sticky twin.
+// `err` points at stats[kStBadDesc] (the kernels' err argument).
+__device__ __forceinline__ void note_bad_desc(uint64_t *err, uint64_t v) {
+  atomicAdd((unsigned long long *)err, (unsigned long long)v);
+  atomicAdd((unsigned long long *)(err + (kStSticky - kStBadDesc)), (unsigned long long)v);
+}
+__device__ __forceinline__ void note_overlap(uint64_t *err, uint64_t total) {
+  err[kStOverlap - kStBadDesc] = total;
+  atomicMax((unsigned long long *)(err + (kStSticky + 1 - kStBadDesc)), (unsigned long long)total);
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Sets the calling thread's HIP device for a scope and restores it after, so
@@ -174,6 +199,8 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
                    ngpu_result *out, hipStream_t s, hipEvent_t ev_first,
                    hipEvent_t ev_groups_start, hipEvent_t ev_groups_end, hipEvent_t ev_end);
 uint64_t blake3_max_groups(uint64_t n, uint64_t data_len, int group_log2);
+// ngpu_config load-mode override (flags bits 8..10 minus one) this build runs.
+bool blake3_load_mode_ok(int lm);
 // True when the call's chunk planning runs inside its leaf kernel
 // (b3_quad_planned: small layers on the quad path) -- there is no planning
 // kernel, so ev_groups_start is not recorded.
@@ -258,7 +285,7 @@ struct Workspace {
   uint64_t *lfirst1 = nullptr;       // {0, n} for single-layer calls
   ngpu_layer_stats *lstats = nullptr;// per-layer stats (internal, cap_layers)
   uint64_t cap_layers = 0;
-  uint64_t *stats = nullptr;      // device-side counters (ngpu_layer_stats)
+  uint64_t *stats = nullptr;      // device-side counters (kSt* words above)
   uint64_t cap_n = 0, cap_g = 0, cap_blobs = 0;
   // node dict exchange: packed digests (n x 32), per-part hits (W x n), hits (n)
   uint8_t *xq = nullptr;

@@ -213,6 +213,45 @@ __device__ __forceinline__ uint64_t layer_bucket(const uint32_t *d, uint32_t lay
   return digest_bucket(d) + (uint64_t)layer * 0xC2B2AE3D27D4EB4Full;
 }
 
+// The unwritten-digest guard.  The digest stage stores kind = NGPU_DIGESTED
+// next to every digest; a record that reaches dedup without the mark (a
+// previous call's record, fresh memory) or with an all-zero digest (no
+// BLAKE3 / SHA-256 output, p = 2^-256) was never written by this call's
+// digest kernels.  Such a chunk must not take part in dedup: two of them with
+// equal lengths would resolve INTRA to each other and one file's bytes would
+// silently point at another's.  It is marked NGPU_UNHASHED instead, counted in
+// unh[0] with ~(its id) max-ed into unh[1] (stats[kStUnhashed..]), and the
+// call fails (NGPU_EDEVICE) when its stats are read.
+__device__ __forceinline__ bool digest_unwritten(const ngpu_result &r, const uint32_t d[8]) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x |= d[i];
+  return r.kind != NGPU_DIGESTED || x == 0;
+}
+
+// unh: two counters, global (grid path) or LDS (one-workgroup paths).
+__device__ __forceinline__ void mark_unhashed(ngpu_result &r, uint64_t c, uint64_t *unh) {
+  r.kind = NGPU_UNHASHED;
+  r.ref = c;
+  r.index = kNone;
+  r.blob_index = kNone;
+  r.dict_blob = 0;
+  r.uncompressed_offset = 0;
+  atomicAdd((unsigned long long *)unh, 1ull);
+  atomicMax((unsigned long long *)(unh + 1), (unsigned long long)~c);
+}
+
+// One-workgroup stages: publish the LDS counters into the call's stats words
+// and their sticky twins (thread 0, after the last barrier).
+__device__ __forceinline__ void publish_unhashed(uint64_t *stats, uint64_t cnt, uint64_t inv_first) {
+  stats[kStUnhashed] = cnt;
+  stats[kStUnhashedFirst] = inv_first;
+  if (cnt) {
+    atomicAdd((unsigned long long *)(stats + kStSticky + 2), (unsigned long long)cnt);
+    atomicMax((unsigned long long *)(stats + kStSticky + 3), (unsigned long long)inv_first);
+  }
+}
+
 // Stage 0 (one grid-stride launch instead of four memsets + a map kernel):
 // reset the per-layer blob first-hit slots, the layer stats, the intra table
 // and the scan tiles, and fill chunk -> layer (binary search in first[0..L]:
@@ -229,6 +268,7 @@ struct DedupInit {
   uint64_t *intra, icap, *tiles, ntw;
   uint64_t *newidx, *uoff, *nbytes, *ndict;
   uint64_t total;
+  uint64_t *stats;  // the call's stats words (the grid path's unhashed counters)
 };
 
 __device__ __forceinline__ void init_item(const DedupInit &a, uint64_t i) {
@@ -261,6 +301,7 @@ __device__ __forceinline__ void init_item(const DedupInit &a, uint64_t i) {
       nbytes[n] = 0;
       ndict[n] = 0;
       if (single) { single[0] = 0; single[1] = n; }
+      if (a.stats) a.stats[kStUnhashed] = a.stats[kStUnhashedFirst] = 0;
     }
   }
 }
@@ -300,17 +341,24 @@ __device__ __forceinline__ bool same_key(const ngpu_result *out, const uint32_t 
 // empty slot, or atomic MIN over the slot holding the same (layer, digest):
 // the first occurrence wins for any schedule).
 // Every lane of the wave must call this (wave_min_u32); c >= n: no chunk.
+// unh: the unhashed-chunk counters (digest_unwritten).
 __device__ __forceinline__ void probe_insert_item(
     uint64_t c, const ngpu_chunk *__restrict__ chunks, uint64_t n, const DictDevice &dict,
     const ngpu_dict_hit *__restrict__ hits, const uint32_t *__restrict__ chunk_layer,
     ngpu_result *__restrict__ out, uint32_t *__restrict__ blob_first, uint32_t n_blobs,
-    uint64_t *__restrict__ table, uint64_t mask) {
-  const bool live = c < n;
+    uint64_t *__restrict__ table, uint64_t mask, uint64_t *unh) {
+  bool live = c < n;
   uint32_t d[8] = {};
   uint32_t layer = 0;
   ngpu_dict_hit h{kNone, 0, 0, 0, 0};
   if (live) {
     load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
+    if (digest_unwritten(out[c], d)) {
+      mark_unhashed(out[c], c, unh);
+      live = false;
+    }
+  }
+  if (live) {
     layer = chunk_layer[c];
     if (hits) {
       h = hits[c];
@@ -357,9 +405,21 @@ __global__ void dedup_probe_insert(const ngpu_chunk *__restrict__ chunks, uint64
                                    const uint32_t *__restrict__ chunk_layer,
                                    ngpu_result *__restrict__ out,
                                    uint32_t *__restrict__ blob_first, uint32_t n_blobs,
-                                   uint64_t *__restrict__ table, uint64_t mask) {
+                                   uint64_t *__restrict__ table, uint64_t mask,
+                                   uint64_t *__restrict__ stats) {
+  __shared__ unsigned long long s_unh[2];  // the workgroup's unhashed chunks, then one atomic
+  if (threadIdx.x == 0) s_unh[0] = s_unh[1] = 0;
+  __syncthreads();
   probe_insert_item(blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, chunks, n, dict, hits,
-                    chunk_layer, out, blob_first, n_blobs, table, mask);
+                    chunk_layer, out, blob_first, n_blobs, table, mask,
+                    reinterpret_cast<uint64_t *>(s_unh));
+  __syncthreads();
+  if (threadIdx.x == 0 && s_unh[0]) {
+    atomicAdd((unsigned long long *)(stats + kStUnhashed), s_unh[0]);
+    atomicMax((unsigned long long *)(stats + kStUnhashedFirst), s_unh[1]);
+    atomicAdd((unsigned long long *)(stats + kStSticky + 2), s_unh[0]);
+    atomicMax((unsigned long long *)(stats + kStSticky + 3), s_unh[1]);
+  }
 }
 
 // Stage 2: INTRA / NEW per chunk.  Writes the four per-chunk quantities the
@@ -375,6 +435,8 @@ __device__ __forceinline__ void resolve_values(
   const uint32_t layer = chunk_layer[c];
   if (r.kind == NGPU_DICT) {
     v[3] = 1;
+  } else if (r.kind == NGPU_UNHASHED) {
+    // no digest: no decision, counted nowhere (the call fails)
   } else {
     uint32_t d[8];
     load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, d);
@@ -589,7 +651,7 @@ __device__ __forceinline__ void finalize_item(uint64_t c, const uint32_t *__rest
     r.index = (uint32_t)(newidx[f] - ib);
     r.uncompressed_offset = uoff[f] - ob;
     r.blob_index = own;
-  } else {
+  } else if (r.kind == NGPU_DICT) {
     r.blob_index = real[r.blob_index];
   }
 }
@@ -633,14 +695,16 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small(
     ngpu_result *__restrict__ out) {
   __shared__ uint32_t fl[1024], used_all;
   __shared__ uint64_t wsum[2][kDedupScans][kSmallThreads / 64];
+  __shared__ unsigned long long s_unh[2];
   const uint64_t n = a.n, mask = a.icap - 1;
   const uint32_t nbo = n_blobs + 1;
+  if (threadIdx.x == 0) s_unh[0] = s_unh[1] = 0;
   for (uint64_t i = threadIdx.x; i < a.total; i += kSmallThreads) init_item(a, i);
   small_phase_end();
   const uint64_t n_up = (n + kSmallThreads - 1) / kSmallThreads * kSmallThreads;
   for (uint64_t c = threadIdx.x; c < n_up; c += kSmallThreads)  // whole waves: wave_min_u32
     probe_insert_item(c, chunks, n, dict, hits, a.chunk_layer, out, a.blob_first, n_blobs, a.intra,
-                      mask);
+                      mask, reinterpret_cast<uint64_t *>(s_unh));
   small_phase_end();
   // Resolve into registers and scan the four arrays together, one row of
   // kSmallThreads chunks at a time (chunk r * kSmallThreads + thread): one
@@ -693,6 +757,7 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small(
   small_phase_end();
   for (uint64_t c = threadIdx.x; c < n; c += kSmallThreads)
     finalize_item(c, a.chunk_layer, lfirst, a.newidx, a.uoff, blob_real, nbo, out);
+  if (threadIdx.x == 0) publish_unhashed(a.stats, s_unh[0], s_unh[1]);
 }
 
 // ---- small single-layer calls: the whole stage in LDS --------------------------
@@ -716,7 +781,8 @@ static_assert(kLdsChunks == kSmallDedupChunks, "one LDS slot per chunk");
 __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
     const ngpu_chunk *__restrict__ chunks, uint64_t n, DictDevice dict,
     const ngpu_dict_hit *__restrict__ hits, uint32_t n_blobs, uint32_t align,
-    ngpu_layer_stats *__restrict__ st, ngpu_result *__restrict__ out) {
+    ngpu_layer_stats *__restrict__ st, ngpu_result *__restrict__ out,
+    uint64_t *__restrict__ stats) {
   __shared__ uint64_t table[kLdsSlots];
   __shared__ uint64_t off[kLdsChunks];   // exclusive prefix of aligned NEW sizes
   __shared__ uint32_t len_s[kLdsChunks];
@@ -724,25 +790,32 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
   __shared__ uint32_t bf[kLdsBlobs], real[kLdsBlobs];
   __shared__ uint64_t wsum[2][4][kSmallThreads / 64];
   __shared__ uint32_t used_all;
+  __shared__ unsigned long long s_unh[2];  // unhashed chunks: count, ~smallest id
   const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const uint32_t nbo = n_blobs + 1;
   uint32_t mask = 63;
   while (mask + 1 < 2 * n) mask = mask * 2 + 1;
   for (uint32_t i = t; i <= mask; i += kSmallThreads) table[i] = kEmpty;
   for (uint32_t i = t; i < nbo; i += kSmallThreads) bf[i] = kNone;
-  if (t == 0) used_all = 0;
+  if (t == 0) used_all = 0, s_unh[0] = s_unh[1] = 0;
   __syncthreads();
   // A: dict decisions (DICT results written now) and the intra-layer table.
   // Item k of thread t is chunk k * kSmallThreads + t (rows, for the scans).
   // Per chunk, for phase B: len_s = length | DICT flag (bit 31), off = the
   // digest's tag : bucket (overwritten by the chunk's offset prefix in B).
   constexpr uint32_t kDictBit = 0x80000000u;
+  constexpr uint32_t kUnhashedBit = 0x20000000u;  // no digest (digest_unwritten)
 #pragma unroll 1
   for (int k = 0; k < kLdsItems; ++k) {
     const uint64_t c = (uint64_t)k * kSmallThreads + t;
     if (c >= n) break;
     uint32_t dg[8];
     load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, dg);
+    if (digest_unwritten(out[c], dg)) {
+      len_s[c] = kUnhashedBit;
+      mark_unhashed(out[c], c, reinterpret_cast<uint64_t *>(s_unh));
+      continue;
+    }
     const uint32_t len = chunks[c].length;
     ngpu_dict_hit h{kNone, 0, 0, 0, 0};
     if (hits) h = hits[c];
@@ -797,6 +870,8 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
       const uint32_t lv = len_s[c];
       if (lv & kDictBit) {
         v[3] = 1;
+      } else if (lv & kUnhashedBit) {
+        // no digest: no decision (the call fails)
       } else {
         const uint64_t tb = off[c];
         const uint32_t tag = (uint32_t)(tb >> 32);
@@ -891,6 +966,8 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
     const uint32_t lv = len_s[c];
     if (lv & kDictBit) {
       r.blob_index = real[r.dict_blob];
+    } else if (lv & kUnhashedBit) {
+      // marked in phase A
     } else if (lv & kIntraBit) {
       const uint32_t f = lv & ~kIntraBit;
       r.kind = NGPU_INTRA;
@@ -917,6 +994,7 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
     x.blobs = used_all;
     x.uncompressed_size = carry[1];
     st[0] = x;
+    publish_unhashed(stats, s_unh[0], s_unh[1]);
   }
 }
 
@@ -1056,10 +1134,10 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
   for (uint64_t v : {nbf, nst, icap, ntw}) total = v > total ? v : total;
   const DedupInit a{lfirst, L, n, single, ws.chunk_layer, ws.blob_first, nbf,
                     reinterpret_cast<uint64_t *>(st), nst, ws.intra, icap, ts, ntw,
-                    ws.newflag, ws.uoff, ws.nbytes, ws.ndict, total};
+                    ws.newflag, ws.uoff, ws.nbytes, ws.ndict, total, ws.stats};
   if (small && single && nbo <= kLdsBlobs) {  // one layer: the whole stage in LDS
     hipExtLaunchKernelGGL(dedup_small_lds, dim3(1), dim3(kSmallThreads), 0, s, nullptr, ev_end, 0,
-                          chunks, n, dict, hits, n_blobs, align, st, out);
+                          chunks, n, dict, hits, n_blobs, align, st, out, ws.stats);
     return;
   }
   if (small) {
@@ -1073,7 +1151,7 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
   if (n) {
     const unsigned blocks = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(dedup_probe_insert, dim3(blocks), dim3(256), 0, s, chunks, n, dict, hits,
-                       ws.chunk_layer, out, ws.blob_first, n_blobs, ws.intra, icap - 1);
+                       ws.chunk_layer, out, ws.blob_first, n_blobs, ws.intra, icap - 1, ws.stats);
     hipLaunchKernelGGL(dedup_resolve, dim3(blocks), dim3(256), 0, s, chunks, n, ws.chunk_layer,
                        ws.intra, icap - 1, out, align, ws.newflag, ws.uoff, ws.nbytes,
                        ws.ndict);

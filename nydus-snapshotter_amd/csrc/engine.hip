@@ -221,6 +221,25 @@ int ws_release(ngpu_engine *e, hipStream_t s, hipEvent_t bound, bool chained) {
   return 0;
 }
 
+// Before timing-ring entry k is recorded again: a workspace slot whose last
+// stage ended on one of k's events must not keep that event as its fence (a
+// later wait on it would wait for the new record, not the slot's stage).  The
+// entry was recorded kTimingRing calls ago, so the host wait is for work long
+// done; the slot is then idle.
+static int ring_reclaim(ngpu_engine *e, int k) {
+  for (auto &sl : e->slots) {
+    if (!sl.pending || !sl.last_ev) continue;
+    for (hipEvent_t ev : e->ev[k])
+      if (sl.last_ev == ev) {
+        HIP_TRY(e, hipEventSynchronize(ev));
+        sl.pending = false;
+        sl.last_ev = nullptr;
+        break;
+      }
+  }
+  return 0;
+}
+
 // Digest stage: resets the layer stats, runs the digest kernels.
 int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
                    const ngpu_chunk *d_chunks, uint64_t n, ngpu_result *d_out,
@@ -232,12 +251,19 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
   if (rc) return rc;
   if ((rc = ws_acquire(e, s))) return rc;
   const bool tm = (e->cfg.flags & NGPU_FLAG_TIMING) != 0;
-  // tuning override: flags bits 8..10 = 1 + BLAKE3 load mode (0 = default)
-  const uint32_t lm = (e->cfg.flags >> 8) & 7;
+  // tuning override: flags bits 8..10 = 1 + BLAKE3 load mode (0 = default;
+  // validated by ngpu_create)
+  const uint32_t lm = (e->cfg.flags >> NGPU_FLAG_LOAD_MODE_SHIFT) & 7;
   ws.load_mode = lm ? (int)(lm - 1) : 0;
   hipEvent_t *ev = nullptr;
   if (tm) {
-    e->tslot = (int)(e->tcalls++ % ngpu_engine::kTimingRing);
+    const int k = (int)(e->tcalls % ngpu_engine::kTimingRing);
+    if ((rc = ring_reclaim(e, k))) return rc;
+    e->tslot = k;
+    ++e->tcalls;
+    e->tshare_slot = e->cur;
+    e->tshare_stream = s;
+    e->tshare_open = true;
     ev = e->ev[e->tslot];
     e->timed[e->tslot] = false;
     e->slot_D[e->tslot] = D;
@@ -252,7 +278,9 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
     // tuning override: flags bits 11..13 = 1 + SHA-256 variant (0 split,
     // 1 pair, 2 lane, 4/5 pair layouts)
     const uint32_t sv = (e->cfg.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7;
-    launch_sha256(d_data, len, d_chunks, n, d_out, ws.stats + 7, sv ? (int)sv - 1 : -1, s);
+    launch_sha256(d_data, len, d_chunks, n, d_out, ws.stats + kStBadDesc, sv ? (int)sv - 1 : -1, s);
+    snprintf(e->cur->path, sizeof e->cur->path, "sha256 variant %d, %llu chunks",
+             sv ? (int)sv - 1 : -1, (unsigned long long)n);
     if (tm) {
       HIP_TRY(e, hipEventRecord(ev[2], s));
       HIP_TRY(e, hipEventRecord(ev[3], s));
@@ -264,6 +292,11 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
     if (launch_blake3(d_data, d_chunks, n, len, D, ws, d_out, s, tm ? ev[0] : nullptr,
                       tm ? ev[1] : nullptr, tm ? ev[2] : nullptr, end))
       bound = end;
+    snprintf(e->cur->path, sizeof e->cur->path, "blake3 %s D=%d, %llu chunks",
+             blake3_planned_in_leaves(n, len, D, ws) ? "quad_planned"
+             : (D == 0 && !ws.grid_stages && len / kLeaf + n <= 32768) ? "quad_leaves"
+                                                                        : "groups",
+             D, (unsigned long long)n);
   }
   HIP_TRY(e, hipGetLastError());
   if ((rc = ws_release(e, s, bound, chained))) return rc;
@@ -294,13 +327,14 @@ int enqueue_dedup(ngpu_engine *e, const ngpu_dict *dict, const ngpu_chunk *d_chu
       (e->cfg.fs_version == 6 || (e->cfg.flags & NGPU_FLAG_ALIGNED_CHUNK)) ? 4096u : 1u;
   // d_lfirst == nullptr: the init kernel writes {0, n} into ws.lfirst1
   // the last dedup kernel records the stage end (timing slot or the slot's done event)
-  hipEvent_t end = tm && e->tcalls      ? e->ev[e->tslot][4]
+  const bool timed = tm && e->tshare_open && e->tshare_slot == e->cur && e->tshare_stream == s;
+  hipEvent_t end = timed                      ? e->ev[e->tslot][4]
                    : ws_lazy_end(e, s, false) ? nullptr
                                               : e->cur->done;
   launch_dedup(d_chunks, n, dict ? dict->dev : DictDevice{}, d_hits, n_blobs, align, d_lfirst, L,
                e->cur->ws, d_out, d_stats, s, end);
   HIP_TRY(e, hipGetLastError());
-  if (tm && e->tcalls) e->timed[e->tslot] = n > 0;
+  if (timed) e->timed[e->tslot] = n > 0, e->tshare_open = false;
   if ((rc = ws_release(e, s, end, false))) return rc;
   return 0;
 }
@@ -387,25 +421,42 @@ int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st, bool fenced)
   uint64_t *h = e->cur->h_stats;  // the slot the call's stages used (e->mu held)
   if (int rc = read_stats_enqueue(e, s, h)) return rc;
   HIP_TRY(e, hipStreamSynchronize(s));
-  return read_stats_parse(e, h, st);
+  return read_stats_parse(e, h, st, e->cur->path);
 }
 
 int read_stats_enqueue(ngpu_engine *e, hipStream_t s, uint64_t *h) {
   const ngpu_ws_slot &sl = *e->cur;
-  HIP_TRY(e, hipMemcpyAsync(h, sl.ws.stats, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  HIP_TRY(e, hipMemcpyAsync(h + 16, sl.ws.lstats, sizeof(ngpu_layer_stats), hipMemcpyDeviceToHost,
-                            s));
+  static_assert(kStWords <= kStatsLayer && kStatsLayer * 8 + sizeof(ngpu_layer_stats) <= 32 * 8,
+                "stats read-back layout fits the 32-word pinned buffers");
+  HIP_TRY(e, hipMemcpyAsync(h, sl.ws.stats, kStWords * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(e, hipMemcpyAsync(h + kStatsLayer, sl.ws.lstats, sizeof(ngpu_layer_stats),
+                            hipMemcpyDeviceToHost, s));
   return 0;
 }
 
-int read_stats_parse(ngpu_engine *e, const uint64_t *h, ngpu_layer_stats *st) {
-  if (h[7])
+// Errors recorded by a stage, in order of precedence (one message).
+static int stats_error(ngpu_engine *e, uint64_t bad, uint64_t over, uint64_t unh,
+                       uint64_t inv_first, const char *path) {
+  if (bad)
     return fail(e, NGPU_EINVAL, "%llu chunk descriptor(s) outside the data buffer",
-                (unsigned long long)h[7]);
-  if (h[8])
+                (unsigned long long)bad);
+  if (over)
     return fail(e, NGPU_EINVAL, "chunk descriptors overlap (%llu leaves, more than the buffer holds)",
-                (unsigned long long)h[8]);
-  if (st) memcpy(st, h + 16, sizeof(ngpu_layer_stats));
+                (unsigned long long)over);
+  if (unh)
+    return fail(e, NGPU_EDEVICE,
+                "%llu chunk(s) reached the dedup stage without a digest, first chunk %llu "
+                "(digest stage: %s); results marked NGPU_UNHASHED",
+                (unsigned long long)unh, (unsigned long long)~inv_first,
+                path && *path ? path : "caller-supplied digests");
+  return 0;
+}
+
+int read_stats_parse(ngpu_engine *e, const uint64_t *h, ngpu_layer_stats *st, const char *path) {
+  if (int rc = stats_error(e, h[kStBadDesc], h[kStOverlap], h[kStUnhashed], h[kStUnhashedFirst],
+                           path))
+    return rc;
+  if (st) memcpy(st, h + kStatsLayer, sizeof(ngpu_layer_stats));
   return 0;
 }
 
@@ -443,6 +494,10 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
     case 0: case 1: case 2: case 3: case 5: case 6: break;
     default: return NGPU_EINVAL;
   }
+  // BLAKE3 load-mode override: only modes this build has a kernel for, all of
+  // which compute the reference digests (the no-load diagnostic is not built)
+  if (const uint32_t lm = (c.flags >> NGPU_FLAG_LOAD_MODE_SHIFT) & 7)
+    if (!blake3_load_mode_ok((int)lm - 1)) return NGPU_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return NGPU_ENODEV;
   if (c.device < 0 || c.device >= ndev) return NGPU_ENODEV;
@@ -505,6 +560,31 @@ void ngpu_destroy(ngpu_engine *e) {
 }
 
 const char *ngpu_last_error(const ngpu_engine *e) { return e ? e->err.c_str() : "null engine"; }
+
+int ngpu_device_status(ngpu_engine *e) {
+  if (!e) return NGPU_EINVAL;
+  return guarded([&]() -> int {
+    std::lock_guard<std::mutex> g(e->mu);
+    DeviceGuard dg(e->device);
+    int first = 0;
+    for (auto &sl : e->slots) {
+      if (!sl.ws.stats) continue;
+      if (sl.pending) {  // wait for the slot's last stage (its stream may be a caller's)
+        if (!sl.last_ev) {  // lazy end: its stream lives as long as the engine
+          HIP_TRY(e, hipEventRecord(sl.done, sl.last));
+          sl.last_ev = sl.done;
+        }
+        HIP_TRY(e, hipEventSynchronize(sl.last_ev));
+      }
+      uint64_t w[4];
+      HIP_TRY(e, hipMemcpy(w, sl.ws.stats + kStSticky, sizeof w, hipMemcpyDeviceToHost));
+      if (!(w[0] | w[1] | w[2])) continue;
+      HIP_TRY(e, hipMemset(sl.ws.stats + kStSticky, 0, sizeof w));
+      if (!first) first = stats_error(e, w[0], w[1], w[2], w[3], sl.path);  // its message kept
+    }
+    return first;
+  });
+}
 
 int ngpu_alloc_pinned(ngpu_engine *e, uint64_t bytes, void **out) {
   if (!e || !out) return NGPU_EINVAL;

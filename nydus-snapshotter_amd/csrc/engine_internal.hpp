@@ -87,6 +87,7 @@ struct ngpu_ws_slot {
   bool pending = false;          // a stage has been enqueued on this slot
   uint64_t *h_stats = nullptr;   // pinned: counters + layer stats read back
   uint64_t tick = 0;             // last use (LRU)
+  char path[48] = "";            // digest kernels of its last digest stage (error messages)
 };
 
 struct ngpu_engine {
@@ -122,6 +123,12 @@ struct ngpu_engine {
   bool slot_fused[kTimingRing] = {};  // planning inside the leaf kernel: digest from ev[0]
   uint64_t tcalls = 0;  // calls recorded so far; the current slot is (tcalls - 1) % ring
   int tslot = 0;
+  // the digest stage that took ring entry tslot: a dedup stage on the same
+  // workspace slot and stream completes that entry (ev[tslot][4]); any other
+  // dedup stage records no timing (it must not re-record another stage's event)
+  ngpu_ws_slot *tshare_slot = nullptr;
+  hipStream_t tshare_stream = nullptr;
+  bool tshare_open = false;
   hipEvent_t host_ev = nullptr;  // host_fence marker (system scope)
   std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu, <= kStagingPool
   static constexpr size_t kStagingPool = 32;   // 16 packs open at once keep theirs
@@ -162,10 +169,13 @@ int host_fence(ngpu_engine *e, hipStream_t s, hipEvent_t ev = nullptr);
 // fenced: host_fence already recorded after the last kernel.
 int read_stats(ngpu_engine *e, hipStream_t s, ngpu_layer_stats *st, bool fenced);
 // The same in two halves, for callers that wait outside e->mu: enqueue the
-// copies of the current slot's counters + layer stats into pinned h (32
-// words) on s (e->mu held); after s is synchronised, check and unpack them.
+// copies of the current slot's counters (kStWords) + layer stats (at
+// kStatsLayer) into pinned h (32 words) on s (e->mu held); after s is
+// synchronised, check and unpack them.
+constexpr int kStatsLayer = 24;
 int read_stats_enqueue(ngpu_engine *e, hipStream_t s, uint64_t *h);
-int read_stats_parse(ngpu_engine *e, const uint64_t *h, ngpu_layer_stats *st);
+int read_stats_parse(ngpu_engine *e, const uint64_t *h, ngpu_layer_stats *st,
+                     const char *path = nullptr);
 // Order a workspace stage on stream s after the previous one (any stream).
 int ws_acquire(ngpu_engine *e, hipStream_t s);
 // Digest then dedup on one stream (digest chained).

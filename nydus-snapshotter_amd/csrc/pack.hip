@@ -675,6 +675,7 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
   ngpu_chunk *ch = nullptr;
   ngpu_result *res = nullptr;
   ngpu_layer_stats st{};
+  std::string path;
   if (!rc) {
     DeviceGuard dg(e->device);
     {
@@ -731,12 +732,13 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
               hipSuccess)
         rc = fail(e, NGPU_EHIP, "pack: result copy failed");
       if (!rc) rc = read_stats_enqueue(e, ps, p->h_stats);
+      path = e->cur->path;  // the digest kernels, for a guard error (read outside the lock)
     }
     // wait for the pack's own stream without the engine lock (other packs
     // and calls keep enqueueing meanwhile), then check its stats
     if (!rc && hipStreamSynchronize(p->stream) != hipSuccess)
       rc = fail(e, NGPU_EHIP, "pack: stream failed");
-    if (!rc) rc = read_stats_parse(e, p->h_stats, &st);
+    if (!rc) rc = read_stats_parse(e, p->h_stats, &st, path.c_str());
     if (!rc && n) memcpy(res, p->h_io, n * sizeof(ngpu_result));
     // the blob stream is host work on the pack's own buffers: no engine lock
     if (!rc && w) rc = write_stream(p, *opt, w, ctx, ch, res, n, st, info);

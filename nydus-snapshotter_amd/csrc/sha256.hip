@@ -142,7 +142,7 @@ __global__ __launch_bounds__(128) void sha256_split(
   if (valid) {
     const ngpu_chunk ch = chunks[c];
     if (ch.offset > data_len || ch.length > data_len - ch.offset) {
-      if (rounds) atomicAdd((unsigned long long *)err, 1ull);
+      if (rounds) note_bad_desc(err, 1);
       valid = false;
     } else {
       len = ch.length;
@@ -209,6 +209,7 @@ __global__ __launch_bounds__(128) void sha256_split(
     uint4 *dd = reinterpret_cast<uint4 *>(out[c].digest);
     dd[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
     dd[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
+    out[c].kind = NGPU_DIGESTED;  // the dedup stage takes only marked records
   }
 }
 
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(256) void sha256_lane(
   if (c >= n) return;
   const ngpu_chunk ch = chunks[c];
   if (ch.offset > data_len || ch.length > data_len - ch.offset) {
-    atomicAdd((unsigned long long *)err, 1ull);
+    note_bad_desc(err, 1);
     return;
   }
   const uint32_t len = ch.length;
@@ -262,6 +263,7 @@ __global__ __launch_bounds__(256) void sha256_lane(
   uint4 *dd = reinterpret_cast<uint4 *>(out[c].digest);
   dd[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
   dd[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
+  out[c].kind = NGPU_DIGESTED;
 }
 
 // Two lanes per chunk for the rounds (few, long chunks: the per-chunk round
@@ -320,7 +322,7 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
   if (valid) {
     const ngpu_chunk ch = chunks[c];
     if (ch.offset > data_len || ch.length > data_len - ch.offset) {
-      if (rounds && side == 0) atomicAdd((unsigned long long *)err, 1ull);
+      if (rounds && side == 0) note_bad_desc(err, 1);
       valid = false;
     } else {
       len = ch.length;
@@ -441,6 +443,7 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
   if (rounds && valid) {
     uint4 *dd = reinterpret_cast<uint4 *>(out[c].digest) + (side ? 0 : 1);
     *dd = make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));
+    if (side) out[c].kind = NGPU_DIGESTED;
   }
 }
 

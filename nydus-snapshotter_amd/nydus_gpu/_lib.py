@@ -16,12 +16,16 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("NYDUS_GPU_LIB") or os.path.join(PKG_DIR, "libnydusgpu.so")
 
 DIGESTERS = {"blake3": 0, "sha256": 1}
-KIND_NAMES = {0: "NEW", 1: "INTRA", 2: "DICT"}
-NEW, INTRA, DICT = 0, 1, 2
+KIND_NAMES = {0: "NEW", 1: "INTRA", 2: "DICT", 3: "DIGESTED", 4: "UNHASHED"}
+# DIGESTED: a digest-stage record (the dedup stage takes only these; callers
+# supplying their own digests set it); UNHASHED: the dedup stage found no
+# digest written for the chunk (the call fails with EDEVICE).
+NEW, INTRA, DICT, DIGESTED, UNHASHED = 0, 1, 2, 3, 4
 
 ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ETAR", -5: "EUNSUPP",
-          -6: "ENODEV", -7: "EIO", -8: "EFORMAT", -9: "ENOTFOUND", -10: "ECANCELED"}
-EINVAL, ENOTFOUND, ECANCELED = -1, -9, -10
+          -6: "ENODEV", -7: "EIO", -8: "EFORMAT", -9: "ENOTFOUND", -10: "ECANCELED",
+          -11: "EDEVICE"}
+EINVAL, EUNSUPP, ENOTFOUND, ECANCELED, EDEVICE = -1, -5, -9, -10, -11
 
 # PackOption.Compressor -> TOCEntry flag values (pkg/converter/types.go:22-31);
 # "" is nydus-image's default (zstd).
@@ -61,7 +65,8 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_dict_probe", "ngpu_process_dict", "ngpu_process_dict_device",
            "ngpu_pack_open_dict", "ngpu_pack_set_cancel", "ngpu_node_create", "ngpu_node_destroy",
            "ngpu_node_size", "ngpu_node_engine", "ngpu_node_dict_open", "ngpu_node_dict_create",
-           "ngpu_node_owner", "ngpu_node_pack_open", "ngpu_node_process_device"]
+           "ngpu_node_owner", "ngpu_node_pack_open", "ngpu_node_process_device",
+           "ngpu_device_status"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
@@ -153,6 +158,7 @@ def lib():
     L.ngpu_destroy.restype = None
     L.ngpu_last_error.argtypes = [vp]
     L.ngpu_last_error.restype = ctypes.c_char_p
+    L.ngpu_device_status.argtypes = [vp]
     L.ngpu_device_count.restype = i32
     L.ngpu_alloc_pinned.argtypes = [vp, u64, ctypes.POINTER(vp)]
     L.ngpu_free_pinned.argtypes = [vp, vp]
@@ -498,6 +504,11 @@ class Engine:
         if rc:
             msg = lib().ngpu_last_error(self._h)
             raise NgpuError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def device_status(self):
+        """ngpu_device_status: raise the first error a device-pointer stage
+        recorded since the last check (waits for the engine's streams)."""
+        self._check(lib().ngpu_device_status(self._h), "device_status")
 
     def dict_load(self, digests, usize, blob_index, chunk_index=None):
         d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1, 32)

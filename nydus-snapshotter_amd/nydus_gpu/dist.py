@@ -52,17 +52,28 @@ class ShardedChunkDict:
         """comm_device: device the all-to-all runs on (None = the tensors' own;
         "cpu" when the process group is gloo and the data lives on a GPU).
 
-        cap > 0 (the same on every rank): at most cap queries per probe, and
-        the exchange uses EQUAL splits -- every rank sends each owner a
-        cap-row slot, padded -- so no split size ever goes to the host: the
-        probe is stream-ordered end to end (no device->host sync between a
-        layer's digest and its dedup).  It moves world x the query bytes and
-        probes world x cap rows (padding included) in exchange.  cap == 0:
-        variable splits, sized on the host from an all-to-all of the counts
-        (one sync per probe, minimal bytes)."""
+        cap > 0 (the same on every rank): the exchange uses EQUAL splits --
+        every rank sends each owner a cap-row slot per round, padded -- so no
+        split size ever goes to the device->host path: the probe is
+        stream-ordered end to end (no sync between a layer's digest and its
+        dedup).  It moves world x the query bytes and probes world x cap rows
+        (padding included) per round.  The round count is agreed on the host
+        first: one all-reduce(MAX) of the ranks' query counts over a gloo
+        group (host integers only, the GPU streams are not touched), so a rank
+        with more than cap queries runs extra rounds TOGETHER with the others
+        instead of failing alone while they block in the collective (ADVICE
+        r2).  cap == 0: variable splits, sized on the host from an all-to-all
+        of the counts (one device sync per probe, minimal bytes)."""
         self.rank, self.world, self.group = rank, world, group
         self.comm_device = comm_device
         self.cap = int(cap)
+        self._meta = None  # gloo group for the round-count agreement (created on every rank)
+        if self.cap and world > 1:
+            import torch.distributed as dist
+            if dist.get_backend(group) == "gloo":
+                self._meta = group
+            else:
+                self._meta = dist.new_group(ranks=list(range(world)), backend="gloo")
         self.local_to_global: Optional[torch.Tensor] = None
         self.n_blobs = 0
         self.probe_fn: Optional[Callable[[torch.Tensor], torch.Tensor]] = None
@@ -114,32 +125,48 @@ class ShardedChunkDict:
         res[order] = back.to(dev)
         return res
 
+    def rounds(self, n: int) -> int:
+        """Equal-split rounds for this probe: ceil(max over ranks of n / cap),
+        agreed on the host (every rank must call it with its own n)."""
+        import torch.distributed as dist
+        t = torch.tensor([n], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._meta)
+        return max(1, -(-int(t.item()) // self.cap))
+
     def _probe_equal(self, digests: torch.Tensor) -> torch.Tensor:
-        """Equal-split exchange (cap rows per owner, see __init__): each query
-        goes to row `pos` of its owner's slot, pos = its rank among this
-        rank's queries for that owner (stable), all computed on the device."""
+        """Equal-split exchange (cap rows per owner and round, see __init__):
+        each query goes to round pos // cap, row pos % cap of its owner's slot,
+        pos = its rank among this rank's queries for that owner (stable), all
+        computed on the device.  Rows of other rounds write a dummy row cap."""
         n, W, cap = digests.shape[0], self.world, self.cap
-        if n > cap:
-            raise ValueError(f"{n} queries > cap {cap}")
+        R = self.rounds(n)
         dev = digests.device
         cdev = torch.device(self.comm_device) if self.comm_device else dev
         own = owner_of(digests, W)
         order = torch.argsort(own, stable=True)
         own_s = own[order]
+        dig_s = digests[order]
         counts = torch.bincount(own, minlength=W)
         start = torch.cumsum(counts, 0) - counts
         pos = torch.arange(n, device=dev) - start[own_s]
-        send = torch.zeros((W, cap, 32), dtype=torch.uint8, device=dev)
-        send[own_s, pos] = digests[order]
-        send = send.view(W * cap, 32).to(cdev)
-        recv = torch.empty_like(send)
-        self._a2a(recv, send, None, None)
-        hits = self._local(recv.to(dev)).to(cdev)  # (W * cap, HIT_WORDS): padding rows ignored
-        back = torch.empty_like(hits)
-        self._a2a(back, hits.contiguous(), None, None)
-        back = back.to(dev).view(W, cap, HIT_WORDS)
+        rnd, row = pos // cap, pos % cap
+        res_s = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=dev)
+        for r in range(R):
+            mine = rnd == r
+            idx = torch.where(mine, row, torch.full_like(row, cap))
+            send = torch.zeros((W, cap + 1, 32), dtype=torch.uint8, device=dev)
+            send[own_s, idx] = dig_s
+            send = send[:, :cap].reshape(W * cap, 32).to(cdev)
+            recv = torch.empty_like(send)
+            self._a2a(recv, send, None, None)
+            hits = self._local(recv.to(dev)).to(cdev)  # (W * cap, HIT_WORDS): padding rows ignored
+            back = torch.empty_like(hits)
+            self._a2a(back, hits.contiguous(), None, None)
+            back = torch.cat([back.to(dev).view(W, cap, HIT_WORDS),
+                              torch.zeros((W, 1, HIT_WORDS), dtype=torch.int32, device=dev)], 1)
+            res_s = torch.where(mine[:, None], back[own_s, idx], res_s)
         res = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=dev)
-        res[order] = back[own_s, pos]
+        res[order] = res_s
         return res
 
     def _local(self, digests: torch.Tensor) -> torch.Tensor:

