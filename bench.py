@@ -96,6 +96,69 @@ def build_layer_on_gpu(torch, n_files, file_size, chunk_size, seed, dup_every=0)
     return buf, ch
 
 
+_B3 = None
+
+
+def ref_digest(data: bytes, digester: str) -> bytes:
+    """An independent host digest for the post-run spot checks: OpenSSL SHA-256
+    (hashlib) or the official BLAKE3 C that ROCm's LLVM vendors
+    (llvm_blake3_* in libclang-cpp.so, ctypes) -- not the repo's oracle."""
+    global _B3
+    if digester == "sha256":
+        import hashlib
+        return hashlib.sha256(data).digest()
+    if _B3 is None:
+        import ctypes
+        for path in ("/opt/rocm/lib/llvm/lib/libclang-cpp.so",
+                     "/usr/lib/x86_64-linux-gnu/libLLVM-15.so.1"):
+            try:
+                lib = ctypes.CDLL(path)
+                lib.llvm_blake3_hasher_init.argtypes = [ctypes.c_void_p]
+                break
+            except (OSError, AttributeError):
+                lib = None
+        if lib is None:
+            raise RuntimeError("no llvm_blake3_* library for the BLAKE3 spot check")
+        lib.llvm_blake3_hasher_update.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
+        lib.llvm_blake3_hasher_finalize.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
+        _B3 = (lib, ctypes.create_string_buffer(8192), ctypes)
+    lib, st, ct = _B3
+    lib.llvm_blake3_hasher_init(st)
+    lib.llvm_blake3_hasher_update(st, data, len(data))
+    out = ct.create_string_buffer(32)
+    lib.llvm_blake3_hasher_finalize(st, out, 32)
+    return out.raw
+
+
+def high_offset_sample(ch: np.ndarray, k: int = 4, seed: int = 5) -> np.ndarray:
+    """Chunk ids past 2^32 worth checking: every chunk that crosses a 4 GiB
+    boundary, the last chunk, and k random chunks above 4 GiB."""
+    off = ch["offset"].astype(np.uint64)
+    end = off + ch["length"].astype(np.uint64) - np.uint64(1)
+    cross = np.nonzero((off >> np.uint64(32)) != (end >> np.uint64(32)))[0]
+    above = np.nonzero(off >= np.uint64(1 << 32))[0]
+    rng = np.random.default_rng(seed)
+    pick = rng.choice(above, min(k, len(above)), replace=False) if len(above) else above
+    return np.unique(np.concatenate([cross, pick, [len(ch) - 1]]).astype(np.int64))
+
+
+def check_high_digests(buf, ch, res, digester) -> dict:
+    """Post-run check: C2/C3 layers reach offset 2^34, so
+    verify the digests of high_offset_sample against ref_digest."""
+    ids = high_offset_sample(ch)
+    bad = []
+    for i in ids:
+        o, ln = int(ch["offset"][i]), int(ch["length"][i])
+        want = ref_digest(buf[o:o + ln].cpu().numpy().tobytes(), digester)
+        if res["digest"][i].tobytes() != want:
+            bad.append(int(i))
+    assert not bad, f"digest mismatch past 4 GiB at chunks {bad}"
+    return {"chunks": len(ids), "max_offset": int(ch["offset"][ids].max()),
+            "crossing_4gib": int(((ch["offset"][ids] >> 32) !=
+                                  ((ch["offset"][ids] + ch["length"][ids] - 1) >> 32)).sum()),
+            "ok": True}
+
+
 def host_cpus():
     """CPUs this process may run on (sched affinity = what `nproc` prints) and
     the cgroup CPU quota in cores, if one is set."""
@@ -1053,6 +1116,8 @@ def main():
         extra["dict"]["dict_hits"] = int(kinds[2])
         assert kinds[2] >= extra["dict"]["expected_dict_hits"] * 0.99, (kinds, extra)
     extra["decisions"] = {"NEW": int(kinds[0]), "INTRA": int(kinds[1]), "DICT": int(kinds[2])}
+    if buf.numel() > (1 << 32) and rank == 0:  # digests at offsets past 2^32 (independent C/OpenSSL)
+        extra["digest_check_past_4gib"] = check_high_digests(buf, ch, res, wl["digester"])
     if wl.get("merge") and world == 1 and rank == 0:
         extra["merge"] = merge_extra(nydus_gpu, ch, res, n_layers, per_layer, wl["chunk"], dict_host)
 

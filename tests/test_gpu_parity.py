@@ -1173,6 +1173,7 @@ def test_reference_v5_bootstrap_as_chunk_dict(tmp_path, oracle):
     res = np.zeros(n, nydus_gpu.RESULT_DTYPE)
     res["digest"] = recs["block_id"][pick]
     res["digest"][::7] = rng.integers(0, 256, (len(res["digest"][::7]), 32), dtype=np.uint8)
+    res["kind"] = nydus_gpu.DIGESTED  # caller-supplied digests enter dedup marked
     ch = np.zeros(n, nydus_gpu.CHUNK_DTYPE)
     ch["length"] = recs["uncompressed_size"][pick]
     ch["length"][::7] = rng.integers(1, 0x100000, len(ch["length"][::7]))
