@@ -451,9 +451,11 @@ int ngpu_chunk_table(const ngpu_chunk *chunks, const ngpu_result *results,
  * (convert_unix.go:486-495): `data | tar_header | ... | toc | tar_header`
  * (convert_unix.go:296-300).  Entries: image.blob (the layer's NEW chunks in
  * index order, each compressed on its own, raw when compression does not
- * shrink it), image.boot (RAFS v6 bootstrap: blob table + chunk table: one
- * record per distinct chunk the layer references -- its NEW chunks and the
- * chunk-dict chunks it reuses, copied with their dict blob placement),
+ * shrink it), image.boot (the RAFS v6 -- or, FsVersion 5, v5 -- bootstrap of
+ * the layer: the tar's whole inode tree, every regular file's chunks, blob
+ * table, prefetch table, and the chunk table: one record per distinct chunk
+ * the layer references -- its NEW chunks and the chunk-dict chunks it reuses,
+ * copied with their dict blob placement),
  * blob.meta + blob.meta.header (convert_unix.go:47-48: the chunk-info array
  * of the layer's blob and its 4 KiB header) and blob.digest (the chunks'
  * digests, index order) when the blob has chunks, and
@@ -490,6 +492,15 @@ typedef struct {
                                 usize, offset 0.  ngpu_pack_finish uses the
                                 pack's dict */
   uint64_t n_dict_chunks;
+  uint32_t fs_version;       /* ngpu_blob_write only: PackOption.FsVersion 5 or 6
+                                (0 -> 6); ngpu_pack_finish uses the engine's.  v6:
+                                RAFS v6 image.boot + blob.meta + TOC (`--features
+                                blob-toc`, builder.go:104-110); v5: RAFS v5
+                                image.boot, no TOC */
+  uint32_t reserved;
+  const char *prefetch_patterns; /* PackOption.PrefetchPatterns: newline-separated
+                                paths (the builder's stdin, builder.go:125-127,
+                                166); NULL or "" -> "/" */
 } ngpu_blob_options;
 
 typedef struct {
@@ -512,7 +523,9 @@ const char *ngpu_host_error(void);
 int ngpu_write_fd(void *ctx, const void *buf, uint64_t len);
 
 /* Host: write the stream of one packed layer whose bytes are in host memory
- * (chunks/results/stats as returned by ngpu_pack_tar / ngpu_process). */
+ * (chunks/results/stats as returned by ngpu_pack_tar).  `data` must be the
+ * layer tar the chunks were cut from: its entries are the bootstrap's inode
+ * tree (NGPU_EINVAL when walking it does not give `chunks`). */
 int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
                     const ngpu_result *results, uint64_t n, const ngpu_layer_stats *stats,
                     const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx,
@@ -536,6 +549,17 @@ int ngpu_pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w
  * zeros when found by tar header.  NGPU_ENOTFOUND = ErrNotFound. */
 int ngpu_unpack_entry(ngpu_read_at_fn ra, void *ctx, uint64_t size, const char *name,
                       ngpu_write_fn w, void *wctx, uint8_t *toc_entry_out);
+
+/* Unpack (convert_unix.go:669-719, `nydus-image unpack`): the nydus stream of
+ * a packed layer (read through ra, `size` bytes) back to an OCI tar written to
+ * w: image.boot's inode tree depth first in name order, each regular file's
+ * chunks read from image.blob and decompressed.  Headers use the Go
+ * archive/tar USTAR encoding (PAX records where USTAR cannot hold a value),
+ * user / group names from the host's passwd / group; a hardlinked inode is a
+ * file at its first path and a hardlink ('1') at the others.  A chunk in
+ * another blob (a chunk-dict blob) is NGPU_ENOTFOUND: only the layer's own
+ * blob travels in its stream. */
+int ngpu_unpack(ngpu_read_at_fn ra, void *ctx, uint64_t size, ngpu_write_fn w, void *wctx);
 
 /* converter.Merge's blob bookkeeping (convert_unix.go:560-666, tool.Merge
  * builder.go:220-294): merge per-layer bootstraps (the image.boot entries)

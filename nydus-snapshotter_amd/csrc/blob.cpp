@@ -32,6 +32,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -46,13 +47,12 @@
 #include <thread>
 
 #include "blob.hpp"
+#include "rafs.hpp"
 
 namespace ngpu {
-namespace {
 
 thread_local std::string g_host_err;
 
-int host_fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 int host_fail(int code, const char *fmt, ...) {
   char buf[512];
   va_list ap;
@@ -83,6 +83,7 @@ struct Codecs {
   size_t (*zstd_decompress_stream)(void *, ZOutBuf *, ZInBuf *) = nullptr;
   int (*lz4_compress)(const char *, char *, int, int) = nullptr;
   int (*lz4_bound)(int) = nullptr;
+  int (*lz4_decompress)(const char *, char *, int, int) = nullptr;
 };
 
 const Codecs &codecs() {
@@ -102,10 +103,32 @@ const Codecs &codecs() {
     if (void *l = dlopen("liblz4.so.1", RTLD_NOW | RTLD_LOCAL)) {
       c.lz4_compress = (decltype(c.lz4_compress))dlsym(l, "LZ4_compress_default");
       c.lz4_bound = (decltype(c.lz4_bound))dlsym(l, "LZ4_compressBound");
+      c.lz4_decompress = (decltype(c.lz4_decompress))dlsym(l, "LZ4_decompress_safe");
     }
   });
   return c;
 }
+
+int decompress_chunk(uint32_t algo, const uint8_t *src, uint64_t csize, uint8_t *dst,
+                     uint64_t usize) {
+  const Codecs &c = codecs();
+  if (algo == 3) {  // zstd
+    if (!c.zstd_decompress) return host_fail(NGPU_EUNSUPP, "zstd unavailable (libzstd.so.1)");
+    const size_t r = c.zstd_decompress(dst, usize, src, csize);
+    if (c.zstd_is_error(r) || r != usize) return host_fail(NGPU_EFORMAT, "bad zstd chunk");
+    return 0;
+  }
+  if (algo == 1) {  // lz4_block
+    if (!c.lz4_decompress) return host_fail(NGPU_EUNSUPP, "lz4 unavailable (liblz4.so.1)");
+    if (csize > 0x7FFFFFFF || usize > 0x7FFFFFFF) return host_fail(NGPU_EFORMAT, "bad lz4 chunk");
+    const int r = c.lz4_decompress((const char *)src, (char *)dst, (int)csize, (int)usize);
+    if (r < 0 || (uint64_t)r != usize) return host_fail(NGPU_EFORMAT, "bad lz4 chunk");
+    return 0;
+  }
+  return host_fail(NGPU_EUNSUPP, "chunk compressed with unknown algorithm %u", algo);
+}
+
+namespace {
 
 uint64_t compress_bound(uint32_t kind, uint32_t n) {
   const Codecs &c = codecs();
@@ -147,6 +170,8 @@ uint64_t super_flags(uint32_t kind, uint32_t digester) {
   return f;
 }
 
+}  // namespace
+
 // ---- SHA-256 (OpenSSL EVP) -------------------------------------------------
 struct Sha {
   EVP_MD_CTX *c = EVP_MD_CTX_new();
@@ -175,6 +200,8 @@ std::string hex(const uint8_t *d, int n) {
   }
   return s;
 }
+
+namespace {
 
 // ---- ustar headers ---------------------------------------------------------
 void put_octal(char *f, int width, uint64_t v) {  // width-1 digits + NUL
@@ -423,7 +450,9 @@ int parse_v5_bootstrap(const uint8_t *p, uint64_t n, uint32_t *digester, uint32_
     bi.blob_index = (uint32_t)i;
     bi.chunk_size = bs;
     bi.digest_algo = dg == NGPU_DIGEST_SHA256 ? 1 : 0;
-    bi.compression_algo = (flags & 0x2) ? 1 : 0;  // lz4_block, as the v6 fixture's flags
+    // RafsSuperFlags compressor bits -> compress::Algorithm (lz4_block 0x2 -> 1, as
+    // the v6 fixture's flags and blob record pair them; zstd 0x80 -> 3)
+    bi.compression_algo = (flags & 0x2) ? 1 : (flags & 0x80) ? 3 : 0;
     if (i < xbent) {
       const uint8_t *x = p + xbto + 64 * i;
       bi.chunk_count = rd_le<uint32_t>(x);
@@ -643,10 +672,14 @@ int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) 
 }
 
 int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_t n,
-                       const ngpu_layer_stats &st, ngpu_blob_info *info) {
+                       const ngpu_layer_stats &st, const std::vector<TarEntry> &entries,
+                       ngpu_blob_info *info) {
   Impl &m = *im_;
   if (m.rc) return m.rc;
   if ((m.rc = m.drain())) return m.rc;
+  const uint32_t fs_version = m.opt.fs_version ? m.opt.fs_version : 6;
+  if (fs_version != 5 && fs_version != 6)
+    return m.rc = host_fail(NGPU_EINVAL, "pack: FsVersion %u", fs_version);
   const uint32_t kind = m.opt.compressor;
   const uint64_t blob_bytes = m.written;
   // image.blob digest; the stream digest continues from the same state
@@ -684,6 +717,29 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
   if (k != m.csize.size()) return host_fail(NGPU_EINVAL, "pack: %llu chunk bodies for %llu NEW chunks",
                                             (unsigned long long)m.csize.size(),
                                             (unsigned long long)k);
+  // every chunk's record, for the inode tree: a NEW or INTRA chunk points at
+  // the NEW record of its index, a DICT chunk at the dict's copy (below)
+  RafsLayerInfo li;
+  li.fs_version = fs_version;
+  li.chunk_size = m.opt.chunk_size;
+  li.digester = m.opt.digester;
+  li.flags = b.flags;
+  if (m.opt.prefetch_patterns) li.prefetch = m.opt.prefetch_patterns;
+  li.refs.resize(n);
+  li.file_of.resize(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    const ngpu_result &r = res[i];
+    li.file_of[i] = chunks[i].file_index;
+    if (r.kind == NGPU_NEW || r.kind == NGPU_INTRA) {
+      if (r.index >= k) return host_fail(NGPU_EINVAL, "pack: chunk %llu index out of range",
+                                         (unsigned long long)i);
+      li.refs[i] = b.chunks[r.index];
+    } else if (r.kind != NGPU_DICT) {
+      return host_fail(NGPU_EINVAL, "pack: chunk %llu has no dedup decision (kind %u)",
+                       (unsigned long long)i, r.kind);
+    }
+    li.refs[i].file_offset = chunks[i].file_offset;
+  }
   // Chunk-dict chunks the layer reuses: one record per distinct (digest, real
   // blob), a copy of the dict's record ([nydus v2.3.0] deduplicate_chunk:
   // chunk.copy_from(cached_chunk) + set_file_offset + the real blob index;
@@ -710,7 +766,7 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
       firsts.push_back(i);
     }
     std::sort(firsts.begin(), firsts.end());
-    for (uint64_t i : firsts) {
+    auto dict_record = [&](uint64_t i) {
       const ngpu_result &r = res[i];
       RafsV6ChunkInfo c;
       memset(&c, 0, sizeof c);
@@ -728,9 +784,13 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
       c.uncompressed_offset = r.uncompressed_offset;
       c.file_offset = chunks[i].file_offset;
       c.index = r.index;
-      b.chunks.push_back(c);
+      return c;
+    };
+    for (uint64_t i : firsts) {
+      b.chunks.push_back(dict_record(i));
       ++ndict;
     }
+    for (uint64_t i : order) li.refs[i] = dict_record(i);
   }
   // blob table in real-index (first-hit) order
   b.blobs.assign(st.blobs, RafsV6BlobInfo{});
@@ -769,8 +829,6 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     if (!set[i]) return host_fail(NGPU_EINVAL, "pack: blob %u never referenced", i);
     b.blobs[i].blob_index = i;
   }
-  const std::vector<uint8_t> boot = write_bootstrap(b);
-  sha256(boot.data(), boot.size(), boot_dig);
 
   // tail (stream offsets from blob_bytes on):
   //   hdr(image.blob) | blob.meta: ci array + ci header | hdr(blob.meta) |
@@ -809,11 +867,14 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
   // one tar entry; the TOC has an entry for each part.  The V2 entry keeps the
   // uncompressed offset in 4 KiB units, so a blob whose offsets are not 4 KiB
   // aligned (RAFS v5 without AlignedChunk) carries no chunk-info array.
+  // RAFS v5 (FsVersion "5"): no `--features blob-toc` (builder.go:104-110),
+  // so no TOC and no blob.meta entries; the bootstrap follows image.blob.
+  const bool v6 = fs_version == 6;
   bool aligned = true;
   for (const RafsV6ChunkInfo &c : b.chunks)
     if (c.blob_index == st.own_blob_index && (c.uncompressed_offset & 4095)) aligned = false;
   uint64_t meta_entries = 0;
-  if (k && aligned) {
+  if (k && aligned && v6) {
     std::vector<uint64_t> ci(3 * k, 0);
     std::vector<uint8_t> dig(32 * k);
     for (const RafsV6ChunkInfo &c : b.chunks) {
@@ -873,15 +934,31 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     hdr("blob.digest", dig.size());
     toc_add("blob.digest", NGPU_COMPRESSOR_NONE, d_dig, d_off, dig.size(), dig.size());
     meta_entries = k;
+    // the own blob's record points at its chunk-info array (the v6 fixture's
+    // blob record: ci compressor, offset, compressed and uncompressed size)
+    uint8_t *bm = b.blobs[st.own_blob_index].meta;
+    memcpy(bm, &ci_algo, 4);
+    memcpy(bm + 4, &ci_off, 8);
+    memcpy(bm + 12, &ci_size, 8);
+    memcpy(bm + 20, &ci_len, 8);
   }
+  // image.boot: the inode tree of the layer (rafs.cpp), RAFS v5 or v6
+  li.blobs = b.blobs;
+  li.table = b.chunks;
+  std::vector<uint8_t> boot;
+  if (int rc = write_rafs(entries, li, &boot)) return m.rc = rc;
+  sha256(boot.data(), boot.size(), boot_dig);
   const uint64_t boot_off = blob_bytes + tail.size();
   put(boot.data(), boot.size());
   hdr("image.boot", boot.size());
   toc_add("image.boot", NGPU_COMPRESSOR_NONE, boot_dig, boot_off, boot.size(), boot.size());
   const uint64_t toc_bytes = toc.size() * sizeof(TocEntry);
-  sha256(toc.data(), toc_bytes, toc_dig);
-  put(toc.data(), toc_bytes);
-  hdr("rafs.blob.toc", toc_bytes);
+  memset(toc_dig, 0, sizeof toc_dig);
+  if (v6) {
+    sha256(toc.data(), toc_bytes, toc_dig);
+    put(toc.data(), toc_bytes);
+    hdr("rafs.blob.toc", toc_bytes);
+  }
   m.stream_sha.update(tail.data(), tail.size());
   m.stream_sha.final(stream_dig);
   if ((m.rc = m.emit(tail.data(), tail.size()))) return m.rc;
@@ -1049,6 +1126,34 @@ int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
       memcpy(&r, (const uint8_t *)opt->dict_chunks + 80 * i, 80);
       place[i] = DictPlace{r.compressed_offset, r.compressed_size, r.flags};
     }
+    // the layer tar's entries: the bootstrap's inode tree.  Walking the tar
+    // must give back the caller's chunk list, or the tree would not match it.
+    std::vector<TarEntry> entries;
+    {
+      struct Cmp : TarSink {
+        const ngpu_chunk *ch;
+        uint64_t n, k = 0;
+        bool same = true;
+        int chunk(uint64_t off, uint32_t l, uint32_t fi, uint64_t fo) override {
+          if (k >= n || ch[k].offset != off || ch[k].length != l || ch[k].file_index != fi ||
+              ch[k].file_offset != fo)
+            same = false;
+          ++k;
+          return 0;
+        }
+        int data(const uint8_t *, uint64_t) override { return 0; }
+      } cmp;
+      cmp.ch = chunks;
+      cmp.n = n;
+      TarScanner sc(opt->chunk_size ? opt->chunk_size : 0x100000);
+      sc.record(&entries);
+      int rc = sc.feed((const uint8_t *)data, len, cmp);
+      if (!rc) rc = sc.finish();
+      if (rc || !cmp.same || cmp.k != n)
+        return host_fail(NGPU_EINVAL,
+                         "ngpu_blob_write: data is not the layer tar the %llu chunks were cut from "
+                         "(chunk_size 0x%x)", (unsigned long long)n, opt->chunk_size);
+    }
     BlobWriter bw(*opt, w, ctx, std::move(dict), place.data(), place.size());
     int rc = bw.init();
     if (rc) return rc;
@@ -1064,7 +1169,7 @@ int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
       lens.push_back(chunks[i].length);
     }
     rc = bw.add(src.data(), lens.data(), src.size());
-    if (!rc) rc = bw.finish(chunks, results, n, *stats, info);
+    if (!rc) rc = bw.finish(chunks, results, n, *stats, entries, info);
     return rc;
   });
   if (rc == NGPU_ENOMEM) host_fail(rc, "ngpu_blob_write: out of memory");
@@ -1108,6 +1213,130 @@ int ngpu_unpack_entry(ngpu_read_at_fn ra, void *ctx, uint64_t size, const char *
     return copy_range(r, off, len, w, wctx);
   });
   if (rc == NGPU_ENOMEM) host_fail(rc, "ngpu_unpack_entry: out of memory");
+  return rc;
+}
+
+namespace {
+// Where an entry of the nydus stream lies: by the TOC (uncompressed entries)
+// or by tar header.  *digest: the TOC's uncompressed sha256, or null.
+int locate(const Reader &r, const char *name, uint64_t *off, uint64_t *len, bool *have_dig,
+           uint8_t dig[32]) {
+  *have_dig = false;
+  uint64_t toff = 0, tlen = 0;
+  int rc = seek_by_tar_header(r, "rafs.blob.toc", 1 << 20, &toff, &tlen);
+  if (rc == 0 && tlen % sizeof(TocEntry) == 0) {
+    std::vector<TocEntry> toc(tlen / sizeof(TocEntry));
+    if ((rc = r.read(toc.data(), tlen, toff))) return rc;
+    for (const TocEntry &e : toc) {
+      if (std::string(e.name, strnlen(e.name, sizeof e.name)) != name) continue;
+      if ((e.flags & 0xf) != NGPU_COMPRESSOR_NONE) break;  // by tar header below
+      *off = e.compressed_offset;
+      *len = e.compressed_size;
+      memcpy(dig, e.uncompressed_digest, 32);
+      *have_dig = true;
+      if (*off > r.size || *len > r.size - *off) return host_fail(NGPU_EFORMAT, "bad TOC entry %s", name);
+      return 0;
+    }
+  } else if (rc && rc != NGPU_ENOTFOUND) {
+    return rc;
+  }
+  return seek_by_tar_header(r, name, -1, off, len);
+}
+}  // namespace
+
+int ngpu_unpack(ngpu_read_at_fn ra, void *ctx, uint64_t size, ngpu_write_fn w, void *wctx) {
+  const int rc = guarded([&]() -> int {
+    if (!ra || !w) return host_fail(NGPU_EINVAL, "ngpu_unpack: bad argument");
+    Reader r{ra, ctx, size};
+    uint64_t boff, blen, doff, dlen;
+    bool bdig, ddig;
+    uint8_t bd[32], dd[32];
+    int rc = locate(r, "image.boot", &boff, &blen, &bdig, bd);
+    if (rc) return rc;
+    if (blen > (8ull << 30)) return host_fail(NGPU_EFORMAT, "bootstrap of %llu bytes", (unsigned long long)blen);
+    std::vector<uint8_t> boot(blen);
+    if ((rc = r.read(boot.data(), blen, boff))) return rc;
+    if ((rc = locate(r, "image.blob", &doff, &dlen, &ddig, dd))) return rc;
+    std::vector<RafsNode> nodes;
+    std::vector<RafsV6BlobInfo> blobs;
+    uint32_t fsv = 0;
+    if ((rc = read_rafs(boot.data(), boot.size(), &nodes, &blobs, &fsv))) return rc;
+    // the layer's own blob: the one named by image.blob's digest (TOC), else
+    // the one whose compressed size is image.blob's size
+    int64_t own = -1;
+    const std::string want = ddig ? hex(dd, 32) : std::string();
+    for (size_t i = 0; i < blobs.size() && own < 0; ++i)
+      if (!want.empty() && blob_id_of(blobs[i]) == want) own = (int64_t)i;
+    for (size_t i = 0; i < blobs.size() && own < 0 && dlen && want.empty(); ++i)
+      if (blobs[i].compressed_size == dlen) own = (int64_t)i;
+    std::vector<uint8_t> out, cbuf, ubuf;
+    std::unordered_map<uint64_t, std::string> first_path;  // ino -> first path (hardlinks)
+    uint64_t flushed = 0;  // bytes already handed to w (tar padding is relative to the stream)
+    auto flush = [&]() -> int {
+      if (!out.empty() && w(wctx, out.data(), out.size()) != 0) return host_fail(NGPU_EIO, "unpack: write failed");
+      flushed += out.size();
+      out.clear();
+      return 0;
+    };
+    for (const RafsNode &nd : nodes) {
+      const uint32_t type = nd.mode & S_IFMT;
+      char tf = '0';
+      std::string link;
+      uint64_t body = 0;
+      if (type == S_IFDIR) tf = '5';
+      else if (type == S_IFLNK) tf = '2', link = nd.link;
+      else if (type == S_IFCHR) tf = '3';
+      else if (type == S_IFBLK) tf = '4';
+      else if (type == S_IFIFO) tf = '6';
+      else if (type != S_IFREG) continue;  // sockets: not representable in a tar
+      if (type != S_IFDIR && nd.nlink > 1) {
+        auto it = first_path.find(nd.ino);
+        if (it != first_path.end()) {
+          tf = '1';
+          link = it->second;
+        } else {
+          first_path.emplace(nd.ino, nd.path);
+        }
+      }
+      if (tf == '0') body = nd.size;
+      tar_entry_header(&out, nd, tf, link, body);
+      if (tf == '0') {
+        uint64_t done = 0;
+        for (const RafsV6ChunkInfo &c : nd.chunks) {
+          if ((int64_t)c.blob_index != own)
+            return host_fail(NGPU_ENOTFOUND, "unpack: %s has a chunk in blob %u (%s), not in this layer",
+                             nd.path.c_str(), c.blob_index,
+                             c.blob_index < blobs.size() ? blob_id_of(blobs[c.blob_index]).c_str() : "?");
+          if (c.compressed_offset > dlen || c.compressed_size > dlen - c.compressed_offset)
+            return host_fail(NGPU_EFORMAT, "unpack: chunk of %s outside image.blob", nd.path.c_str());
+          cbuf.resize(c.compressed_size);
+          if ((rc = r.read(cbuf.data(), c.compressed_size, doff + c.compressed_offset))) return rc;
+          const uint8_t *data = cbuf.data();
+          if (c.flags & 1) {  // compressed with the blob's algorithm
+            ubuf.resize(c.uncompressed_size);
+            if ((rc = decompress_chunk(blobs[own].compression_algo, cbuf.data(), c.compressed_size,
+                                       ubuf.data(), c.uncompressed_size)))
+              return rc;
+            data = ubuf.data();
+          } else if (c.compressed_size != c.uncompressed_size) {
+            return host_fail(NGPU_EFORMAT, "unpack: raw chunk of %s with csize != usize", nd.path.c_str());
+          }
+          const uint64_t take = std::min<uint64_t>(c.uncompressed_size, nd.size - done);
+          out.insert(out.end(), data, data + take);
+          done += take;
+          if (out.size() >= (8u << 20) && (rc = flush())) return rc;
+        }
+        if (done != nd.size) return host_fail(NGPU_EFORMAT, "unpack: %s: %llu of %llu bytes in its chunks",
+                                              nd.path.c_str(), (unsigned long long)done,
+                                              (unsigned long long)nd.size);
+        out.resize(out.size() + (512 - (flushed + out.size()) % 512) % 512, 0);
+      }
+      if (out.size() >= (8u << 20) && (rc = flush())) return rc;
+    }
+    out.resize(out.size() + 1024, 0);  // end of archive: two zero blocks
+    return flush();
+  });
+  if (rc == NGPU_ENOMEM) host_fail(rc, "ngpu_unpack: out of memory");
   return rc;
 }
 

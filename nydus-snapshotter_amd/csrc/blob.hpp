@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "nydus_gpu.h"
+#include "tarstream.hpp"
 
 namespace ngpu {
 
@@ -85,6 +86,21 @@ int guarded(F &&f) noexcept {
   }
 }
 
+// Host helpers (blob.cpp): the thread's last host error (ngpu_host_error),
+// OpenSSL SHA-256, lower-case hex, the dlopen'ed compressors.
+int host_fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+const char *host_error();
+void sha256(const void *p, uint64_t n, uint8_t out[32]);
+std::string hex(const uint8_t *d, int n);
+struct ZInBuf;
+struct ZOutBuf;
+struct Codecs;
+const Codecs &codecs();
+// Decompress one chunk stored with blob compression_algo `algo` (nydus
+// compress::Algorithm: 1 lz4_block, 3 zstd) into exactly `usize` bytes.
+int decompress_chunk(uint32_t algo, const uint8_t *src, uint64_t csize, uint8_t *dst,
+                     uint64_t usize);
+
 // Parsed (minimal) RAFS v6 bootstrap: blob table + chunk table.
 struct Bootstrap {
   uint64_t flags = 0;
@@ -119,9 +135,11 @@ class BlobWriter {
   // NEW chunks in index order (src[k] = host bytes of chunk with index
   // base+k).  The bytes may be reused as soon as the call returns.
   int add(const uint8_t *const *src, const uint32_t *len, uint64_t k);
-  // Writes image.blob's header, image.boot and the TOC.
+  // Writes image.blob's header, blob.meta (v6), image.boot -- the inode tree
+  // of `entries`, the layer tar's entries (tarstream.hpp) -- and the TOC (v6).
   int finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_t n,
-             const ngpu_layer_stats &st, ngpu_blob_info *info);
+             const ngpu_layer_stats &st, const std::vector<TarEntry> &entries,
+             ngpu_blob_info *info);
   const std::string &error() const { return err_; }
   // Cancellation: checked before each compression batch (NGPU_ECANCELED).
   void set_cancel(const volatile int32_t *flag);

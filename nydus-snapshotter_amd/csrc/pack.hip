@@ -159,6 +159,7 @@ struct ngpu_pack : TarSink {
   CopyPool *pool = nullptr;  // created on the first large write
   bool retain = false;       // NGPU_PACK_RETAIN: device segments kept to the end
   std::vector<Seg> segs;
+  std::vector<TarEntry> entries;  // NGPU_PACK_RETAIN: the tar's entries (the bootstrap's inode tree)
   int err = 0;
 
   explicit ngpu_pack(ngpu_engine *eng) : e(eng), sc(eng->cfg.chunk_size) {}
@@ -359,6 +360,7 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
   ngpu_blob_options o = opt;
   o.digester = e->cfg.digester;
   o.chunk_size = e->cfg.chunk_size;
+  o.fs_version = e->cfg.fs_version;
   std::vector<RafsV6BlobInfo> dict;
   const uint8_t *rec = opt.dict_blobs;
   uint64_t nrec = opt.n_dict_blobs;
@@ -475,7 +477,8 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
   }
   cleanup();
   if (rc) return rc;
-  if ((rc = bw.finish(ch, res, n, st, info))) return fail(e, rc, "pack: %s", ngpu_host_error());
+  if ((rc = bw.finish(ch, res, n, st, p->entries, info)))
+    return fail(e, rc, "pack: %s", ngpu_host_error());
   return 0;
 }
 
@@ -499,6 +502,7 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
   dict_ref(dict);
   p->dict = dict;
   p->retain = flags & NGPU_PACK_RETAIN;
+  if (p->retain) p->sc.record(&p->entries);  // the stream's bootstrap lists every entry
   uint64_t cap = e->cfg.staging_bytes;
   if (cap < 4ull * e->cfg.chunk_size) cap = 4ull * e->cfg.chunk_size;
   p->cap = cap;

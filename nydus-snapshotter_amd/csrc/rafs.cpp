@@ -1,0 +1,1234 @@
+// rafs.cpp — RAFS v5 / v6 bootstraps with the layer's whole inode tree (the
+// image.boot of a tar-rafs Pack), their reader, and the OCI tar headers
+// Unpack writes.  Layout notes and the reference each rule is checked on:
+// rafs.hpp.  Host code: the tree is metadata, the chunk digests it lists come
+// from the GPU stage.
+#include "rafs.hpp"
+
+#include <grp.h>
+#include <pwd.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <array>
+#include <functional>
+#include <unordered_map>
+
+namespace ngpu {
+
+// ---- host BLAKE3 (the v5 inode digests) -------------------------------------
+namespace {
+
+constexpr uint32_t kB3IV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
+                               0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
+constexpr uint8_t kB3Perm[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+enum : uint32_t { kStart = 1, kEnd = 2, kParent = 4, kRoot = 8 };
+
+inline uint32_t ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+void b3_compress(const uint32_t cv[8], const uint32_t block[16], uint64_t counter, uint32_t blen,
+                 uint32_t flags, uint32_t out[16]) {
+  uint32_t v[16] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7],
+                    kB3IV[0], kB3IV[1], kB3IV[2], kB3IV[3],
+                    (uint32_t)counter, (uint32_t)(counter >> 32), blen, flags};
+  uint32_t m[16];
+  memcpy(m, block, sizeof m);
+  auto g = [&](int a, int b, int c, int d, uint32_t x, uint32_t y) {
+    v[a] += v[b] + x; v[d] = ror(v[d] ^ v[a], 16); v[c] += v[d]; v[b] = ror(v[b] ^ v[c], 12);
+    v[a] += v[b] + y; v[d] = ror(v[d] ^ v[a], 8);  v[c] += v[d]; v[b] = ror(v[b] ^ v[c], 7);
+  };
+  for (int r = 0; r < 7; ++r) {
+    g(0, 4, 8, 12, m[0], m[1]); g(1, 5, 9, 13, m[2], m[3]);
+    g(2, 6, 10, 14, m[4], m[5]); g(3, 7, 11, 15, m[6], m[7]);
+    g(0, 5, 10, 15, m[8], m[9]); g(1, 6, 11, 12, m[10], m[11]);
+    g(2, 7, 8, 13, m[12], m[13]); g(3, 4, 9, 14, m[14], m[15]);
+    uint32_t t[16];
+    for (int i = 0; i < 16; ++i) t[i] = m[kB3Perm[i]];
+    memcpy(m, t, sizeof m);
+  }
+  for (int i = 0; i < 8; ++i) {
+    out[i] = v[i] ^ v[i + 8];
+    out[i + 8] = v[i + 8] ^ cv[i];
+  }
+}
+
+struct B3Out {
+  uint32_t cv[8], block[16];
+  uint64_t counter;
+  uint32_t blen, flags;
+};
+
+void words(const uint8_t *p, uint32_t n, uint32_t w[16]) {
+  uint8_t b[64] = {};
+  memcpy(b, p, n);
+  for (int i = 0; i < 16; ++i) w[i] = (uint32_t)b[4 * i] | (uint32_t)b[4 * i + 1] << 8 |
+                                      (uint32_t)b[4 * i + 2] << 16 | (uint32_t)b[4 * i + 3] << 24;
+}
+
+// The last block of a <= 1 KiB chunk, every earlier block compressed.
+B3Out chunk_output(const uint8_t *p, uint64_t n, uint64_t counter) {
+  B3Out o;
+  memcpy(o.cv, kB3IV, sizeof o.cv);
+  uint32_t flags = kStart;
+  while (n > 64) {
+    uint32_t w[16], out[16];
+    words(p, 64, w);
+    b3_compress(o.cv, w, counter, 64, flags, out);
+    memcpy(o.cv, out, 32);
+    flags = 0;
+    p += 64;
+    n -= 64;
+  }
+  words(p, (uint32_t)n, o.block);
+  o.counter = counter;
+  o.blen = (uint32_t)n;
+  o.flags = flags | kEnd;
+  return o;
+}
+
+void output_cv(const B3Out &o, uint32_t cv[8]) {
+  uint32_t out[16];
+  b3_compress(o.cv, o.block, o.counter, o.blen, o.flags, out);
+  memcpy(cv, out, 32);
+}
+
+B3Out parent_output(const uint32_t l[8], const uint32_t r[8]) {
+  B3Out o;
+  memcpy(o.cv, kB3IV, sizeof o.cv);
+  memcpy(o.block, l, 32);
+  memcpy(o.block + 8, r, 32);
+  o.counter = 0;
+  o.blen = 64;
+  o.flags = kParent;
+  return o;
+}
+
+}  // namespace
+
+void blake3_host(const void *data, uint64_t n, uint8_t out[32]) {
+  const uint8_t *p = static_cast<const uint8_t *>(data);
+  std::vector<std::array<uint32_t, 8>> stack;
+  uint64_t chunk = 0;
+  while (n > 1024) {  // every chunk but the last: merged into the CV stack
+    std::array<uint32_t, 8> cv;
+    output_cv(chunk_output(p, 1024, chunk), cv.data());
+    ++chunk;
+    for (uint64_t t = chunk; (t & 1) == 0; t >>= 1) {
+      uint32_t m[8];
+      output_cv(parent_output(stack.back().data(), cv.data()), m);
+      stack.pop_back();
+      memcpy(cv.data(), m, sizeof m);
+    }
+    stack.push_back(cv);
+    p += 1024;
+    n -= 1024;
+  }
+  B3Out o = chunk_output(p, n, chunk);
+  while (!stack.empty()) {
+    uint32_t cv[8];
+    output_cv(o, cv);
+    o = parent_output(stack.back().data(), cv);
+    stack.pop_back();
+  }
+  uint32_t w[16];
+  b3_compress(o.cv, o.block, o.counter, o.blen, o.flags | kRoot, w);
+  for (int i = 0; i < 8; ++i)
+    for (int b = 0; b < 4; ++b) out[4 * i + b] = (uint8_t)(w[i] >> (8 * b));
+}
+
+namespace {
+
+// ---- the inode tree ----------------------------------------------------------
+struct Ino {
+  uint32_t mode = 0, uid = 0, gid = 0, rdev = 0, mtime_ns = 0, nlink = 0;
+  int64_t mtime = 0;
+  uint64_t size = 0;
+  std::string link;
+  int64_t file_index = -1;
+  std::vector<std::pair<std::string, std::string>> xattrs;
+  uint64_t ino = 0;    // i_ino: the number of its first dirent
+  uint8_t digest[32] = {};  // v5
+  bool digested = false;
+};
+
+struct Node {
+  std::string name;
+  int parent = -1;
+  std::vector<int> kids;
+  int ino = 0;
+  bool dir = false, dead = false;
+  uint64_t index = 0;        // inode number of this dirent (v5: its record, 1-based)
+  uint64_t child_index = 0;  // v5: first child's number
+  // v6: every dirent has its own inode record (a hardlink too, with its
+  // target's i_ino: fixture perl5.34.0, nid 1555, i_ino 381)
+  uint64_t nid = 0, pos = 0, data_blk = 0;
+  bool placed = false;
+};
+
+struct Tree {
+  std::vector<Node> nodes;
+  std::vector<Ino> inos;
+};
+
+bool is_dir(uint32_t mode) { return (mode & S_IFMT) == S_IFDIR; }
+
+uint32_t type_bits(char t) {
+  switch (t) {
+    case '2': return S_IFLNK;
+    case '3': return S_IFCHR;
+    case '4': return S_IFBLK;
+    case '5': return S_IFDIR;
+    case '6': return S_IFIFO;
+    default: return S_IFREG;
+  }
+}
+
+// Linux new_encode_dev (what st_rdev holds on disk for EROFS and RAFS v5).
+uint32_t encode_dev(uint32_t major, uint32_t minor) {
+  return (minor & 0xff) | (major << 8) | ((minor & ~0xffu) << 12);
+}
+
+void set_meta(Ino &in, const TarEntry &e) {
+  in.mode = type_bits(e.type) | (e.mode & 07777);
+  in.uid = e.uid;
+  in.gid = e.gid;
+  in.mtime = e.mtime;
+  in.mtime_ns = e.mtime_ns;
+  in.xattrs = e.xattrs;
+}
+
+// The tar's entries as a tree: implicit parent directories (0755, root-owned,
+// mtime 0), later entries replacing earlier ones of the same path (a
+// directory entry keeps its children), hardlinks sharing their target's
+// inode.  Entries are sorted by name in every directory.
+int build_tree(const std::vector<TarEntry> &entries, Tree *t) {
+  auto &nodes = t->nodes;
+  auto &inos = t->inos;
+  nodes.assign(1, Node{});
+  nodes[0].name = "/";
+  nodes[0].dir = true;
+  inos.assign(1, Ino{});
+  inos[0].mode = S_IFDIR | 0755;
+  std::unordered_map<std::string, int> by_path{{"", 0}};
+  auto base = [](const std::string &p) {
+    const size_t s = p.rfind('/');
+    return s == std::string::npos ? p : p.substr(s + 1);
+  };
+  auto dirname = [](const std::string &p) {
+    const size_t s = p.rfind('/');
+    return s == std::string::npos ? std::string() : p.substr(0, s);
+  };
+  auto add = [&](int parent, const std::string &path, bool dir, int ino) {
+    Node nd;
+    nd.name = base(path);
+    nd.parent = parent;
+    nd.dir = dir;
+    nd.ino = ino;
+    nodes.push_back(nd);
+    const int id = (int)nodes.size() - 1;
+    nodes[parent].kids.push_back(id);
+    by_path[path] = id;
+    return id;
+  };
+  auto detach = [&](int id) {
+    Node &nd = nodes[id];
+    auto &k = nodes[nd.parent].kids;
+    k.erase(std::remove(k.begin(), k.end(), id), k.end());
+    nd.dead = true;
+  };
+  std::function<int(const std::string &)> dir_node = [&](const std::string &path) -> int {
+    auto it = by_path.find(path);
+    if (it != by_path.end()) {
+      if (!nodes[it->second].dir) return -1;
+      return it->second;
+    }
+    const int parent = dir_node(dirname(path));
+    if (parent < 0) return -1;
+    Ino in;
+    in.mode = S_IFDIR | 0755;
+    inos.push_back(in);
+    return add(parent, path, true, (int)inos.size() - 1);
+  };
+  for (const TarEntry &e : entries) {
+    if (e.path.empty()) {  // "./": the root's own metadata
+      if (e.type == '5') set_meta(inos[0], e);
+      continue;
+    }
+    const int parent = dir_node(dirname(e.path));
+    if (parent < 0)
+      return host_fail(NGPU_EINVAL, "tar entry %s: a parent is not a directory", e.path.c_str());
+    auto it = by_path.find(e.path);
+    if (e.type == '5') {
+      if (it != by_path.end() && nodes[it->second].dir) {
+        set_meta(inos[nodes[it->second].ino], e);
+        continue;
+      }
+      if (it != by_path.end()) detach(it->second);
+      Ino in;
+      set_meta(in, e);
+      inos.push_back(in);
+      add(parent, e.path, true, (int)inos.size() - 1);
+      continue;
+    }
+    int target_ino = -1;
+    if (e.type == '1') {
+      auto tg = by_path.find(e.link);
+      if (tg == by_path.end() || nodes[tg->second].dir)
+        return host_fail(NGPU_EINVAL, "hardlink %s: target %s is not a file in the layer",
+                         e.path.c_str(), e.link.c_str());
+      target_ino = nodes[tg->second].ino;
+    }
+    if (it != by_path.end()) detach(it->second);
+    if (target_ino >= 0) {
+      add(parent, e.path, false, target_ino);
+      continue;
+    }
+    Ino in;
+    set_meta(in, e);
+    in.size = e.type == '0' ? e.size : e.type == '2' ? e.link.size() : 0;
+    if (e.type == '2') in.link = e.link;
+    if (e.type == '3' || e.type == '4') in.rdev = encode_dev(e.devmajor, e.devminor);
+    in.file_index = e.file_index;
+    inos.push_back(in);
+    add(parent, e.path, false, (int)inos.size() - 1);
+  }
+  for (Node &nd : nodes) {
+    if (nd.dead) continue;
+    std::sort(nd.kids.begin(), nd.kids.end(),
+              [&](int a, int b) { return nodes[a].name < nodes[b].name; });
+  }
+  for (Ino &in : inos) in.nlink = is_dir(in.mode) ? 2 : 0;
+  for (const Node &nd : nodes) {
+    if (nd.dead) continue;
+    if (nd.dir && nd.parent >= 0) inos[nodes[nd.parent].ino].nlink++;
+    if (!nd.dir) inos[nd.ino].nlink++;
+  }
+  // inode numbers: root 1; a directory's entries consecutive in name order,
+  // then its subdirectories' (rafs.hpp)
+  uint64_t next = 1;
+  nodes[0].index = next++;
+  inos[0].ino = 1;
+  std::function<void(int)> number = [&](int d) {
+    nodes[d].child_index = next;
+    for (int k : nodes[d].kids) {
+      nodes[k].index = next++;
+      Ino &in = inos[nodes[k].ino];
+      if (!in.ino) in.ino = nodes[k].index;
+    }
+    for (int k : nodes[d].kids)
+      if (nodes[k].dir) number(k);
+  };
+  number(0);
+  return 0;
+}
+
+// Chunk ids of each regular file (file ordinal -> [first, count)).
+struct FileChunks {
+  std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> range;
+};
+
+int file_chunks(const RafsLayerInfo &info, FileChunks *fc) {
+  for (uint64_t i = 0; i < info.file_of.size(); ++i) {
+    auto it = fc->range.find(info.file_of[i]);
+    if (it == fc->range.end()) {
+      fc->range.emplace(info.file_of[i], std::make_pair(i, 1ull));
+    } else {
+      if (it->second.first + it->second.second != i)
+        return host_fail(NGPU_EINVAL, "chunks of file %u are not contiguous", info.file_of[i]);
+      ++it->second.second;
+    }
+  }
+  return 0;
+}
+
+int chunks_of(const Ino &in, const FileChunks &fc, uint32_t chunk_size, uint64_t *first,
+              uint64_t *count) {
+  *first = *count = 0;
+  if ((in.mode & S_IFMT) != S_IFREG || in.size == 0) return 0;
+  const uint64_t want = (in.size + chunk_size - 1) / chunk_size;
+  auto it = in.file_index >= 0 ? fc.range.find((uint32_t)in.file_index) : fc.range.end();
+  if (it == fc.range.end() || it->second.second != want)
+    return host_fail(NGPU_EINVAL, "file #%lld: %llu chunks expected, %llu in the chunk list",
+                     (long long)in.file_index, (unsigned long long)want,
+                     (unsigned long long)(it == fc.range.end() ? 0 : it->second.second));
+  *first = it->second.first;
+  *count = want;
+  return 0;
+}
+
+std::vector<std::string> patterns(const std::string &s) {
+  std::vector<std::string> v;
+  size_t a = 0;
+  while (a <= s.size()) {
+    size_t b = s.find('\n', a);
+    if (b == std::string::npos) b = s.size();
+    std::string p = s.substr(a, b - a);
+    while (!p.empty() && (p.back() == '\r' || p.back() == ' ')) p.pop_back();
+    if (!p.empty()) v.push_back(tar_normalize(p));
+    a = b + 1;
+  }
+  return v;
+}
+
+template <typename T>
+void put(std::vector<uint8_t> &v, uint64_t off, const T &x) {
+  if (v.size() < off + sizeof x) v.resize(off + sizeof x, 0);
+  memcpy(&v[off], &x, sizeof x);
+}
+void put_bytes(std::vector<uint8_t> &v, uint64_t off, const void *p, uint64_t n) {
+  if (!n) return;
+  if (v.size() < off + n) v.resize(off + n, 0);
+  memcpy(&v[off], p, n);
+}
+inline uint64_t align(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+// ---- RAFS v6 ------------------------------------------------------------------
+constexpr uint64_t kBlk = 4096;
+constexpr uint32_t kEroFsFeatureCompatRafsV6 = 0x40000000u;  // fixture super block
+constexpr uint32_t kIncompatChunkedFile = 0x4, kIncompatDeviceTable = 0x8;
+constexpr uint16_t kLayoutPlain = 0, kLayoutInline = 2, kLayoutChunk = 4;
+constexpr uint64_t kDevTableOff = 1408;  // after the 256-B extended super block
+
+uint8_t file_type(uint32_t mode) {
+  switch (mode & S_IFMT) {
+    case S_IFREG: return 1;
+    case S_IFDIR: return 2;
+    case S_IFCHR: return 3;
+    case S_IFBLK: return 4;
+    case S_IFIFO: return 5;
+    case S_IFSOCK: return 6;
+    case S_IFLNK: return 7;
+    default: return 0;
+  }
+}
+
+// EROFS inline xattrs: 12-B ibody header + {name_len u8, name_index u8,
+// value_size u16, name, value} 4-B aligned.  Prefixes: user. 1,
+// system.posix_acl_access 2, system.posix_acl_default 3, trusted. 4, security. 6.
+std::vector<uint8_t> xattr_body(const Ino &in) {
+  std::vector<uint8_t> v;
+  for (const auto &kv : in.xattrs) {
+    static const struct { const char *pre; uint8_t idx; } P[] = {
+        {"user.", 1}, {"system.posix_acl_access", 2}, {"system.posix_acl_default", 3},
+        {"trusted.", 4}, {"security.", 6}};
+    int k = -1;
+    for (int i = 0; i < 5; ++i)
+      if (kv.first.compare(0, strlen(P[i].pre), P[i].pre) == 0) { k = i; break; }
+    if (k < 0 || kv.second.size() > 0xFFFF) continue;  // not representable: dropped
+    const std::string nm = kv.first.substr(strlen(P[k].pre));
+    if (nm.size() > 0xFF) continue;
+    if (v.empty()) v.assign(12, 0);
+    const uint64_t o = v.size();
+    v.resize(align(o + 4 + nm.size() + kv.second.size(), 4), 0);
+    v[o] = (uint8_t)nm.size();
+    v[o + 1] = P[k].idx;
+    const uint16_t vs = (uint16_t)kv.second.size();
+    memcpy(&v[o + 2], &vs, 2);
+    memcpy(&v[o + 4], nm.data(), nm.size());
+    memcpy(&v[o + 4 + nm.size()], kv.second.data(), kv.second.size());
+  }
+  return v;
+}
+
+struct DirBlocks {  // a directory's dirent data, block by block
+  std::vector<std::vector<std::pair<std::string, int>>> blocks;  // (name, node; -1 ".", -2 "..")
+  std::vector<uint32_t> used;
+  uint64_t size = 0;
+};
+
+DirBlocks dir_blocks(const Tree &t, int d) {
+  std::vector<std::pair<std::string, int>> ents{{".", -1}, {"..", -2}};
+  for (int k : t.nodes[d].kids) ents.emplace_back(t.nodes[k].name, k);
+  std::sort(ents.begin(), ents.end(),
+            [](const std::pair<std::string, int> &a, const std::pair<std::string, int> &b) {
+              return a.first < b.first;
+            });
+  DirBlocks db;
+  uint32_t used = 0;
+  for (auto &e : ents) {
+    const uint32_t need = 12 + (uint32_t)e.first.size();
+    if (db.blocks.empty() || used + need > kBlk) {
+      db.blocks.emplace_back();
+      db.used.push_back(0);
+      used = 0;
+    }
+    db.blocks.back().push_back(e);
+    used += need;
+    db.used.back() = used;
+  }
+  db.size = (db.blocks.size() - 1) * kBlk + db.used.back();
+  return db;
+}
+
+void dirent_block(const Tree &t, int d, const std::vector<std::pair<std::string, int>> &ents,
+                  uint8_t *out) {
+  uint16_t nameoff = (uint16_t)(12 * ents.size());
+  for (size_t i = 0; i < ents.size(); ++i) {
+    const int k = ents[i].second;
+    const int nk = k == -1 ? d : k == -2 ? (t.nodes[d].parent < 0 ? d : t.nodes[d].parent) : k;
+    const Ino &in = t.inos[t.nodes[nk].ino];
+    const uint64_t nid = t.nodes[nk].nid;
+    memcpy(out + 12 * i, &nid, 8);
+    memcpy(out + 12 * i + 8, &nameoff, 2);
+    out[12 * i + 10] = file_type(in.mode);
+    out[12 * i + 11] = 0;
+    memcpy(out + nameoff, ents[i].first.data(), ents[i].first.size());
+    nameoff = (uint16_t)(nameoff + ents[i].first.size());
+  }
+}
+
+int write_v6(Tree &t, const RafsLayerInfo &info, std::vector<uint8_t> *outp) {
+  std::vector<uint8_t> &v = *outp;
+  FileChunks fc;
+  if (int rc = file_chunks(info, &fc)) return rc;
+  const uint32_t nb = (uint32_t)info.blobs.size();
+  const uint64_t bto = align(kDevTableOff + 128ull * nb, kBlk);
+  const uint64_t bts = 256ull * nb;
+  std::vector<std::string> pf = patterns(info.prefetch);
+  const uint64_t pto = bto + bts;
+  const uint64_t meta_base = align(pto + 4ull * pf.size(), kBlk);
+  uint64_t chunk_log = 0;
+  while ((4096ull << chunk_log) < info.chunk_size) ++chunk_log;
+
+  // placement: a directory, its non-directory entries, then its subdirectories
+  std::vector<DirBlocks> dirs(t.nodes.size());
+  std::vector<std::vector<uint8_t>> xb(t.inos.size());
+  for (size_t i = 0; i < t.inos.size(); ++i) xb[i] = xattr_body(t.inos[i]);
+  uint64_t pos = meta_base + kBlk;  // root at nid 128, as in the reference fixture
+  std::vector<uint16_t> layout(t.inos.size(), kLayoutPlain);
+  auto place = [&](int node) -> int {
+    Node &nd = t.nodes[node];
+    const int ii = nd.ino;
+    Ino &in = t.inos[ii];
+    nd.placed = true;
+    const uint64_t isz = 64 + xb[ii].size();
+    uint64_t tail = 0, nfull = 0, extra = 0;
+    const uint32_t type = in.mode & S_IFMT;
+    if (type == S_IFDIR || type == S_IFLNK) {
+      const uint64_t sz = type == S_IFDIR ? dirs[node].size : in.link.size();
+      if (type == S_IFDIR) in.size = sz;
+      nfull = sz / kBlk;
+      tail = sz % kBlk;
+      if (isz + tail <= kBlk) {
+        layout[ii] = kLayoutInline;
+      } else {  // the tail does not fit after the inode: every block apart
+        layout[ii] = kLayoutPlain;
+        nfull = (sz + kBlk - 1) / kBlk;
+        tail = 0;
+      }
+    } else if (type == S_IFREG) {
+      uint64_t first, cnt;
+      if (int rc = chunks_of(in, fc, info.chunk_size, &first, &cnt)) return rc;
+      layout[ii] = kLayoutChunk;
+      extra = align(isz, 8) - isz + 8 * cnt;
+    }
+    if (pos % kBlk + isz + tail > kBlk) pos = align(pos, kBlk);
+    nd.pos = pos;
+    nd.nid = (pos - meta_base) / 32;
+    pos = align(pos + isz + tail + extra, 32);
+    if (nfull) {  // full data blocks right after the inode's block (fixture: /usr/bin)
+      nd.data_blk = nd.pos / kBlk + 1;
+      pos = (nd.data_blk + nfull) * kBlk;
+    }
+    return 0;
+  };
+  for (size_t d = 0; d < t.nodes.size(); ++d)
+    if (t.nodes[d].dir && !t.nodes[d].dead) dirs[d] = dir_blocks(t, (int)d);
+  std::function<int(int)> walk = [&](int d) -> int {
+    if (int rc = place(d)) return rc;
+    for (int k : t.nodes[d].kids)
+      if (!t.nodes[k].dir)
+        if (int rc = place(k)) return rc;
+    for (int k : t.nodes[d].kids)
+      if (t.nodes[k].dir)
+        if (int rc = walk(k)) return rc;
+    return 0;
+  };
+  if (int rc = walk(0)) return rc;
+  if (t.nodes[0].nid > 0xFFFF) return host_fail(NGPU_EINVAL, "root nid out of range");
+  const uint64_t cto = align(pos, kBlk);
+  const uint64_t cts = 80ull * info.table.size();
+  const uint64_t total = align(cto + cts, kBlk);
+  v.assign(total, 0);
+
+  // super block (EROFS) + extended super block (RAFS v6)
+  uint64_t ninos = 0;
+  for (const Node &nd : t.nodes) ninos += nd.placed && nd.index == t.inos[nd.ino].ino;
+  put<uint32_t>(v, 1024, kRafsV6Magic);
+  put<uint32_t>(v, 1024 + 8, kEroFsFeatureCompatRafsV6);
+  v[1024 + 12] = 12;  // blkszbits
+  put<uint16_t>(v, 1024 + 14, (uint16_t)t.nodes[0].nid);
+  put<uint64_t>(v, 1024 + 16, ninos);
+  put<uint32_t>(v, 1024 + 36, (uint32_t)(total / kBlk));
+  put<uint32_t>(v, 1024 + 40, (uint32_t)(meta_base / kBlk));
+  put<uint32_t>(v, 1024 + 80, kIncompatChunkedFile | kIncompatDeviceTable);
+  put<uint16_t>(v, 1024 + 86, (uint16_t)nb);
+  put<uint16_t>(v, 1024 + 88, (uint16_t)(kDevTableOff / 128));
+  const uint64_t x = kRafsV6ExtSuperBlockOffset;
+  put<uint64_t>(v, x, info.flags);
+  put<uint64_t>(v, x + 8, nb ? bto : 0);
+  put<uint32_t>(v, x + 16, (uint32_t)bts);
+  put<uint32_t>(v, x + 20, info.chunk_size);
+  put<uint64_t>(v, x + 24, cto);
+  put<uint64_t>(v, x + 32, cts);
+  // device table: blob id, blocks of its uncompressed data
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint64_t o = kDevTableOff + 128ull * b;
+    put_bytes(v, o, info.blobs[b].blob_id, 64);
+    put<uint32_t>(v, o + 64, (uint32_t)((info.blobs[b].uncompressed_size + kBlk - 1) / kBlk));
+  }
+  if (nb) put_bytes(v, bto, info.blobs.data(), bts);
+  // prefetch table: nids of the patterns' inodes ("/" = the root)
+  std::vector<uint32_t> pfn;
+  for (const std::string &p : pf) {
+    int node = 0;
+    size_t a = 0;
+    while (node >= 0 && a < p.size()) {
+      size_t b = p.find('/', a);
+      if (b == std::string::npos) b = p.size();
+      const std::string c = p.substr(a, b - a);
+      int nx = -1;
+      for (int k : t.nodes[node].kids)
+        if (t.nodes[k].name == c) nx = k;
+      node = nx;
+      a = b + 1;
+    }
+    if (node < 0) continue;  // nydus-image ignores patterns that match nothing
+    const uint32_t nid = (uint32_t)t.nodes[node].nid;
+    if (std::find(pfn.begin(), pfn.end(), nid) == pfn.end()) pfn.push_back(nid);
+  }
+  if (!pfn.empty()) {
+    put<uint64_t>(v, x + 40, pto);
+    put<uint32_t>(v, x + 48, (uint32_t)(4 * pfn.size()));
+    put_bytes(v, pto, pfn.data(), 4 * pfn.size());
+  }
+  // inodes
+  for (size_t d = 0; d < t.nodes.size(); ++d) {
+    const Node &nd = t.nodes[d];
+    if (nd.dead) continue;
+    const int ii = nd.ino;
+    const Ino &in = t.inos[ii];
+    if (!nd.placed) continue;
+    const uint64_t o = nd.pos;
+    const uint32_t type = in.mode & S_IFMT;
+    const std::vector<uint8_t> &xa = xb[ii];
+    uint32_t iu = 0;
+    if (layout[ii] == kLayoutChunk) iu = 0x20 | (uint32_t)chunk_log;  // EROFS_CHUNK_FORMAT_INDEXES
+    else if (type == S_IFCHR || type == S_IFBLK) iu = in.rdev;
+    else if (type == S_IFDIR || type == S_IFLNK) iu = (uint32_t)(nd.data_blk ? nd.data_blk : nd.pos / kBlk);
+    put<uint16_t>(v, o, (uint16_t)(1 | (layout[ii] << 1)));  // extended inode
+    put<uint16_t>(v, o + 2, (uint16_t)(xa.empty() ? 0 : (xa.size() - 12) / 4 + 1));
+    put<uint16_t>(v, o + 4, (uint16_t)in.mode);
+    put<uint64_t>(v, o + 8, in.size);
+    put<uint32_t>(v, o + 16, iu);
+    put<uint32_t>(v, o + 20, (uint32_t)in.ino);
+    put<uint32_t>(v, o + 24, in.uid);
+    put<uint32_t>(v, o + 28, in.gid);
+    put<uint64_t>(v, o + 32, (uint64_t)in.mtime);
+    put<uint32_t>(v, o + 40, in.mtime_ns);
+    put<uint32_t>(v, o + 44, in.nlink);
+    put_bytes(v, o + 64, xa.data(), xa.size());
+    const uint64_t body = o + 64 + xa.size();
+    if (type == S_IFDIR) {
+      const DirBlocks &db = dirs[d];
+      const uint64_t nblk = db.blocks.size();
+      for (uint64_t b = 0; b < nblk; ++b) {
+        const bool tail_inline = layout[ii] == kLayoutInline && b + 1 == nblk && db.used[b] < kBlk;
+        uint8_t *dst = tail_inline ? &v[body] : &v[(nd.data_blk + b) * kBlk];
+        dirent_block(t, (int)d, db.blocks[b], dst);
+      }
+    } else if (type == S_IFLNK) {
+      if (layout[ii] == kLayoutInline) {
+        const uint64_t nfull = in.link.size() / kBlk;
+        put_bytes(v, nd.data_blk * kBlk, in.link.data(), nfull * kBlk);
+        put_bytes(v, body, in.link.data() + nfull * kBlk, in.link.size() - nfull * kBlk);
+      } else {
+        put_bytes(v, nd.data_blk * kBlk, in.link.data(), in.link.size());
+      }
+    } else if (layout[ii] == kLayoutChunk) {
+      uint64_t first, cnt;
+      if (int rc = chunks_of(in, fc, info.chunk_size, &first, &cnt)) return rc;
+      uint64_t q = align(body, 8);
+      for (uint64_t k = 0; k < cnt; ++k, q += 8) {
+        const RafsV6ChunkInfo &c = info.refs[first + k];
+        if (c.uncompressed_offset % kBlk)
+          return host_fail(NGPU_EINVAL, "RAFS v6 chunk at unaligned offset %llu",
+                           (unsigned long long)c.uncompressed_offset);
+        put<uint16_t>(v, q, 0);
+        put<uint16_t>(v, q + 2, (uint16_t)(c.blob_index + 1));  // device id: blob + 1
+        put<uint32_t>(v, q + 4, (uint32_t)(c.uncompressed_offset / kBlk));
+      }
+    }
+  }
+  if (cts) put_bytes(v, cto, info.table.data(), cts);
+  return 0;
+}
+
+// ---- RAFS v5 ------------------------------------------------------------------
+constexpr uint64_t kV5SuperBlockSize = 0x2000;
+constexpr uint64_t kV5FlagSymlink = 0x1;
+
+void digest_of(uint32_t digester, const void *p, uint64_t n, uint8_t out[32]) {
+  if (digester == NGPU_DIGEST_SHA256) sha256(p, n, out);
+  else blake3_host(p, n, out);
+}
+
+int write_v5(Tree &t, const RafsLayerInfo &info, std::vector<uint8_t> *outp) {
+  std::vector<uint8_t> &v = *outp;
+  FileChunks fc;
+  if (int rc = file_chunks(info, &fc)) return rc;
+  // records in inode-number order
+  std::vector<int> rec;
+  for (size_t i = 0; i < t.nodes.size(); ++i)
+    if (!t.nodes[i].dead) rec.push_back((int)i);
+  std::sort(rec.begin(), rec.end(),
+            [&](int a, int b) { return t.nodes[a].index < t.nodes[b].index; });
+  // digests, bottom up
+  std::function<int(int)> dig = [&](int d) -> int {
+    Ino &in = t.inos[t.nodes[d].ino];
+    if (in.digested) return 0;
+    const uint32_t type = in.mode & S_IFMT;
+    std::vector<uint8_t> buf;
+    if (type == S_IFDIR) {
+      for (int k : t.nodes[d].kids) {
+        if (int rc = dig(k)) return rc;
+        const Ino &c = t.inos[t.nodes[k].ino];
+        buf.insert(buf.end(), c.digest, c.digest + 32);
+      }
+    } else if (type == S_IFLNK) {
+      buf.assign(in.link.begin(), in.link.end());
+    } else if (type == S_IFREG) {
+      uint64_t first, cnt;
+      if (int rc = chunks_of(in, fc, info.chunk_size, &first, &cnt)) return rc;
+      for (uint64_t k = 0; k < cnt; ++k)
+        buf.insert(buf.end(), info.refs[first + k].block_id, info.refs[first + k].block_id + 32);
+    }
+    digest_of(info.digester, buf.data(), buf.size(), in.digest);
+    in.digested = true;
+    return 0;
+  };
+  if (int rc = dig(0)) return rc;
+  std::vector<std::string> pf = patterns(info.prefetch);
+  std::vector<uint32_t> pfi;
+  for (const std::string &p : pf) {
+    int node = 0;
+    size_t a = 0;
+    while (node >= 0 && a < p.size()) {
+      size_t b = p.find('/', a);
+      if (b == std::string::npos) b = p.size();
+      const std::string c = p.substr(a, b - a);
+      int nx = -1;
+      for (int k : t.nodes[node].kids)
+        if (t.nodes[k].name == c) nx = k;
+      node = nx;
+      a = b + 1;
+    }
+    if (node < 0) continue;
+    const uint32_t ino = (uint32_t)t.inos[t.nodes[node].ino].ino;
+    if (std::find(pfi.begin(), pfi.end(), ino) == pfi.end()) pfi.push_back(ino);
+  }
+  const uint32_t nb = (uint32_t)info.blobs.size();
+  const uint64_t ito = kV5SuperBlockSize;
+  const uint64_t pto = align(ito + 4ull * rec.size(), 8);
+  const uint64_t bto = align(pto + 4ull * pfi.size(), 8);
+  std::vector<uint8_t> bt;  // blob table: {readahead offset, size, id}, NUL-separated, 8-B aligned
+  for (uint32_t b = 0; b < nb; ++b) {
+    bt.resize(bt.size() + 8, 0);
+    const std::string id = blob_id_of(info.blobs[b]);
+    bt.insert(bt.end(), id.begin(), id.end());
+    if (b + 1 < nb) {
+      bt.push_back(0);
+      bt.resize(align(bt.size(), 8), 0);
+    }
+  }
+  const uint64_t xbto = align(bto + bt.size(), 8);
+  uint64_t pos = xbto + 64ull * nb;
+  std::vector<uint64_t> off(rec.size());
+  uint64_t ninos = 0;
+  for (size_t r = 0; r < rec.size(); ++r) {
+    const Node &nd = t.nodes[rec[r]];
+    const Ino &in = t.inos[nd.ino];
+    if (in.ino == nd.index) ++ninos;
+    off[r] = pos;
+    uint64_t sz = 128 + align(nd.name.size(), 8);
+    if ((in.mode & S_IFMT) == S_IFLNK) sz += align(in.link.size(), 8);
+    if ((in.mode & S_IFMT) == S_IFREG) {
+      uint64_t first, cnt;
+      if (int rc = chunks_of(in, fc, info.chunk_size, &first, &cnt)) return rc;
+      sz += 80 * cnt;
+    }
+    pos += sz;
+  }
+  v.assign(pos, 0);
+  put<uint32_t>(v, 0, kRafsV5Magic);
+  put<uint32_t>(v, 4, kRafsV5Version);
+  put<uint32_t>(v, 8, (uint32_t)kV5SuperBlockSize);
+  put<uint32_t>(v, 12, info.chunk_size);
+  put<uint64_t>(v, 16, 0x10 | info.flags);  // EXPLICIT_UID_GID (fixture flags 0x16)
+  put<uint64_t>(v, 24, ninos);
+  put<uint64_t>(v, 32, ito);
+  put<uint64_t>(v, 40, pfi.empty() ? 0 : pto);
+  put<uint64_t>(v, 48, bto);
+  put<uint32_t>(v, 56, (uint32_t)rec.size());
+  put<uint32_t>(v, 60, (uint32_t)pfi.size());
+  put<uint32_t>(v, 64, (uint32_t)bt.size());
+  put<uint32_t>(v, 68, nb);
+  put<uint64_t>(v, 72, xbto);
+  for (size_t r = 0; r < rec.size(); ++r) put<uint32_t>(v, ito + 4 * r, (uint32_t)(off[r] >> 3));
+  put_bytes(v, pto, pfi.data(), 4 * pfi.size());
+  put_bytes(v, bto, bt.data(), bt.size());
+  for (uint32_t b = 0; b < nb; ++b) {  // extended blob table
+    const uint64_t o = xbto + 64ull * b;
+    put<uint32_t>(v, o, info.blobs[b].chunk_count);
+    put<uint64_t>(v, o + 8, info.blobs[b].uncompressed_size);
+    put<uint64_t>(v, o + 16, info.blobs[b].compressed_size);
+  }
+  for (size_t r = 0; r < rec.size(); ++r) {
+    const Node &nd = t.nodes[rec[r]];
+    const Ino &in = t.inos[nd.ino];
+    const uint32_t type = in.mode & S_IFMT;
+    const uint64_t o = off[r];
+    uint64_t first = 0, cnt = 0;
+    if (type == S_IFREG)
+      if (int rc = chunks_of(in, fc, info.chunk_size, &first, &cnt)) return rc;
+    const std::string name = nd.parent < 0 ? "/" : nd.name;
+    put_bytes(v, o, in.digest, 32);
+    put<uint64_t>(v, o + 32, nd.parent < 0 ? 0 : t.inos[t.nodes[nd.parent].ino].ino);
+    put<uint64_t>(v, o + 40, in.ino);
+    put<uint32_t>(v, o + 48, in.uid);
+    put<uint32_t>(v, o + 52, in.gid);
+    put<uint32_t>(v, o + 60, in.mode);
+    const uint64_t size = type == S_IFDIR ? 4096 : in.size;  // fixture: directories 4096
+    put<uint64_t>(v, o + 64, size);
+    put<uint64_t>(v, o + 72, type == S_IFDIR ? 8 : (size + 511) / 512);
+    put<uint64_t>(v, o + 80, type == S_IFLNK ? kV5FlagSymlink : 0);
+    put<uint32_t>(v, o + 88, in.nlink);
+    put<uint32_t>(v, o + 92, type == S_IFDIR ? (uint32_t)nd.child_index : 0);
+    put<uint32_t>(v, o + 96, type == S_IFDIR ? (uint32_t)nd.kids.size() : (uint32_t)cnt);
+    put<uint16_t>(v, o + 100, (uint16_t)name.size());
+    put<uint16_t>(v, o + 102, (uint16_t)(type == S_IFLNK ? in.link.size() : 0));
+    put<uint32_t>(v, o + 104, in.rdev);
+    put<uint32_t>(v, o + 108, in.mtime_ns);
+    put<uint64_t>(v, o + 112, (uint64_t)in.mtime);
+    uint64_t q = o + 128;
+    put_bytes(v, q, name.data(), name.size());
+    q += align(name.size(), 8);
+    if (type == S_IFLNK) {
+      put_bytes(v, q, in.link.data(), in.link.size());
+      q += align(in.link.size(), 8);
+    }
+    for (uint64_t k = 0; k < cnt; ++k, q += 80) put_bytes(v, q, &info.refs[first + k], 80);
+  }
+  return 0;
+}
+
+}  // namespace
+
+int write_rafs(const std::vector<TarEntry> &entries, const RafsLayerInfo &info,
+               std::vector<uint8_t> *out) {
+  Tree t;
+  if (int rc = build_tree(entries, &t)) return rc;
+  if (info.refs.size() != info.file_of.size())
+    return host_fail(NGPU_EINVAL, "chunk records and file ordinals differ in length");
+  return info.fs_version == 5 ? write_v5(t, info, out) : write_v6(t, info, out);
+}
+
+// ---- reader (Unpack) ------------------------------------------------------------
+namespace {
+
+template <typename T>
+bool get(const uint8_t *p, uint64_t n, uint64_t off, T *x) {
+  if (off > n || n - off < sizeof(T)) return false;
+  memcpy(x, p + off, sizeof(T));
+  return true;
+}
+
+struct V6Reader {
+  const uint8_t *p;
+  uint64_t n, base;
+  std::unordered_map<uint64_t, size_t> where;  // (blob << 40 | blkaddr) -> chunk table row
+  std::vector<RafsV6ChunkInfo> table;
+  std::unordered_map<uint64_t, bool> on_path;
+
+  int inode(uint64_t nid, RafsNode *nd, uint16_t *lay, uint64_t *body, uint32_t *iu) {
+    const uint64_t o = base + nid * 32;
+    uint16_t fmt, xic, mode;
+    if (!get(p, n, o, &fmt) || !get(p, n, o + 2, &xic) || !get(p, n, o + 4, &mode))
+      return host_fail(NGPU_EFORMAT, "inode nid %llu out of bounds", (unsigned long long)nid);
+    *lay = (fmt >> 1) & 7;
+    nd->mode = mode;
+    uint64_t isz;
+    if (fmt & 1) {
+      uint32_t ino, uid, gid, nsec, nlink;
+      uint64_t size, mt;
+      if (!get(p, n, o + 8, &size) || !get(p, n, o + 16, iu) || !get(p, n, o + 20, &ino) ||
+          !get(p, n, o + 24, &uid) || !get(p, n, o + 28, &gid) || !get(p, n, o + 32, &mt) ||
+          !get(p, n, o + 40, &nsec) || !get(p, n, o + 44, &nlink))
+        return host_fail(NGPU_EFORMAT, "inode nid %llu truncated", (unsigned long long)nid);
+      nd->size = size;
+      nd->ino = ino;
+      nd->uid = uid;
+      nd->gid = gid;
+      nd->mtime = (int64_t)mt;
+      nd->mtime_ns = nsec;
+      nd->nlink = nlink;
+      isz = 64;
+    } else {  // compact: nlink u16 @6, size u32 @8, i_u @16, ino @20, uid u16 @24, gid u16 @26
+      uint16_t nlink, uid, gid;
+      uint32_t size, ino;
+      if (!get(p, n, o + 6, &nlink) || !get(p, n, o + 8, &size) || !get(p, n, o + 16, iu) ||
+          !get(p, n, o + 20, &ino) || !get(p, n, o + 24, &uid) || !get(p, n, o + 26, &gid))
+        return host_fail(NGPU_EFORMAT, "inode nid %llu truncated", (unsigned long long)nid);
+      nd->size = size;
+      nd->ino = ino;
+      nd->uid = uid;
+      nd->gid = gid;
+      nd->nlink = nlink;
+      isz = 32;
+    }
+    uint64_t xs = 0;
+    if (xic) {
+      xs = 12 + 4ull * (xic - 1);
+      uint64_t q = o + isz + 12, end = o + isz + xs;
+      if (end > n) return host_fail(NGPU_EFORMAT, "xattrs of nid %llu out of bounds", (unsigned long long)nid);
+      uint8_t shared = p[o + isz + 4];
+      q += 4ull * shared;
+      static const char *pre[] = {"", "user.", "system.posix_acl_access", "system.posix_acl_default",
+                                  "trusted.", "", "security."};
+      while (q + 4 <= end) {
+        const uint8_t nl = p[q], idx = p[q + 1];
+        uint16_t vs;
+        memcpy(&vs, p + q + 2, 2);
+        if (q + 4 + nl + vs > end) break;
+        if (idx < 7 && pre[idx][0])
+          nd->xattrs.emplace_back(std::string(pre[idx]) + std::string((const char *)p + q + 4, nl),
+                                  std::string((const char *)p + q + 4 + nl, vs));
+        q = align(q + 4 + nl + vs, 4);
+      }
+    }
+    *body = o + isz + xs;
+    return 0;
+  }
+
+  // data of a flat inode (plain or inline): size bytes
+  int data(uint16_t lay, uint32_t iu, uint64_t body, uint64_t size, std::string *out) {
+    const uint64_t nfull = lay == kLayoutInline ? size / kBlk : (size + kBlk - 1) / kBlk;
+    const uint64_t tail = lay == kLayoutInline ? size % kBlk : 0;
+    const uint64_t fb = (uint64_t)iu * kBlk;
+    const uint64_t full_bytes = lay == kLayoutInline ? nfull * kBlk : size;
+    if ((full_bytes && (fb > n || full_bytes > n - fb)) || body > n || tail > n - body)
+      return host_fail(NGPU_EFORMAT, "inode data out of bounds");
+    out->assign((const char *)p + fb, full_bytes);
+    out->append((const char *)p + body, tail);
+    return 0;
+  }
+
+  int walk(uint64_t nid, const std::string &path, std::vector<RafsNode> *nodes, uint32_t chunk_size,
+           int depth) {
+    if (depth > 4096) return host_fail(NGPU_EFORMAT, "directory tree too deep");
+    RafsNode me;
+    uint16_t lay;
+    uint64_t body;
+    uint32_t iu;
+    if (int rc = inode(nid, &me, &lay, &body, &iu)) return rc;
+    if (!is_dir(me.mode)) return host_fail(NGPU_EFORMAT, "nid %llu is not a directory", (unsigned long long)nid);
+    std::string d;
+    if (int rc = data(lay, iu, body, me.size, &d)) return rc;
+    on_path[nid] = true;
+    for (uint64_t b = 0; b < d.size(); b += kBlk) {
+      const uint8_t *blk = (const uint8_t *)d.data() + b;
+      const uint64_t bl = std::min<uint64_t>(kBlk, d.size() - b);
+      if (bl < 12) return host_fail(NGPU_EFORMAT, "short dirent block");
+      uint16_t first;
+      memcpy(&first, blk + 8, 2);
+      const uint64_t cnt = first / 12;
+      if (cnt == 0 || first > bl) return host_fail(NGPU_EFORMAT, "bad dirent block");
+      for (uint64_t i = 0; i < cnt; ++i) {
+        uint64_t cn;
+        uint16_t no, nx = 0;
+        memcpy(&cn, blk + 12 * i, 8);
+        memcpy(&no, blk + 12 * i + 8, 2);
+        if (i + 1 < cnt) memcpy(&nx, blk + 12 * (i + 1) + 8, 2);
+        const uint64_t end = i + 1 < cnt ? nx : bl;
+        if (no > end || end > bl) return host_fail(NGPU_EFORMAT, "bad dirent name");
+        std::string name((const char *)blk + no, strnlen((const char *)blk + no, end - no));
+        if (name == "." || name == "..") continue;
+        if (on_path.count(cn) && on_path[cn]) return host_fail(NGPU_EFORMAT, "directory cycle");
+        RafsNode c;
+        uint16_t cl;
+        uint64_t cb;
+        uint32_t ciu;
+        if (int rc = inode(cn, &c, &cl, &cb, &ciu)) return rc;
+        c.path = path.empty() ? name : path + "/" + name;
+        const uint32_t type = c.mode & S_IFMT;
+        if (type == S_IFLNK) {
+          if (int rc = data(cl, ciu, cb, c.size, &c.link)) return rc;
+        } else if (type == S_IFCHR || type == S_IFBLK) {
+          c.rdev = ciu;
+        } else if (type == S_IFREG && c.size) {
+          if (cl != kLayoutChunk) return host_fail(NGPU_EFORMAT, "%s: not chunk based", c.path.c_str());
+          const uint64_t csz = kBlk << (ciu & 0x1F);
+          if (csz != chunk_size && chunk_size) return host_fail(NGPU_EFORMAT, "chunk size mismatch");
+          const uint64_t cnt2 = (c.size + csz - 1) / csz;
+          uint64_t q = align(cb, 8);
+          if (q > n || cnt2 > (n - q) / 8) return host_fail(NGPU_EFORMAT, "chunk indexes out of bounds");
+          for (uint64_t k = 0; k < cnt2; ++k) {
+            uint16_t dev;
+            uint32_t blk2;
+            memcpy(&dev, p + q + 8 * k + 2, 2);
+            memcpy(&blk2, p + q + 8 * k + 4, 4);
+            auto it = where.find((uint64_t)(dev - 1) << 40 | blk2);
+            if (!dev || it == where.end())
+              return host_fail(NGPU_EFORMAT, "%s: chunk %llu not in the chunk table", c.path.c_str(),
+                               (unsigned long long)k);
+            c.chunks.push_back(table[it->second]);
+          }
+        }
+        const bool sub = is_dir(c.mode);
+        nodes->push_back(std::move(c));
+        if (sub) {
+          const std::string cp = nodes->back().path;
+          if (int rc = walk(cn, cp, nodes, chunk_size, depth + 1)) return rc;
+        }
+      }
+    }
+    on_path[nid] = false;
+    return 0;
+  }
+};
+
+int read_v6(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
+            std::vector<RafsV6BlobInfo> *blobs) {
+  Bootstrap b;
+  if (int rc = parse_bootstrap(p, n, &b)) return rc;
+  *blobs = b.blobs;
+  uint16_t root;
+  uint32_t meta;
+  if (!get(p, n, 1024 + 14, &root) || !get(p, n, 1024 + 40, &meta))
+    return host_fail(NGPU_EFORMAT, "truncated super block");
+  V6Reader r{p, n, (uint64_t)meta * kBlk, {}, std::move(b.chunks), {}};
+  for (size_t i = 0; i < r.table.size(); ++i)
+    r.where.emplace((uint64_t)r.table[i].blob_index << 40 | (r.table[i].uncompressed_offset / kBlk), i);
+  return r.walk(root, "", nodes, b.chunk_size, 0);
+}
+
+int read_v5(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
+            std::vector<RafsV6BlobInfo> *blobs) {
+  uint32_t dg, cs;
+  std::vector<uint8_t> recs, bl;
+  if (int rc = parse_v5_bootstrap(p, n, &dg, &cs, &recs, &bl)) return rc;
+  blobs->resize(bl.size() / sizeof(RafsV6BlobInfo));
+  if (!bl.empty()) memcpy(blobs->data(), bl.data(), bl.size());
+  uint64_t ito = 0;
+  uint32_t ient = 0;
+  get(p, n, 32, &ito);
+  get(p, n, 56, &ient);
+  auto rec_off = [&](uint64_t idx) -> uint64_t {  // 1-based record -> byte offset (0: bad)
+    uint32_t o;
+    if (idx == 0 || idx > ient || !get(p, n, ito + 4 * (idx - 1), &o)) return 0;
+    return (uint64_t)o << 3;
+  };
+  std::function<int(uint64_t, const std::string &, int)> walk =
+      [&](uint64_t idx, const std::string &path, int depth) -> int {
+    if (depth > 4096) return host_fail(NGPU_EFORMAT, "directory tree too deep");
+    const uint64_t o = rec_off(idx);
+    uint32_t cidx, ccnt;
+    if (!o || !get(p, n, o + 92, &cidx) || !get(p, n, o + 96, &ccnt))
+      return host_fail(NGPU_EFORMAT, "inode %llu out of bounds", (unsigned long long)idx);
+    for (uint64_t k = cidx; k < (uint64_t)cidx + ccnt; ++k) {
+      const uint64_t c = rec_off(k);
+      if (!c || c > n || n - c < 128) return host_fail(NGPU_EFORMAT, "inode %llu out of bounds", (unsigned long long)k);
+      RafsNode nd;
+      uint64_t ino = 0, size = 0, fl = 0, mt = 0;
+      uint32_t uid = 0, gid = 0, mode = 0, nlink = 0, cc = 0, rdev = 0, nsec = 0;
+      uint16_t nsz = 0, slsz = 0;
+      get(p, n, c + 40, &ino); get(p, n, c + 48, &uid); get(p, n, c + 52, &gid);
+      get(p, n, c + 60, &mode); get(p, n, c + 64, &size); get(p, n, c + 80, &fl);
+      get(p, n, c + 88, &nlink); get(p, n, c + 96, &cc); get(p, n, c + 100, &nsz);
+      get(p, n, c + 102, &slsz); get(p, n, c + 104, &rdev); get(p, n, c + 108, &nsec);
+      get(p, n, c + 112, &mt);
+      uint64_t q = c + 128;
+      if (q + nsz > n) return host_fail(NGPU_EFORMAT, "inode name out of bounds");
+      const std::string name((const char *)p + q, nsz);
+      q += align(nsz, 8);
+      nd.path = path.empty() ? name : path + "/" + name;
+      nd.mode = mode;
+      nd.uid = uid;
+      nd.gid = gid;
+      nd.nlink = nlink;
+      nd.size = (mode & S_IFMT) == S_IFDIR ? 0 : size;
+      nd.ino = ino;
+      nd.rdev = rdev;
+      nd.mtime = (int64_t)mt;
+      nd.mtime_ns = nsec;
+      if (fl & kV5FlagSymlink) {
+        if (q + slsz > n) return host_fail(NGPU_EFORMAT, "symlink out of bounds");
+        nd.link.assign((const char *)p + q, slsz);
+        q += align(slsz, 8);
+      }
+      if (fl & 0x4) {
+        uint64_t xs;
+        if (!get(p, n, q, &xs) || xs > n) return host_fail(NGPU_EFORMAT, "bad xattr size");
+        q += 8 + align(xs, 8);
+      }
+      if ((mode & S_IFMT) == S_IFREG && size) {
+        if (q > n || (uint64_t)cc * 80 > n - q) return host_fail(NGPU_EFORMAT, "chunks out of bounds");
+        nd.chunks.resize(cc);
+        memcpy(nd.chunks.data(), p + q, 80ull * cc);
+      }
+      const bool sub = (mode & S_IFMT) == S_IFDIR;
+      nodes->push_back(std::move(nd));
+      if (sub) {
+        const std::string cp = nodes->back().path;
+        if (int rc = walk(k, cp, depth + 1)) return rc;
+      }
+    }
+    return 0;
+  };
+  return walk(1, "", 0);
+}
+
+}  // namespace
+
+int read_rafs(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
+              std::vector<RafsV6BlobInfo> *blobs, uint32_t *fs_version) {
+  nodes->clear();
+  uint32_t m5 = 0, m6 = 0;
+  get(p, n, 0, &m5);
+  get(p, n, kRafsV6SuperBlockOffset, &m6);
+  if (m6 == kRafsV6Magic) {
+    *fs_version = 6;
+    return read_v6(p, n, nodes, blobs);
+  }
+  if (m5 == kRafsV5Magic) {
+    *fs_version = 5;
+    return read_v5(p, n, nodes, blobs);
+  }
+  return host_fail(NGPU_EFORMAT, "not a RAFS bootstrap");
+}
+
+// ---- OCI tar headers (Go archive/tar's encoding) ----------------------------------
+namespace {
+
+void fmt_octal(uint8_t *f, int width, uint64_t v) {  // width-1 digits + NUL
+  for (int i = width - 2; i >= 0; --i, v >>= 3) f[i] = (uint8_t)('0' + (v & 7));
+  f[width - 1] = 0;
+}
+bool fits_octal(int width, uint64_t v) { return v < (1ull << (3 * (width - 1))); }
+void fmt_str(uint8_t *f, int width, const std::string &s) {
+  memcpy(f, s.data(), std::min<size_t>(s.size(), (size_t)width));
+}
+bool ascii(const std::string &s) {
+  for (unsigned char c : s)
+    if (c >= 0x80) return false;
+  return true;
+}
+
+std::string lookup_user(uint32_t uid) {
+  struct passwd pw, *res = nullptr;
+  char buf[4096];
+  if (getpwuid_r(uid, &pw, buf, sizeof buf, &res) == 0 && res) return res->pw_name;
+  return "";
+}
+std::string lookup_group(uint32_t gid) {
+  struct group gr, *res = nullptr;
+  char buf[4096];
+  if (getgrgid_r(gid, &gr, buf, sizeof buf, &res) == 0 && res) return res->gr_name;
+  return "";
+}
+
+// splitUSTARPath: prefix (<= 155) / name (<= 100) at a '/'
+bool split_ustar(const std::string &name, std::string *pre, std::string *suf) {
+  size_t len = name.size();
+  if (len <= 100 || !ascii(name)) return false;
+  if (len > 156) len = 156;
+  else if (name[len - 1] == '/') --len;
+  const size_t i = name.rfind('/', len - 1);
+  if (i == std::string::npos || i == 0) return false;
+  const size_t nlen = name.size() - i - 1;
+  if (nlen > 100 || nlen == 0 || i > 155) return false;
+  *pre = name.substr(0, i);
+  *suf = name.substr(i + 1);
+  return true;
+}
+
+void finish_header(uint8_t *h) {
+  memcpy(h + 257, "ustar\0" "00", 8);
+  memset(h + 148, ' ', 8);
+  uint32_t sum = 0;
+  for (int i = 0; i < 512; ++i) sum += h[i];
+  fmt_octal(h + 148, 7, sum);  // 6 digits + NUL, then the space left in place
+  h[155] = ' ';
+}
+
+std::string pax_record(const std::string &k, const std::string &v) {
+  const size_t base = k.size() + v.size() + 3;  // ' ' '=' '\n'
+  size_t len = base + 1;
+  while (std::to_string(len).size() + base != len) len = std::to_string(len).size() + base;
+  return std::to_string(len) + " " + k + "=" + v + "\n";
+}
+
+}  // namespace
+
+void tar_entry_header(std::vector<uint8_t> *out, const RafsNode &nd, char type,
+                      const std::string &link, uint64_t size) {
+  std::vector<std::pair<std::string, std::string>> pax;
+  std::string name = nd.path, pre;
+  std::string short_name = name;
+  if (name.size() > 100 || !ascii(name)) {
+    std::string suf;
+    if (split_ustar(name, &pre, &suf)) short_name = suf;
+    else pax.emplace_back("path", name), short_name = name.substr(0, 100);
+  }
+  if (link.size() > 100 || !ascii(link)) pax.emplace_back("linkpath", link);
+  if (!fits_octal(12, size)) pax.emplace_back("size", std::to_string(size));
+  if (!fits_octal(8, nd.uid)) pax.emplace_back("uid", std::to_string(nd.uid));
+  if (!fits_octal(8, nd.gid)) pax.emplace_back("gid", std::to_string(nd.gid));
+  const bool mt_ok = nd.mtime >= 0 && fits_octal(12, (uint64_t)nd.mtime);
+  if (!mt_ok) pax.emplace_back("mtime", std::to_string(nd.mtime));
+  for (const auto &kv : nd.xattrs) pax.emplace_back("SCHILY.xattr." + kv.first, kv.second);
+  if (!pax.empty()) {
+    std::sort(pax.begin(), pax.end());
+    std::string data;
+    for (const auto &kv : pax) data += pax_record(kv.first, kv.second);
+    const size_t s = name.rfind('/');
+    std::string pn = s == std::string::npos ? "PaxHeaders.0/" + name
+                                            : name.substr(0, s) + "/PaxHeaders.0/" + name.substr(s + 1);
+    uint8_t h[512] = {};
+    fmt_str(h, 100, pn.substr(0, 100));
+    fmt_octal(h + 100, 8, 0);
+    fmt_octal(h + 108, 8, 0);
+    fmt_octal(h + 116, 8, 0);
+    fmt_octal(h + 124, 12, data.size());
+    fmt_octal(h + 136, 12, 0);
+    h[156] = 'x';
+    fmt_octal(h + 329, 8, 0);
+    fmt_octal(h + 337, 8, 0);
+    finish_header(h);
+    out->insert(out->end(), h, h + 512);
+    out->insert(out->end(), data.begin(), data.end());
+    out->resize(align(out->size(), 512), 0);
+  }
+  uint8_t h[512] = {};
+  fmt_str(h, 100, short_name);
+  fmt_octal(h + 100, 8, nd.mode & 07777);
+  fmt_octal(h + 108, 8, fits_octal(8, nd.uid) ? nd.uid : 0);
+  fmt_octal(h + 116, 8, fits_octal(8, nd.gid) ? nd.gid : 0);
+  fmt_octal(h + 124, 12, fits_octal(12, size) ? size : 0);
+  fmt_octal(h + 136, 12, mt_ok ? (uint64_t)nd.mtime : 0);
+  h[156] = (uint8_t)type;
+  fmt_str(h + 157, 100, link.size() <= 100 ? link : link.substr(0, 100));
+  fmt_str(h + 265, 32, lookup_user(nd.uid));
+  fmt_str(h + 297, 32, lookup_group(nd.gid));
+  const uint32_t major = ((nd.rdev >> 8) & 0xfff), minor = (nd.rdev & 0xff) | ((nd.rdev >> 12) & 0xfff00);
+  fmt_octal(h + 329, 8, type == '3' || type == '4' ? major : 0);
+  fmt_octal(h + 337, 8, type == '3' || type == '4' ? minor : 0);
+  fmt_str(h + 345, 155, pre);
+  finish_header(h);
+  out->insert(out->end(), h, h + 512);
+}
+
+}  // namespace ngpu

@@ -15,13 +15,43 @@
 #pragma once
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "nydus_gpu.h"
 
 namespace ngpu {
+
+// One tar entry's metadata, for the RAFS inode tree (TarScanner::record).
+// GNU long names / links and PAX path, linkpath, size, mtime, uid, gid and
+// SCHILY.xattr.* records are applied.  type: '0' regular (also '\0', '7'),
+// '1' hardlink, '2' symlink, '3' char, '4' block, '5' dir, '6' fifo.
+struct TarEntry {
+  std::string path;   // normalised: no leading "./" or "/", no trailing "/"; "" = root
+  std::string link;   // symlink target (as written), or hardlink target (normalised)
+  char type = '0';
+  uint32_t mode = 0, uid = 0, gid = 0, devmajor = 0, devminor = 0;
+  int64_t mtime = 0;
+  uint32_t mtime_ns = 0;
+  uint64_t size = 0;
+  int64_t file_index = -1;  // regular files: ordinal among regular files (ngpu_chunk.file_index)
+  std::vector<std::pair<std::string, std::string>> xattrs;
+};
+
+inline std::string tar_normalize(std::string p) {
+  for (;;) {
+    if (p.compare(0, 2, "./") == 0) p.erase(0, 2);
+    else if (!p.empty() && p[0] == '/') p.erase(0, 1);
+    else break;
+  }
+  while (!p.empty() && p.back() == '/') p.pop_back();
+  if (p == ".") p.clear();
+  return p;
+}
 
 struct TarSink {
   virtual ~TarSink() = default;
@@ -38,6 +68,9 @@ class TarScanner {
   uint64_t files() const { return files_; }
   uint64_t chunks() const { return chunks_; }
   uint64_t offset() const { return pos_; }
+  // Also collect every entry's metadata (the RAFS inode tree); off by default:
+  // the digest path needs only the chunks.
+  void record(std::vector<TarEntry> *entries) { rec_ = entries; }
 
   // Feed the next bytes of the stream.  Returns 0 or a negative NGPU_E*.
   int feed(const uint8_t *p, uint64_t len, TarSink &sink) {
@@ -82,9 +115,15 @@ class TarScanner {
           adv(p, len, take);
           remain_ -= take;
           if (remain_ == 0) {
-            const int r = pax_size();
-            if (r < 0) return err_ = NGPU_ETAR;
-            enter_skip(pad_, false);
+            if (meta_kind_ == 'L' || meta_kind_ == 'K') {  // GNU long name / link (recording)
+              std::string &dst = meta_kind_ == 'L' ? long_name_ : long_link_;
+              dst.assign(pax_.c_str());  // NUL-terminated in the archive
+              have_long_ |= meta_kind_ == 'L' ? 1 : 2;
+            } else {
+              const int r = pax_size();
+              if (r < 0) return err_ = NGPU_ETAR;
+            }
+            enter_skip(pad_, meta_kind_ != 'x');
           }
           break;
         }
@@ -189,12 +228,24 @@ class TarScanner {
         pax_.clear();
         remain_ = size;
         pad_ = padded - size;
+        meta_kind_ = 'x';
         st_ = size ? PAX : HDR;
         if (!size) enter_skip(0, false);
         return 0;
-      case 'g':
       case 'L':
       case 'K':
+        if (rec_ && size <= (1u << 20)) {  // captured: the next entry's long name / link
+          pax_.clear();
+          remain_ = size;
+          pad_ = padded - size;
+          meta_kind_ = type;
+          st_ = size ? PAX : HDR;
+          if (!size) enter_skip(0, true);
+          return 0;
+        }
+        enter_skip(padded, true);
+        return 0;
+      case 'g':
         enter_skip(padded, true);
         return 0;
       case 'S':
@@ -205,6 +256,7 @@ class TarScanner {
     if (have_pax_) size = pax_sz_;
     have_pax_ = false;
     const uint64_t pad = ((size + 511) & ~511ull) - size;
+    if (rec_) record_entry(type, size);
     if (type == '0' || type == '\0' || type == '7') {
       if (size == 0) {
         ++files_;
@@ -223,6 +275,8 @@ class TarScanner {
   }
 
   // PAX records "len key=value\n"; a "size" record overrides the next entry.
+  // When recording, path / linkpath / mtime / uid / gid / SCHILY.xattr.* are
+  // kept for the next entry too.
   int pax_size() {
     const uint8_t *p = reinterpret_cast<const uint8_t *>(pax_.data());
     const uint64_t n = pax_.size();
@@ -240,10 +294,71 @@ class TarScanner {
         }
         pax_sz_ = v;
         have_pax_ = true;
+      } else if (rec_) {
+        const uint8_t *eq = (const uint8_t *)memchr(kv, '=', end - kv);
+        if (eq) pax_kv_.emplace_back(std::string((const char *)kv, eq - kv),
+                                     std::string((const char *)eq + 1, end - eq - 1));
       }
       i += rl;
     }
     return 0;
+  }
+
+  static std::string field(const uint8_t *f, size_t n) {
+    return std::string(reinterpret_cast<const char *>(f), strnlen(reinterpret_cast<const char *>(f), n));
+  }
+
+  // The entry of the header in hdr_ (type, size already PAX-resolved).
+  void record_entry(char type, uint64_t size) {
+    TarEntry e;
+    const bool posix = memcmp(hdr_ + 257, "ustar\0", 6) == 0;
+    std::string name = field(hdr_, 100);
+    if (posix && hdr_[345]) name = field(hdr_ + 345, 155) + "/" + name;
+    std::string link = field(hdr_ + 157, 100);
+    if (have_long_ & 1) name = long_name_;
+    if (have_long_ & 2) link = long_link_;
+    uint64_t v = 0;
+    e.mode = number(hdr_ + 100, 8, &v) ? (uint32_t)(v & 07777) : 0;
+    e.uid = number(hdr_ + 108, 8, &v) ? (uint32_t)v : 0;
+    e.gid = number(hdr_ + 116, 8, &v) ? (uint32_t)v : 0;
+    e.mtime = number(hdr_ + 136, 12, &v) ? (int64_t)v : 0;
+    if (posix || memcmp(hdr_ + 257, "ustar ", 6) == 0) {
+      e.devmajor = number(hdr_ + 329, 8, &v) ? (uint32_t)v : 0;
+      e.devminor = number(hdr_ + 337, 8, &v) ? (uint32_t)v : 0;
+    }
+    for (auto &kv : pax_kv_) {
+      if (kv.first == "path") name = kv.second;
+      else if (kv.first == "linkpath") link = kv.second;
+      else if (kv.first == "uid") e.uid = (uint32_t)strtoull(kv.second.c_str(), nullptr, 10);
+      else if (kv.first == "gid") e.gid = (uint32_t)strtoull(kv.second.c_str(), nullptr, 10);
+      else if (kv.first == "mtime") {
+        const char *s = kv.second.c_str();
+        char *dot = nullptr;
+        e.mtime = strtoll(s, &dot, 10);
+        if (dot && *dot == '.') {  // fraction: nanoseconds, 9 digits
+          uint32_t ns = 0;
+          int d = 0;
+          for (const char *q = dot + 1; *q >= '0' && *q <= '9' && d < 9; ++q, ++d) ns = ns * 10 + (*q - '0');
+          for (; d < 9; ++d) ns *= 10;
+          e.mtime_ns = ns;
+        }
+      } else if (kv.first.compare(0, 13, "SCHILY.xattr.") == 0) {
+        e.xattrs.emplace_back(kv.first.substr(13), kv.second);
+      }
+    }
+    pax_kv_.clear();
+    have_long_ = 0;
+    e.size = size;
+    switch (type) {
+      case '\0': case '7': case '0': e.type = '0'; e.file_index = (int64_t)files_; break;
+      case '1': e.type = '1'; e.size = 0; link = tar_normalize(link); break;
+      case '2': case '3': case '4': case '5': case '6': e.type = type; break;
+      default: return;  // other types carry no inode (as they carry no chunks)
+    }
+    if (e.type != '0') e.size = e.type == '2' ? link.size() : 0;
+    e.path = tar_normalize(name);
+    e.link = std::move(link);
+    rec_->push_back(std::move(e));
   }
 
   const uint32_t S_;
@@ -257,6 +372,12 @@ class TarScanner {
   uint64_t pax_sz_ = 0;
   std::string pax_;
   int err_ = 0;
+  // entry recording (record())
+  std::vector<TarEntry> *rec_ = nullptr;
+  char meta_kind_ = 'x';
+  int have_long_ = 0;  // bit 0: long_name_, bit 1: long_link_ pending
+  std::string long_name_, long_link_;
+  std::vector<std::pair<std::string, std::string>> pax_kv_;
 };
 
 }  // namespace ngpu

@@ -66,7 +66,7 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_pack_open_dict", "ngpu_pack_set_cancel", "ngpu_node_create", "ngpu_node_destroy",
            "ngpu_node_size", "ngpu_node_engine", "ngpu_node_dict_open", "ngpu_node_dict_create",
            "ngpu_node_owner", "ngpu_node_pack_open", "ngpu_node_process_device",
-           "ngpu_device_status"]
+           "ngpu_device_status", "ngpu_unpack"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
@@ -114,7 +114,8 @@ class NgpuBlobOptions(ctypes.Structure):
                 ("threads", ctypes.c_uint32), ("digester", ctypes.c_uint32),
                 ("chunk_size", ctypes.c_uint32), ("n_dict_blobs", ctypes.c_uint32),
                 ("dict_blobs", ctypes.c_void_p), ("dict_chunks", ctypes.c_void_p),
-                ("n_dict_chunks", ctypes.c_uint64)]
+                ("n_dict_chunks", ctypes.c_uint64), ("fs_version", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("prefetch_patterns", ctypes.c_char_p)]
 
 
 class NgpuBlobInfo(ctypes.Structure):
@@ -200,6 +201,7 @@ def lib():
                                    ctypes.POINTER(vp), ctypes.POINTER(vp), pu64,
                                    ctypes.POINTER(NgpuLayerStats), ctypes.POINTER(NgpuBlobInfo)]
     L.ngpu_unpack_entry.argtypes = [READ_AT_FN, vp, u64, ctypes.c_char_p, WRITE_FN, vp, vp]
+    L.ngpu_unpack.argtypes = [READ_AT_FN, vp, u64, WRITE_FN, vp]
     L.ngpu_merge.argtypes = [ctypes.POINTER(vp), pu64, ctypes.POINTER(ctypes.c_char_p), u64, vp,
                              u64, WRITE_FN, vp, ctypes.POINTER(vp)]
     L.ngpu_dict_open.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
@@ -324,12 +326,14 @@ class _Sink:
 
 def blob_options(compressor: str = "", level: int = 0, threads: int = 0, digester: str = "blake3",
                  chunk_size: int = 0x100000, dict_blobs: np.ndarray = None,
-                 dict_chunks: np.ndarray = None):
+                 dict_chunks: np.ndarray = None, fs_version: int = 6, prefetch_patterns: str = ""):
     if compressor not in COMPRESSORS:
         raise ValueError(f"unsupported compressor {compressor!r}")
+    pf = prefetch_patterns.encode() if prefetch_patterns else None
     o = NgpuBlobOptions(compressor=COMPRESSORS[compressor], level=level, threads=threads,
-                        digester=DIGESTERS[digester], chunk_size=chunk_size)
-    keep = []
+                        digester=DIGESTERS[digester], chunk_size=chunk_size, fs_version=fs_version,
+                        prefetch_patterns=pf)
+    keep = [pf]
     if dict_blobs is not None and len(dict_blobs):
         b = np.ascontiguousarray(dict_blobs).view(np.uint8).reshape(-1)
         o.n_dict_blobs = b.size // 256
@@ -345,7 +349,8 @@ def blob_options(compressor: str = "", level: int = 0, threads: int = 0, digeste
 
 def blob_write(data, chunks, results, stats: dict, dest, compressor: str = "", level: int = 0,
                threads: int = 0, digester: str = "blake3", chunk_size: int = 0x100000,
-               dict_blobs: np.ndarray = None, dict_chunks: np.ndarray = None) -> dict:
+               dict_blobs: np.ndarray = None, dict_chunks: np.ndarray = None, fs_version: int = 6,
+               prefetch_patterns: str = "") -> dict:
     """Host: write the nydus blob stream of a packed layer to `dest` (a
     writable file-like); returns the ngpu_blob_info as a dict."""
     L = lib()
@@ -353,7 +358,8 @@ def blob_write(data, chunks, results, stats: dict, dest, compressor: str = "", l
     ch = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
     rs = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
     st = NgpuLayerStats(**{k: stats[k] for k, _ in NgpuLayerStats._fields_})
-    o, keep = blob_options(compressor, level, threads, digester, chunk_size, dict_blobs, dict_chunks)
+    o, keep = blob_options(compressor, level, threads, digester, chunk_size, dict_blobs, dict_chunks,
+                           fs_version, prefetch_patterns)
     sink = _Sink(dest)
     info = NgpuBlobInfo()
     rc = L.ngpu_blob_write(_ptr(buf), buf.size, _ptr(ch), _ptr(rs), len(ch), ctypes.byref(st),
@@ -385,6 +391,28 @@ def unpack_entry(blob, name: str):
     sink.reraise()
     _host_check(rc, f"unpack_entry {name}")
     return b"".join(out), (toc[0] if toc[0]["name"] else None)
+
+
+def unpack(blob, dest=None):
+    """Unpack (convert_unix.go:669-719): a packed layer's nydus stream (bytes /
+    numpy buffer) back to an OCI tar, written to `dest` (file-like) or
+    returned as bytes."""
+    L = lib()
+    src = _buf(blob)
+
+    def ra(_ctx, buf, n, off):
+        n = min(n, src.size - off)
+        if n <= 0:
+            return -1
+        ctypes.memmove(buf, src.ctypes.data + off, n)
+        return n
+    rfn = READ_AT_FN(ra)
+    out = []
+    sink = _Sink(dest if dest is not None else type("W", (), {"write": lambda _s, b: out.append(b)})())
+    rc = L.ngpu_unpack(rfn, None, src.size, sink.fn, None)
+    sink.reraise()
+    _host_check(rc, "unpack")
+    return None if dest is not None else b"".join(out)
 
 
 def merge(bootstraps, layer_digests, dict_bootstrap: bytes = None):
@@ -741,12 +769,12 @@ class PackWriter:
         return ch, rs, st
 
     def finish(self, dest, compressor: str = "", level: int = 0, threads: int = 0,
-               dict_blobs: np.ndarray = None):
+               dict_blobs: np.ndarray = None, prefetch_patterns: str = ""):
         """close() + write the nydus blob stream to `dest` (needs retain=True).
         Returns (chunks, results, stats, blob info dict)."""
-        return self._finish(dest, compressor, level, threads, dict_blobs)
+        return self._finish(dest, compressor, level, threads, dict_blobs, prefetch_patterns)
 
-    def _finish(self, dest, compressor="", level=0, threads=0, dict_blobs=None):
+    def _finish(self, dest, compressor="", level=0, threads=0, dict_blobs=None, prefetch_patterns=""):
         L = lib()
         pc, pr = ctypes.c_void_p(), ctypes.c_void_p()
         n = ctypes.c_uint64(0)
@@ -759,7 +787,8 @@ class PackWriter:
             sink = None
         else:
             o, keep = blob_options(compressor, level, threads, self._eng.digester,
-                                   self._eng.chunk_size, dict_blobs)
+                                   self._eng.chunk_size, dict_blobs, fs_version=self._eng.fs_version,
+                                   prefetch_patterns=prefetch_patterns)
             sink = _Sink(dest)
             rc = L.ngpu_pack_finish(p, ctypes.byref(o), sink.fn, sink.ctx, ctypes.byref(pc),
                                     ctypes.byref(pr), ctypes.byref(n), ctypes.byref(st),

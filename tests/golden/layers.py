@@ -110,6 +110,77 @@ def oci_upper_tar(mb: int = 3) -> bytes:
     return t.bytes()
 
 
+# ---- Go archive/tar's encoding (the reference tests write their tars with it) ----
+# tar.Writer.WriteHeader of a Header that fits USTAR (writeUSTARHeader /
+# templateV7Plus / setFormat in Go's archive/tar): numbers as zero-padded octal
+# with a NUL (width - 1 digits), a zero ModTime written as 0, magic "ustar\0" +
+# "00", the checksum as 6 octal digits + NUL + space; directories keep the name
+# they were given (no "/" appended, unlike Python's tarfile); Close() ends the
+# archive with two zero blocks and no record padding.
+def _go_octal(n: int, width: int) -> bytes:
+    s = format(n, "o")
+    return ("0" * max(0, width - 1 - len(s)) + s).encode() + b"\0"
+
+
+def go_header(name: str, mode: int, size: int, typeflag: bytes, uid: int = 0, gid: int = 0,
+              uname: str = "root", gname: str = "root", mtime: int = 0, linkname: str = "") -> bytes:
+    h = bytearray(512)
+    nb = name.encode()
+    assert len(nb) <= 100
+    h[0:len(nb)] = nb
+    h[100:108] = _go_octal(mode, 8)
+    h[108:116] = _go_octal(uid, 8)
+    h[116:124] = _go_octal(gid, 8)
+    h[124:136] = _go_octal(size, 12)
+    h[136:148] = _go_octal(mtime, 12)
+    h[156:157] = typeflag
+    lb = linkname.encode()
+    h[157:157 + len(lb)] = lb
+    h[257:265] = b"ustar\x0000"
+    h[265:265 + len(uname)] = uname.encode()
+    h[297:297 + len(gname)] = gname.encode()
+    h[329:337] = _go_octal(0, 8)
+    h[337:345] = _go_octal(0, 8)
+    h[148:156] = b" " * 8
+    h[148:155] = _go_octal(sum(h), 7)
+    h[155] = ord(" ")
+    return bytes(h)
+
+
+class GoTar:
+    """The reference tests' writeFileToTar / writeDirToTar (tests/converter_test.go:
+    129-167): mode 0444, the current user's uid / gid / names (root here)."""
+
+    def __init__(self, uid: int = 0, gid: int = 0, uname: str = "root", gname: str = "root"):
+        self.out = bytearray()
+        self.ids = dict(uid=uid, gid=gid, uname=uname, gname=gname)
+
+    def file(self, name: str, data: bytes):
+        self.out += go_header(name, 0o444, len(data), b"0", **self.ids)
+        self.out += data + bytes((-len(data)) % 512)
+
+    def dir(self, name: str):
+        self.out += go_header(name, 0o444, 0, b"5", **self.ids)
+
+    def bytes(self) -> bytes:
+        return bytes(self.out) + bytes(1024)
+
+
+def oci_upper_tar_go(mb: int = 3) -> bytes:
+    """buildOCIUpperTar (tests/converter_test.go:225-274) in Go's encoding,
+    as TestUnpack (:607-635) packs it and compares the Unpack output's sha256
+    with it."""
+    t = GoTar()
+    t.dir("dir-1")
+    t.file("dir-1/.wh.file-1", b"")
+    t.dir("dir-2")
+    t.file("dir-2/.wh..wh..opq", b"")
+    t.file("dir-2/file-1", huge_string(mb))
+    t.file("dir-2/file-2", b"upper-file-2")
+    t.file("dir-2/file-3", b"upper-file-3")
+    return t.bytes()
+
+
 def edge_tar(fmt=tarfile.PAX_FORMAT, chunk: int = 64 * 1024) -> bytes:
     """Chunker edge cases around a given chunk size."""
     t = _TarBuilder(fmt)

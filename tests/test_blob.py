@@ -406,7 +406,7 @@ def test_reader_mutation_fuzz_asan(oracle, tars, tmp_path):
     subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
                            "-fno-sanitize-recover=all", "-I", os.path.join(ROOT, "include"),
                            "-I", csrc, os.path.join(ROOT, "tests", "cpp", "blob_fuzz.cpp"),
-                           os.path.join(csrc, "blob.cpp"), "-o", exe, "-lcrypto", "-ldl",
+                           os.path.join(csrc, "blob.cpp"), os.path.join(csrc, "rafs.cpp"), "-o", exe, "-lcrypto", "-ldl",
                            "-lpthread"])
     stream, *_ = cpu_stream(oracle, tars["edge_pax"], 0x10000, "zstd")
     sp = tmp_path / "s"
@@ -467,7 +467,7 @@ def test_blob_writer_threads_tsan(oracle, tars, tmp_path):
     subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=thread",
                            "-I", os.path.join(ROOT, "include"), "-I", csrc,
                            os.path.join(ROOT, "tests", "cpp", "blob_tsan.cpp"),
-                           os.path.join(csrc, "blob.cpp"), "-o", exe, "-lcrypto", "-ldl",
+                           os.path.join(csrc, "blob.cpp"), os.path.join(csrc, "rafs.cpp"), "-o", exe, "-lcrypto", "-ldl",
                            "-lpthread"])
     cs, tar = 0x10000, tars["alpine_like"]
     ch, res, st = cpu_results(oracle, tar, cs)

@@ -236,7 +236,7 @@ def test_v5_dict_parser_fuzz_asan(tmp_path):
     subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
                            "-fno-sanitize-recover=all", "-I", os.path.join(ROOT, "include"),
                            "-I", csrc, os.path.join(ROOT, "tests", "cpp", "v5dict_fuzz.cpp"),
-                           os.path.join(csrc, "blob.cpp"), "-o", exe, "-lcrypto", "-ldl",
+                           os.path.join(csrc, "blob.cpp"), os.path.join(csrc, "rafs.cpp"), "-o", exe, "-lcrypto", "-ldl",
                            "-lpthread"])
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0")
     out = subprocess.run([exe, str(bp), "1200", "7"], capture_output=True, text=True, env=env,
