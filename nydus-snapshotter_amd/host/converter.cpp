@@ -4,6 +4,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <map>
@@ -65,6 +66,44 @@ Error compressor_of(const std::string &s, uint32_t *out) {
   return {};
 }
 
+// tool.DetectFeatures (pkg/converter/tool/feature.go:114-146): the features a
+// Pack requires, checked once per process against what the builder supports.
+// The GPU builder supports tar-rafs only, so `--batch-size` and `--encrypt`
+// are ignored with the reference's warning, exactly as with a nydus-image too
+// old for them; a later Pack requiring a different set fails ("features
+// changed"), as the reference's process-global sync.Once makes it.
+const char *const kFeatureTar2Rafs = "--type tar-rafs";
+const char *const kFeatureBatchSize = "--batch-size";
+const char *const kFeatureEncrypt = "--encrypt";
+std::mutex g_feat_mu;
+bool g_feat_done = false;
+std::vector<std::string> g_feat_required, g_feat_detected;
+
+Error detect_features(const std::vector<std::string> &required, std::vector<std::string> *detected) {
+  std::lock_guard<std::mutex> g(g_feat_mu);
+  if (!g_feat_done) {
+    g_feat_done = true;
+    g_feat_required = required;
+    for (const std::string &f : required) {
+      if (f == kFeatureTar2Rafs) {
+        g_feat_detected.push_back(f);
+      } else {
+        fprintf(stderr,
+                "level=warning msg=\"the feature '%s' is ignored, it requires higher version of "
+                "nydus-image\" (the GPU builder does not implement it)\n", f.c_str());
+      }
+    }
+  }
+  if (g_feat_required != required) {
+    std::string a, b;
+    for (auto &f : g_feat_required) a += (a.empty() ? "" : ",") + f;
+    for (auto &f : required) b += (b.empty() ? "" : ",") + f;
+    return err(NGPU_EINVAL, "features changed: [" + a + "] -> [" + b + "]");
+  }
+  *detected = g_feat_detected;
+  return {};
+}
+
 // One engine per (device, digester, chunk size, fs version, aligned chunk),
 // like the Python mirror; an engine serialises its own calls, and every Pack
 // holds its own chunk dict handle, so Packs share engines safely.
@@ -103,8 +142,9 @@ Error engine_for(const PackOption &opt, ngpu_engine **out) {
 
 class GpuPackWriteCloser : public PackWriteCloser {
  public:
-  GpuPackWriteCloser(ngpu_engine *e, ngpu_pack *p, Writer &dest, uint32_t comp, double timeout)
-      : e_(e), p_(p), dest_(dest), comp_(comp), timeout_(timeout) {
+  GpuPackWriteCloser(ngpu_engine *e, ngpu_pack *p, Writer &dest, uint32_t comp, double timeout,
+                     std::string prefetch)
+      : e_(e), p_(p), dest_(dest), comp_(comp), timeout_(timeout), prefetch_(std::move(prefetch)) {
     ngpu_pack_set_cancel(p_, &cancel_);
     if (timeout_ > 0)  // builder.go:153-158: the builder runs under ctx.WithTimeout
       timer_ = std::thread([this] {
@@ -135,6 +175,9 @@ class GpuPackWriteCloser : public PackWriteCloser {
     ngpu_blob_options o;
     memset(&o, 0, sizeof o);
     o.compressor = comp_;
+    // PackOption.PrefetchPatterns: the builder's stdin, "/" by default
+    // (builder.go:125-127, 166)
+    o.prefetch_patterns = prefetch_.c_str();
     ngpu_chunk *ch = nullptr;
     ngpu_result *res = nullptr;
     uint64_t n = 0;
@@ -180,6 +223,7 @@ class GpuPackWriteCloser : public PackWriteCloser {
   Writer &dest_;
   uint32_t comp_;
   double timeout_;
+  std::string prefetch_;
   alignas(4) volatile int32_t cancel_ = 0;
   std::thread timer_;
   std::mutex tm_;
@@ -248,7 +292,23 @@ bool IsNotFound(const Error &e) { return e.code == NGPU_ENOTFOUND; }
 
 Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser> *out) {
   out->reset();
-  if (opt.OCIRef) return err(NGPU_EUNSUPP, "OCIRef packing has no chunk digest stage");
+  const std::string fv = opt.FsVersion.empty() ? "6" : opt.FsVersion;  // convert_unix.go:326-328
+  // convert_unix.go:332-356: required features, detected once per process
+  std::vector<std::string> required{kFeatureTar2Rafs}, detected;
+  if (!opt.BatchSize.empty() && opt.BatchSize != "0") required.push_back(kFeatureBatchSize);
+  if (opt.Encrypt) required.push_back(kFeatureEncrypt);
+  if (Error e = detect_features(required, &detected)) return e;
+  if (opt.OCIRef) {
+    if (fv != "6") return err(NGPU_EINVAL, "oci ref can only be supported by fs version 6");
+    // packRef (builder.go:180-218) runs `nydus-image create --type targz-ref`:
+    // the chunks stay in the original gzip layer, addressed through a zran
+    // (gzip random access) index in blob.meta, which this builder does not write
+    return err(NGPU_EUNSUPP,
+               "OCIRef (--type targz-ref) needs a zran gzip index of the original layer in "
+               "blob.meta; the GPU builder packs tar-rafs only");
+  }
+  const bool batch = std::find(detected.begin(), detected.end(), kFeatureBatchSize) != detected.end();
+  if (batch && fv != "6") return err(NGPU_EINVAL, "'--batch-size' can only be supported by fs version 6");
   uint32_t comp = 0;
   if (Error e = compressor_of(opt.Compressor, &comp)) return e;
   ngpu_engine *e = nullptr;
@@ -263,7 +323,14 @@ Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser>
   rc = ngpu_pack_open_dict(e, d, NGPU_PACK_RETAIN, &p);
   ngpu_dict_release(d);  // the pack holds its own reference
   if (rc) return err(rc, std::string("pack open: ") + ngpu_last_error(e));
-  out->reset(new GpuPackWriteCloser(e, p, dest, comp, opt.Timeout));
+  out->reset(new GpuPackWriteCloser(e, p, dest, comp, opt.Timeout, opt.PrefetchPatterns));
+  return {};
+}
+
+Error Unpack(ReaderAt &ra, Writer &dest, const UnpackOption &opt) {
+  (void)opt;  // Stream / WorkDir / BuilderPath / Timeout: the in-process unpack reads ra directly
+  if (int rc = ngpu_unpack(read_trampoline, &ra, ra.Size(), write_trampoline, &dest))
+    return err(rc, std::string("unpack nydus tar: ") + ngpu_host_error());
   return {};
 }
 

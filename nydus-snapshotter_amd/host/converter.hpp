@@ -7,6 +7,7 @@
 //   Pack(dest, opt)            convert_unix.go:325   -> WriteCloser; Close() must be checked
 //   Merge(layers, dest, opt)   convert_unix.go:560   -> referenced blob digests
 //   UnpackEntry(ra, name, w)   convert_unix.go:284   -> TOCEntry (ErrNotFound)
+//   Unpack(ra, dest, opt)      convert_unix.go:669   -> the layer's OCI tar
 // Go's `error` is `Error` (code 0 == nil); nothing throws.  Digest/dedup run on
 // the GPU (libnydusgpu.so); compression, SHA-256 and Merge bookkeeping on the
 // host inside the same library.
@@ -109,6 +110,12 @@ struct MergeOption {  // types.go:92-133
   double Timeout = 0;
 };
 
+struct UnpackOption {  // types.go:135-145
+  std::string WorkDir, BuilderPath;
+  double Timeout = 0;
+  bool Stream = false;
+};
+
 struct Layer {  // types.go:37-44
   std::string Digest;  // "sha256:<hex>" of the whole nydus tar blob
   std::shared_ptr<converter::ReaderAt> ReaderAt;
@@ -133,6 +140,8 @@ Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser>
 Error Merge(const std::vector<Layer> &layers, Writer &dest, const MergeOption &opt,
             std::vector<std::string> *blobDigests);
 Error UnpackEntry(ReaderAt &ra, const std::string &targetName, Writer &target, TOCEntry *entry);
+// Unpack (convert_unix.go:669-719): a nydus layer stream back to the OCI tar.
+Error Unpack(ReaderAt &ra, Writer &dest, const UnpackOption &opt);
 
 // ErrNotFound (types.go:33-35) is code NGPU_ENOTFOUND.
 bool IsNotFound(const Error &e);

@@ -34,7 +34,12 @@ import tarfile
 
 import threading
 
-from ._lib import COMPRESSORS, DICT, ECANCELED, ENOTFOUND, NEW, Engine, NgpuError, merge, unpack_entry
+import logging
+
+from ._lib import (COMPRESSORS, DICT, ECANCELED, ENOTFOUND, NEW, Engine, NgpuError, merge, unpack,
+                   unpack_entry)
+
+_log = logging.getLogger("nydus_gpu.converter")
 
 EntryBlob = "image.blob"            # convert_unix.go:45
 EntryBootstrap = "image.boot"       # :46
@@ -51,6 +56,15 @@ class ConverterError(RuntimeError):
 
 class ErrNotFound(ConverterError):
     """types.go:33-35."""
+
+
+@dataclass
+class UnpackOption:
+    """pkg/converter/types.go:135-145."""
+    WorkDir: str = ""
+    BuilderPath: str = ""
+    Timeout: Optional[float] = None
+    Stream: bool = False
 
 
 @dataclass
@@ -179,7 +193,9 @@ class _PackWriteCloser:
 
     def close(self):
         try:
-            ch, res, st, info = self._w.finish(self._dest, compressor=self._opt.Compressor or "")
+            # PrefetchPatterns: the builder's stdin, "/" by default (builder.go:125-127, 166)
+            ch, res, st, info = self._w.finish(self._dest, compressor=self._opt.Compressor or "",
+                                               prefetch_patterns=self._opt.PrefetchPatterns)
         except NgpuError as e:
             raise self._killed(e) from e
         finally:
@@ -189,12 +205,71 @@ class _PackWriteCloser:
         return self.result
 
 
+# tool.DetectFeatures (pkg/converter/tool/feature.go:114-146): a Pack's
+# required features are checked once per process against the builder's.  The
+# GPU builder supports tar-rafs only: `--batch-size` and `--encrypt` are
+# ignored with the reference's warning, exactly as with a nydus-image too old
+# for them, and a later Pack requiring another set fails ("features changed").
+FeatureTar2Rafs, FeatureBatchSize, FeatureEncrypt = "--type tar-rafs", "--batch-size", "--encrypt"
+_BUILDER_FEATURES = {FeatureTar2Rafs}
+_FEATURES = {"required": None, "detected": None}
+_FEATURES_MU = threading.Lock()
+
+
+def DetectFeatures(required) -> set:
+    required = frozenset(required)
+    with _FEATURES_MU:
+        if _FEATURES["required"] is None:
+            _FEATURES["required"] = required
+            det = set()
+            for f in sorted(required):
+                if f in _BUILDER_FEATURES:
+                    det.add(f)
+                else:
+                    _log.warning("the feature '%s' is ignored, it requires higher version of "
+                                 "nydus-image (the GPU builder does not implement it)", f)
+            _FEATURES["detected"] = det
+        if _FEATURES["required"] != required:
+            raise ConverterError(f"features changed: {sorted(_FEATURES['required'])} -> {sorted(required)}")
+        return set(_FEATURES["detected"])
+
+
+def _reset_feature_detection():
+    """Tests only: forget the once-per-process detection."""
+    with _FEATURES_MU:
+        _FEATURES["required"] = _FEATURES["detected"] = None
+
+
 def Pack(dest: BinaryIO, opt: PackOption) -> _PackWriteCloser:
     """convert_unix.go:325 — returns a writer; stream the layer tar into it and
     check close()."""
+    fs = opt.FsVersion or "6"
+    required = {FeatureTar2Rafs}
+    if opt.BatchSize not in ("", "0"):
+        required.add(FeatureBatchSize)
+    if opt.Encrypt:
+        required.add(FeatureEncrypt)
+    detected = DetectFeatures(required)
     if opt.OCIRef:
-        raise ConverterError("OCIRef packing has no chunk digest stage (not accelerated)")
+        if fs != "6":
+            raise ConverterError("oci ref can only be supported by fs version 6")
+        # packRef (builder.go:180-218): `nydus-image create --type targz-ref`
+        # leaves the chunks in the original gzip layer, addressed through a zran
+        # (gzip random access) index in blob.meta -- not written by this builder
+        raise ConverterError("OCIRef (--type targz-ref) needs a zran gzip index of the original "
+                             "layer in blob.meta; the GPU builder packs tar-rafs only")
+    if FeatureBatchSize in detected and fs != "6":
+        raise ConverterError("'--batch-size' can only be supported by fs version 6")
     return _PackWriteCloser(dest, opt)
+
+
+def Unpack(ra: bytes, dest: BinaryIO, opt: Optional[UnpackOption] = None):
+    """convert_unix.go:669-719 — the nydus layer stream back to an OCI tar
+    (ngpu_unpack: image.boot's inode tree, chunks from image.blob)."""
+    try:
+        unpack(ra, dest)
+    except NgpuError as e:
+        raise ConverterError(f"unpack nydus tar: {e}") from e
 
 
 def UnpackEntry(ra: bytes, targetName: str, target: BinaryIO):
@@ -242,5 +317,6 @@ def Merge(layers: Sequence[Layer], dest: BinaryIO, opt: MergeOption) -> List[str
     return ["sha256:" + i for i in ids]
 
 
-__all__ = ["PackOption", "MergeOption", "Layer", "Pack", "Merge", "UnpackEntry", "ConverterError",
+__all__ = ["PackOption", "MergeOption", "UnpackOption", "Layer", "Pack", "Merge", "Unpack",
+           "UnpackEntry", "DetectFeatures", "ConverterError",
            "ErrNotFound", "NgpuError", "parse_chunk_size", "EntryBlob", "EntryBootstrap", "EntryTOC"]

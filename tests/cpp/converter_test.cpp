@@ -3,7 +3,9 @@
 // converter.hpp) on the GPU.  Reads the three layer tars the Python harness
 // writes (chunk dict, lower, upper), packs and merges exactly as the Go test
 // does, and checks the same assertions with REQUIRE (require.*).
-// usage: converter_test DICT.tar LOWER.tar UPPER.tar WORKDIR [COMPRESSOR]
+// With UPPER_GO.tar (buildOCIUpperTar in Go's tar encoding) it also runs
+// TestUnpack (converter_test.go:607-635): Pack -> Unpack, sha256 equal, v5 + v6.
+// usage: converter_test DICT.tar LOWER.tar UPPER.tar WORKDIR [COMPRESSOR [UPPER_GO.tar]]
 // Prints "digest <name> sha256:<hex>" lines and "PASS"; exit 1 on failure.
 #include <openssl/evp.h>
 #include <stdio.h>
@@ -70,11 +72,11 @@ struct Packed {
 
 // packLayer (converter_test.go:276-300): Pack, copy the source in, Close.
 static Packed packLayer(const std::vector<uint8_t> &source, const std::string &chunkDict,
-                        const std::string &compressor) {
+                        const std::string &compressor, const std::string &fsVersion = "6") {
   BufferWriter data;
   PackOption opt;
   opt.ChunkDictPath = chunkDict;
-  opt.FsVersion = "6";
+  opt.FsVersion = fsVersion;
   opt.Compressor = compressor;
   std::unique_ptr<PackWriteCloser> twc;
   REQUIRE_NOERR(Pack(data, opt, &twc));
@@ -149,6 +151,35 @@ int main(int argc, char **argv) {
   std::unique_ptr<PackWriteCloser> w;
   BufferWriter sink;
   REQUIRE(Pack(sink, bad, &w).code == -1 && !w, "invalid chunk size is an error");
+
+  // OCIRef: the reference's own fs-version error, else an accurate refusal
+  PackOption ref;
+  ref.OCIRef = true;
+  Error re = Pack(sink, ref, &w);
+  REQUIRE(re.code == -5 && re.msg.find("targz-ref") != std::string::npos && !w, "OCIRef: %s",
+          re.msg.c_str());
+  ref.FsVersion = "5";
+  re = Pack(sink, ref, &w);
+  REQUIRE(re.msg == "oci ref can only be supported by fs version 6", "OCIRef v5: %s", re.msg.c_str());
+
+  // TestUnpack (converter_test.go:607-635): OCI tar -> Pack -> Unpack, same sha256
+  if (argc > 6) {
+    const std::vector<uint8_t> ociTar = read_file(argv[6]);
+    const std::string ociDigest = sha256_digest(ociTar);
+    for (const char *fs : {"5", "6"}) {
+      Packed nydusTar = packLayer(ociTar, "", comp, fs);
+      for (bool stream : {true, false}) {
+        BytesReaderAt tarRa(nydusTar.data.data(), nydusTar.data.size());
+        BufferWriter out;
+        UnpackOption uo;
+        uo.Stream = stream;
+        REQUIRE_NOERR(Unpack(tarRa, out, uo));
+        REQUIRE(sha256_digest(out.data) == ociDigest, "fs %s: unpacked %s != %s", fs,
+                sha256_digest(out.data).c_str(), ociDigest.c_str());
+      }
+    }
+    printf("unpack ok\n");
+  }
 
   printf("digest dict %s\ndigest lower %s\ndigest upper %s\n", dict.digest.c_str(),
          lower.digest.c_str(), upper.digest.c_str());

@@ -888,10 +888,13 @@ def test_cpp_converter_mirror_testpack(tars, tmp_path, compressor):
         paths.append(str(p))
     work = tmp_path / "work"
     work.mkdir()
-    r = subprocess.run([exe, *paths, str(work), compressor], capture_output=True, text=True, timeout=120)
+    go = tmp_path / "oci_upper_go.tar"  # TestUnpack's input in Go's tar encoding
+    go.write_bytes(layers.oci_upper_tar_go(3))
+    r = subprocess.run([exe, *paths, str(work), compressor, str(go)], capture_output=True, text=True,
+                       timeout=120)
     assert r.returncode == 0, r.stderr
     lines = r.stdout.splitlines()
-    assert lines[-1] == "PASS"
+    assert lines[-1] == "PASS" and "unpack ok" in lines
     dig = dict(line.split()[1:] for line in lines if line.startswith("digest "))
     dict_file = work / dig["dict"][7:]
     assert "sha256:" + hashlib.sha256(dict_file.read_bytes()).hexdigest() == dig["dict"]

@@ -1,0 +1,95 @@
+"""converter.Pack -> Unpack through the GPU engine (VERDICT r2 "What's
+missing" 1-2, done-criteria): the streaming Pack (ngpu_pack_* with
+NGPU_PACK_RETAIN, digests and dedup on the GPU, the host writer's RAFS v5 / v6
+bootstrap with the tar's inode tree) and ngpu_unpack give back the tar:
+
+  * TestUnpack (tests/converter_test.go:607-635) restated: buildOCIUpperTar in
+    Go's archive/tar encoding, FsVersion "5" and "6", sha256 equal;
+  * the fixture decoders read the GPU Pack's image.boot into the tar's files,
+    with the GPU's digests in the chunk records;
+  * a Pack against a chunk dict still lists the DICT records it reuses, and
+    its Unpack reports the dict blob it needs (ENOTFOUND)."""
+import hashlib
+import io
+import tarfile
+
+import numpy as np
+import pytest
+
+import nydus_gpu
+import rafs_fixtures as rf
+
+import layers
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_pack(eng, tar, compressor="zstd", prefetch="", split=1 << 20, dict=nydus_gpu.DEFAULT_DICT):
+    w = eng.pack(retain=True, dict=dict)
+    for a in range(0, len(tar), split):
+        w.write(tar[a:a + split])
+    out = io.BytesIO()
+    ch, res, st, info = w.finish(out, compressor=compressor, prefetch_patterns=prefetch)
+    return out.getvalue(), ch, res, st, info
+
+
+@pytest.mark.parametrize("fs", [5, 6])
+@pytest.mark.parametrize("cs", [0x100000, 0x10000])
+def test_pack_unpack_restates_testunpack(fs, cs):
+    tar = layers.oci_upper_tar_go(3)
+    eng = nydus_gpu.Engine(chunk_size=cs, fs_version=fs)
+    try:
+        for comp in ("zstd", "lz4_block", "none"):
+            blob, ch, res, st, info = _gpu_pack(eng, tar, compressor=comp)
+            back = nydus_gpu.unpack(blob)
+            assert hashlib.sha256(back).hexdigest() == hashlib.sha256(tar).hexdigest(), (fs, cs, comp)
+            # v6 streams carry the TOC; v5 streams find their entries by tar header
+            assert (info["toc_digest"] != "0" * 64) == (fs == 6)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("fs", [5, 6])
+def test_gpu_pack_bootstrap_lists_the_tar(fs, oracle):
+    tar = layers.alpine_like_tar()
+    eng = nydus_gpu.Engine(chunk_size=0x10000, fs_version=fs)
+    try:
+        blob, ch, res, st, info = _gpu_pack(eng, tar)
+    finally:
+        eng.close()
+    boot = nydus_gpu.unpack_entry(blob, "image.boot")[0]
+    dig = oracle.digest_chunks(tar, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    assert np.array_equal(res["digest"], dig)
+    if fs == 6:
+        files = rf.read_v6_files(boot)
+        got = np.concatenate([f[3]["block_id"] for f in files])
+    else:
+        files = rf.read_v5(boot)["files"]
+        got = np.concatenate([f[4]["block_id"] for f in files])
+    # every chunk reference of every regular file, in the tar's own order
+    # (inode-number order == tar order for this layer), is the GPU digest
+    assert len(got) == len(ch)
+    assert {bytes(d) for d in got} == {bytes(d) for d in dig}
+    tf = tarfile.open(fileobj=io.BytesIO(nydus_gpu.unpack(blob)))
+    src = tarfile.open(fileobj=io.BytesIO(tar))
+    assert sorted(m.name.rstrip("/") for m in src) == sorted(m.name for m in tf)
+
+
+def test_dict_pack_lists_dict_records_and_unpack_names_the_dict_blob(golden_layers, tars):
+    tp = golden_layers["testpack"]
+    dd = np.frombuffer(b"".join(bytes.fromhex(e[0]) for e in tp["dict"]), np.uint8).reshape(-1, 32)
+    arrs = (dd, np.array([e[1] for e in tp["dict"]], np.uint32),
+            np.array([e[2] for e in tp["dict"]], np.uint32), np.array([e[3] for e in tp["dict"]], np.uint32))
+    eng = nydus_gpu.Engine(chunk_size=0x100000)
+    try:
+        eng.dict_load(*arrs)
+        blob, ch, res, st, info = _gpu_pack(eng, tars["oci_lower"])
+    finally:
+        eng.close()
+    assert (res["kind"] == nydus_gpu.DICT).all() and info["dict_records"] > 0
+    boot = nydus_gpu.unpack_entry(blob, "image.boot")[0]
+    files = rf.read_v6_files(boot)  # every file's chunk indexes resolve to the DICT records
+    assert sum(len(f[3]) for f in files) == len(ch)
+    with pytest.raises(nydus_gpu.NgpuError) as e:
+        nydus_gpu.unpack(blob)
+    assert e.value.code == nydus_gpu.ENOTFOUND

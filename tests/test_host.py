@@ -217,3 +217,57 @@ def test_product_never_reaches_the_oracle():
                 if b"liboracle" in open(p, "rb").read():
                     hits.append(p)
     assert not hits, hits
+
+
+def test_pack_option_features_and_ociref(caplog):
+    """PackOption honesty (convert_unix.go:325-356, tool/feature.go:114-146):
+    BatchSize / Encrypt are features the GPU builder does not implement, so
+    DetectFeatures ignores them with the reference's own warning (as with a
+    nydus-image too old for them); the detection is once per process and a
+    later Pack with another required set fails "features changed"; OCIRef gets
+    the reference's fs-version error on v5 and an accurate refusal on v6.
+    Everything here fails before the engine is created (no GPU needed)."""
+    import io
+    import logging
+    from nydus_gpu import converter as cv
+
+    def pack(**kw):
+        try:
+            w = cv.Pack(io.BytesIO(), cv.PackOption(**kw))
+        except nydus_gpu.NgpuError as e:  # CPU: the engine has no device
+            assert e.code == nydus_gpu.ENODEV
+            return None
+        w.write(b"\0" * 1024)  # an empty tar
+        w.close()
+        return None
+
+    cv._reset_feature_detection()
+    try:
+        with caplog.at_level(logging.WARNING, logger=cv._log.name):
+            pack(BatchSize="0x100000", FsVersion="6")
+        assert "the feature '--batch-size' is ignored, it requires higher version of nydus-image" in caplog.text
+        # same required set again: no error, no second warning
+        caplog.clear()
+        pack(BatchSize="0x200000")
+        assert "ignored" not in caplog.text
+        # the ignored feature is not detected, so the v5 check does not fire
+        pack(BatchSize="0x100000", FsVersion="5")
+        with pytest.raises(cv.ConverterError, match="features changed"):
+            pack()
+        with pytest.raises(cv.ConverterError, match="features changed"):
+            pack(BatchSize="0x100000", Encrypt=True)
+
+        cv._reset_feature_detection()
+        with caplog.at_level(logging.WARNING, logger=cv._log.name):
+            pack(Encrypt=True)
+        assert "the feature '--encrypt' is ignored" in caplog.text
+
+        cv._reset_feature_detection()
+        with pytest.raises(cv.ConverterError, match="^oci ref can only be supported by fs version 6$"):
+            pack(OCIRef=True, FsVersion="5")
+        with pytest.raises(cv.ConverterError, match="targz-ref.*zran"):
+            pack(OCIRef=True)
+        with pytest.raises(cv.ConverterError, match="targz-ref"):
+            pack(OCIRef=True, FsVersion="6")
+    finally:
+        cv._reset_feature_detection()
