@@ -37,7 +37,7 @@ void dict_ref(ngpu_dict *d) {
 
 void dict_unref(ngpu_dict *d) {
   if (!d || d->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
-  if (!d->io.empty() || !d->parts.empty()) node_dict_free(d);
+  if (!d->req.empty() || !d->parts.empty()) node_dict_free(d);
   DeviceGuard g(d->device);
   // hipFree waits for the device, so no queued probe still reads the table
   for (void *p : d->allocs) (void)hipFree(p);

@@ -504,7 +504,9 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) return NGPU_ENODEV;
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NGPU_ENODEV;
+  static std::atomic<uint64_t> next_uid{1};
   ngpu_engine *e = new ngpu_engine();
+  e->uid = next_uid.fetch_add(1, std::memory_order_relaxed);
   e->cfg = c;
   // NGPU_WS_SLOTS: workspace slots = calls on distinct streams that may run
   // at once (default 4, the hardware queues HIP gives a process)

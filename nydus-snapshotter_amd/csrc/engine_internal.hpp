@@ -4,6 +4,7 @@
 #pragma once
 
 #include <atomic>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -54,19 +55,29 @@ struct ngpu_dict {
   uint64_t st_dev = 0, st_ino = 0, st_size = 0;
   int64_t st_mtime_ns = 0;
   // node dicts (node.hip): one part per node device -- a digest-prefix shard
-  // (its records carry their global entry ids) or a full replica --
-  // and per part a probe stream plus the exchange buffers on its device.
+  // (its records carry their global entry ids) or a full replica.
   // dev.m / dev.n_blobs are the global counts; dev.rec / dev.table stay null.
+  // The exchange runs over one channel per (owner part, requester engine):
+  // a probe stream, the query/hit buffers and a cached `done` event on the
+  // owner's device, so requesters never share a buffer, stream or lock.
   struct PartIO {
     hipStream_t stream = nullptr;
     uint8_t *q = nullptr;        // requester digests (n x 32), copied in
     ngpu_dict_hit *h = nullptr;  // this part's hits (n), copied back
     uint64_t cap = 0;
+    hipEvent_t done = nullptr;   // recorded on `stream` after the hits copy back
+  };
+  struct Requester {
+    uint64_t engine_uid = 0;
+    int device = 0;
+    hipEvent_t ready = nullptr;  // on the requester's device: its queries are packed
+    std::vector<PartIO> io;      // one per owner part
+    std::mutex mu;               // one exchange at a time per requester
   };
   std::vector<ngpu_dict *> parts;
-  std::vector<PartIO> io;
+  std::vector<std::unique_ptr<Requester>> req;
+  std::mutex req_mu;  // held only to find or add a requester
   bool replicated = false;
-  std::mutex io_mu;
 };
 
 // One HBM workspace and its cross-stream ordering state.  Every stage that
@@ -92,6 +103,7 @@ struct ngpu_ws_slot {
 
 struct ngpu_engine {
   std::atomic<int> refs{1};  // the creator + every open pack
+  uint64_t uid = 0;          // unique for the process's lifetime (node exchange channels)
   ngpu_config cfg{};
   int device = 0;
   hipStream_t stream = nullptr;

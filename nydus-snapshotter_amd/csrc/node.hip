@@ -12,9 +12,12 @@
 //
 // The exchange (the north star's digest-prefix all-to-all, in-process): the
 // requester packs its chunk digests (n x 32 B), every owner receives them over
-// xGMI with hipMemcpyPeerAsync on its own probe stream, probes the rows it
-// owns, and its hit array (n x 24 B) goes back the same way; the requester
-// merges the W arrays by owner.  Copies, not peer loads/stores from kernels:
+// xGMI with hipMemcpyPeerAsync, probes the rows it owns, and its hit array
+// (n x 24 B) goes back the same way; the requester merges the W arrays by
+// owner.  Every (owner, requester) pair has its own channel -- probe stream,
+// buffers and cached done event on the owner -- so W requesters exchange at
+// once with no shared lock, buffer or queue between them; an owner's W
+// probes run concurrently on its CUs.  Copies, not peer loads/stores from kernels:
 // the DMA engines keep coarse-grained HBM coherent across the GPUs, and the
 // payload is tiny (16K chunks of a 16 GiB layer = 512 KiB out, 384 KiB back
 // per owner), so the exchange is latency-bound, not link-bound.
@@ -50,6 +53,41 @@ static void free_io(ngpu_dict::PartIO &io, int device) {
   io.cap = 0;
 }
 
+// The requester's channel set: found (or added) under req_mu, which is held
+// for the lookup only -- the enqueue itself runs under the requester's own mu.
+static ngpu_dict::Requester *requester_of(ngpu_engine *e, ngpu_dict *d) {
+  std::lock_guard<std::mutex> g(d->req_mu);
+  for (auto &r : d->req)
+    if (r->engine_uid == e->uid) return r.get();
+  d->req.emplace_back(new ngpu_dict::Requester());
+  ngpu_dict::Requester *r = d->req.back().get();
+  r->engine_uid = e->uid;
+  r->device = e->device;
+  r->io.resize(d->parts.size());
+  return r;
+}
+
+// One owner's channel for this requester: stream, buffers for n rows and the
+// done event on the owner's device (created once, reused by every call).
+static int channel_ready(ngpu_engine *e, ngpu_dict::PartIO &io, int device, uint64_t n,
+                         uint64_t cap) {
+  DeviceGuard dg(device);
+  if (!io.stream && hipStreamCreateWithFlags(&io.stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(e, NGPU_EHIP, "node dict: probe stream on device %d", device);
+  if (!io.done && hipEventCreateWithFlags(&io.done, hipEventDisableTiming) != hipSuccess)
+    return fail(e, NGPU_EHIP, "node dict: exchange event on device %d", device);
+  if (n > io.cap) {
+    free_io(io, device);  // the stream's earlier exchanges finish first
+    if (hipMalloc((void **)&io.q, cap * 32) != hipSuccess ||
+        hipMalloc((void **)&io.h, cap * sizeof(ngpu_dict_hit)) != hipSuccess) {
+      free_io(io, device);
+      return fail(e, NGPU_ENOMEM, "node dict: exchange buffers on device %d", device);
+    }
+    io.cap = cap;
+  }
+  return 0;
+}
+
 int node_dict_hits(ngpu_engine *e, ngpu_dict *d, const uint8_t *digests, uint64_t stride,
                    uint64_t n, hipStream_t s, const ngpu_dict_hit **hits, ngpu_dict **replica) {
   *hits = nullptr;
@@ -82,49 +120,33 @@ int node_dict_hits(ngpu_engine *e, ngpu_dict *d, const uint8_t *digests, uint64_
   }
   *hits = ws.xhits;
   if (n == 0) return 0;
+  ngpu_dict::Requester *r = requester_of(e, d);
+  std::lock_guard<std::mutex> g(r->mu);  // this requester's channels only
+  if (!r->ready) HIP_TRY(e, hipEventCreateWithFlags(&r->ready, hipEventDisableTiming));
   launch_pack_digests(digests, stride, n, ws.xq, s);
-  hipEvent_t ready = nullptr;
-  HIP_TRY(e, hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-  HIP_TRY(e, hipEventRecord(ready, s));
-  std::vector<hipEvent_t> done(W, nullptr);
+  HIP_TRY(e, hipEventRecord(r->ready, s));
   int rc = 0;
-  {
-    std::lock_guard<std::mutex> g(d->io_mu);  // the parts' buffers are shared by requesters
-    for (uint32_t o = 0; o < W && !rc; ++o) {
-      ngpu_dict *p = d->parts[o];
-      ngpu_dict::PartIO &io = d->io[o];
-      DeviceGuard dg(p->device);
-      if (n > io.cap) {
-        free_io(io, p->device);
-        const uint64_t c = ws.cap_x;
-        if (hipMalloc((void **)&io.q, c * 32) != hipSuccess ||
-            hipMalloc((void **)&io.h, c * sizeof(ngpu_dict_hit)) != hipSuccess) {
-          free_io(io, p->device);
-          rc = fail(e, NGPU_ENOMEM, "node dict: exchange buffers on device %d", p->device);
-          break;
-        }
-        io.cap = c;
-      }
-      const bool ok =
-          hipStreamWaitEvent(io.stream, ready, 0) == hipSuccess &&
-          hipMemcpyPeerAsync(io.q, p->device, ws.xq, e->device, n * 32, io.stream) == hipSuccess;
-      if (ok) launch_dict_probe_owned(io.q, n, o, W, p->dev, io.h, io.stream);
-      if (!ok || hipGetLastError() != hipSuccess ||
-          hipMemcpyPeerAsync(ws.xparts + (uint64_t)o * n, e->device, io.h, p->device,
-                             n * sizeof(ngpu_dict_hit), io.stream) != hipSuccess ||
-          hipEventCreateWithFlags(&done[o], hipEventDisableTiming) != hipSuccess ||
-          hipEventRecord(done[o], io.stream) != hipSuccess)
-        rc = fail(e, NGPU_EHIP, "node dict: exchange with device %d failed", p->device);
-    }
+  uint32_t sent = 0;
+  for (uint32_t o = 0; o < W && !rc; ++o, ++sent) {
+    ngpu_dict *p = d->parts[o];
+    ngpu_dict::PartIO &io = r->io[o];
+    if ((rc = channel_ready(e, io, p->device, n, ws.cap_x))) break;
+    DeviceGuard dg(p->device);
+    const bool ok =
+        hipStreamWaitEvent(io.stream, r->ready, 0) == hipSuccess &&
+        hipMemcpyPeerAsync(io.q, p->device, ws.xq, e->device, n * 32, io.stream) == hipSuccess;
+    if (ok) launch_dict_probe_owned(io.q, n, o, W, p->dev, io.h, io.stream);
+    if (!ok || hipGetLastError() != hipSuccess ||
+        hipMemcpyPeerAsync(ws.xparts + (uint64_t)o * n, e->device, io.h, p->device,
+                           n * sizeof(ngpu_dict_hit), io.stream) != hipSuccess ||
+        hipEventRecord(io.done, io.stream) != hipSuccess)
+      rc = fail(e, NGPU_EHIP, "node dict: exchange with device %d failed", p->device);
   }
-  for (uint32_t o = 0; o < W; ++o) {
-    if (!done[o]) continue;
-    if (!rc && hipStreamWaitEvent(s, done[o], 0) != hipSuccess)
+  // the requester's stream waits for every owner it enqueued, even on failure,
+  // so no later stage reuses ws.xq / ws.xparts under a copy still in flight
+  for (uint32_t o = 0; o < sent && o < W; ++o)
+    if (r->io[o].done && hipStreamWaitEvent(s, r->io[o].done, 0) != hipSuccess && !rc)
       rc = fail(e, NGPU_EHIP, "node dict: cross-device wait failed");
-    DeviceGuard dg(d->parts[o]->device);
-    (void)hipEventDestroy(done[o]);
-  }
-  (void)hipEventDestroy(ready);
   if (rc) return rc;
   launch_hits_merge(ws.xq, n, W, ws.xparts, ws.xhits, s);
   HIP_TRY(e, hipGetLastError());
@@ -175,7 +197,6 @@ int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint
     }
   }
   int rc = 0;
-  d->io.resize(W);
   for (uint32_t o = 0; o < W && !rc; ++o) {
     ngpu_engine *e = node->eng[o];
     std::lock_guard<std::mutex> g(e->mu);
@@ -188,8 +209,6 @@ int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint
     p->dev.n_blobs = nb;
     p->place.clear();  // the global table (d->place) answers the writer
     d->parts.push_back(p);
-    if (hipStreamCreateWithFlags(&d->io[o].stream, hipStreamNonBlocking) != hipSuccess)
-      rc = fail(e, NGPU_EHIP, "node dict: probe stream");
   }
   if (rc) {
     dict_unref(d);
@@ -203,14 +222,21 @@ int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint
 
 // Called by dict_unref for a node dict.
 void node_dict_free(ngpu_dict *d) {
-  for (size_t o = 0; o < d->io.size(); ++o) {
-    const int dev = o < d->parts.size() ? d->parts[o]->device : d->device;
-    free_io(d->io[o], dev);
-    if (d->io[o].stream) {
+  for (auto &r : d->req) {
+    for (size_t o = 0; o < r->io.size() && o < d->parts.size(); ++o) {
+      ngpu_dict::PartIO &io = r->io[o];
+      const int dev = d->parts[o]->device;
+      free_io(io, dev);
       DeviceGuard g(dev);
-      (void)hipStreamDestroy(d->io[o].stream);
+      if (io.stream) (void)hipStreamDestroy(io.stream);
+      if (io.done) (void)hipEventDestroy(io.done);
+    }
+    if (r->ready) {
+      DeviceGuard g(r->device);
+      (void)hipEventDestroy(r->ready);
     }
   }
+  d->req.clear();
   for (ngpu_dict *p : d->parts) dict_unref(p);
   d->parts.clear();
 }

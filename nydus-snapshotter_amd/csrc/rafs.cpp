@@ -1077,7 +1077,7 @@ int read_v5(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
       if ((mode & S_IFMT) == S_IFREG && size) {
         if (q > n || (uint64_t)cc * 80 > n - q) return host_fail(NGPU_EFORMAT, "chunks out of bounds");
         nd.chunks.resize(cc);
-        memcpy(nd.chunks.data(), p + q, 80ull * cc);
+        if (cc) memcpy(nd.chunks.data(), p + q, 80ull * cc);
       }
       const bool sub = (mode & S_IFMT) == S_IFDIR;
       nodes->push_back(std::move(nd));

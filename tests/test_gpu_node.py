@@ -140,3 +140,59 @@ def test_node_packs_round_robin_write_dict_records(oracle, tars, tmp_path):
         assert info is not None
     finally:
         node.close()
+
+
+def test_node_four_requesters_at_once_vs_oracle(oracle):
+    """a 4-part node (device 0 listed 4x) with 4 requester
+    threads exchanging at the same time, each on its own engine and stream,
+    several rounds each: every (owner, requester) pair has its own channel, so
+    the results equal the oracle's with the whole dict however the calls
+    interleave.  ctypes drops the GIL for the C calls, so the enqueues overlap."""
+    import threading
+    import torch
+    W, rounds = 4, 3
+    rng = np.random.default_rng(77)
+    cs = 0x10000
+    layers = [[_layer(rng, 6 << 20, cs) for _ in range(rounds)] for _ in range(W)]
+    digs = [[oracle.digest_chunks(d, c.view(oracle.CHUNK_DTYPE), "blake3") for d, c in ls] for ls in layers]
+    recs = _dict_records(rng, np.concatenate([x for ds in digs for x in ds]),
+                         np.concatenate([c["length"] for ls in layers for _, c in ls]))
+    blobs = rafs.make_blob_table([f"{i:064x}" for i in range(7)], cs)
+    exp = [[_expect(oracle, digs[i][k], layers[i][k][1], recs) for k in range(rounds)] for i in range(W)]
+    node = nydus_gpu.Node([0] * W, chunk_size=cs)
+    try:
+        d = node.dict_create(recs, blobs, mode=nydus_gpu.NODE_DICT_PARTITION)
+        dev = [[(_to_dev(np.frombuffer(data, np.uint8)), _to_dev(ch)) for data, ch in ls] for ls in layers]
+        outs = [[torch.zeros(len(ch) * 64, dtype=torch.uint8, device="cuda") for _, ch in ls] for ls in layers]
+        torch.cuda.synchronize()
+        go, errs = threading.Barrier(W), []
+
+        def requester(i):
+            try:
+                s = torch.cuda.Stream()
+                go.wait(timeout=60)
+                for k in range(rounds):
+                    d_data, d_ch = dev[i][k]
+                    node.process_device(i, d, d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(),
+                                        len(layers[i][k][1]), outs[i][k].data_ptr(), stream=s.cuda_stream)
+                s.synchronize()
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errs.append((i, e))
+
+        ts = [threading.Thread(target=requester, args=(i,)) for i in range(W)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        assert not any(t.is_alive() for t in ts) and not errs, errs
+        for i in range(W):
+            for k in range(rounds):
+                got = outs[i][k].cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+                assert np.array_equal(got["digest"], digs[i][k]), (i, k)
+                for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+                    assert np.array_equal(got[f], exp[i][k][f]), (i, k, f)
+                assert (exp[i][k]["kind"] == 2).sum() > 0
+            node.engines[i].device_status()  # no sticky device error on any requester
+        d.release()
+    finally:
+        node.close()

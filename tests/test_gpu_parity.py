@@ -11,6 +11,8 @@ from nydus_gpu import rafs
 
 from conftest import kat_input
 
+import layers
+
 pytestmark = pytest.mark.gpu
 
 LANES = [1, 2, 4, 8, 16]

@@ -16,6 +16,7 @@ FsVersion says, and Unpack turns the stream back into the tar:
     digests, extended inodes / chunk-based files, root nid, prefetch table."""
 import hashlib
 import io
+import os
 import stat
 import struct
 import tarfile
@@ -301,3 +302,33 @@ def test_unpack_of_a_dict_layer_needs_the_dict_blob(oracle, golden_layers, tars)
     with pytest.raises(nydus_gpu.NgpuError) as e:
         nydus_gpu.unpack(out.getvalue())
     assert e.value.code == nydus_gpu.ENOTFOUND
+
+
+@pytest.mark.parametrize("fs", [5, 6])
+def test_bootstrap_reader_and_unpack_mutation_fuzz_asan(oracle, tmp_path, fs):
+    """read_rafs + ngpu_unpack on mutated bootstraps (tests/cpp/unpack_fuzz.cpp,
+    built with ASan/UBSan, host only): image.boot is untrusted input -- byte
+    flips and whole 16/32/64-bit fields (0, all-ones, powers of two, small
+    and random values) over the superblocks, tables, inodes and dirents, and
+    the odd flipped blob byte.  Every case must end in a return code: no
+    memory error, no UB, no runaway output.  Both outcomes must occur, so the
+    mutations reach past the superblock checks."""
+    import subprocess
+    from conftest import ROOT
+    exe = str(tmp_path / "unpack_fuzz")
+    csrc = os.path.join(ROOT, "nydus-snapshotter_amd", "csrc")
+    subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
+                           "-fno-sanitize-recover=all", "-I", os.path.join(ROOT, "include"),
+                           "-I", csrc, os.path.join(ROOT, "tests", "cpp", "unpack_fuzz.cpp"),
+                           os.path.join(csrc, "blob.cpp"), os.path.join(csrc, "rafs.cpp"), "-o", exe,
+                           "-lcrypto", "-ldl", "-lpthread"])
+    blob, *_ = _pack(oracle, layers.oci_upper_tar_go(3), cs=0x10000, fs=fs, comp="zstd")
+    sp = tmp_path / "s"
+    sp.write_bytes(blob)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:allocator_may_return_null=1")
+    out = subprocess.run([exe, str(sp), "800", str(17 + fs)], capture_output=True, text=True, env=env,
+                         timeout=600)
+    assert out.returncode == 0, (out.stdout[-500:], out.stderr[-3000:])
+    f = dict(kv.split("=") for kv in out.stdout.split())
+    assert int(f["read_ok"]) > 30 and int(f["unpack_ok"]) > 30, out.stdout
+    assert int(f["cases"]) - int(f["unpack_ok"]) > 30, out.stdout
