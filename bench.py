@@ -852,11 +852,33 @@ def node_bench(args):
                     e.device_status()
                     alone.append(float(np.mean([a.elapsed_time(b) for a, b in ev[5:]])))
                 e.set_dict(None)
+            # all W requesters' dedup stages at once (each engine on its own
+            # stream): the exchange under contention, host-timed from the first
+            # enqueue to the last stream's end
+            for i, p in enumerate(per):
+                node.engines[i].set_dict(d)
+            conc = []
+            for r in range(15):
+                for p in per:
+                    with torch.cuda.device(p["dev"]), torch.cuda.stream(p["stream"]):
+                        p["out"].view(torch.int32).view(p["n"], 16)[:, 8].fill_(nydus_gpu.DIGESTED)
+                sync()
+                t0 = time.perf_counter()
+                for i, p in enumerate(per):
+                    node.engines[i].dedup_layers_device(p["d_ch"].data_ptr(), p["n"], p["out"].data_ptr(),
+                                                        p["first"].data_ptr(), L, p["st"].data_ptr(),
+                                                        stream=p["stream"].cuda_stream)
+                sync()
+                conc.append((time.perf_counter() - t0) * 1e3)
+            for i, p in enumerate(per):
+                node.engines[i].device_status()
+                node.engines[i].set_dict(None)
             modes[name] = {"dict_build_s": round(build_s, 2), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
                            "value_gbs": round(total / elapsed / 1e9, 1),
                            "digest_ms": round(float(np.mean([t["digest_ms"] for t in tm])), 3),
                            "dedup_ms": round(float(np.mean([t["dedup_ms"] for t in tm])), 3),
                            "dedup_alone_ms": [round(a, 4) for a in alone],
+                           "dedup_all_requesters_at_once_ms": round(float(np.median(conc[3:])), 4),
                            "dict_hits": hits}
             d.release()
         ex = float(np.mean(modes["partition"]["dedup_alone_ms"])) - \
@@ -875,10 +897,14 @@ def node_bench(args):
                        "parallelism": f"node x{W} (ngpu_node_*, one process)"},
             "modes": modes,
             "exchange": {"dedup_alone_ms_partition_minus_replicate": round(ex, 4),
-                         "bytes_per_step": n_all * (32 + 24) * (W - 1) // W,
-                         "note": "per step every device sends its digests (32 B/chunk) to each owner "
-                                 "and gets 24-B hits back; on a one-GPU rehearsal the peer copies "
-                                 "stay in one HBM and the W engines share the GPU"},
+                         "all_requesters_at_once_ms_partition_minus_replicate": round(
+                             modes["partition"]["dedup_all_requesters_at_once_ms"]
+                             - modes["replicate"]["dedup_all_requesters_at_once_ms"], 4),
+                         "peer_bytes_per_step": n_all * (32 + 24) * (W - 1),
+                         "note": "per step every device sends its digests (32 B/chunk) to each of the "
+                                 "W-1 other owners and gets 24-B hits back from each; on a one-GPU "
+                                 "rehearsal the peer copies stay in one HBM and the W engines share "
+                                 "the GPU"},
         }
         print(json.dumps(line), flush=True)
     finally:
