@@ -561,16 +561,42 @@ int ngpu_unpack_entry(ngpu_read_at_fn ra, void *ctx, uint64_t size, const char *
  * blob travels in its stream. */
 int ngpu_unpack(ngpu_read_at_fn ra, void *ctx, uint64_t size, ngpu_write_fn w, void *wctx);
 
-/* converter.Merge's blob bookkeeping (convert_unix.go:560-666, tool.Merge
- * builder.go:220-294): merge per-layer bootstraps (the image.boot entries)
- * into one written to w.  A layer's own blob (any blob not in the chunk dict
- * bootstrap's blob table) is named layer_digests[l] (hex of Layer.Digest, the
- * bootstrap file name the reference passes to nydus-image merge); at most one
- * per layer.  *blob_ids_out (malloc'd, ngpu_free_host) = comma-separated blob
- * ids in first-appearance order (the output JSON's "Blobs"). */
+/* converter.Merge (convert_unix.go:560-666) -> tool.Merge (builder.go:220-294,
+ * `nydus-image merge --prefetch-policy fs [--chunk-dict] [--parent-bootstrap]`):
+ * per-layer bootstraps (the image.boot entries, lowest layer first) into the
+ * image's bootstrap, written to w in the layers' RAFS version (v5 or v6; all
+ * layers must share it and the chunk size).  The inode trees are overlaid
+ * with the OCI layer rules: an upper entry replaces the lower one of its path,
+ * directories merge, `.wh.<name>` removes <name> and its subtree from the
+ * layers below, `.wh..wh..opq` hides everything below its directory, and the
+ * whiteouts themselves are dropped.  Chunk records keep their placement; their
+ * blob indices point into the merged blob table.  A layer's own blob (any
+ * blob not in the chunk dict bootstrap's blob table) is named
+ * layer_digests[l] (hex of Layer.Digest, the bootstrap file name the
+ * reference passes to nydus-image merge); at most one per layer.
+ * *blob_ids_out (malloc'd, ngpu_free_host) = comma-separated blob ids in
+ * first-appearance order (the output JSON's "Blobs"). */
 int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
                const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
                uint64_t dict_size, ngpu_write_fn w, void *ctx, char **blob_ids_out);
+
+/* MergeOption fields beyond the chunk dict (types.go:92-133). */
+typedef struct ngpu_merge_options {
+  /* ParentBootstrapPath's contents (--parent-bootstrap): the lowest layer,
+   * its blobs keep their ids (any number of them); NULL = none */
+  const void *parent_bootstrap;
+  uint64_t parent_size;
+  /* PrefetchPatterns (the builder's stdin, builder.go:238-240, 269):
+   * newline-separated paths; NULL or "" = "/" */
+  const char *prefetch_patterns;
+} ngpu_merge_options;
+
+/* ngpu_merge with MergeOption's parent bootstrap and prefetch patterns
+ * (opt may be NULL: ngpu_merge). */
+int ngpu_merge_ex(const void *const *bootstraps, const uint64_t *sizes,
+                  const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
+                  uint64_t dict_size, const ngpu_merge_options *opt, ngpu_write_fn w, void *ctx,
+                  char **blob_ids_out);
 
 #ifdef __cplusplus
 }

@@ -1340,11 +1340,13 @@ int ngpu_unpack(ngpu_read_at_fn ra, void *ctx, uint64_t size, ngpu_write_fn w, v
   return rc;
 }
 
-int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
-               const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
-               uint64_t dict_size, ngpu_write_fn w, void *ctx, char **blob_ids_out) {
+int ngpu_merge_ex(const void *const *bootstraps, const uint64_t *sizes,
+                  const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
+                  uint64_t dict_size, const ngpu_merge_options *opt, ngpu_write_fn w, void *ctx,
+                  char **blob_ids_out) {
   const int rc = guarded([&]() -> int {
-    if ((n && (!bootstraps || !sizes)) || !blob_ids_out)
+    if ((n && (!bootstraps || !sizes)) || !blob_ids_out ||
+        (opt && opt->parent_size && !opt->parent_bootstrap))
       return host_fail(NGPU_EINVAL, "ngpu_merge: bad argument");
     *blob_ids_out = nullptr;
     std::vector<std::string> dict_ids;
@@ -1354,83 +1356,28 @@ int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
       if (rc) return rc;
       for (auto &b : d.blobs) dict_ids.push_back(blob_id_of(b));
     }
-    Bootstrap out;
-    std::vector<std::string> ids;
-    std::unordered_map<std::string, uint32_t> id_index;  // ids[] position of a blob id
-    // (digest, merged blob index) keys already in the merged table: a flat
-    // open-addressing table of positions in out.chunks (digests are uniform,
-    // so their first 8 bytes mixed with the blob index hash well).  A std::set
-    // of 36-B keys -- a node allocation and a tree walk per record -- took
-    // 0.6 s of C5's 1000-layer, 1M-record Merge.
-    uint64_t total = 0;
-    for (uint64_t l = 0; l < n; ++l) total += sizes[l] / sizeof(RafsV6ChunkInfo);
-    uint64_t cap = 1024;
-    while (cap < 2 * total) cap <<= 1;
-    std::vector<uint32_t> slot(cap, 0xFFFFFFFFu);
-    out.chunks.reserve((size_t)total);
-    auto key_hash = [](const RafsV6ChunkInfo &c) {
-      uint64_t a, b;
-      memcpy(&a, c.block_id, 8);
-      memcpy(&b, c.block_id + 8, 8);
-      return (a ^ (b * 0x9E3779B97F4A7C15ull)) + c.blob_index * 0xC2B2AE3D27D4EB4Full;
-    };
-    for (uint64_t l = 0; l < n; ++l) {
-      Bootstrap b;
-      int rc = parse_bootstrap((const uint8_t *)bootstraps[l], sizes[l], &b);
-      if (rc) return rc;
-      if (!out.chunk_size) {
-        out.chunk_size = b.chunk_size;
-        out.flags = b.flags;
-      }
-      std::vector<uint32_t> local(b.blobs.size());
-      int own = 0;
-      for (size_t i = 0; i < b.blobs.size(); ++i) {
-        std::string id = blob_id_of(b.blobs[i]);
-        // A layer's own (non-dict) blob is named after the layer: the digest of
-        // its whole nydus tar stream, which Merge receives as Layer.Digest and
-        // uses as the bootstrap file name (convert_unix.go:567-573, 595-599).
-        const bool is_dict = std::find(dict_ids.begin(), dict_ids.end(), id) != dict_ids.end();
-        if (!is_dict) {
-          if (++own > 1)
-            return host_fail(NGPU_EFORMAT, "layer %llu has more than one non-dict blob",
-                             (unsigned long long)l);
-          if (layer_digests && layer_digests[l] && layer_digests[l][0]) id = layer_digests[l];
-        }
-        auto it = id_index.find(id);
-        if (it == id_index.end()) {
-          id_index.emplace(id, (uint32_t)ids.size());
-          ids.push_back(id);
-          RafsV6BlobInfo nb = b.blobs[i];
-          memset(nb.blob_id, 0, sizeof nb.blob_id);
-          memcpy(nb.blob_id, id.data(), std::min<size_t>(id.size(), 64));
-          nb.blob_index = (uint32_t)out.blobs.size();
-          out.blobs.push_back(nb);
-          local[i] = nb.blob_index;
-        } else {
-          local[i] = it->second;
-        }
-      }
-      for (RafsV6ChunkInfo c : b.chunks) {
-        if (c.blob_index >= local.size()) return host_fail(NGPU_EFORMAT, "chunk blob index out of range");
-        c.blob_index = local[c.blob_index];
-        // layers packed against one chunk dict each carry the dict chunks they
-        // reuse: the merged table keeps one record per (digest, blob)
-        uint64_t h = key_hash(c) & (cap - 1);
-        bool dup = false;
-        for (; slot[h] != 0xFFFFFFFFu; h = (h + 1) & (cap - 1)) {
-          const RafsV6ChunkInfo &o = out.chunks[slot[h]];
-          if (o.blob_index == c.blob_index && memcmp(o.block_id, c.block_id, 32) == 0) {
-            dup = true;
-            break;
-          }
-        }
-        if (dup) continue;
-        slot[h] = (uint32_t)out.chunks.size();
-        out.chunks.push_back(c);
-      }
+    std::vector<MergeInput> in;
+    if (opt && opt->parent_bootstrap) {
+      MergeInput m;
+      m.p = (const uint8_t *)opt->parent_bootstrap;
+      m.n = opt->parent_size;
+      m.parent = true;
+      in.push_back(m);
     }
-    if (!out.chunk_size) out.chunk_size = 0x100000;
-    const std::vector<uint8_t> boot = write_bootstrap(out);
+    for (uint64_t l = 0; l < n; ++l) {
+      MergeInput m;
+      m.p = (const uint8_t *)bootstraps[l];
+      m.n = sizes[l];
+      // A layer's own (non-dict) blob is named after the layer: the digest of
+      // its whole nydus tar stream, which Merge receives as Layer.Digest and
+      // uses as the bootstrap file name (convert_unix.go:567-573, 595-599).
+      if (layer_digests && layer_digests[l]) m.own_name = layer_digests[l];
+      in.push_back(m);
+    }
+    std::vector<uint8_t> boot;
+    std::vector<std::string> ids;
+    const std::string pf = opt && opt->prefetch_patterns ? opt->prefetch_patterns : "";
+    if (int rc = merge_rafs(in, dict_ids, pf, &boot, &ids)) return rc;
     if (w && w(ctx, boot.data(), boot.size()) != 0) return host_fail(NGPU_EIO, "write failed");
     std::string s;
     for (size_t i = 0; i < ids.size(); ++i) s += (i ? "," : "") + ids[i];
@@ -1442,6 +1389,13 @@ int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
   });
   if (rc == NGPU_ENOMEM) host_fail(rc, "ngpu_merge: out of memory");
   return rc;
+}
+
+int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
+               const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
+               uint64_t dict_size, ngpu_write_fn w, void *ctx, char **blob_ids_out) {
+  return ngpu_merge_ex(bootstraps, sizes, layer_digests, n, dict_bootstrap, dict_size, nullptr, w,
+                       ctx, blob_ids_out);
 }
 
 }  // extern "C"

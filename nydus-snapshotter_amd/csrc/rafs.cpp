@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <array>
 #include <functional>
+#include <map>
 #include <unordered_map>
 
 namespace ngpu {
@@ -63,7 +64,7 @@ struct B3Out {
 
 void words(const uint8_t *p, uint32_t n, uint32_t w[16]) {
   uint8_t b[64] = {};
-  memcpy(b, p, n);
+  if (n) memcpy(b, p, n);
   for (int i = 0; i < 16; ++i) w[i] = (uint32_t)b[4 * i] | (uint32_t)b[4 * i + 1] << 8 |
                                       (uint32_t)b[4 * i + 2] << 16 | (uint32_t)b[4 * i + 3] << 24;
 }
@@ -927,7 +928,7 @@ struct V6Reader {
   }
 
   int walk(uint64_t nid, const std::string &path, std::vector<RafsNode> *nodes, uint32_t chunk_size,
-           int depth) {
+           int depth, RafsNode *root = nullptr) {
     if (depth > 4096) return host_fail(NGPU_EFORMAT, "directory tree too deep");
     RafsNode me;
     uint16_t lay;
@@ -935,6 +936,7 @@ struct V6Reader {
     uint32_t iu;
     if (int rc = inode(nid, &me, &lay, &body, &iu)) return rc;
     if (!is_dir(me.mode)) return host_fail(NGPU_EFORMAT, "nid %llu is not a directory", (unsigned long long)nid);
+    if (root) *root = me;
     std::string d;
     if (int rc = data(lay, iu, body, me.size, &d)) return rc;
     on_path[nid] = true;
@@ -1001,7 +1003,7 @@ struct V6Reader {
 };
 
 int read_v6(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
-            std::vector<RafsV6BlobInfo> *blobs) {
+            std::vector<RafsV6BlobInfo> *blobs, RafsNode *rootp) {
   Bootstrap b;
   if (int rc = parse_bootstrap(p, n, &b)) return rc;
   *blobs = b.blobs;
@@ -1012,11 +1014,11 @@ int read_v6(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
   V6Reader r{p, n, (uint64_t)meta * kBlk, {}, std::move(b.chunks), {}};
   for (size_t i = 0; i < r.table.size(); ++i)
     r.where.emplace((uint64_t)r.table[i].blob_index << 40 | (r.table[i].uncompressed_offset / kBlk), i);
-  return r.walk(root, "", nodes, b.chunk_size, 0);
+  return r.walk(root, "", nodes, b.chunk_size, 0, rootp);
 }
 
 int read_v5(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
-            std::vector<RafsV6BlobInfo> *blobs) {
+            std::vector<RafsV6BlobInfo> *blobs, RafsNode *root) {
   uint32_t dg, cs;
   std::vector<uint8_t> recs, bl;
   if (int rc = parse_v5_bootstrap(p, n, &dg, &cs, &recs, &bl)) return rc;
@@ -1088,24 +1090,37 @@ int read_v5(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
     }
     return 0;
   };
+  if (root) {  // the root's own record (inode 1)
+    const uint64_t o = rec_off(1);
+    uint32_t uid = 0, gid = 0, mode = 0, nsec = 0;
+    uint64_t mt = 0;
+    if (!o || !get(p, n, o + 48, &uid) || !get(p, n, o + 52, &gid) || !get(p, n, o + 60, &mode) ||
+        !get(p, n, o + 108, &nsec) || !get(p, n, o + 112, &mt))
+      return host_fail(NGPU_EFORMAT, "root inode out of bounds");
+    root->mode = mode;
+    root->uid = uid;
+    root->gid = gid;
+    root->mtime = (int64_t)mt;
+    root->mtime_ns = nsec;
+  }
   return walk(1, "", 0);
 }
 
 }  // namespace
 
 int read_rafs(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
-              std::vector<RafsV6BlobInfo> *blobs, uint32_t *fs_version) {
+              std::vector<RafsV6BlobInfo> *blobs, uint32_t *fs_version, RafsNode *root) {
   nodes->clear();
   uint32_t m5 = 0, m6 = 0;
   get(p, n, 0, &m5);
   get(p, n, kRafsV6SuperBlockOffset, &m6);
   if (m6 == kRafsV6Magic) {
     *fs_version = 6;
-    return read_v6(p, n, nodes, blobs);
+    return read_v6(p, n, nodes, blobs, root);
   }
   if (m5 == kRafsV5Magic) {
     *fs_version = 5;
-    return read_v5(p, n, nodes, blobs);
+    return read_v5(p, n, nodes, blobs, root);
   }
   return host_fail(NGPU_EFORMAT, "not a RAFS bootstrap");
 }
@@ -1229,6 +1244,244 @@ void tar_entry_header(std::vector<uint8_t> *out, const RafsNode &nd, char type,
   fmt_str(h + 345, 155, pre);
   finish_header(h);
   out->insert(out->end(), h, h + 512);
+}
+
+
+// ---- Merge ---------------------------------------------------------------------
+int merge_rafs(const std::vector<MergeInput> &layers, const std::vector<std::string> &dict_ids,
+               const std::string &prefetch, std::vector<uint8_t> *out, std::vector<std::string> *blob_ids) {
+  struct Entry {
+    RafsNode nd;  // chunk blob indices already in the merged blob table
+    uint32_t layer = 0;
+  };
+  std::map<std::string, Entry> tree;  // path -> entry; a prefix range is a subtree
+  RafsNode root;
+  root.mode = S_IFDIR | 0755;
+  RafsLayerInfo li;
+  li.prefetch = prefetch.empty() ? "/" : prefetch;
+  uint32_t fsv = 0, cs = 0;
+  uint64_t flags = 0;
+  std::unordered_map<std::string, uint32_t> id_index;
+  blob_ids->clear();
+  // (digest, merged blob) records already in the merged chunk table: flat
+  // open addressing over li.table positions
+  std::vector<uint32_t> slot(1024, 0xFFFFFFFFu);
+  auto key_hash = [](const RafsV6ChunkInfo &c) {
+    uint64_t a, b;
+    memcpy(&a, c.block_id, 8);
+    memcpy(&b, c.block_id + 8, 8);
+    return (a ^ (b * 0x9E3779B97F4A7C15ull)) + c.blob_index * 0xC2B2AE3D27D4EB4Full;
+  };
+  auto add_record = [&](const RafsV6ChunkInfo &c) {
+    if (2 * (li.table.size() + 1) > slot.size()) {  // grow and rehash
+      std::vector<uint32_t> ns(slot.size() * 2, 0xFFFFFFFFu);
+      for (uint32_t i = 0; i < li.table.size(); ++i) {
+        uint64_t h = key_hash(li.table[i]) & (ns.size() - 1);
+        while (ns[h] != 0xFFFFFFFFu) h = (h + 1) & (ns.size() - 1);
+        ns[h] = i;
+      }
+      slot.swap(ns);
+    }
+    uint64_t h = key_hash(c) & (slot.size() - 1);
+    for (; slot[h] != 0xFFFFFFFFu; h = (h + 1) & (slot.size() - 1)) {
+      const RafsV6ChunkInfo &o = li.table[slot[h]];
+      if (o.blob_index == c.blob_index && memcmp(o.block_id, c.block_id, 32) == 0) return;
+    }
+    slot[h] = (uint32_t)li.table.size();
+    li.table.push_back(c);
+  };
+  auto erase_below = [&](const std::string &pre) {  // every path starting with pre
+    for (auto it = tree.lower_bound(pre); it != tree.end() && it->first.compare(0, pre.size(), pre) == 0;)
+      it = tree.erase(it);
+  };
+  auto erase_subtree = [&](const std::string &path) {
+    tree.erase(path);
+    erase_below(path + "/");
+  };
+  for (size_t l = 0; l < layers.size(); ++l) {
+    const MergeInput &in = layers[l];
+    std::vector<RafsNode> nodes;
+    std::vector<RafsV6BlobInfo> blobs;
+    std::vector<RafsV6ChunkInfo> recs;  // the layer's chunk records (its chunk table)
+    RafsNode lroot;
+    bool has_tree = true;
+    uint32_t lv = 0, lcs = 0;
+    uint64_t lflags = 0;
+    uint32_t m5 = 0, meta = 0;
+    get(in.p, in.n, 0, &m5);
+    if (m5 == kRafsV5Magic) {
+      uint32_t dg;
+      std::vector<uint8_t> r5, b5;
+      if (int rc = parse_v5_bootstrap(in.p, in.n, &dg, &lcs, &r5, &b5)) return rc;
+      recs.resize(r5.size() / sizeof(RafsV6ChunkInfo));
+      if (!r5.empty()) memcpy(recs.data(), r5.data(), recs.size() * sizeof(RafsV6ChunkInfo));
+      if (!get(in.p, in.n, 16, &lflags)) return host_fail(NGPU_EFORMAT, "merge: truncated v5 super block");
+      lflags &= ~0x10ull;  // EXPLICIT_UID_GID: the v5 writer sets it again
+      if (int rc = read_rafs(in.p, in.n, &nodes, &blobs, &lv, &lroot)) return rc;
+    } else {
+      Bootstrap b;
+      if (int rc = parse_bootstrap(in.p, in.n, &b)) return rc;
+      lv = 6;
+      lcs = b.chunk_size;
+      lflags = b.flags;
+      recs = std::move(b.chunks);
+      if (!get(in.p, in.n, kRafsV6SuperBlockOffset + 40, &meta) || meta == 0) {
+        has_tree = false;  // chunk table only: no inode may sit on the super block
+        blobs = std::move(b.blobs);
+      } else if (int rc = read_rafs(in.p, in.n, &nodes, &blobs, &lv, &lroot)) {
+        return rc;
+      }
+    }
+    if (!fsv) {
+      fsv = lv;
+      cs = lcs;
+      flags = lflags;
+    } else if (fsv != lv) {
+      return host_fail(NGPU_EINVAL, "merge: layer %zu is RAFS v%u, layer 0 is v%u", l, lv, fsv);
+    } else if (cs != lcs) {
+      return host_fail(NGPU_EINVAL, "merge: layer %zu has chunk size 0x%x, layer 0 0x%x", l, lcs, cs);
+    }
+    // blob table: first appearance order; a layer's own blob renamed
+    std::vector<uint32_t> local(blobs.size());
+    int own = 0;
+    for (size_t i = 0; i < blobs.size(); ++i) {
+      std::string id = blob_id_of(blobs[i]);
+      const bool is_dict = std::find(dict_ids.begin(), dict_ids.end(), id) != dict_ids.end();
+      if (!is_dict && !in.parent) {
+        if (++own > 1) return host_fail(NGPU_EFORMAT, "layer %zu has more than one non-dict blob", l);
+        if (!in.own_name.empty()) id = in.own_name;
+      }
+      auto it = id_index.find(id);
+      if (it == id_index.end()) {
+        RafsV6BlobInfo nb = blobs[i];
+        memset(nb.blob_id, 0, sizeof nb.blob_id);
+        memcpy(nb.blob_id, id.data(), std::min<size_t>(id.size(), sizeof nb.blob_id));
+        nb.blob_index = (uint32_t)li.blobs.size();
+        it = id_index.emplace(id, nb.blob_index).first;
+        blob_ids->push_back(id);
+        li.blobs.push_back(nb);
+      }
+      local[i] = it->second;
+    }
+    auto remap = [&](RafsV6ChunkInfo &c) -> bool {
+      if (c.blob_index >= local.size()) return false;
+      c.blob_index = local[c.blob_index];
+      return true;
+    };
+    if (fsv == 6 || !has_tree) {
+      for (RafsV6ChunkInfo c : recs) {
+        if (!remap(c)) return host_fail(NGPU_EFORMAT, "merge: layer %zu: chunk blob index out of range", l);
+        add_record(c);
+      }
+    }
+    if (!has_tree) continue;
+    for (RafsNode &nd : nodes)
+      for (RafsV6ChunkInfo &c : nd.chunks) {
+        if (!remap(c)) return host_fail(NGPU_EFORMAT, "merge: %s: chunk blob index out of range", nd.path.c_str());
+        if (fsv == 5) add_record(c);
+      }
+    // whiteouts first, against the layers below only
+    auto base_of = [](const std::string &p) {
+      const size_t k = p.rfind('/');
+      return k == std::string::npos ? p : p.substr(k + 1);
+    };
+    auto dir_of = [](const std::string &p) {
+      const size_t k = p.rfind('/');
+      return k == std::string::npos ? std::string() : p.substr(0, k);
+    };
+    for (const RafsNode &nd : nodes) {
+      const std::string b = base_of(nd.path), d = dir_of(nd.path);
+      if (b == ".wh..wh..opq") {
+        if (d.empty()) tree.clear();
+        else erase_below(d + "/");
+      } else if (b.compare(0, 4, ".wh.") == 0 && b.size() > 4) {
+        erase_subtree(d.empty() ? b.substr(4) : d + "/" + b.substr(4));
+      }
+    }
+    for (RafsNode &nd : nodes) {
+      if (base_of(nd.path).compare(0, 4, ".wh.") == 0) continue;
+      auto it = tree.find(nd.path);
+      if (it != tree.end()) {
+        const bool both_dirs = is_dir(it->second.nd.mode) && is_dir(nd.mode);
+        if (!both_dirs) erase_subtree(nd.path);  // a replaced directory hides its lower entries
+      }
+      // a parent that a lower layer had as a non-directory is replaced by this
+      // layer's own directory entry, which comes first (depth-first order)
+      Entry &e = tree[nd.path];
+      e.nd = std::move(nd);
+      e.layer = (uint32_t)l;
+    }
+    root.mode = lroot.mode ? lroot.mode : root.mode;
+    root.uid = lroot.uid;
+    root.gid = lroot.gid;
+    root.mtime = lroot.mtime;
+    root.mtime_ns = lroot.mtime_ns;
+    root.xattrs = lroot.xattrs;
+  }
+  // the merged tree as tar entries; a hardlinked inode (same layer, same
+  // i_ino) is a file at its first path and hardlinks at the others
+  std::vector<TarEntry> entries;
+  TarEntry re;
+  re.type = '5';
+  re.mode = root.mode & 07777;
+  re.uid = root.uid;
+  re.gid = root.gid;
+  re.mtime = root.mtime;
+  re.mtime_ns = root.mtime_ns;
+  re.xattrs = root.xattrs;
+  entries.push_back(re);
+  std::map<std::pair<uint32_t, uint64_t>, std::string> first_path;
+  int64_t files = 0;
+  for (auto &kv : tree) {
+    const RafsNode &nd = kv.second.nd;
+    TarEntry e;
+    e.path = kv.first;
+    e.mode = nd.mode & 07777;
+    e.uid = nd.uid;
+    e.gid = nd.gid;
+    e.mtime = nd.mtime;
+    e.mtime_ns = nd.mtime_ns;
+    e.xattrs = nd.xattrs;
+    const uint32_t type = nd.mode & S_IFMT;
+    if (type != S_IFDIR && nd.nlink > 1) {
+      auto key = std::make_pair(kv.second.layer, nd.ino);
+      auto f = first_path.find(key);
+      if (f != first_path.end()) {
+        e.type = '1';
+        e.link = f->second;
+        entries.push_back(std::move(e));
+        continue;
+      }
+      first_path.emplace(key, kv.first);
+    }
+    switch (type) {
+      case S_IFDIR: e.type = '5'; break;
+      case S_IFLNK: e.type = '2'; e.link = nd.link; break;
+      case S_IFCHR: e.type = '3'; break;
+      case S_IFBLK: e.type = '4'; break;
+      case S_IFIFO: e.type = '6'; break;
+      case S_IFREG: e.type = '0'; break;
+      default: continue;  // sockets have no tar type
+    }
+    if (e.type == '3' || e.type == '4') {
+      e.devmajor = (nd.rdev >> 8) & 0xfff;
+      e.devminor = (nd.rdev & 0xff) | ((nd.rdev >> 12) & 0xfff00);
+    }
+    if (e.type == '0') {
+      e.size = nd.size;
+      e.file_index = files++;
+      for (const RafsV6ChunkInfo &c : nd.chunks) {
+        li.refs.push_back(c);
+        li.file_of.push_back((uint32_t)e.file_index);
+      }
+    }
+    entries.push_back(std::move(e));
+  }
+  li.fs_version = fsv ? fsv : 6;
+  li.chunk_size = cs ? cs : 0x100000;
+  li.flags = flags;
+  li.digester = (flags & 0x8) ? NGPU_DIGEST_SHA256 : NGPU_DIGEST_BLAKE3;
+  return write_rafs(entries, li, out);
 }
 
 }  // namespace ngpu

@@ -70,10 +70,31 @@ struct RafsNode {
 };
 
 // Every inode but the root, depth first in name order (the order a tar of the
-// tree lists them in); blobs of the blob table.  v5 or v6.  Untrusted input:
-// bounds-checked (NGPU_EFORMAT).
+// tree lists them in); blobs of the blob table; the root's own metadata in
+// *root when asked.  v5 or v6.  Untrusted input: bounds-checked (NGPU_EFORMAT).
 int read_rafs(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
-              std::vector<RafsV6BlobInfo> *blobs, uint32_t *fs_version);
+              std::vector<RafsV6BlobInfo> *blobs, uint32_t *fs_version, RafsNode *root = nullptr);
+
+// nydus-image merge (tool.Merge, builder.go:220-294; [nydus v2.3.0]
+// builder/src/merge.rs, VERIFY): per-layer bootstraps, lowest first, into one
+// bootstrap of the image.  The inode trees are overlaid with the OCI rules
+// (an upper entry replaces a lower one, directories merge, `.wh.<name>`
+// removes <name> and its subtree from the layers below, `.wh..wh..opq` hides
+// everything below its directory; whiteouts themselves do not survive), chunk
+// records keep their placement with blob indices remapped into the merged
+// blob table.  Blob ids: a parent bootstrap's and the chunk dict's keep
+// theirs; a layer's own (non-dict) blob -- at most one -- takes own_name when
+// given (the layer digest, convert_unix.go:567-573).  A v6 bootstrap with no
+// inode tree (meta_blkaddr 0: chunk table only) contributes its chunks and
+// blobs.  Layers must share the RAFS version and chunk size.
+struct MergeInput {
+  const uint8_t *p = nullptr;
+  uint64_t n = 0;
+  std::string own_name;  // "" = keep the blob id
+  bool parent = false;   // MergeOption.ParentBootstrapPath: blobs keep their ids, any number
+};
+int merge_rafs(const std::vector<MergeInput> &layers, const std::vector<std::string> &dict_ids,
+               const std::string &prefetch, std::vector<uint8_t> *out, std::vector<std::string> *blob_ids);
 
 // An OCI tar header (the Go archive/tar USTAR encoding; PAX records for what
 // USTAR cannot hold) for one node.  type: tar typeflag; link: linkname.

@@ -372,11 +372,25 @@ Error Merge(const std::vector<Layer> &layers, Writer &dest, const MergeOption &o
     sizes.push_back(boots[i].data.size());
     names.push_back(hexes[i].c_str());
   }
+  std::vector<uint8_t> parent;  // --parent-bootstrap (builder.go:235-237)
+  if (!opt.ParentBootstrapPath.empty()) {
+    FILE *f = fopen(opt.ParentBootstrapPath.c_str(), "rb");
+    if (!f) return err(NGPU_EIO, "open parent bootstrap " + opt.ParentBootstrapPath);
+    uint8_t buf[1 << 16];
+    size_t r;
+    while ((r = fread(buf, 1, sizeof buf, f)) > 0) parent.insert(parent.end(), buf, buf + r);
+    fclose(f);
+  }
+  ngpu_merge_options mo;
+  memset(&mo, 0, sizeof mo);
+  mo.parent_bootstrap = parent.empty() ? nullptr : parent.data();
+  mo.parent_size = parent.size();
+  mo.prefetch_patterns = opt.PrefetchPatterns.c_str();  // the builder's stdin (builder.go:238-240)
   BufferWriter merged;
   char *ids = nullptr;
-  const int rc = ngpu_merge(ptrs.data(), sizes.data(), names.data(), layers.size(),
-                            dict.empty() ? nullptr : dict.data(), dict.size(), write_trampoline,
-                            &merged, &ids);
+  const int rc = ngpu_merge_ex(ptrs.data(), sizes.data(), names.data(), layers.size(),
+                               dict.empty() ? nullptr : dict.data(), dict.size(), &mo,
+                               write_trampoline, &merged, &ids);
   if (rc) return err(rc, std::string("merge bootstrap: ") + ngpu_host_error());
   for (const char *s = ids; s && *s;) {
     const char *c = strchr(s, ',');

@@ -59,7 +59,7 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_pack_open", "ngpu_pack_write", "ngpu_pack_reserve", "ngpu_pack_commit",
            "ngpu_pack_close", "ngpu_pack_abort", "ngpu_dedup_layers_device",
            "ngpu_process_layers_device", "ngpu_host_error", "ngpu_blob_write",
-           "ngpu_pack_open_ex", "ngpu_pack_finish", "ngpu_unpack_entry", "ngpu_merge",
+           "ngpu_pack_open_ex", "ngpu_pack_finish", "ngpu_unpack_entry", "ngpu_merge", "ngpu_merge_ex",
            "ngpu_write_fd", "ngpu_dict_open", "ngpu_dict_create", "ngpu_dict_create_device",
            "ngpu_dict_retain", "ngpu_dict_release", "ngpu_dict_entries", "ngpu_set_dict",
            "ngpu_dict_probe", "ngpu_process_dict", "ngpu_process_dict_device",
@@ -204,6 +204,8 @@ def lib():
     L.ngpu_unpack.argtypes = [READ_AT_FN, vp, u64, WRITE_FN, vp]
     L.ngpu_merge.argtypes = [ctypes.POINTER(vp), pu64, ctypes.POINTER(ctypes.c_char_p), u64, vp,
                              u64, WRITE_FN, vp, ctypes.POINTER(vp)]
+    L.ngpu_merge_ex.argtypes = [ctypes.POINTER(vp), pu64, ctypes.POINTER(ctypes.c_char_p), u64, vp,
+                                u64, ctypes.POINTER(NgpuMergeOptions), WRITE_FN, vp, ctypes.POINTER(vp)]
     L.ngpu_dict_open.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
     L.ngpu_dict_create.argtypes = [vp, vp, u64, vp, u32, ctypes.POINTER(vp)]
     L.ngpu_dict_create_device.argtypes = [vp, vp, vp, vp, vp, vp, u64, u32, ctypes.POINTER(vp)]
@@ -415,9 +417,16 @@ def unpack(blob, dest=None):
     return None if dest is not None else b"".join(out)
 
 
-def merge(bootstraps, layer_digests, dict_bootstrap: bytes = None):
-    """ngpu_merge: per-layer bootstraps (bytes) + layer digest hex strings ->
-    (merged bootstrap bytes, [blob ids in first-appearance order])."""
+class NgpuMergeOptions(ctypes.Structure):
+    _fields_ = [("parent_bootstrap", ctypes.c_void_p), ("parent_size", ctypes.c_uint64),
+                ("prefetch_patterns", ctypes.c_char_p)]
+
+
+def merge(bootstraps, layer_digests, dict_bootstrap: bytes = None, parent_bootstrap: bytes = None,
+          prefetch_patterns: str = ""):
+    """ngpu_merge_ex: per-layer bootstraps (bytes, lowest first) + layer digest
+    hex strings -> (merged bootstrap bytes, [blob ids in first-appearance
+    order]).  The merged bootstrap holds the overlaid inode tree."""
     L = lib()
     bufs = [_buf(b) for b in bootstraps]
     n = len(bufs)
@@ -428,8 +437,12 @@ def merge(bootstraps, layer_digests, dict_bootstrap: bytes = None):
     out = []
     sink = _Sink(type("W", (), {"write": lambda _s, b: out.append(b)})())
     ids = ctypes.c_void_p()
-    rc = L.ngpu_merge(ptrs, sizes, digs, n, _ptr(dbuf) if dbuf is not None else None,
-                      dbuf.size if dbuf is not None else 0, sink.fn, None, ctypes.byref(ids))
+    pbuf = _buf(parent_bootstrap) if parent_bootstrap is not None else None
+    opt = NgpuMergeOptions(_ptr(pbuf) if pbuf is not None else None, pbuf.size if pbuf is not None else 0,
+                           (prefetch_patterns or "").encode())
+    rc = L.ngpu_merge_ex(ptrs, sizes, digs, n, _ptr(dbuf) if dbuf is not None else None,
+                         dbuf.size if dbuf is not None else 0, ctypes.byref(opt), sink.fn, None,
+                         ctypes.byref(ids))
     sink.reraise()
     _host_check(rc, "merge")
     try:

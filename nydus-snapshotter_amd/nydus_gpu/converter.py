@@ -68,6 +68,14 @@ class UnpackOption:
 
 
 @dataclass
+class File:
+    """utils.go:24-28: an extra file packToTar puts beside image.boot."""
+    Name: str
+    Reader: BinaryIO
+    Size: int
+
+
+@dataclass
 class Layer:
     """types.go:37-44: Digest of the whole nydus tar blob ("sha256:<hex>") and
     its bytes (ReaderAt)."""
@@ -297,11 +305,18 @@ def Merge(layers: Sequence[Layer], dest: BinaryIO, opt: MergeOption) -> List[str
             raise ConverterError(f"unpack all bootstraps: unpack nydus tar: {e}") from e
         boots.append(b.getvalue())
         digests.append(layer.Digest.split(":", 1)[-1])
-    dict_boot = None
+    dict_boot = parent = None
     if opt.ChunkDictPath:
         with open(opt.ChunkDictPath, "rb") as f:
             dict_boot = f.read()
-    merged, ids = merge(boots, digests, dict_boot)
+    if opt.ParentBootstrapPath:  # --parent-bootstrap (builder.go:235-237)
+        with open(opt.ParentBootstrapPath, "rb") as f:
+            parent = f.read()
+    try:
+        merged, ids = merge(boots, digests, dict_boot, parent_bootstrap=parent,
+                            prefetch_patterns=opt.PrefetchPatterns)
+    except NgpuError as e:
+        raise ConverterError(f"merge bootstrap: {e}") from e
     if opt.WithTar:  # packToTar (utils.go:92-160): image/ + image/image.boot
         out = io.BytesIO()
         with tarfile.open(fileobj=out, mode="w", format=tarfile.PAX_FORMAT) as tw:
@@ -311,12 +326,16 @@ def Merge(layers: Sequence[Layer], dest: BinaryIO, opt: MergeOption) -> List[str
             h = tarfile.TarInfo("image/" + EntryBootstrap)
             h.mode, h.size = 0o444, len(merged)
             tw.addfile(h, io.BytesIO(merged))
+            for f in opt.AppendFiles:  # File{Name, Reader, Size} (utils.go:24-28)
+                h = tarfile.TarInfo("image/" + f.Name)
+                h.mode, h.size = 0o444, f.Size
+                tw.addfile(h, f.Reader)
         dest.write(out.getvalue())
     else:
         dest.write(merged)
     return ["sha256:" + i for i in ids]
 
 
-__all__ = ["PackOption", "MergeOption", "UnpackOption", "Layer", "Pack", "Merge", "Unpack",
+__all__ = ["PackOption", "MergeOption", "UnpackOption", "Layer", "File", "Pack", "Merge", "Unpack",
            "UnpackEntry", "DetectFeatures", "ConverterError",
            "ErrNotFound", "NgpuError", "parse_chunk_size", "EntryBlob", "EntryBootstrap", "EntryTOC"]

@@ -5,7 +5,8 @@
 // flips, 16/32/64-bit fields set to 0 / all-ones / huge / small values at
 // aligned offsets, concentrated on the superblocks, inode and dirent areas)
 // and sometimes the blob data, then runs read_rafs on the mutated bootstrap
-// and ngpu_unpack on the whole mutated stream.  Every outcome must be a
+// ngpu_unpack on the whole mutated stream and ngpu_merge of the layer with
+// its mutated copy.  Every outcome must be a
 // return code (0 or NGPU_E*): no memory error, no crash, no unbounded output.
 // Prints "cases=<n> read_ok=<n> unpack_ok=<n> rc:<code>=<n> ...".
 // usage: unpack_fuzz STREAM CASES SEED
@@ -61,7 +62,7 @@ int main(int argc, char **argv) {
   const int cases = atoi(argv[2]);
   std::mt19937_64 rng(strtoull(argv[3], nullptr, 0));
   std::map<int, int> rcs;
-  int read_ok = 0, unpack_ok = 0;
+  int read_ok = 0, unpack_ok = 0, merge_ok = 0;
   for (int c = 0; c < cases; ++c) {
     std::vector<uint8_t> s = base;
     uint8_t *b = s.data() + boff;
@@ -99,8 +100,16 @@ int main(int argc, char **argv) {
     const int rc = ngpu_unpack(ra, &s, s.size(), wr, &o);
     ++rcs[rc];
     if (rc == 0) ++unpack_ok;
+    // Merge reads the same tree (overlaid over the unmutated layer)
+    const void *boots[2] = {boot.v.data(), b};
+    const uint64_t sizes[2] = {blen, blen};
+    const char *names[2] = {"", ""};
+    Out mo;
+    char *ids = nullptr;
+    if (ngpu_merge(boots, sizes, names, 2, nullptr, 0, wr, &mo, &ids) == 0) ++merge_ok;
+    free(ids);  // malloc'd (ngpu_free_host lives in the GPU library)
   }
-  printf("cases=%d read_ok=%d unpack_ok=%d", cases, read_ok, unpack_ok);
+  printf("cases=%d read_ok=%d unpack_ok=%d merge_ok=%d", cases, read_ok, unpack_ok, merge_ok);
   for (auto &kv : rcs) printf(" rc:%d=%d", kv.first, kv.second);
   printf("\n");
   return 0;

@@ -25,6 +25,7 @@ import numpy as np
 import pytest
 
 import nydus_gpu
+from nydus_gpu import rafs
 import rafs_fixtures as rf
 
 import layers
@@ -332,3 +333,171 @@ def test_bootstrap_reader_and_unpack_mutation_fuzz_asan(oracle, tmp_path, fs):
     f = dict(kv.split("=") for kv in out.stdout.split())
     assert int(f["read_ok"]) > 30 and int(f["unpack_ok"]) > 30, out.stdout
     assert int(f["cases"]) - int(f["unpack_ok"]) > 30, out.stdout
+
+
+# ---- Merge: the overlaid inode tree ------------------------------------------------
+
+def _tar(entries):
+    """entries: (name, kind, payload) with kind file/dir/symlink/hardlink;
+    PAX tar like buildOCIUpperTar's writer would produce."""
+    out = io.BytesIO()
+    with tarfile.open(fileobj=out, mode="w", format=tarfile.PAX_FORMAT) as tw:
+        for name, kind, payload, *mode in entries:
+            ti = tarfile.TarInfo(name)
+            ti.mtime = 1_700_000_000
+            if kind == "dir":
+                ti.type, ti.mode = tarfile.DIRTYPE, (mode[0] if mode else 0o755)
+                tw.addfile(ti)
+            elif kind == "symlink":
+                ti.type, ti.linkname = tarfile.SYMTYPE, payload
+                tw.addfile(ti)
+            elif kind == "hardlink":
+                ti.type, ti.linkname = tarfile.LNKTYPE, payload
+                tw.addfile(ti)
+            else:
+                ti.size, ti.mode = len(payload), 0o644
+                tw.addfile(ti, io.BytesIO(payload))
+    return out.getvalue()
+
+
+def _overlay(layer_entries):
+    """The OCI overlay of the layers, restated independently: path -> (kind,
+    payload, layer); whiteouts remove from the layers below and vanish."""
+    tree = {}
+    for li, ents in enumerate(layer_entries):
+        for name, kind, payload, *_ in ents:
+            base, d = name.rsplit("/", 1)[-1], name.rsplit("/", 1)[0] if "/" in name else ""
+            if base == ".wh..wh..opq":
+                for p in [p for p in tree if p.startswith(d + "/") or not d]:
+                    del tree[p]
+            elif base.startswith(".wh."):
+                gone = (d + "/" if d else "") + base[4:]
+                for p in [p for p in tree if p == gone or p.startswith(gone + "/")]:
+                    del tree[p]
+        for name, kind, payload, *_ in ents:
+            if name.rsplit("/", 1)[-1].startswith(".wh."):
+                continue
+            old = tree.get(name)
+            if old and not (old[0] == "dir" and kind == "dir"):
+                for p in [p for p in tree if p.startswith(name + "/")]:
+                    del tree[p]
+            if kind == "hardlink":
+                kind, payload = "file", tree[payload][1]
+            tree[name] = (kind, payload, li)
+    return tree
+
+
+def _v6_tree(boot):
+    """path -> (mode, inode dict) of every inode but the root."""
+    base = struct.unpack_from("<I", boot, 1024 + 40)[0] * 4096
+    root = struct.unpack_from("<H", boot, 1024 + 14)[0]
+    out, queue = {}, [("", root)]
+    while queue:
+        path, nid = queue.pop(0)
+        for name, cnid in rf._v6_dirents(boot, rf._v6_inode(boot, base, nid)):
+            if name in (b".", b".."):
+                continue
+            ci = rf._v6_inode(boot, base, cnid)
+            p = (path + "/" if path else "") + name.decode()
+            out[p] = ci
+            if stat.S_ISDIR(ci["mode"]):
+                queue.append((p, cnid))
+    return out
+
+
+MERGE_LAYERS = [
+    [("a", "dir", None), ("a/x", "file", bytes(range(256)) * 1000), ("a/y", "file", b"y0" * 5000),
+     ("b", "dir", None), ("b/z", "file", b"z" * 70000), ("c", "file", b"c" * 10),
+     ("d", "dir", None), ("d/e", "file", b"e" * 100), ("hl1", "file", b"h" * 90000),
+     ("hl2", "hardlink", "hl1"), ("link", "symlink", "a/x")],
+    [("a", "dir", None), ("a/.wh.x", "file", b""), ("a/y", "file", b"y1" * 7000),
+     ("b", "dir", None), ("b/.wh..wh..opq", "file", b""), ("b/new", "file", b"n" * 3000),
+     ("c", "dir", None), ("c/f", "file", b"f" * 66000), (".wh.d", "file", b""),
+     ("n", "file", b"nn" * 40000)],
+    [("a", "dir", None, 0o700), ("a/x", "file", b"x2" * 50000), ("g", "dir", None),
+     ("g/h1", "file", b"q" * 5000), ("g/h2", "hardlink", "g/h1")],
+]
+
+
+@pytest.mark.parametrize("fs", [5, 6])
+def test_merge_overlays_the_layer_trees(oracle, fs):
+    """ngpu_merge (nydus-image merge, builder.go:220-294) writes the image's
+    bootstrap with the overlaid inode tree: whiteouts and opaque directories
+    hide the layers below, an upper file replaces a lower one (a file replaces
+    a directory and vice versa), directories merge and take the upper
+    metadata, hardlinks share an inode; every file's chunk records are its
+    merged content's digests and point at the blob of the layer that supplied
+    it (the layer digest names that blob).  Checked against an independent
+    Python overlay of the same tars, through the fixture decoders."""
+    cs = 0x10000
+    boots = []
+    for ents in MERGE_LAYERS:
+        blob, *_ = _pack(oracle, _tar(ents), cs=cs, fs=fs, comp="lz4_block")
+        boots.append(_boot(blob))
+    names = ["11" * 32, "22" * 32, "33" * 32]
+    merged, ids = nydus_gpu.merge(boots, names, prefetch_patterns="/a/x\n/n")
+    assert ids == names
+    exp = _overlay(MERGE_LAYERS)
+    exp_files = {p: (v[1], v[2]) for p, v in exp.items() if v[0] == "file" and v[1]}
+
+    def digests(data):
+        n = (len(data) + cs - 1) // cs
+        ch = np.zeros(n, oracle.CHUNK_DTYPE)
+        ch["offset"] = np.arange(n) * cs
+        ch["length"] = [min(cs, len(data) - k * cs) for k in range(n)]
+        return oracle.digest_chunks(data, ch, "blake3")
+
+    if fs == 6:
+        tree = _v6_tree(merged)
+        assert set(tree) == set(exp), sorted(set(tree) ^ set(exp))
+        kinds = {stat.S_IFDIR: "dir", stat.S_IFREG: "file", stat.S_IFLNK: "symlink"}
+        assert {p: kinds[stat.S_IFMT(i["mode"])] for p, i in tree.items()} == {p: v[0] for p, v in exp.items()}
+        assert stat.S_IMODE(tree["a"]["mode"]) == 0o700  # the upper directory's metadata
+        assert tree["hl1"]["ino"] == tree["hl2"]["ino"] and tree["g/h1"]["ino"] == tree["g/h2"]["ino"]
+        files = {f[0].lstrip("/"): f for f in rf.read_v6_files(merged)}
+        assert set(files) == set(exp_files)
+        blob_ids = rafs.read_v6(merged)["blob_ids"]
+        for p, (data, layer) in exp_files.items():
+            recs = files[p][3]
+            assert files[p][2] == len(data)
+            assert np.array_equal(recs["block_id"], digests(data)), p
+            assert {blob_ids[b] for b in recs["blob_index"]} == {names[layer]}, p
+        # the prefetch table names the patterns' inodes (ext SB +40/+48)
+        po, ps = struct.unpack_from("<QI", merged, 1152 + 40)
+        nids = struct.unpack_from(f"<{ps // 4}I", merged, po)
+        assert len(nids) == 2
+    else:
+        v5 = rf.read_v5(merged)
+        assert v5["blob_ids"] == names
+        got = sorted((f[0], f[2]) for f in v5["files"])
+        assert got == sorted((p.rsplit("/", 1)[-1], len(d)) for p, (d, _) in exp_files.items())
+        by_name = {}
+        for f in v5["files"]:
+            by_name.setdefault(f[0], []).append(f)
+        for p, (data, layer) in exp_files.items():
+            cands = by_name[p.rsplit("/", 1)[-1]]
+            assert any(np.array_equal(f[4]["block_id"], digests(data)) and
+                       {v5["blob_ids"][b] for b in f[4]["blob_index"]} == {names[layer]} for f in cands), p
+    # merging is deterministic and a one-layer merge keeps the layer's tree
+    assert nydus_gpu.merge(boots, names, prefetch_patterns="/a/x\n/n")[0] == merged
+    one, _ = nydus_gpu.merge(boots[:1], names[:1])
+    if fs == 6:
+        assert set(_v6_tree(one)) == set(_overlay(MERGE_LAYERS[:1]))
+
+
+def test_merge_parent_bootstrap_and_version_mismatch(oracle):
+    """MergeOption.ParentBootstrapPath (--parent-bootstrap): the parent's tree
+    is the lowest layer and its blobs keep their ids; layers of different RAFS
+    versions are refused."""
+    cs = 0x10000
+    b6 = [_boot(_pack(oracle, _tar(e), cs=cs, fs=6, comp="none")[0]) for e in MERGE_LAYERS]
+    parent, pids = nydus_gpu.merge(b6[:2], ["11" * 32, "22" * 32])
+    merged, ids = nydus_gpu.merge(b6[2:], ["33" * 32], parent_bootstrap=parent)
+    assert ids == pids + ["33" * 32]
+    assert set(_v6_tree(merged)) == set(_overlay(MERGE_LAYERS))
+    full, _ = nydus_gpu.merge(b6, ["11" * 32, "22" * 32, "33" * 32])
+    assert merged == full
+    b5 = _boot(_pack(oracle, _tar(MERGE_LAYERS[0]), cs=cs, fs=5, comp="none")[0])
+    with pytest.raises(nydus_gpu.NgpuError) as e:
+        nydus_gpu.merge([b6[0], b5], ["11" * 32, "22" * 32])
+    assert e.value.code == nydus_gpu.EINVAL
