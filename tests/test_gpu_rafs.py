@@ -93,3 +93,27 @@ def test_dict_pack_lists_dict_records_and_unpack_names_the_dict_blob(golden_laye
     with pytest.raises(nydus_gpu.NgpuError) as e:
         nydus_gpu.unpack(blob)
     assert e.value.code == nydus_gpu.ENOTFOUND
+
+
+@pytest.mark.parametrize("fs", [5, 6])
+def test_gpu_packs_merge_like_cpu_packs(oracle, fs):
+    """Merge of GPU-packed layers (whiteouts, opaque dirs, replacements,
+    hardlinks: test_rafs.MERGE_LAYERS) is byte-identical to the Merge of the
+    same layers packed from the CPU oracle's decisions, whose overlay
+    test_rafs checks against an independent Python overlay."""
+    import test_rafs as tr
+    names = ["11" * 32, "22" * 32, "33" * 32]
+    eng = nydus_gpu.Engine(chunk_size=0x10000, fs_version=fs)
+    try:
+        gpu_boots = []
+        for ents in tr.MERGE_LAYERS:
+            blob, *_ = _gpu_pack(eng, tr._tar(ents), compressor="lz4_block")
+            gpu_boots.append(nydus_gpu.unpack_entry(blob, "image.boot")[0])
+    finally:
+        eng.close()
+    cpu_boots = [tr._boot(tr._pack(oracle, tr._tar(e), cs=0x10000, fs=fs, comp="lz4_block")[0])
+                 for e in tr.MERGE_LAYERS]
+    assert gpu_boots == cpu_boots
+    got, ids = nydus_gpu.merge(gpu_boots, names, prefetch_patterns="/a/x\n/n")
+    exp, _ = nydus_gpu.merge(cpu_boots, names, prefetch_patterns="/a/x\n/n")
+    assert ids == names and got == exp
