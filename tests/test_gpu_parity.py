@@ -1,6 +1,7 @@
 """GPU parity: the HIP path (through the C ABI) against the golden fixtures
 and the CPU oracle, bit-exact.  Run on a gfx950 box: pytest -m gpu."""
 import os
+import struct
 import tempfile
 
 import numpy as np
@@ -701,20 +702,26 @@ def test_multi_layer_dedup_matches_per_layer(oracle, L, fl):
         assert stats[l]["own_blob_index"] == (0xFFFFFFFF if own is None else own)
 
 
-def test_converter_testpack_flow(tars, oracle, tmp_path):
-    """tests/converter_test.go:420-528 through the converter mirror on the GPU:
-    buildChunkDict (Pack + Merge -> [sha256(dict Pack output)], :446-448),
-    Pack lower/upper against the dict bootstrap, Merge -> [dict blob,
-    sha256(upper Pack output)] (:513-519).  Every Pack output is byte-equal to
-    the host writer fed with the CPU oracle's decisions."""
+@pytest.mark.parametrize("fs", ["5", "6"])
+def test_converter_testpack_flow(tars, oracle, tmp_path, fs):
+    """tests/converter_test.go:459-528 (testPack for FsVersion "5" and "6")
+    through the converter mirror on the GPU: buildChunkDict (Pack + Merge ->
+    [sha256(dict Pack output)], :446-448), Pack lower/upper against the dict
+    bootstrap, Merge -> [dict blob, sha256(upper Pack output)] (:513-519), and
+    verify (:358-418) restated: the merged bootstrap reads back the expected
+    overlay file tree from the dict and upper blobs alone (the lower layer's
+    chunks are all in the dict: its blob is never read, :526).  v6 Pack
+    outputs are byte-equal to the host writer fed with the CPU oracle's
+    decisions."""
     import hashlib
     import io as _io
+    import rafs_fixtures as rf
     from nydus_gpu import converter as cv
     from test_blob import check_stream, cpu_stream
 
     def pack(tar, dict_path=""):
         out = _io.BytesIO()
-        w = cv.Pack(out, cv.PackOption(FsVersion="6", ChunkDictPath=dict_path))
+        w = cv.Pack(out, cv.PackOption(FsVersion=fs, ChunkDictPath=dict_path))
         for a in range(0, len(tar), 100_000):
             w.write(tar[a:a + 100_000])
         res = w.close()
@@ -723,7 +730,8 @@ def test_converter_testpack_flow(tars, oracle, tmp_path):
         return s, res
 
     dstream, dres = pack(tars["chunk_dict"])
-    assert dstream == cpu_stream(oracle, tars["chunk_dict"], 0x100000, "zstd")[0]
+    if fs == "6":
+        assert dstream == cpu_stream(oracle, tars["chunk_dict"], 0x100000, "zstd")[0]
     merged = _io.BytesIO()
     blobs = cv.Merge([cv.Layer(dres["digest"], dstream)], merged, cv.MergeOption())
     assert blobs == [dres["digest"]]
@@ -734,26 +742,35 @@ def test_converter_testpack_flow(tars, oracle, tmp_path):
     lstream, lres = pack(tars["oci_lower"], dict_path)
     ustream, ures = pack(tars["oci_upper"], dict_path)
     assert (lres["results"]["kind"] == nydus_gpu.DICT).all()
-    from nydus_gpu import inspect as ni
-    for tar, stream, res in ((tars["oci_lower"], lstream, lres), (tars["oci_upper"], ustream, ures)):
-        ref = cpu_stream(oracle, tar, 0x100000, "zstd", dict_boot=merged.getvalue())
-        assert stream == ref[0]
-        # the layer bootstrap lists its dict chunks under the dict blob, copied
-        # from the dict's records (check_stream compares them to the expectation)
-        check_stream(oracle, stream, res["info"], tar, res["chunks"], res["results"], "zstd",
-                     dict_boot=merged.getvalue())
-        a, b = tmp_path / "gpu.stream", tmp_path / "oracle.stream"
-        a.write_bytes(stream)
-        b.write_bytes(ref[0])
-        assert ni.main(["--diff", str(a), str(b)]) == 0
-        assert ni.canonical(ni.load_bootstrap(stream)) == ni.canonical(ni.load_bootstrap(ref[0]))
-    assert lres["info"]["dict_records"] == len({bytes(d) for d in lres["results"]["digest"]}) > 0
+    if fs == "6":
+        from nydus_gpu import inspect as ni
+        for tar, stream, res in ((tars["oci_lower"], lstream, lres), (tars["oci_upper"], ustream, ures)):
+            ref = cpu_stream(oracle, tar, 0x100000, "zstd", dict_boot=merged.getvalue())
+            assert stream == ref[0]
+            # the layer bootstrap lists its dict chunks under the dict blob, copied
+            # from the dict's records (check_stream compares them to the expectation)
+            check_stream(oracle, stream, res["info"], tar, res["chunks"], res["results"], "zstd",
+                         dict_boot=merged.getvalue())
+            a, b = tmp_path / "gpu.stream", tmp_path / "oracle.stream"
+            a.write_bytes(stream)
+            b.write_bytes(ref[0])
+            assert ni.main(["--diff", str(a), str(b)]) == 0
+            assert ni.canonical(ni.load_bootstrap(stream)) == ni.canonical(ni.load_bootstrap(ref[0]))
+        assert lres["info"]["dict_records"] == len({bytes(d) for d in lres["results"]["digest"]}) > 0
     out = _io.BytesIO()
     blobs = cv.Merge([cv.Layer(lres["digest"], lstream), cv.Layer(ures["digest"], ustream)], out,
                      cv.MergeOption(ChunkDictPath=dict_path))
     assert blobs == [dres["digest"], ures["digest"]]
-    b = rafs.read_v6(out.getvalue())
-    assert b["blob_ids"] == [dres["digest"][7:], ures["digest"][7:]]
+    boot = out.getvalue()
+    assert (struct.unpack_from("<I", boot, 0)[0] == 0x52414653) == (fs == "5")
+    if fs == "6":
+        assert rafs.read_v6(boot)["blob_ids"] == [dres["digest"][7:], ures["digest"][7:]]
+    # verify: the blob directory holds the dict and upper blobs only
+    blob_dir = {d["digest"][7:]: nydus_gpu.unpack_entry(st, "image.blob")[0]
+                for d, st in ((dres, dstream), (ures, ustream))}
+    view = rf.mount_view(boot, blob_dir)
+    from test_rafs import tar_overlay
+    assert view == tar_overlay([tars["oci_lower"], tars["oci_upper"]])
 
 
 @pytest.mark.parametrize("compressor", ["none", "zstd", "lz4_block"])

@@ -501,3 +501,71 @@ def test_merge_parent_bootstrap_and_version_mismatch(oracle):
     with pytest.raises(nydus_gpu.NgpuError) as e:
         nydus_gpu.merge([b6[0], b5], ["11" * 32, "22" * 32])
     assert e.value.code == nydus_gpu.EINVAL
+
+
+@pytest.mark.parametrize("fs", [5, 6])
+@pytest.mark.parametrize("comp", ["zstd", "lz4_block", "none"])
+def test_merged_image_reads_back_the_overlay(oracle, fs, comp):
+    """tests/converter_test.go's verify (:358-418) restated without nydusd:
+    the merged bootstrap, with each layer's image.blob under the blob id Merge
+    gave it (the layer digest), reads back every path of the overlaid tree
+    with its bytes (rafs_fixtures.mount_view: each chunk record's range of its
+    blob, decompressed)."""
+    cs = 0x10000
+    streams = [_pack(oracle, _tar(e), cs=cs, fs=fs, comp=comp)[0] for e in MERGE_LAYERS]
+    names = [hashlib.sha256(s).hexdigest() for s in streams]
+    merged, ids = nydus_gpu.merge([_boot(s) for s in streams], names)
+    assert ids == names
+    blobs = {n: nydus_gpu.unpack_entry(s, "image.blob")[0] for n, s in zip(names, streams)}
+    view = rf.mount_view(merged, blobs)
+    exp = _overlay(MERGE_LAYERS)
+    want = {p: (b"" if k == "dir" else d) for p, (k, d, _l) in exp.items() if k != "symlink"}
+    want["link"] = exp["a/x"][1]  # read through the symlink
+    assert view.keys() == want.keys()
+    for p in want:
+        assert view[p] == want[p], p
+
+
+def tar_overlay(tar_list):
+    """The expected file tree of TestPack's verify (converter_test.go:196-273,
+    expectedOverlayFileTree) from the layer tars: _overlay over their members;
+    path -> bytes ("" for directories)."""
+    layers_e = []
+    for t in tar_list:
+        ents = []
+        tf = tarfile.open(fileobj=io.BytesIO(t))
+        for m in tf:
+            name = m.name.strip("/")
+            if m.isdir():
+                ents.append((name, "dir", None))
+            elif m.issym():
+                ents.append((name, "symlink", m.linkname))
+            elif m.islnk():
+                ents.append((name, "hardlink", m.linkname.strip("/")))
+            elif m.isfile():
+                ents.append((name, "file", tf.extractfile(m).read()))
+        layers_e.append(ents)
+    return {p: (b"" if k == "dir" else d) for p, (k, d, _l) in _overlay(layers_e).items()}
+
+
+def test_testpack_verify_on_cpu_decisions(oracle, tars):
+    """TestPack (converter_test.go:459-528, FsVersion 6) on the CPU oracle's
+    decisions, through verify (:358-418) restated: the chunk dict built by
+    Pack + Merge, lower and upper packed against it (every lower chunk is a
+    DICT chunk), Merge -> [dict blob, upper blob], and the merged image reads
+    back buildOCIUpperTar's expected overlay from those two blobs alone."""
+    from test_blob import cpu_stream
+    cs = 0x100000
+    dstream = cpu_stream(oracle, tars["chunk_dict"], cs, "zstd")[0]
+    ddig = hashlib.sha256(dstream).hexdigest()
+    dict_boot, ids = nydus_gpu.merge([_boot(dstream)], [ddig])
+    assert ids == [ddig]
+    lstream, _, _, lres, _ = cpu_stream(oracle, tars["oci_lower"], cs, "zstd", dict_boot=dict_boot)
+    ustream = cpu_stream(oracle, tars["oci_upper"], cs, "zstd", dict_boot=dict_boot)[0]
+    assert (lres["kind"] == nydus_gpu.DICT).all()
+    ldig, udig = hashlib.sha256(lstream).hexdigest(), hashlib.sha256(ustream).hexdigest()
+    merged, ids = nydus_gpu.merge([_boot(lstream), _boot(ustream)], [ldig, udig], dict_boot)
+    assert ids == [ddig, udig]
+    blob_dir = {ddig: nydus_gpu.unpack_entry(dstream, "image.blob")[0],
+                udig: nydus_gpu.unpack_entry(ustream, "image.blob")[0]}
+    assert rf.mount_view(merged, blob_dir) == tar_overlay([tars["oci_lower"], tars["oci_upper"]])
