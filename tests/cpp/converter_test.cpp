@@ -127,6 +127,30 @@ int main(int argc, char **argv) {
               blobDigests[1] == upper.digest,
           "expectedBlobDigests := [chunkDictBlobDigest, upperNydusBlobDigest]");
   write_file(workDir + "/bootstrap", bootstrap.data);
+  write_file(workDir + "/" + upper.digest.substr(7), upper.data);
+
+  // testPack(t, "5"): the same flow with RAFS v5 bootstraps (a v5 chunk dict)
+  Packed dict5 = packLayer(dictTar, "", comp, "5");
+  write_file(workDir + "/" + dict5.digest.substr(7), dict5.data);
+  std::vector<Layer> d5{{dict5.digest, std::make_shared<BytesReaderAt>(dict5.data.data(), dict5.data.size())}};
+  BufferWriter dictBoot5;
+  REQUIRE_NOERR(Merge(d5, dictBoot5, MergeOption{}, &blobDigests));
+  const std::string dict5Path = workDir + "/dict-bootstrap-v5";
+  write_file(dict5Path, dictBoot5.data);
+  Packed lower5 = packLayer(lowerTar, dict5Path, comp, "5");
+  Packed upper5 = packLayer(upperTar, dict5Path, comp, "5");
+  REQUIRE(lower5.stats.DictChunks == lower5.stats.Chunks, "v5 lower layer is all chunk-dict hits");
+  std::vector<Layer> two5{
+      {lower5.digest, std::make_shared<BytesReaderAt>(lower5.data.data(), lower5.data.size())},
+      {upper5.digest, std::make_shared<BytesReaderAt>(upper5.data.data(), upper5.data.size())}};
+  BufferWriter bootstrap5;
+  MergeOption mo5;
+  mo5.ChunkDictPath = dict5Path;
+  REQUIRE_NOERR(Merge(two5, bootstrap5, mo5, &blobDigests));
+  REQUIRE(blobDigests.size() == 2 && blobDigests[0] == dict5.digest && blobDigests[1] == upper5.digest,
+          "v5: expectedBlobDigests := [chunkDictBlobDigest, upperNydusBlobDigest]");
+  write_file(workDir + "/bootstrap-v5", bootstrap5.data);
+  write_file(workDir + "/" + upper5.digest.substr(7), upper5.data);
 
   // UnpackEntry finds the bootstrap through the TOC; ErrNotFound otherwise
   BytesReaderAt ra(upper.data.data(), upper.data.size());
@@ -183,6 +207,8 @@ int main(int argc, char **argv) {
 
   printf("digest dict %s\ndigest lower %s\ndigest upper %s\n", dict.digest.c_str(),
          lower.digest.c_str(), upper.digest.c_str());
+  printf("digest5 dict %s\ndigest5 lower %s\ndigest5 upper %s\n", dict5.digest.c_str(),
+         lower5.digest.c_str(), upper5.digest.c_str());
   printf("PASS\n");
   return 0;
 }

@@ -919,6 +919,16 @@ def test_cpp_converter_mirror_testpack(tars, tmp_path, compressor):
     assert "sha256:" + hashlib.sha256(dict_file.read_bytes()).hexdigest() == dig["dict"]
     merged = rafs.read_v6((work / "bootstrap").read_bytes())
     assert merged["blob_ids"] == [dig["dict"][7:], dig["upper"][7:]]
+    # verify (converter_test.go:358-418) of both merged images from the dict
+    # and upper blobs the binary wrote
+    import rafs_fixtures as rf
+    from test_rafs import tar_overlay
+    dig5 = dict(line.split()[1:] for line in lines if line.startswith("digest5 "))
+    want = tar_overlay([tars["oci_lower"], tars["oci_upper"]])
+    for boot, dg in (("bootstrap", dig), ("bootstrap-v5", dig5)):
+        blob_dir = {dg[k][7:]: nydus_gpu.unpack_entry((work / dg[k][7:]).read_bytes(), "image.blob")[0]
+                    for k in ("dict", "upper")}
+        assert rf.mount_view((work / boot).read_bytes(), blob_dir) == want, boot
 
 
 def test_engine_thread_safety(oracle):
