@@ -916,6 +916,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--settle-s", type=float, default=1.0,
+                    help="after the W warmup steps, more untimed steps until the warm-up has "
+                         "lasted this long (GPU clock ramp); 0 = W steps only")
     ap.add_argument("--warmup", type=int, default=None,
                     help="untimed steps (default 20; 80 for the pool/dict workloads, whose setup -- "
                          "64 GiB of pool hashed, a 16M-200M entry dict built, GBs freed -- leaves "
@@ -1111,9 +1114,26 @@ def main():
             copy_done[k] = torch.cuda.Event()
             copy_done[k].record(copy_stream)
 
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         step()
     stream.synchronize()
+    # Clock settle: the GPU's clocks ramp over the first ~0.5 s of load (a
+    # rocprofv3 trace of 7 back-to-back C2 launches: 7.68, 6.06, 5.79, 5.66,
+    # 5.57, 5.55, 5.51 ms), longer than W short steps take.  Untimed steps
+    # continue until the warm-up has lasted args.settle_s; the line reports
+    # them apart from W ("warmup_settle").
+    settle = 0
+    # (a step with a collective -- the sharded dict's probe routing -- keeps
+    # every rank at the same step count, so it is never settled per rank)
+    while sdict is None and time.perf_counter() - tw < args.settle_s and settle < 10000:
+        step()
+        settle += 1
+        if settle % 8 == 0:
+            stream.synchronize()
+    stream.synchronize()
+    extra["warmup_settle"] = {"extra_untimed_steps": settle, "warm_s": round(time.perf_counter() - tw, 3),
+                              "settle_s": args.settle_s}
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
