@@ -580,6 +580,20 @@ int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
                const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
                uint64_t dict_size, ngpu_write_fn w, void *ctx, char **blob_ids_out);
 
+/* `nydus-image inspect`, restated (north_star: bootstraps "compared via
+ * nydus-image inspect"): one JSON object for a RAFS
+ * v5 or v6 bootstrap, written to w --
+ *   {"fs_version", "chunk_size", "flags", "blobs": [{"id", "chunk_count",
+ *    "compressed_size", "uncompressed_size"}], "inodes": [{"path" ("/" first,
+ *    then depth first in name order), "mode", "uid", "gid", "size", "nlink",
+ *    "ino", "rdev", "mtime", "mtime_ns", "link" (symlinks), "xattrs" (name ->
+ *    hex value), "chunks": [[digest hex, blob index, flags, compressed
+ *    offset, compressed size, uncompressed offset, uncompressed size, file
+ *    offset, chunk index], ...]}]}
+ * Bytes outside printable ASCII in names are \u00XX escapes (latin-1).
+ * Untrusted input: bounds-checked (NGPU_EFORMAT). */
+int ngpu_rafs_dump(const void *bootstrap, uint64_t size, ngpu_write_fn w, void *ctx);
+
 /* MergeOption fields beyond the chunk dict (types.go:92-133). */
 typedef struct ngpu_merge_options {
   /* ParentBootstrapPath's contents (--parent-bootstrap): the lowest layer,

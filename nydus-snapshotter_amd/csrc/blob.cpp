@@ -1391,6 +1391,18 @@ int ngpu_merge_ex(const void *const *bootstraps, const uint64_t *sizes,
   return rc;
 }
 
+int ngpu_rafs_dump(const void *bootstrap, uint64_t size, ngpu_write_fn w, void *ctx) {
+  const int rc = guarded([&]() -> int {
+    if (!bootstrap || !w) return host_fail(NGPU_EINVAL, "ngpu_rafs_dump: bad argument");
+    std::string js;
+    if (int rc = rafs_dump_json((const uint8_t *)bootstrap, size, &js)) return rc;
+    if (w(ctx, js.data(), js.size()) != 0) return host_fail(NGPU_EIO, "ngpu_rafs_dump: write failed");
+    return 0;
+  });
+  if (rc == NGPU_ENOMEM) host_fail(rc, "ngpu_rafs_dump: out of memory");
+  return rc;
+}
+
 int ngpu_merge(const void *const *bootstraps, const uint64_t *sizes,
                const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
                uint64_t dict_size, ngpu_write_fn w, void *ctx, char **blob_ids_out) {

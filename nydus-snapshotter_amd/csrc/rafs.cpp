@@ -1484,4 +1484,103 @@ int merge_rafs(const std::vector<MergeInput> &layers, const std::vector<std::str
   return write_rafs(entries, li, out);
 }
 
+
+// ---- inspect: a canonical dump of a bootstrap -------------------------------------
+namespace {
+void json_str(std::string *o, const std::string &s) {
+  static const char *hx = "0123456789abcdef";
+  o->push_back('"');
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') {
+      o->push_back('\\');
+      o->push_back((char)c);
+    } else if (c < 0x20 || c >= 0x7f) {  // control and non-ASCII bytes as \u00XX (latin-1)
+      *o += "\\u00";
+      o->push_back(hx[c >> 4]);
+      o->push_back(hx[c & 15]);
+    } else {
+      o->push_back((char)c);
+    }
+  }
+  o->push_back('"');
+}
+}  // namespace
+
+int rafs_dump_json(const uint8_t *p, uint64_t n, std::string *out) {
+  std::vector<RafsNode> nodes;
+  std::vector<RafsV6BlobInfo> blobs;
+  uint32_t fsv = 0;
+  RafsNode root;
+  if (int rc = read_rafs(p, n, &nodes, &blobs, &fsv, &root)) return rc;
+  uint64_t flags = 0;
+  uint32_t cs = 0;
+  if (fsv == 5) {
+    get(p, n, 12, &cs);
+    get(p, n, 16, &flags);
+  } else {
+    get(p, n, 1152, &flags);
+    get(p, n, 1152 + 20, &cs);
+  }
+  std::string &o = *out;
+  char b[256];
+  snprintf(b, sizeof b, "{\"fs_version\":%u,\"chunk_size\":%u,\"flags\":%llu,\"blobs\":[", fsv, cs,
+           (unsigned long long)flags);
+  o = b;
+  for (size_t i = 0; i < blobs.size(); ++i) {
+    o += i ? ",{\"id\":" : "{\"id\":";
+    json_str(&o, blob_id_of(blobs[i]));
+    snprintf(b, sizeof b, ",\"chunk_count\":%u,\"compressed_size\":%llu,\"uncompressed_size\":%llu}",
+             blobs[i].chunk_count, (unsigned long long)blobs[i].compressed_size,
+             (unsigned long long)blobs[i].uncompressed_size);
+    o += b;
+  }
+  o += "],\"inodes\":[";
+  root.path = "/";
+  auto one = [&](const RafsNode &nd, bool first) {
+    o += first ? "{\"path\":" : ",{\"path\":";
+    json_str(&o, nd.path == "/" ? nd.path : "/" + nd.path);
+    snprintf(b, sizeof b,
+             ",\"mode\":%u,\"uid\":%u,\"gid\":%u,\"size\":%llu,\"nlink\":%u,\"ino\":%llu,\"rdev\":%u,"
+             "\"mtime\":%lld,\"mtime_ns\":%u",
+             nd.mode, nd.uid, nd.gid, (unsigned long long)nd.size, nd.nlink, (unsigned long long)nd.ino,
+             nd.rdev, (long long)nd.mtime, nd.mtime_ns);
+    o += b;
+    if ((nd.mode & S_IFMT) == S_IFLNK) {
+      o += ",\"link\":";
+      json_str(&o, nd.link);
+    }
+    if (!nd.xattrs.empty()) {
+      o += ",\"xattrs\":{";
+      for (size_t k = 0; k < nd.xattrs.size(); ++k) {
+        if (k) o += ",";
+        json_str(&o, nd.xattrs[k].first);
+        o += ":";
+        json_str(&o, hex((const uint8_t *)nd.xattrs[k].second.data(), (int)nd.xattrs[k].second.size()));
+      }
+      o += "}";
+    }
+    if (!nd.chunks.empty()) {
+      // [digest, blob index, flags, compressed offset, compressed size,
+      //  uncompressed offset, uncompressed size, file offset, chunk index]
+      o += ",\"chunks\":[";
+      for (size_t k = 0; k < nd.chunks.size(); ++k) {
+        const RafsV6ChunkInfo &c = nd.chunks[k];
+        o += k ? ",[\"" : "[\"";
+        o += hex(c.block_id, 32);
+        snprintf(b, sizeof b, "\",%u,%u,%llu,%u,%llu,%u,%llu,%u]", c.blob_index, c.flags,
+                 (unsigned long long)c.compressed_offset, c.compressed_size,
+                 (unsigned long long)c.uncompressed_offset, c.uncompressed_size,
+                 (unsigned long long)c.file_offset, c.index);
+        o += b;
+      }
+      o += "]";
+    }
+    o += "}";
+  };
+  one(root, true);
+  for (const RafsNode &nd : nodes) one(nd, false);
+  o += "]}";
+  return 0;
+}
+
 }  // namespace ngpu

@@ -96,6 +96,9 @@ struct MergeInput {
 int merge_rafs(const std::vector<MergeInput> &layers, const std::vector<std::string> &dict_ids,
                const std::string &prefetch, std::vector<uint8_t> *out, std::vector<std::string> *blob_ids);
 
+// ngpu_rafs_dump's JSON (include/nydus_gpu.h) for a v5 or v6 bootstrap.
+int rafs_dump_json(const uint8_t *p, uint64_t n, std::string *out);
+
 // An OCI tar header (the Go archive/tar USTAR encoding; PAX records for what
 // USTAR cannot hold) for one node.  type: tar typeflag; link: linkname.
 void tar_entry_header(std::vector<uint8_t> *out, const RafsNode &nd, char type,

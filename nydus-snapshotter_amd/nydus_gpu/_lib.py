@@ -59,7 +59,7 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_pack_open", "ngpu_pack_write", "ngpu_pack_reserve", "ngpu_pack_commit",
            "ngpu_pack_close", "ngpu_pack_abort", "ngpu_dedup_layers_device",
            "ngpu_process_layers_device", "ngpu_host_error", "ngpu_blob_write",
-           "ngpu_pack_open_ex", "ngpu_pack_finish", "ngpu_unpack_entry", "ngpu_merge", "ngpu_merge_ex",
+           "ngpu_pack_open_ex", "ngpu_pack_finish", "ngpu_unpack_entry", "ngpu_merge", "ngpu_merge_ex", "ngpu_rafs_dump",
            "ngpu_write_fd", "ngpu_dict_open", "ngpu_dict_create", "ngpu_dict_create_device",
            "ngpu_dict_retain", "ngpu_dict_release", "ngpu_dict_entries", "ngpu_set_dict",
            "ngpu_dict_probe", "ngpu_process_dict", "ngpu_process_dict_device",
@@ -202,6 +202,7 @@ def lib():
                                    ctypes.POINTER(NgpuLayerStats), ctypes.POINTER(NgpuBlobInfo)]
     L.ngpu_unpack_entry.argtypes = [READ_AT_FN, vp, u64, ctypes.c_char_p, WRITE_FN, vp, vp]
     L.ngpu_unpack.argtypes = [READ_AT_FN, vp, u64, WRITE_FN, vp]
+    L.ngpu_rafs_dump.argtypes = [vp, u64, WRITE_FN, vp]
     L.ngpu_merge.argtypes = [ctypes.POINTER(vp), pu64, ctypes.POINTER(ctypes.c_char_p), u64, vp,
                              u64, WRITE_FN, vp, ctypes.POINTER(vp)]
     L.ngpu_merge_ex.argtypes = [ctypes.POINTER(vp), pu64, ctypes.POINTER(ctypes.c_char_p), u64, vp,
@@ -415,6 +416,20 @@ def unpack(blob, dest=None):
     sink.reraise()
     _host_check(rc, "unpack")
     return None if dest is not None else b"".join(out)
+
+
+def rafs_dump(bootstrap: bytes) -> dict:
+    """ngpu_rafs_dump: the canonical JSON view of a RAFS v5 / v6 bootstrap
+    (the `nydus-image inspect` restatement), parsed."""
+    import json
+    L = lib()
+    buf = _buf(bootstrap)
+    out = []
+    sink = _Sink(type("W", (), {"write": lambda _s, b: out.append(b)})())
+    rc = L.ngpu_rafs_dump(_ptr(buf), buf.size, sink.fn, None)
+    sink.reraise()
+    _host_check(rc, "rafs_dump")
+    return json.loads(b"".join(out).decode("ascii"))
 
 
 class NgpuMergeOptions(ctypes.Structure):

@@ -569,3 +569,76 @@ def test_testpack_verify_on_cpu_decisions(oracle, tars):
     blob_dir = {ddig: nydus_gpu.unpack_entry(dstream, "image.blob")[0],
                 udig: nydus_gpu.unpack_entry(ustream, "image.blob")[0]}
     assert rf.mount_view(merged, blob_dir) == tar_overlay([tars["oci_lower"], tars["oci_upper"]])
+
+
+@pytest.mark.parametrize("fs", [5, 6])
+def test_rafs_dump_reads_the_reference_fixtures(fs):
+    """ngpu_rafs_dump (the `nydus-image inspect` restatement) over nydus-image's
+    own bootstraps (pkg/filesystem/testdata): every regular file with its size
+    and chunk digests, as the independent fixture decoders read them; one
+    inode per dirent; v5 paths, v6 paths."""
+    from conftest import GOLDEN
+    name = "v5-bootstrap-file-size-736032.tar.gz" if fs == 5 else "v6-bootstrap-chunk-pos-438272.tar.gz"
+    boot = rf.boot_from_targz(os.path.join(GOLDEN, name))
+    d = nydus_gpu.rafs_dump(boot)
+    assert d["fs_version"] == fs and d["inodes"][0]["path"] == "/"
+    files = [i for i in d["inodes"] if stat.S_ISREG(i["mode"]) and i["size"]]
+    got = sorted((i["path"], i["size"], tuple(c[0] for c in i["chunks"])) for i in files)
+    if fs == 6:
+        exp = sorted((p, size, tuple(bytes(x).hex() for x in ch["block_id"]))
+                     for p, _ino, size, ch in rf.read_v6_files(boot))
+        assert got == exp
+        assert d["blobs"][0]["id"] == rafs.read_v6(boot)["blob_ids"][0]
+    else:
+        exp = sorted((n, size, tuple(bytes(x).hex() for x in ch["block_id"]))
+                     for n, _ino, size, _nl, ch in rf.read_v5(boot)["files"])
+        assert sorted((p.rsplit("/", 1)[-1], s, c) for p, s, c in got) == exp
+        assert [b["id"] for b in d["blobs"]] == rf.read_v5(boot)["blob_ids"]
+        walk = rf._v5_walk(boot)  # every record but the root, with its path
+        assert sorted(i["path"] for i in d["inodes"][1:]) == sorted("/" + w[0] for w in walk)
+    # paths are unique and every parent directory is listed before its children
+    paths = [i["path"] for i in d["inodes"]]
+    assert len(paths) == len(set(paths)) > 2000
+    seen = {"/"}
+    for p in paths[1:]:
+        assert (p.rsplit("/", 1)[0] or "/") in seen, p
+        seen.add(p)
+
+
+def test_rafs_dump_of_a_pack_matches_its_tar(oracle):
+    """The dump of a Pack's bootstrap lists the tar's entries with their
+    metadata (mode, uid/gid, size, symlink targets, hardlinks sharing ino)."""
+    tar = layers.alpine_like_tar()
+    for fs in (5, 6):
+        blob, *_ = _pack(oracle, tar, cs=0x10000, fs=fs)
+        d = nydus_gpu.rafs_dump(_boot(blob))
+        by = {i["path"]: i for i in d["inodes"]}
+        for m in tarfile.open(fileobj=io.BytesIO(tar)):
+            i = by["/" + m.name.strip("/")]
+            assert stat.S_IMODE(i["mode"]) == m.mode & 0o7777, m.name
+            assert (i["uid"], i["gid"]) == (m.uid, m.gid), m.name
+            if m.isfile() and not m.islnk():
+                assert i["size"] == m.size and len(i.get("chunks", [])) == -(-m.size // 0x10000)
+            if m.issym():
+                assert i["link"] == m.linkname
+            if m.islnk():
+                assert i["ino"] == by["/" + m.linkname.strip("/")]["ino"]
+
+
+def test_inspect_tree_and_v5_chunk_sets(oracle, tmp_path):
+    """nydus_gpu.inspect over v5 as well as v6: the chunk set of a v5 Pack is
+    its files' distinct chunk records, equal (as a set keyed by digest and
+    blob) to the v6 Pack's chunk table of the same tar; `--tree --diff` finds
+    no difference between a Pack and itself and names a changed path."""
+    from nydus_gpu import inspect as ni
+    tar = layers.alpine_like_tar()
+    b5 = _pack(oracle, tar, cs=0x10000, fs=5, comp="none")[0]
+    b6 = _pack(oracle, tar, cs=0x10000, fs=6, comp="none")[0]
+    c5, c6 = ni.canonical(ni.load_bootstrap(b5)), ni.canonical(ni.load_bootstrap(b6))
+    key = ("digest", "blob_id", "uncompressed_size", "compressed_size")
+    assert ni.diff(c5, c6, key) == [] and len(c5["chunks"]) > 50
+    (tmp_path / "a").write_bytes(b6)
+    assert ni.main(["--tree", "--diff", str(tmp_path / "a"), str(tmp_path / "a")]) == 0
+    other = layers.alpine_like_tar(seed=7)
+    (tmp_path / "b").write_bytes(_pack(oracle, other, cs=0x10000, fs=6, comp="none")[0])
+    assert ni.main(["--tree", "--diff", str(tmp_path / "a"), str(tmp_path / "b")]) == 1
