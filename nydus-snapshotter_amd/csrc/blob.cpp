@@ -1350,11 +1350,24 @@ int ngpu_merge_ex(const void *const *bootstraps, const uint64_t *sizes,
       return host_fail(NGPU_EINVAL, "ngpu_merge: bad argument");
     *blob_ids_out = nullptr;
     std::vector<std::string> dict_ids;
-    if (dict_bootstrap) {
-      Bootstrap d;
-      int rc = parse_bootstrap((const uint8_t *)dict_bootstrap, dict_size, &d, false);
-      if (rc) return rc;
-      for (auto &b : d.blobs) dict_ids.push_back(blob_id_of(b));
+    if (dict_bootstrap) {  // --chunk-dict bootstrap=P: RAFS v6 or v5
+      const uint8_t *dp = (const uint8_t *)dict_bootstrap;
+      uint32_t m5 = 0;
+      if (dict_size >= 4) memcpy(&m5, dp, 4);
+      if (m5 == kRafsV5Magic) {
+        uint32_t dg, cs;
+        std::vector<uint8_t> recs, blobs;
+        if (int rc = parse_v5_bootstrap(dp, dict_size, &dg, &cs, &recs, &blobs)) return rc;
+        for (size_t i = 0; i + sizeof(RafsV6BlobInfo) <= blobs.size(); i += sizeof(RafsV6BlobInfo)) {
+          RafsV6BlobInfo b;
+          memcpy(&b, blobs.data() + i, sizeof b);
+          dict_ids.push_back(blob_id_of(b));
+        }
+      } else {
+        Bootstrap d;
+        if (int rc = parse_bootstrap(dp, dict_size, &d, false)) return rc;
+        for (auto &b : d.blobs) dict_ids.push_back(blob_id_of(b));
+      }
     }
     std::vector<MergeInput> in;
     if (opt && opt->parent_bootstrap) {

@@ -642,3 +642,17 @@ def test_inspect_tree_and_v5_chunk_sets(oracle, tmp_path):
     other = layers.alpine_like_tar(seed=7)
     (tmp_path / "b").write_bytes(_pack(oracle, other, cs=0x10000, fs=6, comp="none")[0])
     assert ni.main(["--tree", "--diff", str(tmp_path / "a"), str(tmp_path / "b")]) == 1
+
+
+def test_merge_with_a_v5_chunk_dict(oracle):
+    """Merge with --chunk-dict naming a RAFS v5 dict bootstrap (testPack(t, "5")):
+    a blob the dict lists keeps its id, a layer's own blob takes the layer digest."""
+    cs = 0x10000
+    dstream = _pack(oracle, _tar(MERGE_LAYERS[0]), cs=cs, fs=5, comp="none")[0]
+    ddig = hashlib.sha256(dstream).hexdigest()
+    dict_boot, ids = nydus_gpu.merge([_boot(dstream)], [ddig])
+    assert ids == [ddig] and struct.unpack_from("<I", dict_boot, 0)[0] == 0x52414653
+    upper = _boot(_pack(oracle, _tar(MERGE_LAYERS[1]), cs=cs, fs=5, comp="none")[0])
+    merged, ids = nydus_gpu.merge([dict_boot, upper], ["aa" * 32, "bb" * 32], dict_boot)
+    assert ids == [ddig, "bb" * 32]
+    assert rf.read_v5(merged)["blob_ids"] == ids
