@@ -353,6 +353,10 @@ def probe_bench(torch, nydus_gpu, eng, dd, Q, build_s, reps=5):
             "ms": round(t * 1e3, 4), "gprobes_s": round(Q / t / 1e9, 2),
             "bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": round(PEAK_HBM / 1e9, 1),
             "unit": "GB/s", "frac": round(alg / t / PEAK_HBM, 4), "algorithmic_bytes": alg,
+            # SURVEY.md §8(d)'s per-probe model: 32-B query + one 128-B bucket
+            # line + 8-B result, + 32-B digest verify on a hit (~200 B)
+            "line_model": {"bytes": Q * (32 + 128 + 8) + nhit * 32,
+                           "frac": round((Q * (32 + 128 + 8) + nhit * 32) / t / PEAK_HBM, 4)},
             "build": {"kernel": "dict_insert", "entries": m, "s": round(build_s, 4),
                       "gentries_s": round(m / build_s / 1e9, 2)}}
 
