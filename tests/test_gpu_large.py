@@ -203,3 +203,66 @@ def test_c5_1000_layers_one_call(oracle):
     finally:
         del buf
         torch.cuda.empty_cache()
+
+
+def test_streaming_pack_of_a_9gib_file(oracle):
+    """One regular file larger than 8 GiB in a layer tar (its size needs the
+    GNU base-256 encoding: tarfile's GNU header) streamed through
+    converter.Pack's path (ngpu_pack_write in 64 MiB pieces): chunk k of the
+    file has file_offset k * S past 2^32 and 2^33, the tail chunk is partial,
+    a small file after it is chunked from the right stream offset, and the
+    sampled digests (first, around 4 GiB and 8 GiB, last, the small file)
+    equal the oracle's.  Pieces are a fixed random block xor its index, so
+    every chunk is distinct (all NEW)."""
+    import io
+    import tarfile
+    S, piece = MiB, 64 * MiB
+    size = 9 * (1 << 30) + 12345
+    base = np.random.default_rng(0x9B16).integers(0, 256, piece, dtype=np.uint8)
+
+    def chunk_of(p):  # piece p of the file's bytes
+        x = base.copy()
+        x.view(np.uint64)[::4096] ^= np.uint64(p + 1)  # distinct in every 1 MiB chunk
+        return x
+
+    hi = tarfile.TarInfo("big.bin")
+    hi.size, hi.mode, hi.mtime = size, 0o644, 1_700_000_000
+    head = hi.tobuf(format=tarfile.GNU_FORMAT)
+    assert head[124] & 0x80  # base-256 size field
+    small = bytes(range(256)) * 40
+    si = tarfile.TarInfo("after.txt")
+    si.size = len(small)
+    tail_tar = si.tobuf(format=tarfile.GNU_FORMAT) + small + bytes(-len(small) % 512) + bytes(1024)
+    eng = nydus_gpu.Engine(chunk_size=S)
+    want = {}
+    sample = {0, 1, 4095, 4096, 4097, 8191, 8192, 8193, size // S}
+    try:
+        w = eng.pack()
+        w.write(head)
+        done = 0
+        p = 0
+        while done < size:
+            data = chunk_of(p)[: min(piece, size - done)]
+            for k in range(done // S, (done + len(data) + S - 1) // S):
+                if k in sample:
+                    a = k * S - done
+                    want[k] = oracle.blake3(data[a:a + S].tobytes())
+            w.write(data)
+            done += len(data)
+            p += 1
+        w.write(bytes(-size % 512) + tail_tar)
+        ch, res, st = w.close()
+    finally:
+        eng.close()
+    n_big = -(-size // S)
+    assert len(ch) == n_big + 1 and st["chunks"] == n_big + 1
+    big = ch[:n_big]
+    assert (big["file_index"] == 0).all() and (ch["file_index"][-1] == 1)
+    assert np.array_equal(big["file_offset"], np.arange(n_big, dtype=np.uint64) * S)
+    assert int(big["file_offset"][-1]) > (1 << 33) and int(big["length"][-1]) == size - (n_big - 1) * S
+    assert np.array_equal(big["offset"], 512 + np.arange(n_big, dtype=np.uint64) * S)
+    assert int(ch["offset"][-1]) == 512 + -(-size // 512) * 512 + 512
+    for k, d in want.items():
+        assert res["digest"][k].tobytes() == d, k
+    assert res["digest"][-1].tobytes() == oracle.blake3(small)
+    assert (res["kind"] == nydus_gpu.NEW).all() and st["new_chunks"] == n_big + 1
