@@ -656,3 +656,49 @@ def test_merge_with_a_v5_chunk_dict(oracle):
     merged, ids = nydus_gpu.merge([dict_boot, upper], ["aa" * 32, "bb" * 32], dict_boot)
     assert ids == [ddig, "bb" * 32]
     assert rf.read_v5(merged)["blob_ids"] == ids
+
+
+@pytest.mark.parametrize("fs", [5, 6])
+def test_writer_reproduces_nydus_image_bootstraps(fs):
+    """The strongest pin of the RAFS writer (csrc/rafs.cpp): nydus-image's own
+    bootstraps (pkg/filesystem/testdata), read back into their inode trees and
+    chunk records and written again (a one-layer Merge: read_rafs ->
+    write_rafs), are byte-identical to the originals -- every inode position
+    (nid, including the free-tail placement of v6), field, dirent block,
+    chunk index (advise = chunk index), chunk table, blob and device table,
+    prefetch table and super block -- except for fields the tree cannot
+    determine:
+      * v6: EROFS s_blocks (super block +36): the fixture holds 4096, the
+        writer the bootstrap's own block count;
+      * v5: the size / blocks of 3 directories (bin, gconv 12288 B, info
+        20480 B): the fixture was built from a directory, and those are the
+        source file system's directory sizes (ext4 grows a directory by 4 KiB
+        blocks); a tar carries none, and the other 675 directories say 4096.
+    The v6 fixture's prefetch table names /bin (nid 142), the v5 one the root."""
+    from conftest import GOLDEN
+    name = "v5-bootstrap-file-size-736032.tar.gz" if fs == 5 else "v6-bootstrap-chunk-pos-438272.tar.gz"
+    fx = rf.boot_from_targz(os.path.join(GOLDEN, name))
+    ours, ids = nydus_gpu.merge([fx], [""], prefetch_patterns="/bin" if fs == 6 else "/")
+    assert len(ours) == len(fx)
+    diff = [i for i in range(len(fx)) if fx[i] != ours[i]]
+    if fs == 6:
+        assert diff == [1060, 1061]  # s_blocks
+        assert struct.unpack_from("<I", fx, 1060)[0] == 4096
+        assert struct.unpack_from("<I", ours, 1060)[0] == len(ours) // 4096
+    else:
+        walk = {p: mode for p, mode, *_ in rf._v5_walk(fx)}
+        (*_, ito, _pto, _bto, ient, _pe, _bs, _xb, _xbo) = struct.unpack_from(rf._SB, fx, 0)
+        offs = struct.unpack_from(f"<{ient}I", fx, ito)
+        big = set()
+        for o in offs:  # the records whose size (+64) / blocks (+72) differ
+            off = o << 3
+            if fx[off + 64:off + 80] != ours[off + 64:off + 80]:
+                big.add(fx[off + 128:off + 128 + struct.unpack_from("<H", fx, off + 100)[0]].decode())
+                assert stat.S_ISDIR(struct.unpack_from("<I", fx, off + 60)[0])
+                assert struct.unpack_from("<Q", fx, off + 64)[0] in (12288, 20480)
+                assert struct.unpack_from("<Q", ours, off + 64)[0] == 4096
+                for i in range(off + 64, off + 80):
+                    if fx[i] != ours[i]:
+                        diff.remove(i)
+        assert big == {"bin", "gconv", "info"} and diff == []
+        assert len(walk) == 3516
