@@ -934,13 +934,24 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     hdr("blob.digest", dig.size());
     toc_add("blob.digest", NGPU_COMPRESSOR_NONE, d_dig, d_off, dig.size(), dig.size());
     meta_entries = k;
-    // the own blob's record points at its chunk-info array (the v6 fixture's
-    // blob record: ci compressor, offset, compressed and uncompressed size)
-    uint8_t *bm = b.blobs[st.own_blob_index].meta;
-    memcpy(bm, &ci_algo, 4);
-    memcpy(bm + 4, &ci_off, 8);
-    memcpy(bm + 12, &ci_size, 8);
-    memcpy(bm + 20, &ci_len, 8);
+    // the own blob's record points at its chunk-info array.  RafsV6Blob after
+    // uncompressed_size ([nydus v2.3.0] rafs/src/metadata/layout/v6.rs,
+    // VERIFY; its offsets pinned by the reference v6 fixture's record, whose
+    // values are ci_compressor 1 (lz4_block), ci_offset = the blob's compressed
+    // size, 35,949 / 40,240 compressed / uncompressed bytes = 2,515 x 16-B v1
+    // entries): blob_toc_size u32 (0 with inlined meta), ci_compressor u32,
+    // ci_offset, ci_compressed_size, ci_uncompressed_size u64, then the ToC /
+    // meta digests and size (zero with inlined meta).  Its features are the
+    // blob's, as in the chunk-info header.
+    RafsV6BlobInfo &ob = b.blobs[st.own_blob_index];
+    uint8_t *bm = ob.meta;
+    const uint32_t toc_size = 0;
+    memcpy(bm, &toc_size, 4);
+    memcpy(bm + 4, &ci_algo, 4);
+    memcpy(bm + 8, &ci_off, 8);
+    memcpy(bm + 16, &ci_size, 8);
+    memcpy(bm + 24, &ci_len, 8);
+    ob.features = feat;
   }
   // image.boot: the inode tree of the layer (rafs.cpp), RAFS v5 or v6
   li.blobs = b.blobs;

@@ -192,6 +192,17 @@ def check_blob_meta(stream, info, recs):
     assert (ci[:, 2] == 0).all()
     assert dig == np.ascontiguousarray(r["block_id"]).tobytes()
     assert e_dig["uncompressed_digest"] == hashlib.sha256(dig).hexdigest()
+    # the own blob's RafsV6Blob record points at the same array, with the
+    # field offsets of the reference fixture's record (+104: blob_toc_size,
+    # ci_compressor, ci_offset, ci_compressed_size, ci_uncompressed_size)
+    boot = blob_ref.unpack_entry(stream, "image.boot")[0]
+    bto, bts = struct.unpack_from("<QI", boot, 1152 + 8)
+    own = [boot[bto + 256 * i: bto + 256 * (i + 1)] for i in range(bts // 256)
+           if struct.unpack_from("<Q", boot, bto + 256 * i + 104 + 8)[0]]
+    assert len(own) == 1
+    toc_size, rec_algo, rec_off, rec_cs, rec_us = struct.unpack_from("<IIQQQ", own[0], 104)
+    assert (toc_size, rec_algo, rec_off, rec_cs, rec_us) == (0, ci_algo, ci_off, ci_csize, ci_usize)
+    assert struct.unpack_from("<I", own[0], 84)[0] == feat  # the blob's features
 
 
 @pytest.mark.parametrize("compressor", ["none", "zstd", "lz4_block", ""])
