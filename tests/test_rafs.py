@@ -702,3 +702,88 @@ def test_writer_reproduces_nydus_image_bootstraps(fs):
                         diff.remove(i)
         assert big == {"bin", "gconv", "info"} and diff == []
         assert len(walk) == 3516
+
+
+def _tar_of_tree(dump):
+    """A PAX tar of a bootstrap's inode tree (ngpu_rafs_dump), depth first as
+    listed: directories, symlinks, devices, fifos, xattrs, hardlinks as '1'
+    entries to their first path, regular files zero-filled to their size."""
+    out, first = io.BytesIO(), {}
+    with tarfile.open(fileobj=out, mode="w", format=tarfile.PAX_FORMAT) as tw:
+        for i in dump["inodes"]:
+            p = i["path"].lstrip("/") or "."
+            ti = tarfile.TarInfo(p)
+            m = i["mode"]
+            ti.mode, ti.uid, ti.gid, ti.mtime = stat.S_IMODE(m), i["uid"], i["gid"], i["mtime"]
+            if "xattrs" in i:
+                ti.pax_headers = {"SCHILY.xattr." + k: bytes.fromhex(v).decode("latin-1")
+                                  for k, v in i["xattrs"].items()}
+            data = None
+            if stat.S_ISDIR(m):
+                ti.type = tarfile.DIRTYPE
+            elif stat.S_ISLNK(m):
+                ti.type, ti.linkname = tarfile.SYMTYPE, i["link"]
+            elif stat.S_ISREG(m) and i["nlink"] > 1 and i["ino"] in first:
+                ti.type, ti.linkname = tarfile.LNKTYPE, first[i["ino"]]
+            elif stat.S_ISREG(m):
+                first[i["ino"]] = p
+                ti.size, data = i["size"], io.BytesIO(bytes(i["size"]))
+            elif stat.S_ISCHR(m) or stat.S_ISBLK(m):
+                ti.type = tarfile.CHRTYPE if stat.S_ISCHR(m) else tarfile.BLKTYPE
+                r = i["rdev"]
+                ti.devmajor, ti.devminor = (r >> 8) & 0xfff, (r & 0xff) | ((r >> 12) & 0xfff00)
+            elif stat.S_ISFIFO(m):
+                ti.type = tarfile.FIFOTYPE
+            tw.addfile(ti, data)
+    return out.getvalue()
+
+
+@pytest.mark.parametrize("fs", [5, 6])
+def test_pack_of_the_fixture_tree_reproduces_its_layout(oracle, fs):
+    """tar-rafs end to end against nydus-image's own layout: the reference
+    fixture's inode tree written as a tar (hardlinks as '1' entries, the files
+    zero-filled, so only the chunk digests differ) and packed (CPU decisions,
+    the product writer) gives a bootstrap with every inode at the fixture's
+    position (v6 nid / v5 inode-table record) and every inode field equal --
+    the tar walk, implicit directories, hardlinks, name order and placement
+    as nydus-image builds them."""
+    from conftest import GOLDEN
+    name = "v5-bootstrap-file-size-736032.tar.gz" if fs == 5 else "v6-bootstrap-chunk-pos-438272.tar.gz"
+    fx = rf.boot_from_targz(os.path.join(GOLDEN, name))
+    want = nydus_gpu.rafs_dump(fx)
+    blob, *_ = _pack(oracle, _tar_of_tree(want), cs=want["chunk_size"], fs=fs, comp="none",
+                     prefetch="/bin" if fs == 6 else "/")
+    boot = _boot(blob)
+    got = nydus_gpu.rafs_dump(boot)
+    assert [i["path"] for i in got["inodes"]] == [i["path"] for i in want["inodes"]]
+    for a, b in zip(want["inodes"], got["inodes"]):
+        a, b = dict(a), dict(b)
+        ca, cb = a.pop("chunks", []), b.pop("chunks", [])
+        assert a == b, a["path"]
+        assert len(ca) == len(cb), a["path"]
+    if fs == 6:
+        assert rf.read_v6_files(fx) and {p: n for p, n in _v6_nids(fx).items()} == _v6_nids(boot)
+    else:
+        assert [w[0] for w in rf._v5_walk(fx)] == [w[0] for w in rf._v5_walk(boot)]
+        ito_a, n_a = struct.unpack_from("<Q", fx, 32)[0], struct.unpack_from("<I", fx, 56)[0]
+        ito_b, n_b = struct.unpack_from("<Q", boot, 32)[0], struct.unpack_from("<I", boot, 56)[0]
+        assert n_a == n_b
+        names = lambda b, ito, n: [b[(o << 3) + 128:(o << 3) + 128 + struct.unpack_from("<H", b, (o << 3) + 100)[0]]
+                                   for o in struct.unpack_from(f"<{n}I", b, ito)]
+        assert names(fx, ito_a, n_a) == names(boot, ito_b, n_b)  # inode-table (number) order
+
+
+def _v6_nids(boot):
+    root = struct.unpack_from("<H", boot, 1024 + 14)[0]
+    base = struct.unpack_from("<I", boot, 1024 + 40)[0] * 4096
+    out, queue = {}, [("", root)]
+    while queue:
+        path, nid = queue.pop(0)
+        for nm, cn in rf._v6_dirents(boot, rf._v6_inode(boot, base, nid)):
+            if nm in (b".", b".."):
+                continue
+            p = path + "/" + nm.decode(errors="replace")
+            out[p] = cn
+            if stat.S_ISDIR(rf._v6_inode(boot, base, cn)["mode"]):
+                queue.append((p, cn))
+    return out
