@@ -892,15 +892,19 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     uint8_t ci_dig[32];
     sha256(ci_raw, ci_len, ci_dig);
     std::vector<uint8_t> z;
+    // The array is compressed with the blob's own compressor when that shrinks
+    // it, as the reference v6 fixture's lz4_block blob has its array
+    // lz4_block-compressed (ci_compressor 1: 40,240 -> 35,949 B); the TOC
+    // entry carries the same compressor (the Go reader opens zstd / none only,
+    // convert_unix.go:219-276: an lz4_block blob's blob.meta is for nydusd).
     uint32_t ci_algo = 0, ci_flag = NGPU_COMPRESSOR_NONE;  // compress::Algorithm None = 0
     if (kind == NGPU_COMPRESSOR_ZSTD || kind == NGPU_COMPRESSOR_LZ4_BLOCK) {
-      z.resize(compress_bound(NGPU_COMPRESSOR_ZSTD, (uint32_t)ci_len));
-      const uint64_t zl = compress_one(NGPU_COMPRESSOR_ZSTD, 0, ci_raw, (uint32_t)ci_len, z.data(),
-                                       z.size());
-      if (zl) {  // the ci array is stored zstd-compressed when that shrinks it
+      z.resize(compress_bound(kind, (uint32_t)ci_len));
+      const uint64_t zl = compress_one(kind, 0, ci_raw, (uint32_t)ci_len, z.data(), z.size());
+      if (zl) {
         z.resize(zl);
-        ci_algo = 3;  // compress::Algorithm::Zstd
-        ci_flag = NGPU_COMPRESSOR_ZSTD;
+        ci_algo = kind == NGPU_COMPRESSOR_ZSTD ? 3 : 1;  // compress::Algorithm Zstd / Lz4Block
+        ci_flag = kind;
       }
     }
     const uint8_t *ci_data = ci_flag == NGPU_COMPRESSOR_NONE ? ci_raw : z.data();

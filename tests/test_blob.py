@@ -171,17 +171,28 @@ def check_blob_meta(stream, info, recs):
                 blob_ref.unpack_entry(stream, name)
         return
     assert info["meta_entries"] == len(r)
-    meta, e_meta = blob_ref.unpack_entry(stream, "blob.meta")
+    toff, tsize = blob_ref.seek_file_by_tar_header(stream, blob_ref.ENTRY_TOC)
+    e_meta = next(e for e in blob_ref.parse_toc(stream[toff:toff + tsize]) if e["name"] == "blob.meta")
+    if e_meta["flags"] & 0xF == blob_ref.COMPRESSOR_LZ4_BLOCK:
+        # the array of an lz4_block blob is lz4_block too (the fixture's
+        # ci_compressor 1); the Go reader opens zstd / none entries only
+        with pytest.raises(ValueError, match="unsupported compressor"):
+            blob_ref.unpack_entry(stream, "blob.meta")
+        raw = stream[e_meta["compressed_offset"]:e_meta["compressed_offset"] + e_meta["compressed_size"]]
+        meta = blob_ref.lz4_block_decompress(raw, e_meta["uncompressed_size"])
+    else:
+        meta, e_meta = blob_ref.unpack_entry(stream, "blob.meta")
+        assert meta == nydus_gpu.unpack_entry(stream, "blob.meta")[0]
     hdr, e_hdr = blob_ref.unpack_entry(stream, "blob.meta.header")
     dig, e_dig = blob_ref.unpack_entry(stream, "blob.digest")
-    assert meta == nydus_gpu.unpack_entry(stream, "blob.meta")[0]
     assert len(hdr) == 4096 and e_hdr["compressed_offset"] == e_meta["compressed_offset"] + e_meta["compressed_size"]
     magic, feat, ci_algo, n, ci_off, ci_csize, ci_usize = struct.unpack_from("<IIIIQQQ", hdr, 0)
     assert magic == BLOB_CCT_MAGIC == struct.unpack_from("<I", hdr, 4088)[0]
     assert feat & 0x4 and feat & 0x20  # CHUNK_INFO_V2, INLINED_CHUNK_DIGEST
     assert n == len(r) and ci_usize == len(meta) == 24 * len(r)
     assert ci_off == e_meta["compressed_offset"] and ci_csize == e_meta["compressed_size"]
-    assert ci_algo == (3 if e_meta["flags"] & 0xF == 0x2 else 0)
+    assert ci_algo == {0x1: 0, 0x2: 3, 0x4: 1}[e_meta["flags"] & 0xF]
+    assert e_meta["uncompressed_digest"] == hashlib.sha256(meta).hexdigest()
     ci = np.frombuffer(meta, "<u8").reshape(-1, 3)
     u, c = ci[:, 0], ci[:, 1]
     assert np.array_equal((u & 0xFFFFFFFF) << 12, r["uncompressed_offset"])
