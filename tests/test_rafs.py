@@ -787,3 +787,18 @@ def _v6_nids(boot):
             if stat.S_ISDIR(rf._v6_inode(boot, base, cn)["mode"]):
                 queue.append((p, cn))
     return out
+
+
+def test_merged_chunk_table_holds_what_the_tree_references(oracle):
+    """The merged v6 chunk table lists the distinct (digest, blob) chunks the
+    merged tree's files reference -- the chunks of files a later layer
+    removed or replaced are gone -- in the layers' table order."""
+    cs = 0x10000
+    boots = [_boot(_pack(oracle, _tar(e), cs=cs, fs=6, comp="none")[0]) for e in MERGE_LAYERS]
+    merged, ids = nydus_gpu.merge(boots, ["11" * 32, "22" * 32, "33" * 32])
+    table = rafs.read_v6(merged)["chunks"]
+    keys = [(bytes(r["block_id"]), int(r["blob_index"])) for r in table]
+    refs = {(bytes(c["block_id"]), int(c["blob_index"])) for f in rf.read_v6_files(merged) for c in f[3]}
+    assert len(keys) == len(set(keys)) and set(keys) == refs
+    every = sum(len(rafs.read_v6(b)["chunks"]) for b in boots)
+    assert len(keys) < every  # a/x (layer 0), b/z, d/e and a/y (layer 0) are not referenced
