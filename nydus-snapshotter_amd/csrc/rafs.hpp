@@ -15,12 +15,15 @@
 //     numbered (depth first); a hardlink takes a number but keeps its
 //     target's i_ino (3,515 of 3,517 fixture inodes, the other 2 hardlinks);
 //   * v6: extended (64-B) EROFS inodes; directory and symlink data inline
-//     after the inode (FLAT_INLINE, full directory blocks right after the
-//     inode's block), regular files CHUNK_BASED with 8-B indexes {advise,
-//     device id = blob + 1, blkaddr = uncompressed offset / 4 KiB}; inodes
-//     laid out depth first (a directory, its non-directory entries, then its
-//     subdirectories), root at nid 128; device table after the extended
-//     super block, blob table at 4096, prefetch table (nids) after it;
+//     after the inode (FLAT_INLINE, full directory blocks in the blocks after
+//     it) or in blocks of their own (FLAT_PLAIN), regular files CHUNK_BASED
+//     with 8-B indexes {advise = chunk index, device id = blob + 1, blkaddr =
+//     uncompressed offset / 4 KiB}; inodes laid out depth first (a directory,
+//     its non-directory entries, then its subdirectories), root at nid 128,
+//     later inodes filling the free tails of earlier blocks; device table
+//     after the extended super block, blob table at 4096, prefetch table
+//     (nids) after it -- re-encoding the v6 fixture is byte-identical but
+//     for s_blocks;
 //   * v5: 128-B inodes in inode-number order with their name, symlink target
 //     and chunk infos; i_digest = H(chunk digests) for files, H(target) for
 //     symlinks, H(children's digests) for directories (all 3,517 fixture
