@@ -75,6 +75,8 @@ struct ngpu_dict {
     std::mutex mu;               // one exchange at a time per requester
   };
   std::vector<ngpu_dict *> parts;
+  // one entry per engine that has exchanged through this dict (the node's
+  // engines, normally W of them); freed with the dict
   std::vector<std::unique_ptr<Requester>> req;
   std::mutex req_mu;  // held only to find or add a requester
   bool replicated = false;
