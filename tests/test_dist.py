@@ -132,3 +132,19 @@ def test_equal_splits_overflow_runs_extra_rounds_together():
     ret = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), ret, 128, [90, 700]), nprocs=world, join=True)
     assert ret[0][0] and ret[1][0]
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("cap,nq", [(0, None), (96, [40, 300, 0, 96, 97, 500, 1, 250])])
+def test_sharded_dict_eight_ranks(cap, nq):
+    """The driver's node size, rehearsed on the CPU (gloo, 8 ranks): variable
+    splits, and equal padded splits where the ranks' query counts differ
+    (one empty, some past cap: extra rounds agreed on the host); every rank's
+    hits equal the whole dict's first-occurrence answers and the partition
+    covers the dict once."""
+    world = 8
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), ret, cap, nq), nprocs=world, join=True)
+    assert all(ret[r][0] for r in range(world))
+    assert sum(ret[r][1] for r in range(world)) == 5000
