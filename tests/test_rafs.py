@@ -305,8 +305,24 @@ def test_unpack_of_a_dict_layer_needs_the_dict_blob(oracle, golden_layers, tars)
     assert e.value.code == nydus_gpu.ENOTFOUND
 
 
+@pytest.fixture(scope="module")
+def unpack_fuzz_exe(tmp_path_factory):
+    """tests/cpp/unpack_fuzz.cpp with the host reader / writer, ASan + UBSan
+    (built once per module)."""
+    import subprocess
+    from conftest import ROOT
+    exe = str(tmp_path_factory.mktemp("fuzz") / "unpack_fuzz")
+    csrc = os.path.join(ROOT, "nydus-snapshotter_amd", "csrc")
+    subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
+                           "-fno-sanitize-recover=all", "-I", os.path.join(ROOT, "include"),
+                           "-I", csrc, os.path.join(ROOT, "tests", "cpp", "unpack_fuzz.cpp"),
+                           os.path.join(csrc, "blob.cpp"), os.path.join(csrc, "rafs.cpp"), "-o", exe,
+                           "-lcrypto", "-ldl", "-lpthread"])
+    return exe
+
+
 @pytest.mark.parametrize("fs", [5, 6])
-def test_bootstrap_reader_and_unpack_mutation_fuzz_asan(oracle, tmp_path, fs):
+def test_bootstrap_reader_and_unpack_mutation_fuzz_asan(oracle, tmp_path, fs, unpack_fuzz_exe):
     """read_rafs + ngpu_unpack on mutated bootstraps (tests/cpp/unpack_fuzz.cpp,
     built with ASan/UBSan, host only): image.boot is untrusted input -- byte
     flips and whole 16/32/64-bit fields (0, all-ones, powers of two, small
@@ -315,14 +331,7 @@ def test_bootstrap_reader_and_unpack_mutation_fuzz_asan(oracle, tmp_path, fs):
     memory error, no UB, no runaway output.  Both outcomes must occur, so the
     mutations reach past the superblock checks."""
     import subprocess
-    from conftest import ROOT
-    exe = str(tmp_path / "unpack_fuzz")
-    csrc = os.path.join(ROOT, "nydus-snapshotter_amd", "csrc")
-    subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
-                           "-fno-sanitize-recover=all", "-I", os.path.join(ROOT, "include"),
-                           "-I", csrc, os.path.join(ROOT, "tests", "cpp", "unpack_fuzz.cpp"),
-                           os.path.join(csrc, "blob.cpp"), os.path.join(csrc, "rafs.cpp"), "-o", exe,
-                           "-lcrypto", "-ldl", "-lpthread"])
+    exe = unpack_fuzz_exe
     blob, *_ = _pack(oracle, layers.oci_upper_tar_go(3), cs=0x10000, fs=fs, comp="zstd")
     sp = tmp_path / "s"
     sp.write_bytes(blob)
