@@ -733,7 +733,30 @@ int write_v6(Tree &t, const RafsLayerInfo &info, std::vector<uint8_t> *outp) {
 
 // ---- RAFS v5 ------------------------------------------------------------------
 constexpr uint64_t kV5SuperBlockSize = 0x2000;
-constexpr uint64_t kV5FlagSymlink = 0x1;
+constexpr uint64_t kV5FlagSymlink = 0x1, kV5FlagXattr = 0x4;
+
+// RAFS v5 inode xattrs ([nydus v2.3.0] RafsXAttrs::store_v5, VERIFY): a u64
+// table size, then per pair (name order) {u32 size of name + NUL + value,
+// name, NUL, value}, the pairs 8-B padded; the reader skips it by its size.
+std::vector<uint8_t> xattr_v5(const Ino &in) {
+  std::vector<uint8_t> v;
+  if (in.xattrs.empty()) return v;
+  std::vector<std::pair<std::string, std::string>> kv = in.xattrs;
+  std::sort(kv.begin(), kv.end());
+  v.resize(8, 0);
+  for (const auto &x : kv) {
+    const uint32_t sz = (uint32_t)(x.first.size() + 1 + x.second.size());
+    const size_t o = v.size();
+    v.resize(o + 4 + sz, 0);
+    memcpy(&v[o], &sz, 4);
+    memcpy(&v[o + 4], x.first.data(), x.first.size());
+    memcpy(&v[o + 4 + x.first.size() + 1], x.second.data(), x.second.size());
+  }
+  const uint64_t pairs = align(v.size() - 8, 8);
+  memcpy(&v[0], &pairs, 8);
+  v.resize(8 + pairs, 0);
+  return v;
+}
 
 void digest_of(uint32_t digester, const void *p, uint64_t n, uint8_t out[32]) {
   if (digester == NGPU_DIGEST_SHA256) sha256(p, n, out);
@@ -819,6 +842,7 @@ int write_v5(Tree &t, const RafsLayerInfo &info, std::vector<uint8_t> *outp) {
     off[r] = pos;
     uint64_t sz = 128 + align(nd.name.size(), 8);
     if ((in.mode & S_IFMT) == S_IFLNK) sz += align(in.link.size(), 8);
+    sz += xattr_v5(in).size();
     if ((in.mode & S_IFMT) == S_IFREG) {
       uint64_t first, cnt;
       if (int rc = chunks_of(in, fc, info.chunk_size, &first, &cnt)) return rc;
@@ -868,7 +892,8 @@ int write_v5(Tree &t, const RafsLayerInfo &info, std::vector<uint8_t> *outp) {
     const uint64_t size = type == S_IFDIR ? 4096 : in.size;  // fixture: directories 4096
     put<uint64_t>(v, o + 64, size);
     put<uint64_t>(v, o + 72, type == S_IFDIR ? 8 : (size + 511) / 512);
-    put<uint64_t>(v, o + 80, type == S_IFLNK ? kV5FlagSymlink : 0);
+    const std::vector<uint8_t> xa = xattr_v5(in);
+    put<uint64_t>(v, o + 80, (type == S_IFLNK ? kV5FlagSymlink : 0) | (xa.empty() ? 0 : kV5FlagXattr));
     put<uint32_t>(v, o + 88, in.nlink);
     put<uint32_t>(v, o + 92, type == S_IFDIR ? (uint32_t)nd.child_index : 0);
     put<uint32_t>(v, o + 96, type == S_IFDIR ? (uint32_t)nd.kids.size() : (uint32_t)cnt);
@@ -884,6 +909,8 @@ int write_v5(Tree &t, const RafsLayerInfo &info, std::vector<uint8_t> *outp) {
       put_bytes(v, q, in.link.data(), in.link.size());
       q += align(in.link.size(), 8);
     }
+    put_bytes(v, q, xa.data(), xa.size());
+    q += xa.size();
     for (uint64_t k = 0; k < cnt; ++k, q += 80) put_bytes(v, q, &info.refs[first + k], 80);
   }
   return 0;
@@ -1134,9 +1161,18 @@ int read_v5(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
         nd.link.assign((const char *)p + q, slsz);
         q += align(slsz, 8);
       }
-      if (fl & 0x4) {
+      if (fl & kV5FlagXattr) {
         uint64_t xs;
-        if (!get(p, n, q, &xs) || xs > n) return host_fail(NGPU_EFORMAT, "bad xattr size");
+        if (!get(p, n, q, &xs) || xs > n || q + 8 + xs > n) return host_fail(NGPU_EFORMAT, "bad xattr size");
+        for (uint64_t a = q + 8, e = q + 8 + xs; a + 4 <= e;) {  // pairs (padding ends the walk)
+          uint32_t ps;
+          memcpy(&ps, p + a, 4);
+          if (ps == 0 || ps > e - a - 4) break;
+          const char *kvp = (const char *)p + a + 4;
+          const size_t kl = strnlen(kvp, ps);
+          if (kl < ps) nd.xattrs.emplace_back(std::string(kvp, kl), std::string(kvp + kl + 1, ps - kl - 1));
+          a += 4 + ps;
+        }
         q += 8 + align(xs, 8);
       }
       if ((mode & S_IFMT) == S_IFREG && size) {

@@ -811,3 +811,99 @@ def test_merged_chunk_table_holds_what_the_tree_references(oracle):
     assert len(keys) == len(set(keys)) and set(keys) == refs
     every = sum(len(rafs.read_v6(b)["chunks"]) for b in boots)
     assert len(keys) < every  # a/x (layer 0), b/z, d/e and a/y (layer 0) are not referenced
+
+
+def _random_tar(seed):
+    """A random layer: nested directories (some only implied by their
+    children), files of random sizes (empty, partial chunks, several chunks),
+    symlinks, hardlinks, char / block devices, fifos, PAX xattrs and long
+    names, a later entry replacing an earlier one, whiteouts kept as files."""
+    rng = np.random.default_rng(seed)
+    out, files, dirs = io.BytesIO(), [], ["", "a", "a/b", "c", "c/" + "d" * 120]
+    with tarfile.open(fileobj=out, mode="w", format=tarfile.PAX_FORMAT) as tw:
+        def info(name, **kw):
+            ti = tarfile.TarInfo(name)
+            ti.mtime = int(rng.integers(0, 2_000_000_000))
+            ti.mode = int(rng.choice([0o644, 0o755, 0o600, 0o4755]))
+            ti.uid, ti.gid = int(rng.integers(0, 70000)), int(rng.integers(0, 70000))
+            for k, v in kw.items():
+                setattr(ti, k, v)
+            return ti
+        for d in dirs[1:]:
+            if rng.random() < 0.7:  # else only implied
+                tw.addfile(info(d, type=tarfile.DIRTYPE, mode=0o755))
+        for k in range(int(rng.integers(20, 60))):
+            d = dirs[int(rng.integers(0, len(dirs)))]
+            name = (d + "/" if d else "") + f"f{k}" + ("x" * int(rng.integers(0, 3)) * 60)
+            r = rng.random()
+            if r < 0.55 or not files:
+                size = int(rng.choice([0, 1, 4095, 4096, 65536, 70000, 200000]))
+                ti = info(name, size=size)
+                if rng.random() < 0.2:
+                    ti.pax_headers = {"SCHILY.xattr.user.k": "v" * int(rng.integers(1, 40))}
+                tw.addfile(ti, io.BytesIO(rng.integers(0, 256, size, dtype=np.uint8).tobytes()))
+                files.append(name)
+            elif r < 0.7:
+                tw.addfile(info(name, type=tarfile.SYMTYPE, linkname="../" * int(rng.integers(0, 3)) + "t" * 90))
+            elif r < 0.8:
+                tw.addfile(info(name, type=tarfile.LNKTYPE, linkname=files[int(rng.integers(0, len(files)))]))
+            elif r < 0.87:
+                tw.addfile(info(name, type=tarfile.CHRTYPE, devmajor=int(rng.integers(0, 300)),
+                                devminor=int(rng.integers(0, 70000))))
+            elif r < 0.92:
+                tw.addfile(info(name, type=tarfile.FIFOTYPE))
+            elif r < 0.96:
+                tw.addfile(info((d + "/" if d else "") + ".wh.gone", size=0), io.BytesIO(b""))
+            else:  # replaces an earlier file of the same path
+                old = files[int(rng.integers(0, len(files)))]
+                tw.addfile(info(old, size=3), io.BytesIO(b"new"))
+    return out.getvalue()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_trees_reencode_and_unpack(oracle, seed):
+    """Random trees through Pack, for both RAFS versions: the bootstrap reader
+    and writer are inverse (re-encoding the Pack's own image.boot -- a
+    one-layer Merge -- gives the same bytes), and Unpack gives back every
+    entry of the tar with its type, metadata, contents and link target (the
+    tar's last entry of a path wins, hardlinks point at their first path)."""
+    tar = _random_tar(seed)
+    fs = 5 if seed % 2 else 6
+    cs = 0x10000 if seed % 3 else 0x1000
+    blob, *_ = _pack(oracle, tar, cs=cs, fs=fs, comp="zstd" if seed % 4 else "none")
+    boot = _boot(blob)
+    again, _ = nydus_gpu.merge([boot], [""])
+    src, replaced = {}, False
+    for m in tarfile.open(fileobj=io.BytesIO(tar)):
+        replaced |= m.name.strip("/") in src and m.isfile()
+        src[m.name.strip("/")] = m
+    if replaced:
+        # a file a later entry replaced keeps its chunks in the Pack's blob
+        # (and chunk table); a Merge keeps only what the tree references
+        assert nydus_gpu.merge([again], [""])[0] == again
+        assert len(rafs.read_v6(again)["chunks"] if fs == 6 else again) <= len(
+            rafs.read_v6(boot)["chunks"] if fs == 6 else boot)
+    else:
+        assert again == boot
+    back = tarfile.open(fileobj=io.BytesIO(nydus_gpu.unpack(blob)))
+    seen = set()
+    data = tarfile.open(fileobj=io.BytesIO(tar))
+    for m in back:
+        p = m.name.strip("/")
+        seen.add(p)
+        s = src.get(p)
+        if s is None:  # an implied directory
+            assert m.isdir()
+            continue
+        if not (s.islnk() or m.islnk()):
+            assert (m.type, m.mode, m.uid, m.gid, m.mtime) == (s.type, s.mode, s.uid, s.gid, s.mtime), p
+        if m.isfile() and not m.islnk():
+            assert back.extractfile(m).read() == data.extractfile(s).read(), p
+        if m.issym():
+            assert m.linkname == s.linkname
+        if m.ischr():
+            assert (m.devmajor, m.devminor) == (s.devmajor, s.devminor)
+        if not (s.islnk() or m.islnk()) and (m.pax_headers.get("SCHILY.xattr.user.k") or
+                                             s.pax_headers.get("SCHILY.xattr.user.k")):
+            assert m.pax_headers.get("SCHILY.xattr.user.k") == s.pax_headers.get("SCHILY.xattr.user.k")
+    assert set(src) <= seen
