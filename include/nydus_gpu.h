@@ -130,7 +130,8 @@ typedef struct {
  * (by chunk count); other values are rejected (NGPU_EINVAL). */
 #define NGPU_FLAG_SHA_MODE_SHIFT 11
 
-/* Errors of device-pointer calls that read no stats (stats == NULL,
+/* The builder's exit status (builder.go:169-175) for work enqueued on a
+ * caller's stream: errors of device-pointer calls that read no stats (stats == NULL,
  * ngpu_digest_device, the *_layers_device calls): synchronises every stream
  * the engine's workspaces were last used on, returns the first error any
  * stage recorded since the previous ngpu_device_status (NGPU_EINVAL for bad or
