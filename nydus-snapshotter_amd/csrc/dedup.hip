@@ -775,10 +775,13 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small(
 constexpr uint32_t kLdsChunks = 4096;   // == kSmallDedupChunks
 constexpr uint32_t kLdsSlots = 8192;    // next_pow2(2n) for n <= 4096
 constexpr uint32_t kLdsBlobs = 1024;    // dict blobs + own
-constexpr int kLdsItems = (int)(kLdsChunks / kSmallThreads);
 static_assert(kLdsChunks == kSmallDedupChunks, "one LDS slot per chunk");
 
-__global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
+// T threads: 1024, or 256 for a layer of at most 256 chunks (C1: 108), whose
+// one row of chunks then spans 4 waves instead of 16 (cheaper barriers and
+// cross-wave scans; same decisions).
+template <uint32_t T>
+__global__ __launch_bounds__(T) void dedup_small_lds(
     const ngpu_chunk *__restrict__ chunks, uint64_t n, DictDevice dict,
     const ngpu_dict_hit *__restrict__ hits, uint32_t n_blobs, uint32_t align,
     ngpu_layer_stats *__restrict__ st, ngpu_result *__restrict__ out,
@@ -788,26 +791,26 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
   __shared__ uint32_t len_s[kLdsChunks];
   __shared__ uint32_t nidx[kLdsChunks];  // exclusive prefix of NEW flags
   __shared__ uint32_t bf[kLdsBlobs], real[kLdsBlobs];
-  __shared__ uint64_t wsum[2][4][kSmallThreads / 64];
+  __shared__ uint64_t wsum[2][4][T / 64];
   __shared__ uint32_t used_all;
   __shared__ unsigned long long s_unh[2];  // unhashed chunks: count, ~smallest id
   const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const uint32_t nbo = n_blobs + 1;
   uint32_t mask = 63;
   while (mask + 1 < 2 * n) mask = mask * 2 + 1;
-  for (uint32_t i = t; i <= mask; i += kSmallThreads) table[i] = kEmpty;
-  for (uint32_t i = t; i < nbo; i += kSmallThreads) bf[i] = kNone;
+  for (uint32_t i = t; i <= mask; i += T) table[i] = kEmpty;
+  for (uint32_t i = t; i < nbo; i += T) bf[i] = kNone;
   if (t == 0) used_all = 0, s_unh[0] = s_unh[1] = 0;
   __syncthreads();
   // A: dict decisions (DICT results written now) and the intra-layer table.
-  // Item k of thread t is chunk k * kSmallThreads + t (rows, for the scans).
+  // Item k of thread t is chunk k * T + t (rows, for the scans).
   // Per chunk, for phase B: len_s = length | DICT flag (bit 31), off = the
   // digest's tag : bucket (overwritten by the chunk's offset prefix in B).
   constexpr uint32_t kDictBit = 0x80000000u;
   constexpr uint32_t kUnhashedBit = 0x20000000u;  // no digest (digest_unwritten)
 #pragma unroll 1
-  for (int k = 0; k < kLdsItems; ++k) {
-    const uint64_t c = (uint64_t)k * kSmallThreads + t;
+  for (int k = 0; k < (int)(kLdsChunks / T); ++k) {
+    const uint64_t c = (uint64_t)k * T + t;
     if (c >= n) break;
     uint32_t dg[8];
     load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, dg);
@@ -854,7 +857,7 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
   }
   __syncthreads();
   // B: resolve INTRA / NEW and scan the four per-chunk quantities in chunk
-  // order, one row of kSmallThreads chunks at a time (one barrier per row).
+  // order, one row of T chunks at a time (one barrier per row).
   // an INTRA chunk's len_s becomes kIntraBit | its first occurrence once
   // resolved: no later chunk reads it (a first occurrence is always the
   // smallest id of its digest, never an INTRA chunk)
@@ -863,8 +866,8 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
   __shared__ uint32_t own_first;
   if (t == 0) own_first = kNone;
 #pragma unroll 1
-  for (int k = 0; k < kLdsItems; ++k) {
-    const uint64_t c = (uint64_t)k * kSmallThreads + t;
+  for (int k = 0; k < (int)(kLdsChunks / T); ++k) {
+    const uint64_t c = (uint64_t)k * T + t;
     uint64_t v[4] = {0, 0, 0, 0};  // NEW, aligned size, bytes, DICT
     if (c < n) {
       const uint32_t lv = len_s[c];
@@ -902,7 +905,7 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
         }
       }
     }
-    if ((uint64_t)k * kSmallThreads >= n) break;  // uniform: the row is empty
+    if ((uint64_t)k * T >= n) break;  // uniform: the row is empty
     uint64_t x[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) x[q] = v[q];
@@ -924,7 +927,7 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll 4
-      for (int w = 0; w < (int)(kSmallThreads / 64); ++w) {
+      for (int w = 0; w < (int)(T / 64); ++w) {
         const uint64_t y = wsum[b][q][w];
         if (w < (int)wid) pre[q] += y;
         tot[q] += y;
@@ -944,7 +947,7 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
   if (t == 0) bf[nbo - 1] = own_first;
   __syncthreads();
   uint32_t used = 0;
-  for (uint32_t b = t; b < nbo; b += kSmallThreads) {
+  for (uint32_t b = t; b < nbo; b += T) {
     const uint32_t fb = bf[b];
     uint32_t rank = kNone;
     if (fb != kNone) {
@@ -959,8 +962,8 @@ __global__ __launch_bounds__(kSmallThreads) void dedup_small_lds(
   // D: final per-chunk fields and the layer stats
   const uint32_t own = real[nbo - 1];
 #pragma unroll 1
-  for (int k = 0; k < kLdsItems; ++k) {
-    const uint64_t c = (uint64_t)k * kSmallThreads + t;
+  for (int k = 0; k < (int)(kLdsChunks / T); ++k) {
+    const uint64_t c = (uint64_t)k * T + t;
     if (c >= n) break;
     ngpu_result &r = out[c];
     const uint32_t lv = len_s[c];
@@ -1136,8 +1139,18 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                     reinterpret_cast<uint64_t *>(st), nst, ws.intra, icap, ts, ntw,
                     ws.newflag, ws.uoff, ws.nbytes, ws.ndict, total, ws.stats};
   if (small && single && nbo <= kLdsBlobs) {  // one layer: the whole stage in LDS
-    hipExtLaunchKernelGGL(dedup_small_lds, dim3(1), dim3(kSmallThreads), 0, s, nullptr, ev_end, 0,
-                          chunks, n, dict, hits, n_blobs, align, st, out, ws.stats);
+    // NGPU_DEDUP_LDS_THREADS=1024: the wide workgroup for every size (A/B knob)
+    static const bool wide = [] {
+      const char *v = getenv("NGPU_DEDUP_LDS_THREADS");
+      return v && atoi(v) == 1024;
+    }();
+    if (n <= 256 && !wide)
+      hipExtLaunchKernelGGL(dedup_small_lds<256>, dim3(1), dim3(256), 0, s, nullptr, ev_end, 0,
+                            chunks, n, dict, hits, n_blobs, align, st, out, ws.stats);
+    else
+      hipExtLaunchKernelGGL(dedup_small_lds<kSmallThreads>, dim3(1), dim3(kSmallThreads), 0, s,
+                            nullptr, ev_end, 0, chunks, n, dict, hits, n_blobs, align, st, out,
+                            ws.stats);
     return;
   }
   if (small) {
