@@ -393,6 +393,7 @@ void engine_unref(ngpu_engine *e) {
     if (b.fence) (void)hipEventDestroy(b.fence);
     if (b.h_stats) (void)hipHostFree(b.h_stats);
     if (b.h_io) (void)hipHostFree(b.h_io);
+    blob_windows_free(b.win);
   }
   for (hipStream_t x : e->streams)  // every pack compute stream (+ the engine's)
     if (x != e->stream) (void)hipStreamDestroy(x);

@@ -26,6 +26,17 @@ struct ngpu_staging_buf {
 // of a small layer's streaming Pack: 0.9 ms for C1's 10 MB).  `stream` is the
 // pack's compute stream: packs open at once run side by side on the GPU.
 // Compute streams live until the engine is destroyed (ngpu_engine::streams).
+// The double-buffered gather windows of a Pack's blob stream: device window
+// + descriptors and the pinned descriptor staging, per buffer (allocated per
+// Pack close until round 3: two hipMalloc/hipHostMalloc pairs of 5 MB and a
+// staging-sized window each time).
+struct BlobWindows {
+  uint8_t *dwin[2] = {}, *ddesc[2] = {}, *hdesc[2] = {};
+  hipEvent_t ev[2] = {};
+  uint64_t cap = 0, kcap = 0;  // window bytes, descriptors per window
+};
+void blob_windows_free(BlobWindows &w);  // (pack.hip)
+
 struct ngpu_pack_bufs {
   hipStream_t copy = nullptr;
   hipStream_t stream = nullptr;
@@ -37,6 +48,7 @@ struct ngpu_pack_bufs {
   uint64_t res_cap = 0;
   ngpu_chunk *d_all = nullptr;
   uint64_t all_cap = 0;
+  BlobWindows win;              // the blob stream's gather windows (ngpu_pack_finish)
 };
 
 // A chunk dict ([nydus v2.3.0] HashChunkDict): HBM-resident, read-only once

@@ -156,6 +156,7 @@ struct ngpu_pack : TarSink {
   uint64_t *h_stats = nullptr;   // pinned: its stats, read after the engine lock is let go
   uint8_t *h_io = nullptr;       // pinned staging of the chunk table / results at close
   uint64_t io_cap = 0;
+  BlobWindows win;           // blob stream gather windows (kept by the engine's pack_pool)
   CopyPool *pool = nullptr;  // created on the first large write
   bool retain = false;       // NGPU_PACK_RETAIN: device segments kept to the end
   std::vector<Seg> segs;
@@ -214,7 +215,8 @@ void release(ngpu_pack *p) {
     std::lock_guard<std::mutex> g(p->e->pool_mu);
     if (p->stream) {
       p->e->pack_pool.push_back({p->copy, p->stream, p->fence, p->h_stats, p->h_io, p->io_cap,
-                                 p->d_res, p->res_cap, p->d_all, p->all_cap});
+                                 p->d_res, p->res_cap, p->d_all, p->all_cap, p->win});
+      p->win = BlobWindows{};
       p->h_io = nullptr;
       p->copy = nullptr;
       p->stream = nullptr;
@@ -230,6 +232,7 @@ void release(ngpu_pack *p) {
   if (p->fence) (void)hipEventDestroy(p->fence);
   if (p->h_stats) (void)hipHostFree(p->h_stats);
   if (p->h_io) (void)hipHostFree(p->h_io);
+  blob_windows_free(p->win);
   delete p->pool;
   delete p;
   dict_unref(dict);
@@ -411,45 +414,49 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
   }
   wstart.push_back(k);
   const uint64_t nw = k ? wstart.size() - 1 : 0;  // no NEW chunk: no window
-  uint8_t *dwin[2] = {}, *ddesc[2] = {}, *hdesc[2] = {};
-  hipEvent_t ev[2] = {};
-  const uint64_t desc_bytes = maxk * (8 + 8 + 4);
-  auto cleanup = [&] {
-    (void)hipStreamSynchronize(p->stream);
-    for (int i = 0; i < 2; ++i) {
-      if (dwin[i]) (void)hipFree(dwin[i]);
-      if (ddesc[i]) (void)hipFree(ddesc[i]);
-      if (hdesc[i]) (void)hipHostFree(hdesc[i]);
-      if (ev[i]) (void)hipEventDestroy(ev[i]);
+  // the gather windows (pooled with the pack's other buffers): descriptors
+  // sized to the layer's NEW chunks, at least 4K, at most maxk per window
+  uint64_t kneed = 4096;
+  while (kneed < k && kneed < maxk) kneed *= 2;
+  BlobWindows &bw_ = p->win;
+  if (nw && (bw_.cap < cap || bw_.kcap < kneed || !bw_.ev[0])) {
+    (void)hipStreamSynchronize(p->stream);  // a previous Pack's windows may still be read
+    blob_windows_free(bw_);
+    bool ok = true;
+    for (int i = 0; i < 2 && ok; ++i)
+      ok = hipMalloc((void **)&bw_.dwin[i], cap) == hipSuccess &&
+           hipMalloc((void **)&bw_.ddesc[i], kneed * 20) == hipSuccess &&
+           hipHostMalloc((void **)&bw_.hdesc[i], kneed * 20, hipHostMallocDefault) == hipSuccess &&
+           hipEventCreateWithFlags(&bw_.ev[i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      (void)hipGetLastError();
+      blob_windows_free(bw_);
+      return fail(e, NGPU_ENOMEM, "pack: blob window allocation failed");
     }
-  };
-  bool ok = true;
-  for (int i = 0; i < 2 && ok; ++i)
-    ok = hipMalloc((void **)&dwin[i], cap) == hipSuccess &&
-         hipMalloc((void **)&ddesc[i], desc_bytes) == hipSuccess &&
-         hipHostMalloc((void **)&hdesc[i], desc_bytes, hipHostMallocDefault) == hipSuccess &&
-         hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess;
-  if (!ok) {
-    cleanup();
-    return fail(e, NGPU_ENOMEM, "pack: blob window allocation failed");
+    bw_.cap = cap;
+    bw_.kcap = kneed;
   }
+  uint8_t *const *dwin = bw_.dwin, *const *ddesc = bw_.ddesc, *const *hdesc = bw_.hdesc;
+  const hipEvent_t *ev = bw_.ev;
+  const uint64_t kc = bw_.kcap;  // descriptor slots per window buffer
+  auto cleanup = [&] { (void)hipStreamSynchronize(p->stream); };
   auto enqueue = [&](uint64_t wi) -> int {
     const int b = wi & 1;
     const uint64_t a = wstart[wi], c = wstart[wi + 1] - a;
     uint64_t *hs = (uint64_t *)hdesc[b];
-    uint64_t *ho = hs + maxk;
-    uint32_t *hl = (uint32_t *)(ho + maxk);
+    uint64_t *ho = hs + kc;
+    uint32_t *hl = (uint32_t *)(ho + kc);
     memcpy(hs, &src[a], c * 8);
     for (uint64_t i = 0; i < c; ++i) ho[i] = doff[a + i];
     memcpy(hl, &len[a], c * 4);
     uint64_t *ds = (uint64_t *)ddesc[b];
     hipStream_t ps = p->stream;
     HIP_TRY(e, hipMemcpyAsync(ds, hs, c * 8, hipMemcpyHostToDevice, ps));
-    HIP_TRY(e, hipMemcpyAsync(ds + maxk, ho, c * 8, hipMemcpyHostToDevice, ps));
-    HIP_TRY(e, hipMemcpyAsync(ds + 2 * maxk, hl, c * 4, hipMemcpyHostToDevice, ps));
+    HIP_TRY(e, hipMemcpyAsync(ds + kc, ho, c * 8, hipMemcpyHostToDevice, ps));
+    HIP_TRY(e, hipMemcpyAsync(ds + 2 * kc, hl, c * 4, hipMemcpyHostToDevice, ps));
     const unsigned grid = (unsigned)(c < 2048 ? c : 2048);
-    hipLaunchKernelGGL(gather_chunks, dim3(grid), dim3(256), 0, ps, ds, (uint32_t *)(ds + 2 * maxk),
-                       ds + maxk, c, dwin[b]);
+    hipLaunchKernelGGL(gather_chunks, dim3(grid), dim3(256), 0, ps, ds, (uint32_t *)(ds + 2 * kc),
+                       ds + kc, c, dwin[b]);
     HIP_TRY(e, hipGetLastError());
     const uint64_t bytes = doff[a + c - 1] + len[a + c - 1];
     if (int rc = host_fence(e, ps, p->fence)) return rc;
@@ -483,6 +490,16 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
 }
 
 }  // namespace
+
+void blob_windows_free(BlobWindows &w) {
+  for (int i = 0; i < 2; ++i) {
+    if (w.dwin[i]) (void)hipFree(w.dwin[i]);
+    if (w.ddesc[i]) (void)hipFree(w.ddesc[i]);
+    if (w.hdesc[i]) (void)hipHostFree(w.hdesc[i]);
+    if (w.ev[i]) (void)hipEventDestroy(w.ev[i]);
+  }
+  w = BlobWindows{};
+}
 
 extern "C" {
 
@@ -523,6 +540,7 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
       p->res_cap = b.res_cap;
       p->d_all = b.d_all;
       p->all_cap = b.all_cap;
+      p->win = b.win;
     }
     for (Slot &s : p->slot) {
       auto &pool = e->staging_pool;
