@@ -641,6 +641,49 @@ def end_to_end(torch, nydus_gpu, buf, wl, stride, device, sample_bytes=2 << 30):
     return res
 
 
+def node_e2e(torch, dist, nydus_gpu, buf, wl, stride, device, backend, sample_bytes):
+    """N > 1: every rank converts a sample of its layer from its own pinned host
+    memory at the same time (ngpu_pack_tar: tar walk + H2D + digest + dedup +
+    results back), barrier-bracketed, max time over ranks -- the node's
+    PCIe-inclusive rate over all its GPUs' links together (one Gen5 x16 link
+    per GPU), with the host memory they share.  Reported beside the line,
+    never as `value`."""
+    import ctypes
+    n_files = (buf.numel() - 1024) // stride
+    sample_files = max(1, min(n_files, sample_bytes // stride))
+    nbytes = sample_files * stride
+    eng = nydus_gpu.Engine(device=device, digester=wl["digester"], chunk_size=wl["chunk"])
+    L = nydus_gpu.lib()
+    hp = ctypes.c_void_p()
+    assert L.ngpu_alloc_pinned(eng._h, nbytes + 1024, ctypes.byref(hp)) == 0
+    try:
+        host = np.ctypeslib.as_array((ctypes.c_uint8 * (nbytes + 1024)).from_address(hp.value))
+        host[:nbytes] = buf[:nbytes].cpu().numpy()
+        host[nbytes:] = 0
+        file_bytes = sample_files * wl["file_size"]
+        eng.pack_tar(host)  # warm
+        reps = 3
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            eng.pack_tar(host)
+        dist.barrier()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    finally:
+        L.ngpu_free_pinned(eng._h, hp)
+        eng.close()
+    world = dist.get_world_size()
+    return {"host_path_gbs": round(file_bytes * reps * world / el / 1e9, 1),
+            "per_gpu_gbs": round(file_bytes * reps / el / 1e9, 1),
+            "sample_bytes_per_gpu": nbytes + 1024, "reps": reps,
+            "path": "ngpu_pack_tar from pinned host memory on every rank at once",
+            "bound": "one PCIe Gen5 x16 link per GPU (~50-55 GB/s H2D) and the host DRAM they share"}
+
+
 def concurrent_bench(args):
     """`--streams K` (tar workloads, e.g. c1): ONE engine converts K copies of
     the layer side by side, one caller stream each -- the shape of containerd
@@ -1288,7 +1331,9 @@ def main():
     dog = None
     printed = [False]
     print_mu = __import__("threading").Lock()  # the line is printed once: here or by the watchdog
-    if dist and sdict is None and n_layers == 1 and not args.no_sharded_extra:
+    sharded_extra = dist and sdict is None and n_layers == 1 and not args.no_sharded_extra
+    node_pcie = dist and stride and not wl.get("dict_entries") and not wl.get("pool") and not args.no_e2e
+    if sharded_extra or node_pcie:
         # the headline is already measured; a watchdog keeps a stuck collective
         # (here, or in the closing barrier after a rank failed in here) from
         # costing the line: on expiry rank 0 prints it if it has not yet, and
@@ -1303,16 +1348,23 @@ def main():
                 print(json.dumps(dict(line, sharded_dict={"error": "timeout"})), flush=True)
             sys.stdout.flush()
             os._exit(3)
-        dog = threading.Timer(120.0, stuck)
+        dog = threading.Timer(180.0, stuck)
         dog.daemon = True
         dog.start()
-        try:
-            sx = sharded_dict_extra(torch, dist, eng, buf, d_ch, n, stream, rank, world,
-                                    args.dist_backend)
-            sx["gbs"] = round(file_bytes * sx["steps"] * world / sx.pop("_elapsed") / 1e9, 2)
-            line["sharded_dict"] = sx
-        except Exception as ex:  # reported, never fatal to the headline line
-            line["sharded_dict"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
+        if sharded_extra:
+            try:
+                sx = sharded_dict_extra(torch, dist, eng, buf, d_ch, n, stream, rank, world,
+                                        args.dist_backend)
+                sx["gbs"] = round(file_bytes * sx["steps"] * world / sx.pop("_elapsed") / 1e9, 2)
+                line["sharded_dict"] = sx
+            except Exception as ex:  # reported, never fatal to the headline line
+                line["sharded_dict"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
+        if node_pcie:
+            try:
+                line["e2e_pcie_node"] = node_e2e(torch, dist, nydus_gpu, buf, wl, stride, local,
+                                                 args.dist_backend, min(args.e2e_mib, 1024) << 20)
+            except Exception as ex:  # reported, never fatal to the headline line
+                line["e2e_pcie_node"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
     if rank == 0:
         with print_mu:
             first = not printed[0]
