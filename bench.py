@@ -1229,8 +1229,8 @@ def main():
         # compressions done by b3_groups: all leaf blocks + in-group parents
         comp = blocks + (leaves - groups)
         achieved = comp * OPS_PER_COMPRESSION / (dig_ms / 1e3)
-        # launch_blake3's rule: one leaf per lane quad for <= 32K leaves at D = 0
-        quad = D == 0 and int(buf.numel()) // 1024 + n <= 32768
+        # launch_blake3's rule: one leaf per lane quad for <= 40K leaves + chunks at D = 0
+        quad = D == 0 and int(buf.numel()) // 1024 + n <= 40960
         # <= 4096 chunks: planning inside the leaf kernel (b3_quad_planned)
         kname = (("b3_quad_planned" if n <= 4096 else "b3_quad_leaves") if quad
                  else f"b3_groups<{D}>")

@@ -744,15 +744,18 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
 // offsets fixed for the kernel) -- the "message words staged in LDS" of the
 // north star.  Chunk trees above the leaves go to b3_tree.
 constexpr int kQuadThreads = 256;           // 64 quads = 64 leaves per workgroup
-// Up to 32K leaves (<= 2 quad waves per SIMD).  Measured crossover with the
+// Up to 40K leaves (<= 2.5 quad waves per SIMD).  Measured crossover with the
 // lane-per-leaf path (profiles/r2/quad_threshold_r2qt.json, digest ms, lane vs
 // quad): 8 MiB 0.030 / 0.018, 16 MiB 0.030 / 0.020, 32 MiB 0.033 / 0.026,
-// 48 MiB 0.033 / 0.032, 64 MiB equal.
+// 48 MiB 0.033 / 0.032, 64 MiB equal.  Round 3 (profiles/r3/ab_quad_max/,
+// builds alternated on one box): a 32 MiB layer (32,768 leaves + its chunks)
+// missed the old 32K limit by its chunk count: 467-486 GB/s on b3_groups<0>,
+// 577 on the quad path; 48 MiB ties (0.032 ms both ways).
 #ifndef B3_QUAD_PF
 #define B3_QUAD_PF 1
 #endif
 #ifndef B3_QUAD_MAX_LEAVES
-#define B3_QUAD_MAX_LEAVES 32768
+#define B3_QUAD_MAX_LEAVES 40960
 #endif
 constexpr uint64_t kQuadMaxLeaves = B3_QUAD_MAX_LEAVES;
 constexpr int kQP1 = 0x39, kQP2 = 0x4E, kQP3 = 0x93;  // quad_perm: lane i reads lane i+1/+2/+3
@@ -1177,6 +1180,8 @@ static bool launch_groups(const uint8_t *data, uint64_t data_len,
 bool blake3_load_mode_ok(int lm) {
   return lm == 0 || lm == 1 || lm == 2 || lm == 3 || lm == 5 || (NGPU_DIAG_NOLOAD && lm == 4);
 }
+
+uint64_t blake3_quad_max_leaves() { return kQuadMaxLeaves; }
 
 bool blake3_planned_in_leaves(uint64_t n, uint64_t data_len, int D, const Workspace &ws) {
   return D == 0 && !ws.grid_stages && n <= kSmallPlanChunks &&

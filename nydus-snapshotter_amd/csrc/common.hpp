@@ -205,6 +205,8 @@ bool blake3_load_mode_ok(int lm);
 // (b3_quad_planned: small layers on the quad path) -- there is no planning
 // kernel, so ev_groups_start is not recorded.
 bool blake3_planned_in_leaves(uint64_t n, uint64_t data_len, int group_log2, const Workspace &ws);
+// Leaves + chunks up to which D = 0 calls hash one leaf per lane quad.
+uint64_t blake3_quad_max_leaves();
 // sha256.hip
 void launch_sha256(const uint8_t *data, uint64_t data_len,
                    const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,

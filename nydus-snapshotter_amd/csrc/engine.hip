@@ -294,7 +294,7 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
       bound = end;
     snprintf(e->cur->path, sizeof e->cur->path, "blake3 %s D=%d, %llu chunks",
              blake3_planned_in_leaves(n, len, D, ws) ? "quad_planned"
-             : (D == 0 && !ws.grid_stages && len / kLeaf + n <= 32768) ? "quad_leaves"
+             : (D == 0 && !ws.grid_stages && len / kLeaf + n <= blake3_quad_max_leaves()) ? "quad_leaves"
                                                                         : "groups",
              D, (unsigned long long)n);
   }

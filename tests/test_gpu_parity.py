@@ -195,8 +195,9 @@ def _random_layer(rng, total, chunk_size, dup_frac=0.2, unaligned=False):
 @pytest.mark.parametrize("seed,chunk_size,unaligned,total", [
     (1, 0x1000, False, 8 << 20), (2, 0x4000, True, 8 << 20), (3, 0x10000, False, 8 << 20),
     (4, 0x100000, False, 48 << 20), (5, 0x100000, True, 48 << 20), (6, 0x1000000, False, 48 << 20),
-    # just under the 32K-leaf limit of the quad-lane BLAKE3 path, unaligned
-    (7, 0x100000, True, 31 << 20)])
+    # just under the 40K-leaf limit of the quad-lane BLAKE3 path, unaligned; and a
+    # 32 MiB layer, quad since round 3
+    (7, 0x100000, True, 39 << 20), (8, 0x100000, False, 32 << 20)])
 def test_random_vs_oracle(engines, oracle, seed, chunk_size, unaligned, total):
     rng = np.random.default_rng(seed)
     data, ch = _random_layer(rng, total, chunk_size, unaligned=unaligned)
