@@ -1,0 +1,120 @@
+"""GPU soak: many random layer tars through ngpu_pack_tar and the streaming
+Pack, every digest and decision checked against the CPU oracle (test
+infrastructure: the oracle is the checker).  Random file-size mixes (empty,
+a few bytes, around the 64-B block / 1 KiB leaf / chunk edges, multi-chunk),
+chunk sizes 4 KiB .. 4 MiB, both digesters, every BLAKE3 lanes setting and
+the grid-stage flag, engines reused across cases (as a converter's cached
+engine is).  A failure names the case, the engine and the first bad chunk;
+the digest guard turns an unwritten digest into NGPU_EDEVICE.
+
+usage: python scripts/gpu_soak.py [cases] [seed]
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "nydus-snapshotter_amd"), os.path.join(ROOT, "oracle"),
+          os.path.join(ROOT, "tests", "golden")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: F401,E402  (one HIP runtime per process: torch's, loaded first)
+import numpy as np  # noqa: E402
+
+import layers  # noqa: E402
+import nydus_gpu  # noqa: E402
+import oracle_py as oracle  # noqa: E402
+
+EDGES = [0, 1, 12, 63, 64, 65, 1023, 1024, 1025, 2047, 2048, 4095, 4096, 4097, 65535, 65536,
+         65537, 1 << 20, (1 << 20) + 1]
+
+
+def random_tar(rng, chunk):
+    t = layers._TarBuilder()
+    t.dir("d")
+    n = int(rng.integers(1, 60))
+    total = 0
+    for i in range(n):
+        r = rng.random()
+        if r < 0.35:
+            size = int(rng.choice(EDGES))
+        elif r < 0.55:
+            size = int(chunk * rng.integers(1, 4) + rng.integers(-2, 3))
+        elif r < 0.9:
+            size = int(rng.integers(0, 200_000))
+        else:
+            size = int(rng.integers(0, 6 << 20))
+        size = max(0, min(size, (24 << 20) - total))
+        total += size
+        data = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        if i and rng.random() < 0.1:  # a whole-file duplicate (INTRA)
+            t.file(f"d/dup{i}", data)
+        t.file(f"d/f{i}", data)
+        if rng.random() < 0.05:
+            t.symlink(f"d/l{i}", f"f{i}")
+    return t.bytes()
+
+
+def check(tag, ch, out, tar, chunk, digester):
+    ech = oracle.tar_chunks(tar, chunk)
+    if ch.tobytes() != ech.tobytes():
+        raise AssertionError(f"{tag}: chunk table differs ({len(ch)} vs {len(ech)})")
+    dig = oracle.digest_chunks(tar, ech, digester)
+    dec, _ = oracle.dedup(dig, ech["length"])
+    bad = np.nonzero((out["digest"] != dig).any(axis=1))[0]
+    if len(bad):
+        i = int(bad[0])
+        raise AssertionError(f"{tag}: {len(bad)} digest(s) differ, first chunk {i} "
+                             f"(len {int(ech['length'][i])}, kind {int(out['kind'][i])}, "
+                             f"got {out['digest'][i].tobytes().hex()})")
+    for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+        if not np.array_equal(out[f], dec[f]):
+            raise AssertionError(f"{tag}: decision field {f} differs")
+
+
+def main():
+    cases = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    seed = int(sys.argv[2]) if len(sys.argv) > 2 else 0x50A4
+    rng = np.random.default_rng(seed)
+    engines = {}
+    t0 = time.time()
+    stats = {"cases": 0, "calls": 0, "chunks": 0, "bytes": 0}
+    for case in range(cases):
+        chunk = int(rng.choice([0x1000, 0x4000, 0x10000, 0x100000, 0x400000]))
+        digester = "sha256" if rng.random() < 0.25 else "blake3"
+        lanes = 0 if digester == "sha256" else int(rng.choice([0, 1, 2, 4, 8, 16]))
+        flags = nydus_gpu.FLAG_GRID_STAGES if rng.random() < 0.2 else 0
+        key = (chunk, digester, lanes, flags)
+        if key not in engines:
+            engines[key] = nydus_gpu.Engine(digester=digester, chunk_size=chunk,
+                                            leaves_per_lane=lanes, flags=flags,
+                                            staging_bytes=int(rng.choice([0, 4 * chunk])))
+        eng = engines[key]
+        tar = random_tar(rng, chunk)
+        tag = f"case {case} (chunk {chunk:#x}, {digester}, lanes {lanes}, flags {flags:#x}, {len(tar)} B)"
+        ch, out, st = eng.pack_tar(tar)
+        check(tag + " pack_tar", ch, out, tar, chunk, digester)
+        w = eng.pack()
+        pos = 0
+        while pos < len(tar):
+            k = int(rng.integers(1, 3 << 20))
+            w.write(tar[pos:pos + k])
+            pos += k
+        ch2, out2, st2 = w.close()
+        check(tag + " stream", ch2, out2, tar, chunk, digester)
+        stats["cases"] += 1
+        stats["calls"] += 2
+        stats["chunks"] += 2 * len(ch)
+        stats["bytes"] += 2 * len(tar)
+        if case % 20 == 0:
+            print(f"case {case}: ok ({time.time() - t0:.0f} s)", flush=True)
+    for e in engines.values():
+        e.close()
+    stats["engines"] = len(engines)
+    stats["seconds"] = round(time.time() - t0, 1)
+    print(json.dumps({"soak": "ok", **stats}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
