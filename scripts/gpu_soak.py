@@ -8,7 +8,13 @@ engine is).  A failure names the case, the engine and the first bad chunk;
 the digest guard turns an unwritten digest into NGPU_EDEVICE.
 
 usage: python scripts/gpu_soak.py [cases] [seed]
+       python scripts/gpu_soak.py --threads T [cases] [seed]
+  --threads: T host threads share four cached engines and convert at once --
+  pack_tar (engine stream), streaming Packs (per-Pack streams), device calls on
+  each thread's own stream, Packs against a chunk dict -- every result checked
+  (the workspace slots, Pack pools and lazy stage-end events under load).
 """
+import threading
 import json
 import os
 import sys
@@ -30,9 +36,13 @@ EDGES = [0, 1, 12, 63, 64, 65, 1023, 1024, 1025, 2047, 2048, 4095, 4096, 4097, 6
          65537, 1 << 20, (1 << 20) + 1]
 
 
-def random_tar(rng, chunk):
+def random_tar(rng, chunk, files=None, first=()):
+    """A random layer tar; `files` (a list) collects (name, bytes) of its
+    regular files; `first`: files written before the random ones."""
     t = layers._TarBuilder()
     t.dir("d")
+    for name, data in first:
+        t.file(name, data)
     n = int(rng.integers(1, 60))
     total = 0
     for i in range(n):
@@ -51,17 +61,24 @@ def random_tar(rng, chunk):
         if i and rng.random() < 0.1:  # a whole-file duplicate (INTRA)
             t.file(f"d/dup{i}", data)
         t.file(f"d/f{i}", data)
+        if files is not None:
+            files.append((f"base/f{i}", data))
         if rng.random() < 0.05:
             t.symlink(f"d/l{i}", f"f{i}")
     return t.bytes()
 
 
-def check(tag, ch, out, tar, chunk, digester):
+def check(tag, ch, out, tar, chunk, digester, recs=None):
     ech = oracle.tar_chunks(tar, chunk)
     if ch.tobytes() != ech.tobytes():
         raise AssertionError(f"{tag}: chunk table differs ({len(ch)} vs {len(ech)})")
     dig = oracle.digest_chunks(tar, ech, digester)
-    dec, _ = oracle.dedup(dig, ech["length"])
+    kw = {}
+    if recs is not None:
+        kw = dict(dict_digests=recs["block_id"], dict_sizes=recs["uncompressed_size"],
+                  dict_blob=recs["blob_index"], dict_index=recs["index"],
+                  dict_uoff=recs["uncompressed_offset"])
+    dec, _ = oracle.dedup(dig, ech["length"], **kw)
     bad = np.nonzero((out["digest"] != dig).any(axis=1))[0]
     if len(bad):
         i = int(bad[0])
@@ -73,7 +90,91 @@ def check(tag, ch, out, tar, chunk, digester):
             raise AssertionError(f"{tag}: decision field {f} differs")
 
 
+def concurrent(threads, cases, seed):
+    """T threads, shared engines, every call checked (see the module doc)."""
+    import torch
+    from nydus_gpu import rafs
+    rng0 = np.random.default_rng(seed)
+    configs = [(0x10000, "blake3", 0), (0x100000, "blake3", 0), (0x100000, "blake3", 8),
+               (0x10000, "sha256", 0)]
+    shared = []
+    for chunk, dg, lanes in configs:
+        eng = nydus_gpu.Engine(digester=dg, chunk_size=chunk, leaves_per_lane=lanes)
+        base = []  # the dict: a layer's own records; its files are planted in later layers
+        ch, out, _ = eng.pack_tar(random_tar(rng0, chunk, files=base))
+        recs = nydus_gpu.chunk_table(ch, out).view(rafs.CHUNK_INFO_DTYPE).reshape(-1).copy()
+        d = eng.dict_create(recs)
+        shared.append((eng, chunk, dg, lanes, base, recs, d))
+    counts = {"calls": 0, "chunks": 0}
+    mu = threading.Lock()
+    errors = []
+
+    def worker(tid):
+        rng = np.random.default_rng(seed * 1000 + tid)
+        stream = torch.cuda.Stream()
+        try:
+            for case in range(cases):
+                eng, chunk, dg, lanes, base, recs, d = shared[int(rng.integers(0, len(shared)))]
+                plant = base if rng.random() < 0.3 else ()  # the dict layer's files: DICT hits
+                tar = random_tar(rng, chunk, first=plant)
+                op = int(rng.integers(0, 4))
+                tag = f"thread {tid} case {case} op {op} (chunk {chunk:#x}, {dg}, lanes {lanes})"
+                if op == 0:
+                    ch, out, _ = eng.pack_tar(tar)
+                    check(tag, ch, out, tar, chunk, dg)
+                elif op in (1, 2):
+                    use = d if op == 2 else None
+                    w = eng.pack(dict=use)
+                    pos = 0
+                    while pos < len(tar):
+                        k = int(rng.integers(1, 3 << 20))
+                        w.write(tar[pos:pos + k])
+                        pos += k
+                    ch, out, _ = w.close()
+                    check(tag, ch, out, tar, chunk, dg, recs if op == 2 else None)
+                else:
+                    ch = nydus_gpu.tar_chunks(tar, chunk)
+                    n = len(ch)
+                    with torch.cuda.stream(stream):
+                        dbuf = torch.frombuffer(bytearray(tar), dtype=torch.uint8).to("cuda", non_blocking=False)
+                        dch = torch.from_numpy(ch.view(np.uint8).copy()).to("cuda")
+                        dout = torch.empty(max(n, 1) * 64, dtype=torch.uint8, device="cuda")
+                        eng.process_dict_device(None, dbuf.data_ptr(), dbuf.numel(), dch.data_ptr(), n,
+                                                dout.data_ptr(), stream=stream.cuda_stream)
+                        host = dout.cpu()
+                    stream.synchronize()
+                    st = eng.device_status()
+                    if st:
+                        raise AssertionError(f"{tag}: device status {st}")
+                    out = host.numpy()[: n * 64].view(nydus_gpu.RESULT_DTYPE)
+                    check(tag, ch, out, tar, chunk, dg)
+                with mu:
+                    counts["calls"] += 1
+                    counts["chunks"] += len(ch)
+        except Exception as ex:  # reported by main
+            errors.append(f"{type(ex).__name__}: {ex}")
+
+    t0 = time.time()
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for eng, *_rest, d in shared:
+        d.release()
+        eng.close()
+    if errors:
+        print(json.dumps({"soak": "FAILED", "errors": errors[:5]}), flush=True)
+        sys.exit(1)
+    print(json.dumps({"soak": "ok", "threads": threads, "cases_per_thread": cases, **counts,
+                      "engines": len(shared), "seconds": round(time.time() - t0, 1)}), flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--threads":
+        threads = int(sys.argv[2])
+        rest = sys.argv[3:]
+        return concurrent(threads, int(rest[0]) if rest else 50, int(rest[1]) if len(rest) > 1 else 0x50A5)
     cases = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 0x50A4
     rng = np.random.default_rng(seed)
