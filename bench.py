@@ -47,6 +47,9 @@ CLOCK_HZ = 2.4e9
 PEAK_INT_OPS = 256 * 4 * 16 * 2.4e9
 PEAK_HBM = 8.0e12
 OPS_PER_COMPRESSION = 680  # 7 rounds x 8 G x 12 ops + 8 output xors
+QUAD_COMPRESS_DEP_OPS = 190  # compress_quad: VALU ops per lane, one dependent chain
+DEP_OP_CYCLES = 8.5          # a lone wave's dependent VALU op (tools/valu_exec.hip, profiles/r1/valu_exec_issue.jsonl)
+KERNEL_BOUNDARY_S = 4.65e-6  # an empty kernel in a small call's trace (profiles/r2/c1_trace_diag_r2dg.txt)
 
 
 def synthetic_layout(n_files: int, file_size: int, chunk_size: int):
@@ -1239,6 +1242,27 @@ def main():
                 "frac": round(achieved / PEAK_INT_OPS, 4), "traffic": None,
                 "hbm_gbs": round(file_bytes / (dig_ms / 1e3) / 1e9, 1),
                 "hbm_frac": round(file_bytes / (dig_ms / 1e3) / PEAK_HBM, 4)}
+        if quad and n_layers == 1:
+            # A small layer fills a fraction of the lanes: its bound is the
+            # longest chunk's dependency chain, not chip throughput.  16 chained
+            # compressions per 1 KiB leaf, then ceil(log2 leaves) tree levels, each
+            # one compress_quad (~190 dependent VALU ops per lane at ~8.5 cycles per
+            # dependent op for a lone wave, profiles/r1/valu_exec_issue.jsonl), plus the call's
+            # three kernel boundaries (~4.65 us each: an empty kernel's duration in
+            # a rocprofv3 trace, profiles/r2/c1_trace_diag_r2dg.txt).
+            lmax = int(((ch["length"].astype(np.int64) + 1023) // 1024).max())
+            chain = min(16, max(1, (int(ch["length"].max()) + 63) // 64)) + (
+                int(np.ceil(np.log2(lmax))) if lmax > 1 else 0)
+            chain_s = chain * QUAD_COMPRESS_DEP_OPS * DEP_OP_CYCLES / CLOCK_HZ
+            launch_s = 3 * KERNEL_BOUNDARY_S
+            step_s = elapsed / args.steps
+            roof.update({"latency_bound": {
+                "critical_chain_compressions": chain, "chain_ms": round(chain_s * 1e3, 4),
+                "kernel_boundaries_ms": round(launch_s * 1e3, 4),
+                "bound_ms": round((chain_s + launch_s) * 1e3, 4),
+                "frac_of_step": round((chain_s + launch_s) / step_s, 3),
+                "model": "longest chunk: leaf blocks + tree levels, x ~190 dependent ops x 8.5 "
+                         "cycles at 2.4 GHz, + 3 kernel boundaries x 4.65 us"}})
     else:
         blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).sum())
         ops = blocks * 1384  # SURVEY.md §8(d) SHA-256 op count
