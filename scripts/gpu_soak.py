@@ -105,7 +105,15 @@ def concurrent(threads, cases, seed):
         recs = nydus_gpu.chunk_table(ch, out).view(rafs.CHUNK_INFO_DTYPE).reshape(-1).copy()
         d = eng.dict_create(recs)
         shared.append((eng, chunk, dg, lanes, base, recs, d))
-    counts = {"calls": 0, "chunks": 0}
+    # a one-process node of 4 parts on device 0 with a digest-prefix partitioned
+    # dict: concurrent requesters exchange through their own (owner, requester)
+    # channels (ngpu_node_*, node.hip)
+    node = nydus_gpu.Node([0, 0, 0, 0], chunk_size=0x10000)
+    nbase = []
+    nch, nout, _ = node.engines[0].pack_tar(random_tar(rng0, 0x10000, files=nbase))
+    nrecs = nydus_gpu.chunk_table(nch, nout).view(rafs.CHUNK_INFO_DTYPE).reshape(-1).copy()
+    nd = node.dict_create(nrecs)
+    counts = {"calls": 0, "chunks": 0, "node_calls": 0}
     mu = threading.Lock()
     errors = []
 
@@ -117,9 +125,18 @@ def concurrent(threads, cases, seed):
                 eng, chunk, dg, lanes, base, recs, d = shared[int(rng.integers(0, len(shared)))]
                 plant = base if rng.random() < 0.3 else ()  # the dict layer's files: DICT hits
                 tar = random_tar(rng, chunk, first=plant)
-                op = int(rng.integers(0, 4))
+                op = int(rng.integers(0, 5))
                 tag = f"thread {tid} case {case} op {op} (chunk {chunk:#x}, {dg}, lanes {lanes})"
-                if op == 0:
+                if op == 4:  # node Pack against the partitioned dict
+                    plant = nbase if rng.random() < 0.5 else ()
+                    tar = random_tar(rng, 0x10000, first=plant)
+                    w = node.pack(dict=nd)
+                    w.write(tar)
+                    ch, out, _ = w.close()
+                    check(tag + " node", ch, out, tar, 0x10000, "blake3", nrecs)
+                    with mu:
+                        counts["node_calls"] += 1
+                elif op == 0:
                     ch, out, _ = eng.pack_tar(tar)
                     check(tag, ch, out, tar, chunk, dg)
                 elif op in (1, 2):
@@ -163,6 +180,8 @@ def concurrent(threads, cases, seed):
     for eng, *_rest, d in shared:
         d.release()
         eng.close()
+    nd.release()
+    node.close()
     if errors:
         print(json.dumps({"soak": "FAILED", "errors": errors[:5]}), flush=True)
         sys.exit(1)
