@@ -687,6 +687,40 @@ def node_e2e(torch, dist, nydus_gpu, buf, wl, stride, device, backend, sample_by
             "bound": "one PCIe Gen5 x16 link per GPU (~50-55 GB/s H2D) and the host DRAM they share"}
 
 
+def node_cabi_extra(world, timeout_s=150):
+    """N > 1, rank 0, after the headline: the C ABI's one-process node
+    (ngpu_node_*, csrc/node.hip) over the run's GPUs, in a child process
+    (`bench.py --node 0,1,..`, C4-shaped layers, a 1M-entry dict partitioned
+    by digest prefix, then replicated): the in-process xGMI probe exchange a cgo
+    caller gets, measured on the node's real links.  A child, so that a failure
+    there costs only this entry.  NYDUS_NODE_EXTRA_DEVICES overrides the device
+    list (one-GPU rehearsal: "0,0")."""
+    import subprocess
+    devs = os.environ.get("NYDUS_NODE_EXTRA_DEVICES") or ",".join(str(i) for i in range(world))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--node", devs, "--workload", "c4-16",
+           "--steps", "5", "--warmup", "5", "--dict-entries", "1000000"]
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timeout after {timeout_s} s", "devices": devs}
+    lines = [x for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    if r.returncode or not lines:
+        return {"error": f"rc {r.returncode}: {(r.stderr or '')[-300:]}", "devices": devs}
+    d = json.loads(lines[-1])
+    part, rep = d["modes"]["partition"], d["modes"]["replicate"]
+    return {"devices": d["node_devices"], "path": "ngpu_node_* in one process, peer-copy exchange",
+            "workload": "c4-16 layers per device, 1M-entry dict", "seconds": round(time.perf_counter() - t0, 1),
+            "partition_gbs": part["value_gbs"], "replicate_gbs": rep["value_gbs"],
+            "dedup_alone_ms_partition": part["dedup_alone_ms"],
+            "dedup_alone_ms_replicate": rep["dedup_alone_ms"],
+            "all_requesters_at_once_ms": {"partition": part["dedup_all_requesters_at_once_ms"],
+                                          "replicate": rep["dedup_all_requesters_at_once_ms"]},
+            "peer_bytes_per_step": d["exchange"]["peer_bytes_per_step"],
+            "dict_hits_partition": part["dict_hits"], "dict_hits_replicate": rep["dict_hits"],
+            "hits_equal": part["dict_hits"] == rep["dict_hits"]}
+
+
 def concurrent_bench(args):
     """`--streams K` (tar workloads, e.g. c1): ONE engine converts K copies of
     the layer side by side, one caller stream each -- the shape of containerd
@@ -993,6 +1027,9 @@ def main():
     ap.add_argument("--no-sharded-extra", action="store_true",
                     help="N > 1: skip the RCCL-routed partitioned-dict step run after the "
                          "headline measurement")
+    ap.add_argument("--no-node-extra", action="store_true",
+                    help="N > 1: skip rank 0's child run of the C ABI node (ngpu_node_*) over "
+                         "the run's GPUs after the headline measurement")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--probe-queries", type=int, default=16 << 20,
                     help="dict workloads: queries of the probe-only roofline measurement (0 = skip)")
@@ -1029,6 +1066,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.dist_backend)
+        # host-side barriers (the closing one): while rank 0 runs the node child
+        # on every GPU, the other ranks wait on the CPU, not in an RCCL kernel
+        cpu_group = dist.new_group(backend="gloo")
 
     wl = dict(WORKLOADS[args.workload])
     if args.dict_entries:
@@ -1357,7 +1397,8 @@ def main():
     print_mu = __import__("threading").Lock()  # the line is printed once: here or by the watchdog
     sharded_extra = dist and sdict is None and n_layers == 1 and not args.no_sharded_extra
     node_pcie = dist and stride and not wl.get("dict_entries") and not wl.get("pool") and not args.no_e2e
-    if sharded_extra or node_pcie:
+    node_cabi = dist and stride and not wl.get("dict_entries") and not wl.get("pool") and not args.no_node_extra
+    if sharded_extra or node_pcie or node_cabi:
         # the headline is already measured; a watchdog keeps a stuck collective
         # (here, or in the closing barrier after a rank failed in here) from
         # costing the line: on expiry rank 0 prints it if it has not yet, and
@@ -1372,7 +1413,7 @@ def main():
                 print(json.dumps(dict(line, sharded_dict={"error": "timeout"})), flush=True)
             sys.stdout.flush()
             os._exit(3)
-        dog = threading.Timer(180.0, stuck)
+        dog = threading.Timer(360.0 if node_cabi else 180.0, stuck)
         dog.daemon = True
         dog.start()
         if sharded_extra:
@@ -1389,6 +1430,11 @@ def main():
                                                  args.dist_backend, min(args.e2e_mib, 1024) << 20)
             except Exception as ex:  # reported, never fatal to the headline line
                 line["e2e_pcie_node"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
+        if node_cabi and rank == 0:  # the other ranks wait in the closing barrier
+            try:
+                line["node_cabi"] = node_cabi_extra(world)
+            except Exception as ex:  # reported, never fatal to the headline line
+                line["node_cabi"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
     if rank == 0:
         with print_mu:
             first = not printed[0]
@@ -1397,7 +1443,7 @@ def main():
             print(json.dumps(line), flush=True)
     eng.close()
     if dist:
-        dist.barrier()
+        dist.barrier(group=cpu_group)
         dist.destroy_process_group()
     if dog:
         dog.cancel()

@@ -8,7 +8,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+NYDUS_NODE_EXTRA_DEVICES=${NYDUS_NODE_EXTRA_DEVICES:-0,0} timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 10 --warmup 5 \
   --dist-backend gloo > "$OUT/bench_c2_n2_gloo.json" 2> "$OUT/bench_c2_n2_gloo.err"
 rc=$?
