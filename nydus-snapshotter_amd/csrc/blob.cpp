@@ -1128,6 +1128,14 @@ int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
   const int rc = guarded([&]() -> int {
     if ((n && (!data || !chunks || !results)) || !stats || !opt || !w)
       return host_fail(NGPU_EINVAL, "ngpu_blob_write: bad argument");
+    // 0 = the default 1 MiB (what the tar re-scan below uses); anything else
+    // must be a power of two in [0x1000, 0x1000000] (types.go:76), as the
+    // bootstrap writer divides by it
+    ngpu_blob_options o = *opt;
+    if (!o.chunk_size) o.chunk_size = 0x100000;
+    if (o.chunk_size < 0x1000 || o.chunk_size > 0x1000000 || (o.chunk_size & (o.chunk_size - 1)))
+      return host_fail(NGPU_EINVAL, "ngpu_blob_write: invalid chunk size 0x%x", o.chunk_size);
+    opt = &o;
     std::vector<RafsV6BlobInfo> dict(opt->n_dict_blobs);
     if (opt->n_dict_blobs) {
       if (!opt->dict_blobs) return host_fail(NGPU_EINVAL, "ngpu_blob_write: dict_blobs is NULL");
@@ -1160,7 +1168,7 @@ int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
       } cmp;
       cmp.ch = chunks;
       cmp.n = n;
-      TarScanner sc(opt->chunk_size ? opt->chunk_size : 0x100000);
+      TarScanner sc(opt->chunk_size);
       sc.record(&entries);
       int rc = sc.feed((const uint8_t *)data, len, cmp);
       if (!rc) rc = sc.finish();
@@ -1324,6 +1332,13 @@ int ngpu_unpack(ngpu_read_at_fn ra, void *ctx, uint64_t size, ngpu_write_fn w, v
                              c.blob_index < blobs.size() ? blob_id_of(blobs[c.blob_index]).c_str() : "?");
           if (c.compressed_offset > dlen || c.compressed_size > dlen - c.compressed_offset)
             return host_fail(NGPU_EFORMAT, "unpack: chunk of %s outside image.blob", nd.path.c_str());
+          // sizes come from an untrusted bootstrap: a chunk never holds more
+          // than the blob's chunk size or the file bytes still to emit, so
+          // neither sizes the buffer past that
+          const uint32_t bcs = blobs[own].chunk_size;
+          if (c.uncompressed_size > nd.size - done || (bcs && c.uncompressed_size > bcs))
+            return host_fail(NGPU_EFORMAT, "unpack: chunk of %s larger than its file or chunk size",
+                             nd.path.c_str());
           cbuf.resize(c.compressed_size);
           if ((rc = r.read(cbuf.data(), c.compressed_size, doff + c.compressed_offset))) return rc;
           const uint8_t *data = cbuf.data();

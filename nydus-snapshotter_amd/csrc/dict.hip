@@ -94,19 +94,44 @@ ngpu_dict *dict_new(ngpu_engine *e) {
   return d;
 }
 
+namespace {
+
+// A dict build runs on a stream of its own, outside the engine lock: a load
+// of a 200M-entry bootstrap takes seconds, and under e->mu (round 3) it stalled
+// every Pack of the engine for that long, while its stream syncs on the
+// engine's own stream waited for their work too.
+struct BuildStream {
+  hipStream_t s = nullptr;
+  explicit BuildStream(int device) {
+    DeviceGuard g(device);
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      s = nullptr;
+    }
+  }
+  ~BuildStream() {
+    if (s) (void)hipStreamDestroy(s);
+  }
+};
+
+}  // namespace
+
 // Build the hash table over the uploaded digests (first table entry wins).
-int dict_build(ngpu_engine *e, ngpu_dict *d) {
-  launch_dict_build(d->dev.rec, d->dev.m, const_cast<uint64_t *>(d->dev.table), d->dev.mask + 1,
-                    e->stream);
+int dict_build(ngpu_engine *e, ngpu_dict *d, hipStream_t s) {
+  launch_dict_build(d->dev.rec, d->dev.m, const_cast<uint64_t *>(d->dev.table), d->dev.mask + 1, s);
   HIP_TRY(e, hipGetLastError());
-  HIP_TRY(e, hipStreamSynchronize(e->stream));
+  HIP_TRY(e, hipStreamSynchronize(s));
   return 0;
 }
 
-// From 80-B RAFS v6 chunk records in host memory (e->mu held); gids: the
-// records' global entry ids (node shards), null = their positions.
+// From 80-B RAFS v6 chunk records in host memory (no engine lock needed: the
+// upload and build run on their own stream); gids: the records' global entry
+// ids (node shards), null = their positions.
 int dict_from_records(ngpu_engine *e, const uint8_t *recs, uint64_t m, const uint8_t *blobs,
                       uint32_t n_blobs, ngpu_dict **out, const uint32_t *gids) {
+  DeviceGuard dg(e->device);
+  BuildStream bs(e->device);
+  if (!bs.s) return fail(e, NGPU_EHIP, "chunk dict: no build stream");
   if (m >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "chunk dict too large (%llu entries)",
                                       (unsigned long long)m);
   uint32_t nb = 0;
@@ -145,19 +170,19 @@ int dict_from_records(ngpu_engine *e, const uint8_t *recs, uint64_t m, const uin
   DictRec *rec = const_cast<DictRec *>(d->dev.rec);
   for (uint64_t a = 0; a < m && !rc; a += batch) {
     const uint64_t k = std::min(batch, m - a);
-    if (hipMemcpyAsync(tmp, recs + 80 * a, k * 80, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
-        (gids && hipMemcpyAsync(tmp_gid, gids + a, k * 4, hipMemcpyHostToDevice, e->stream) !=
+    if (hipMemcpyAsync(tmp, recs + 80 * a, k * 80, hipMemcpyHostToDevice, bs.s) != hipSuccess ||
+        (gids && hipMemcpyAsync(tmp_gid, gids + a, k * 4, hipMemcpyHostToDevice, bs.s) !=
                      hipSuccess)) {
       rc = fail(e, NGPU_EHIP, "chunk dict: upload failed");
       break;
     }
-    launch_dict_unpack(tmp, k, gids ? tmp_gid : nullptr, (uint32_t)a, rec + a, e->stream);
+    launch_dict_unpack(tmp, k, gids ? tmp_gid : nullptr, (uint32_t)a, rec + a, bs.s);
     // the next batch overwrites tmp
-    if (hipStreamSynchronize(e->stream) != hipSuccess) rc = fail(e, NGPU_EHIP, "chunk dict: unpack failed");
+    if (hipStreamSynchronize(bs.s) != hipSuccess) rc = fail(e, NGPU_EHIP, "chunk dict: unpack failed");
   }
   if (tmp_gid) (void)hipFree(tmp_gid);
   if (tmp) (void)hipFree(tmp);
-  if (!rc) rc = dict_build(e, d);
+  if (!rc) rc = dict_build(e, d, bs.s);
   if (rc) {
     dict_unref(d);
     return rc;
@@ -166,10 +191,14 @@ int dict_from_records(ngpu_engine *e, const uint8_t *recs, uint64_t m, const uin
   return 0;
 }
 
-// SoA arrays (host or device memory, `kind`) -> dict (e->mu held).
+// SoA arrays (host or device memory, `kind`) -> dict (no engine lock; own
+// stream, like dict_from_records).
 int dict_from_arrays(ngpu_engine *e, const uint8_t *dg, const uint32_t *us, const uint32_t *bl,
                      const uint32_t *ix, const uint64_t *uo, uint64_t m, uint32_t n_blobs,
                      hipMemcpyKind kind, ngpu_dict **out) {
+  DeviceGuard dgd(e->device);
+  BuildStream bs(e->device);
+  if (!bs.s) return fail(e, NGPU_EHIP, "chunk dict: no build stream");
   if (m >= 0xFFFFFFFFull) return fail(e, NGPU_EINVAL, "chunk dict too large (%llu entries)",
                                       (unsigned long long)m);
   if (n_blobs > (1u << 20)) return fail(e, NGPU_EINVAL, "chunk dict blob index %u too large",
@@ -193,14 +222,14 @@ int dict_from_arrays(ngpu_engine *e, const uint8_t *dg, const uint32_t *us, cons
       r.gid = (uint32_t)i;
       r.uoff = uo ? uo[i] : 0;
     }
-    if (hipMemcpyAsync(rec, h.data(), m * sizeof(DictRec), kind, e->stream) != hipSuccess ||
-        hipStreamSynchronize(e->stream) != hipSuccess)
+    if (hipMemcpyAsync(rec, h.data(), m * sizeof(DictRec), kind, bs.s) != hipSuccess ||
+        hipStreamSynchronize(bs.s) != hipSuccess)
       rc = fail(e, NGPU_EHIP, "chunk dict: upload failed");
   } else if (m) {
-    launch_dict_pack(dg, us, bl, ix, uo, m, rec, e->stream);
+    launch_dict_pack(dg, us, bl, ix, uo, m, rec, bs.s);
     if (hipGetLastError() != hipSuccess) rc = fail(e, NGPU_EHIP, "chunk dict: pack failed");
   }
-  if (!rc) rc = dict_build(e, d);
+  if (!rc) rc = dict_build(e, d, bs.s);
   if (rc) {
     dict_unref(d);
     return rc;
@@ -310,7 +339,7 @@ int read_dict_bootstrap(ngpu_engine *e, const char *path, uint64_t file_size,
 
 namespace {
 
-// Parse + check + load a RAFS v6 chunk-dict bootstrap (e->mu held).
+// Parse + check + load a RAFS v5/v6 chunk-dict bootstrap (no engine lock).
 int dict_load_file(ngpu_engine *e, const char *path, const struct stat &st, ngpu_dict **out) {
   std::vector<uint8_t> recs, blobs;
   int rc = read_dict_bootstrap(e, path, (uint64_t)st.st_size, &recs, &blobs);
@@ -341,37 +370,72 @@ int ngpu_dict_open(ngpu_engine *e, const char *path, ngpu_dict **out) {
   return guarded([&] { return dict_open(e, path, out); });
 }
 
+static bool same_file(const ngpu_dict *d, const char *path, const struct stat &st, int64_t mt) {
+  return d->path == path && d->st_dev == (uint64_t)st.st_dev && d->st_ino == (uint64_t)st.st_ino &&
+         d->st_size == (uint64_t)st.st_size && d->st_mtime_ns == mt;
+}
+
+// The engine lock covers only the cache lookups and the insert: the bootstrap
+// is read, parsed and built in HBM without it, and dicts leaving the cache are
+// released after it is dropped (the last release hipFrees, a device-wide wait).
+// Two threads opening the same changed file may both load it; the second
+// insert finds the first and drops its own copy.
 static int dict_open(ngpu_engine *e, const char *path, ngpu_dict **out) {
   if (!e || !path || !out) return NGPU_EINVAL;
   *out = nullptr;
   struct stat st;
   if (stat(path, &st) != 0) return fail(e, NGPU_EIO, "stat chunk dict %s", path);
   const int64_t mt = (int64_t)st.st_mtim.tv_sec * 1000000000 + st.st_mtim.tv_nsec;
-  std::lock_guard<std::mutex> g(e->mu);
-  DeviceGuard dg(e->device);
-  auto &c = e->dict_cache;
-  for (size_t i = 0; i < c.size(); ++i) {
-    ngpu_dict *d = c[i];
-    if (d->path != path) continue;
-    if (d->st_dev == (uint64_t)st.st_dev && d->st_ino == (uint64_t)st.st_ino &&
-        d->st_size == (uint64_t)st.st_size && d->st_mtime_ns == mt) {
-      dict_ref(d);
-      *out = d;
-      return 0;
+  std::vector<ngpu_dict *> drop;
+  auto release_dropped = [&] {
+    for (ngpu_dict *x : drop) dict_unref(x);
+    drop.clear();
+  };
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    auto &c = e->dict_cache;
+    for (size_t i = 0; i < c.size(); ++i) {
+      ngpu_dict *d = c[i];
+      if (d->path != path) continue;
+      if (same_file(d, path, st, mt)) {
+        dict_ref(d);
+        *out = d;
+        return 0;
+      }
+      c.erase(c.begin() + (long)i);  // the file changed: forget the old load
+      drop.push_back(d);
+      break;
     }
-    c.erase(c.begin() + (long)i);  // the file changed: forget the old load
-    dict_unref(d);
-    break;
   }
+  release_dropped();
   ngpu_dict *d = nullptr;
-  int rc = dict_load_file(e, path, st, &d);
-  if (rc) return rc;
-  if (c.size() >= kDictCache) {
-    dict_unref(c.front());
-    c.erase(c.begin());
+  if (int rc = dict_load_file(e, path, st, &d)) return rc;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    auto &c = e->dict_cache;
+    for (ngpu_dict *x : c)
+      if (same_file(x, path, st, mt)) {  // another thread loaded it meanwhile
+        dict_ref(x);
+        drop.push_back(d);
+        d = x;
+        break;
+      }
+    if (std::find(c.begin(), c.end(), d) == c.end()) {
+      for (size_t i = 0; i < c.size(); ++i)
+        if (c[i]->path == path) {  // an older load of the same path
+          drop.push_back(c[i]);
+          c.erase(c.begin() + (long)i);
+          break;
+        }
+      if (c.size() >= kDictCache) {
+        drop.push_back(c.front());
+        c.erase(c.begin());
+      }
+      dict_ref(d);  // the cache's reference
+      c.push_back(d);
+    }
   }
-  dict_ref(d);  // the cache's reference
-  c.push_back(d);
+  release_dropped();
   *out = d;
   return 0;
 }
@@ -380,8 +444,6 @@ int ngpu_dict_create(ngpu_engine *e, const void *records, uint64_t n, const void
                      uint32_t n_blobs, ngpu_dict **out) {
   if (!e || !out || (n && !records) || (n_blobs && !blob_table)) return NGPU_EINVAL;
   *out = nullptr;
-  std::lock_guard<std::mutex> g(e->mu);
-  DeviceGuard dg(e->device);
   return guarded([&] {
     return dict_from_records(e, (const uint8_t *)records, n, (const uint8_t *)blob_table, n_blobs,
                              out, nullptr);
@@ -395,8 +457,6 @@ int ngpu_dict_create_device(ngpu_engine *e, const uint8_t *d_digests, const uint
   if (!e || !out || (n && (!d_digests || !d_usize || !d_blob_index))) return NGPU_EINVAL;
   *out = nullptr;
   if (n_blobs == 0 || n_blobs > (1u << 20)) return fail(e, NGPU_EINVAL, "bad n_blobs %u", n_blobs);
-  std::lock_guard<std::mutex> g(e->mu);
-  DeviceGuard dg(e->device);
   return dict_from_arrays(e, d_digests, d_usize, d_blob_index, d_chunk_index, d_uoff, n, n_blobs,
                           hipMemcpyDeviceToDevice, out);
 }
@@ -407,12 +467,15 @@ uint64_t ngpu_dict_entries(const ngpu_dict *d) { return d ? d->dev.m : 0; }
 
 int ngpu_set_dict(ngpu_engine *e, ngpu_dict *d) {
   if (!e) return NGPU_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  if (int rc = dict_check(e, d)) return rc;
-  dict_ref(d);
-  ngpu_dict *old = e->dict;
-  e->dict = d;
-  dict_unref(old);  // packs that captured it keep their own reference
+  ngpu_dict *old;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = dict_check(e, d)) return rc;
+    dict_ref(d);
+    old = e->dict;
+    e->dict = d;
+  }
+  dict_unref(old);  // outside the lock; packs that captured it keep their own reference
   return 0;
 }
 
@@ -421,12 +484,12 @@ int ngpu_dict_load(ngpu_engine *e, const uint8_t *digests, const uint32_t *usize
   if (!e || (n && (!digests || !usize || !blob_index))) return NGPU_EINVAL;
   ngpu_dict *d = nullptr;
   {
-    std::lock_guard<std::mutex> g(e->mu);
-    DeviceGuard dg(e->device);
     uint32_t nb = 0;
     for (uint64_t i = 0; i < n; ++i) nb = std::max(nb, blob_index[i] + 1);
-    if (int rc = dict_from_arrays(e, digests, usize, blob_index, chunk_index, nullptr, n, nb,
-                                  hipMemcpyHostToDevice, &d))
+    if (int rc = guarded([&] {
+          return dict_from_arrays(e, digests, usize, blob_index, chunk_index, nullptr, n, nb,
+                                  hipMemcpyHostToDevice, &d);
+        }))
       return rc;
   }
   const int rc = ngpu_set_dict(e, n ? d : nullptr);

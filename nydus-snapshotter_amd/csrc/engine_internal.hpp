@@ -228,7 +228,7 @@ int dict_check(ngpu_engine *e, const ngpu_dict *d);
 ngpu_dict *default_dict(ngpu_engine *e);
 inline uint32_t dict_blobs(const ngpu_dict *d) { return d ? d->dev.n_blobs : 0; }
 uint64_t next_pow2(uint64_t x);
-// From 80-B RAFS v6 records in host memory on engine e's device (e->mu held).
+// From 80-B RAFS v6 records in host memory on engine e's device (own stream, no lock).
 int dict_from_records(ngpu_engine *e, const uint8_t *recs, uint64_t m, const uint8_t *blobs,
                       uint32_t n_blobs, ngpu_dict **out, const uint32_t *gids);
 int read_dict_bootstrap(ngpu_engine *e, const char *path, uint64_t file_size,

@@ -155,7 +155,8 @@ int node_dict_hits(ngpu_engine *e, ngpu_dict *d, const uint8_t *digests, uint64_
 
 namespace {
 
-// A node dict over records in host memory (each engine's mu taken in turn).
+// A node dict over records in host memory (each part built on its device's
+// own build stream, no engine lock held).
 int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint8_t *blobs,
                     uint32_t n_blobs, uint32_t mode, ngpu_dict **out) {
   ngpu_engine *e0 = node->eng[0];
@@ -199,7 +200,6 @@ int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint
   int rc = 0;
   for (uint32_t o = 0; o < W && !rc; ++o) {
     ngpu_engine *e = node->eng[o];
-    std::lock_guard<std::mutex> g(e->mu);
     DeviceGuard dg(e->device);
     ngpu_dict *p = nullptr;
     const uint8_t *pr = d->replicated ? recs : part_recs[o].data();
@@ -316,12 +316,7 @@ int ngpu_node_dict_open(ngpu_node *node, const char *path, uint32_t mode, ngpu_d
     ngpu_engine *e0 = node->eng[0];
     if (stat(path, &st) != 0) return fail(e0, NGPU_EIO, "stat chunk dict %s", path);
     std::vector<uint8_t> recs, blobs;
-    int rc;
-    {
-      std::lock_guard<std::mutex> g(e0->mu);
-      rc = read_dict_bootstrap(e0, path, (uint64_t)st.st_size, &recs, &blobs);
-    }
-    if (rc) return rc;
+    if (int rc = read_dict_bootstrap(e0, path, (uint64_t)st.st_size, &recs, &blobs)) return rc;
     return node_dict_build(node, recs.data(), recs.size() / 80, blobs.data(),
                            (uint32_t)(blobs.size() / 256), mode, out);
   });

@@ -18,6 +18,7 @@
 #include <functional>
 #include <map>
 #include <unordered_map>
+#include <unordered_set>
 
 namespace ngpu {
 
@@ -236,11 +237,24 @@ int build_tree(const std::vector<TarEntry> &entries, Tree *t) {
     by_path[path] = id;
     return id;
   };
-  auto detach = [&](int id) {
+  // A replaced node leaves the tree with its whole subtree: its descendants
+  // leave by_path too, so a later entry under the old path recreates its
+  // parents (or fails the parent check) instead of landing in the orphaned
+  // subtree and vanishing from the bootstrap.
+  std::function<void(int, const std::string &)> forget = [&](int id, const std::string &path) {
+    for (int c : nodes[id].kids) {
+      const std::string cp = path + "/" + nodes[c].name;
+      auto it = by_path.find(cp);
+      if (it != by_path.end() && it->second == c) by_path.erase(it);
+      if (nodes[c].dir) forget(c, cp);
+    }
+  };
+  auto detach = [&](int id, const std::string &path) {
     Node &nd = nodes[id];
     auto &k = nodes[nd.parent].kids;
     k.erase(std::remove(k.begin(), k.end(), id), k.end());
     nd.dead = true;
+    if (nd.dir) forget(id, path);
   };
   std::function<int(const std::string &)> dir_node = [&](const std::string &path) -> int {
     auto it = by_path.find(path);
@@ -269,7 +283,7 @@ int build_tree(const std::vector<TarEntry> &entries, Tree *t) {
         set_meta(inos[nodes[it->second].ino], e);
         continue;
       }
-      if (it != by_path.end()) detach(it->second);
+      if (it != by_path.end()) detach(it->second, e.path);
       Ino in;
       set_meta(in, e);
       inos.push_back(in);
@@ -284,7 +298,7 @@ int build_tree(const std::vector<TarEntry> &entries, Tree *t) {
                          e.path.c_str(), e.link.c_str());
       target_ino = nodes[tg->second].ino;
     }
-    if (it != by_path.end()) detach(it->second);
+    if (it != by_path.end()) detach(it->second, e.path);
     if (target_ino >= 0) {
       add(parent, e.path, false, target_ino);
       continue;
@@ -920,6 +934,8 @@ int write_v5(Tree &t, const RafsLayerInfo &info, std::vector<uint8_t> *outp) {
 
 int write_rafs(const std::vector<TarEntry> &entries, const RafsLayerInfo &info,
                std::vector<uint8_t> *out) {
+  if (!info.chunk_size || (info.chunk_size & (info.chunk_size - 1)))
+    return host_fail(NGPU_EINVAL, "bootstrap: invalid chunk size 0x%x", info.chunk_size);
   Tree t;
   if (int rc = build_tree(entries, &t)) return rc;
   if (info.refs.size() != info.file_of.size())
@@ -942,7 +958,10 @@ struct V6Reader {
   uint64_t n, base;
   std::unordered_map<uint64_t, size_t> where;  // (blob << 40 | blkaddr) -> chunk table row
   std::vector<RafsV6ChunkInfo> table;
-  std::unordered_map<uint64_t, bool> on_path;
+  // every directory nid walked so far: a bootstrap whose directories share a
+  // subdirectory (a DAG) or loop is rejected, so a few KiB cannot make the
+  // walk exponential (2^depth visits) or endless
+  std::unordered_set<uint64_t> dirs_seen;
 
   int inode(uint64_t nid, RafsNode *nd, uint16_t *lay, uint64_t *body, uint32_t *iu) {
     const uint64_t o = base + nid * 32;
@@ -1020,6 +1039,9 @@ struct V6Reader {
   int walk(uint64_t nid, const std::string &path, std::vector<RafsNode> *nodes, uint32_t chunk_size,
            int depth, RafsNode *root = nullptr) {
     if (depth > 4096) return host_fail(NGPU_EFORMAT, "directory tree too deep");
+    if (!dirs_seen.insert(nid).second)
+      return host_fail(NGPU_EFORMAT, "directory nid %llu reached twice (cycle or shared subtree)",
+                       (unsigned long long)nid);
     RafsNode me;
     uint16_t lay;
     uint64_t body;
@@ -1029,7 +1051,6 @@ struct V6Reader {
     if (root) *root = me;
     std::string d;
     if (int rc = data(lay, iu, body, me.size, &d)) return rc;
-    on_path[nid] = true;
     for (uint64_t b = 0; b < d.size(); b += kBlk) {
       const uint8_t *blk = (const uint8_t *)d.data() + b;
       const uint64_t bl = std::min<uint64_t>(kBlk, d.size() - b);
@@ -1048,7 +1069,8 @@ struct V6Reader {
         if (no > end || end > bl) return host_fail(NGPU_EFORMAT, "bad dirent name");
         std::string name((const char *)blk + no, strnlen((const char *)blk + no, end - no));
         if (name == "." || name == "..") continue;
-        if (on_path.count(cn) && on_path[cn]) return host_fail(NGPU_EFORMAT, "directory cycle");
+        if (nodes->size() >= n / 12 + 1)  // each node is a 12-B dirent of this bootstrap
+          return host_fail(NGPU_EFORMAT, "more dirents than the bootstrap can hold");
         RafsNode c;
         uint16_t cl;
         uint64_t cb;
@@ -1087,7 +1109,6 @@ struct V6Reader {
         }
       }
     }
-    on_path[nid] = false;
     return 0;
   }
 };
@@ -1123,6 +1144,12 @@ int read_v5(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
     if (idx == 0 || idx > ient || !get(p, n, ito + 4 * (idx - 1), &o)) return 0;
     return (uint64_t)o << 3;
   };
+  // every inode record reached so far: each v5 record (one per path, hardlinks
+  // included) belongs to one directory's child range, so a record reached
+  // twice -- overlapping child ranges, a directory listing itself or an
+  // ancestor -- is rejected instead of walked again (a few KiB could otherwise
+  // make 2^depth visits)
+  std::vector<bool> seen((size_t)ient + 1, false);
   std::function<int(uint64_t, const std::string &, int)> walk =
       [&](uint64_t idx, const std::string &path, int depth) -> int {
     if (depth > 4096) return host_fail(NGPU_EFORMAT, "directory tree too deep");
@@ -1133,6 +1160,10 @@ int read_v5(const uint8_t *p, uint64_t n, std::vector<RafsNode> *nodes,
     for (uint64_t k = cidx; k < (uint64_t)cidx + ccnt; ++k) {
       const uint64_t c = rec_off(k);
       if (!c || c > n || n - c < 128) return host_fail(NGPU_EFORMAT, "inode %llu out of bounds", (unsigned long long)k);
+      if (k == 1 || seen[k])
+        return host_fail(NGPU_EFORMAT, "inode record %llu reached twice (cycle or shared subtree)",
+                         (unsigned long long)k);
+      seen[k] = true;
       RafsNode nd;
       uint64_t ino = 0, size = 0, fl = 0, mt = 0;
       uint32_t uid = 0, gid = 0, mode = 0, nlink = 0, cc = 0, rdev = 0, nsec = 0;

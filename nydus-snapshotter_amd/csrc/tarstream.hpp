@@ -234,7 +234,11 @@ class TarScanner {
         return 0;
       case 'L':
       case 'K':
-        if (rec_ && size <= (1u << 20)) {  // captured: the next entry's long name / link
+        // a long name / link the tree needs but will not capture would leave
+        // the next entry under its truncated ustar name: fail like Go's
+        // archive/tar (ErrFieldTooLong)
+        if (rec_ && size > (1u << 20)) return NGPU_ETAR;
+        if (rec_) {  // captured: the next entry's long name / link
           pax_.clear();
           remain_ = size;
           pad_ = padded - size;

@@ -68,10 +68,15 @@ Error compressor_of(const std::string &s, uint32_t *out) {
 
 // tool.DetectFeatures (pkg/converter/tool/feature.go:114-146): the features a
 // Pack requires, checked once per process against what the builder supports.
-// The GPU builder supports tar-rafs only, so `--batch-size` and `--encrypt`
-// are ignored with the reference's warning, exactly as with a nydus-image too
-// old for them; a later Pack requiring a different set fails ("features
-// changed"), as the reference's process-global sync.Once makes it.
+// The builder emulated is the pinned nydus-image v2.3.0
+// (misc/snapshotter/Dockerfile:5), whose `create -h` lists all three
+// features (feature_test.go:255, 379), so all are detected and none is
+// ignored.  The GPU builder then refuses what it does not implement
+// (`--batch-size`, `--encrypt`) with NGPU_EUNSUPP at Pack(): the reference
+// passes both flags to the builder unconditionally (builder.go:137-142), so it
+// never returns a blob without them.  A later Pack requiring a different set
+// fails ("features changed"), as the reference's process-global sync.Once
+// makes it.
 const char *const kFeatureTar2Rafs = "--type tar-rafs";
 const char *const kFeatureBatchSize = "--batch-size";
 const char *const kFeatureEncrypt = "--encrypt";
@@ -84,15 +89,9 @@ Error detect_features(const std::vector<std::string> &required, std::vector<std:
   if (!g_feat_done) {
     g_feat_done = true;
     g_feat_required = required;
-    for (const std::string &f : required) {
-      if (f == kFeatureTar2Rafs) {
+    for (const std::string &f : required)
+      if (f == kFeatureTar2Rafs || f == kFeatureBatchSize || f == kFeatureEncrypt)
         g_feat_detected.push_back(f);
-      } else {
-        fprintf(stderr,
-                "level=warning msg=\"the feature '%s' is ignored, it requires higher version of "
-                "nydus-image\" (the GPU builder does not implement it)\n", f.c_str());
-      }
-    }
   }
   if (g_feat_required != required) {
     std::string a, b;
@@ -309,6 +308,13 @@ Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser>
   }
   const bool batch = std::find(detected.begin(), detected.end(), kFeatureBatchSize) != detected.end();
   if (batch && fv != "6") return err(NGPU_EINVAL, "'--batch-size' can only be supported by fs version 6");
+  // v2.3.0 would write batch chunks (several small chunks compressed as one,
+  // a different blob.meta) or an encrypted blob; this builder writes neither,
+  // so it refuses instead of returning a blob the reference would not produce
+  if (batch)
+    return err(NGPU_EUNSUPP, "batch chunks (--batch-size " + opt.BatchSize +
+                                 ") not implemented by the GPU builder");
+  if (opt.Encrypt) return err(NGPU_EUNSUPP, "blob encryption (--encrypt) not implemented by the GPU builder");
   uint32_t comp = 0;
   if (Error e = compressor_of(opt.Compressor, &comp)) return e;
   ngpu_engine *e = nullptr;

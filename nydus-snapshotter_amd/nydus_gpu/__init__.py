@@ -5,7 +5,7 @@ replaces the digest/dedup stage that pkg/converter hands to
 `nydus-image create` (pkg/converter/tool/builder.go:148-178).
 """
 from ._lib import (CHUNK_DTYPE, COMPRESSORS, DEFAULT_DICT, DICT, DIGESTED, DIGESTERS,  # noqa: F401
-                   ECANCELED, EDEVICE, EINVAL, ENODEV, EUNSUPP, UNHASHED,
+                   ECANCELED, EDEVICE, EFORMAT, EINVAL, ENODEV, EUNSUPP, UNHASHED,
                    ENOTFOUND, EXPORTS, FLAG_GRID_STAGES, HIT_DTYPE, FdWriter, INTRA, KIND_NAMES, LAYER_STATS_DTYPE, MISS, NEW,
                    RESULT_DTYPE, TOC_ENTRY_DTYPE, ChunkDict, Engine, Node, NODE_DICT_PARTITION,
                    NODE_DICT_REPLICATE, NgpuError, blob_write, chunk_table,
@@ -14,4 +14,4 @@ from ._lib import (CHUNK_DTYPE, COMPRESSORS, DEFAULT_DICT, DICT, DIGESTED, DIGES
 __all__ = ["Engine", "Node", "NODE_DICT_PARTITION", "NODE_DICT_REPLICATE", "ChunkDict", "DEFAULT_DICT", "NgpuError", "tar_chunks", "chunk_table", "lib", "CHUNK_DTYPE",
            "RESULT_DTYPE", "HIT_DTYPE", "MISS", "NEW", "INTRA", "DICT", "DIGESTED", "UNHASHED", "KIND_NAMES", "DIGESTERS", "EXPORTS",
            "COMPRESSORS", "TOC_ENTRY_DTYPE", "FdWriter", "blob_write", "unpack_entry", "unpack", "merge", "rafs_dump",
-           "FLAG_GRID_STAGES", "EINVAL", "ENODEV", "EUNSUPP", "ENOTFOUND", "ECANCELED", "EDEVICE"]
+           "FLAG_GRID_STAGES", "EINVAL", "EFORMAT", "ENODEV", "EUNSUPP", "ENOTFOUND", "ECANCELED", "EDEVICE"]

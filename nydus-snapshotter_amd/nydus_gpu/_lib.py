@@ -25,7 +25,7 @@ NEW, INTRA, DICT, DIGESTED, UNHASHED = 0, 1, 2, 3, 4
 ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ETAR", -5: "EUNSUPP",
           -6: "ENODEV", -7: "EIO", -8: "EFORMAT", -9: "ENOTFOUND", -10: "ECANCELED",
           -11: "EDEVICE"}
-EINVAL, EUNSUPP, ENODEV, ENOTFOUND, ECANCELED, EDEVICE = -1, -5, -6, -9, -10, -11
+EINVAL, EUNSUPP, ENODEV, EFORMAT, ENOTFOUND, ECANCELED, EDEVICE = -1, -5, -6, -8, -9, -10, -11
 
 # PackOption.Compressor -> TOCEntry flag values (pkg/converter/types.go:22-31);
 # "" is nydus-image's default (zstd).

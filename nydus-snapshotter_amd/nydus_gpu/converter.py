@@ -36,7 +36,7 @@ import threading
 
 import logging
 
-from ._lib import (COMPRESSORS, DICT, ECANCELED, ENOTFOUND, NEW, Engine, NgpuError, merge, unpack,
+from ._lib import (COMPRESSORS, DICT, ECANCELED, ENOTFOUND, EUNSUPP, NEW, Engine, NgpuError, merge, unpack,
                    unpack_entry)
 
 _log = logging.getLogger("nydus_gpu.converter")
@@ -51,7 +51,13 @@ _ENGINES = {}
 
 
 class ConverterError(RuntimeError):
-    pass
+    """A Go `error` of pkg/converter; `code` is the NGPU_E* code when the
+    library refused the request (EUNSUPP: an option the builder does not
+    implement)."""
+
+    def __init__(self, msg="", code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 class ErrNotFound(ConverterError):
@@ -215,11 +221,15 @@ class _PackWriteCloser:
 
 # tool.DetectFeatures (pkg/converter/tool/feature.go:114-146): a Pack's
 # required features are checked once per process against the builder's.  The
-# GPU builder supports tar-rafs only: `--batch-size` and `--encrypt` are
-# ignored with the reference's warning, exactly as with a nydus-image too old
-# for them, and a later Pack requiring another set fails ("features changed").
+# builder emulated is the pinned nydus-image v2.3.0 (misc/snapshotter/
+# Dockerfile:5), whose `create -h` lists all three (feature_test.go:255, 379),
+# so every feature is detected.  Pack() then refuses the two this builder does
+# not implement (batch chunks, encryption) with EUNSUPP: the reference hands
+# both flags to the builder unconditionally (builder.go:137-142) and never
+# returns a blob without them.  A later Pack requiring another set fails
+# ("features changed").
 FeatureTar2Rafs, FeatureBatchSize, FeatureEncrypt = "--type tar-rafs", "--batch-size", "--encrypt"
-_BUILDER_FEATURES = {FeatureTar2Rafs}
+_BUILDER_FEATURES = {FeatureTar2Rafs, FeatureBatchSize, FeatureEncrypt}
 _FEATURES = {"required": None, "detected": None}
 _FEATURES_MU = threading.Lock()
 
@@ -268,6 +278,14 @@ def Pack(dest: BinaryIO, opt: PackOption) -> _PackWriteCloser:
                              "layer in blob.meta; the GPU builder packs tar-rafs only")
     if FeatureBatchSize in detected and fs != "6":
         raise ConverterError("'--batch-size' can only be supported by fs version 6")
+    # v2.3.0 would write batch chunks (small chunks compressed as one, another
+    # blob.meta) or an encrypted blob: refused, never silently dropped
+    if FeatureBatchSize in detected:
+        raise ConverterError(f"batch chunks (--batch-size {opt.BatchSize}) not implemented by the "
+                             "GPU builder", code=EUNSUPP)
+    if FeatureEncrypt in detected:
+        raise ConverterError("blob encryption (--encrypt) not implemented by the GPU builder",
+                             code=EUNSUPP)
     return _PackWriteCloser(dest, opt)
 
 

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-4 check: GPU suite (optionally a -k filter), smoke, default bench line.
+# usage: scripts/gpu_r4.sh TAG [pytest -k expression]
+set -u
+TAG=${1:-r4}
+KEXPR=${2:-}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+ok() { local rc=$1 what=$2; echo "$what rc=$rc"; if [ "$rc" -ne 0 ]; then echo "stopping after $what"; exit "$rc"; fi; }
+if [ -n "$KEXPR" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread -k "$KEXPR" > "$OUT/pytest_gpu.log" 2>&1
+else
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+fi
+ok $? pytest-gpu
+tail -1 "$OUT/pytest_gpu.log"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+ok $? smoke
+timeout -k 10 600 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+ok $? bench
+python3 -c "import json; d=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1]); print(d['value'], d['roofline']['frac'], d['cpu_baseline']['value'])"

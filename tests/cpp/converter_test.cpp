@@ -194,6 +194,20 @@ int main(int argc, char **argv) {
   re = Pack(sink, ref, &w);
   REQUIRE(re.msg == "oci ref can only be supported by fs version 6", "OCIRef v5: %s", re.msg.c_str());
 
+  // BatchSize / Encrypt: the pinned v2.3.0 builder honours both
+  // (builder.go:137-142), so no Pack may return rc 0 without them.  This
+  // process detected its features on the first Pack (tar-rafs only), so the
+  // reference's "features changed" comes first; tests/test_host.py checks the
+  // NGPU_EUNSUPP refusal with a fresh detection.
+  PackOption enc;
+  enc.Encrypt = true;
+  Error ee = Pack(sink, enc, &w);
+  REQUIRE(ee.code != 0 && !w, "Encrypt must not pack: %s", ee.msg.c_str());
+  PackOption batch;
+  batch.BatchSize = "0x100000";
+  Error be = Pack(sink, batch, &w);
+  REQUIRE(be.code != 0 && !w, "BatchSize must not pack: %s", be.msg.c_str());
+
   // TestUnpack (converter_test.go:607-635): OCI tar -> Pack -> Unpack, same sha256
   if (argc > 6) {
     const std::vector<uint8_t> ociTar = read_file(argv[6]);

@@ -151,6 +151,87 @@ def test_dict_open_is_cached_per_unchanged_file(tars, oracle, tmp_path):
         d.release()
 
 
+def test_dict_reload_does_not_stall_concurrent_packs(tars, oracle, tmp_path):
+    """A thread rewrites the ChunkDictPath file and reopens it (a 2M-entry
+    bootstrap: parse, upload and table build) while 3 threads run Packs on the
+    same engine against the dict they opened first.  Every Pack equals the
+    oracle, and Pack closes complete while a reload is in flight: the load runs
+    outside the engine lock on its own stream (round 3 held e->mu across it and
+    its stream syncs)."""
+    cs = 0x10000
+    eng = nydus_gpu.Engine(chunk_size=cs)
+    try:
+        recs = _pack_records(eng, tars["chunk_dict"])
+        rng = np.random.default_rng(11)
+
+        def with_filler(seed):
+            f = np.zeros(2_000_000, dtype=recs.dtype)
+            f["block_id"] = np.random.default_rng(seed).integers(0, 256, (len(f), 32), dtype=np.uint8)
+            f["uncompressed_size"] = cs
+            f["index"] = np.arange(len(f), dtype=np.uint32) + 100_000
+            return np.concatenate([recs, f])
+
+        path = str(tmp_path / "dict")
+        _bootstrap(path, with_filler(1), cs)
+        d0 = eng.dict_open(path)
+        tar = tars["oci_lower"]
+        _, dig, dec = _oracle_expect(oracle, tar, cs, "blake3", recs)
+        stop = threading.Event()
+        reloads, closes, errors = [], [], []
+
+        def reloader():
+            try:
+                k = 2
+                while not stop.is_set() and len(reloads) < 6:
+                    _bootstrap(path, with_filler(k), cs)
+                    t0 = time.monotonic()
+                    d = eng.dict_open(path)
+                    reloads.append((t0, time.monotonic()))
+                    assert d.entries == len(recs) + 2_000_000
+                    d.release()
+                    k += 1
+            except Exception as ex:  # pragma: no cover - reported below
+                errors.append(repr(ex))
+
+        def packer(i):
+            try:
+                r = np.random.default_rng(100 + i)
+                while not stop.is_set():
+                    w = eng.pack(dict=d0)
+                    pos = 0
+                    while pos < len(tar):
+                        k = int(r.integers(1, 300_000))
+                        w.write(tar[pos:pos + k])
+                        pos += k
+                    t0 = time.monotonic()
+                    ch, out, st = w.close()
+                    closes.append((t0, time.monotonic()))
+                    _same(out, dig, dec, f"packer {i}")
+            except Exception as ex:  # pragma: no cover - reported below
+                errors.append(repr(ex))
+
+        ts = [threading.Thread(target=packer, args=(i,)) for i in range(3)]
+        rt = threading.Thread(target=reloader)
+        for t in ts:
+            t.start()
+        rt.start()
+        rt.join(timeout=90)
+        stop.set()
+        for t in ts:
+            t.join(timeout=30)
+        d0.release()
+        assert not errors, errors
+        assert not rt.is_alive() and not any(t.is_alive() for t in ts)
+        assert len(reloads) == 6 and len(closes) >= 6
+        inside = sum(1 for a, b in closes for r0, r1 in reloads if r0 <= a and b <= r1)
+        longest = max(b - a for a, b in reloads)
+        print(f"reloads {len(reloads)} (longest {longest * 1e3:.0f} ms), closes {len(closes)}, "
+              f"{inside} completed inside a reload")
+        assert inside >= 1, "every Pack close waited for the dict reload"
+    finally:
+        eng.close()
+
+
 def test_incompatible_dict_is_rejected(tars, tmp_path):
     """nydus-image rejects a chunk-dict bootstrap whose digester / chunk size /
     RAFS version differs from the build's ([nydus v2.3.0]

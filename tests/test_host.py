@@ -220,13 +220,16 @@ def test_product_never_reaches_the_oracle():
 
 
 def test_pack_option_features_and_ociref(caplog):
-    """PackOption honesty (convert_unix.go:325-356, tool/feature.go:114-146):
-    BatchSize / Encrypt are features the GPU builder does not implement, so
-    DetectFeatures ignores them with the reference's own warning (as with a
-    nydus-image too old for them); the detection is once per process and a
-    later Pack with another required set fails "features changed"; OCIRef gets
-    the reference's fs-version error on v5 and an accurate refusal on v6.
-    Everything here fails before the engine is created (no GPU needed)."""
+    """PackOption parity with the pinned builder (convert_unix.go:325-356,
+    tool/feature.go:114-146, builder.go:137-142): nydus-image v2.3.0 supports
+    `--batch-size` and `--encrypt` (feature_test.go:255, 379), so DetectFeatures
+    detects them with no warning, and the reference passes both flags on.  The
+    GPU builder implements neither, so Pack() refuses them with EUNSUPP -- no
+    option combination returns a blob v2.3.0 would not produce.  The
+    reference's own checks keep their order: the v5 batch-size error, the
+    once-per-process detection ("features changed"), and OCIRef's fs-version
+    error on v5 with an accurate refusal on v6.  Everything here fails before
+    the engine is created (no GPU needed)."""
     import io
     import logging
     from nydus_gpu import converter as cv
@@ -244,23 +247,30 @@ def test_pack_option_features_and_ociref(caplog):
     cv._reset_feature_detection()
     try:
         with caplog.at_level(logging.WARNING, logger=cv._log.name):
-            pack(BatchSize="0x100000", FsVersion="6")
-        assert "the feature '--batch-size' is ignored, it requires higher version of nydus-image" in caplog.text
-        # same required set again: no error, no second warning
-        caplog.clear()
-        pack(BatchSize="0x200000")
-        assert "ignored" not in caplog.text
-        # the ignored feature is not detected, so the v5 check does not fire
-        pack(BatchSize="0x100000", FsVersion="5")
+            with pytest.raises(cv.ConverterError, match=r"batch chunks \(--batch-size 0x100000\) not implemented") as ei:
+                pack(BatchSize="0x100000", FsVersion="6")
+        assert ei.value.code == nydus_gpu.EUNSUPP
+        assert "ignored" not in caplog.text  # v2.3.0 has the feature: detected, no warning
+        # the detected feature makes the reference's v5 check fire first
+        with pytest.raises(cv.ConverterError, match="^'--batch-size' can only be supported by fs version 6$"):
+            pack(BatchSize="0x200000", FsVersion="5")
+        # detection is once per process: another required set fails
         with pytest.raises(cv.ConverterError, match="features changed"):
             pack()
         with pytest.raises(cv.ConverterError, match="features changed"):
             pack(BatchSize="0x100000", Encrypt=True)
 
         cv._reset_feature_detection()
-        with caplog.at_level(logging.WARNING, logger=cv._log.name):
+        with pytest.raises(cv.ConverterError, match=r"blob encryption \(--encrypt\) not implemented") as ei:
             pack(Encrypt=True)
-        assert "the feature '--encrypt' is ignored" in caplog.text
+        assert ei.value.code == nydus_gpu.EUNSUPP
+        cv._reset_feature_detection()
+        with pytest.raises(cv.ConverterError, match="not implemented") as ei:
+            pack(Encrypt=True, BatchSize="0x100000")
+        assert ei.value.code == nydus_gpu.EUNSUPP
+        # BatchSize "0" / "" is no batch feature at all (convert_unix.go:333)
+        cv._reset_feature_detection()
+        pack(BatchSize="0")
 
         cv._reset_feature_detection()
         with pytest.raises(cv.ConverterError, match="^oci ref can only be supported by fs version 6$"):

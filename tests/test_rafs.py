@@ -907,3 +907,152 @@ def test_random_trees_reencode_and_unpack(oracle, seed):
                                              s.pax_headers.get("SCHILY.xattr.user.k")):
             assert m.pax_headers.get("SCHILY.xattr.user.k") == s.pax_headers.get("SCHILY.xattr.user.k")
     assert set(src) <= seen
+
+
+# ---- untrusted bootstraps shaped as a DAG -----------------------
+
+def _chain_tar(depth):
+    """x/x/.../x (depth levels), each level with a sibling directory y and a
+    small file, so every directory's dirents hold one x and one y."""
+    ents, p = [], ""
+    for _ in range(depth):
+        p = p + "/x" if p else "x"
+        ents.append((p, "dir", None))
+        ents.append((p + "/y", "dir", None))
+        ents.append((p + "/f", "file", b"z" * 100))
+    return _tar(ents)
+
+
+def test_bootstrap_shared_subtree_is_rejected_v6(oracle):
+    """Point every y dirent of a 24-level v6 tree at its sibling x: each
+    directory is then reachable along 2^k paths.  read_rafs (Unpack, Merge,
+    inspect) must reject the second arrival at a directory nid with
+    NGPU_EFORMAT at once instead of walking 2^24 subtrees."""
+    import time
+    blob, *_ = _pack(oracle, _chain_tar(24), cs=0x10000, fs=6, comp="none")
+    boot = bytearray(_boot(blob))
+    assert len(nydus_gpu.rafs_dump(bytes(boot))["inodes"]) == 3 * 24 + 1
+    root = struct.unpack_from("<H", boot, 1024 + 14)[0]
+    base = struct.unpack_from("<I", boot, 1024 + 40)[0] * 4096
+    patched, nid = 0, root
+    while True:
+        ino = rf._v6_inode(bytes(boot), base, nid)
+        kids = dict(rf._v6_dirents(bytes(boot), ino))
+        if b"x" not in kids:
+            break
+        # rewrite the y dirent's nid in place (dirent = nid u64, nameoff u16, ...)
+        ino_data_start = ino["iu"] * 4096 if ino["layout"] == 0 else ino["body"]
+        blk = bytes(boot[ino_data_start:ino_data_start + max(ino["size"], 12)])
+        n = struct.unpack_from("<H", blk, 8)[0] // 12
+        for i in range(n):
+            cn, no = struct.unpack_from("<QH", blk, 12 * i)
+            end = struct.unpack_from("<H", blk, 12 * (i + 1) + 8)[0] if i + 1 < n else len(blk)
+            if blk[no:end].split(b"\0")[0] == b"y":
+                struct.pack_into("<Q", boot, ino_data_start + 12 * i, kids[b"x"])
+                patched += 1
+        nid = kids[b"x"]
+    assert patched == 23  # every level but the deepest (no x below it)
+    t0 = time.monotonic()
+    with pytest.raises(nydus_gpu.NgpuError) as e:
+        nydus_gpu.rafs_dump(bytes(boot))
+    assert e.value.code == nydus_gpu.EFORMAT and "reached twice" in str(e.value)
+    assert time.monotonic() - t0 < 5
+
+
+def test_bootstrap_shared_subtree_is_rejected_v5(oracle):
+    """The v5 form: every y record's inode-table entry made to point at its
+    sibling x's record, so x's child range is listed from two parents at
+    every level.  A record index reached twice is NGPU_EFORMAT."""
+    import time
+    blob, *_ = _pack(oracle, _chain_tar(24), cs=0x10000, fs=5, comp="none")
+    boot = bytearray(_boot(blob))
+    assert len(nydus_gpu.rafs_dump(bytes(boot))["inodes"]) == 3 * 24 + 1
+    ito, = struct.unpack_from("<Q", boot, 32)
+    ient, = struct.unpack_from("<I", boot, 56)
+    offs = list(struct.unpack_from(f"<{ient}I", boot, ito))
+    by_name = {}
+    for idx in range(1, ient + 1):
+        off = offs[idx - 1] << 3
+        nsz, = struct.unpack_from("<H", boot, off + 100)
+        cidx, ccnt = struct.unpack_from("<II", boot, off + 92)
+        by_name.setdefault(bytes(boot[off + 128:off + 128 + nsz]), []).append((idx, cidx, ccnt))
+    # each directory's children are consecutive records: pair x and y by parent range
+    xs = {c for c in by_name[b"x"]}
+    patched = 0
+    for yi, _c, _n in by_name[b"y"]:
+        for xi, _c2, _n2 in xs:
+            if abs(xi - yi) <= 2:  # siblings sit side by side in the child range
+                struct.pack_into("<I", boot, ito + 4 * (yi - 1), offs[xi - 1])
+                patched += 1
+                break
+    assert patched >= 23
+    t0 = time.monotonic()
+    with pytest.raises(nydus_gpu.NgpuError) as e:
+        nydus_gpu.rafs_dump(bytes(boot))
+    assert e.value.code == nydus_gpu.EFORMAT and "reached twice" in str(e.value)
+    assert time.monotonic() - t0 < 5
+
+
+def test_replaced_directory_forgets_its_subtree(oracle):
+    """a/, a/x/, then a file `a`, then a/x/y: the file replaces the directory
+    and its subtree; a/x/y's parent `a` is now a file, so the Pack fails the
+    parent check (NGPU_EINVAL) instead of attaching a/x/y to the orphaned
+    a/x and silently leaving it out of the bootstrap."""
+    tar = _tar([("a", "dir", None), ("a/x", "dir", None), ("a", "file", b"1"),
+                ("a/x/y", "file", b"2")])
+    with pytest.raises(nydus_gpu.NgpuError) as e:
+        _pack(oracle, tar, cs=0x10000, fs=6, comp="none")
+    assert e.value.code == nydus_gpu.EINVAL and "parent is not a directory" in str(e.value)
+    # a directory replaced by a directory keeps its children (OCI semantics)
+    tar = _tar([("a", "dir", None), ("a/x", "dir", None), ("a", "dir", None),
+                ("a/x/y", "file", b"2")])
+    blob, *_ = _pack(oracle, tar, cs=0x10000, fs=6, comp="none")
+    paths = {n["path"] for n in nydus_gpu.rafs_dump(_boot(blob))["inodes"]}
+    assert {"/a", "/a/x", "/a/x/y"} <= paths
+
+
+def test_blob_write_chunk_size_zero_is_the_default():
+    """ngpu_blob_options.chunk_size 0 means 1 MiB (the tar re-scan's default);
+    other non-powers of two are NGPU_EINVAL, never a divide by zero."""
+    tar = layers.oci_upper_tar_go(1)
+    ch = nydus_gpu.tar_chunks(tar, 0x100000)
+    res = np.zeros(len(ch), nydus_gpu.RESULT_DTYPE)
+    res["kind"] = nydus_gpu.NEW
+    res["index"] = np.arange(len(ch))
+    res["digest"][:, 0] = np.arange(len(ch)) + 1
+    st = dict(chunks=len(ch), new_chunks=len(ch), intra_chunks=0, dict_chunks=0, new_bytes=0,
+              own_blob_index=0, blobs=1, uncompressed_size=0)
+    out = io.BytesIO()
+    nydus_gpu.blob_write(tar, ch, res, st, out, compressor="none", chunk_size=0)
+    assert len(out.getvalue()) > 0
+    for bad in (0x1001, 0x800, 0x2000000):
+        with pytest.raises(nydus_gpu.NgpuError) as e:
+            nydus_gpu.blob_write(tar, ch, res, st, io.BytesIO(), compressor="none", chunk_size=bad)
+        assert e.value.code == nydus_gpu.EINVAL
+
+
+def test_oversized_gnu_long_name_fails_the_bootstrap():
+    """A GNU 'L' record longer than 1 MiB is not captured; while the bootstrap's
+    entries are recorded that is NGPU_ETAR (Go's archive/tar: ErrFieldTooLong),
+    not an entry silently filed under its truncated 100-byte ustar name
+    (ADVICE r3 low).  The chunk walk alone still skips it."""
+    name = "d/" + "n" * (1 << 20) + "/file"
+    out = io.BytesIO()
+    with tarfile.open(fileobj=out, mode="w", format=tarfile.GNU_FORMAT) as tw:
+        ti = tarfile.TarInfo("d")
+        ti.type = tarfile.DIRTYPE
+        tw.addfile(ti)
+        ti = tarfile.TarInfo(name)
+        ti.size = 10
+        tw.addfile(ti, io.BytesIO(b"0123456789"))
+    tar = out.getvalue()
+    ch = nydus_gpu.tar_chunks(tar, 0x100000)
+    assert len(ch) == 1
+    res = np.zeros(len(ch), nydus_gpu.RESULT_DTYPE)
+    res["kind"] = nydus_gpu.NEW
+    res["digest"][:, 0] = 1
+    st = dict(chunks=1, new_chunks=1, intra_chunks=0, dict_chunks=0, new_bytes=0,
+              own_blob_index=0, blobs=1, uncompressed_size=0)
+    with pytest.raises(nydus_gpu.NgpuError) as e:
+        nydus_gpu.blob_write(tar, ch, res, st, io.BytesIO(), compressor="none")
+    assert e.value.code in (nydus_gpu.EINVAL, -4)  # the re-scan's ETAR, reported by blob_write
