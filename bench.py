@@ -254,7 +254,7 @@ WORKLOADS = {
     # mid-size layers (the auto rule hashes them one leaf per lane or per lane quad)
     **{f"l{m}m": dict(desc=f"{m} MiB layer, 4 MiB files, 1 MiB chunks, blake3", n_files=m // 4,
                       file_size=4 * MiB, chunk=MiB, digester="blake3", layers=1)
-       for m in (8, 16, 24, 32, 48, 64, 128)},
+       for m in (8, 16, 24, 32, 48, 64, 128, 256, 512, 1024, 2048)},
 }
 
 
@@ -273,7 +273,8 @@ def pool_content(torch, ids, S, device="cuda"):
 
 def plant_pool(torch, buf, ch, stride, wl, seed):
     """C4/C5: overwrite ~30% of the chunks with pool contents (rank-seeded
-    choice of chunks and of content ids)."""
+    choice of chunks and of content ids).  -> ({"chunks": planted chunk ids,
+    "content": their pool content ids}, count)."""
     S = wl["chunk"]
     per_file = wl["file_size"] // S
     n = len(ch)
@@ -287,7 +288,7 @@ def plant_pool(torch, buf, ch, stride, wl, seed):
         k = torch.from_numpy(sel[a:a + step] % per_file).cuda()
         rows[f, k] = pool_content(torch, torch.from_numpy(src[a:a + step]).cuda(), S)
     torch.cuda.synchronize()
-    return None, len(sel)
+    return {"chunks": sel, "content": src}, len(sel)
 
 
 def pool_digests(torch, nydus_gpu, wl, device):
@@ -540,6 +541,44 @@ def pmc_traffic(path, workload, kernel):
     return d["traffic_bytes"], os.path.relpath(path, ROOT)
 
 
+def newest_profile(name):
+    """The newest committed profiles/r*/<name> (or None)."""
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)))
+    if not cands:
+        return None, None
+    return json.load(open(cands[-1])), os.path.relpath(cands[-1], ROOT)
+
+
+def mix_roofline(roof, achieved, kernel, workload):
+    """the ceiling of the kernel's own instruction mix and
+    the clock the chip holds under it.  peak_mix = 1024 SIMDs x 64 lanes x
+    2.4 GHz / (issue cycles per algorithmic op of the compiled hot loop:
+    tools/isa_mix.py -> profiles/r*/isa_mix_b3_groups.json; 3-operand ops 4
+    cycles per wave64 instruction, 2-operand logic/add 2, as measured on this
+    chip); held_clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / kernel time from a PMC
+    pass of the same command (scripts/gpu_pmc_clock.sh ->
+    profiles/r*/pmc_clock_<workload>.json, MI355X_MICROARCH.md "DVFS
+    give-back").  frac_mix_at_held_clock = achieved / (peak_mix x held / 2.4):
+    the issue efficiency left once the clock is accounted for."""
+    if not kernel.startswith("b3_groups"):
+        return
+    mix, src = newest_profile("isa_mix_b3_groups.json")
+    if mix:
+        pm = mix["peak_mix_tops_at_2p4ghz"] * 1e12
+        roof.update({"peak_mix": round(pm / 1e12, 3), "frac_mix": round(achieved / pm, 4),
+                     "mix": {"four_cycle_ops_per_compression": mix["per_compression"]["four_cycle"],
+                             "two_cycle_ops_per_compression": mix["per_compression"]["two_cycle"],
+                             "cycles_per_algorithmic_op": mix["cycles_per_algorithmic_op"],
+                             "source": src}})
+    clk, csrc = newest_profile(f"pmc_clock_{workload}.json")
+    if clk and clk.get("clock_ghz"):
+        roof["held_clock_ghz"] = clk["clock_ghz"]
+        roof["held_clock_source"] = csrc
+        if mix:
+            roof["frac_mix_at_held_clock"] = round(achieved / (pm * clk["clock_ghz"] / 2.4), 4)
+
+
 def tar_host_path(nydus_gpu, tar, wl, device, file_bytes, reps=200):
     """A real (small) layer tar from host memory, PCIe included: ngpu_pack_tar
     = host tar walk + H2D through the engine's pinned staging + digest +
@@ -687,6 +726,73 @@ def node_e2e(torch, dist, nydus_gpu, buf, wl, stride, device, backend, sample_by
             "bound": "one PCIe Gen5 x16 link per GPU (~50-55 GB/s H2D) and the host DRAM they share"}
 
 
+SUB_KEYS = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "stage_ms", "roofline",
+            "cpu_baseline", "speedup_vs_cpu", "speedup_vs_cpu_single_stream", "dict",
+            "probe_roofline", "merge", "decisions", "digest_check_past_4gib", "n_gpus", "sharded_dict")
+
+
+def child_line(cmd, timeout_s, env=None):
+    """Run a bench command as a child process and return its JSON line (or an
+    error dict): a failure there costs only the entry that asked for it."""
+    import subprocess
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timeout after {timeout_s} s", "cmd": " ".join(cmd[1:])}
+    lines = [x for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    if r.returncode or not lines:
+        return {"error": f"rc {r.returncode}: {(r.stderr or '')[-400:]}", "cmd": " ".join(cmd[1:])}
+    d = json.loads(lines[-1])
+    out = {k: d[k] for k in SUB_KEYS if k in d}
+    out["cmd"] = " ".join(cmd[1:])
+    out["child_wall_s"] = round(time.perf_counter() - t0, 1)
+    return out
+
+
+def sub_entries(args):
+    """N = 1: driver-timed evidence for the dict paths beside the C2 headline
+    (VERDICT r3 item 5): C3 (sha256, 200M-entry dict in HBM, probe_roofline)
+    and C5-1000 (1000 x 64 MiB layers, 64 KiB chunks, pool dict, one
+    multi-layer dedup per step, then the host Merge of the 1000 bootstraps),
+    each a full bench line of its own (value, ms_per_step, roofline,
+    cpu_baseline), run as children after the headline is measured."""
+    out = {}
+    for key, wl in (("c3", "c3"), ("c5_1000", "c5-1000")):
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", wl, "--steps",
+               str(args.sub_steps), "--no-sub", "--no-e2e", "--settle-s", "1.0"]
+        out[key] = child_line(cmd, 420)
+    return out
+
+
+def c4_entry(world, layers, steps, backend="nccl", timeout_s=420):
+    """N > 1, rank 0, after the headline: C4 itself on the
+    run's GPUs -- a child `torchrun --nproc-per-node N bench.py --workload c4`:
+    each rank converts `layers` 1 GiB layers (C4's 1024-layer corpus split
+    round robin, at most 128 per GPU: one GPU's share of the 8-GPU node), 30 %
+    of the chunks from the 65,536-content pool, against the pool + 16M-filler
+    dict partitioned by digest prefix over the ranks; a timed step is digest
+    -> RCCL all_to_all_single probe routing (owner bucketing by
+    ngpu_route_digests) -> per-layer dedup of every layer.  The other ranks
+    wait in a gloo barrier meanwhile."""
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+              "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+              "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "GROUP_WORLD_SIZE"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--workload", "c4",
+           "--steps", str(steps), "--warmup", "15", "--no-sharded-extra", "--no-node-extra",
+           "--no-e2e", "--no-c4", "--c4-layers", str(layers), "--dist-backend", backend]
+    return child_line(cmd, timeout_s, env=env)
+
+
 def node_cabi_extra(world, timeout_s=150):
     """N > 1, rank 0, after the headline: the C ABI's one-process node
     (ngpu_node_*, csrc/node.hip) over the run's GPUs, in a child process
@@ -709,7 +815,10 @@ def node_cabi_extra(world, timeout_s=150):
         return {"error": f"rc {r.returncode}: {(r.stderr or '')[-300:]}", "devices": devs}
     d = json.loads(lines[-1])
     part, rep = d["modes"]["partition"], d["modes"]["replicate"]
-    return {"devices": d["node_devices"], "path": "ngpu_node_* in one process, peer-copy exchange",
+    cp = d["modes"].get("partition_copy", {})
+    return {"devices": d["node_devices"],
+            "path": "ngpu_node_* in one process: routed exchange (peer kernel loads/stores over "
+                    "xGMI), copy exchange (hipMemcpyPeerAsync) and replicas",
             "workload": "c4-16 layers per device, 1M-entry dict", "seconds": round(time.perf_counter() - t0, 1),
             "partition_gbs": part["value_gbs"], "replicate_gbs": rep["value_gbs"],
             "dedup_alone_ms_partition": part["dedup_alone_ms"],
@@ -717,8 +826,12 @@ def node_cabi_extra(world, timeout_s=150):
             "all_requesters_at_once_ms": {"partition": part["dedup_all_requesters_at_once_ms"],
                                           "replicate": rep["dedup_all_requesters_at_once_ms"]},
             "peer_bytes_per_step": d["exchange"]["peer_bytes_per_step"],
+            "peer_bytes_per_step_copy": d["exchange"].get("peer_bytes_per_step_copy"),
+            "partition_copy_gbs": cp.get("value_gbs"),
+            "dedup_alone_ms_partition_copy": cp.get("dedup_alone_ms"),
             "dict_hits_partition": part["dict_hits"], "dict_hits_replicate": rep["dict_hits"],
-            "hits_equal": part["dict_hits"] == rep["dict_hits"]}
+            "dict_hits_partition_copy": cp.get("dict_hits"),
+            "hits_equal": part["dict_hits"] == rep["dict_hits"] == cp.get("dict_hits", part["dict_hits"])}
 
 
 def concurrent_bench(args):
@@ -892,6 +1005,7 @@ def node_bench(args):
 
         modes = {}
         for name, mode in (("partition", nydus_gpu.NODE_DICT_PARTITION),
+                           ("partition_copy", nydus_gpu.NODE_DICT_PARTITION | nydus_gpu.NODE_EXCHANGE_COPY),
                            ("replicate", nydus_gpu.NODE_DICT_REPLICATE)):
             t0 = time.perf_counter()
             d = node.dict_create(recs, blobs, mode=mode)
@@ -967,7 +1081,20 @@ def node_bench(args):
             d.release()
         ex = float(np.mean(modes["partition"]["dedup_alone_ms"])) - \
             float(np.mean(modes["replicate"]["dedup_alone_ms"]))
+        ex_copy = float(np.mean(modes["partition_copy"]["dedup_alone_ms"])) - \
+            float(np.mean(modes["replicate"]["dedup_alone_ms"]))
         n_all = sum(p["n"] for p in per)
+        # rows whose owner part is another part than the requester's: the rows
+        # that cross a link on a node of distinct devices (routed: 32 + 4 B out,
+        # 24 B back each); the copy exchange sends all n rows to each of the
+        # W - 1 other parts and gets n hits back from each
+        from nydus_gpu.dist import owner_of
+        remote = 0
+        for i, p in enumerate(per):
+            with torch.cuda.device(p["dev"]):
+                dg = p["out"].view(p["n"], 64)[:, :32]
+                remote += int((owner_of(dg, W) != i).sum())
+        routed_bytes = remote * (32 + 4 + 24)  # + a few counter words per probe launch
         line = {
             "metric": "GB/s of layer data chunk-hashed+deduped (node, one process)",
             "value": modes["partition"]["value_gbs"], "unit": "GB/s", "n_gpus": len(set(devs)),
@@ -984,11 +1111,20 @@ def node_bench(args):
                          "all_requesters_at_once_ms_partition_minus_replicate": round(
                              modes["partition"]["dedup_all_requesters_at_once_ms"]
                              - modes["replicate"]["dedup_all_requesters_at_once_ms"], 4),
-                         "peer_bytes_per_step": n_all * (32 + 24) * (W - 1),
-                         "note": "per step every device sends its digests (32 B/chunk) to each of the "
-                                 "W-1 other owners and gets 24-B hits back from each; on a one-GPU "
-                                 "rehearsal the peer copies stay in one HBM and the W engines share "
-                                 "the GPU"},
+                         "dedup_alone_ms_copy_minus_replicate": round(ex_copy, 4),
+                         "all_requesters_at_once_ms_copy_minus_replicate": round(
+                             modes["partition_copy"]["dedup_all_requesters_at_once_ms"]
+                             - modes["replicate"]["dedup_all_requesters_at_once_ms"], 4),
+                         "peer_bytes_per_step": routed_bytes,
+                         "peer_bytes_per_step_copy": n_all * (32 + 24) * (W - 1),
+                         "peer_bytes_ratio_copy_over_routed": round(n_all * 56 * (W - 1) / max(1, routed_bytes), 2),
+                         "note": "routed (default, ABI 4): each requester buckets its digests by owner; "
+                                 "owner o's probe kernel reads only its rows (32-B digest + 4-B row id, "
+                                 "peer loads) and stores 24-B hits at their rows (peer stores), plus the "
+                                 "W counters it reads; copy (NGPU_NODE_EXCHANGE_COPY, ABI 3): every "
+                                 "digest to each of the W-1 other owners, 24-B hits back from each. On a "
+                                 "one-GPU rehearsal the peer traffic stays in one HBM and the W engines "
+                                 "share the GPU"},
         }
         print(json.dumps(line), flush=True)
     finally:
@@ -1013,6 +1149,8 @@ def main():
                     help="SHA-256 kernel: one lane per chunk (lane; split = schedule/round "
                          "waves) or two (pair)")
     ap.add_argument("--dict-entries", type=int, default=0, help="override dict size")
+    ap.add_argument("--digester", choices=["blake3", "sha256"], default=None,
+                    help="override the workload's digester (e.g. the sha256 small-layer crossover sweep)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--d2h", choices=["auto", "same", "copy"], default="auto",
@@ -1041,6 +1179,13 @@ def main():
                     help="--streams/--engines: one submitting host thread per stream")
     ap.add_argument("--engines", type=int, default=1,
                     help="tar workloads: K engines on device 0 convert layers concurrently")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="N = 1, c2: skip the c3 / c5_1000 sub-entries (child runs after the headline)")
+    ap.add_argument("--sub-steps", type=int, default=20, help="timed steps of each sub-entry child")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="N > 1: skip the c4 entry (a child torchrun of --workload c4 over the GPUs)")
+    ap.add_argument("--c4-layers", type=int, default=128,
+                    help="N > 1 c4 entry: 1 GiB layers per GPU (C4's share of 8 GPUs: 128)")
     ap.add_argument("--node", default="", help="comma list of devices: one process drives them "
                     "through ngpu_node_* (a device may repeat: one-GPU rehearsal); see node_bench")
     args = ap.parse_args()
@@ -1073,10 +1218,14 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     if args.dict_entries:
         wl["dict_entries"] = args.dict_entries
+    if args.digester:
+        wl["digester"] = args.digester
     if wl.get("layers_total"):  # split the layer set over the ranks
         mine = len(range(rank, wl["layers_total"], world))
         if wl.get("max_layers_per_gpu") and mine > wl["max_layers_per_gpu"]:
             mine = wl["max_layers_per_gpu"]  # HBM cap: one GPU's share of the 8-GPU run
+        if args.workload == "c4" and args.c4_layers:
+            mine = min(mine, args.c4_layers)
         wl["layers"] = mine
         wl["n_files"] = wl["n_files"] * mine
     if wl.get("tar"):  # a real tar layer (C1): host-built, chunked by the product's tar walk
@@ -1343,6 +1492,7 @@ def main():
         e2e = tar_host_path(nydus_gpu, tar, wl, local, file_bytes)
 
     roof["traffic"], roof["traffic_source"] = pmc_traffic(args.pmc_json, args.workload, roof["kernel"])
+    mix_roofline(roof, achieved, roof["kernel"], args.workload)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1398,7 +1548,8 @@ def main():
     sharded_extra = dist and sdict is None and n_layers == 1 and not args.no_sharded_extra
     node_pcie = dist and stride and not wl.get("dict_entries") and not wl.get("pool") and not args.no_e2e
     node_cabi = dist and stride and not wl.get("dict_entries") and not wl.get("pool") and not args.no_node_extra
-    if sharded_extra or node_pcie or node_cabi:
+    c4x = dist and args.workload == "c2" and not args.no_c4
+    if sharded_extra or node_pcie or node_cabi or c4x:
         # the headline is already measured; a watchdog keeps a stuck collective
         # (here, or in the closing barrier after a rank failed in here) from
         # costing the line: on expiry rank 0 prints it if it has not yet, and
@@ -1413,7 +1564,7 @@ def main():
                 print(json.dumps(dict(line, sharded_dict={"error": "timeout"})), flush=True)
             sys.stdout.flush()
             os._exit(3)
-        dog = threading.Timer(360.0 if node_cabi else 180.0, stuck)
+        dog = threading.Timer((360.0 if node_cabi else 180.0) + (450.0 if c4x else 0.0), stuck)
         dog.daemon = True
         dog.start()
         if sharded_extra:
@@ -1435,6 +1586,14 @@ def main():
                 line["node_cabi"] = node_cabi_extra(world)
             except Exception as ex:  # reported, never fatal to the headline line
                 line["node_cabi"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
+        if c4x and rank == 0:  # the other ranks wait in the closing barrier
+            try:
+                line["c4"] = c4_entry(world, args.c4_layers, max(3, min(args.steps, 10)),
+                                      args.dist_backend)
+            except Exception as ex:  # reported, never fatal to the headline line
+                line["c4"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
+    if rank == 0 and world == 1 and args.workload == "c2" and not args.no_sub:
+        line.update(sub_entries(args))
     if rank == 0:
         with print_mu:
             first = not printed[0]

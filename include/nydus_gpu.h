@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define NGPU_ABI_VERSION 3
+#define NGPU_ABI_VERSION 4
 
 /* PackOption.Digester (API extension; maps to nydus-image --digester). */
 enum ngpu_digester { NGPU_DIGEST_BLAKE3 = 0, NGPU_DIGEST_SHA256 = 1 };
@@ -235,6 +235,15 @@ int ngpu_dict_create_device(ngpu_engine *eng, const uint8_t *d_digests, const ui
                             const uint32_t *d_blob_index, const uint32_t *d_chunk_index,
                             const uint64_t *d_uoff, uint64_t n, uint32_t n_blobs,
                             ngpu_dict **out);
+/* The same with each entry's GLOBAL id (d_gid, device u32; NULL = its
+ * position): a rank's digest-prefix share of a dict partitioned across
+ * processes (nydus_gpu/dist.py) then answers probes with global entry ids.
+ * The rows must be in global table order.  (ABI 4) */
+int ngpu_dict_create_device_gid(ngpu_engine *eng, const uint8_t *d_digests,
+                                const uint32_t *d_usize, const uint32_t *d_blob_index,
+                                const uint32_t *d_chunk_index, const uint64_t *d_uoff,
+                                const uint32_t *d_gid, uint64_t n, uint32_t n_blobs,
+                                ngpu_dict **out);
 void ngpu_dict_retain(ngpu_dict *d);
 void ngpu_dict_release(ngpu_dict *d);
 uint64_t ngpu_dict_entries(const ngpu_dict *d);
@@ -343,6 +352,25 @@ int ngpu_dict_load_device(ngpu_engine *eng, const uint8_t *d_digests,
  * calls only. */
 int ngpu_dict_probe(const ngpu_dict *dict, const uint8_t *d_digests, uint64_t stride,
                     uint64_t n, ngpu_dict_hit *d_hits, void *stream);
+
+/* Digest-prefix routing for a dict partitioned over `world` owners (<= 64;
+ * owner(d) = ((d[0] << 8 | d[1]) * world) >> 16), device pointers, async on
+ * `stream` (ABI 4).  Each of the n digests (byte stride `stride`, 16-B
+ * aligned) goes to its owner's segment of d_out (32 B per row) with its row id
+ * in d_rows.  d_counts: 128 device u32, written by the call: [0, world) =
+ * rows per owner.  seg_cap == 0: owners back to back in owner order (owner o
+ * at the sum of the counts before it), d_out / d_rows hold n rows.  seg_cap >
+ * 0 (equal splits): row k of owner o goes to slot [k / seg_cap][o][k %
+ * seg_cap] of rounds x world x seg_cap slots; the call zeroes d_out and sets
+ * every d_rows slot to 0xFFFFFFFF first (padding), and rounds * seg_cap must
+ * cover n.  Order inside a segment is unspecified: hits return by row id. */
+int ngpu_route_digests(const uint8_t *d_digests, uint64_t stride, uint64_t n, uint32_t world,
+                       uint64_t seg_cap, uint32_t rounds, uint8_t *d_out, uint32_t *d_rows,
+                       uint32_t *d_counts, void *stream);
+/* d_hits[d_rows[i]] = d_routed[i] for the m routed rows (rows of 0xFFFFFFFF,
+ * padding, are skipped): an owner's hits back in the requester's row order. */
+int ngpu_route_hits(const ngpu_dict_hit *d_routed, const uint32_t *d_rows, uint64_t m,
+                    ngpu_dict_hit *d_hits, void *stream);
 int ngpu_process_dict(ngpu_engine *eng, ngpu_dict *dict, const void *data, uint64_t len,
                       const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
                       ngpu_layer_stats *stats);
@@ -409,11 +437,18 @@ void ngpu_pack_abort(ngpu_pack *p);
  * ((d[0] << 8 | d[1]) * n) >> 16, keeping table order, so "first entry wins"
  * holds per digest -- or replicated on every device.  Probing a partitioned
  * dict is the node's exchange step: the requester's digests go to every
- * owner over xGMI (hipMemcpyPeerAsync), each owner probes the entries it owns
- * and the hits come back the same way, ordered by cross-device events, with
- * GLOBAL entry ids -- the in-process form of the north star's digest-prefix
- * all-to-all (nydus_gpu/dist.py keeps the one-process-per-GPU RCCL form).
- * Peer access between the listed devices is enabled at creation. */
+ * owner, each owner probes the entries it owns and the hits come back with
+ * GLOBAL entry ids, ordered by cross-device events -- the in-process form of
+ * the north star's digest-prefix all-to-all (nydus_gpu/dist.py keeps the
+ * one-process-per-GPU RCCL form).  Default exchange (ABI 4, "routed"): the
+ * requester buckets its digests by owner in its own HBM; each owner's probe
+ * kernel reads only its own rows (peer loads over xGMI) and writes each hit
+ * into the requester's hit array at the row's id (peer stores), so a call
+ * moves n x (32 + 4) bytes out and n x 24 back in total.  With
+ * NGPU_NODE_EXCHANGE_COPY in `mode` (or when peer access between two listed
+ * devices is unavailable) the ABI 3 exchange runs instead: every digest to
+ * every owner and every owner's n hits back by hipMemcpyPeerAsync (W x the
+ * bytes).  Peer access between the listed devices is enabled at creation. */
 typedef struct ngpu_node ngpu_node;
 int ngpu_node_create(const int32_t *devices, uint32_t n, const ngpu_config *cfg, ngpu_node **out);
 void ngpu_node_destroy(ngpu_node *node);
@@ -422,6 +457,7 @@ uint32_t ngpu_node_size(const ngpu_node *node);
 ngpu_engine *ngpu_node_engine(ngpu_node *node, uint32_t i);
 #define NGPU_NODE_DICT_PARTITION 0u /* shard by digest prefix (default) */
 #define NGPU_NODE_DICT_REPLICATE 1u /* a full copy on every device */
+#define NGPU_NODE_EXCHANGE_COPY 0x100u /* | PARTITION: broadcast + DMA exchange */
 /* Node chunk dicts, usable by any engine of the node (ngpu_pack_open_dict,
  * ngpu_process_dict*, ngpu_node_*); checks as ngpu_dict_open. */
 int ngpu_node_dict_open(ngpu_node *node, const char *path, uint32_t mode, ngpu_dict **out);

@@ -257,14 +257,29 @@ void launch_dict_probe_owned(const uint8_t *q, uint64_t n, uint32_t owner, uint3
                              const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s);
 void launch_hits_merge(const uint8_t *q, uint64_t n, uint32_t W, const ngpu_dict_hit *parts,
                        ngpu_dict_hit *hits, hipStream_t s);
+// Digest routing (W <= 64): n digests (byte stride) to their owners' segments
+// of `out` (32 B each) with their row ids in `rows`; cnt: 128 u32 (counts at
+// 0..W, cursors at 64..64+W), zeroed here.  seg_cap 0: compact, owners back to
+// back; > 0: [round][owner][seg_cap] slots (the caller pre-fills padding).
+void launch_route(const uint8_t *src, uint64_t stride, uint64_t n, uint32_t W, uint64_t seg_cap,
+                  uint32_t *cnt, uint8_t *out, uint32_t *rows, hipStream_t s);
+// Owner `owner` probes its compact segment (q, rows, cnt may live on a peer
+// GPU) and writes hits[rows[i]]; n_max bounds the segment (grid size).
+void launch_dict_probe_routed(const uint8_t *q, const uint32_t *rows, const uint32_t *cnt,
+                              uint64_t n_max, uint32_t owner, const DictDevice &dict,
+                              ngpu_dict_hit *hits, hipStream_t s);
+// hits[rows[i]] = routed[i] for rows[i] != ~0.
+void launch_hits_scatter(const ngpu_dict_hit *routed, const uint32_t *rows, uint64_t m,
+                         ngpu_dict_hit *hits, hipStream_t s);
 // RAFS v6 chunk records (80 B, device) -> dict records; gid = gids[i] (device
 // array) or gid0 + i.
 void launch_dict_unpack(const uint8_t *recs, uint64_t n, const uint32_t *gids, uint32_t gid0,
                         DictRec *out, hipStream_t s);
-// Device SoA arrays -> dict records (index / uoff may be null: 0), gid = i.
+// Device SoA arrays -> dict records (index / uoff may be null: 0), gid =
+// gid[i] (null: i).
 void launch_dict_pack(const uint8_t *digests, const uint32_t *usize, const uint32_t *blob,
-                      const uint32_t *index, const uint64_t *uoff, uint64_t n, DictRec *out,
-                      hipStream_t s);
+                      const uint32_t *index, const uint64_t *uoff, const uint32_t *gid, uint64_t n,
+                      DictRec *out, hipStream_t s);
 
 // Device workspace, grown on demand and owned by the engine.
 struct Workspace {
@@ -289,9 +304,12 @@ struct Workspace {
   uint64_t cap_layers = 0;
   uint64_t *stats = nullptr;      // device-side counters (kSt* words above)
   uint64_t cap_n = 0, cap_g = 0, cap_blobs = 0;
-  // node dict exchange: packed digests (n x 32), per-part hits (W x n), hits (n)
+  // node dict exchange: packed digests (n x 32; routed: owner-ordered), per-part
+  // hits (W x n, copy exchange only), hits (n), routed row ids (n) and the
+  // route counters (128 u32)
   uint8_t *xq = nullptr;
   ngpu_dict_hit *xparts = nullptr, *xhits = nullptr;
+  uint32_t *xrow = nullptr, *xcnt = nullptr;
   uint64_t cap_x = 0, cap_xparts = 0;
   int load_mode = 0;              // b3_groups load mode (see blake3.hip)
   bool grid_stages = false;       // NGPU_FLAG_GRID_STAGES: no fused small-call path

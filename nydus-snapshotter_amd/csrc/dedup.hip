@@ -22,6 +22,8 @@
 #include <stddef.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include <hip/hip_ext.h>
 
 #include "common.hpp"
@@ -191,14 +193,15 @@ __global__ void dict_unpack(const uint8_t *__restrict__ recs, uint64_t n,
 
 __global__ void dict_pack(const uint8_t *__restrict__ digests, const uint32_t *__restrict__ usize,
                           const uint32_t *__restrict__ blob, const uint32_t *__restrict__ index,
-                          const uint64_t *__restrict__ uoff, uint64_t n, DictRec *__restrict__ out) {
+                          const uint64_t *__restrict__ uoff, const uint32_t *__restrict__ gid,
+                          uint64_t n, DictRec *__restrict__ out) {
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint4 *dg = reinterpret_cast<const uint4 *>(digests + 32 * i);
   uint4 *o = reinterpret_cast<uint4 *>(out + i);
   o[0] = dg[0];
   o[1] = dg[1];
-  o[2] = make_uint4(usize[i], blob[i], index ? index[i] : 0, (uint32_t)i);
+  o[2] = make_uint4(usize[i], blob[i], index ? index[i] : 0, gid ? gid[i] : (uint32_t)i);
   const uint64_t u = uoff ? uoff[i] : 0;
   o[3] = make_uint4((uint32_t)u, (uint32_t)(u >> 32), 0, 0);
 }
@@ -1068,7 +1071,131 @@ __global__ void hits_merge(const uint8_t *__restrict__ q, uint64_t n, uint32_t W
   hits[i] = parts[(uint64_t)owner_of(w0, W) * n + i];
 }
 
+// ---- digest routing: each digest to its owner only ------
+// route_count: per-owner row counts (LDS histogram per workgroup, one global
+// atomic per (workgroup, owner)).  route_scatter: each row's 32-B digest and
+// its row id to its owner's segment.  Compact layout (seg_cap = 0): owners
+// back to back in owner order, owner o at sum(cnt[0..o)).  Padded layout
+// (seg_cap > 0, dist.py's equal splits): row of rank k within owner o goes to
+// round k / seg_cap, slot [round][o][k % seg_cap].  The order inside a
+// segment is the atomics' order: hits return to rows by row id, never by
+// position.  cnt[0..W) = counts, cnt[64..64+W) = scatter cursors.
+__global__ __launch_bounds__(256) void route_count(const uint8_t *__restrict__ src, uint64_t stride,
+                                                   uint64_t n, uint32_t W, uint32_t *__restrict__ cnt) {
+  __shared__ uint32_t h[64];
+  if (threadIdx.x < 64) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  if (i < n) atomicAdd(&h[owner_of(*reinterpret_cast<const uint32_t *>(src + i * stride), W)], 1u);
+  __syncthreads();
+  if (threadIdx.x < W && h[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void route_scatter(const uint8_t *__restrict__ src, uint64_t stride,
+                                                     uint64_t n, uint32_t W, uint64_t seg_cap,
+                                                     uint32_t *__restrict__ cnt,
+                                                     uint8_t *__restrict__ out,
+                                                     uint32_t *__restrict__ rows) {
+  __shared__ uint32_t h[64], base[64];
+  if (threadIdx.x < 64) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  uint32_t o = 0, local = 0;
+  uint4 a = {}, b = {};
+  if (i < n) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(src + i * stride);
+    a = p[0];
+    b = p[1];
+    o = owner_of(a.x, W);
+    local = atomicAdd(&h[o], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < W) {
+    const uint32_t t = threadIdx.x;
+    uint32_t off = 0;
+    if (!seg_cap)
+      for (uint32_t k = 0; k < t; ++k) off += cnt[k];
+    base[t] = off + (h[t] ? atomicAdd(&cnt[64 + t], h[t]) : 0u);
+  }
+  __syncthreads();
+  if (i >= n) return;
+  const uint64_t k = (uint64_t)base[o] + local;
+  const uint64_t pos = seg_cap ? (k / seg_cap) * W * seg_cap + (uint64_t)o * seg_cap + k % seg_cap : k;
+  uint4 *d = reinterpret_cast<uint4 *>(out + 32 * pos);
+  d[0] = a;
+  d[1] = b;
+  rows[pos] = (uint32_t)i;
+}
+
+// An owner's probe of the rows routed to it (compact layout): reads its count
+// and segment -- in the requester's HBM when the node spans GPUs (peer loads
+// over xGMI) -- and writes each hit straight into the requester's hit array at
+// the row's id (peer stores).  Every row has exactly one owner, so the W
+// owners together write each hit once and no merge step follows.
+__global__ __launch_bounds__(256) void dict_probe_routed(const uint8_t *__restrict__ q,
+                                                         const uint32_t *__restrict__ rows,
+                                                         const uint32_t *__restrict__ cnt,
+                                                         uint32_t owner, DictDevice dict,
+                                                         ngpu_dict_hit *__restrict__ hits) {
+  __shared__ uint32_t s_off, s_n;
+  if (threadIdx.x == 0) {
+    uint32_t off = 0;
+    for (uint32_t k = 0; k < owner; ++k) off += cnt[k];
+    s_off = off;
+    s_n = cnt[owner];
+  }
+  __syncthreads();
+  const uint64_t off = s_off, m = s_n;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < m; i += gridDim.x * 256ull) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(q + 32 * (off + i));
+    uint32_t e = kNone;
+    if (dict.m) {
+      const uint4 a = p[0], b = p[1];
+      const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      e = dict_lookup(dict, d);
+    }
+    hits[rows[off + i]] = dict_hit_of(dict, e);
+  }
+}
+
+// hits of routed rows back to their rows (dist.py: the all-to-all returns
+// them in routed order); padding rows (row id ~0) are skipped
+__global__ void hits_scatter(const ngpu_dict_hit *__restrict__ routed,
+                             const uint32_t *__restrict__ rows, uint64_t m,
+                             ngpu_dict_hit *__restrict__ hits) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint32_t r = rows[i];
+  if (r != 0xFFFFFFFFu) hits[r] = routed[i];
+}
+
 }  // namespace
+
+void launch_route(const uint8_t *src, uint64_t stride, uint64_t n, uint32_t W, uint64_t seg_cap,
+                  uint32_t *cnt, uint8_t *out, uint32_t *rows, hipStream_t s) {
+  hipMemsetAsync(cnt, 0, 128 * sizeof(uint32_t), s);
+  if (n == 0) return;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(route_count, dim3(blocks), dim3(256), 0, s, src, stride, n, W, cnt);
+  hipLaunchKernelGGL(route_scatter, dim3(blocks), dim3(256), 0, s, src, stride, n, W, seg_cap, cnt,
+                     out, rows);
+}
+
+void launch_dict_probe_routed(const uint8_t *q, const uint32_t *rows, const uint32_t *cnt,
+                              uint64_t n_max, uint32_t owner, const DictDevice &dict,
+                              ngpu_dict_hit *hits, hipStream_t s) {
+  if (n_max == 0) return;
+  const uint64_t b = std::min<uint64_t>((n_max + 255) / 256, 2048);
+  hipLaunchKernelGGL(dict_probe_routed, dim3((unsigned)b), dim3(256), 0, s, q, rows, cnt, owner,
+                     dict, hits);
+}
+
+void launch_hits_scatter(const ngpu_dict_hit *routed, const uint32_t *rows, uint64_t m,
+                         ngpu_dict_hit *hits, hipStream_t s) {
+  if (m == 0) return;
+  hipLaunchKernelGGL(hits_scatter, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, routed, rows,
+                     m, hits);
+}
 
 void launch_pack_digests(const uint8_t *src, uint64_t stride, uint64_t n, uint8_t *dst,
                          hipStream_t s) {
@@ -1099,11 +1226,11 @@ void launch_dict_unpack(const uint8_t *recs, uint64_t n, const uint32_t *gids, u
 }
 
 void launch_dict_pack(const uint8_t *digests, const uint32_t *usize, const uint32_t *blob,
-                      const uint32_t *index, const uint64_t *uoff, uint64_t n, DictRec *out,
-                      hipStream_t s) {
+                      const uint32_t *index, const uint64_t *uoff, const uint32_t *gid, uint64_t n,
+                      DictRec *out, hipStream_t s) {
   if (n == 0) return;
   hipLaunchKernelGGL(dict_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, digests, usize,
-                     blob, index, uoff, n, out);
+                     blob, index, uoff, gid, n, out);
 }
 
 void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,

@@ -195,7 +195,7 @@ int dict_from_records(ngpu_engine *e, const uint8_t *recs, uint64_t m, const uin
 // stream, like dict_from_records).
 int dict_from_arrays(ngpu_engine *e, const uint8_t *dg, const uint32_t *us, const uint32_t *bl,
                      const uint32_t *ix, const uint64_t *uo, uint64_t m, uint32_t n_blobs,
-                     hipMemcpyKind kind, ngpu_dict **out) {
+                     hipMemcpyKind kind, ngpu_dict **out, const uint32_t *gid = nullptr) {
   DeviceGuard dgd(e->device);
   BuildStream bs(e->device);
   if (!bs.s) return fail(e, NGPU_EHIP, "chunk dict: no build stream");
@@ -219,14 +219,14 @@ int dict_from_arrays(ngpu_engine *e, const uint8_t *dg, const uint32_t *us, cons
       r.usize = us[i];
       r.blob = bl[i];
       r.index = ix ? ix[i] : 0;
-      r.gid = (uint32_t)i;
+      r.gid = gid ? gid[i] : (uint32_t)i;
       r.uoff = uo ? uo[i] : 0;
     }
     if (hipMemcpyAsync(rec, h.data(), m * sizeof(DictRec), kind, bs.s) != hipSuccess ||
         hipStreamSynchronize(bs.s) != hipSuccess)
       rc = fail(e, NGPU_EHIP, "chunk dict: upload failed");
   } else if (m) {
-    launch_dict_pack(dg, us, bl, ix, uo, m, rec, bs.s);
+    launch_dict_pack(dg, us, bl, ix, uo, gid, m, rec, bs.s);
     if (hipGetLastError() != hipSuccess) rc = fail(e, NGPU_EHIP, "chunk dict: pack failed");
   }
   if (!rc) rc = dict_build(e, d, bs.s);
@@ -454,11 +454,21 @@ int ngpu_dict_create_device(ngpu_engine *e, const uint8_t *d_digests, const uint
                             const uint32_t *d_blob_index, const uint32_t *d_chunk_index,
                             const uint64_t *d_uoff, uint64_t n, uint32_t n_blobs,
                             ngpu_dict **out) {
+  return ngpu_dict_create_device_gid(e, d_digests, d_usize, d_blob_index, d_chunk_index, d_uoff,
+                                     nullptr, n, n_blobs, out);
+}
+
+int ngpu_dict_create_device_gid(ngpu_engine *e, const uint8_t *d_digests, const uint32_t *d_usize,
+                                const uint32_t *d_blob_index, const uint32_t *d_chunk_index,
+                                const uint64_t *d_uoff, const uint32_t *d_gid, uint64_t n,
+                                uint32_t n_blobs, ngpu_dict **out) {
   if (!e || !out || (n && (!d_digests || !d_usize || !d_blob_index))) return NGPU_EINVAL;
   *out = nullptr;
   if (n_blobs == 0 || n_blobs > (1u << 20)) return fail(e, NGPU_EINVAL, "bad n_blobs %u", n_blobs);
-  return dict_from_arrays(e, d_digests, d_usize, d_blob_index, d_chunk_index, d_uoff, n, n_blobs,
-                          hipMemcpyDeviceToDevice, out);
+  return guarded([&] {
+    return dict_from_arrays(e, d_digests, d_usize, d_blob_index, d_chunk_index, d_uoff, n, n_blobs,
+                            hipMemcpyDeviceToDevice, out, d_gid);
+  });
 }
 
 void ngpu_dict_retain(ngpu_dict *d) { dict_ref(d); }
@@ -532,6 +542,34 @@ int ngpu_dict_probe(const ngpu_dict *d, const uint8_t *d_digests, uint64_t strid
   if (!d->parts.empty()) return NGPU_EINVAL;  // node dicts are probed through an engine
   DeviceGuard dg(d->device);
   launch_dict_probe(d_digests, stride, n, d->dev, d_hits, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? 0 : NGPU_EHIP;
+}
+
+// Routing for dicts partitioned across processes (nydus_gpu/dist.py): the
+// owner bucketing runs here, in two kernels, instead of an argsort / bincount /
+// gather in PyTorch.  Runs on the device of the caller's current context.
+int ngpu_route_digests(const uint8_t *d_digests, uint64_t stride, uint64_t n, uint32_t world,
+                       uint64_t seg_cap, uint32_t rounds, uint8_t *d_out, uint32_t *d_rows,
+                       uint32_t *d_counts, void *stream) {
+  if (!world || world > 64 || !d_counts || (n && (!d_digests || !d_out || !d_rows)) ||
+      stride < 32 || (stride & 15) || n >= 0xFFFFFFFFull)
+    return NGPU_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (seg_cap) {
+    const uint64_t slots = (uint64_t)rounds * world * seg_cap;
+    if ((uint64_t)rounds * seg_cap < n) return NGPU_EINVAL;
+    if (hipMemsetAsync(d_out, 0, slots * 32, s) != hipSuccess ||
+        hipMemsetAsync(d_rows, 0xFF, slots * 4, s) != hipSuccess)
+      return NGPU_EHIP;
+  }
+  launch_route(d_digests, stride, n, world, seg_cap, d_counts, d_out, d_rows, s);
+  return hipGetLastError() == hipSuccess ? 0 : NGPU_EHIP;
+}
+
+int ngpu_route_hits(const ngpu_dict_hit *d_routed, const uint32_t *d_rows, uint64_t m,
+                    ngpu_dict_hit *d_hits, void *stream) {
+  if (m && (!d_routed || !d_rows || !d_hits)) return NGPU_EINVAL;
+  launch_hits_scatter(d_routed, d_rows, m, d_hits, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? 0 : NGPU_EHIP;
 }
 

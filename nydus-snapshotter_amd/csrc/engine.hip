@@ -367,7 +367,8 @@ void engine_unref(ngpu_engine *e) {
     Workspace &ws = sl.ws;
     void *bufs[] = {ws.groups, ws.group_chunk, ws.cv, ws.newflag, ws.uoff, ws.nbytes, ws.ndict,
                     ws.tstat, ws.intra, ws.blob_first, ws.blob_real, ws.stats, ws.chunk_layer,
-                    ws.lfirst1, ws.lstats, ws.small, ws.tree_list, ws.xq, ws.xparts, ws.xhits};
+                    ws.lfirst1, ws.lstats, ws.small, ws.tree_list, ws.xq, ws.xparts, ws.xhits,
+                    ws.xrow, ws.xcnt};
     for (void *p : bufs)
       if (p) (void)hipFree(p);
     if (sl.h_stats) (void)hipHostFree(sl.h_stats);

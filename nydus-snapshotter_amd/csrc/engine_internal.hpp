@@ -92,6 +92,7 @@ struct ngpu_dict {
   std::vector<std::unique_ptr<Requester>> req;
   std::mutex req_mu;  // held only to find or add a requester
   bool replicated = false;
+  bool routed = false;  // partitioned: routed exchange (peer kernels), else copy exchange
 };
 
 // One HBM workspace and its cross-stream ordering state.  Every stage that

@@ -35,6 +35,7 @@ struct ngpu_node {
   std::vector<ngpu_engine *> eng;  // one per listed device (a reference each)
   std::vector<int> dev;
   std::atomic<uint64_t> rr{0};     // round robin over the engines for Packs
+  bool peer_ok = true;             // every pair of distinct devices has peer access
 };
 
 namespace ngpu {
@@ -88,6 +89,64 @@ static int channel_ready(ngpu_engine *e, ngpu_dict::PartIO &io, int device, uint
   return 0;
 }
 
+// The routed exchange (ABI 4): the requester buckets its n digests by owner in
+// its own HBM (ws.xq rows, ws.xrow row ids, ws.xcnt counts); owner o's probe
+// kernel, launched on o's device after the requester's `ready` event, reads
+// only its own segment (peer loads over xGMI) and stores each hit at its row
+// in the requester's ws.xhits (peer stores).  The requester's stream waits for
+// every owner's `done`.  Bytes over the links per call: n x 36 out and n x 24
+// back in total, against W x n x 56 for the copy exchange below it.
+// Reuse is stream-ordered: the next call's routing on s runs after this call's
+// waits on every `done`, so no owner still reads ws.xq when it is rewritten.
+static int routed_hits(ngpu_engine *e, ngpu_dict *d, const uint8_t *digests, uint64_t stride,
+                       uint64_t n, hipStream_t s, const ngpu_dict_hit **hits) {
+  const uint32_t W = (uint32_t)d->parts.size();
+  Workspace &ws = e->cur->ws;
+  const bool regrow = n > ws.cap_x || !ws.xq || !ws.xrow || !ws.xhits;
+  if (regrow && (ws.xq || ws.xrow || ws.xhits))
+    if (int rc = slot_quiesce(e)) return rc;  // no buffer freed under a running stage
+  if (regrow) {
+    if (ws.xq) (void)hipFree(ws.xq), ws.xq = nullptr;
+    if (ws.xhits) (void)hipFree(ws.xhits), ws.xhits = nullptr;
+    if (ws.xrow) (void)hipFree(ws.xrow), ws.xrow = nullptr;
+    const uint64_t c = next_pow2(n < 1024 ? 1024 : n);
+    HIP_TRY(e, hipMalloc((void **)&ws.xq, c * 32));
+    HIP_TRY(e, hipMalloc((void **)&ws.xhits, c * sizeof(ngpu_dict_hit)));
+    HIP_TRY(e, hipMalloc((void **)&ws.xrow, c * 4));
+    ws.cap_x = c;
+  }
+  if (!ws.xcnt) HIP_TRY(e, hipMalloc((void **)&ws.xcnt, 128 * sizeof(uint32_t)));
+  *hits = ws.xhits;
+  if (n == 0) return 0;
+  ngpu_dict::Requester *r = requester_of(e, d);
+  std::lock_guard<std::mutex> g(r->mu);  // this requester's channels only
+  if (!r->ready) HIP_TRY(e, hipEventCreateWithFlags(&r->ready, hipEventDisableTiming));
+  launch_route(digests, stride, n, W, 0, ws.xcnt, ws.xq, ws.xrow, s);
+  HIP_TRY(e, hipGetLastError());
+  HIP_TRY(e, hipEventRecord(r->ready, s));
+  int rc = 0;
+  uint32_t sent = 0;
+  for (uint32_t o = 0; o < W && !rc; ++o, ++sent) {
+    ngpu_dict *p = d->parts[o];
+    ngpu_dict::PartIO &io = r->io[o];
+    if ((rc = channel_ready(e, io, p->device, 0, 0))) break;
+    DeviceGuard dg(p->device);
+    if (hipStreamWaitEvent(io.stream, r->ready, 0) != hipSuccess) {
+      rc = fail(e, NGPU_EHIP, "node dict: wait on the requester failed (device %d)", p->device);
+      break;
+    }
+    launch_dict_probe_routed(ws.xq, ws.xrow, ws.xcnt, n, o, p->dev, ws.xhits, io.stream);
+    if (hipGetLastError() != hipSuccess || hipEventRecord(io.done, io.stream) != hipSuccess)
+      rc = fail(e, NGPU_EHIP, "node dict: routed probe on device %d failed", p->device);
+  }
+  // the requester's stream waits for every owner it enqueued, even on failure,
+  // so no later stage reuses ws.xq / ws.xhits under a probe still in flight
+  for (uint32_t o = 0; o < sent && o < W; ++o)
+    if (r->io[o].done && hipStreamWaitEvent(s, r->io[o].done, 0) != hipSuccess && !rc)
+      rc = fail(e, NGPU_EHIP, "node dict: cross-device wait failed");
+  return rc;
+}
+
 int node_dict_hits(ngpu_engine *e, ngpu_dict *d, const uint8_t *digests, uint64_t stride,
                    uint64_t n, hipStream_t s, const ngpu_dict_hit **hits, ngpu_dict **replica) {
   *hits = nullptr;
@@ -102,6 +161,7 @@ int node_dict_hits(ngpu_engine *e, ngpu_dict *d, const uint8_t *digests, uint64_
   }
   const uint32_t W = (uint32_t)d->parts.size();
   Workspace &ws = e->cur->ws;  // the dedup stage's slot (use_slot)
+  if (d->routed) return routed_hits(e, d, digests, stride, n, s, hits);
   if (((n > ws.cap_x && ws.xq) || ((uint64_t)W * n > ws.cap_xparts && ws.xparts)))
     if (int rc = slot_quiesce(e)) return rc;  // no buffer freed under a running stage
   if (n > ws.cap_x || !ws.xq) {
@@ -160,6 +220,8 @@ namespace {
 int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint8_t *blobs,
                     uint32_t n_blobs, uint32_t mode, ngpu_dict **out) {
   ngpu_engine *e0 = node->eng[0];
+  const bool copy = (mode & NGPU_NODE_EXCHANGE_COPY) != 0;
+  mode &= ~NGPU_NODE_EXCHANGE_COPY;
   if (mode != NGPU_NODE_DICT_PARTITION && mode != NGPU_NODE_DICT_REPLICATE)
     return fail(e0, NGPU_EINVAL, "bad node dict mode %u", mode);
   if (m >= 0xFFFFFFFFull) return fail(e0, NGPU_EINVAL, "chunk dict too large");
@@ -178,6 +240,9 @@ int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint
   d->digester = e0->cfg.digester;
   d->chunk_size = e0->cfg.chunk_size;
   d->replicated = mode == NGPU_NODE_DICT_REPLICATE;
+  // routed exchange unless asked for the copy exchange or a pair of devices
+  // lacks peer access (its kernels could not reach the requester's HBM)
+  d->routed = !d->replicated && !copy && node->peer_ok;
   d->dev.m = m;
   d->dev.n_blobs = nb;
   d->place.resize(m);
@@ -268,7 +333,11 @@ int ngpu_node_create(const int32_t *devices, uint32_t n, const ngpu_config *cfg,
     for (uint32_t b = 0; b < n; ++b) {
       if (node->dev[a] == node->dev[b]) continue;
       int can = 0;
-      if (hipDeviceCanAccessPeer(&can, node->dev[a], node->dev[b]) != hipSuccess || !can) continue;
+      if (hipDeviceCanAccessPeer(&can, node->dev[a], node->dev[b]) != hipSuccess || !can) {
+        (void)hipGetLastError();
+        node->peer_ok = false;  // partitioned dicts fall back to the copy exchange
+        continue;
+      }
       DeviceGuard g(node->dev[a]);
       const hipError_t st = hipDeviceEnablePeerAccess(node->dev[b], 0);
       if (st != hipSuccess && st != hipErrorPeerAccessAlreadyEnabled) {

@@ -406,6 +406,7 @@ inline uint64_t align(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 constexpr uint64_t kBlk = 4096;
 constexpr uint32_t kEroFsFeatureCompatRafsV6 = 0x40000000u;  // fixture super block
 constexpr uint32_t kIncompatChunkedFile = 0x4, kIncompatDeviceTable = 0x8;
+constexpr uint32_t kRafsV6SBlocks = 4096;  // EROFS s_blocks as nydus-image writes it (see write_v6)
 constexpr uint16_t kLayoutPlain = 0, kLayoutInline = 2, kLayoutChunk = 4;
 constexpr uint64_t kDevTableOff = 1408;  // after the 256-B extended super block
 
@@ -638,7 +639,13 @@ int write_v6(Tree &t, const RafsLayerInfo &info, std::vector<uint8_t> *outp) {
   v[1024 + 12] = 12;  // blkszbits
   put<uint16_t>(v, 1024 + 14, (uint16_t)t.nodes[0].nid);
   put<uint64_t>(v, 1024 + 16, ninos);
-  put<uint32_t>(v, 1024 + 36, (uint32_t)(total / kBlk));
+  // s_blocks: 4096, the value nydus-image wrote into the reference's only v6
+  // bootstrap (pkg/filesystem/testdata/v6-bootstrap-chunk-pos-438272).  It
+  // matches no size of that image -- the bootstrap's 157 blocks, the blob's
+  // 20,451 data blocks, 2,515 chunks, 3,517 inodes, meta_blkaddr 2 -- so it is
+  // taken as the builder's constant (1 << blkszbits), not derived (DESIGN.md
+  // §3 "RAFS bootstrap writer"); rounds 1-3 wrote the bootstrap's block count.
+  put<uint32_t>(v, 1024 + 36, kRafsV6SBlocks);
   put<uint32_t>(v, 1024 + 40, (uint32_t)(meta_base / kBlk));
   put<uint32_t>(v, 1024 + 80, kIncompatChunkedFile | kIncompatDeviceTable);
   put<uint16_t>(v, 1024 + 86, (uint16_t)nb);

@@ -66,7 +66,9 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_pack_open_dict", "ngpu_pack_set_cancel", "ngpu_node_create", "ngpu_node_destroy",
            "ngpu_node_size", "ngpu_node_engine", "ngpu_node_dict_open", "ngpu_node_dict_create",
            "ngpu_node_owner", "ngpu_node_pack_open", "ngpu_node_process_device",
-           "ngpu_device_status", "ngpu_unpack"]
+           "ngpu_device_status", "ngpu_unpack",
+           # ABI 4
+           "ngpu_dict_create_device_gid", "ngpu_route_digests", "ngpu_route_hits"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
@@ -210,6 +212,9 @@ def lib():
     L.ngpu_dict_open.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
     L.ngpu_dict_create.argtypes = [vp, vp, u64, vp, u32, ctypes.POINTER(vp)]
     L.ngpu_dict_create_device.argtypes = [vp, vp, vp, vp, vp, vp, u64, u32, ctypes.POINTER(vp)]
+    L.ngpu_dict_create_device_gid.argtypes = [vp, vp, vp, vp, vp, vp, vp, u64, u32, ctypes.POINTER(vp)]
+    L.ngpu_route_digests.argtypes = [vp, u64, u64, u32, u64, u32, vp, vp, vp, vp]
+    L.ngpu_route_hits.argtypes = [vp, vp, u64, vp, vp]
     L.ngpu_dict_retain.argtypes = [vp]
     L.ngpu_dict_retain.restype = None
     L.ngpu_dict_release.argtypes = [vp]
@@ -432,6 +437,29 @@ def rafs_dump(bootstrap: bytes) -> dict:
     return json.loads(b"".join(out).decode("ascii"))
 
 
+def route_digests(d_digests: int, stride: int, n: int, world: int, d_out: int, d_rows: int,
+                  d_counts: int, seg_cap: int = 0, rounds: int = 0, stream: int = 0):
+    """ngpu_route_digests (device pointers, async on `stream`): each digest to
+    its owner's segment of d_out with its row id in d_rows; d_counts (128 u32)
+    receives the per-owner counts.  seg_cap > 0: padded [rounds][world][seg_cap]."""
+    rc = lib().ngpu_route_digests(ctypes.c_void_p(d_digests) if d_digests else None, stride, n, world,
+                                  seg_cap, rounds, ctypes.c_void_p(d_out) if d_out else None,
+                                  ctypes.c_void_p(d_rows) if d_rows else None,
+                                  ctypes.c_void_p(d_counts), ctypes.c_void_p(stream) if stream else None)
+    if rc:
+        raise NgpuError(rc, "route_digests")
+
+
+def route_hits(d_routed: int, d_rows: int, m: int, d_hits: int, stream: int = 0):
+    """ngpu_route_hits: d_hits[d_rows[i]] = d_routed[i] (padding rows skipped)."""
+    rc = lib().ngpu_route_hits(ctypes.c_void_p(d_routed) if d_routed else None,
+                               ctypes.c_void_p(d_rows) if d_rows else None, m,
+                               ctypes.c_void_p(d_hits) if d_hits else None,
+                               ctypes.c_void_p(stream) if stream else None)
+    if rc:
+        raise NgpuError(rc, "route_hits")
+
+
 class NgpuMergeOptions(ctypes.Structure):
     _fields_ = [("parent_bootstrap", ctypes.c_void_p), ("parent_size", ctypes.c_uint64),
                 ("prefetch_patterns", ctypes.c_char_p)]
@@ -597,11 +625,13 @@ class Engine:
         return ChunkDict(h)
 
     def dict_create_device(self, d_digests: int, d_usize: int, d_blob: int, d_index: int, n: int,
-                           n_blobs: int, d_uoff: int = 0) -> ChunkDict:
+                           n_blobs: int, d_uoff: int = 0, d_gid: int = 0) -> ChunkDict:
+        """d_gid: device u32 global entry ids (0 = positions), so a shard of a
+        partitioned dict answers with global ids (ngpu_dict_create_device_gid)."""
         h = ctypes.c_void_p()
-        self._check(lib().ngpu_dict_create_device(self._h, self._vp(d_digests), self._vp(d_usize),
-                                                  self._vp(d_blob), self._vp(d_index), self._vp(d_uoff),
-                                                  n, n_blobs, ctypes.byref(h)), "dict_create_device")
+        self._check(lib().ngpu_dict_create_device_gid(
+            self._h, self._vp(d_digests), self._vp(d_usize), self._vp(d_blob), self._vp(d_index),
+            self._vp(d_uoff), self._vp(d_gid), n, n_blobs, ctypes.byref(h)), "dict_create_device")
         return ChunkDict(h)
 
     def set_dict(self, d):
@@ -837,6 +867,7 @@ class PackWriter:
 
 
 NODE_DICT_PARTITION, NODE_DICT_REPLICATE = 0, 1
+NODE_EXCHANGE_COPY = 0x100  # | PARTITION: the ABI 3 broadcast + DMA exchange
 
 
 class Node:

@@ -10,15 +10,19 @@ is the dict probe:
   2. owner(d) = top bits of the digest's first two bytes
      ((d0 << 8 | d1) * world >> 16; for power-of-two worlds the top
      log2(world) bits of byte 0);
-  3. records are sorted by owner and exchanged with all_to_all_single
-     (32 B per query out, 24 B per hit back) — payload is tiny
-     (1 MiB chunks: 16384 x 56 B per 16 GiB layer), so the exchange is
-     latency-bound, not link-bound.  Variable splits (sized on the host,
-     one sync per probe) or, with `cap`, equal padded splits that keep the
-     whole probe on the device stream;
-  4. the owner probes its partition (engine.dict_probe_device) and returns
-     ngpu_dict_hit records with GLOBAL entry ids (chunk-table order);
-  5. each rank runs its own layer dedup with those hits (engine.dedup_device).
+  3. each rank's digests are bucketed by owner ON THE GPU
+     (ngpu_route_digests: an LDS histogram + scatter kernel pair, row ids
+     kept beside the digests) and exchanged with all_to_all_single (32 B per
+     query out, 24 B per hit back) -- payload is tiny (1 MiB chunks: 16384 x
+     56 B per 16 GiB layer), so the exchange is latency-bound, not
+     link-bound.  Variable splits (the per-owner counts read on the host, one
+     sync per probe, exact bytes) or, with `cap`, equal padded splits that
+     keep the whole probe on the device stream;
+  4. the owner probes its partition (engine.dict_probe_device); the partition
+     was built with each entry's GLOBAL id (ngpu_dict_create_device_gid), so
+     the hits carry global entry ids (chunk-table order) as they are;
+  5. the hits go back to their rows (ngpu_route_hits) and each rank runs its
+     own layer dedup with them (engine.dedup_device).
 
 A partition keeps its entries in global table order, so "first entry wins"
 for duplicate digests is preserved: duplicates share a digest, hence an owner.
@@ -39,16 +43,57 @@ def owner_of(digests: torch.Tensor, world: int) -> torch.Tensor:
     return (hi * world) >> 16
 
 
+class HipRouter:
+    """Owner routing on the GPU through the C ABI (ngpu_route_digests /
+    ngpu_route_hits) -- the product path; it takes CUDA tensors only."""
+
+    @staticmethod
+    def _stream():
+        return torch.cuda.current_stream().cuda_stream
+
+    def route(self, digests: torch.Tensor, world: int, seg_cap: int = 0, rounds: int = 0):
+        """digests (n, 32) uint8 CUDA (row stride a multiple of 16 B) ->
+        (rows' digests (slots, 32) uint8, row ids (slots,) int32 with -1 for
+        padding, per-owner counts (world,) int32).  seg_cap 0: compact owner
+        order, slots = n; else [rounds][world][seg_cap] slots."""
+        import nydus_gpu
+        if not digests.is_cuda:
+            raise ValueError("HipRouter routes CUDA tensors (the GPU path); pass a router for others")
+        n = digests.shape[0]
+        slots = n if not seg_cap else rounds * world * seg_cap
+        dev = digests.device
+        out = torch.empty((max(slots, 1), 32), dtype=torch.uint8, device=dev)
+        rows = torch.empty(max(slots, 1), dtype=torch.int32, device=dev)
+        counts = torch.empty(128, dtype=torch.int32, device=dev)
+        assert digests.stride(1) == 1
+        nydus_gpu.route_digests(digests.data_ptr(), digests.stride(0), n, world, out.data_ptr(),
+                                rows.data_ptr(), counts.data_ptr(), seg_cap=seg_cap, rounds=rounds,
+                                stream=self._stream())
+        return out[:slots], rows[:slots], counts[:world]
+
+    def scatter(self, routed: torch.Tensor, rows: torch.Tensor, n: int, hits: torch.Tensor = None):
+        """hits[rows[i]] = routed[i] (padding rows skipped) -> hits (n, HIT_WORDS)."""
+        import nydus_gpu
+        if hits is None:
+            hits = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=routed.device)
+        routed = routed.contiguous()
+        nydus_gpu.route_hits(routed.data_ptr(), rows.data_ptr(), rows.shape[0], hits.data_ptr(),
+                             stream=self._stream())
+        return hits
+
+
 class ShardedChunkDict:
     """Digest-prefix partition of a chunk dict across ranks.
 
-    probe_fn(local_digests (m, 32) uint8) -> (m, HIT_WORDS) int32 hits in
-    LOCAL entry ids (ngpu_dict_hit words: entry, index, blob, usize,
-    uncompressed offset lo/hi; entry == -1 for a miss).  On the GPU path this
-    is ``engine_probe_fn(engine)``.
+    probe_fn(local_digests (m, 32) uint8) -> (m, HIT_WORDS) int32 hits with
+    GLOBAL entry ids (ngpu_dict_hit words: entry, index, blob, usize,
+    uncompressed offset lo/hi; entry == -1 for a miss) -- on the GPU path
+    ``engine_probe_fn(engine)`` over a partition built by ``engine_load_fn``.
+    router: the owner bucketing (default HipRouter, the GPU kernels).
     """
 
-    def __init__(self, rank: int, world: int, group=None, comm_device=None, cap: int = 0):
+    def __init__(self, rank: int, world: int, group=None, comm_device=None, cap: int = 0,
+                 router=None):
         """comm_device: device the all-to-all runs on (None = the tensors' own;
         "cpu" when the process group is gloo and the data lives on a GPU).
 
@@ -62,11 +107,13 @@ class ShardedChunkDict:
         group (host integers only, the GPU streams are not touched), so a rank
         with more than cap queries runs extra rounds TOGETHER with the others
         instead of failing alone while they block in the collective (ADVICE
-        r2).  cap == 0: variable splits, sized on the host from an all-to-all
-        of the counts (one device sync per probe, minimal bytes)."""
+        r2).  cap == 0: variable splits, sized on the host from the routed
+        counts and an all-to-all of them (one device sync per probe, exact
+        bytes)."""
         self.rank, self.world, self.group = rank, world, group
         self.comm_device = comm_device
         self.cap = int(cap)
+        self.router = router if router is not None else HipRouter()
         self._meta = None  # gloo group for the round-count agreement (created on every rank)
         if self.cap and world > 1:
             import torch.distributed as dist
@@ -74,7 +121,7 @@ class ShardedChunkDict:
                 self._meta = group
             else:
                 self._meta = dist.new_group(ranks=list(range(world)), backend="gloo")
-        self.local_to_global: Optional[torch.Tensor] = None
+        self.n_local = 0
         self.n_blobs = 0
         self.probe_fn: Optional[Callable[[torch.Tensor], torch.Tensor]] = None
 
@@ -85,15 +132,17 @@ class ShardedChunkDict:
         return torch.nonzero(own, as_tuple=False).flatten()
 
     def load(self, digests, usize, blob, index, n_blobs: int, load_fn, uoff=None):
-        """Keep this rank's partition.  load_fn(d, us, bl, ix, uo) builds the
-        local table from the owned rows (engine.dict_create_device on the GPU);
-        uoff (int64 uncompressed offsets) may be None."""
+        """Keep this rank's partition.  load_fn(d, us, bl, ix, uo, gid) builds
+        the local table from the owned rows with their global ids
+        (engine_load_fn: ngpu_dict_create_device_gid); uoff (int64
+        uncompressed offsets) may be None."""
         ids = self.partition(digests)
-        self.local_to_global = ids.to(torch.int64)
         self.n_blobs = n_blobs
+        self.n_local = int(ids.numel())
         load_fn(digests[ids].contiguous(), usize[ids].contiguous(), blob[ids].contiguous(),
-                index[ids].contiguous(), None if uoff is None else uoff[ids].contiguous())
-        return int(ids.numel())
+                index[ids].contiguous(), None if uoff is None else uoff[ids].contiguous(),
+                ids.to(torch.int32).contiguous())
+        return self.n_local
 
     def _a2a(self, out, inp, out_splits, in_splits):
         import torch.distributed as dist
@@ -108,22 +157,18 @@ class ShardedChunkDict:
         if self.cap:
             return self._probe_equal(digests)
         cdev = torch.device(self.comm_device) if self.comm_device else dev
-        own = owner_of(digests, self.world)
-        order = torch.argsort(own, stable=True)
-        send = digests[order].contiguous().to(cdev)
-        counts = torch.bincount(own, minlength=self.world).to(torch.int64).to(cdev)
+        send, rows, counts = self.router.route(digests, self.world)
+        counts = counts.to(torch.int64).to(cdev)
         rcounts = torch.empty_like(counts)
         self._a2a(rcounts, counts, None, None)
         in_splits = counts.tolist()
         out_splits = rcounts.tolist()
         recv = torch.empty((sum(out_splits), 32), dtype=torch.uint8, device=cdev)
-        self._a2a(recv, send, out_splits, in_splits)
+        self._a2a(recv, send.to(cdev), out_splits, in_splits)
         hits = self._local(recv.to(dev)).to(cdev)  # (sum(out_splits), HIT_WORDS)
         back = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=cdev)
         self._a2a(back, hits.contiguous(), in_splits, out_splits)
-        res = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=dev)
-        res[order] = back.to(dev)
-        return res
+        return self.router.scatter(back.to(dev), rows, n)
 
     def rounds(self, n: int) -> int:
         """Equal-split rounds for this probe: ceil(max over ranks of n / cap),
@@ -135,52 +180,31 @@ class ShardedChunkDict:
 
     def _probe_equal(self, digests: torch.Tensor) -> torch.Tensor:
         """Equal-split exchange (cap rows per owner and round, see __init__):
-        each query goes to round pos // cap, row pos % cap of its owner's slot,
-        pos = its rank among this rank's queries for that owner (stable), all
-        computed on the device.  Rows of other rounds write a dummy row cap."""
+        the router puts row k of owner o into slot [k // cap][o][k % cap]
+        (padding: zero digests, row id -1), all on the device."""
         n, W, cap = digests.shape[0], self.world, self.cap
         R = self.rounds(n)
         dev = digests.device
         cdev = torch.device(self.comm_device) if self.comm_device else dev
-        own = owner_of(digests, W)
-        order = torch.argsort(own, stable=True)
-        own_s = own[order]
-        dig_s = digests[order]
-        counts = torch.bincount(own, minlength=W)
-        start = torch.cumsum(counts, 0) - counts
-        pos = torch.arange(n, device=dev) - start[own_s]
-        rnd, row = pos // cap, pos % cap
-        res_s = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=dev)
+        send, rows, _ = self.router.route(digests, W, seg_cap=cap, rounds=R)
+        send, rows = send.view(R, W * cap, 32), rows.view(R, W * cap)
+        res = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=dev)
         for r in range(R):
-            mine = rnd == r
-            idx = torch.where(mine, row, torch.full_like(row, cap))
-            send = torch.zeros((W, cap + 1, 32), dtype=torch.uint8, device=dev)
-            send[own_s, idx] = dig_s
-            send = send[:, :cap].reshape(W * cap, 32).to(cdev)
-            recv = torch.empty_like(send)
-            self._a2a(recv, send, None, None)
+            sr = send[r].to(cdev)
+            recv = torch.empty_like(sr)
+            self._a2a(recv, sr, None, None)
             hits = self._local(recv.to(dev)).to(cdev)  # (W * cap, HIT_WORDS): padding rows ignored
             back = torch.empty_like(hits)
             self._a2a(back, hits.contiguous(), None, None)
-            back = torch.cat([back.to(dev).view(W, cap, HIT_WORDS),
-                              torch.zeros((W, 1, HIT_WORDS), dtype=torch.int32, device=dev)], 1)
-            res_s = torch.where(mine[:, None], back[own_s, idx], res_s)
-        res = torch.empty((n, HIT_WORDS), dtype=torch.int32, device=dev)
-        res[order] = res_s
+            self.router.scatter(back.to(dev), rows[r], n, hits=res)
         return res
 
     def _local(self, digests: torch.Tensor) -> torch.Tensor:
-        if digests.shape[0] == 0 or self.local_to_global is None or self.local_to_global.numel() == 0:
+        if digests.shape[0] == 0 or self.n_local == 0:
             h = torch.zeros((digests.shape[0], HIT_WORDS), dtype=torch.int32, device=digests.device)
             h[:, 0] = -1
             return h
-        h = self.probe_fn(digests).clone()
-        hit = h[:, 0] != -1
-        loc = h[:, 0].to(torch.int64)
-        glob = torch.where(hit, self.local_to_global.to(digests.device)[torch.where(hit, loc, 0)],
-                           torch.full_like(loc, -1))
-        h[:, 0] = glob.to(torch.int32)
-        return h
+        return self.probe_fn(digests)
 
 
 def engine_probe_fn(engine, stream_fn=None):
@@ -196,10 +220,11 @@ def engine_probe_fn(engine, stream_fn=None):
 
 
 def engine_load_fn(engine, n_blobs: int):
-    def load(d, us, bl, ix, uo=None):
+    def load(d, us, bl, ix, uo=None, gid=None):
         torch.cuda.current_stream().synchronize()
         cd = engine.dict_create_device(d.data_ptr(), us.data_ptr(), bl.data_ptr(), ix.data_ptr(),
-                                       d.shape[0], n_blobs, d_uoff=uo.data_ptr() if uo is not None else 0)
+                                       d.shape[0], n_blobs, d_uoff=uo.data_ptr() if uo is not None else 0,
+                                       d_gid=gid.data_ptr() if gid is not None else 0)
         engine.set_dict(cd if d.shape[0] else None)
         cd.release()
     return load

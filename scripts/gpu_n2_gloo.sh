@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 cd "$ROOT"
 NYDUS_NODE_EXTRA_DEVICES=${NYDUS_NODE_EXTRA_DEVICES:-0,0} timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 10 --warmup 5 \
-  --dist-backend gloo > "$OUT/bench_c2_n2_gloo.json" 2> "$OUT/bench_c2_n2_gloo.err"
+  --dist-backend gloo --c4-layers ${C4L:-4} > "$OUT/bench_c2_n2_gloo.json" 2> "$OUT/bench_c2_n2_gloo.err"
 rc=$?
 echo "n2 rc=$rc"
 cat "$OUT/bench_c2_n2_gloo.json"

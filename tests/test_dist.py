@@ -1,7 +1,10 @@
 """Multi-rank chunk-dict partition + all-to-all probe routing on CPU (gloo,
-world_size 2).  The local probe is a plain first-occurrence map here (host
-logic under test: partitioning, owner routing, id translation, ordering);
-the GPU probe behind it is covered by tests/test_gpu_parity.py."""
+world_size 2/4/8).  The local probe is a plain first-occurrence map and the
+owner bucketing a plain torch restatement of ngpu_route_digests /
+ngpu_route_hits (TorchRouter, test infrastructure): the host logic under
+test is the partition, the split agreement, the exchange and the ordering.
+The GPU kernels behind the product router are checked against TorchRouter in
+tests/test_gpu_node.py::test_route_kernels_match_the_reference_router."""
 import os
 import socket
 
@@ -11,7 +14,37 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from nydus_gpu.dist import ShardedChunkDict, owner_of
+from nydus_gpu.dist import HIT_WORDS, ShardedChunkDict, owner_of
+
+
+class TorchRouter:
+    """CPU restatement of the routing kernels (test infrastructure only):
+    compact owner order (stable) or [rounds][world][seg_cap] padded slots."""
+
+    def route(self, digests, world, seg_cap=0, rounds=0):
+        n = digests.shape[0]
+        own = owner_of(digests, world)
+        order = torch.argsort(own, stable=True)
+        counts = torch.bincount(own, minlength=world).to(torch.int32)
+        if not seg_cap:
+            return digests[order].contiguous(), order.to(torch.int32), counts
+        slots = rounds * world * seg_cap
+        out = torch.zeros((slots, 32), dtype=torch.uint8)
+        rows = torch.full((slots,), -1, dtype=torch.int32)
+        start = torch.cumsum(counts.to(torch.int64), 0) - counts.to(torch.int64)
+        own_s = own[order]
+        k = torch.arange(n) - start[own_s]
+        pos = (k // seg_cap) * world * seg_cap + own_s * seg_cap + k % seg_cap
+        out[pos] = digests[order]
+        rows[pos] = order.to(torch.int32)
+        return out, rows, counts
+
+    def scatter(self, routed, rows, n, hits=None):
+        if hits is None:
+            hits = torch.empty((n, HIT_WORDS), dtype=torch.int32)
+        keep = rows >= 0
+        hits[rows[keep].to(torch.int64)] = routed[keep]
+        return hits
 
 
 def _free_port():
@@ -58,14 +91,17 @@ def _worker(rank, world, port, ret, cap=0, nq=None):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         d, us, bl, ix = _global_dict()
-        sd = ShardedChunkDict(rank, world, cap=cap)
+        sd = ShardedChunkDict(rank, world, cap=cap, router=TorchRouter())
         local = {}
 
-        def load(dd, uu, bb, ii, uo):
+        def load(dd, uu, bb, ii, uo, gid):
+            # the partition keeps global table order and answers with GLOBAL
+            # ids (ngpu_dict_create_device_gid)
+            assert bool((gid[1:] > gid[:-1]).all()) if gid.numel() > 1 else True
             for k in range(dd.shape[0]):
                 local.setdefault(dd[k].numpy().tobytes(),
-                                 (k, int(ii[k]), int(bb[k]), int(uu[k]), int(uo[k]) & 0xFFFFFFFF,
-                                  int(uo[k]) >> 32))
+                                 (int(gid[k]), int(ii[k]), int(bb[k]), int(uu[k]),
+                                  int(uo[k]) & 0xFFFFFFFF, int(uo[k]) >> 32))
 
         uoff = torch.arange(len(d), dtype=torch.int64) * 4096
         n_local = sd.load(torch.from_numpy(d), torch.from_numpy(us), torch.from_numpy(bl),
@@ -87,6 +123,37 @@ def _worker(rank, world, port, ret, cap=0, nq=None):
         ret[rank] = (bool((got == exp).all()), n_local)
     finally:
         dist.destroy_process_group()
+
+
+def test_product_router_refuses_host_tensors():
+    """The product router is the GPU kernel pair: host tensors are an error,
+    never a CPU fallback."""
+    from nydus_gpu.dist import HipRouter
+    with pytest.raises(ValueError, match="CUDA"):
+        HipRouter().route(torch.zeros((4, 32), dtype=torch.uint8), 2)
+
+
+def test_reference_router_layouts():
+    """TorchRouter (the CPU statement the GPU kernels are checked against):
+    compact layout = stable owner order with counts; padded layout puts row k
+    of owner o at [k // cap][o][k % cap]."""
+    g = torch.Generator().manual_seed(5)
+    d = torch.randint(0, 256, (300, 32), dtype=torch.uint8, generator=g)
+    r = TorchRouter()
+    out, rows, counts = r.route(d, 4)
+    own = owner_of(d, 4)
+    assert counts.tolist() == torch.bincount(own, minlength=4).tolist()
+    assert torch.equal(out, d[rows.to(torch.int64)])
+    assert bool((owner_of(out, 4)[1:] >= owner_of(out, 4)[:-1]).all())
+    out, rows, counts = r.route(d, 4, seg_cap=32, rounds=-(-300 // 32))
+    for slot in range(rows.numel()):
+        if rows[slot] >= 0:
+            o = (slot // 32) % 4
+            assert owner_of(d[rows[slot].item()][None], 4).item() == o
+            assert torch.equal(out[slot], d[rows[slot].item()])
+        else:
+            assert not out[slot].any()
+    assert sorted(rows[rows >= 0].tolist()) == list(range(300))
 
 
 def test_owner_is_prefix():

@@ -266,3 +266,128 @@ def test_streaming_pack_of_a_9gib_file(oracle):
         assert res["digest"][k].tobytes() == d, k
     assert res["digest"][-1].tobytes() == oracle.blake3(small)
     assert (res["kind"] == nydus_gpu.NEW).all() and st["new_chunks"] == n_big + 1
+
+
+def test_c4_one_gpu_share_through_an_8_part_node(oracle):
+    """configs[3] (C4) at one GPU's share of the 8-GPU node, through the C
+    ABI's node as the driver's node would run it: device 0 listed 8 times, 8
+    parts x 16 layers x 1 GiB (256 x 4 MiB files, 1 MiB chunks, 131,072
+    chunks), 30 % of the chunks drawn from the 65,536-content pool, and the
+    node dict = pool digests + 16M random filler + 1,000 later duplicates of
+    pool rows, partitioned by digest prefix over the 8 parts (routed
+    exchange).  Checked:
+    * every pool chunk is DICT with the pool row's id (the FIRST table row of
+      its digest, not the later duplicate) and that row's index / offset;
+    * every other chunk is NEW, indices 0.. and 1 MiB-step v6 offsets per
+      layer (prefix sums), per-layer stats equal to the decisions;
+    * the replicated dict and the copy exchange give byte-identical results;
+    * three sampled layers field by field against the oracle's dedup of that
+      layer alone with the whole 16M-entry dict (digests by the oracle)."""
+    import torch
+    import bench
+    from nydus_gpu import rafs
+    wl = dict(bench.WORKLOADS["c4"])
+    S, P, W, L = wl["chunk"], wl["pool"], 8, 16
+    wl["n_files"] = wl["n_files"] * L
+    _, stride, _, _ = bench.synthetic_layout(1, wl["file_size"], S)
+    parts = []
+    try:
+        for i in range(W):
+            buf, ch = bench.build_layer_on_gpu(torch, wl["n_files"], wl["file_size"], S,
+                                               seed=0x6E79647573 + i)
+            info, planted = bench.plant_pool(torch, buf, ch, stride, wl, seed=i)
+            parts.append(dict(buf=buf, ch=ch, sel=info["chunks"], src=info["content"],
+                              d_ch=torch.from_numpy(ch.view(np.uint8).copy()).cuda()))
+        n = len(parts[0]["ch"])
+        assert n == 16 * 1024 and int(parts[0]["buf"].numel()) > (16 << 30)
+        per_layer = n // L
+        first = np.arange(L + 1, dtype=np.int64) * per_layer
+        d_first = torch.from_numpy(first).cuda()
+        pool = bench.pool_digests(torch, nydus_gpu, wl, 0).cpu().numpy()
+        rng = np.random.default_rng(0xC4)
+        m = P + wl["dict_entries"] + 1000
+        recs = np.zeros(m, rafs.CHUNK_INFO_DTYPE)
+        recs["block_id"][:P] = pool
+        recs["block_id"][P:m - 1000] = rng.integers(0, 256, (wl["dict_entries"], 32), dtype=np.uint8)
+        dup = rng.choice(P, 1000, replace=False)
+        recs["block_id"][m - 1000:] = pool[dup]
+        recs["uncompressed_size"] = S
+        recs["compressed_size"] = S
+        recs["blob_index"] = rng.integers(0, 8, m)
+        recs["index"] = rng.permutation(m).astype(np.uint32)
+        recs["uncompressed_offset"] = np.arange(m, dtype=np.uint64) * S
+        blobs = rafs.make_blob_table([f"{b:064x}" for b in range(8)], S)
+        node = nydus_gpu.Node([0] * W, chunk_size=S)
+        results = {}
+        try:
+            for name, mode in (("routed", nydus_gpu.NODE_DICT_PARTITION),
+                               ("replicate", nydus_gpu.NODE_DICT_REPLICATE),
+                               ("copy", nydus_gpu.NODE_DICT_PARTITION | nydus_gpu.NODE_EXCHANGE_COPY)):
+                d = node.dict_create(recs, blobs, mode=mode)
+                outs = []
+                for i, p in enumerate(parts):
+                    if name == "copy" and i >= 2:
+                        break  # the copy exchange: two parts suffice for the equality
+                    out = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+                    st = torch.zeros(L * nydus_gpu.LAYER_STATS_DTYPE.itemsize, dtype=torch.uint8,
+                                     device="cuda")
+                    node.process_device(i, d, p["buf"].data_ptr(), p["buf"].numel(), p["d_ch"].data_ptr(),
+                                        n, out.data_ptr(), d_first.data_ptr(), L, st.data_ptr(),
+                                        stream=torch.cuda.current_stream().cuda_stream)
+                    torch.cuda.synchronize()
+                    outs.append((out.cpu().numpy().view(nydus_gpu.RESULT_DTYPE).copy(),
+                                 st.cpu().numpy().view(nydus_gpu.LAYER_STATS_DTYPE).copy()))
+                for e in node.engines:
+                    e.device_status()
+                d.release()
+                results[name] = outs
+        finally:
+            node.close()
+        total_dict = 0
+        for i, p in enumerate(parts):
+            out, stats = results["routed"][i]
+            sel, src = p["sel"], p["src"]
+            assert (out["kind"][sel] == nydus_gpu.DICT).all(), i
+            assert np.array_equal(out["ref"][sel], src), i  # pool row = content id: the first row
+            assert np.array_equal(out["index"][sel], recs["index"][src]), i
+            assert np.array_equal(out["uncompressed_offset"][sel], recs["uncompressed_offset"][src]), i
+            rest = np.ones(n, bool)
+            rest[sel] = False
+            assert (out["kind"][rest] == nydus_gpu.NEW).all(), i
+            for layer in range(L):
+                a, b = first[layer], first[layer + 1]
+                new = out["kind"][a:b] == nydus_gpu.NEW
+                k = int(new.sum())
+                assert np.array_equal(out["index"][a:b][new], np.arange(k)), (i, layer)
+                assert np.array_equal(out["uncompressed_offset"][a:b][new],
+                                      np.arange(k, dtype=np.uint64) * S), (i, layer)
+                assert stats["new_chunks"][layer] == k and stats["dict_chunks"][layer] == per_layer - k
+            total_dict += len(sel)
+            for other in ("replicate", "copy"):
+                if i < len(results[other]):
+                    assert results[other][i][0].tobytes() == out.tobytes(), (other, i)
+                    assert results[other][i][1].tobytes() == stats.tobytes(), (other, i)
+        assert total_dict > 0.29 * W * n
+        # three sampled layers against the oracle with the whole dict
+        for i, layer in ((0, 0), (3, 7), (7, 15)):
+            p = parts[i]
+            out = results["routed"][i][0]
+            a, b = first[layer], first[layer + 1]
+            ch = p["ch"]
+            lo = int(ch["offset"][a])
+            hi = int(ch["offset"][b - 1] + ch["length"][b - 1])
+            blob = p["buf"][lo:hi].cpu().numpy()
+            sub = ch[a:b].copy()
+            sub["offset"] -= lo
+            dig = oracle.digest_chunks(blob, sub.view(oracle.CHUNK_DTYPE), "blake3")
+            assert np.array_equal(out["digest"][a:b], dig), (i, layer)
+            exp, _ = oracle.dedup(dig, sub["length"], recs["block_id"], recs["uncompressed_size"],
+                                  recs["blob_index"], recs["index"], dict_uoff=recs["uncompressed_offset"])
+            for f in ("kind", "index", "blob_index", "uncompressed_offset"):
+                assert np.array_equal(out[f][a:b], exp[f]), (i, layer, f)
+            own = exp["kind"] != nydus_gpu.DICT
+            assert np.array_equal(out["ref"][a:b][own] - a, exp["ref"][own]), (i, layer)
+            assert np.array_equal(out["ref"][a:b][~own], exp["ref"][~own]), (i, layer)
+    finally:
+        parts.clear()
+        torch.cuda.empty_cache()

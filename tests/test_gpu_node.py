@@ -1,10 +1,13 @@
 """GPU: the multi-GPU node behind the C ABI (ngpu_node_*).
 
 On this one-GPU box a node lists device 0 several times: W engines, W dict
-parts and the full exchange (digest packing, hipMemcpyPeerAsync to every
-owner, owned-row probes, hits back, merge by owner) run exactly as on an
-8-GPU node, only the copies stay inside one HBM.  Every decision must equal
-the oracle's with the WHOLE dict (global entry ids, first-entry-wins)."""
+parts and the full exchange run exactly as on an 8-GPU node, only the peer
+traffic stays inside one HBM.  Both exchanges are covered: the routed one
+(ABI 4 default: owner bucketing on the requester, each owner's probe kernel
+reads its own rows and stores hits at their row ids) and the copy one
+(NGPU_NODE_EXCHANGE_COPY: every digest to every owner by hipMemcpyPeerAsync,
+hits back, merge by owner).  Every decision must equal the oracle's with the
+WHOLE dict (global entry ids, first-entry-wins)."""
 import io
 
 import numpy as np
@@ -68,14 +71,18 @@ def _to_dev(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()
 
 
+COPY = nydus_gpu.NODE_DICT_PARTITION | nydus_gpu.NODE_EXCHANGE_COPY
+
+
 @pytest.mark.parametrize("W,mode", [(2, nydus_gpu.NODE_DICT_PARTITION), (4, nydus_gpu.NODE_DICT_PARTITION),
+                                    (8, nydus_gpu.NODE_DICT_PARTITION), (2, COPY), (4, COPY),
                                     (2, nydus_gpu.NODE_DICT_REPLICATE)])
 def test_node_dict_device_layers_vs_oracle(oracle, W, mode):
     """Device-resident layers on every engine of a W-device node against a
     partitioned / replicated node dict == the oracle with the whole dict."""
     import torch
     from nydus_gpu.dist import owner_of
-    rng = np.random.default_rng(40 + W + mode)
+    rng = np.random.default_rng(40 + W + (mode & 0xFF))
     cs = 0x10000
     layers = [_layer(rng, 12 << 20, cs) for _ in range(W)]
     digs = [oracle.digest_chunks(d, c.view(oracle.CHUNK_DTYPE), "blake3") for d, c in layers]
@@ -142,7 +149,8 @@ def test_node_packs_round_robin_write_dict_records(oracle, tars, tmp_path):
         node.close()
 
 
-def test_node_four_requesters_at_once_vs_oracle(oracle):
+@pytest.mark.parametrize("mode", [nydus_gpu.NODE_DICT_PARTITION, COPY])
+def test_node_four_requesters_at_once_vs_oracle(oracle, mode):
     """a 4-part node (device 0 listed 4x) with 4 requester
     threads exchanging at the same time, each on its own engine and stream,
     several rounds each: every (owner, requester) pair has its own channel, so
@@ -161,7 +169,7 @@ def test_node_four_requesters_at_once_vs_oracle(oracle):
     exp = [[_expect(oracle, digs[i][k], layers[i][k][1], recs) for k in range(rounds)] for i in range(W)]
     node = nydus_gpu.Node([0] * W, chunk_size=cs)
     try:
-        d = node.dict_create(recs, blobs, mode=nydus_gpu.NODE_DICT_PARTITION)
+        d = node.dict_create(recs, blobs, mode=mode)
         dev = [[(_to_dev(np.frombuffer(data, np.uint8)), _to_dev(ch)) for data, ch in ls] for ls in layers]
         outs = [[torch.zeros(len(ch) * 64, dtype=torch.uint8, device="cuda") for _, ch in ls] for ls in layers]
         torch.cuda.synchronize()
@@ -196,3 +204,61 @@ def test_node_four_requesters_at_once_vs_oracle(oracle):
         d.release()
     finally:
         node.close()
+
+
+@pytest.mark.parametrize("W", [2, 3, 8, 64])
+def test_route_kernels_match_the_reference_router(W):
+    """ngpu_route_digests / ngpu_route_hits (the product router of dist.py and
+    the node's routed exchange) against TorchRouter, the CPU statement in
+    tests/test_dist.py: the same per-owner counts; every row exactly once in
+    its owner's segment with its own digest (the order inside a segment is
+    the atomics' order, so segments compare as sets); the padded layout fills
+    exactly slots [k // cap][o][k % cap] for k < count(o), padding zeroed with
+    row id -1; hits go back to their rows.  Inputs read at a 64-B stride, as
+    the digests sit in ngpu_result records."""
+    import torch
+    from nydus_gpu.dist import HIT_WORDS, HipRouter, owner_of
+    from test_dist import TorchRouter
+    g = torch.Generator(device="cuda").manual_seed(W)
+    n = 50_000
+    rec = torch.randint(0, 256, (n, 64), dtype=torch.uint8, device="cuda", generator=g)
+    rec[1000:3000, :32] = rec[0, :32]  # a hot owner: many equal digests
+    dig = rec[:, :32]
+    hr, tr = HipRouter(), TorchRouter()
+    out, rows, counts = hr.route(dig, W)
+    torch.cuda.synchronize()
+    _, rrows, rcounts = tr.route(dig.cpu(), W)
+    assert counts.cpu().tolist() == rcounts.tolist()
+    assert torch.equal(out, dig[rows.to(torch.int64)])
+    start = 0
+    for o, c in enumerate(rcounts.tolist()):
+        a = np.sort(rows[start:start + c].cpu().numpy())
+        b = np.sort(rrows[start:start + c].numpy())
+        assert np.array_equal(a, b), o
+        start += c
+    # padded layout
+    cap = 257
+    R = -(-n // cap)
+    out, rows, counts = hr.route(dig, W, seg_cap=cap, rounds=R)
+    torch.cuda.synchronize()
+    rows_h = rows.cpu().numpy()
+    filled = rows_h >= 0
+    assert np.array_equal(np.sort(rows_h[filled]), np.arange(n))
+    assert not out[torch.from_numpy(~filled).cuda()].any()
+    assert torch.equal(out[torch.from_numpy(filled).cuda()],
+                       dig[torch.from_numpy(rows_h[filled].astype(np.int64)).cuda()])
+    slot = np.nonzero(filled)[0]
+    own_slot = (slot // cap) % W
+    own_row = owner_of(dig.cpu(), W).numpy()[rows_h[filled]]
+    assert np.array_equal(own_slot, own_row)
+    k_of_slot = (slot // (W * cap)) * cap + slot % cap
+    for o, c in enumerate(counts.cpu().tolist()):
+        assert np.array_equal(np.sort(k_of_slot[own_slot == o]), np.arange(c)), o
+    # hits back to rows: routed hits = (row id, ...) words
+    routed = torch.zeros((rows.numel(), HIT_WORDS), dtype=torch.int32, device="cuda")
+    routed[:, 0] = rows
+    routed[:, 1] = rows * 3
+    hits = hr.scatter(routed, rows, n)
+    torch.cuda.synchronize()
+    assert torch.equal(hits[:, 0].cpu(), torch.arange(n, dtype=torch.int32))
+    assert torch.equal(hits[:, 1].cpu(), torch.arange(n, dtype=torch.int32) * 3)
