@@ -574,10 +574,43 @@ int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
  * the host and compress them.  ngpu_pack_finish = ngpu_pack_close + stream
  * (releases the pack in every case). */
 #define NGPU_PACK_RETAIN 0x1u
+/* PackOption.OCIRef (ABI 4; `nydus-image create --type targz-ref`,
+ * builder.go:180-218): ngpu_pack_write takes the ORIGINAL gzip layer blob.  The
+ * library inflates it on the host (one gzip member), the tar stream takes the
+ * tar-rafs path (tar walk, GPU digests, layered dedup; no chunk dict, as
+ * packRef passes none), and a checkpoint of the deflate stream is kept every
+ * max(chunk size, 1 MiB) of output.  The output stream holds no image.blob:
+ * blob.meta (chunk-info array with each chunk's checkpoint, the checkpoint
+ * table and the 32 KiB dictionaries), blob.digest, image.boot and the TOC; the
+ * bootstrap's own blob is the gzip blob (id = its sha256, the digest Merge
+ * returns for the layer, converter_test.go TestPackRef), each chunk record
+ * carrying the deflate range that produces it.  Layout restated (VERIFY).
+ * ngpu_pack_reserve / ngpu_pack_commit are not available (EINVAL). */
+#define NGPU_PACK_OCIREF 0x2u
+/* The reader side of an OCIRef layer (host; what nydusd does with a targz-ref
+ * blob): chunk `index` of the layer's own blob, located through `blob_meta`
+ * (the layer stream's blob.meta entry: chunk-info array, checkpoint table,
+ * dictionaries, header) and inflated out of the original gzip blob `gz` from
+ * its checkpoint.  *len_out = the chunk's size (<= cap).  (ABI 4) */
+int ngpu_ref_chunk_read(const void *gz, uint64_t gz_len, const void *blob_meta, uint64_t meta_len,
+                        uint32_t index, void *out, uint32_t cap, uint32_t *len_out);
 int ngpu_pack_open_ex(ngpu_engine *eng, uint32_t flags, ngpu_pack **out);
 int ngpu_pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx,
                      ngpu_chunk **chunks_out, ngpu_result **results_out, uint64_t *n_out,
                      ngpu_layer_stats *stats, ngpu_blob_info *info);
+/* Early emission (ABI 4): give a NGPU_PACK_RETAIN pack its output before the
+ * first write (converter.Pack knows `dest` when it opens, convert_unix.go:325).
+ * An emitter thread then writes the blob stream while the tar is still
+ * arriving: after each staging slot is digested it dedups the prefix so far
+ * (a chunk's decision depends only on the chunks before it) and compresses,
+ * hashes and writes the NEW chunks that became final, so the sequential host
+ * SHA-256 of the stream overlaps the copies and digests of the rest of the
+ * layer.  Finish with ngpu_pack_finish(p, NULL, NULL, NULL, ...): it writes the
+ * rest, image.boot and the TOC.  The bytes are the same as with a writer given
+ * to ngpu_pack_finish.  `opt` is copied (prefetch_patterns too); dict_blobs /
+ * dict_chunks must stay valid until finish.  w is called from the library's
+ * threads.  An emitter error fails the next write and the finish. */
+int ngpu_pack_set_output(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx);
 
 /* UnpackEntry (convert_unix.go:284-320): find `name` through the TOC
  * (seekFileByTOC :219-276; entry compressor none or zstd), else by walking

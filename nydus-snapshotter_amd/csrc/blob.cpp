@@ -172,18 +172,7 @@ uint64_t super_flags(uint32_t kind, uint32_t digester) {
 
 }  // namespace
 
-// ---- SHA-256 (OpenSSL EVP) -------------------------------------------------
-struct Sha {
-  EVP_MD_CTX *c = EVP_MD_CTX_new();
-  Sha() { EVP_DigestInit_ex(c, EVP_sha256(), nullptr); }
-  ~Sha() { EVP_MD_CTX_free(c); }
-  void update(const void *p, uint64_t n) { EVP_DigestUpdate(c, p, n); }
-  void final(uint8_t out[32]) {
-    unsigned int l = 32;
-    EVP_DigestFinal_ex(c, out, &l);
-  }
-  void copy_from(const Sha &o) { EVP_MD_CTX_copy_ex(c, o.c); }
-};
+// ---- SHA-256 (OpenSSL EVP; Sha in blob.hpp) --------------------------------
 
 void sha256(const void *p, uint64_t n, uint8_t out[32]) {
   Sha s;
@@ -494,6 +483,7 @@ struct BlobWriter::Impl {
   const DictPlace *dict_place = nullptr;
   uint64_t n_place = 0;
   const volatile int32_t *cancel = nullptr;
+  const ZranRef *zref = nullptr;  // OCIRef: the own blob is the original gzip blob
   std::unique_ptr<Pool> pool;
   Sha blob_sha;      // image.blob data
   Sha stream_sha;    // whole stream (continued from blob_sha)
@@ -594,6 +584,7 @@ BlobWriter::BlobWriter(const ngpu_blob_options &opt, ngpu_write_fn w, void *ctx,
 }
 
 void BlobWriter::set_cancel(const volatile int32_t *flag) { im_->cancel = flag; }
+void BlobWriter::set_zran(const ZranRef *z) { im_->zref = z; }
 
 BlobWriter::~BlobWriter() = default;
 
@@ -691,32 +682,40 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
   Bootstrap b;
   b.flags = super_flags(kind, m.opt.digester);
   b.chunk_size = m.opt.chunk_size;
+  const ZranRef *zr = m.zref;
+  if (zr) b.flags = (b.flags & ~0x83ull) | 0x40;  // RafsSuperFlags COMPRESSION_GZIP (VERIFY)
+  const uint64_t bodies = zr ? zr->coff.size() : m.csize.size();
   uint64_t k = 0, coff = 0, uend = 0;
   for (uint64_t i = 0; i < n; ++i) {
     const ngpu_result &r = res[i];
     if (r.kind != NGPU_NEW) continue;
-    if (r.index != k || k >= m.csize.size())
+    if (r.index != k || k >= bodies)
       return host_fail(NGPU_EINVAL, "pack: NEW chunk %llu out of index order",
                        (unsigned long long)i);
     RafsV6ChunkInfo c;
     memset(&c, 0, sizeof c);
     memcpy(c.block_id, r.digest, 32);
     c.blob_index = r.blob_index;
-    c.flags = m.cflag[k];
-    c.compressed_size = m.csize[k];
+    if (zr) {  // targz-ref: the chunk's deflate range in the original gzip blob
+      c.flags = 1;  // compressed (gzip, through its checkpoint)
+      c.compressed_size = (uint32_t)zr->csize[k];
+      c.compressed_offset = zr->coff[k];
+    } else {
+      c.flags = m.cflag[k];
+      c.compressed_size = m.csize[k];
+      c.compressed_offset = coff;
+      coff += m.csize[k];
+    }
     c.uncompressed_size = chunks[i].length;
-    c.compressed_offset = coff;
     c.uncompressed_offset = r.uncompressed_offset;
     c.file_offset = chunks[i].file_offset;
     c.index = r.index;
     b.chunks.push_back(c);
-    coff += m.csize[k];
     uend = std::max<uint64_t>(uend, r.uncompressed_offset + chunks[i].length);
     ++k;
   }
-  if (k != m.csize.size()) return host_fail(NGPU_EINVAL, "pack: %llu chunk bodies for %llu NEW chunks",
-                                            (unsigned long long)m.csize.size(),
-                                            (unsigned long long)k);
+  if (k != bodies) return host_fail(NGPU_EINVAL, "pack: %llu chunk bodies for %llu NEW chunks",
+                                    (unsigned long long)bodies, (unsigned long long)k);
   // every chunk's record, for the inode tree: a NEW or INTRA chunk points at
   // the NEW record of its index, a DICT chunk at the dict's copy (below)
   RafsLayerInfo li;
@@ -798,14 +797,14 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
   if (st.own_blob_index != 0xFFFFFFFFu) {
     if (st.own_blob_index >= st.blobs) return host_fail(NGPU_EINVAL, "pack: bad own blob index");
     RafsV6BlobInfo &o = b.blobs[st.own_blob_index];
-    const std::string id = hex(blob_dig, 32);
+    const std::string id = hex(zr ? zr->digest : blob_dig, 32);  // targz-ref: the gzip blob's digest
     memcpy(o.blob_id, id.data(), 64);
     o.chunk_size = m.opt.chunk_size;
     o.chunk_count = (uint32_t)k;
-    o.compression_algo = blob_compression_algo(kind);
+    o.compression_algo = zr ? 2 : blob_compression_algo(kind);  // compress::Algorithm GZip (VERIFY)
     o.digest_algo = m.opt.digester == NGPU_DIGEST_SHA256 ? 1 : 0;
     o.features = 1;
-    o.compressed_size = coff;
+    o.compressed_size = zr ? zr->gz_size : coff;
     o.uncompressed_size = (uend + 4095) / 4096 * 4096;
     set[st.own_blob_index] = true;
   }
@@ -855,8 +854,10 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     e.uncompressed_size = usize;
     toc.push_back(e);
   };
-  toc_add("image.blob", NGPU_COMPRESSOR_NONE, blob_dig, 0, blob_bytes, blob_bytes);
-  hdr("image.blob", blob_bytes);
+  if (!zr) {  // targz-ref: the data stays in the original gzip blob, no image.blob
+    toc_add("image.blob", NGPU_COMPRESSOR_NONE, blob_dig, 0, blob_bytes, blob_bytes);
+    hdr("image.blob", blob_bytes);
+  }
   // blob.meta / blob.meta.header / blob.digest (convert_unix.go:47-48 names the
   // first two; `--blob-inline-meta --features blob-toc`, builder.go:97-110,
   // makes nydus-image write all three for a blob with chunks).  Restated from
@@ -885,10 +886,23 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
                   ((uint64_t)(c.flags & 1) << 56);  // CHUNK_V2_FLAG_COMPRESSED
       ci[3 * x + 1] = (c.compressed_offset & 0xFFFFFFFFFFull) |
                       ((uint64_t)(c.compressed_size - 1) << 40);
+      if (zr) {  // CHUNK_V2_FLAG_ZRAN; data = checkpoint index << 32 | offset in its output (VERIFY)
+        ci[3 * x] |= 0x2ull << 56;
+        ci[3 * x + 2] = (uint64_t)zr->ctx[x] << 32 | zr->ctx_off[x];
+      }
       memcpy(&dig[32 * x], c.block_id, 32);
     }
-    const uint8_t *ci_raw = (const uint8_t *)ci.data();
-    const uint64_t ci_len = ci.size() * 8;
+    // targz-ref: the checkpoint table and dictionaries follow the chunk-info
+    // array inside blob.meta (ZranInflateContext records, VERIFY)
+    const uint64_t ci_entries_len = ci.size() * 8;
+    std::vector<uint8_t> ci_all;
+    if (zr) {
+      ci_all.assign((const uint8_t *)ci.data(), (const uint8_t *)ci.data() + ci_entries_len);
+      ci_all.insert(ci_all.end(), zr->table.begin(), zr->table.end());
+      ci_all.insert(ci_all.end(), zr->dicts.begin(), zr->dicts.end());
+    }
+    const uint8_t *ci_raw = zr ? ci_all.data() : (const uint8_t *)ci.data();
+    const uint64_t ci_len = zr ? ci_all.size() : ci_entries_len;
     uint8_t ci_dig[32];
     sha256(ci_raw, ci_len, ci_dig);
     std::vector<uint8_t> z;
@@ -898,7 +912,7 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     // entry carries the same compressor (the Go reader opens zstd / none only,
     // convert_unix.go:219-276: an lz4_block blob's blob.meta is for nydusd).
     uint32_t ci_algo = 0, ci_flag = NGPU_COMPRESSOR_NONE;  // compress::Algorithm None = 0
-    if (kind == NGPU_COMPRESSOR_ZSTD || kind == NGPU_COMPRESSOR_LZ4_BLOCK) {
+    if (!zr && (kind == NGPU_COMPRESSOR_ZSTD || kind == NGPU_COMPRESSOR_LZ4_BLOCK)) {
       z.resize(compress_bound(kind, (uint32_t)ci_len));
       const uint64_t zl = compress_one(kind, 0, ci_raw, (uint32_t)ci_len, z.data(), z.size());
       if (zl) {
@@ -915,7 +929,9 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     const uint32_t magic = 0xB10BB10Bu;  // BLOB_CCT_MAGIC
     // BlobFeatures: ALIGNED | INLINED_FS_META | CHUNK_INFO_V2 | INLINED_CHUNK_DIGEST |
     // HAS_TAR_HEADER | HAS_TOC | CAP_TAR_TOC
-    const uint32_t feat = 0x1 | 0x2 | 0x4 | 0x20 | 0x10000000u | 0x20000000u | 0x40000000u;
+    // (+ ZRAN 0x8 for targz-ref, VERIFY)
+    const uint32_t feat = 0x1 | 0x2 | 0x4 | 0x20 | 0x10000000u | 0x20000000u | 0x40000000u |
+                          (zr ? 0x8u : 0u);
     const uint32_t nent = (uint32_t)k;
     memcpy(h + 0, &magic, 4);
     memcpy(h + 4, &feat, 4);
@@ -924,6 +940,15 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     memcpy(h + 16, &ci_off, 8);
     memcpy(h + 24, &ci_size, 8);
     memcpy(h + 32, &ci_len, 8);
+    if (zr) {  // where the checkpoint table and dictionaries sit (offsets in the uncompressed blob.meta)
+      const uint64_t zt_off = ci_entries_len, zt_size = zr->table.size(), zt_cnt = zr->n_points;
+      const uint64_t zd_off = zt_off + zt_size, zd_size = zr->dicts.size();
+      memcpy(h + 40, &zt_off, 8);
+      memcpy(h + 48, &zt_size, 8);
+      memcpy(h + 56, &zt_cnt, 8);
+      memcpy(h + 64, &zd_off, 8);
+      memcpy(h + 72, &zd_size, 8);
+    }
     memcpy(h + 4088, &magic, 4);  // s_magic2
     uint8_t h_dig[32], d_dig[32];
     sha256(h, sizeof h, h_dig);
@@ -987,7 +1012,7 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     info->dict_records = ndict;
     info->meta_entries = meta_entries;
     memcpy(info->stream_digest, stream_dig, 32);
-    memcpy(info->blob_digest, blob_dig, 32);
+    memcpy(info->blob_digest, zr ? zr->digest : blob_dig, 32);  // targz-ref: the gzip blob
     memcpy(info->toc_digest, toc_dig, 32);
   }
   return 0;

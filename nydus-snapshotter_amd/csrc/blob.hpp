@@ -13,6 +13,8 @@
 #include <string>
 #include <vector>
 
+#include <openssl/evp.h>
+
 #include "nydus_gpu.h"
 #include "tarstream.hpp"
 
@@ -86,6 +88,21 @@ int guarded(F &&f) noexcept {
   }
 }
 
+// Incremental SHA-256 (OpenSSL EVP).
+struct Sha {
+  EVP_MD_CTX *c = EVP_MD_CTX_new();
+  Sha() { EVP_DigestInit_ex(c, EVP_sha256(), nullptr); }
+  ~Sha() { EVP_MD_CTX_free(c); }
+  Sha(const Sha &) = delete;
+  Sha &operator=(const Sha &) = delete;
+  void update(const void *p, uint64_t n) { EVP_DigestUpdate(c, p, n); }
+  void final(uint8_t out[32]) {
+    unsigned int l = 32;
+    EVP_DigestFinal_ex(c, out, &l);
+  }
+  void copy_from(const Sha &o) { EVP_MD_CTX_copy_ex(c, o.c); }
+};
+
 // Host helpers (blob.cpp): the thread's last host error (ngpu_host_error),
 // OpenSSL SHA-256, lower-case hex, the dlopen'ed compressors.
 int host_fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -121,6 +138,21 @@ int parse_bootstrap(const uint8_t *p, uint64_t n, Bootstrap *out, bool with_chun
 std::vector<uint8_t> write_bootstrap(const Bootstrap &b);
 std::string blob_id_of(const RafsV6BlobInfo &b);
 
+// An OCIRef layer's own blob is the ORIGINAL gzip blob (targz-ref): its
+// chunks are addressed through gzip checkpoints (zran.hpp) instead of image.blob
+// data.  Per NEW chunk (index order): the checkpoint it starts after, its
+// offset in that checkpoint's output, and the compressed range that produces
+// it; the checkpoint table and dictionaries go into blob.meta.
+struct ZranRef {
+  uint8_t digest[32];        // sha256 of the gzip blob: the own blob's id
+  uint64_t gz_size = 0, tar_size = 0;
+  std::vector<uint64_t> coff, csize;   // per NEW chunk: compressed range in the gzip blob
+  std::vector<uint32_t> ctx, ctx_off;  // per NEW chunk: checkpoint index, offset in its output
+  // checkpoint table (40-B records) and dictionary area, as written to blob.meta
+  std::vector<uint8_t> table, dicts;
+  uint64_t n_points = 0;
+};
+
 // Sequential writer of the nydus formatted stream for one layer.
 class BlobWriter {
  public:
@@ -143,6 +175,9 @@ class BlobWriter {
   const std::string &error() const { return err_; }
   // Cancellation: checked before each compression batch (NGPU_ECANCELED).
   void set_cancel(const volatile int32_t *flag);
+  // OCIRef (targz-ref): finish() writes no image.blob; the own blob is the
+  // gzip blob of `z` (set before finish; add() is not called).
+  void set_zran(const ZranRef *z);
 
  private:
   struct Impl;

@@ -268,6 +268,9 @@ void launch_route(const uint8_t *src, uint64_t stride, uint64_t n, uint32_t W, u
 void launch_dict_probe_routed(const uint8_t *q, const uint32_t *rows, const uint32_t *cnt,
                               uint64_t n_max, uint32_t owner, const DictDevice &dict,
                               ngpu_dict_hit *hits, hipStream_t s);
+// Records [0, n) a dedup stage accepted get kind = NGPU_DIGESTED again
+// (rejected ones keep NGPU_UNHASHED): a later dedup over a longer prefix.
+void launch_remark_digested(ngpu_result *res, uint64_t n, hipStream_t s);
 // hits[rows[i]] = routed[i] for rows[i] != ~0.
 void launch_hits_scatter(const ngpu_dict_hit *routed, const uint32_t *rows, uint64_t m,
                          ngpu_dict_hit *hits, hipStream_t s);

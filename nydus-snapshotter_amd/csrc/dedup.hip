@@ -1171,6 +1171,22 @@ __global__ void hits_scatter(const ngpu_dict_hit *__restrict__ routed,
 
 }  // namespace
 
+namespace {
+// A record a dedup stage accepted (NEW / INTRA / DICT) gets its digest mark
+// back, so a later dedup over a longer prefix of the same layer accepts it
+// again; a record the stage rejected (NGPU_UNHASHED) keeps that mark, so the
+// digest guard still fires on it (streaming Pack emission, pack.hip).
+__global__ void remark_digested(ngpu_result *__restrict__ r, uint64_t n) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i < n && r[i].kind <= NGPU_DICT) r[i].kind = NGPU_DIGESTED;
+}
+}  // namespace
+
+void launch_remark_digested(ngpu_result *res, uint64_t n, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(remark_digested, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, res, n);
+}
+
 void launch_route(const uint8_t *src, uint64_t stride, uint64_t n, uint32_t W, uint64_t seg_cap,
                   uint32_t *cnt, uint8_t *out, uint32_t *rows, hipStream_t s) {
   hipMemsetAsync(cnt, 0, 128 * sizeof(uint32_t), s);

@@ -24,16 +24,30 @@
 // GPU into window buffers in blob (index) order and only those bytes cross
 // PCIe, window k+1's gather + D2H overlapping the host compression of window k
 // (blob.cpp BlobWriter).
+//
+// ngpu_pack_set_output (early emission): with the output
+// known when the Pack opens (converter.Pack's `dest`, convert_unix.go:325), an
+// emitter thread writes the blob stream while the caller is still writing the
+// tar.  A chunk's decision depends only on the chunks before it (stream order),
+// so after each staging slot is digested the emitter dedups the whole prefix
+// dispatched so far and the NEW chunks of the new part are final: they are
+// gathered, copied back and handed to the BlobWriter, whose sequential
+// SHA-256 -- the bound of converter.Pack end to end -- then runs alongside the
+// H2D copies and digests of the rest of the layer instead of after them.
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <condition_variable>
+#include <memory>
+#include <string>
 #include <thread>
 #include <vector>
 
 #include "blob.hpp"
 #include "engine_internal.hpp"
 #include "tarstream.hpp"
+#include "zran.hpp"
 
 using namespace ngpu;
 
@@ -57,6 +71,32 @@ struct Seg {
   uint8_t *d = nullptr;
   uint64_t base = 0;     // stream offset of d[0]
   uint64_t a = 0, b = 0; // chunks [a, b) live here
+};
+
+// Early emission state (ngpu_pack_set_output).  ch / dptr / avail / deduped
+// are guarded by the engine lock (dispatch appends under it); emitted and rc
+// belong to the emitter thread until it is joined.
+struct Emit {
+  ngpu_blob_options opt{};
+  std::string prefetch;
+  std::unique_ptr<BlobWriter> bw;
+  std::vector<ngpu_chunk> ch;    // dispatched chunks (stream offsets)
+  std::vector<uint64_t> dptr;    // device address of each dispatched chunk's bytes
+  uint64_t avail = 0;            // chunks dispatched
+  uint64_t deduped = 0;          // prefix covered by the last dedup stage (remarked before the next)
+  uint64_t emitted = 0;          // chunks whose NEW bytes went to the writer
+  uint64_t new_emitted = 0;      // NEW chunks among them
+  std::atomic<uint64_t> hint{0}; // = avail, for the emitter's wait
+  std::atomic<int> rc{0};
+  std::thread th;
+  std::mutex m;
+  std::condition_variable cv;
+  bool stop = false;
+  ngpu_result *h_res = nullptr;  // pinned landing of the prefix results
+  uint64_t h_cap = 0;
+  uint64_t *h_stats = nullptr;   // pinned: the prefix stage's counters (digest guard)
+  hipEvent_t ev = nullptr;
+  ngpu_staging_buf land[2];      // pinned landing of the blob windows (engine staging pool)
 };
 
 // Copies chunk k (src[k], len[k] bytes) to dst + doff[k] (16-B aligned).
@@ -161,6 +201,8 @@ struct ngpu_pack : TarSink {
   bool retain = false;       // NGPU_PACK_RETAIN: device segments kept to the end
   std::vector<Seg> segs;
   std::vector<TarEntry> entries;  // NGPU_PACK_RETAIN: the tar's entries (the bootstrap's inode tree)
+  Emit *em = nullptr;              // ngpu_pack_set_output: the stream leaves while the tar arrives
+  std::unique_ptr<GzipIndexer> gz; // NGPU_PACK_OCIREF: the gzip blob is inflated and indexed
   int err = 0;
 
   explicit ngpu_pack(ngpu_engine *eng) : e(eng), sc(eng->cfg.chunk_size) {}
@@ -178,11 +220,14 @@ bool cancelled(const ngpu_pack *p) {
   return p->cancel && __atomic_load_n(p->cancel, __ATOMIC_RELAXED) != 0;
 }
 
+void emit_stop(ngpu_pack *p);  // below
+
 void release(ngpu_pack *p) {
   if (!p) return;
   ngpu_engine *e = p->e;
   ngpu_dict *dict = p->dict;
   DeviceGuard dg(e->device);
+  emit_stop(p);
   for (Slot &s : p->slot) {
     if (s.done) (void)hipEventSynchronize(s.done);
   }
@@ -207,6 +252,31 @@ void release(ngpu_pack *p) {
     if (s.done) (void)hipEventDestroy(s.done);
   }
   for (Seg &g : p->segs) (void)hipFree(g.d);
+  if (Emit *em = p->em) {  // its landing buffers go back to the staging pool
+    std::lock_guard<std::mutex> g(e->pool_mu);
+    for (ngpu_staging_buf &b : em->land) {
+      if (!b.h) continue;
+      const bool whole = b.h_ch && b.d_ch && b.copied && b.done;  // a pool entry (else: own landing)
+      if (whole && e->staging_pool.size() < ngpu_engine::kStagingPool) {
+        e->staging_pool.push_back(b);
+      } else {
+        (void)hipHostFree(b.h);
+        if (b.h_ch) (void)hipHostFree(b.h_ch);
+        if (b.d) (void)hipFree(b.d);
+        if (b.d_ch) (void)hipFree(b.d_ch);
+        if (b.copied) (void)hipEventDestroy(b.copied);
+        if (b.done) (void)hipEventDestroy(b.done);
+      }
+      b = ngpu_staging_buf{};
+    }
+  }
+  if (Emit *em = p->em) {
+    if (em->h_res) (void)hipHostFree(em->h_res);
+    if (em->h_stats) (void)hipHostFree(em->h_stats);
+    if (em->ev) (void)hipEventDestroy(em->ev);
+    delete em;
+    p->em = nullptr;
+  }
   {
     // the streams are idle (synchronised above).  Every compute stream goes
     // back to the pool: the engine's workspace slots may still name it as
@@ -256,6 +326,25 @@ int grow_results(ngpu_pack *p, uint64_t want) {
   return 0;
 }
 
+// The layer's device chunk table (p->d_all) holds at least `want` entries,
+// its contents kept (e->mu held; a regrow waits for the pack's stream).
+int grow_all(ngpu_pack *p, uint64_t want) {
+  if (want <= p->all_cap) return 0;
+  uint64_t c = p->all_cap ? p->all_cap : 4096;
+  while (c < want) c *= 2;
+  ngpu_chunk *n = nullptr;
+  HIP_TRY(p->e, hipMalloc((void **)&n, c * sizeof(ngpu_chunk)));
+  if (p->d_all) {
+    HIP_TRY(p->e, hipMemcpyAsync(n, p->d_all, p->all_cap * sizeof(ngpu_chunk),
+                                 hipMemcpyDeviceToDevice, p->stream));
+    HIP_TRY(p->e, hipStreamSynchronize(p->stream));
+    (void)hipFree(p->d_all);
+  }
+  p->d_all = n;
+  p->all_cap = c;
+  return 0;
+}
+
 // Copy the slot to HBM and digest chunks [a, b) (all inside the slot).
 int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
   if (b == a) return 0;
@@ -288,11 +377,28 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
                             p->copy));
   HIP_TRY(e, hipEventRecord(s.copied, p->copy));
   HIP_TRY(e, hipStreamWaitEvent(p->stream, s.copied, 0));
+  if (p->em && !p->gz) {  // the prefix dedups read lengths from the layer's device chunk table
+    if ((rc = grow_all(p, b + 1))) return rc;
+    HIP_TRY(e, hipMemcpyAsync(p->d_all + a, s.d_ch, nch * sizeof(ngpu_chunk),
+                              hipMemcpyDeviceToDevice, p->stream));
+  }
   rc = enqueue_digest(e, dev, s.fill, s.d_ch, nch, p->d_res + a, p->stream);
   if (rc) return rc;
   HIP_TRY(e, hipEventRecord(s.done, p->stream));
   s.busy = true;
   p->dispatched = b;
+  if (Emit *em = p->gz ? nullptr : p->em) {  // the new range is the emitter's (e->mu held)
+    for (uint64_t k = a; k < b; ++k) {
+      em->ch.push_back(p->chunks[k]);
+      em->dptr.push_back((uint64_t)(uintptr_t)(dev + (p->chunks[k].offset - s.base)));
+    }
+    em->avail = b;
+    {
+      std::lock_guard<std::mutex> g(em->m);
+      em->hint.store(b);
+    }
+    em->cv.notify_one();
+  }
   return 0;
 }
 
@@ -352,13 +458,10 @@ int eager_copy(ngpu_pack *p, Slot &s) {
   return 0;
 }
 
-// After dedup: gather the NEW chunks from the retained segments in blob
-// (index) order into window buffers, copy each window to the host and hand it
-// to the BlobWriter; window k+1's gather + D2H run while the host compresses
-// window k.  Called with e->mu held.
-int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, void *ctx,
-                 const ngpu_chunk *ch, const ngpu_result *res, uint64_t n,
-                 const ngpu_layer_stats &st, ngpu_blob_info *info) {
+// The pack's BlobWriter: dict blob table and compressed placements from the
+// caller's options or the pack's dict (RAFS options from the engine).
+int make_writer(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, void *ctx,
+                std::unique_ptr<BlobWriter> *out) {
   ngpu_engine *e = p->e;
   ngpu_blob_options o = opt;
   o.digester = e->cfg.digester;
@@ -379,25 +482,31 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
     place = p->dict->place.data();
     nplace = p->dict->place.size();
   }
-  BlobWriter bw(o, w, ctx, std::move(dict), place, nplace);
-  bw.set_cancel(p->cancel);
-  int rc = bw.init();
-  if (rc) return fail(e, rc, "pack: %s", ngpu_host_error());
+  out->reset(new BlobWriter(o, w, ctx, std::move(dict), place, nplace));
+  (*out)->set_cancel(p->cancel);
+  if (int rc = (*out)->init()) return fail(e, rc, "pack: %s", ngpu_host_error());
+  return 0;
+}
 
-  // device address of every NEW chunk (index order == stream order)
+// Gather the NEW chunks among `count` decided chunks (device address dptr[i],
+// stream descriptor ch[i], decision res[i]; index order == stream order) into
+// window buffers on the GPU, copy each window to a pinned landing buffer
+// (land[0/1], alternating) and hand it to the BlobWriter; window k+1's gather
+// + D2H run while the host compresses window k.  Enqueues on the pack's
+// stream without the engine lock (pack-owned buffers only).
+int emit_range(ngpu_pack *p, BlobWriter &bw, const ngpu_chunk *ch, const uint64_t *dptr,
+               const ngpu_result *res, uint64_t count, uint8_t *const land[2],
+               uint64_t *new_out) {
+  ngpu_engine *e = p->e;
   std::vector<uint64_t> src;
   std::vector<uint32_t> len;
-  size_t g = 0;
-  for (uint64_t i = 0; i < n; ++i) {
+  for (uint64_t i = 0; i < count; ++i) {
     if (res[i].kind != NGPU_NEW) continue;
-    while (g < p->segs.size() && p->segs[g].b <= i) ++g;
-    if (g == p->segs.size()) return fail(e, NGPU_EINVAL, "pack: chunk %llu has no segment",
-                                         (unsigned long long)i);
-    const Seg &sg = p->segs[g];
-    src.push_back((uint64_t)(uintptr_t)(sg.d + (ch[i].offset - sg.base)));
+    src.push_back(dptr[i]);
     len.push_back(ch[i].length);
   }
   const uint64_t k = src.size();
+  if (new_out) *new_out += k;
   // windows of <= cap bytes (16-B aligned placement) and <= maxk chunks
   const uint64_t cap = p->cap, maxk = 1ull << 18;
   std::vector<uint64_t> wstart{0};
@@ -420,7 +529,7 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
   while (kneed < k && kneed < maxk) kneed *= 2;
   BlobWindows &bw_ = p->win;
   if (nw && (bw_.cap < cap || bw_.kcap < kneed || !bw_.ev[0])) {
-    (void)hipStreamSynchronize(p->stream);  // a previous Pack's windows may still be read
+    (void)hipStreamSynchronize(p->stream);  // a previous range's windows may still be read
     blob_windows_free(bw_);
     bool ok = true;
     for (int i = 0; i < 2 && ok; ++i)
@@ -439,7 +548,6 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
   uint8_t *const *dwin = bw_.dwin, *const *ddesc = bw_.ddesc, *const *hdesc = bw_.hdesc;
   const hipEvent_t *ev = bw_.ev;
   const uint64_t kc = bw_.kcap;  // descriptor slots per window buffer
-  auto cleanup = [&] { (void)hipStreamSynchronize(p->stream); };
   auto enqueue = [&](uint64_t wi) -> int {
     const int b = wi & 1;
     const uint64_t a = wstart[wi], c = wstart[wi + 1] - a;
@@ -460,10 +568,11 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
     HIP_TRY(e, hipGetLastError());
     const uint64_t bytes = doff[a + c - 1] + len[a + c - 1];
     if (int rc = host_fence(e, ps, p->fence)) return rc;
-    HIP_TRY(e, hipMemcpyAsync(p->slot[b].h, dwin[b], bytes, hipMemcpyDeviceToHost, ps));
+    HIP_TRY(e, hipMemcpyAsync(land[b], dwin[b], bytes, hipMemcpyDeviceToHost, ps));
     HIP_TRY(e, hipEventRecord(ev[b], ps));
     return 0;
   };
+  int rc = 0;
   std::vector<const uint8_t *> hp;
   if (nw) rc = enqueue(0);
   for (uint64_t wi = 0; wi < nw && !rc; ++wi) {
@@ -479,14 +588,200 @@ int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, vo
     }
     const uint64_t a = wstart[wi], c = wstart[wi + 1] - a;
     hp.resize(c);
-    for (uint64_t i = 0; i < c; ++i) hp[i] = p->slot[b].h + doff[a + i];
+    for (uint64_t i = 0; i < c; ++i) hp[i] = land[b] + doff[a + i];
     if ((rc = bw.add(hp.data(), &len[a], c))) rc = fail(e, rc, "pack: %s", ngpu_host_error());
   }
-  cleanup();
-  if (rc) return rc;
-  if ((rc = bw.finish(ch, res, n, st, p->entries, info)))
+  // every window was waited for on success; after an error the next one may
+  // still be in flight
+  if (rc) (void)hipStreamSynchronize(p->stream);
+  return rc;
+}
+
+// Device address of every chunk of the layer in the retained segments.
+int chunk_addresses(ngpu_pack *p, const ngpu_chunk *ch, uint64_t from, uint64_t n,
+                    std::vector<uint64_t> *dptr) {
+  dptr->resize(n - from);
+  size_t g = 0;
+  for (uint64_t i = from; i < n; ++i) {
+    while (g < p->segs.size() && p->segs[g].b <= i) ++g;
+    if (g == p->segs.size())
+      return fail(p->e, NGPU_EINVAL, "pack: chunk %llu has no segment", (unsigned long long)i);
+    const Seg &sg = p->segs[g];
+    (*dptr)[i - from] = (uint64_t)(uintptr_t)(sg.d + (ch[i].offset - sg.base));
+  }
+  return 0;
+}
+
+// The whole stream at close (no early emission): every NEW chunk, then the
+// headers, blob.meta, image.boot and TOC.  The landing buffers are the pinned
+// staging slots (the layer's bytes are all written by now).
+int write_stream(ngpu_pack *p, const ngpu_blob_options &opt, ngpu_write_fn w, void *ctx,
+                 const ngpu_chunk *ch, const ngpu_result *res, uint64_t n,
+                 const ngpu_layer_stats &st, ngpu_blob_info *info) {
+  std::unique_ptr<BlobWriter> bw;
+  if (int rc = make_writer(p, opt, w, ctx, &bw)) return rc;
+  std::vector<uint64_t> dptr;
+  if (int rc = chunk_addresses(p, ch, 0, n, &dptr)) return rc;
+  uint8_t *const land[2] = {p->slot[0].h, p->slot[1].h};
+  if (int rc = emit_range(p, *bw, ch, dptr.data(), res, n, land, nullptr)) return rc;
+  if (int rc = bw->finish(ch, res, n, st, p->entries, info))
+    return fail(p->e, rc, "pack: %s", ngpu_host_error());
+  return 0;
+}
+
+// ---- early emission -----------------------------------------------------------
+// One iteration of the emitter: dedup the dispatched prefix [0, k) (its
+// records from the previous prefix remarked first), copy the decisions of
+// [emitted, k) back, check the digest guard, write their NEW chunks.
+int emit_step(ngpu_pack *p, Emit *em) {
+  ngpu_engine *e = p->e;
+  const uint64_t a = em->emitted;
+  uint64_t k = 0;
+  std::vector<ngpu_chunk> ch;
+  std::vector<uint64_t> dptr;
+  std::string path;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    DeviceGuard dg(e->device);
+    k = em->avail;
+    if (k <= a) return 0;
+    ch.assign(em->ch.begin() + (long)a, em->ch.begin() + (long)k);
+    dptr.assign(em->dptr.begin() + (long)a, em->dptr.begin() + (long)k);
+    if (k - a > em->h_cap) {
+      uint64_t c = em->h_cap ? em->h_cap : 4096;
+      while (c < k - a) c *= 2;
+      if (em->h_res) (void)hipHostFree(em->h_res), em->h_res = nullptr, em->h_cap = 0;
+      HIP_TRY(e, hipHostMalloc((void **)&em->h_res, c * sizeof(ngpu_result), hipHostMallocDefault));
+      em->h_cap = c;
+    }
+    hipStream_t ps = p->stream;
+    launch_remark_digested(p->d_res, em->deduped, ps);
+    HIP_TRY(e, hipGetLastError());
+    if (int rc = enqueue_dedup(e, p->dict, p->d_all, k, p->d_res, nullptr, 0, ps, nullptr, 1, nullptr))
+      return rc;
+    em->deduped = k;
+    if (int rc = host_fence(e, ps, p->fence)) return rc;
+    HIP_TRY(e, hipMemcpyAsync(em->h_res, p->d_res + a, (k - a) * sizeof(ngpu_result),
+                              hipMemcpyDeviceToHost, ps));
+    if (int rc = read_stats_enqueue(e, ps, em->h_stats)) return rc;
+    HIP_TRY(e, hipEventRecord(em->ev, ps));
+    path = e->cur->path;
+  }
+  HIP_TRY(e, hipEventSynchronize(em->ev));
+  ngpu_layer_stats st{};
+  if (int rc = read_stats_parse(e, em->h_stats, &st, path.c_str())) return rc;  // digest guard
+  uint8_t *const land[2] = {(uint8_t *)em->land[0].h, (uint8_t *)em->land[1].h};
+  if (int rc = emit_range(p, *em->bw, ch.data(), dptr.data(), em->h_res, k - a, land,
+                          &em->new_emitted))
+    return rc;
+  em->emitted = k;
+  return 0;
+}
+
+void emit_loop(ngpu_pack *p, Emit *em) {
+  DeviceGuard dg(p->e->device);
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> g(em->m);
+      em->cv.wait(g, [&] { return em->stop || em->hint.load() > em->emitted; });
+      if (em->stop) return;
+    }
+    if (cancelled(p)) {
+      em->rc = fail(p->e, NGPU_ECANCELED, "pack: cancelled");
+      return;
+    }
+    if (int rc = emit_step(p, em)) {
+      em->rc = rc;
+      return;
+    }
+  }
+}
+
+// Close of an OCIRef Pack (targz-ref): the gzip stream must have ended; the
+// own blob is the gzip blob, each NEW chunk addressed by the checkpoint it
+// starts after and the deflate range that produces it (ZranRef, blob.hpp).
+int ref_finish(ngpu_pack *p, BlobWriter &bw, const ngpu_chunk *ch, const ngpu_result *res,
+               uint64_t n, const ngpu_layer_stats &st, ngpu_blob_info *info) {
+  ngpu_engine *e = p->e;
+  GzipIndexer &gz = *p->gz;
+  if (int rc = gz.finish()) return fail(e, rc, "pack: %s", ngpu_host_error());
+  ZranRef zr;
+  gz.blob_digest(zr.digest);
+  zr.gz_size = gz.in_bytes();
+  zr.tar_size = gz.out_bytes();
+  const std::vector<ZranPoint> &pts = gz.points();
+  zr.n_points = pts.size();
+  zr.dicts = gz.dicts();
+  // ZranInflateContext records, 40 B (restated, VERIFY): in_offset u64,
+  // out_offset u64, in_len u32, out_len u32 (to the next checkpoint), ctx_byte
+  // u8, ctx_bits u8, reserved u16, dict_size u32, dict_offset u64
+  zr.table.assign(40 * pts.size(), 0);
+  for (size_t i = 0; i < pts.size(); ++i) {
+    const ZranPoint &x = pts[i];
+    const uint64_t in_next = i + 1 < pts.size() ? pts[i + 1].in_offset : zr.gz_size;
+    const uint64_t out_next = i + 1 < pts.size() ? pts[i + 1].out_offset : zr.tar_size;
+    const uint32_t in_len = (uint32_t)(in_next - x.in_offset), out_len = (uint32_t)(out_next - x.out_offset);
+    uint8_t *r = zr.table.data() + 40 * i;
+    memcpy(r, &x.in_offset, 8);
+    memcpy(r + 8, &x.out_offset, 8);
+    memcpy(r + 16, &in_len, 4);
+    memcpy(r + 20, &out_len, 4);
+    r[24] = (uint8_t)x.byte;
+    r[25] = (uint8_t)x.bits;
+    memcpy(r + 28, &x.dict_size, 4);
+    memcpy(r + 32, &x.dict_offset, 8);
+  }
+  for (uint64_t i = 0; i < n; ++i) {
+    if (res[i].kind != NGPU_NEW) continue;
+    const uint64_t off = ch[i].offset, end = off + ch[i].length;
+    if (pts.empty() || end > zr.tar_size)
+      return fail(e, NGPU_EINVAL, "pack: OCIRef chunk %llu outside the inflated stream",
+                  (unsigned long long)i);
+    const uint64_t k = gz.point_of(off);
+    const ZranPoint &x = pts[k];
+    const uint64_t coff = x.in_offset - (x.bits ? 1 : 0);
+    zr.coff.push_back(coff);
+    zr.csize.push_back(gz.in_end_of(end) - coff);
+    zr.ctx.push_back((uint32_t)k);
+    zr.ctx_off.push_back((uint32_t)(off - x.out_offset));
+  }
+  bw.set_zran(&zr);
+  if (int rc = bw.finish(ch, res, n, st, p->entries, info))
     return fail(e, rc, "pack: %s", ngpu_host_error());
   return 0;
+}
+
+// Close of an early-emission Pack: the final dedup over the whole layer gave
+// the same decisions for the chunks already written (stream order; checked by
+// their NEW count), so the rest [emitted, n) follows and the writer finishes.
+int emit_finish(ngpu_pack *p, Emit *em, const ngpu_chunk *ch, const ngpu_result *res, uint64_t n,
+                const ngpu_layer_stats &st, ngpu_blob_info *info) {
+  ngpu_engine *e = p->e;
+  uint64_t same = 0;
+  for (uint64_t i = 0; i < em->emitted && i < n; ++i) same += res[i].kind == NGPU_NEW;
+  if (em->emitted > n || same != em->new_emitted)
+    return fail(e, NGPU_EDEVICE, "pack: %llu NEW chunks written early, %llu in the final decisions",
+                (unsigned long long)em->new_emitted, (unsigned long long)same);
+  std::vector<uint64_t> dptr;
+  if (int rc = chunk_addresses(p, ch, em->emitted, n, &dptr)) return rc;
+  uint8_t *const land[2] = {(uint8_t *)em->land[0].h, (uint8_t *)em->land[1].h};
+  if (int rc = emit_range(p, *em->bw, ch + em->emitted, dptr.data(), res + em->emitted,
+                          n - em->emitted, land, &em->new_emitted))
+    return rc;
+  if (int rc = em->bw->finish(ch, res, n, st, p->entries, info))
+    return fail(e, rc, "pack: %s", ngpu_host_error());
+  return 0;
+}
+
+void emit_stop(ngpu_pack *p) {
+  Emit *em = p->em;
+  if (!em || !em->th.joinable()) return;
+  {
+    std::lock_guard<std::mutex> g(em->m);
+    em->stop = true;
+  }
+  em->cv.notify_all();
+  em->th.join();
 }
 
 }  // namespace
@@ -508,8 +803,17 @@ int ngpu_pack_open(ngpu_engine *e, ngpu_pack **out) { return ngpu_pack_open_ex(e
 static ngpu_dict *const kDefaultDict = reinterpret_cast<ngpu_dict *>(1);
 
 static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack **out) {
-  if (!e || !out || (flags & ~NGPU_PACK_RETAIN)) return NGPU_EINVAL;
+  if (!e || !out || (flags & ~(NGPU_PACK_RETAIN | NGPU_PACK_OCIREF))) return NGPU_EINVAL;
   *out = nullptr;
+  const bool ociref = (flags & NGPU_PACK_OCIREF) != 0;
+  std::unique_ptr<GzipIndexer> gz;
+  if (ociref) {  // packRef (builder.go:180-218) passes no --chunk-dict
+    if (dict != kDefaultDict && dict)
+      return fail(e, NGPU_EINVAL, "OCIRef (targz-ref) takes no chunk dict");
+    dict = nullptr;
+    gz.reset(new GzipIndexer(std::max<uint64_t>(e->cfg.chunk_size, 1ull << 20)));
+    if (int rc = gz->init()) return fail(e, rc, "pack: %s", ngpu_host_error());
+  }
   std::lock_guard<std::mutex> g(e->mu);
   DeviceGuard dg(e->device);
   if (dict == kDefaultDict) dict = e->dict;
@@ -519,7 +823,9 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
   dict_ref(dict);
   p->dict = dict;
   p->retain = flags & NGPU_PACK_RETAIN;
-  if (p->retain) p->sc.record(&p->entries);  // the stream's bootstrap lists every entry
+  p->gz = std::move(gz);
+  // the stream's bootstrap lists every entry (OCIRef: the bootstrap is all it carries)
+  if (p->retain || p->gz) p->sc.record(&p->entries);
   uint64_t cap = e->cfg.staging_bytes;
   if (cap < 4ull * e->cfg.chunk_size) cap = 4ull * e->cfg.chunk_size;
   p->cap = cap;
@@ -604,15 +910,70 @@ int ngpu_pack_open_dict(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pa
   return pack_open(e, dict, flags, out);
 }
 
+int ngpu_pack_set_output(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn w, void *ctx) {
+  if (!p || !opt || !w) return NGPU_EINVAL;
+  return guarded([&]() -> int {
+    ngpu_engine *e = p->e;
+    if (!p->retain && !p->gz)
+      return fail(e, NGPU_EINVAL, "pack: early output needs NGPU_PACK_RETAIN");
+    if (p->em || !p->chunks.empty() || p->slot[p->cur].fill || p->dispatched)
+      return fail(e, NGPU_EINVAL, "pack: the output is set once, before the first write");
+    DeviceGuard dg(e->device);
+    Emit *em = new Emit();
+    p->em = em;
+    em->opt = *opt;
+    em->prefetch = opt->prefetch_patterns ? opt->prefetch_patterns : "";
+    // NULL stays NULL: the writer's default patterns ("/") apply to it
+    em->opt.prefetch_patterns = opt->prefetch_patterns ? em->prefetch.c_str() : nullptr;
+    if (int rc = make_writer(p, em->opt, w, ctx, &em->bw)) return rc;
+    HIP_TRY(e, hipHostMalloc((void **)&em->h_stats, 32 * sizeof(uint64_t), hipHostMallocDefault));
+    HIP_TRY(e, hipEventCreateWithFlags(&em->ev, hipEventDisableTiming));
+    {  // window landing buffers: staging slots from the engine's pool when it has them
+      std::lock_guard<std::mutex> g(e->pool_mu);
+      auto &pool = e->staging_pool;
+      for (ngpu_staging_buf &b : em->land)
+        for (size_t i = 0; i < pool.size(); ++i)
+          if (pool[i].cap == p->cap) {
+            b = pool[i];
+            pool.erase(pool.begin() + (long)i);
+            break;
+          }
+    }
+    for (ngpu_staging_buf &b : em->land)
+      if (!b.h) {
+        HIP_TRY(e, hipHostMalloc(&b.h, p->cap, hipHostMallocDefault));
+        b.cap = p->cap;
+      }
+    // OCIRef: the stream carries no chunk data, nothing leaves before the close
+    if (!p->gz) em->th = std::thread([p, em] { emit_loop(p, em); });
+    return 0;
+  });
+}
+
 int ngpu_pack_set_cancel(ngpu_pack *p, const volatile int32_t *flag) {
   if (!p) return NGPU_EINVAL;
   p->cancel = flag;
   return 0;
 }
 
+static int pack_reserve(ngpu_pack *p, void **ptr, uint64_t *avail);
+static int pack_commit(ngpu_pack *p, uint64_t n);
+
 int ngpu_pack_reserve(ngpu_pack *p, void **ptr, uint64_t *avail) {
   if (!p || !ptr || !avail) return NGPU_EINVAL;
+  if (p->gz) return fail(p->e, NGPU_EINVAL, "pack: an OCIRef pack takes gzip bytes through ngpu_pack_write");
+  return pack_reserve(p, ptr, avail);
+}
+
+int ngpu_pack_commit(ngpu_pack *p, uint64_t n) {
+  if (!p) return NGPU_EINVAL;
+  if (p->gz) return fail(p->e, NGPU_EINVAL, "pack: an OCIRef pack takes gzip bytes through ngpu_pack_write");
+  return pack_commit(p, n);
+}
+
+static int pack_reserve(ngpu_pack *p, void **ptr, uint64_t *avail) {
   if (p->err) return p->err;
+  if (p->em && p->em->rc.load()) return p->err = p->em->rc.load();  // the emitter failed
   if (cancelled(p)) return p->err = fail(p->e, NGPU_ECANCELED, "pack: cancelled");
   Slot &s = p->slot[p->cur];
   if (s.fill == p->cap) {
@@ -626,8 +987,7 @@ int ngpu_pack_reserve(ngpu_pack *p, void **ptr, uint64_t *avail) {
   return 0;
 }
 
-int ngpu_pack_commit(ngpu_pack *p, uint64_t n) {
-  if (!p) return NGPU_EINVAL;
+static int pack_commit(ngpu_pack *p, uint64_t n) {
   if (p->err) return p->err;
   if (cancelled(p)) return p->err = fail(p->e, NGPU_ECANCELED, "pack: cancelled");
   Slot &s = p->slot[p->cur];
@@ -639,12 +999,32 @@ int ngpu_pack_commit(ngpu_pack *p, uint64_t n) {
   return 0;
 }
 
+static int pack_write_plain(ngpu_pack *p, const void *buf, uint64_t len);
+
 int ngpu_pack_write(ngpu_pack *p, const void *buf, uint64_t len) {
+  if (!p) return NGPU_EINVAL;
+  if (p->gz) {  // OCIRef: inflate the gzip blob into the tar path, indexing as it goes
+    if (p->err) return p->err;
+    if (!len) return 0;
+    const int rc = guarded([&] {
+      return p->gz->feed((const uint8_t *)buf, len,
+                         [&](const uint8_t *t, uint64_t n) { return pack_write_plain(p, t, n); });
+    });
+    if (rc) {
+      if (!p->err) p->err = fail(p->e, rc, "OCIRef: %s", ngpu_host_error());
+      return p->err;
+    }
+    return 0;
+  }
+  return pack_write_plain(p, buf, len);
+}
+
+static int pack_write_plain(ngpu_pack *p, const void *buf, uint64_t len) {
   const uint8_t *b = (const uint8_t *)buf;
   while (len) {
     void *dst;
     uint64_t avail;
-    int rc = ngpu_pack_reserve(p, &dst, &avail);
+    int rc = pack_reserve(p, &dst, &avail);
     if (rc) return rc;
     const uint64_t take = len < avail ? len : avail;
     if (take >= (8ull << 20)) {
@@ -662,7 +1042,7 @@ int ngpu_pack_write(ngpu_pack *p, const void *buf, uint64_t len) {
     } else {
       memcpy(dst, b, take);
     }
-    rc = ngpu_pack_commit(p, take);
+    rc = pack_commit(p, take);
     if (rc) return rc;
     b += take;
     len -= take;
@@ -689,10 +1069,14 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
   *results_out = nullptr;
   *n_out = 0;
   ngpu_engine *e = p->e;
-  int rc = p->err ? p->err : p->sc.finish();
+  Emit *em = p->em;
+  emit_stop(p);  // the emitter stops after its current range; the rest is written below
+  int rc = p->err ? p->err : (em && em->rc.load()) ? em->rc.load() : p->sc.finish();
   if (!rc && cancelled(p)) rc = fail(e, NGPU_ECANCELED, "pack: cancelled");
-  if (!rc && w && !p->retain)
+  if (!rc && w && !p->retain && !p->gz)
     rc = fail(e, NGPU_EINVAL, "pack: writing the blob stream needs ngpu_pack_open_ex(NGPU_PACK_RETAIN)");
+  if (!rc && w && em)
+    rc = fail(e, NGPU_EINVAL, "pack: the output was set by ngpu_pack_set_output");
   const uint64_t n = p->chunks.size();
   ngpu_chunk *ch = nullptr;
   ngpu_result *res = nullptr;
@@ -745,6 +1129,10 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
           rc = fail(e, NGPU_EHIP, "pack: chunk table copy failed");
         d_dedup = p->d_all;
       }
+      if (!rc && em) {  // records the emitter's last prefix stage decided get their mark back
+        launch_remark_digested(p->d_res, em->deduped, ps);
+        if (hipGetLastError() != hipSuccess) rc = fail(e, NGPU_EHIP, "pack: remark failed");
+      }
       if (!rc)
         rc = enqueue_dedup(e, p->dict, d_dedup, n, p->d_res, nullptr, 0, ps, nullptr, 1, nullptr);
       if (!rc) rc = host_fence(e, ps, p->fence);
@@ -763,7 +1151,15 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
     if (!rc) rc = read_stats_parse(e, p->h_stats, &st, path.c_str());
     if (!rc && n) memcpy(res, p->h_io, n * sizeof(ngpu_result));
     // the blob stream is host work on the pack's own buffers: no engine lock
-    if (!rc && w) rc = write_stream(p, *opt, w, ctx, ch, res, n, st, info);
+    if (!rc && w && p->gz) {
+      std::unique_ptr<BlobWriter> bw;
+      rc = make_writer(p, *opt, w, ctx, &bw);
+      if (!rc) rc = ref_finish(p, *bw, ch, res, n, st, info);
+    } else if (!rc && w) {
+      rc = write_stream(p, *opt, w, ctx, ch, res, n, st, info);
+    }
+    if (!rc && em) rc = p->gz ? ref_finish(p, *em->bw, ch, res, n, st, info)
+                              : emit_finish(p, em, ch, res, n, st, info);
   }
   release(p);
   if (rc) {

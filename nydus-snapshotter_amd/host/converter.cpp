@@ -142,9 +142,17 @@ Error engine_for(const PackOption &opt, ngpu_engine **out) {
 class GpuPackWriteCloser : public PackWriteCloser {
  public:
   GpuPackWriteCloser(ngpu_engine *e, ngpu_pack *p, Writer &dest, uint32_t comp, double timeout,
-                     std::string prefetch)
+                     std::string prefetch, bool ociref = false)
       : e_(e), p_(p), dest_(dest), comp_(comp), timeout_(timeout), prefetch_(std::move(prefetch)) {
     ngpu_pack_set_cancel(p_, &cancel_);
+    // `dest` is known at Pack() (convert_unix.go:325): the stream leaves while
+    // the tar arrives (ngpu_pack_set_output, early emission); Close finishes it.
+    // PrefetchPatterns: the builder's stdin, "/" by default (builder.go:125-127, 166)
+    ngpu_blob_options o;
+    memset(&o, 0, sizeof o);
+    o.compressor = comp_;
+    o.prefetch_patterns = ociref ? nullptr : prefetch_.c_str();
+    out_rc_ = ngpu_pack_set_output(p_, &o, write_trampoline, &dest_);
     if (timeout_ > 0)  // builder.go:153-158: the builder runs under ctx.WithTimeout
       timer_ = std::thread([this] {
         std::unique_lock<std::mutex> g(tm_);
@@ -159,6 +167,13 @@ class GpuPackWriteCloser : public PackWriteCloser {
   void Cancel() override { __atomic_store_n(&cancel_, 1, __ATOMIC_RELAXED); }
   Error Write(const void *p, size_t n) override {
     if (!p_) return err(NGPU_EINVAL, "write to a closed pack");
+    if (out_rc_) {
+      Error e = err(out_rc_, std::string("pack output: ") + ngpu_last_error(e_));
+      ngpu_pack_abort(p_);
+      p_ = nullptr;
+      StopTimer();
+      return e;
+    }
     if (!n) return {};
     if (int rc = ngpu_pack_write(p_, p, n)) {
       Error e = Killed(rc, std::string("pack write: ") + ngpu_last_error(e_));
@@ -171,12 +186,13 @@ class GpuPackWriteCloser : public PackWriteCloser {
   }
   Error Close() override {
     if (!p_) return err(NGPU_EINVAL, "pack already closed");
-    ngpu_blob_options o;
-    memset(&o, 0, sizeof o);
-    o.compressor = comp_;
-    // PackOption.PrefetchPatterns: the builder's stdin, "/" by default
-    // (builder.go:125-127, 166)
-    o.prefetch_patterns = prefetch_.c_str();
+    if (out_rc_) {
+      Error e = err(out_rc_, std::string("pack output: ") + ngpu_last_error(e_));
+      ngpu_pack_abort(p_);
+      p_ = nullptr;
+      StopTimer();
+      return e;
+    }
     ngpu_chunk *ch = nullptr;
     ngpu_result *res = nullptr;
     uint64_t n = 0;
@@ -184,7 +200,7 @@ class GpuPackWriteCloser : public PackWriteCloser {
     ngpu_blob_info info;
     ngpu_pack *p = p_;
     p_ = nullptr;
-    const int rc = ngpu_pack_finish(p, &o, write_trampoline, &dest_, &ch, &res, &n, &st, &info);
+    const int rc = ngpu_pack_finish(p, nullptr, nullptr, nullptr, &ch, &res, &n, &st, &info);
     StopTimer();
     if (rc) return Killed(rc, std::string("convert nydus ref: ") + ngpu_last_error(e_));
     ngpu_free_host(ch);
@@ -224,6 +240,7 @@ class GpuPackWriteCloser : public PackWriteCloser {
   double timeout_;
   std::string prefetch_;
   alignas(4) volatile int32_t cancel_ = 0;
+  int out_rc_ = 0;  // ngpu_pack_set_output at construction
   std::thread timer_;
   std::mutex tm_;
   std::condition_variable tcv_;
@@ -299,12 +316,20 @@ Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser>
   if (Error e = detect_features(required, &detected)) return e;
   if (opt.OCIRef) {
     if (fv != "6") return err(NGPU_EINVAL, "oci ref can only be supported by fs version 6");
-    // packRef (builder.go:180-218) runs `nydus-image create --type targz-ref`:
-    // the chunks stay in the original gzip layer, addressed through a zran
-    // (gzip random access) index in blob.meta, which this builder does not write
-    return err(NGPU_EUNSUPP,
-               "OCIRef (--type targz-ref) needs a zran gzip index of the original layer in "
-               "blob.meta; the GPU builder packs tar-rafs only");
+    // packRef (builder.go:180-218): `nydus-image create --type targz-ref` with
+    // nydus-image's defaults (v6, 1 MiB chunks, blake3, no chunk dict).  The
+    // writer takes the ORIGINAL gzip layer (convert_unix.go:857-859):
+    // inflated and indexed on the host, digested and deduped on the GPU; the
+    // stream holds blob.meta (chunk infos + gzip checkpoints), image.boot, TOC.
+    PackOption ref;
+    ref.Device = opt.Device;
+    ngpu_engine *e = nullptr;
+    if (Error x = engine_for(ref, &e)) return x;
+    ngpu_pack *p = nullptr;
+    if (int rc = ngpu_pack_open_dict(e, nullptr, NGPU_PACK_OCIREF, &p))
+      return err(rc, std::string("pack open: ") + ngpu_last_error(e));
+    out->reset(new GpuPackWriteCloser(e, p, dest, NGPU_COMPRESSOR_NONE, opt.Timeout, "", true));
+    return {};
   }
   const bool batch = std::find(detected.begin(), detected.end(), kFeatureBatchSize) != detected.end();
   if (batch && fv != "6") return err(NGPU_EINVAL, "'--batch-size' can only be supported by fs version 6");
@@ -358,7 +383,9 @@ Error Merge(const std::vector<Layer> &layers, Writer &dest, const MergeOption &o
     if (!layers[i].ReaderAt) return err(NGPU_EINVAL, "layer without reader");
     if (Error e = UnpackEntry(*layers[i].ReaderAt, EntryBootstrap, boots[i], nullptr))
       return err(e.code, "unpack all bootstraps: unpack nydus tar: " + e.msg);
-    const std::string &d = layers[i].Digest;
+    // an OCIRef layer's blob is its original gzip blob, named by its
+    // OriginalDigest (getBootstrapPath, convert_unix.go:567-573)
+    const std::string &d = layers[i].OriginalDigest.empty() ? layers[i].Digest : layers[i].OriginalDigest;
     hexes[i] = d.compare(0, 7, "sha256:") == 0 ? d.substr(7) : d;
   }
   std::vector<uint8_t> dict;

@@ -119,6 +119,7 @@ struct UnpackOption {  // types.go:135-145
 struct Layer {  // types.go:37-44
   std::string Digest;  // "sha256:<hex>" of the whole nydus tar blob
   std::shared_ptr<converter::ReaderAt> ReaderAt;
+  std::string OriginalDigest;  // OCIRef: "sha256:<hex>" of the original gzip layer (or empty)
 };
 
 // Pack result details beyond the Go API (the digest LayerConvertFunc computes

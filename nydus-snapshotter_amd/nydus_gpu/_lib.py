@@ -31,6 +31,7 @@ EINVAL, EUNSUPP, ENODEV, EFORMAT, ENOTFOUND, ECANCELED, EDEVICE = -1, -5, -6, -8
 # "" is nydus-image's default (zstd).
 COMPRESSORS = {"": 0x2, "none": 0x1, "zstd": 0x2, "lz4_block": 0x4}
 PACK_RETAIN = 0x1
+PACK_OCIREF = 0x2  # ngpu_pack_write takes the original gzip layer (targz-ref)
 
 WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
 READ_AT_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
@@ -68,7 +69,8 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_node_owner", "ngpu_node_pack_open", "ngpu_node_process_device",
            "ngpu_device_status", "ngpu_unpack",
            # ABI 4
-           "ngpu_dict_create_device_gid", "ngpu_route_digests", "ngpu_route_hits"]
+           "ngpu_dict_create_device_gid", "ngpu_route_digests", "ngpu_route_hits",
+           "ngpu_pack_set_output", "ngpu_ref_chunk_read"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
@@ -215,6 +217,8 @@ def lib():
     L.ngpu_dict_create_device_gid.argtypes = [vp, vp, vp, vp, vp, vp, vp, u64, u32, ctypes.POINTER(vp)]
     L.ngpu_route_digests.argtypes = [vp, u64, u64, u32, u64, u32, vp, vp, vp, vp]
     L.ngpu_route_hits.argtypes = [vp, vp, u64, vp, vp]
+    L.ngpu_pack_set_output.argtypes = [vp, ctypes.c_void_p, WRITE_FN, vp]
+    L.ngpu_ref_chunk_read.argtypes = [vp, u64, vp, u64, u32, vp, u32, ctypes.POINTER(u32)]
     L.ngpu_dict_retain.argtypes = [vp]
     L.ngpu_dict_retain.restype = None
     L.ngpu_dict_release.argtypes = [vp]
@@ -435,6 +439,17 @@ def rafs_dump(bootstrap: bytes) -> dict:
     sink.reraise()
     _host_check(rc, "rafs_dump")
     return json.loads(b"".join(out).decode("ascii"))
+
+
+def ref_chunk_read(gz, blob_meta, index: int, cap: int = 1 << 24) -> bytes:
+    """ngpu_ref_chunk_read: chunk `index` of an OCIRef layer's own blob, out of
+    the original gzip blob through the checkpoints in its blob.meta entry."""
+    g, m = _buf(gz), _buf(blob_meta)
+    out = np.empty(cap, np.uint8)
+    n = ctypes.c_uint32(0)
+    _host_check(lib().ngpu_ref_chunk_read(_ptr(g), g.size, _ptr(m), m.size, index, _ptr(out), cap,
+                                          ctypes.byref(n)), "ref_chunk_read")
+    return out[: n.value].tobytes()
 
 
 def route_digests(d_digests: int, stride: int, n: int, world: int, d_out: int, d_rows: int,
@@ -736,11 +751,13 @@ class Engine:
         self._check(lib().ngpu_timing_at(self._h, back, ctypes.byref(t)), "timing_at")
         return t.as_dict()
 
-    def pack(self, retain: bool = False, dict=DEFAULT_DICT) -> "PackWriter":
+    def pack(self, retain: bool = False, dict=DEFAULT_DICT, ociref: bool = False) -> "PackWriter":
         """Streaming Pack (converter.Pack mirror): returns a writer.  retain=True
         keeps the layer in HBM so finish() can write the nydus blob stream.
-        dict: a ChunkDict, None, or the engine's default at open time."""
-        return PackWriter(self, retain, dict)
+        dict: a ChunkDict, None, or the engine's default at open time.
+        ociref=True (PackOption.OCIRef, targz-ref): write() takes the original
+        gzip layer blob; no chunk dict."""
+        return PackWriter(self, retain, None if ociref else dict, ociref)
 
     def pack_tar(self, tar):
         """Whole tar layer -> (chunks, results, stats)."""
@@ -770,19 +787,37 @@ class PackWriter:
     any split, close() -> (chunks, results, stats).  Errors raise NgpuError;
     a failed writer is released (like Close() reporting the builder error)."""
 
-    def __init__(self, engine: Engine, retain: bool = False, dict=DEFAULT_DICT):
+    _out = None  # set_output: (options, keep-alive arrays, sink)
+
+    def __init__(self, engine: Engine, retain: bool = False, dict=DEFAULT_DICT, ociref: bool = False):
         self._eng = engine
         h = ctypes.c_void_p()
-        fl = PACK_RETAIN if retain else 0
+        fl = (PACK_RETAIN if retain else 0) | (PACK_OCIREF if ociref else 0)
         if dict is DEFAULT_DICT:
             rc = lib().ngpu_pack_open_ex(engine._h, fl, ctypes.byref(h))
         else:
             rc = lib().ngpu_pack_open_dict(engine._h, _dict_arg(dict), fl, ctypes.byref(h))
         engine._check(rc, "pack_open")
         self._p = h
+        self._out = None  # set_output: (options, keep-alive arrays, sink)
         # cancel flag (ngpu_pack_set_cancel): caller-owned, outlives the pack
         self._cancel = ctypes.c_int32(0)
         lib().ngpu_pack_set_cancel(self._p, ctypes.byref(self._cancel))
+
+    def set_output(self, dest, compressor: str = "", level: int = 0, threads: int = 0,
+                   dict_blobs: np.ndarray = None, prefetch_patterns: str = ""):
+        """ngpu_pack_set_output (needs retain=True, before the first write): the
+        blob stream goes to `dest` while the tar is written; finish() then
+        completes it (call finish() with no dest)."""
+        o, keep = blob_options(compressor, level, threads, self._eng.digester, self._eng.chunk_size,
+                               dict_blobs, fs_version=self._eng.fs_version,
+                               prefetch_patterns=prefetch_patterns)
+        sink = _Sink(dest)
+        rc = lib().ngpu_pack_set_output(self._p, ctypes.byref(o), sink.fn, sink.ctx)
+        if rc:
+            self.abort()
+            self._eng._check(rc, "pack_set_output")
+        self._out = (o, keep, sink)
 
     def cancel(self):
         """ctx.Done(): the running or next write / close fails with ECANCELED.
@@ -794,6 +829,8 @@ class PackWriter:
         rc = lib().ngpu_pack_write(self._p, _ptr(buf), buf.size)
         if rc:
             self.abort()
+            if self._out is not None:
+                self._out[2].reraise()  # dest failed under the emitter
             self._eng._check(rc, "pack_write")
         return buf.size
 
@@ -839,7 +876,13 @@ class PackWriter:
         st = NgpuLayerStats()
         info = NgpuBlobInfo()
         p, self._p = self._p, None
-        if dest is None:
+        if dest is None and self._out is not None:  # the stream already flows (set_output)
+            sink = self._out[2]
+            rc = L.ngpu_pack_finish(p, None, WRITE_FN(), None, ctypes.byref(pc), ctypes.byref(pr),
+                                    ctypes.byref(n), ctypes.byref(st), ctypes.byref(info))
+            sink.reraise()
+            dest = sink.dest
+        elif dest is None:
             rc = L.ngpu_pack_finish(p, None, WRITE_FN(), None, ctypes.byref(pc), ctypes.byref(pr),
                                     ctypes.byref(n), ctypes.byref(st), None)
             sink = None

@@ -158,22 +158,33 @@ class _PackWriteCloser:
     cancel flag, so concurrent Packs on one cached engine never see each
     other's dict (the reference runs one nydus-image per Pack)."""
 
-    def __init__(self, dest: BinaryIO, opt: PackOption):
+    def __init__(self, dest: BinaryIO, opt: PackOption, ociref: bool = False):
         self._dest, self._opt = dest, opt
         if (opt.Compressor or "") not in COMPRESSORS:
             raise ConverterError(f"unsupported compressor {opt.Compressor!r}")
-        self._eng = _engine(opt)
+        # OCIRef: packRef (builder.go:180-218) passes none of the options but
+        # the blob and the source, so nydus-image's defaults apply (v6, 1 MiB
+        # chunks, blake3, no chunk dict)
+        self._eng = _engine(PackOption(Device=opt.Device) if ociref else opt)
         cd = None
-        if opt.ChunkDictPath:
+        if opt.ChunkDictPath and not ociref:
             try:
                 cd = self._eng.dict_open(opt.ChunkDictPath)
             except NgpuError as e:
                 raise ConverterError(f"load chunk dict {opt.ChunkDictPath}: {e}") from e
         try:
-            self._w = self._eng.pack(retain=True, dict=cd)
+            self._w = self._eng.pack(retain=not ociref, dict=cd, ociref=ociref)
         finally:
             if cd is not None:
                 cd.release()  # the pack holds its own reference
+        # `dest` is known now (convert_unix.go:325): the blob stream leaves while
+        # the tar arrives (ngpu_pack_set_output, early emission).
+        # PrefetchPatterns: the builder's stdin, "/" by default (builder.go:125-127, 166)
+        try:
+            self._w.set_output(dest, compressor="" if ociref else (opt.Compressor or ""),
+                               prefetch_patterns="" if ociref else opt.PrefetchPatterns)
+        except NgpuError as e:
+            raise ConverterError(f"pack output: {e}") from e
         self._timer = None
         if opt.Timeout:
             # builder.go:153-158: exec.CommandContext(ctx with Timeout) kills the
@@ -207,9 +218,7 @@ class _PackWriteCloser:
 
     def close(self):
         try:
-            # PrefetchPatterns: the builder's stdin, "/" by default (builder.go:125-127, 166)
-            ch, res, st, info = self._w.finish(self._dest, compressor=self._opt.Compressor or "",
-                                               prefetch_patterns=self._opt.PrefetchPatterns)
+            ch, res, st, info = self._w.finish(None)  # the rest of the stream (set_output)
         except NgpuError as e:
             raise self._killed(e) from e
         finally:
@@ -271,11 +280,13 @@ def Pack(dest: BinaryIO, opt: PackOption) -> _PackWriteCloser:
     if opt.OCIRef:
         if fs != "6":
             raise ConverterError("oci ref can only be supported by fs version 6")
-        # packRef (builder.go:180-218): `nydus-image create --type targz-ref`
-        # leaves the chunks in the original gzip layer, addressed through a zran
-        # (gzip random access) index in blob.meta -- not written by this builder
-        raise ConverterError("OCIRef (--type targz-ref) needs a zran gzip index of the original "
-                             "layer in blob.meta; the GPU builder packs tar-rafs only")
+        # packRef (builder.go:180-218): `nydus-image create --type targz-ref`.
+        # The writer takes the ORIGINAL gzip layer (LayerConvertFunc passes it
+        # undecompressed, convert_unix.go:857-859): inflated and indexed on the
+        # host (gzip checkpoints), digested and deduped on the GPU; the stream
+        # holds blob.meta (chunk infos + checkpoints), image.boot and the TOC,
+        # and the bootstrap's own blob is the gzip blob.
+        return _PackWriteCloser(dest, opt, ociref=True)
     if FeatureBatchSize in detected and fs != "6":
         raise ConverterError("'--batch-size' can only be supported by fs version 6")
     # v2.3.0 would write batch chunks (small chunks compressed as one, another
@@ -322,7 +333,9 @@ def Merge(layers: Sequence[Layer], dest: BinaryIO, opt: MergeOption) -> List[str
         except ConverterError as e:
             raise ConverterError(f"unpack all bootstraps: unpack nydus tar: {e}") from e
         boots.append(b.getvalue())
-        digests.append(layer.Digest.split(":", 1)[-1])
+        # an OCIRef layer's blob is its original gzip blob, named by its
+        # OriginalDigest (getBootstrapPath, convert_unix.go:567-573)
+        digests.append((layer.OriginalDigest or layer.Digest).split(":", 1)[-1])
     dict_boot = parent = None
     if opt.ChunkDictPath:
         with open(opt.ChunkDictPath, "rb") as f:

@@ -8,6 +8,7 @@
 // usage: converter_test DICT.tar LOWER.tar UPPER.tar WORKDIR [COMPRESSOR [UPPER_GO.tar]]
 // Prints "digest <name> sha256:<hex>" lines and "PASS"; exit 1 on failure.
 #include <openssl/evp.h>
+#include <zlib.h>
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -47,6 +48,22 @@ static void write_file(const std::string &p, const std::vector<uint8_t> &v) {
 }
 
 // digest.Canonical.Digester() over the Pack output
+// gzip.NewWriter (compress/gzip, default level), as TestPackRef compresses
+// the lower tar
+static std::vector<uint8_t> gzip_bytes(const std::vector<uint8_t> &in) {
+  z_stream zs{};
+  deflateInit2(&zs, Z_DEFAULT_COMPRESSION, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY);
+  std::vector<uint8_t> out(deflateBound(&zs, in.size()) + 64);
+  zs.next_in = const_cast<Bytef *>(in.data());
+  zs.avail_in = (uInt)in.size();
+  zs.next_out = out.data();
+  zs.avail_out = (uInt)out.size();
+  deflate(&zs, Z_FINISH);
+  out.resize(zs.total_out);
+  deflateEnd(&zs);
+  return out;
+}
+
 static std::string sha256_digest(const std::vector<uint8_t> &v) {
   uint8_t d[32];
   unsigned int l = 32;
@@ -184,14 +201,49 @@ int main(int argc, char **argv) {
   BufferWriter sink;
   REQUIRE(Pack(sink, bad, &w).code == -1 && !w, "invalid chunk size is an error");
 
-  // OCIRef: the reference's own fs-version error, else an accurate refusal
-  PackOption ref;
-  ref.OCIRef = true;
-  Error re = Pack(sink, ref, &w);
-  REQUIRE(re.code == -5 && re.msg.find("targz-ref") != std::string::npos && !w, "OCIRef: %s",
-          re.msg.c_str());
-  ref.FsVersion = "5";
-  re = Pack(sink, ref, &w);
+  // TestPackRef (converter_test.go:530-605): Pack(OCIRef) of the gzipped lower
+  // tar -> a stream whose TOC finds image.boot and blob.meta with their
+  // uncompressed digests; Merge(OCIRef) of that layer with OriginalDigest =
+  // the gzip digest returns [gzip digest]
+  {
+    const std::vector<uint8_t> gz = gzip_bytes(lowerTar);
+    const std::string gzDigest = sha256_digest(gz);
+    PackOption ref;
+    ref.OCIRef = true;
+    BufferWriter refOut;
+    std::unique_ptr<PackWriteCloser> rw;
+    REQUIRE_NOERR(Pack(refOut, ref, &rw));
+    for (size_t a = 0; a < gz.size(); a += 70000)
+      REQUIRE_NOERR(rw->Write(gz.data() + a, std::min<size_t>(70000, gz.size() - a)));
+    REQUIRE_NOERR(rw->Close());
+    BytesReaderAt refRa(refOut.data.data(), refOut.data.size());
+    BufferWriter boot, meta;
+    TOCEntry bootToc, metaToc;
+    REQUIRE_NOERR(UnpackEntry(refRa, EntryBootstrap, boot, &bootToc));
+    REQUIRE_NOERR(UnpackEntry(refRa, EntryBlobMeta, meta, &metaToc));
+    REQUIRE(bootToc.GetUncompressedDigest() == sha256_digest(boot.data).substr(7),
+            "OCIRef: bootstrap TOC digest");
+    REQUIRE(metaToc.GetUncompressedDigest() == sha256_digest(meta.data).substr(7),
+            "OCIRef: blob.meta TOC digest");
+    BufferWriter none;
+    REQUIRE(IsNotFound(UnpackEntry(refRa, EntryBlob, none, nullptr)),
+            "OCIRef: no image.blob (the data stays in the gzip blob)");
+    std::vector<Layer> refLayers{{sha256_digest(refOut.data),
+                                  std::make_shared<BytesReaderAt>(refOut.data.data(),
+                                                                  refOut.data.size()),
+                                  gzDigest}};
+    BufferWriter merged;
+    std::vector<std::string> refBlobs;
+    MergeOption mo;
+    mo.OCIRef = true;
+    REQUIRE_NOERR(Merge(refLayers, merged, mo, &refBlobs));
+    REQUIRE(refBlobs.size() == 1 && refBlobs[0] == gzDigest, "OCIRef Merge blobs: %s",
+            refBlobs.empty() ? "-" : refBlobs[0].c_str());
+  }
+  PackOption ref5;
+  ref5.OCIRef = true;
+  ref5.FsVersion = "5";
+  Error re = Pack(sink, ref5, &w);
   REQUIRE(re.msg == "oci ref can only be supported by fs version 6", "OCIRef v5: %s", re.msg.c_str());
 
   // BatchSize / Encrypt: the pinned v2.3.0 builder honours both
