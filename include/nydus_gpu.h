@@ -589,8 +589,9 @@ int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
 #define NGPU_PACK_OCIREF 0x2u
 /* The reader side of an OCIRef layer (host; what nydusd does with a targz-ref
  * blob): chunk `index` of the layer's own blob, located through `blob_meta`
- * (the layer stream's blob.meta entry: chunk-info array, checkpoint table,
- * dictionaries, header) and inflated out of the original gzip blob `gz` from
+ * (the layer stream's blob.meta tar entry: chunk-info array, checkpoint table,
+ * dictionaries, then the 4 KiB header -- through the TOC, the "blob.meta"
+ * entry followed by "blob.meta.header") and inflated out of the original gzip blob `gz` from
  * its checkpoint.  *len_out = the chunk's size (<= cap).  (ABI 4) */
 int ngpu_ref_chunk_read(const void *gz, uint64_t gz_len, const void *blob_meta, uint64_t meta_len,
                         uint32_t index, void *out, uint32_t cap, uint32_t *len_out);

@@ -580,6 +580,17 @@ __device__ __forceinline__ uint32_t group_work(uint32_t len, uint32_t j) {
 #ifndef B3_WAVES_PER_EU
 #define B3_WAVES_PER_EU 0
 #endif
+
+// In-window tree levels by lane quads (defined with compress_quad below).
+#ifndef B3_WG_QUAD
+#define B3_WG_QUAD 1
+#endif
+#if B3_WG_QUAD
+__device__ __forceinline__ void wg_tree_quad(uint32_t *b0, uint32_t *b1, uint32_t *nit, bool inwg,
+                                             uint32_t k, uint32_t j, uint32_t o, uint32_t c,
+                                             const uint32_t cur[8], uint32_t slot,
+                                             ngpu_result *__restrict__ out);
+#endif
 #if B3_WAVES_PER_EU
 #define B3_OCC __attribute__((amdgpu_waves_per_eu(B3_WAVES_PER_EU)))
 #else
@@ -596,6 +607,9 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
     const uint32_t *__restrict__ small, const uint64_t *__restrict__ nsmall,
     uint32_t *__restrict__ tree_list) {
   __shared__ uint32_t lcv[256 * 8];
+#if B3_WG_QUAD
+  __shared__ uint32_t lcv2[256 * 8];  // ping-pong partner of lcv
+#endif
   // groups [0, gm): multi-group chunks in chunk order; [gm, gm + ns): the
   // single-group chunks, largest first
   const uint64_t gm = gbase[n];
@@ -689,9 +703,16 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
     d[0] = make_uint4(cur[0], cur[1], cur[2], cur[3]);
     d[1] = make_uint4(cur[4], cur[5], cur[6], cur[7]);
   }
+#if B3_WG_QUAD
+  __shared__ uint32_t nit[2];
+  if (threadIdx.x == 0) nit[0] = nit[1] = 0;
+#endif
   if (!__syncthreads_or(inwg)) return;
   const uint32_t o = (uint32_t)(base - g0);  // chunk's first slot in lcv
   uint32_t k = inwg ? (uint32_t)ng : 1;
+#if B3_WG_QUAD
+  wg_tree_quad(lcv, lcv2, nit, inwg, k, j, o, c, cur, slot, out);
+#else
   if (inwg) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) lcv[8 * slot + i] = cur[i];
@@ -727,6 +748,7 @@ __global__ __launch_bounds__(256) B3_OCC void b3_groups(
     }
     k = active ? p + (k & 1) : 1;
   }
+#endif
 }
 
 // Upper levels: one workgroup per chunk with more than one leaf group.
@@ -818,6 +840,81 @@ constexpr QuadSched make_quad_sched() {
   return t;
 }
 constexpr QuadSched kQuadSched = make_quad_sched();
+
+#if B3_WG_QUAD
+// The upper levels of the chunks whose groups all sit in one b3_groups
+// workgroup.  Each level lists its parents in LDS (source pair, destination
+// slot, ROOT, chunk) and the workgroup's 64 quads take them one per quad
+// (compress_quad: ~190 VALU per lane), reading one CV buffer and writing the
+// other, so a level costs one barrier after its list and one after its
+// compressions.  One compression per lane instead ran a 680-op compression in
+// every wave holding a parent, however few: on C2 (two 1 MiB chunks of 128
+// groups per workgroup) 14 wave-compressions for 3.97 of parent work, about
+// 2.7 % of the kernel's issued VALU.  The chunk's own lanes (slot o + j,
+// group j of k) list the level's parents and promote an odd tail.
+__device__ __forceinline__ void wg_tree_quad(uint32_t *b0, uint32_t *b1, uint32_t *nit, bool inwg,
+                                             uint32_t k, uint32_t j, uint32_t o, uint32_t c,
+                                             const uint32_t cur[8], uint32_t slot,
+                                             ngpu_result *__restrict__ out) {
+  __shared__ uint32_t item[128], item_c[128];  // <= 128 parents per level (256 slots)
+  const uint32_t q = threadIdx.x & 3, quad = threadIdx.x >> 2;
+  if (inwg) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b0[8 * slot + i] = cur[i];
+  }
+  uint32_t *src = b0, *dst = b1;
+  for (uint32_t lv = 0;; ++lv) {
+    const bool active = k > 1;
+    const uint32_t p = k >> 1;
+    if (active && j < p) {
+      const uint32_t at = atomicAdd(&nit[lv & 1], 1u);
+      item[at] = (o + 2 * j) | ((o + j) << 8) | (k == 2 ? 1u << 16 : 0u);
+      item_c[at] = c;
+    }
+    if (active && (k & 1) && j == p) {  // odd tail promoted
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dst[8 * (o + p) + i] = src[8 * (o + k - 1) + i];
+    }
+    if (!__syncthreads_or(active)) break;
+    const uint32_t ni = nit[lv & 1];
+    // the other counter was last read before the previous level's final barrier
+    if (threadIdx.x == 0) nit[(lv & 1) ^ 1] = 0;
+    for (uint32_t it = quad; it < ni; it += 64) {
+      uint32_t wo[28];
+#pragma unroll
+      for (int r = 0; r < 7; ++r)
+#pragma unroll
+        for (int sl = 0; sl < 4; ++sl) wo[4 * r + sl] = (kQuadSched.w[r][sl] >> (4 * q)) & 15u;
+      const uint32_t w = item[it];
+      const uint32_t *t = src + 8 * (w & 255u);
+      uint32_t m[28];
+#pragma unroll
+      for (int k2 = 0; k2 < 28; ++k2) m[k2] = t[wo[k2]];
+      const bool root = (w >> 16) & 1u;
+      const uint32_t ivq = q == 0 ? IV0 : q == 1 ? IV1 : q == 2 ? IV2 : IV3;
+      const uint32_t ivh = q == 0 ? IV4 : q == 1 ? IV5 : q == 2 ? IV6 : IV7;
+      const uint32_t dq = q == 2 ? 64u : q == 3 ? (PARENT | (root ? ROOT : 0u)) : 0u;
+      uint32_t x = ivq, y = ivh;
+      compress_quad(x, y, m, ivq, dq);
+      const uint32_t d = (w >> 8) & 255u;
+      dst[8 * d + q] = x;
+      dst[8 * d + 4 + q] = y;
+      if (root) {
+        const uint32_t cc = item_c[it];
+        uint32_t *dg = reinterpret_cast<uint32_t *>(out[cc].digest);
+        dg[q] = x;
+        dg[4 + q] = y;
+        if (q == 0) out[cc].kind = NGPU_DIGESTED;
+      }
+    }
+    __syncthreads();
+    uint32_t *tmp = src;
+    src = dst;
+    dst = tmp;
+    k = active ? p + (k & 1) : 1;
+  }
+}
+#endif
 
 // The lane's 16 bytes of a block: valid (0..16) bytes, zero padded; byte
 // loads when partial or unaligned (never past the chunk).

@@ -12,6 +12,6 @@ while [ $# -ge 2 ]; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc $FLAGS \
     -c csrc/blake3.hip -o build/ab/blake3_$NAME.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/ab/$NAME.so \
-    build/ab/blake3_$NAME.o $OTHER -lcrypto -ldl -lpthread
+    build/ab/blake3_$NAME.o $OTHER -lcrypto -lz -ldl -lpthread
   echo "built build/ab/$NAME.so ($FLAGS)"
 done

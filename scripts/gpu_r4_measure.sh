@@ -7,7 +7,7 @@
 set -u
 TAG=${1:-r4m}
 shift || true
-STEPS=${*:-clock insts stats sha node n2}
+STEPS=${*:-clock insts insts0 stats early sha node n2}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -24,6 +24,10 @@ for s in $STEPS; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-include-regex "$K" --output-format csv -d "$OUT/ins" -o pmc -- python3 "$ROOT/bench.py" --steps 20 --warmup 10 --no-cpu-baseline --no-e2e --no-sub > "$OUT/ins.log" 2>&1)
       ok $? insts
       python3 "$ROOT/scripts/pmc_summary.py" "$OUT/pmc_insts_c2.json" "$K" "$OUT/ins" ;;
+    insts0)  # the same pass on the A/B build without the quad in-window tree
+      (cd /tmp && NYDUS_GPU_LIB="$ROOT/nydus-snapshotter_amd/build/ab/wgq0.so" timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-include-regex "$K" --output-format csv -d "$OUT/ins0" -o pmc -- python3 "$ROOT/bench.py" --steps 20 --warmup 10 --no-cpu-baseline --no-e2e --no-sub > "$OUT/ins0.log" 2>&1)
+      ok $? insts0
+      python3 "$ROOT/scripts/pmc_summary.py" "$OUT/pmc_insts_c2_wgq0.json" "$K" "$OUT/ins0" ;;
     stats)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c2 -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-sub > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err")
       ok $? stats ;;
@@ -35,6 +39,10 @@ for s in $STEPS; do
       (cd "$ROOT" && timeout -k 10 400 python3 bench.py --node 0,0,0,0,0,0,0,0 --workload c4-16 --steps 10 --warmup 10 > "$OUT/node_w8.json" 2> "$OUT/node_w8.err")
       ok $? node
       python3 -c "import json; d=json.load(open('$OUT/node_w8.json')); print(json.dumps(d['exchange']))" ;;
+    early)
+      (cd "$ROOT" && timeout -k 10 300 python3 tools/e2e_early.py 3 32 > "$OUT/e2e_early.json" 2> "$OUT/e2e_early.err")
+      ok $? early
+      cat "$OUT/e2e_early.json" ;;
     n2)
       (cd "$ROOT" && C4L=4 bash scripts/gpu_n2_gloo.sh "$TAG" > "$OUT/n2.log" 2>&1)
       ok $? n2

@@ -60,9 +60,15 @@ def _check_layer(oracle, tar, gz, stream, S=0x100000):
     import blob_ref
     boot, e_boot = blob_ref.unpack_entry(stream, blob_ref.ENTRY_BOOTSTRAP)
     meta, e_meta = blob_ref.unpack_entry(stream, "blob.meta")
-    assert e_boot is not None and e_meta is not None  # found through the TOC
+    header, e_hdr = blob_ref.unpack_entry(stream, "blob.meta.header")
+    assert e_boot is not None and e_meta is not None and e_hdr is not None  # found through the TOC
     assert e_boot["uncompressed_digest"] == hashlib.sha256(boot).hexdigest()
     assert e_meta["uncompressed_digest"] == hashlib.sha256(meta).hexdigest()
+    assert len(header) == 4096
+    # the tar entry "blob.meta" is the (uncompressed) array + tables, then the header
+    off, size = blob_ref.seek_file_by_tar_header(stream, "blob.meta")
+    assert stream[off:off + size] == meta + header
+    meta = meta + header
     with pytest.raises(blob_ref.NotFound):  # no image.blob: the data stays in the gzip blob
         blob_ref.unpack_entry(stream, blob_ref.ENTRY_BLOB)
     dump = nydus_gpu.rafs_dump(boot)
