@@ -22,11 +22,11 @@ timeout -s KILL 120 rocprofv3 --pmc $S2 --output-format csv -d "$OUT/cal2" -o pm
 ok $? cal2
 fi
 K='b3_groups|b3_quad_leaves|b3_quad_planned|sha256_split|sha256_pair|sha256_lane'
-timeout -k 10 300 rocprofv3 --pmc $S1 --kernel-include-regex "$K" --output-format csv -d "$OUT/k1" -o pmc -- python3 "$ROOT/bench.py" --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > "$OUT/k1.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc $S1 --kernel-include-regex "$K" --output-format csv -d "$OUT/k1" -o pmc -- python3 "$ROOT/bench.py" --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-sub > "$OUT/k1.log" 2>&1
 ok $? k1
-timeout -k 10 300 rocprofv3 --pmc $S2 --kernel-include-regex "$K" --output-format csv -d "$OUT/k2" -o pmc -- python3 "$ROOT/bench.py" --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > "$OUT/k2.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc $S2 --kernel-include-regex "$K" --output-format csv -d "$OUT/k2" -o pmc -- python3 "$ROOT/bench.py" --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-sub > "$OUT/k2.log" 2>&1
 ok $? k2
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" --output-format csv -d "$OUT/k3" -o pmc -- python3 "$ROOT/bench.py" --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > "$OUT/k3.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" --output-format csv -d "$OUT/k3" -o pmc -- python3 "$ROOT/bench.py" --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-sub > "$OUT/k3.log" 2>&1
 ok $? k3
 if [ "$CAL" = 1 ]; then
 for k in coalesced 'lane_stream<0>' 'lane_stream<680>'; do

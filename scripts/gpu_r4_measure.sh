@@ -28,6 +28,10 @@ for s in $STEPS; do
       (cd /tmp && NYDUS_GPU_LIB="$ROOT/nydus-snapshotter_amd/build/ab/wgq0.so" timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-include-regex "$K" --output-format csv -d "$OUT/ins0" -o pmc -- python3 "$ROOT/bench.py" --steps 20 --warmup 10 --no-cpu-baseline --no-e2e --no-sub > "$OUT/ins0.log" 2>&1)
       ok $? insts0
       python3 "$ROOT/scripts/pmc_summary.py" "$OUT/pmc_insts_c2_wgq0.json" "$K" "$OUT/ins0" ;;
+    req)  # request-size traffic of the dominant kernel (roofline.traffic)
+      CAL=0 bash "$ROOT/scripts/gpu_pmc_req.sh" "$TAG/req" c2 > "$OUT/req.log" 2>&1
+      ok $? req
+      cp "$OUT/req/pmc_req_c2.json" "$OUT/pmc_req_c2.json" ;;
     stats)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c2 -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-sub > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err")
       ok $? stats ;;
