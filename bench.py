@@ -550,7 +550,7 @@ def newest_profile(name):
     return json.load(open(cands[-1])), os.path.relpath(cands[-1], ROOT)
 
 
-def mix_roofline(roof, achieved, kernel, workload):
+def mix_roofline(roof, achieved, kernel, workload, comp=0):
     """the ceiling of the kernel's own instruction mix and
     the clock the chip holds under it.  peak_mix = 1024 SIMDs x 64 lanes x
     2.4 GHz / (issue cycles per algorithmic op of the compiled hot loop:
@@ -577,6 +577,27 @@ def mix_roofline(roof, achieved, kernel, workload):
         roof["held_clock_source"] = csrc
         if mix:
             roof["frac_mix_at_held_clock"] = round(achieved / (pm * clk["clock_ghz"] / 2.4), 4)
+    # where the rest goes: issued VALU wave-instructions
+    # (PMC SQ_INSTS_VALU of the same command, scripts/gpu_r4_measure.sh insts)
+    # over the algorithmic ones (comp x 680 / 64 lanes); frac_mix factors into
+    # clock (held / 2.4) x algorithmic / issued x the issue efficiency left
+    # (the mixed 2- / 4-cycle stream against the linear cycle model)
+    ins, isrc = newest_profile(f"pmc_insts_{workload}.json")
+    if (ins and comp and "SQ_INSTS_VALU" in ins.get("counters", {})
+            and (ins.get("kernel") or "").startswith(kernel.split("<")[0])):
+        alg_wi = comp * OPS_PER_COMPRESSION / 64
+        issued = ins["counters"]["SQ_INSTS_VALU"]
+        d = {"valu_wave_instructions_issued": int(issued),
+             "valu_wave_instructions_algorithmic": int(alg_wi),
+             "issued_over_algorithmic": round(issued / alg_wi, 4), "source": isrc}
+        if mix and clk and clk.get("clock_ghz"):
+            cf = clk["clock_ghz"] / 2.4
+            d["clock_factor"] = round(cf, 4)
+            d["issue_efficiency_left"] = round(roof["frac_mix"] / cf / (alg_wi / issued), 4)
+            d["note"] = ("frac_mix = clock_factor x (algorithmic / issued) x issue_efficiency_left; "
+                         "the held clock is a profiled pass's (guide: profiled passes run up to "
+                         "~5 % below an unprofiled run's clock)")
+        roof["frac_mix_breakdown"] = d
 
 
 def tar_host_path(nydus_gpu, tar, wl, device, file_bytes, reps=200):
@@ -1503,7 +1524,8 @@ def main():
         e2e = tar_host_path(nydus_gpu, tar, wl, local, file_bytes)
 
     roof["traffic"], roof["traffic_source"] = pmc_traffic(args.pmc_json, args.workload, roof["kernel"])
-    mix_roofline(roof, achieved, roof["kernel"], args.workload)
+    mix_roofline(roof, achieved, roof["kernel"], args.workload,
+                 comp if wl["digester"] == "blake3" else 0)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

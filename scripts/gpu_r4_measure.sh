@@ -32,6 +32,15 @@ for s in $STEPS; do
       CAL=0 bash "$ROOT/scripts/gpu_pmc_req.sh" "$TAG/req" c2 > "$OUT/req.log" 2>&1
       ok $? req
       cp "$OUT/req/pmc_req_c2.json" "$OUT/pmc_req_c2.json" ;;
+    ceiling)  # the compression stream alone (tools/b3_ceiling.hip), then its clock at 4 and 8 waves/SIMD
+      timeout -k 10 120 "$ROOT/tools/b3_ceiling" 1 2 3 4 5 6 8 > "$OUT/b3_ceiling.jsonl" 2> "$OUT/b3_ceiling.err"
+      ok $? ceiling
+      cat "$OUT/b3_ceiling.jsonl"
+      for w in 4 8; do
+        (cd /tmp && timeout -k 10 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/ceil_clk$w" -o pmc -- "$ROOT/tools/b3_ceiling" $w > "$OUT/ceil_clk$w.log" 2>&1)
+        ok $? ceiling-clock-$w
+        python3 "$ROOT/scripts/pmc_summary.py" "$OUT/pmc_clock_b3_ceiling_w$w.json" 'b3_ceiling' "$OUT/ceil_clk$w"
+      done ;;
     stats)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c2 -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-sub > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err")
       ok $? stats ;;
