@@ -598,6 +598,27 @@ def mix_roofline(roof, achieved, kernel, workload, comp=0):
                          "the held clock is a profiled pass's (guide: profiled passes run up to "
                          "~5 % below an unprofiled run's clock)")
         roof["frac_mix_breakdown"] = d
+    # the measured ceiling of the same compression stream with no memory
+    # traffic (tools/b3_ceiling.hip at the kernel's occupancy, clock from its
+    # own PMC pass): frac_ceiling = achieved / that rate; per-clock = the same
+    # ratio with each side divided by the clock it held
+    ceil_, ceil_src = newest_profile("b3_ceiling.json")
+    if ceil_:
+        w = str(ceil_["kernel_occupancy_waves_per_simd"])
+        ct = ceil_["ceiling_tops_at_kernel_occupancy"] * 1e12
+        roof["ceiling_measured"] = {"tops": round(ct / 1e12, 3), "waves_per_simd": int(w),
+                                    "clock_ghz": ceil_["held_clock_ghz"].get(w), "source": ceil_src}
+        roof["frac_ceiling"] = round(achieved / ct, 4)
+        # per cycle: the kernel's algorithmic ops over its GRBM_GUI_ACTIVE / 8
+        # cycles per launch (the clock pass; the cycle count, unlike the clock,
+        # does not depend on the profiler slowing the launch down) against the
+        # ceiling's ops per cycle
+        cyc = (clk or {}).get("counters", {}).get("GRBM_GUI_ACTIVE")
+        if comp and cyc and ceil_["held_clock_ghz"].get(w):
+            k_opc = comp * OPS_PER_COMPRESSION / (cyc / 8)
+            c_opc = ct / (ceil_["held_clock_ghz"][w] * 1e9)
+            roof["ops_per_cycle"] = {"kernel": round(k_opc), "ceiling": round(c_opc)}
+            roof["frac_ceiling_per_cycle"] = round(k_opc / c_opc, 4)
 
 
 def tar_host_path(nydus_gpu, tar, wl, device, file_bytes, reps=200):

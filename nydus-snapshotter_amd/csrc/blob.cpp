@@ -44,6 +44,7 @@
 #include <mutex>
 #include <set>
 #include <unordered_map>
+#include <chrono>
 #include <thread>
 
 #include "blob.hpp"
@@ -514,10 +515,18 @@ struct BlobWriter::Impl {
     written += n;
     return 0;
   }
+  // NGPU_SINK_STATS=1: the sink's time split, printed to stderr when the
+  // writer goes (diagnostic of the stream's single-thread bound)
+  double t_wait = 0, t_sha = 0, t_emit = 0;
+  uint64_t n_batches = 0;
   void sink_loop() {
+    using clk = std::chrono::steady_clock;
     std::unique_lock<std::mutex> g(qm);
     for (;;) {
+      const auto t0 = clk::now();
       qcv.wait(g, [&] { return stop || !q.empty(); });
+      const auto t1 = clk::now();
+      if (n_batches) t_wait += std::chrono::duration<double>(t1 - t0).count();
       if (q.empty()) return;
       std::vector<uint8_t> b = std::move(q.front());
       q.pop_front();
@@ -527,8 +536,12 @@ struct BlobWriter::Impl {
       int r = 0;
       if (!failed) {
         blob_sha.update(b.data(), b.size());
+        const auto t2 = clk::now();
         r = emit(b.data(), b.size());
+        t_sha += std::chrono::duration<double>(t2 - t1).count();
+        t_emit += std::chrono::duration<double>(clk::now() - t2).count();
       }
+      ++n_batches;
       g.lock();
       if (r && !sink_rc) {
         sink_rc = r;
@@ -567,6 +580,11 @@ struct BlobWriter::Impl {
     }
     qcv.notify_all();
     if (sink.joinable()) sink.join();
+    const char *v = getenv("NGPU_SINK_STATS");
+    if (v && *v == '1')
+      fprintf(stderr, "{\"sink_batches\": %llu, \"sink_wait_s\": %.4f, \"sink_sha_s\": %.4f, "
+              "\"sink_emit_s\": %.4f, \"bytes\": %llu}\n", (unsigned long long)n_batches, t_wait,
+              t_sha, t_emit, (unsigned long long)written);
   }
 };
 

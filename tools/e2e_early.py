@@ -6,7 +6,9 @@ host memory, packed to /dev/null three ways, alternated:
   finish  -- retain + finish(dest) after the last write (no early emission);
   early   -- retain + set_output(dest) before the first write, finish(None).
 Per run: seconds to the end of the writes and to the end of the call.
-usage: tools/e2e_early.py [ROUNDS] [WRITE_MIB] [FILES]  -> one JSON line"""
+usage: tools/e2e_early.py [ROUNDS] [WRITE_MIB] [FILES] [THREADS,...]  -> one JSON line
+THREADS: BlobWriter pool sizes for the early mode (0 = the default min(16, CPUs));
+each gets its own mode "early_t<N>"."""
 import ctypes
 import hashlib
 import json
@@ -25,6 +27,7 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     piece = (int(sys.argv[2]) if len(sys.argv) > 2 else 32) << 20
     n_files = int(sys.argv[3]) if len(sys.argv) > 3 else 512
+    threads = [int(x) for x in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0]
     import torch
     import nydus_gpu
     import bench
@@ -46,20 +49,23 @@ def main():
                 hashlib.sha256(memoryview(host)).digest()
                 return {"mode": mode, "total_s": time.perf_counter() - t0}
             w = eng.pack(retain=True)
-            if mode == "early":
-                w.set_output(nydus_gpu.FdWriter(fd), compressor="none")
+            early = mode.startswith("early")
+            if early:
+                t = int(mode[7:]) if mode.startswith("early_t") else 0
+                w.set_output(nydus_gpu.FdWriter(fd), compressor="none", threads=t)
             for a in range(0, nbytes, piece):
                 w.write(host[a:a + piece])
             tw = time.perf_counter() - t0
-            if mode == "early":
+            if early:
                 info = w.finish(None)[3]
             else:
                 info = w.finish(nydus_gpu.FdWriter(fd), compressor="none")[3]
             return {"mode": mode, "writes_s": tw, "total_s": time.perf_counter() - t0,
                     "stream": info["stream_digest"]}
         run("early")  # warm
+        modes = ["sha", "finish"] + (["early"] if threads == [0] else [f"early_t{t}" for t in threads])
         for _ in range(rounds):
-            for m in ("sha", "finish", "early"):
+            for m in modes:
                 res["runs"].append(run(m))
     finally:
         os.close(fd)
@@ -67,7 +73,7 @@ def main():
         eng.close()
     digs = {r["stream"] for r in res["runs"] if "stream" in r}
     res["streams_equal"] = len(digs) == 1
-    for m in ("sha", "finish", "early"):
+    for m in modes:
         ts = sorted(r["total_s"] for r in res["runs"] if r["mode"] == m)
         res[f"{m}_gbs_med"] = round(nbytes / ts[len(ts) // 2] / 1e9, 3)
     for r in res["runs"]:
