@@ -234,7 +234,7 @@ extern "C" int ngpu_ref_chunk_read(const void *gz, uint64_t gz_len, const void *
     if (magic != 0xB10BB10Bu || !(feat & 0x8) || algo != 0)
       return host_fail(NGPU_EFORMAT, "blob.meta: not an uncompressed zran chunk-info array");
     if (index >= entries || (uint64_t)entries * 24 > body || zt_off > body || zt_size > body - zt_off ||
-        zt_cnt * 40 != zt_size || zd_off > body || zd_size > body - zd_off)
+        zt_size % 40 || zt_cnt != zt_size / 40 || zd_off > body || zd_size > body - zd_off)
       return host_fail(NGPU_EFORMAT, "blob.meta: bad zran table bounds");
     uint64_t w[3];
     memcpy(w, m + 24ull * index, 24);
