@@ -884,7 +884,8 @@ def node_cabi_extra(world, timeout_s=150):
             "dedup_alone_ms_partition_copy": cp.get("dedup_alone_ms"),
             "dict_hits_partition": part["dict_hits"], "dict_hits_replicate": rep["dict_hits"],
             "dict_hits_partition_copy": cp.get("dict_hits"),
-            "hits_equal": part["dict_hits"] == rep["dict_hits"] == cp.get("dict_hits", part["dict_hits"])}
+            "hits_equal": part["dict_hits"] == rep["dict_hits"] == cp.get("dict_hits", part["dict_hits"]),
+            "node_step": d.get("node_step")}
 
 
 def concurrent_bench(args):
@@ -1132,6 +1133,43 @@ def node_bench(args):
                            "dedup_all_requesters_at_once_ms": round(float(np.median(conc[3:])), 4),
                            "dict_hits": hits}
             d.release()
+        # the bulk node step (ngpu_node_process_step, ABI 5): all devices at
+        # once, one all-to-all-v of digests and one of hits per step -- over
+        # RCCL (ncclAllToAllv) when the devices are distinct, and by peer
+        # copies (any node, the one-GPU rehearsal too)
+        step_modes = {}
+        d = node.dict_create(recs, blobs, mode=nydus_gpu.NODE_DICT_PARTITION)
+        parts = [{"d_data": p["buf"].data_ptr(), "len": p["buf"].numel(), "d_chunks": p["d_ch"].data_ptr(),
+                  "n": p["n"], "d_out": p["out"].data_ptr(), "d_layer_first": p["first"].data_ptr(),
+                  "n_layers": L, "d_stats": p["st"].data_ptr(), "stream": p["stream"].cuda_stream}
+                 for p in per]
+        for tname, rccl in (("copy", False), ("rccl", True)):
+            if rccl and len(set(devs)) != W:
+                step_modes[tname] = {"skipped": "RCCL takes one rank per GPU; devices repeat"}
+                continue
+            try:
+                for _ in range(args.warmup):
+                    node.process_step(d, parts, rccl=rccl)
+                sync()
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    node.process_step(d, parts, rccl=rccl)
+                sync()
+                elapsed = time.perf_counter() - t0
+            except nydus_gpu.NgpuError as ex_:
+                step_modes[tname] = {"error": str(ex_)}
+                continue
+            hits = []
+            for p in per:
+                res = p["out"].cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+                hits.append(int((res["kind"] == nydus_gpu.DICT).sum()))
+            total = sum(p["bytes"] for p in per) * args.steps
+            step_modes[tname] = {"ms_per_step": round(elapsed / args.steps * 1e3, 3),
+                                 "value_gbs": round(total / elapsed / 1e9, 1), "dict_hits": hits,
+                                 "hits_equal_partition": hits == modes["partition"]["dict_hits"]}
+        for e in node.engines:
+            e.device_status()
+        d.release()
         ex = float(np.mean(modes["partition"]["dedup_alone_ms"])) - \
             float(np.mean(modes["replicate"]["dedup_alone_ms"]))
         ex_copy = float(np.mean(modes["partition_copy"]["dedup_alone_ms"])) - \
@@ -1160,6 +1198,7 @@ def node_bench(args):
                        "chunks_per_device": per[0]["n"], "dict_entries": m,
                        "parallelism": f"node x{W} (ngpu_node_*, one process)"},
             "modes": modes,
+            "node_step": step_modes,
             "exchange": {"dedup_alone_ms_partition_minus_replicate": round(ex, 4),
                          "all_requesters_at_once_ms_partition_minus_replicate": round(
                              modes["partition"]["dedup_all_requesters_at_once_ms"]

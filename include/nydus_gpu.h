@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define NGPU_ABI_VERSION 4
+#define NGPU_ABI_VERSION 5
 
 /* PackOption.Digester (API extension; maps to nydus-image --digester). */
 enum ngpu_digester { NGPU_DIGEST_BLAKE3 = 0, NGPU_DIGEST_SHA256 = 1 };
@@ -471,6 +471,40 @@ int ngpu_node_process_device(ngpu_node *node, uint32_t i, ngpu_dict *dict, const
                              uint64_t len, const ngpu_chunk *d_chunks, uint64_t n,
                              ngpu_result *d_out, const uint64_t *d_layer_first,
                              uint64_t n_layers, ngpu_layer_stats *d_stats, void *stream);
+
+/* ---- node step: every device at once, one all-to-all each way (ABI 5) ----
+ * The bulk-synchronous form of the exchange, for a caller that converts one
+ * batch of layers per device per step (C4: layers round robin over the
+ * node's GPUs; convert_unix.go:467-538 runs a layer per goroutine): part i
+ * (device-resident layers on node device i, its own stream there; n = 0
+ * takes part with nothing) is digested, its digests are bucketed by owner
+ * (ngpu_route_digests), every part's segments cross the node in ONE
+ * all-to-all-v, each owner probes what it received against its partition,
+ * the hits return in one all-to-all-v the other way, go back to their rows
+ * and each part dedups its own layers.  The per-owner row counts reach the
+ * host once per step (they size the all-to-all).
+ * flags NGPU_NODE_STEP_RCCL: the two all-to-alls are RCCL ncclAllToAllv
+ * calls over a communicator of the node's devices (ncclCommInitAll, created on
+ * the first such step; RCCL takes one rank per GPU, so a node listing a
+ * device twice returns NGPU_EUNSUPP).  Without it the same segments move
+ * by hipMemcpyPeerAsync (any node, also one GPU listed several times).
+ * dict: a partitioned node dict (replicated or NULL: no exchange, each part
+ * is processed on its own).  Returns once everything is enqueued; each
+ * part's results are ready when its stream is. */
+typedef struct {
+  const void *d_data;             /* part's layer bytes on its device */
+  uint64_t len;
+  const ngpu_chunk *d_chunks;     /* n descriptors (device) */
+  uint64_t n;
+  ngpu_result *d_out;             /* n results (device) */
+  const uint64_t *d_layer_first;  /* n_layers + 1 (device), or NULL: one layer */
+  uint64_t n_layers;
+  ngpu_layer_stats *d_stats;      /* device, n_layers, or NULL */
+  void *stream;                   /* on the part's device (NULL: its null stream) */
+} ngpu_node_part;
+#define NGPU_NODE_STEP_RCCL 1u
+int ngpu_node_process_step(ngpu_node *node, ngpu_dict *dict, const ngpu_node_part *parts,
+                           uint32_t n_parts, uint32_t flags);
 
 /* ---- RAFS v6 chunk table ---------------------------- */
 /* Serialise the layer's unique chunk records (NEW chunks in index order) as

@@ -258,6 +258,7 @@ class Pool {
   explicit Pool(unsigned n) {
     for (unsigned i = 0; i + 1 < n; ++i) th_.emplace_back([this] { loop(); });
   }
+  unsigned size() const { return (unsigned)th_.size() + 1; }
   ~Pool() {
     {
       std::lock_guard<std::mutex> g(m_);
@@ -309,6 +310,70 @@ class Pool {
   bool stop_ = false;
   std::mutex m_;
   std::condition_variable cv_, done_;
+};
+
+// A batch buffer of the blob stream, grown by new[] -- no zero fill (a 64 MiB
+// std::vector resize is ~10 ms of memset on a writer's first batches; every
+// byte is written before the sink reads it).
+struct Batch {
+  std::unique_ptr<uint8_t[]> p;
+  uint64_t cap = 0, n = 0;
+  void resize(uint64_t k) {
+    if (k > cap) {
+      p.reset(new uint8_t[k]);
+      cap = k;
+    }
+    n = k;
+  }
+  uint8_t *data() { return p.get(); }
+  uint64_t size() const { return n; }
+  uint8_t &operator[](uint64_t i) { return p[i]; }
+};
+
+// A writer lives for one Pack; its compression pool and batch buffers stay
+// for the next writer (joining a 16-thread pool and unmapping three 64 MiB
+// buffers were ~20 ms of every early-emission Pack's close, and the next
+// writer's first batches paid the page faults again).  Process-wide, never
+// destroyed (no exit-time teardown of idle threads).
+struct WriterCache {
+  static constexpr size_t kPools = 8, kBufs = 8;
+  static constexpr uint64_t kBufMax = 64ull << 20;
+  std::mutex m;
+  std::vector<std::unique_ptr<Pool>> pools;
+  std::vector<Batch> bufs;
+  static WriterCache &get() {
+    static WriterCache *c = new WriterCache;
+    return *c;
+  }
+  std::unique_ptr<Pool> take_pool(unsigned n) {
+    {
+      std::lock_guard<std::mutex> g(m);
+      for (size_t i = 0; i < pools.size(); ++i)
+        if (pools[i]->size() == n) {
+          std::unique_ptr<Pool> p = std::move(pools[i]);
+          pools.erase(pools.begin() + (long)i);
+          return p;
+        }
+    }
+    return std::unique_ptr<Pool>(new Pool(n));
+  }
+  void put_pool(std::unique_ptr<Pool> p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(m);
+    if (pools.size() < kPools) pools.push_back(std::move(p));
+  }
+  bool take_buf(Batch *b) {
+    std::lock_guard<std::mutex> g(m);
+    if (bufs.empty()) return false;
+    *b = std::move(bufs.back());
+    bufs.pop_back();
+    return true;
+  }
+  void put_buf(Batch &&b) {
+    if (!b.p || b.cap > kBufMax) return;
+    std::lock_guard<std::mutex> g(m);
+    if (bufs.size() < kBufs) bufs.push_back(std::move(b));
+  }
 };
 
 }  // namespace
@@ -501,10 +566,11 @@ struct BlobWriter::Impl {
   // sequential hash overlaps the next batch's compression / copy and the
   // GPU gather of the next window (at most kDepth batches in flight).
   static constexpr size_t kDepth = 2;
+
   std::thread sink;
   std::mutex qm;
   std::condition_variable qcv;
-  std::deque<std::vector<uint8_t>> q, free_bufs;
+  std::deque<Batch> q, free_bufs;
   bool busy = false, stop = false;
   int sink_rc = 0;
   std::string sink_err;
@@ -517,8 +583,9 @@ struct BlobWriter::Impl {
   }
   // NGPU_SINK_STATS=1: the sink's time split, printed to stderr when the
   // writer goes (diagnostic of the stream's single-thread bound)
-  double t_wait = 0, t_sha = 0, t_emit = 0;
+  double t_wait = 0, t_sha = 0, t_emit = 0, t_first = -1, t_last = 0;
   uint64_t n_batches = 0;
+  const std::chrono::steady_clock::time_point t_born = std::chrono::steady_clock::now();
   void sink_loop() {
     using clk = std::chrono::steady_clock;
     std::unique_lock<std::mutex> g(qm);
@@ -527,8 +594,9 @@ struct BlobWriter::Impl {
       qcv.wait(g, [&] { return stop || !q.empty(); });
       const auto t1 = clk::now();
       if (n_batches) t_wait += std::chrono::duration<double>(t1 - t0).count();
+      else t_first = std::chrono::duration<double>(t1 - t_born).count();
       if (q.empty()) return;
-      std::vector<uint8_t> b = std::move(q.front());
+      Batch b = std::move(q.front());
       q.pop_front();
       busy = true;
       const bool failed = sink_rc != 0;
@@ -542,6 +610,7 @@ struct BlobWriter::Impl {
         t_emit += std::chrono::duration<double>(clk::now() - t2).count();
       }
       ++n_batches;
+      t_last = std::chrono::duration<double>(clk::now() - t_born).count();
       g.lock();
       if (r && !sink_rc) {
         sink_rc = r;
@@ -552,15 +621,19 @@ struct BlobWriter::Impl {
       qcv.notify_all();
     }
   }
-  std::vector<uint8_t> take_buffer() {
+  Batch take_buffer() {
     std::unique_lock<std::mutex> g(qm);
     qcv.wait(g, [&] { return q.size() < kDepth; });
-    if (free_bufs.empty()) return {};
-    std::vector<uint8_t> b = std::move(free_bufs.front());
+    Batch b;
+    if (free_bufs.empty()) {
+      (void)WriterCache::get().take_buf(&b);  // one an earlier writer left
+      return b;
+    }
+    b = std::move(free_bufs.front());
     free_bufs.pop_front();
     return b;
   }
-  int submit(std::vector<uint8_t> &&b) {
+  int submit(Batch &&b) {
     std::lock_guard<std::mutex> g(qm);
     if (sink_rc) return host_fail(sink_rc, "%s", sink_err.c_str());
     q.push_back(std::move(b));
@@ -580,11 +653,18 @@ struct BlobWriter::Impl {
     }
     qcv.notify_all();
     if (sink.joinable()) sink.join();
+    WriterCache &wc = WriterCache::get();
+    wc.put_pool(std::move(pool));
+    for (Batch &b : free_bufs) wc.put_buf(std::move(b));
+    for (Batch &b : q) wc.put_buf(std::move(b));
     const char *v = getenv("NGPU_SINK_STATS");
     if (v && *v == '1')
       fprintf(stderr, "{\"sink_batches\": %llu, \"sink_wait_s\": %.4f, \"sink_sha_s\": %.4f, "
-              "\"sink_emit_s\": %.4f, \"bytes\": %llu}\n", (unsigned long long)n_batches, t_wait,
-              t_sha, t_emit, (unsigned long long)written);
+              "\"sink_emit_s\": %.4f, \"first_batch_at_s\": %.4f, \"last_batch_done_at_s\": %.4f, "
+              "\"writer_gone_at_s\": %.4f, \"bytes\": %llu}\n", (unsigned long long)n_batches, t_wait,
+              t_sha, t_emit, t_first, t_last,
+              std::chrono::duration<double>(std::chrono::steady_clock::now() - t_born).count(),
+              (unsigned long long)written);
   }
 };
 
@@ -620,7 +700,7 @@ int BlobWriter::init() {
     const unsigned hw = std::thread::hardware_concurrency();
     t = hw ? std::min(16u, hw) : 4u;
   }
-  im_->pool.reset(new Pool(t));
+  im_->pool = WriterCache::get().take_pool(t);
   Impl *m = im_.get();
   m->sink = std::thread([m] { m->sink_loop(); });
   return 0;
@@ -638,7 +718,7 @@ int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) 
     uint64_t b = a, bytes = 0;
     while (b < k && (b == a || bytes + len[b] <= (64ull << 20))) bytes += len[b++];
     const uint64_t nb = b - a;
-    std::vector<uint8_t> out = m.take_buffer();
+    Batch out = m.take_buffer();
     if (kind == NGPU_COMPRESSOR_NONE) {
       out.resize(bytes);
       m.slot_off.resize(nb + 1);

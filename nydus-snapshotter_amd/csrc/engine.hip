@@ -123,7 +123,15 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
     uint64_t c = 0, c1 = 0;
     if (grow(e, &ws.stats, c, 16)) return NGPU_ENOMEM;
     if (grow(e, &ws.lfirst1, c1, 2)) return NGPU_ENOMEM;
-    HIP_TRY(e, hipMemset(ws.stats, 0, c * sizeof(uint64_t)));  // no stale error counter
+    // no stale error counter.  hipMemset is asynchronous to the host and runs on
+    // the null stream, which does not order against a caller's non-blocking
+    // stream: unwaited, the zeroing could land AFTER this call's first digest
+    // kernel wrote the counters -- b3_tree then found its queue count zeroed
+    // and the multi-leaf chunks kept no digest (the digest guard's NGPU_EDEVICE;
+    // reproduced by the first node step on 8 streams, tools/step_diag.py).
+    // The counters are zeroed and waited for here, before any stage uses them.
+    HIP_TRY(e, hipMemsetAsync(ws.stats, 0, c * sizeof(uint64_t), nullptr));
+    HIP_TRY(e, hipStreamSynchronize(nullptr));
   }
   if (L > ws.cap_layers || !ws.lstats) {
     uint64_t c = ws.cap_layers;
@@ -387,6 +395,7 @@ void engine_unref(ngpu_engine *e) {
     if (b.copied) (void)hipEventDestroy(b.copied);
     if (b.done) (void)hipEventDestroy(b.done);
   }
+  for (auto &b : e->land_pool) (void)hipHostFree(b.first);
   for (auto &b : e->pack_pool) {
     if (b.d_res) (void)hipFree(b.d_res);
     if (b.d_all) (void)hipFree(b.d_all);
@@ -533,6 +542,18 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
           ngpu_destroy(e);
           return NGPU_EHIP;
         }
+  // Retained Pack segments (pack.hip) come from the device's stream-ordered
+  // pool: a layer's 64 MiB segments go back to it at the Pack's end without
+  // hipFree's device-wide wait (~0.5 ms each), and the next Pack reuses them.
+  // The pool keeps up to NGPU_SEG_POOL_MIB (default 4096) cached.
+  {
+    hipMemPool_t mp = nullptr;
+    uint64_t keep = 4096ull << 20;
+    if (const char *v = getenv("NGPU_SEG_POOL_MIB")) keep = strtoull(v, nullptr, 10) << 20;
+    if (hipDeviceGetDefaultMemPool(&mp, c.device) == hipSuccess && mp)
+      (void)hipMemPoolSetAttribute(mp, hipMemPoolAttrReleaseThreshold, &keep);
+    (void)hipGetLastError();
+  }
   bool ok = hipEventCreateWithFlags(&e->host_ev, hipEventDisableTiming) == hipSuccess &&
             hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess;
   if (ok) e->streams.push_back(e->stream);
@@ -583,7 +604,10 @@ int ngpu_device_status(ngpu_engine *e) {
       uint64_t w[4];
       HIP_TRY(e, hipMemcpy(w, sl.ws.stats + kStSticky, sizeof w, hipMemcpyDeviceToHost));
       if (!(w[0] | w[1] | w[2])) continue;
-      HIP_TRY(e, hipMemset(sl.ws.stats + kStSticky, 0, sizeof w));
+      // waited for (see ensure_workspace): a later stage's error counts on a
+      // non-blocking stream must not be cleared by a null-stream memset still queued
+      HIP_TRY(e, hipMemsetAsync(sl.ws.stats + kStSticky, 0, sizeof w, nullptr));
+      HIP_TRY(e, hipStreamSynchronize(nullptr));
       if (!first) first = stats_error(e, w[0], w[1], w[2], w[3], sl.path);  // its message kept
     }
     return first;

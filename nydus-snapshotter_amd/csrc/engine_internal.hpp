@@ -160,6 +160,9 @@ struct ngpu_engine {
   std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu, <= kStagingPool
   static constexpr size_t kStagingPool = 32;   // 16 packs open at once keep theirs
   std::vector<ngpu_pack_bufs> pack_pool;        // guarded by pool_mu
+  // pinned landing buffers of early-emission Packs that did not come from the
+  // staging pool (ngpu_pack_set_output): kept, not hipHostFree'd (~5 ms each)
+  std::vector<std::pair<void *, uint64_t>> land_pool;  // guarded by pool_mu, <= kStagingPool
   std::mutex pool_mu;
   std::string err;
   std::mutex err_mu;  // fail() may run outside mu (a pack's blob stream)

@@ -21,21 +21,47 @@
 // the DMA engines keep coarse-grained HBM coherent across the GPUs, and the
 // payload is tiny (16K chunks of a 16 GiB layer = 512 KiB out, 384 KiB back
 // per owner), so the exchange is latency-bound, not link-bound.
+#include <dlfcn.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
 
 #include <algorithm>
 
+#include <rccl/rccl.h>
+
 #include "engine_internal.hpp"
 
 using namespace ngpu;
+
+namespace {
+// Buffers of one part of a node step (ngpu_node_process_step), on its device.
+struct StepBuf {
+  uint8_t *xq = nullptr;          // its digests bucketed by owner (n x 32)
+  uint32_t *xrow = nullptr;       // their row ids
+  ngpu_dict_hit *sh = nullptr;    // hits returned, same (owner-bucketed) order
+  ngpu_dict_hit *hits = nullptr;  // hits by row
+  uint64_t cap = 0;
+  uint8_t *rq = nullptr;          // digests it received as owner (R x 32)
+  ngpu_dict_hit *rh = nullptr;    // its hits for them
+  uint64_t rcap = 0;
+  uint32_t *cnt = nullptr;        // 128 u32: per-owner counts (+ scatter cursors)
+  uint32_t *h_cnt = nullptr;      // pinned copy of the counts
+  hipEvent_t counted = nullptr, sent = nullptr, returned = nullptr, done = nullptr;
+};
+}  // namespace
 
 struct ngpu_node {
   std::vector<ngpu_engine *> eng;  // one per listed device (a reference each)
   std::vector<int> dev;
   std::atomic<uint64_t> rr{0};     // round robin over the engines for Packs
   bool peer_ok = true;             // every pair of distinct devices has peer access
+  // node steps (ngpu_node_process_step): one at a time, buffers per part,
+  // the RCCL communicator of the node's devices once a step asked for it
+  std::mutex step_mu;
+  std::vector<StepBuf> sb;
+  bool stepped = false;            // sb[*].done recorded by a previous step
+  std::vector<ncclComm_t> comms;
 };
 
 namespace ngpu {
@@ -306,6 +332,280 @@ void node_dict_free(ngpu_dict *d) {
   d->parts.clear();
 }
 
+// ---- node step ---------------------------------------------------------------
+namespace {
+
+// RCCL is loaded when a step first asks for it (dlopen): processes that never
+// run an RCCL step do not map its 570 MB library or register its kernels.
+struct Rccl {
+  decltype(&ncclCommInitAll) init = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclAllToAllv) alltoallv = nullptr;
+  decltype(&ncclGetErrorString) err = nullptr;
+  bool ok = false;
+};
+const Rccl &rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return x;
+    x.init = (decltype(x.init))dlsym(h, "ncclCommInitAll");
+    x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
+    x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
+    x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
+    x.alltoallv = (decltype(x.alltoallv))dlsym(h, "ncclAllToAllv");
+    x.err = (decltype(x.err))dlsym(h, "ncclGetErrorString");
+    x.ok = x.init && x.destroy && x.group_start && x.group_end && x.alltoallv && x.err;
+    return x;
+  }();
+  return r;
+}
+
+void step_free(ngpu_node *node) {
+  for (size_t i = 0; i < node->sb.size(); ++i) {
+    StepBuf &b = node->sb[i];
+    DeviceGuard g(node->dev[i]);
+    if (b.done) (void)hipEventSynchronize(b.done);
+    for (void *p : {(void *)b.xq, (void *)b.xrow, (void *)b.sh, (void *)b.hits, (void *)b.rq,
+                    (void *)b.rh, (void *)b.cnt})
+      if (p) (void)hipFree(p);
+    if (b.h_cnt) (void)hipHostFree(b.h_cnt);
+    for (hipEvent_t ev : {b.counted, b.sent, b.returned, b.done})
+      if (ev) (void)hipEventDestroy(ev);
+  }
+  node->sb.clear();
+  for (ncclComm_t c : node->comms)
+    if (c) (void)rccl().destroy(c);
+  node->comms.clear();
+}
+
+// The node's RCCL communicator (one rank per device), created on first use.
+int step_comms(ngpu_node *node) {
+  ngpu_engine *e0 = node->eng[0];
+  if (!node->comms.empty()) return 0;
+  if (!rccl().ok) return fail(e0, NGPU_EUNSUPP, "node step over RCCL: librccl.so.1 not loadable");
+  const int W = (int)node->dev.size();
+  for (int a = 0; a < W; ++a)
+    for (int b = a + 1; b < W; ++b)
+      if (node->dev[a] == node->dev[b])
+        return fail(e0, NGPU_EUNSUPP, "node step over RCCL: device %d is listed twice (RCCL "
+                    "takes one rank per GPU)", node->dev[a]);
+  std::vector<ncclComm_t> c((size_t)W);
+  const ncclResult_t r = rccl().init(c.data(), W, node->dev.data());
+  if (r != ncclSuccess)
+    return fail(e0, NGPU_EHIP, "node step: ncclCommInitAll over %d devices: %s", W,
+                rccl().err(r));
+  node->comms = std::move(c);
+  return 0;
+}
+
+int step_grow(ngpu_engine *e, StepBuf &b, uint64_t n, uint64_t r) {
+  if (!b.cnt) HIP_TRY(e, hipMalloc((void **)&b.cnt, 128 * sizeof(uint32_t)));
+  if (!b.h_cnt) HIP_TRY(e, hipHostMalloc((void **)&b.h_cnt, 64 * sizeof(uint32_t), hipHostMallocDefault));
+  for (hipEvent_t *ev : {&b.counted, &b.sent, &b.returned, &b.done})
+    if (!*ev) HIP_TRY(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  if (n > b.cap || !b.xq) {
+    for (void *p : {(void *)b.xq, (void *)b.xrow, (void *)b.sh, (void *)b.hits})
+      if (p) (void)hipFree(p);
+    b.xq = nullptr, b.xrow = nullptr, b.sh = nullptr, b.hits = nullptr, b.cap = 0;
+    const uint64_t c = next_pow2(n < 1024 ? 1024 : n);
+    HIP_TRY(e, hipMalloc((void **)&b.xq, c * 32));
+    HIP_TRY(e, hipMalloc((void **)&b.xrow, c * 4));
+    HIP_TRY(e, hipMalloc((void **)&b.sh, c * sizeof(ngpu_dict_hit)));
+    HIP_TRY(e, hipMalloc((void **)&b.hits, c * sizeof(ngpu_dict_hit)));
+    b.cap = c;
+  }
+  if (r > b.rcap || !b.rq) {
+    if (b.rq) (void)hipFree(b.rq);
+    if (b.rh) (void)hipFree(b.rh);
+    b.rq = nullptr, b.rh = nullptr, b.rcap = 0;
+    const uint64_t c = next_pow2(r < 1024 ? 1024 : r);
+    HIP_TRY(e, hipMalloc((void **)&b.rq, c * 32));
+    HIP_TRY(e, hipMalloc((void **)&b.rh, c * sizeof(ngpu_dict_hit)));
+    b.rcap = c;
+  }
+  return 0;
+}
+
+#define NCCL_TRY(e, x)                                                                  \
+  do {                                                                                  \
+    const ncclResult_t r_ = (x);                                                        \
+    if (r_ != ncclSuccess) return fail(e, NGPU_EHIP, "node step: %s: %s", #x, rccl().err(r_)); \
+  } while (0)
+
+// One all-to-all-v of `row`-byte rows: part i sends cnt_send(i, j) rows from
+// src[i] + sdis(i, j) to part j, which stores them at dst[j] + rdis(j, i).
+template <class CntF, class SdisF, class RdisF>
+int step_alltoallv(ngpu_node *node, bool use_rccl, const std::vector<hipStream_t> &s,
+                   const std::vector<const uint8_t *> &src, const std::vector<uint8_t *> &dst,
+                   uint64_t row, CntF cnt_send, SdisF sdis, RdisF rdis, hipEvent_t StepBuf::*mark) {
+  ngpu_engine *e0 = node->eng[0];
+  const uint32_t W = (uint32_t)node->eng.size();
+  if (use_rccl) {
+    std::vector<size_t> sc(W), sd(W), rc(W), rd(W);
+    NCCL_TRY(e0, rccl().group_start());
+    for (uint32_t i = 0; i < W; ++i) {
+      for (uint32_t j = 0; j < W; ++j) {
+        sc[j] = cnt_send(i, j) * row;
+        sd[j] = sdis(i, j) * row;
+        rc[j] = cnt_send(j, i) * row;
+        rd[j] = rdis(i, j) * row;
+      }
+      const ncclResult_t r = rccl().alltoallv(src[i], sc.data(), sd.data(), dst[i], rc.data(),
+                                              rd.data(), ncclUint8, node->comms[i], s[i]);
+      if (r != ncclSuccess) {
+        (void)rccl().group_end();
+        return fail(e0, NGPU_EHIP, "node step: ncclAllToAllv: %s", rccl().err(r));
+      }
+    }
+    NCCL_TRY(e0, rccl().group_end());
+    return 0;
+  }
+  // peer copies on the sender's stream; every receiver waits for every sender
+  for (uint32_t i = 0; i < W; ++i) {
+    DeviceGuard g(node->dev[i]);
+    for (uint32_t j = 0; j < W; ++j) {
+      const uint64_t c = cnt_send(i, j);
+      if (c)
+        HIP_TRY(e0, hipMemcpyPeerAsync(dst[j] + rdis(j, i) * row, node->dev[j],
+                                       src[i] + sdis(i, j) * row, node->dev[i], c * row, s[i]));
+    }
+    HIP_TRY(e0, hipEventRecord(node->sb[i].*mark, s[i]));
+  }
+  for (uint32_t j = 0; j < W; ++j) {
+    DeviceGuard g(node->dev[j]);
+    for (uint32_t i = 0; i < W; ++i)
+      if (i != j) HIP_TRY(e0, hipStreamWaitEvent(s[j], node->sb[i].*mark, 0));
+  }
+  return 0;
+}
+
+int node_step(ngpu_node *node, ngpu_dict *d, const ngpu_node_part *pt, uint32_t np, uint32_t flags) {
+  ngpu_engine *e0 = node->eng[0];
+  const uint32_t W = (uint32_t)node->eng.size();
+  if (np != W) return fail(e0, NGPU_EINVAL, "node step: %u parts for a node of %u devices", np, W);
+  for (uint32_t i = 0; i < W; ++i) {
+    const ngpu_node_part &p = pt[i];
+    if ((p.n && (!p.d_data || !p.d_chunks || !p.d_out)) || (p.d_layer_first && !p.n_layers) ||
+        p.n >= 0xFFFFFFFFull)
+      return fail(e0, NGPU_EINVAL, "node step: bad part %u", i);
+  }
+  if (!d || d->parts.empty() || d->replicated) {  // no exchange: each part on its own
+    for (uint32_t i = 0; i < W; ++i) {
+      const ngpu_node_part &p = pt[i];
+      if (int rc = ngpu_process_dict_device(node->eng[i], d, p.d_data, p.len, p.d_chunks, p.n,
+                                            p.d_out, p.d_layer_first, p.n_layers, p.d_stats,
+                                            p.stream, nullptr))
+        return rc;
+    }
+    return 0;
+  }
+  if (d->parts.size() != W) return fail(e0, NGPU_EINVAL, "node step: the dict has %zu parts, the node %u devices",
+                                        d->parts.size(), W);
+  for (uint32_t i = 0; i < W; ++i)
+    if (d->parts[i]->device != node->dev[i])
+      return fail(e0, NGPU_EINVAL, "node step: dict part %u is not on node device %u", i, i);
+  const bool use_rccl = (flags & NGPU_NODE_STEP_RCCL) != 0;
+  std::lock_guard<std::mutex> g(node->step_mu);
+  if (use_rccl)
+    if (int rc = step_comms(node)) return rc;
+  node->sb.resize(W);
+  std::vector<hipStream_t> s(W);
+  for (uint32_t i = 0; i < W; ++i) s[i] = (hipStream_t)pt[i].stream;
+  // buffers are reused: this step's streams start after every part of the last
+  for (uint32_t i = 0; i < W; ++i) {
+    DeviceGuard dg(node->dev[i]);
+    if (int rc = step_grow(node->eng[i], node->sb[i], pt[i].n, 0)) return rc;
+    if (node->stepped)
+      for (uint32_t j = 0; j < W; ++j) HIP_TRY(e0, hipStreamWaitEvent(s[i], node->sb[j].done, 0));
+  }
+  // 1. digests; 2. bucket them by owner, counts to the host
+  for (uint32_t i = 0; i < W; ++i) {
+    const ngpu_node_part &p = pt[i];
+    StepBuf &b = node->sb[i];
+    if (p.n)
+      if (int rc = ngpu_digest_device(node->eng[i], p.d_data, p.len, p.d_chunks, p.n, p.d_out, p.stream))
+        return rc;
+    DeviceGuard dg(node->dev[i]);
+    launch_route(reinterpret_cast<const uint8_t *>(p.d_out), sizeof(ngpu_result), p.n, W, 0, b.cnt,
+                 b.xq, b.xrow, s[i]);
+    HIP_TRY(e0, hipGetLastError());
+    HIP_TRY(e0, hipMemcpyAsync(b.h_cnt, b.cnt, W * sizeof(uint32_t), hipMemcpyDeviceToHost, s[i]));
+    HIP_TRY(e0, hipEventRecord(b.counted, s[i]));
+  }
+  std::vector<uint64_t> c((size_t)W * W), off((size_t)W * W), roff((size_t)W * W), R(W, 0);
+  for (uint32_t i = 0; i < W; ++i) {
+    HIP_TRY(e0, hipEventSynchronize(node->sb[i].counted));
+    uint64_t o = 0;
+    for (uint32_t j = 0; j < W; ++j) {
+      c[i * W + j] = node->sb[i].h_cnt[j];
+      off[i * W + j] = o;  // requester i's segment for owner j
+      o += c[i * W + j];
+    }
+    if (o != pt[i].n) return fail(e0, NGPU_EDEVICE, "node step: part %u routed %llu of %llu rows", i,
+                                  (unsigned long long)o, (unsigned long long)pt[i].n);
+  }
+  for (uint32_t j = 0; j < W; ++j)
+    for (uint32_t i = 0; i < W; ++i) {
+      roff[j * W + i] = R[j];  // owner j's segment from requester i
+      R[j] += c[i * W + j];
+    }
+  for (uint32_t j = 0; j < W; ++j) {
+    DeviceGuard dg(node->dev[j]);
+    if (int rc = step_grow(node->eng[j], node->sb[j], pt[j].n, R[j])) return rc;
+  }
+  auto cnt_fwd = [&](uint32_t i, uint32_t j) { return c[i * W + j]; };
+  auto sdis_fwd = [&](uint32_t i, uint32_t j) { return off[i * W + j]; };
+  auto rdis_fwd = [&](uint32_t j, uint32_t i) { return roff[j * W + i]; };
+  std::vector<const uint8_t *> src(W);
+  std::vector<uint8_t *> dst(W);
+  // 3. digests to their owners
+  for (uint32_t i = 0; i < W; ++i) src[i] = node->sb[i].xq, dst[i] = node->sb[i].rq;
+  if (int rc = step_alltoallv(node, use_rccl, s, src, dst, 32, cnt_fwd, sdis_fwd, rdis_fwd, &StepBuf::sent))
+    return rc;
+  // 4. owners probe their partitions
+  for (uint32_t j = 0; j < W; ++j) {
+    DeviceGuard dg(node->dev[j]);
+    launch_dict_probe(node->sb[j].rq, 32, R[j], d->parts[j]->dev, node->sb[j].rh, s[j]);
+    HIP_TRY(e0, hipGetLastError());
+  }
+  // 5. hits back: owner j sends requester i's rows from roff(j, i) to off(i, j)
+  for (uint32_t j = 0; j < W; ++j)
+    src[j] = reinterpret_cast<const uint8_t *>(node->sb[j].rh),
+    dst[j] = reinterpret_cast<uint8_t *>(node->sb[j].sh);
+  auto cnt_back = [&](uint32_t j, uint32_t i) { return c[i * W + j]; };
+  auto sdis_back = [&](uint32_t j, uint32_t i) { return roff[j * W + i]; };
+  auto rdis_back = [&](uint32_t i, uint32_t j) { return off[i * W + j]; };
+  if (int rc = step_alltoallv(node, use_rccl, s, src, dst, sizeof(ngpu_dict_hit), cnt_back, sdis_back,
+                              rdis_back, &StepBuf::returned))
+    return rc;
+  // 6. hits to their rows, then each part's own dedup
+  const uint32_t nb = d->dev.n_blobs ? d->dev.n_blobs : 1;
+  for (uint32_t i = 0; i < W; ++i) {
+    const ngpu_node_part &p = pt[i];
+    StepBuf &b = node->sb[i];
+    ngpu_engine *e = node->eng[i];
+    if (p.n) {
+      DeviceGuard dg(e->device);
+      launch_hits_scatter(b.sh, b.xrow, p.n, b.hits, s[i]);
+      HIP_TRY(e0, hipGetLastError());
+      std::lock_guard<std::mutex> eg(e->mu);
+      if (int rc = enqueue_dedup(e, nullptr, p.d_chunks, p.n, p.d_out, b.hits, nb, s[i],
+                                 p.d_layer_first, p.d_layer_first ? p.n_layers : 1, p.d_stats))
+        return rc;
+    }
+    DeviceGuard dg(node->dev[i]);
+    HIP_TRY(e0, hipEventRecord(b.done, s[i]));
+  }
+  node->stepped = true;
+  return 0;
+}
+
+}  // namespace
+
 }  // namespace ngpu
 
 extern "C" {
@@ -352,6 +652,7 @@ int ngpu_node_create(const int32_t *devices, uint32_t n, const ngpu_config *cfg,
 
 void ngpu_node_destroy(ngpu_node *node) {
   if (!node) return;
+  step_free(node);
   for (ngpu_engine *e : node->eng) ngpu_destroy(e);
   delete node;
 }
@@ -404,6 +705,12 @@ int ngpu_node_process_device(ngpu_node *node, uint32_t i, ngpu_dict *dict, const
   if (!node || i >= node->eng.size()) return NGPU_EINVAL;
   return ngpu_process_dict_device(node->eng[i], dict, d_data, len, d_chunks, n, d_out,
                                   d_layer_first, n_layers, d_stats, stream, nullptr);
+}
+
+int ngpu_node_process_step(ngpu_node *node, ngpu_dict *dict, const ngpu_node_part *parts,
+                           uint32_t n_parts, uint32_t flags) {
+  if (!node || !parts || (flags & ~NGPU_NODE_STEP_RCCL)) return NGPU_EINVAL;
+  return guarded([&] { return node_step(node, dict, parts, n_parts, flags); });
 }
 
 }  // extern "C"

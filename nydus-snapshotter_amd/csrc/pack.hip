@@ -38,6 +38,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <memory>
 #include <string>
@@ -205,6 +206,8 @@ struct ngpu_pack : TarSink {
   std::unique_ptr<GzipIndexer> gz; // NGPU_PACK_OCIREF: the gzip blob is inflated and indexed
   int err = 0;
 
+  std::chrono::steady_clock::time_point born = std::chrono::steady_clock::now();
+
   explicit ngpu_pack(ngpu_engine *eng) : e(eng), sc(eng->cfg.chunk_size) {}
 
   int chunk(uint64_t off, uint32_t len, uint32_t fi, uint64_t fo) override {
@@ -215,6 +218,17 @@ struct ngpu_pack : TarSink {
 };
 
 namespace {
+
+// NGPU_PACK_TRACE=1: phase timestamps of a Pack's close, on stderr (diagnostic)
+void ptrace(const ngpu_pack *p, const char *what) {
+  static const bool on = [] {
+    const char *v = getenv("NGPU_PACK_TRACE");
+    return v && *v == '1';
+  }();
+  if (!on) return;
+  const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - p->born).count();
+  fprintf(stderr, "{\"pack_trace\": \"%s\", \"t_s\": %.4f}\n", what, t);
+}
 
 bool cancelled(const ngpu_pack *p) {
   return p->cancel && __atomic_load_n(p->cancel, __ATOMIC_RELAXED) != 0;
@@ -227,12 +241,14 @@ void release(ngpu_pack *p) {
   ngpu_engine *e = p->e;
   ngpu_dict *dict = p->dict;
   DeviceGuard dg(e->device);
+  ptrace(p, "release");
   emit_stop(p);
   for (Slot &s : p->slot) {
     if (s.done) (void)hipEventSynchronize(s.done);
   }
   if (p->copy) (void)hipStreamSynchronize(p->copy);
   if (p->stream) (void)hipStreamSynchronize(p->stream);
+  ptrace(p, "release_synced");
   {
     std::lock_guard<std::mutex> g(p->e->pool_mu);
     for (Slot &s : p->slot) {
@@ -251,7 +267,8 @@ void release(ngpu_pack *p) {
     if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.done) (void)hipEventDestroy(s.done);
   }
-  for (Seg &g : p->segs) (void)hipFree(g.d);
+  for (Seg &g : p->segs) (void)hipFreeAsync(g.d, p->stream);  // the streams are idle
+  ptrace(p, "release_segments");
   if (Emit *em = p->em) {  // its landing buffers go back to the staging pool
     std::lock_guard<std::mutex> g(e->pool_mu);
     for (ngpu_staging_buf &b : em->land) {
@@ -259,6 +276,8 @@ void release(ngpu_pack *p) {
       const bool whole = b.h_ch && b.d_ch && b.copied && b.done;  // a pool entry (else: own landing)
       if (whole && e->staging_pool.size() < ngpu_engine::kStagingPool) {
         e->staging_pool.push_back(b);
+      } else if (!whole && !b.d && e->land_pool.size() < ngpu_engine::kStagingPool) {
+        e->land_pool.push_back({b.h, b.cap});  // an own landing: kept for the next Pack
       } else {
         (void)hipHostFree(b.h);
         if (b.h_ch) (void)hipHostFree(b.h_ch);
@@ -270,12 +289,14 @@ void release(ngpu_pack *p) {
       b = ngpu_staging_buf{};
     }
   }
+  ptrace(p, "release_landing");
   if (Emit *em = p->em) {
     if (em->h_res) (void)hipHostFree(em->h_res);
     if (em->h_stats) (void)hipHostFree(em->h_stats);
     if (em->ev) (void)hipEventDestroy(em->ev);
     delete em;
     p->em = nullptr;
+    ptrace(p, "release_writer_gone");
   }
   {
     // the streams are idle (synchronised above).  Every compute stream goes
@@ -360,7 +381,8 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
   uint8_t *dev = s.d;
   if (p->retain) {  // this slot's bytes get their own resident segment
     Seg g;
-    HIP_TRY(e, hipMalloc((void **)&g.d, s.fill));
+    // stream-ordered (the device pool, engine.hip): freed without a device-wide wait
+    HIP_TRY(e, hipMallocAsync((void **)&g.d, s.fill, p->copy));
     g.base = s.base;
     g.a = a;
     g.b = b;
@@ -768,6 +790,7 @@ int emit_finish(ngpu_pack *p, Emit *em, const ngpu_chunk *ch, const ngpu_result 
   if (int rc = emit_range(p, *em->bw, ch + em->emitted, dptr.data(), res + em->emitted,
                           n - em->emitted, land, &em->new_emitted))
     return rc;
+  ptrace(p, "finish_rest_emitted");
   if (int rc = em->bw->finish(ch, res, n, st, p->entries, info))
     return fail(e, rc, "pack: %s", ngpu_host_error());
   return 0;
@@ -931,13 +954,21 @@ int ngpu_pack_set_output(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_
     {  // window landing buffers: staging slots from the engine's pool when it has them
       std::lock_guard<std::mutex> g(e->pool_mu);
       auto &pool = e->staging_pool;
-      for (ngpu_staging_buf &b : em->land)
+      for (ngpu_staging_buf &b : em->land) {
         for (size_t i = 0; i < pool.size(); ++i)
           if (pool[i].cap == p->cap) {
             b = pool[i];
             pool.erase(pool.begin() + (long)i);
             break;
           }
+        auto &lp = e->land_pool;  // else a landing kept by an earlier Pack
+        for (size_t i = 0; !b.h && i < lp.size(); ++i)
+          if (lp[i].second == p->cap) {
+            b.h = lp[i].first;
+            b.cap = lp[i].second;
+            lp.erase(lp.begin() + (long)i);
+          }
+      }
     }
     for (ngpu_staging_buf &b : em->land)
       if (!b.h) {
@@ -1070,7 +1101,9 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
   *n_out = 0;
   ngpu_engine *e = p->e;
   Emit *em = p->em;
+  ptrace(p, "finish");
   emit_stop(p);  // the emitter stops after its current range; the rest is written below
+  ptrace(p, "finish_emitter_stopped");
   int rc = p->err ? p->err : (em && em->rc.load()) ? em->rc.load() : p->sc.finish();
   if (!rc && cancelled(p)) rc = fail(e, NGPU_ECANCELED, "pack: cancelled");
   if (!rc && w && !p->retain && !p->gz)
@@ -1148,6 +1181,7 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
     // and calls keep enqueueing meanwhile), then check its stats
     if (!rc && hipStreamSynchronize(p->stream) != hipSuccess)
       rc = fail(e, NGPU_EHIP, "pack: stream failed");
+    ptrace(p, "finish_dedup_done");
     if (!rc) rc = read_stats_parse(e, p->h_stats, &st, path.c_str());
     if (!rc && n) memcpy(res, p->h_io, n * sizeof(ngpu_result));
     // the blob stream is host work on the pack's own buffers: no engine lock
@@ -1160,6 +1194,7 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
     }
     if (!rc && em) rc = p->gz ? ref_finish(p, *em->bw, ch, res, n, st, info)
                               : emit_finish(p, em, ch, res, n, st, info);
+    ptrace(p, "finish_stream_done");
   }
   release(p);
   if (rc) {

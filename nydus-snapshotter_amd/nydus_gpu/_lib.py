@@ -70,7 +70,9 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_device_status", "ngpu_unpack",
            # ABI 4
            "ngpu_dict_create_device_gid", "ngpu_route_digests", "ngpu_route_hits",
-           "ngpu_pack_set_output", "ngpu_ref_chunk_read"]
+           "ngpu_pack_set_output", "ngpu_ref_chunk_read",
+           # ABI 5
+           "ngpu_node_process_step"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
@@ -245,6 +247,7 @@ def lib():
     L.ngpu_node_owner.restype = u32
     L.ngpu_node_pack_open.argtypes = [vp, vp, u32, ctypes.POINTER(vp)]
     L.ngpu_node_process_device.argtypes = [vp, u32, vp, vp, u64, vp, u64, vp, vp, u64, vp, vp]
+    L.ngpu_node_process_step.argtypes = [vp, vp, ctypes.POINTER(NgpuNodePart), u32, u32]
     _lib = L
     return L
 
@@ -909,6 +912,14 @@ class PackWriter:
         return ch, rs, st.as_dict(), (info.as_dict() if dest is not None else None)
 
 
+class NgpuNodePart(ctypes.Structure):
+    """ngpu_node_part: one device's share of a node step (device pointers)."""
+    _fields_ = [("d_data", ctypes.c_void_p), ("len", ctypes.c_uint64), ("d_chunks", ctypes.c_void_p),
+                ("n", ctypes.c_uint64), ("d_out", ctypes.c_void_p), ("d_layer_first", ctypes.c_void_p),
+                ("n_layers", ctypes.c_uint64), ("d_stats", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
+
+
+NODE_STEP_RCCL = 1  # ngpu_node_process_step: the all-to-alls are RCCL ncclAllToAllv
 NODE_DICT_PARTITION, NODE_DICT_REPLICATE = 0, 1
 NODE_EXCHANGE_COPY = 0x100  # | PARTITION: the ABI 3 broadcast + DMA exchange
 
@@ -990,6 +1001,20 @@ class Node:
         w._cancel = ctypes.c_int32(0)
         lib().ngpu_pack_set_cancel(w._p, ctypes.byref(w._cancel))
         return w
+
+    def process_step(self, dict, parts, rccl: bool = False):
+        """ngpu_node_process_step: every device's part at once, one all-to-all-v
+        each way (RCCL with rccl=True, peer copies otherwise).  parts: one dict
+        per node device with keys d_data, len, d_chunks, n, d_out and optionally
+        d_layer_first, n_layers, d_stats, stream (ints: device pointers)."""
+        arr = (NgpuNodePart * len(parts))()
+        for i, p in enumerate(parts):
+            arr[i] = NgpuNodePart(p.get("d_data", 0) or None, p.get("len", 0),
+                                  p.get("d_chunks", 0) or None, p.get("n", 0), p.get("d_out", 0) or None,
+                                  p.get("d_layer_first", 0) or None, p.get("n_layers", 1 if p.get("d_layer_first") else 0),
+                                  p.get("d_stats", 0) or None, p.get("stream", 0) or None)
+        self._err(lib().ngpu_node_process_step(self._h, _dict_arg(dict), arr, len(parts),
+                                               NODE_STEP_RCCL if rccl else 0), "node_process_step")
 
     def process_device(self, i: int, dict, d_data: int, length: int, d_chunks: int, n: int,
                        d_out: int, d_layer_first: int = 0, n_layers: int = 1, d_stats: int = 0,

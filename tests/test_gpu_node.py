@@ -262,3 +262,125 @@ def test_route_kernels_match_the_reference_router(W):
     torch.cuda.synchronize()
     assert torch.equal(hits[:, 0].cpu(), torch.arange(n, dtype=torch.int32))
     assert torch.equal(hits[:, 1].cpu(), torch.arange(n, dtype=torch.int32) * 3)
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_node_step_all_devices_at_once_vs_oracle(oracle, W):
+    """ngpu_node_process_step (ABI 5): every part of a W-device node (device 0
+    listed W times) in one bulk step -- digests, owner bucketing, one
+    all-to-all-v of digests, owner probes, one all-to-all-v of hits back, each
+    part's own dedup.  Peer-copy transport (RCCL takes one rank per GPU, so a
+    one-GPU node cannot build its communicator).  Parts hold 1-3 layers each
+    (per-layer decisions restart) and one part is empty; three steps in a row
+    reuse the step buffers.  Every decision equals the oracle's with the whole
+    dict, per layer."""
+    import torch
+    rng = np.random.default_rng(900 + W)
+    cs = 0x10000
+    steps = 3
+    parts = []  # [step][part] = list of (data, ch) layers
+    for _ in range(steps):
+        row = []
+        for i in range(W):
+            k = 0 if i == W - 1 else int(rng.integers(1, 4))
+            row.append([_layer(rng, int(rng.integers(2, 7)) << 20, cs) for _ in range(k)])
+        parts.append(row)
+    digs = [[[oracle.digest_chunks(d, c.view(oracle.CHUNK_DTYPE), "blake3") for d, c in ls] for ls in row]
+            for row in parts]
+    alld = [x for row in digs for ds in row for x in ds]
+    alls = [c["length"] for row in parts for ls in row for _, c in ls]
+    recs = _dict_records(rng, np.concatenate(alld), np.concatenate(alls))
+    blobs = rafs.make_blob_table([f"{i:064x}" for i in range(7)], cs)
+    node = nydus_gpu.Node([0] * W, chunk_size=cs)
+    try:
+        d = node.dict_create(recs, blobs, mode=nydus_gpu.NODE_DICT_PARTITION)
+        streams = [torch.cuda.Stream() for _ in range(W)]
+        for k in range(steps):
+            args, keep = [], []
+            for i in range(W):
+                ls = parts[k][i]
+                if not ls:
+                    args.append({"n": 0, "stream": streams[i].cuda_stream})
+                    continue
+                # the part's layers back to back in one buffer, chunk offsets shifted
+                base, bufs, chs, first = 0, [], [], [0]
+                for data, ch in ls:
+                    c = ch.copy()
+                    c["offset"] += base
+                    bufs.append(np.frombuffer(data, np.uint8))
+                    chs.append(c)
+                    base += len(data)
+                    first.append(first[-1] + len(ch))
+                buf, ch = np.concatenate(bufs), np.concatenate(chs)
+                d_data, d_ch = _to_dev(buf), _to_dev(ch)
+                d_first = _to_dev(np.array(first, np.uint64))
+                out = torch.zeros(len(ch) * 64, dtype=torch.uint8, device="cuda")
+                keep.append((d_data, d_ch, d_first, out))
+                args.append({"d_data": d_data.data_ptr(), "len": d_data.numel(), "d_chunks": d_ch.data_ptr(),
+                             "n": len(ch), "d_out": out.data_ptr(), "d_layer_first": d_first.data_ptr(),
+                             "n_layers": len(ls), "stream": streams[i].cuda_stream, "_first": first,
+                             "_out": out})
+            torch.cuda.synchronize()
+            node.process_step(d, args)
+            for s in streams:
+                s.synchronize()
+            for i in range(W):
+                if not parts[k][i]:
+                    continue
+                got = args[i]["_out"].cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+                first = args[i]["_first"]
+                for l, (_, ch) in enumerate(parts[k][i]):
+                    a, b = first[l], first[l + 1]
+                    exp = _expect(oracle, digs[k][i][l], ch, recs)
+                    assert np.array_equal(got["digest"][a:b], digs[k][i][l]), (k, i, l)
+                    for f in ("kind", "index", "blob_index", "uncompressed_offset"):
+                        assert np.array_equal(got[f][a:b], exp[f]), (k, i, l, f)
+                    own = exp["kind"] != nydus_gpu.DICT
+                    assert np.array_equal(got["ref"][a:b][own] - a, exp["ref"][own]), (k, i, l)
+                    assert np.array_equal(got["ref"][a:b][~own], exp["ref"][~own]), (k, i, l)
+            for e in node.engines:
+                e.device_status()
+        # RCCL needs distinct devices: the one-GPU node is refused, cleanly
+        with pytest.raises(nydus_gpu.NgpuError) as ei:
+            node.process_step(d, [{"n": 0} for _ in range(W)], rccl=True)
+        assert ei.value.code == nydus_gpu.EUNSUPP
+        d.release()
+    finally:
+        node.close()
+
+
+def test_node_step_without_a_partitioned_dict(oracle):
+    """A node step against a replicated dict (or none) runs each part on its
+    own: the same decisions as ngpu_node_process_device."""
+    import torch
+    rng = np.random.default_rng(5150)
+    cs = 0x10000
+    W = 2
+    layers = [_layer(rng, 4 << 20, cs) for _ in range(W)]
+    digs = [oracle.digest_chunks(d, c.view(oracle.CHUNK_DTYPE), "blake3") for d, c in layers]
+    recs = _dict_records(rng, np.concatenate(digs), np.concatenate([c["length"] for _, c in layers]))
+    node = nydus_gpu.Node([0] * W, chunk_size=cs)
+    try:
+        for dd in (node.dict_create(recs, mode=nydus_gpu.NODE_DICT_REPLICATE), None):
+            keep, args = [], []
+            for data, ch in layers:
+                d_data, d_ch = _to_dev(np.frombuffer(data, np.uint8)), _to_dev(ch)
+                out = torch.zeros(len(ch) * 64, dtype=torch.uint8, device="cuda")
+                keep.append((d_data, d_ch, out))
+                args.append({"d_data": d_data.data_ptr(), "len": d_data.numel(), "d_chunks": d_ch.data_ptr(),
+                             "n": len(ch), "d_out": out.data_ptr()})
+            torch.cuda.synchronize()
+            node.process_step(dd, args)
+            torch.cuda.synchronize()
+            for i, (_, ch) in enumerate(layers):
+                got = keep[i][2].cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+                if dd is None:
+                    exp, _ = oracle.dedup(digs[i], ch["length"])
+                else:
+                    exp = _expect(oracle, digs[i], ch, recs)
+                for f in ("kind", "index", "ref", "blob_index", "uncompressed_offset"):
+                    assert np.array_equal(got[f], exp[f]), (i, f)
+            if dd is not None:
+                dd.release()
+    finally:
+        node.close()

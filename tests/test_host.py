@@ -23,7 +23,7 @@ def test_header_symbols_exported():
     L = nydus_gpu.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.ngpu_abi_version() == 4
+    assert L.ngpu_abi_version() == 5
 
 
 def test_struct_sizes():
