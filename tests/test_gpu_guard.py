@@ -144,3 +144,46 @@ def test_bad_descriptor_reported_by_device_status():
         eng.device_status()
     finally:
         eng.close()
+
+
+def test_first_call_of_fresh_engines_on_nonblocking_streams(oracle):
+    """The round-2 zero digest, root-caused in round 4: an engine's first call
+    zeroed its new stats words with hipMemset, which is asynchronous to the
+    host and runs on the null stream -- unordered with a caller's
+    non-blocking stream.  Landing after the first digest kernel wrote its
+    counters, it zeroed b3_tree's queue count and the multi-leaf chunks kept
+    no digest (tools/step_diag.py reproduced it on 2 of 3 first node steps
+    over 8 streams).  Sixteen fresh engines, each called once on its own torch
+    (non-blocking) stream with no synchronisation between the enqueues: every
+    digest must equal the oracle's and no guard may fire."""
+    import torch
+    rng = np.random.default_rng(2024)
+    cs = 0x10000
+    total = 6 << 20
+    data = rng.integers(0, 256, total, dtype=np.uint8)
+    ch = np.zeros(total // cs, nydus_gpu.CHUNK_DTYPE)
+    ch["offset"] = np.arange(len(ch)) * cs
+    ch["length"] = cs
+    ch["length"][::7] = rng.integers(1, cs, len(ch[::7]))
+    ch["file_index"] = np.arange(len(ch))
+    dig = oracle.digest_chunks(data.tobytes(), ch.view(oracle.CHUNK_DTYPE), "blake3")
+    d_data = torch.from_numpy(data).cuda()
+    d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+    engines, outs, streams = [], [], []
+    try:
+        for _ in range(16):
+            engines.append(nydus_gpu.Engine(device=0, chunk_size=cs))
+            outs.append(torch.zeros(len(ch) * 64, dtype=torch.uint8, device="cuda"))
+            streams.append(torch.cuda.Stream())
+        torch.cuda.synchronize()
+        for e, o, s in zip(engines, outs, streams):
+            e.process_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), len(ch), o.data_ptr(),
+                             stream=s.cuda_stream)
+        torch.cuda.synchronize()
+        for k, (e, o) in enumerate(zip(engines, outs)):
+            e.device_status()
+            got = o.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
+            assert np.array_equal(got["digest"], dig), k
+    finally:
+        for e in engines:
+            e.close()
