@@ -483,6 +483,11 @@ int step_alltoallv(ngpu_node *node, bool use_rccl, const std::vector<hipStream_t
   return 0;
 }
 
+int node_step_enqueue(ngpu_node *node, ngpu_dict *d, const ngpu_node_part *pt, uint32_t W,
+                      bool use_rccl);
+
+// A failed step may have enqueued part of its work on the parts' streams: it
+// is waited for before the step buffers can be reused (or freed).
 int node_step(ngpu_node *node, ngpu_dict *d, const ngpu_node_part *pt, uint32_t np, uint32_t flags) {
   ngpu_engine *e0 = node->eng[0];
   const uint32_t W = (uint32_t)node->eng.size();
@@ -512,6 +517,20 @@ int node_step(ngpu_node *node, ngpu_dict *d, const ngpu_node_part *pt, uint32_t 
   std::lock_guard<std::mutex> g(node->step_mu);
   if (use_rccl)
     if (int rc = step_comms(node)) return rc;
+  const int rc = node_step_enqueue(node, d, pt, W, use_rccl);
+  if (rc) {
+    for (uint32_t i = 0; i < W; ++i) {
+      DeviceGuard dg(node->dev[i]);
+      (void)hipStreamSynchronize((hipStream_t)pt[i].stream);
+    }
+    node->stepped = false;  // nothing of this step is still in flight
+  }
+  return rc;
+}
+
+int node_step_enqueue(ngpu_node *node, ngpu_dict *d, const ngpu_node_part *pt, uint32_t W,
+                      bool use_rccl) {
+  ngpu_engine *e0 = node->eng[0];
   node->sb.resize(W);
   std::vector<hipStream_t> s(W);
   for (uint32_t i = 0; i < W; ++i) s[i] = (hipStream_t)pt[i].stream;
