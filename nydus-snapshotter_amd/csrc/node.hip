@@ -402,11 +402,15 @@ int step_comms(ngpu_node *node) {
   return 0;
 }
 
-int step_grow(ngpu_engine *e, StepBuf &b, uint64_t n, uint64_t r) {
+// quiesce: waits for the previous step before a buffer it may still use is freed
+template <class Q>
+int step_grow(ngpu_engine *e, StepBuf &b, uint64_t n, uint64_t r, Q &&quiesce) {
   if (!b.cnt) HIP_TRY(e, hipMalloc((void **)&b.cnt, 128 * sizeof(uint32_t)));
   if (!b.h_cnt) HIP_TRY(e, hipHostMalloc((void **)&b.h_cnt, 64 * sizeof(uint32_t), hipHostMallocDefault));
   for (hipEvent_t *ev : {&b.counted, &b.sent, &b.returned, &b.done})
     if (!*ev) HIP_TRY(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  if ((n > b.cap && b.xq) || (r > b.rcap && b.rq))
+    if (int rc = quiesce()) return rc;
   if (n > b.cap || !b.xq) {
     for (void *p : {(void *)b.xq, (void *)b.xrow, (void *)b.sh, (void *)b.hits})
       if (p) (void)hipFree(p);
@@ -532,12 +536,21 @@ int node_step_enqueue(ngpu_node *node, ngpu_dict *d, const ngpu_node_part *pt, u
                       bool use_rccl) {
   ngpu_engine *e0 = node->eng[0];
   node->sb.resize(W);
+  bool quiet = !node->stepped;
+  auto quiesce = [&]() -> int {  // the previous step done on every device
+    for (uint32_t j = 0; j < W && !quiet; ++j) {
+      DeviceGuard dg(node->dev[j]);
+      HIP_TRY(e0, hipEventSynchronize(node->sb[j].done));
+    }
+    quiet = true;
+    return 0;
+  };
   std::vector<hipStream_t> s(W);
   for (uint32_t i = 0; i < W; ++i) s[i] = (hipStream_t)pt[i].stream;
   // buffers are reused: this step's streams start after every part of the last
   for (uint32_t i = 0; i < W; ++i) {
     DeviceGuard dg(node->dev[i]);
-    if (int rc = step_grow(node->eng[i], node->sb[i], pt[i].n, 0)) return rc;
+    if (int rc = step_grow(node->eng[i], node->sb[i], pt[i].n, 0, quiesce)) return rc;
     if (node->stepped)
       for (uint32_t j = 0; j < W; ++j) HIP_TRY(e0, hipStreamWaitEvent(s[i], node->sb[j].done, 0));
   }
@@ -574,7 +587,7 @@ int node_step_enqueue(ngpu_node *node, ngpu_dict *d, const ngpu_node_part *pt, u
     }
   for (uint32_t j = 0; j < W; ++j) {
     DeviceGuard dg(node->dev[j]);
-    if (int rc = step_grow(node->eng[j], node->sb[j], pt[j].n, R[j])) return rc;
+    if (int rc = step_grow(node->eng[j], node->sb[j], pt[j].n, R[j], quiesce)) return rc;
   }
   auto cnt_fwd = [&](uint32_t i, uint32_t j) { return c[i * W + j]; };
   auto sdis_fwd = [&](uint32_t i, uint32_t j) { return off[i * W + j]; };
