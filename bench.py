@@ -781,7 +781,8 @@ def node_e2e(torch, dist, nydus_gpu, buf, wl, stride, device, backend, sample_by
 
 SUB_KEYS = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "stage_ms", "roofline",
             "cpu_baseline", "speedup_vs_cpu", "speedup_vs_cpu_single_stream", "dict",
-            "probe_roofline", "merge", "decisions", "digest_check_past_4gib", "n_gpus", "sharded_dict")
+            "probe_roofline", "merge", "decisions", "digest_check_past_4gib", "n_gpus", "sharded_dict",
+            "e2e_pcie", "tar_host_path")
 
 
 def child_line(cmd, timeout_s, env=None):
@@ -804,16 +805,21 @@ def child_line(cmd, timeout_s, env=None):
 
 
 def sub_entries(args):
-    """N = 1: driver-timed evidence for the dict paths beside the C2 headline
-    (VERDICT r3 item 5): C3 (sha256, 200M-entry dict in HBM, probe_roofline)
+    """N = 1: driver-timed evidence beside the C2 headline: C1 (the small
+    alpine-like layer, with its host path), and for the dict paths (VERDICT r3
+    item 5) C3 (sha256, 200M-entry dict in HBM, probe_roofline)
     and C5-1000 (1000 x 64 MiB layers, 64 KiB chunks, pool dict, one
     multi-layer dedup per step, then the host Merge of the 1000 bootstraps),
     each a full bench line of its own (value, ms_per_step, roofline,
     cpu_baseline), run as children after the headline is measured."""
     out = {}
-    for key, wl in (("c3", "c3"), ("c5_1000", "c5-1000")):
+    for key, wl in (("c1", "c1"), ("c3", "c3"), ("c5_1000", "c5-1000")):
+        # C1 (configs[0], the reference's CPU-runnable case: one ~10 MB layer)
+        # keeps its host path (ngpu_pack_tar from pinned host memory) and more
+        # steps: a step is ~0.06 ms
+        steps = args.sub_steps * 10 if wl == "c1" else args.sub_steps
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", wl, "--steps",
-               str(args.sub_steps), "--no-sub", "--no-e2e", "--settle-s", "1.0"]
+               str(steps), "--no-sub", "--settle-s", "1.0"] + ([] if wl == "c1" else ["--no-e2e"])
         out[key] = child_line(cmd, 420)
     return out
 
