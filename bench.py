@@ -1243,6 +1243,9 @@ def main():
                          "the GPU ~30%% slow for ~150 ms after it: profiles/r2/c4-16_warmup_r2u.json)")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--lanes", type=int, default=0, help="leaves per lane (0=auto)")
+    ap.add_argument("--load-mode", type=int, default=-1,
+                    help="BLAKE3 load mode override (diagnostics: 4 = no loads, needs a "
+                         "-DNGPU_DIAG_NOLOAD=1 build via NYDUS_GPU_LIB; its digests are not BLAKE3)")
     ap.add_argument("--sha-mode", choices=["auto", "split", "pair", "lane"], default="auto",
                     help="SHA-256 kernel: one lane per chunk (lane; split = schedule/round "
                          "waves) or two (pair)")
@@ -1344,7 +1347,8 @@ def main():
     h_out = torch.empty(n * 64, dtype=torch.uint8, pin_memory=True)
     eng = nydus_gpu.Engine(device=local, digester=wl["digester"], chunk_size=wl["chunk"],
                            leaves_per_lane=args.lanes, timing=True,
-                           flags=SHA_MODES[args.sha_mode] << 11)
+                           flags=(SHA_MODES[args.sha_mode] << 11)
+                           | ((args.load_mode + 1) << 8 if args.load_mode >= 0 else 0))
     stream = torch.cuda.Stream()
     extra = {}
     n_layers = wl["layers"]
