@@ -1497,13 +1497,14 @@ def main():
     # correctness spot checks of the last step
     res = h_outs[(nstep[0] - 1) % 2].numpy().view(nydus_gpu.RESULT_DTYPE)
     kinds = np.bincount(res["kind"], minlength=3)
-    if not wl.get("dict_entries") and not wl.get("pool") and not wl.get("tar"):
+    no_load = args.load_mode == 4  # diagnostic: not BLAKE3 digests, decisions unchecked
+    if not wl.get("dict_entries") and not wl.get("pool") and not wl.get("tar") and not no_load:
         assert kinds[0] == n and (res["index"] == np.arange(n)).all()
     if wl.get("dict_entries"):
         extra["dict"]["dict_hits"] = int(kinds[2])
         assert kinds[2] >= extra["dict"]["expected_dict_hits"] * 0.99, (kinds, extra)
     extra["decisions"] = {"NEW": int(kinds[0]), "INTRA": int(kinds[1]), "DICT": int(kinds[2])}
-    if buf.numel() > (1 << 32) and rank == 0:  # digests at offsets past 2^32 (independent C/OpenSSL)
+    if buf.numel() > (1 << 32) and rank == 0 and not no_load:  # digests past 2^32 (independent C/OpenSSL)
         extra["digest_check_past_4gib"] = check_high_digests(buf, ch, res, wl["digester"])
     if wl.get("merge") and world == 1 and rank == 0:
         extra["merge"] = merge_extra(nydus_gpu, ch, res, n_layers, per_layer, wl["chunk"], dict_host)
