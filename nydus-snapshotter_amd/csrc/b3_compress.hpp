@@ -104,6 +104,9 @@ constexpr Sched kSched = make_sched();
 #ifndef B3_FOLD
 #define B3_FOLD 1
 #endif
+#ifndef B3_FAST_NT
+#define B3_FAST_NT 0
+#endif
 #ifndef B3_LOAD128
 #define B3_LOAD128 1
 #endif

@@ -367,8 +367,16 @@ __device__ __forceinline__ int group_cv(const uint8_t *__restrict__ data, uint64
       // L2 to evict it: 14 % of the lines were fetched twice (TCC_EA0_RDREQ_128B,
       // profiles/r1/pmc_req_c2.json).
       for (uint32_t b = 0; b < 16; b += 2, q += 8) {
+#if B3_FAST_NT  // A/B only (default 0): the same line pair with non-temporal loads
+        const uint8_t *qb = reinterpret_cast<const uint8_t *>(q);
+        const u32x4 x0 = load_nt16(qb), x1 = load_nt16(qb + 16), x2 = load_nt16(qb + 32),
+                    x3 = load_nt16(qb + 48);
+        const u32x4 x4 = load_nt16(qb + 64), x5 = load_nt16(qb + 80), x6 = load_nt16(qb + 96),
+                    x7 = load_nt16(qb + 112);
+#else
         const u32x4 x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3];
         const u32x4 x4 = q[4], x5 = q[5], x6 = q[6], x7 = q[7];
+#endif
         m[0] = x0.x; m[1] = x0.y; m[2] = x0.z; m[3] = x0.w;
         m[4] = x1.x; m[5] = x1.y; m[6] = x1.z; m[7] = x1.w;
         m[8] = x2.x; m[9] = x2.y; m[10] = x2.z; m[11] = x2.w;
