@@ -201,6 +201,11 @@ struct ngpu_pack : TarSink {
   CopyPool *pool = nullptr;  // created on the first large write
   bool retain = false;       // NGPU_PACK_RETAIN: device segments kept to the end
   std::vector<Seg> segs;
+  // NGPU_PACK_RETAIN: the segments are carved out of arenas that double in
+  // size (1 slot, 2, 4, ... up to 1 GiB): a 2 GiB layer frees 6 arenas at the end
+  // instead of 32 slot-sized segments (~0.17 ms per free)
+  struct Arena { uint8_t *d = nullptr; uint64_t cap = 0, used = 0; };
+  std::vector<Arena> arenas;
   std::vector<TarEntry> entries;  // NGPU_PACK_RETAIN: the tar's entries (the bootstrap's inode tree)
   Emit *em = nullptr;              // ngpu_pack_set_output: the stream leaves while the tar arrives
   std::unique_ptr<GzipIndexer> gz; // NGPU_PACK_OCIREF: the gzip blob is inflated and indexed
@@ -267,7 +272,7 @@ void release(ngpu_pack *p) {
     if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.done) (void)hipEventDestroy(s.done);
   }
-  for (Seg &g : p->segs) (void)hipFreeAsync(g.d, p->stream);  // the streams are idle
+  for (ngpu_pack::Arena &ar : p->arenas) (void)hipFreeAsync(ar.d, p->stream);  // the streams are idle
   ptrace(p, "release_segments");
   if (Emit *em = p->em) {  // its landing buffers go back to the staging pool
     std::lock_guard<std::mutex> g(e->pool_mu);
@@ -381,8 +386,19 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
   uint8_t *dev = s.d;
   if (p->retain) {  // this slot's bytes get their own resident segment
     Seg g;
-    // stream-ordered (the device pool, engine.hip): freed without a device-wide wait
-    HIP_TRY(e, hipMallocAsync((void **)&g.d, s.fill, p->copy));
+    const uint64_t need = (s.fill + 255) & ~255ull;
+    if (p->arenas.empty() || p->arenas.back().cap - p->arenas.back().used < need) {
+      // stream-ordered (the device pool, engine.hip): freed without a device-wide wait
+      uint64_t cap = p->arenas.empty() ? p->cap : std::min<uint64_t>(2 * p->arenas.back().cap, 1ull << 30);
+      if (cap < need) cap = need;
+      ngpu_pack::Arena ar;
+      HIP_TRY(e, hipMallocAsync((void **)&ar.d, cap, p->copy));
+      ar.cap = cap;
+      p->arenas.push_back(ar);
+    }
+    ngpu_pack::Arena &ar = p->arenas.back();
+    g.d = ar.d + ar.used;
+    ar.used += need;
     g.base = s.base;
     g.a = a;
     g.b = b;
