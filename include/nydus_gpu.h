@@ -230,7 +230,10 @@ int ngpu_dict_open(ngpu_engine *eng, const char *path, ngpu_dict **out);
 int ngpu_dict_create(ngpu_engine *eng, const void *records, uint64_t n,
                      const void *blob_table, uint32_t n_blobs, ngpu_dict **out);
 /* From device-resident arrays (entry order = table order), e.g. a 200M-entry
- * dict built on the GPU.  d_uoff (u64 uncompressed offsets) may be NULL. */
+ * dict built on the GPU.  d_uoff (u64 uncompressed offsets) may be NULL.
+ * The build runs on a stream of the library's own and returns when it is
+ * done; it does not wait for the caller's streams, so the arrays must be
+ * complete when the call is made (synchronise the stream that wrote them). */
 int ngpu_dict_create_device(ngpu_engine *eng, const uint8_t *d_digests, const uint32_t *d_usize,
                             const uint32_t *d_blob_index, const uint32_t *d_chunk_index,
                             const uint64_t *d_uoff, uint64_t n, uint32_t n_blobs,

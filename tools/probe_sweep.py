@@ -30,6 +30,7 @@ def main():
         us = torch.full((m,), 1 << 20, dtype=torch.int32, device="cuda")
         bl = torch.zeros(m, dtype=torch.int32, device="cuda")
         ix = torch.arange(m, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()  # the build reads the arrays from its own stream
         eng.dict_load_device(dd.data_ptr(), us.data_ptr(), bl.data_ptr(), ix.data_ptr(), m, 1)
         q = torch.empty((Q, 32), dtype=torch.uint8, device="cuda")
         q.random_(0, 256, generator=g)
