@@ -151,15 +151,18 @@ def test_first_call_of_fresh_engines_on_nonblocking_streams(oracle):
     zeroed its new stats words with hipMemset, which is asynchronous to the
     host and runs on the null stream -- unordered with a caller's
     non-blocking stream.  Landing after the first digest kernel wrote its
-    counters, it zeroed b3_tree's queue count and the multi-leaf chunks kept
-    no digest (tools/step_diag.py reproduced it on 2 of 3 first node steps
-    over 8 streams).  Sixteen fresh engines, each called once on its own torch
-    (non-blocking) stream with no synchronisation between the enqueues: every
-    digest must equal the oracle's and no guard may fire."""
+    counters and before b3_tree read them, it zeroed the tree queue count and
+    the multi-leaf chunks kept no digest (tools/step_diag.py reproduced it on
+    2 of 3 first node steps over 8 streams).  Here the null stream is kept
+    busy by a fill of a different length before each fresh engine's first
+    call on its own non-blocking stream, so a queued memset lands at a
+    different point of that call's digest each time: every digest must equal
+    the oracle's and no guard may fire (scripts/gpu_race_ab.sh runs this
+    against the pre-fix build)."""
     import torch
     rng = np.random.default_rng(2024)
     cs = 0x10000
-    total = 6 << 20
+    total = 24 << 20  # quad path, planning in the leaf kernel: b3_tree reads the queue count
     data = rng.integers(0, 256, total, dtype=np.uint8)
     ch = np.zeros(total // cs, nydus_gpu.CHUNK_DTYPE)
     ch["offset"] = np.arange(len(ch)) * cs
@@ -169,21 +172,26 @@ def test_first_call_of_fresh_engines_on_nonblocking_streams(oracle):
     dig = oracle.digest_chunks(data.tobytes(), ch.view(oracle.CHUNK_DTYPE), "blake3")
     d_data = torch.from_numpy(data).cuda()
     d_ch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+    big = torch.empty(2 << 30, dtype=torch.uint8, device="cuda")
+    assert torch.cuda.current_stream().cuda_stream == 0  # fills go to the null stream
+    fills = [0] + [(1 << 20) << k for k in range(12)]  # 0, 1 MiB .. 2 GiB
     engines, outs, streams = [], [], []
     try:
-        for _ in range(16):
+        for _ in fills:
             engines.append(nydus_gpu.Engine(device=0, chunk_size=cs))
             outs.append(torch.zeros(len(ch) * 64, dtype=torch.uint8, device="cuda"))
             streams.append(torch.cuda.Stream())
         torch.cuda.synchronize()
-        for e, o, s in zip(engines, outs, streams):
+        for e, o, s, f in zip(engines, outs, streams, fills):
+            if f:
+                big[:f].fill_(f & 0xFF)  # null stream busy for ~f / 4 TB/s
             e.process_device(d_data.data_ptr(), d_data.numel(), d_ch.data_ptr(), len(ch), o.data_ptr(),
                              stream=s.cuda_stream)
         torch.cuda.synchronize()
         for k, (e, o) in enumerate(zip(engines, outs)):
-            e.device_status()
             got = o.cpu().numpy().view(nydus_gpu.RESULT_DTYPE)
-            assert np.array_equal(got["digest"], dig), k
+            assert np.array_equal(got["digest"], dig), (k, fills[k])
+            e.device_status()
     finally:
         for e in engines:
             e.close()
