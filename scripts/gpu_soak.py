@@ -125,7 +125,7 @@ def concurrent(threads, cases, seed):
                 eng, chunk, dg, lanes, base, recs, d = shared[int(rng.integers(0, len(shared)))]
                 plant = base if rng.random() < 0.3 else ()  # the dict layer's files: DICT hits
                 tar = random_tar(rng, chunk, first=plant)
-                op = int(rng.integers(0, 5))
+                op = int(rng.integers(0, 6))
                 tag = f"thread {tid} case {case} op {op} (chunk {chunk:#x}, {dg}, lanes {lanes})"
                 if op == 4:  # node Pack against the partitioned dict
                     plant = nbase if rng.random() < 0.5 else ()
@@ -136,6 +136,22 @@ def concurrent(threads, cases, seed):
                     check(tag + " node", ch, out, tar, 0x10000, "blake3", nrecs)
                     with mu:
                         counts["node_calls"] += 1
+                elif op == 5:  # early emission (ngpu_pack_set_output, the mirrors' Pack)
+                    import hashlib
+                    import io
+                    sink = io.BytesIO()
+                    use = d if rng.random() < 0.5 else None
+                    w = eng.pack(dict=use, retain=True)
+                    w.set_output(sink, compressor=str(rng.choice(["none", "zstd"])))
+                    pos = 0
+                    while pos < len(tar):
+                        k = int(rng.integers(1, 3 << 20))
+                        w.write(tar[pos:pos + k])
+                        pos += k
+                    ch, out, _, info = w.finish(None)
+                    check(tag + " early", ch, out, tar, chunk, dg, recs if use is not None else None)
+                    if hashlib.sha256(sink.getvalue()).hexdigest() != info["stream_digest"]:
+                        raise AssertionError(f"{tag}: early stream digest differs from its bytes")
                 elif op == 0:
                     ch, out, _ = eng.pack_tar(tar)
                     check(tag, ch, out, tar, chunk, dg)
