@@ -109,20 +109,43 @@ __device__ __forceinline__ ngpu_dict_hit dict_hit_of(const DictDevice &dict, uin
   return ngpu_dict_hit{f.w, f.z, f.y, f.x, uo};
 }
 
-// Look n digests (byte stride `stride`) up in the dict.
-__global__ void dict_probe_records(const uint8_t *__restrict__ digests, uint64_t stride,
-                                   uint64_t n, DictDevice dict,
-                                   ngpu_dict_hit *__restrict__ hits) {
-  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (q >= n) return;
-  uint32_t e = kNone;
-  if (dict.m) {
-    const uint4 *p = reinterpret_cast<const uint4 *>(digests + q * stride);
-    const uint4 a = p[0], b = p[1];
-    const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    e = dict_lookup(dict, d);
+// Look n digests (byte stride `stride`) up in the dict.  The 24-B hits of a
+// workgroup are staged in LDS and leave as lane-contiguous 16-B stores, so
+// each store instruction writes whole 128-B lines: a lane's own 24-B record
+// write covers no line in one instruction, and the L2 then read every hit
+// line from HBM before merging (~0.19 of the probe's ~1.96 line requests;
+// tools/probe_sweep.py).  256 threads per workgroup (launch_dict_probe).
+__global__ __launch_bounds__(256) void dict_probe_records(const uint8_t *__restrict__ digests,
+                                                          uint64_t stride, uint64_t n,
+                                                          DictDevice dict,
+                                                          ngpu_dict_hit *__restrict__ hits) {
+  __shared__ uint4 stage[256 * sizeof(ngpu_dict_hit) / 16];
+  const uint64_t q0 = blockIdx.x * 256ull;
+  const uint64_t q = q0 + threadIdx.x;
+  if (q < n) {
+    uint32_t e = kNone;
+    if (dict.m) {
+      const uint4 *p = reinterpret_cast<const uint4 *>(digests + q * stride);
+      const uint4 a = p[0], b = p[1];
+      const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      e = dict_lookup(dict, d);
+    }
+    reinterpret_cast<ngpu_dict_hit *>(stage)[threadIdx.x] = dict_hit_of(dict, e);
   }
-  hits[q] = dict_hit_of(dict, e);
+  __syncthreads();
+  const uint64_t m = n - q0 < 256 ? n - q0 : 256;  // this workgroup's hits
+  const uint32_t bytes = (uint32_t)m * (uint32_t)sizeof(ngpu_dict_hit);
+  uint8_t *dst = reinterpret_cast<uint8_t *>(hits + q0);
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    for (uint32_t i = threadIdx.x; i < bytes / 16; i += 256)
+      reinterpret_cast<uint4 *>(dst)[i] = stage[i];
+    if ((bytes & 15) && threadIdx.x == 0)  // an odd count leaves one 8-B half
+      reinterpret_cast<uint2 *>(dst + (bytes & ~15u))[0] =
+          reinterpret_cast<const uint2 *>(stage)[(bytes & ~15u) / 8];
+  } else {  // (hit arrays from hipMalloc / torch are 256-B aligned)
+    for (uint32_t i = threadIdx.x; i < bytes / 8; i += 256)
+      reinterpret_cast<uint2 *>(dst)[i] = reinterpret_cast<const uint2 *>(stage)[i];
+  }
 }
 
 // The wavefront-cooperative form of the same lookup (the north star's
