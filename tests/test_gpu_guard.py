@@ -157,8 +157,11 @@ def test_first_call_of_fresh_engines_on_nonblocking_streams(oracle):
     busy by a fill of a different length before each fresh engine's first
     call on its own non-blocking stream, so a queued memset lands at a
     different point of that call's digest each time: every digest must equal
-    the oracle's and no guard may fire (scripts/gpu_race_ab.sh runs this
-    against the pre-fix build)."""
+    the oracle's and no guard may fire.  (On this pool the pre-fix build
+    passes this test too -- the null stream and a caller's stream may share a
+    hardware queue, which orders them; the reproducer is the first 8-stream
+    node step, test_gpu_node.py::test_node_step_all_devices_at_once_vs_oracle[8]
+    and scripts/gpu_race_ab.sh.)"""
     import torch
     rng = np.random.default_rng(2024)
     cs = 0x10000
