@@ -148,6 +148,67 @@ __global__ __launch_bounds__(256) void dict_probe_records(const uint8_t *__restr
   }
 }
 
+// A/B variants of the same probe (NGPU_PROBE_VARIANT, read per call; bench /
+// tools/probe_sweep.py): where do the line requests beyond query + slot +
+// record come from?  QV: the workgroup's queries (stride 32) are read into
+// LDS with lane-contiguous 16-B loads -- one instruction per line -- instead
+// of two 16-B loads per lane, each touching every query line of the wave.
+// RV: a tag-matched record is read and compared 16 B at a time (the second
+// half only if the first matched) instead of two loads issued together.
+template <int QV, int RV>
+__global__ __launch_bounds__(256) void dict_probe_variant(const uint8_t *__restrict__ digests,
+                                                          uint64_t stride, uint64_t n,
+                                                          DictDevice dict,
+                                                          ngpu_dict_hit *__restrict__ hits) {
+  __shared__ uint4 qs[QV ? 512 : 1];
+  const uint64_t q0 = blockIdx.x * 256ull;
+  const uint64_t q = q0 + threadIdx.x;
+  uint32_t d[8] = {};
+  if (QV && stride == 32) {
+    const uint64_t m = n - q0 < 256 ? n - q0 : 256;
+    const uint4 *src = reinterpret_cast<const uint4 *>(digests + q0 * 32);
+    for (uint32_t i = threadIdx.x; i < 2 * m; i += 256) qs[i] = src[i];
+    __syncthreads();
+    if (q < n) {
+      const uint4 a = qs[2 * threadIdx.x], b = qs[2 * threadIdx.x + 1];
+      d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+    }
+  } else if (q < n) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(digests + q * stride);
+    const uint4 a = p[0], b = p[1];
+    d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+  }
+  if (q >= n) return;
+  uint32_t e = kNone;
+  if (dict.m) {
+    const uint32_t tag = digest_tag(d);
+    for (uint64_t pos = digest_bucket(d) & dict.mask;; pos = (pos + 1) & dict.mask) {
+      const uint64_t sv = dict.table[pos];
+      if (sv == kEmpty) break;
+      if ((uint32_t)(sv >> 32) != tag) continue;
+      const uint4 *r = reinterpret_cast<const uint4 *>(dict.rec + (uint32_t)sv);
+      bool eq;
+      if (RV) {
+        const uint4 a = r[0];
+        eq = ((a.x ^ d[0]) | (a.y ^ d[1]) | (a.z ^ d[2]) | (a.w ^ d[3])) == 0;
+        if (eq) {
+          const uint4 b = r[1];
+          eq = ((b.x ^ d[4]) | (b.y ^ d[5]) | (b.z ^ d[6]) | (b.w ^ d[7])) == 0;
+        }
+      } else {
+        const uint4 a = r[0], b = r[1];
+        eq = ((a.x ^ d[0]) | (a.y ^ d[1]) | (a.z ^ d[2]) | (a.w ^ d[3]) | (b.x ^ d[4]) |
+              (b.y ^ d[5]) | (b.z ^ d[6]) | (b.w ^ d[7])) == 0;
+      }
+      if (eq) {
+        e = (uint32_t)sv;
+        break;
+      }
+    }
+  }
+  hits[q] = dict_hit_of(dict, e);
+}
+
 // The wavefront-cooperative form of the same lookup (the north star's
 // "chunk-dict hash table ... probed with wavefront-cooperative open
 // addressing"; A/B against dict_probe_records, NGPU_PROBE_COOP=1): 16 lanes
@@ -1047,8 +1108,17 @@ void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
                        digests, stride, n, dict, hits);
     return;
   }
-  hipLaunchKernelGGL(dict_probe_records, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                     digests, stride, n, dict, hits);
+  const char *var = getenv("NGPU_PROBE_VARIANT");
+  const int v = var ? atoi(var) : 0;
+  const dim3 g((unsigned)((n + 255) / 256));
+  switch (v) {
+    case 1: hipLaunchKernelGGL((dict_probe_variant<1, 0>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    case 2: hipLaunchKernelGGL((dict_probe_variant<0, 1>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    case 3: hipLaunchKernelGGL((dict_probe_variant<1, 1>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    case 4: hipLaunchKernelGGL((dict_probe_variant<0, 0>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    default: break;
+  }
+  hipLaunchKernelGGL(dict_probe_records, g, dim3(256), 0, s, digests, stride, n, dict, hits);
 }
 
 // ---- node dict exchange (node.hip) -------------------------------------------

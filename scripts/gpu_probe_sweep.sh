@@ -1,20 +1,21 @@
 #!/bin/bash
 # Probe line requests by dict size (tools/probe_sweep.py): a timing run, then one
 # request-size PMC pass (kernel trace only); per-size averages by launch order.
-# usage: scripts/gpu_probe_sweep.sh TAG
+# usage: scripts/gpu_probe_sweep.sh TAG [SIZES_M]   (NGPU_PROBE_VARIANT passes through)
 set -u
 TAG=${1:-psweep}
+SIZES=${2:-1,16,64,200}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 ok() { local rc=$1 what=$2; echo "$what rc=$rc"; if [ "$rc" -ne 0 ]; then echo "stopping after $what"; exit "$rc"; fi; }
 cd "$ROOT"
-timeout -k 10 300 python3 tools/probe_sweep.py 16 1,16,64,200 > "$OUT/sweep.jsonl" 2> "$OUT/sweep.err"
+timeout -k 10 300 python3 tools/probe_sweep.py 16 $SIZES > "$OUT/sweep.jsonl" 2> "$OUT/sweep.err"
 ok $? sweep
 cat "$OUT/sweep.jsonl"
 cd /tmp
-timeout -k 10 400 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --kernel-include-regex dict_probe_records --output-format csv -d "$OUT/pmc" -o pmc -- python3 "$ROOT/tools/probe_sweep.py" 16 1,16,64,200 > "$OUT/pmc.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --kernel-include-regex dict_probe_records --output-format csv -d "$OUT/pmc" -o pmc -- python3 "$ROOT/tools/probe_sweep.py" 16 $SIZES > "$OUT/pmc.log" 2>&1
 ok $? pmc
 python3 - "$OUT" <<'PY'
 import csv, glob, json, sys
