@@ -16,20 +16,34 @@ from collections import defaultdict
 
 def main():
     out, pat, dirs = sys.argv[1], re.compile(sys.argv[2]), sys.argv[3:]
-    vals = defaultdict(list)
-    durs = []
-    name = None
+    rows = []
     for d in dirs:
         for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(f)):
                 if not pat.search(r["Kernel_Name"]):
                     continue
-                m = re.search(r"(b3_groups<[^>]*>|b3_quad_leaves|sha256_\w+)", r["Kernel_Name"])
-                name = m.group(1) if m else r["Kernel_Name"]
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-                durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+                m = re.search(r"(b3_groups<[^>]*>|b3_quad_\w+|sha256_\w+)", r["Kernel_Name"])
+                rows.append((m.group(1) if m else r["Kernel_Name"], r["Counter_Name"],
+                             float(r["Counter_Value"]),
+                             (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+    # the workload's own launches only: a bench also runs the same kernels on
+    # small setup inputs (C5's shared pool, dict fixtures), orders of magnitude
+    # shorter; keep the launches within 2x of the longest
+    top = max((r[3] for r in rows), default=0.0)
+    vals = defaultdict(list)
+    durs = []
+    name = None
+    dropped = 0
+    for nm, cn, v, du in rows:
+        if du < 0.5 * top:
+            dropped += 1
+            continue
+        name = nm
+        vals[cn].append(v)
+        durs.append(du)
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
     res = {"kernel": name, "launches_sampled": {k: len(v) for k, v in vals.items()},
+           "short_launch_rows_dropped": dropped,
            "avg_duration_ms_profiled": round(sum(durs) / max(1, len(durs)), 4), "counters": avg}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         res["traffic_bytes"] = int((2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024)
