@@ -353,6 +353,20 @@ def probe_bench(torch, nydus_gpu, eng, dd, Q, build_s, reps=5):
               "traffic_gbs": round(traffic / t / 1e9, 1),
               "traffic_frac": round(traffic / t / PEAK_HBM, 4),
               "lines_per_probe": round(traffic / 128 / Q, 2)}
+        # the measured ceiling of random 128-B line reads on this chip
+        # (tools/random_calib.hip: one random 8-B read, or a slot read and a
+        # dependent 64-B record read, per thread over a table >= 4 GiB; the
+        # request counters read exactly 1.000 / 2.000 lines per thread there)
+        cal, csrc = newest_profile("random_calib.json")
+        pm, _ = newest_profile("pmc_req_probe.json")
+        if cal and pm and "read_request_bytes" in pm:
+            big = [c for c in cal if c["table_bytes"] >= 4 << 30 and c["mode"] in (0, 3)]
+            if big:
+                ceil = max(c["reads"] * c["lines_per_read"] / (c["best_ms"] / 1e3) for c in big)
+                lines_s = pm["read_request_bytes"] / 128 / t
+                tr["random_line_ceiling"] = {
+                    "glines_s": round(ceil / 1e9, 2), "probe_glines_s": round(lines_s / 1e9, 2),
+                    "frac": round(lines_s / ceil, 4), "source": csrc}
     return {"kernel": "dict_probe_records", "queries": Q, "hits": nhit, "dict_entries": m, **tr,
             "ms": round(t * 1e3, 4), "gprobes_s": round(Q / t / 1e9, 2),
             "bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": round(PEAK_HBM / 1e9, 1),
