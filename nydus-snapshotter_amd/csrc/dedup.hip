@@ -109,6 +109,30 @@ __device__ __forceinline__ ngpu_dict_hit dict_hit_of(const DictDevice &dict, uin
   return ngpu_dict_hit{f.w, f.z, f.y, f.x, uo};
 }
 
+// Lookup + hit in one pass: at a tag match the whole 64-B record is read (its
+// four loads issued together), compared, and the hit built from registers.
+// dict_hit_of(dict_lookup()) re-read the record's second half after the
+// probe loop, i.e. after the wave's LONGEST chain had finished; by then the
+// line had often left the L2 (random lines turn the L2 over in a few us) and
+// the re-read went to HBM: +0.35 line per probe at 30 % hits (1.94 -> 1.60;
+// dict_probe_variant RV 2..4 took the probe apart, tools/probe_sweep.py).
+__device__ __forceinline__ ngpu_dict_hit dict_find(const DictDevice &dict, const uint32_t d[8]) {
+  const uint32_t tag = digest_tag(d);
+  for (uint64_t p = digest_bucket(d) & dict.mask;; p = (p + 1) & dict.mask) {
+    const uint64_t s = dict.table[p];
+    if (s == kEmpty) break;
+    if ((uint32_t)(s >> 32) != tag) continue;
+    const uint32_t e = (uint32_t)s;
+    const uint4 *r = reinterpret_cast<const uint4 *>(dict.rec + e);
+    const uint4 a = r[0], b = r[1], f = r[2];
+    const uint64_t uo = dict.rec[e].uoff;
+    if (((a.x ^ d[0]) | (a.y ^ d[1]) | (a.z ^ d[2]) | (a.w ^ d[3]) | (b.x ^ d[4]) |
+         (b.y ^ d[5]) | (b.z ^ d[6]) | (b.w ^ d[7])) == 0)
+      return ngpu_dict_hit{f.w, f.z, f.y, f.x, uo};  // gid, index, blob, usize
+  }
+  return ngpu_dict_hit{kNone, 0, 0, 0, 0};
+}
+
 // Look n digests (byte stride `stride`) up in the dict.  The 24-B hits of a
 // workgroup are staged in LDS and leave as lane-contiguous 16-B stores, so
 // each store instruction writes whole 128-B lines: a lane's own 24-B record
@@ -123,14 +147,14 @@ __global__ __launch_bounds__(256) void dict_probe_records(const uint8_t *__restr
   const uint64_t q0 = blockIdx.x * 256ull;
   const uint64_t q = q0 + threadIdx.x;
   if (q < n) {
-    uint32_t e = kNone;
+    ngpu_dict_hit h{kNone, 0, 0, 0, 0};
     if (dict.m) {
       const uint4 *p = reinterpret_cast<const uint4 *>(digests + q * stride);
       const uint4 a = p[0], b = p[1];
       const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      e = dict_lookup(dict, d);
+      h = dict_find(dict, d);
     }
-    reinterpret_cast<ngpu_dict_hit *>(stage)[threadIdx.x] = dict_hit_of(dict, e);
+    reinterpret_cast<ngpu_dict_hit *>(stage)[threadIdx.x] = h;
   }
   __syncthreads();
   const uint64_t m = n - q0 < 256 ? n - q0 : 256;  // this workgroup's hits
@@ -155,6 +179,10 @@ __global__ __launch_bounds__(256) void dict_probe_records(const uint8_t *__restr
 // of two 16-B loads per lane, each touching every query line of the wave.
 // RV: a tag-matched record is read and compared 16 B at a time (the second
 // half only if the first matched) instead of two loads issued together.
+// RV 2..4 take the probe apart (their decisions are NOT the dict's: request
+// counting only, never parity): 2 trusts the tag (no compare, the hit record
+// still read), 3 trusts the tag and reads no record, 4 reads only the home
+// slot (no chain, no record).
 template <int QV, int RV>
 __global__ __launch_bounds__(256) void dict_probe_variant(const uint8_t *__restrict__ digests,
                                                           uint64_t stride, uint64_t n,
@@ -184,11 +212,19 @@ __global__ __launch_bounds__(256) void dict_probe_variant(const uint8_t *__restr
     const uint32_t tag = digest_tag(d);
     for (uint64_t pos = digest_bucket(d) & dict.mask;; pos = (pos + 1) & dict.mask) {
       const uint64_t sv = dict.table[pos];
+      if (RV == 4) {
+        if (sv != kEmpty && (uint32_t)(sv >> 32) == tag) e = (uint32_t)sv;
+        break;
+      }
       if (sv == kEmpty) break;
       if ((uint32_t)(sv >> 32) != tag) continue;
+      if (RV == 2 || RV == 3) {
+        e = (uint32_t)sv;
+        break;
+      }
       const uint4 *r = reinterpret_cast<const uint4 *>(dict.rec + (uint32_t)sv);
       bool eq;
-      if (RV) {
+      if (RV == 1) {
         const uint4 a = r[0];
         eq = ((a.x ^ d[0]) | (a.y ^ d[1]) | (a.z ^ d[2]) | (a.w ^ d[3])) == 0;
         if (eq) {
@@ -206,7 +242,10 @@ __global__ __launch_bounds__(256) void dict_probe_variant(const uint8_t *__restr
       }
     }
   }
-  hits[q] = dict_hit_of(dict, e);
+  if (RV >= 3)
+    hits[q] = ngpu_dict_hit{e, 0, 0, 0, 0};
+  else
+    hits[q] = dict_hit_of(dict, e);
 }
 
 // The wavefront-cooperative form of the same lookup (the north star's
@@ -450,7 +489,7 @@ __device__ __forceinline__ void probe_insert_item(
     if (hits) {
       h = hits[c];
     } else if (dict.m) {
-      h = dict_hit_of(dict, dict_lookup(dict, d));
+      h = dict_find(dict, d);
     }
   }
   const bool is_dict = live && h.entry != kNone &&
@@ -909,7 +948,7 @@ __global__ __launch_bounds__(T) void dedup_small_lds(
     const uint32_t len = chunks[c].length;
     ngpu_dict_hit h{kNone, 0, 0, 0, 0};
     if (hits) h = hits[c];
-    else if (dict.m) h = dict_hit_of(dict, dict_lookup(dict, dg));
+    else if (dict.m) h = dict_find(dict, dg);
     ngpu_result &r = out[c];
     if (h.entry != kNone && (h.usize == 0 || h.usize == len) && h.blob < n_blobs) {
       len_s[c] = len | kDictBit;
@@ -1116,6 +1155,9 @@ void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
     case 2: hipLaunchKernelGGL((dict_probe_variant<0, 1>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
     case 3: hipLaunchKernelGGL((dict_probe_variant<1, 1>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
     case 4: hipLaunchKernelGGL((dict_probe_variant<0, 0>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    case 5: hipLaunchKernelGGL((dict_probe_variant<0, 2>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    case 6: hipLaunchKernelGGL((dict_probe_variant<0, 3>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    case 7: hipLaunchKernelGGL((dict_probe_variant<0, 4>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
     default: break;
   }
   hipLaunchKernelGGL(dict_probe_records, g, dim3(256), 0, s, digests, stride, n, dict, hits);
@@ -1146,13 +1188,13 @@ __global__ void dict_probe_owned(const uint8_t *__restrict__ q, uint64_t n, uint
   const uint4 *p = reinterpret_cast<const uint4 *>(q + 32 * i);
   const uint4 a = p[0];
   if (owner_of(a.x, W) != owner) return;  // another part answers this one
-  uint32_t e = kNone;
+  ngpu_dict_hit h{kNone, 0, 0, 0, 0};
   if (dict.m) {
     const uint4 b = p[1];
     const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    e = dict_lookup(dict, d);
+    h = dict_find(dict, d);
   }
-  hits[i] = dict_hit_of(dict, e);
+  hits[i] = h;
 }
 
 __global__ void hits_merge(const uint8_t *__restrict__ q, uint64_t n, uint32_t W,
@@ -1241,13 +1283,13 @@ __global__ __launch_bounds__(256) void dict_probe_routed(const uint8_t *__restri
   const uint64_t off = s_off, m = s_n;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < m; i += gridDim.x * 256ull) {
     const uint4 *p = reinterpret_cast<const uint4 *>(q + 32 * (off + i));
-    uint32_t e = kNone;
+    ngpu_dict_hit h{kNone, 0, 0, 0, 0};
     if (dict.m) {
       const uint4 a = p[0], b = p[1];
       const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      e = dict_lookup(dict, d);
+      h = dict_find(dict, d);
     }
-    hits[rows[off + i]] = dict_hit_of(dict, e);
+    hits[rows[off + i]] = h;
   }
 }
 
