@@ -172,6 +172,94 @@ __global__ __launch_bounds__(256) void dict_probe_records(const uint8_t *__restr
   }
 }
 
+// K queries per thread, their probe chains stepped in lockstep: each step
+// issues the K slot loads (and the K record loads of tag matches) together,
+// so a wave has K independent random requests in flight where
+// dict_probe_records has one.  Same decisions as dict_find (slots in chain
+// order, first equal record, stop at an empty slot).  Hits staged as there.
+template <int K>
+__global__ __launch_bounds__(256) void dict_probe_multi(const uint8_t *__restrict__ digests,
+                                                        uint64_t stride, uint64_t n,
+                                                        DictDevice dict,
+                                                        ngpu_dict_hit *__restrict__ hits) {
+  __shared__ uint4 stage[K * 256 * sizeof(ngpu_dict_hit) / 16];
+  const uint64_t q0 = blockIdx.x * (256ull * K);
+  uint32_t d[K][8], tag[K];
+  uint64_t pos[K];
+  bool live[K];
+  ngpu_dict_hit h[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint64_t q = q0 + threadIdx.x + 256u * j;
+    live[j] = q < n && dict.m;
+    h[j] = ngpu_dict_hit{kNone, 0, 0, 0, 0};
+    uint4 a = make_uint4(0, 0, 0, 0), b = a;
+    if (live[j]) {
+      const uint4 *p = reinterpret_cast<const uint4 *>(digests + q * stride);
+      a = p[0];
+      b = p[1];
+    }
+    d[j][0] = a.x; d[j][1] = a.y; d[j][2] = a.z; d[j][3] = a.w;
+    d[j][4] = b.x; d[j][5] = b.y; d[j][6] = b.z; d[j][7] = b.w;
+    tag[j] = digest_tag(d[j]);
+    pos[j] = digest_bucket(d[j]) & dict.mask;
+  }
+  for (;;) {
+    uint64_t sv[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sv[j] = live[j] ? dict.table[pos[j]] : kEmpty;
+    bool cand[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (sv[j] == kEmpty) live[j] = false;
+      cand[j] = live[j] && (uint32_t)(sv[j] >> 32) == tag[j];
+    }
+    uint4 ra[K], rb[K], rf[K];
+    uint64_t ru[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (cand[j]) {
+        const uint4 *r = reinterpret_cast<const uint4 *>(dict.rec + (uint32_t)sv[j]);
+        ra[j] = r[0];
+        rb[j] = r[1];
+        rf[j] = r[2];
+        ru[j] = dict.rec[(uint32_t)sv[j]].uoff;
+      }
+    }
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (cand[j] && ((ra[j].x ^ d[j][0]) | (ra[j].y ^ d[j][1]) | (ra[j].z ^ d[j][2]) |
+                      (ra[j].w ^ d[j][3]) | (rb[j].x ^ d[j][4]) | (rb[j].y ^ d[j][5]) |
+                      (rb[j].z ^ d[j][6]) | (rb[j].w ^ d[j][7])) == 0) {
+        h[j] = ngpu_dict_hit{rf[j].w, rf[j].z, rf[j].y, rf[j].x, ru[j]};
+        live[j] = false;
+      }
+      if (live[j]) pos[j] = (pos[j] + 1) & dict.mask;
+      any |= live[j];
+    }
+    if (!any) break;
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    if (q0 + threadIdx.x + 256u * j < n)
+      reinterpret_cast<ngpu_dict_hit *>(stage)[threadIdx.x + 256u * j] = h[j];
+  __syncthreads();
+  const uint64_t m = n - q0 < 256ull * K ? n - q0 : 256ull * K;
+  const uint32_t bytes = (uint32_t)m * (uint32_t)sizeof(ngpu_dict_hit);
+  uint8_t *dst = reinterpret_cast<uint8_t *>(hits + q0);
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    for (uint32_t i = threadIdx.x; i < bytes / 16; i += 256)
+      reinterpret_cast<uint4 *>(dst)[i] = stage[i];
+    if ((bytes & 15) && threadIdx.x == 0)
+      reinterpret_cast<uint2 *>(dst + (bytes & ~15u))[0] =
+          reinterpret_cast<const uint2 *>(stage)[(bytes & ~15u) / 8];
+  } else {
+    for (uint32_t i = threadIdx.x; i < bytes / 8; i += 256)
+      reinterpret_cast<uint2 *>(dst)[i] = reinterpret_cast<const uint2 *>(stage)[i];
+  }
+}
+
 // A/B variants of the same probe (NGPU_PROBE_VARIANT, read per call; bench /
 // tools/probe_sweep.py): where do the line requests beyond query + slot +
 // record come from?  QV: the workgroup's queries (stride 32) are read into
@@ -1158,6 +1246,8 @@ void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
     case 5: hipLaunchKernelGGL((dict_probe_variant<0, 2>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
     case 6: hipLaunchKernelGGL((dict_probe_variant<0, 3>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
     case 7: hipLaunchKernelGGL((dict_probe_variant<0, 4>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    case 8: hipLaunchKernelGGL((dict_probe_multi<2>), dim3((unsigned)((n + 511) / 512)), dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    case 9: hipLaunchKernelGGL((dict_probe_multi<4>), dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, s, digests, stride, n, dict, hits); return;
     default: break;
   }
   hipLaunchKernelGGL(dict_probe_records, g, dim3(256), 0, s, digests, stride, n, dict, hits);
