@@ -491,3 +491,58 @@ def test_aligned_chunk_v5(oracle):
         finally:
             eng.close()
         _same(out, dig, exp, aligned)
+
+
+def test_probe_walks_tag_collisions_and_keeps_first_row():
+    """The probe's record compare (dict_find, dedup.hip): entries sharing the
+    bucket words AND the tag word (digest words 0-2) but not the rest sit in
+    one probe chain with equal tags, so the probe must read and compare each
+    record and walk past the unequal ones; a digest listed twice resolves to
+    its earlier row (ht_insert_min; the oracle's first-occurrence rule,
+    oracle_py.dedup); a query that shares words 0-2 with the chain but equals
+    none of it walks the chain to the empty slot (a miss).  Expected values
+    are computed here by a plain scan of the table rows."""
+    import torch
+    rng = np.random.default_rng(0x7A6)
+    m = 4096
+    dd = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+    coll = [100, 200, 300, 400, 500, 600, 700, 800, 1000, 1100, 1200, 1300]
+    for r in coll:
+        dd[r, :12] = dd[100, :12]           # same bucket words and tag, tails differ
+    dd[900] = dd[300]                        # a later duplicate: row 300 wins
+    dd[50] = dd[700]                         # an earlier duplicate: row 50 wins
+    miss_chain = dd[100].copy()
+    miss_chain[12:] = rng.integers(0, 256, 20, dtype=np.uint8)
+    near = dd[400].copy()
+    near[31] ^= 1                            # equal in 31 bytes, bucket and tag included
+    q = np.stack([dd[r] for r in coll] + [dd[900], dd[50], miss_chain, near] +
+                 [rng.integers(0, 256, 32, dtype=np.uint8) for _ in range(8)] +
+                 [dd[r] for r in rng.choice(m, 64, replace=False)])
+    exp = []
+    for row in q:
+        eq = np.flatnonzero((dd == row).all(axis=1))
+        exp.append(int(eq[0]) if len(eq) else nydus_gpu.MISS)
+    exp = np.array(exp, np.uint32)
+    idx = (np.arange(m, dtype=np.int32) * 7 + 3)
+    usz = (np.arange(m, dtype=np.int32) % 5 + 1) * 4096
+    blb = (np.arange(m, dtype=np.int32) % 3)
+    d_dd = torch.from_numpy(dd).cuda()
+    d_us, d_bl, d_ix = (torch.from_numpy(a).cuda() for a in (usz, blb, idx))
+    d_q = torch.from_numpy(q).cuda()
+    d_hits = torch.zeros(len(q) * 24, dtype=torch.uint8, device="cuda")
+    eng = nydus_gpu.Engine(chunk_size=0x10000)
+    try:
+        torch.cuda.synchronize()             # the build reads the arrays from its own stream
+        eng.dict_load_device(d_dd.data_ptr(), d_us.data_ptr(), d_bl.data_ptr(), d_ix.data_ptr(), m, 3)
+        eng.dict_probe_device(d_q.data_ptr(), 32, len(q), d_hits.data_ptr(),
+                              stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        eng.close()
+    hits = d_hits.cpu().numpy().view(nydus_gpu.HIT_DTYPE)
+    assert np.array_equal(hits["entry"], exp), (hits["entry"][:20], exp[:20])
+    hit = exp != nydus_gpu.MISS
+    assert hit.sum() == len(coll) + 2 + 64 and not hit[len(coll) + 2:len(coll) + 12].any()
+    assert np.array_equal(hits["index"][hit], idx[exp[hit]].astype(np.uint32))
+    assert np.array_equal(hits["usize"][hit], usz[exp[hit]].astype(np.uint32))
+    assert np.array_equal(hits["blob"][hit], blb[exp[hit]].astype(np.uint32))
