@@ -260,6 +260,84 @@ __global__ __launch_bounds__(256) void dict_probe_multi(const uint8_t *__restric
   }
 }
 
+// dict_probe_multi with the queries kept in LDS instead of registers (the
+// compare reads them back), so K = 2 fits 8 waves per SIMD without spills.
+template <int K>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void
+dict_probe_multi_lds(const uint8_t *__restrict__ digests, uint64_t stride, uint64_t n,
+                     DictDevice dict, ngpu_dict_hit *__restrict__ hits) {
+  __shared__ uint4 qs[K * 256 * 2];  // the queries, then (after a barrier) the staged hits
+  uint4 *stage = qs;
+  const uint64_t q0 = blockIdx.x * (256ull * K);
+  uint32_t tag[K];
+  uint64_t pos[K];
+  bool live[K];
+  ngpu_dict_hit h[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint32_t t = threadIdx.x + 256u * j;
+    const uint64_t q = q0 + t;
+    live[j] = q < n && dict.m;
+    h[j] = ngpu_dict_hit{kNone, 0, 0, 0, 0};
+    uint4 a = make_uint4(0, 0, 0, 0), b = a;
+    if (live[j]) {
+      const uint4 *p = reinterpret_cast<const uint4 *>(digests + q * stride);
+      a = p[0];
+      b = p[1];
+    }
+    qs[2 * t] = a;
+    qs[2 * t + 1] = b;
+    const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    tag[j] = digest_tag(d);
+    pos[j] = digest_bucket(d) & dict.mask;
+  }
+  for (;;) {
+    uint64_t sv[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sv[j] = live[j] ? dict.table[pos[j]] : kEmpty;
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (sv[j] == kEmpty) live[j] = false;
+      if (live[j] && (uint32_t)(sv[j] >> 32) == tag[j]) {
+        const uint32_t e = (uint32_t)sv[j];
+        const uint4 *r = reinterpret_cast<const uint4 *>(dict.rec + e);
+        const uint4 ra = r[0], rb = r[1], rf = r[2];
+        const uint64_t ru = dict.rec[e].uoff;
+        const uint32_t t = threadIdx.x + 256u * j;
+        const uint4 a = qs[2 * t], b = qs[2 * t + 1];
+        if (((ra.x ^ a.x) | (ra.y ^ a.y) | (ra.z ^ a.z) | (ra.w ^ a.w) | (rb.x ^ b.x) |
+             (rb.y ^ b.y) | (rb.z ^ b.z) | (rb.w ^ b.w)) == 0) {
+          h[j] = ngpu_dict_hit{rf.w, rf.z, rf.y, rf.x, ru};
+          live[j] = false;
+        }
+      }
+      if (live[j]) pos[j] = (pos[j] + 1) & dict.mask;
+      any |= live[j];
+    }
+    if (!any) break;
+  }
+  __syncthreads();  // every query compare of the workgroup is done with qs
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    if (q0 + threadIdx.x + 256u * j < n)
+      reinterpret_cast<ngpu_dict_hit *>(stage)[threadIdx.x + 256u * j] = h[j];
+  __syncthreads();
+  const uint64_t m = n - q0 < 256ull * K ? n - q0 : 256ull * K;
+  const uint32_t bytes = (uint32_t)m * (uint32_t)sizeof(ngpu_dict_hit);
+  uint8_t *dst = reinterpret_cast<uint8_t *>(hits + q0);
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    for (uint32_t i = threadIdx.x; i < bytes / 16; i += 256)
+      reinterpret_cast<uint4 *>(dst)[i] = stage[i];
+    if ((bytes & 15) && threadIdx.x == 0)
+      reinterpret_cast<uint2 *>(dst + (bytes & ~15u))[0] =
+          reinterpret_cast<const uint2 *>(stage)[(bytes & ~15u) / 8];
+  } else {
+    for (uint32_t i = threadIdx.x; i < bytes / 8; i += 256)
+      reinterpret_cast<uint2 *>(dst)[i] = reinterpret_cast<const uint2 *>(stage)[i];
+  }
+}
+
 // A/B variants of the same probe (NGPU_PROBE_VARIANT, read per call; bench /
 // tools/probe_sweep.py): where do the line requests beyond query + slot +
 // record come from?  QV: the workgroup's queries (stride 32) are read into
@@ -1248,6 +1326,8 @@ void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
     case 7: hipLaunchKernelGGL((dict_probe_variant<0, 4>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
     case 8: hipLaunchKernelGGL((dict_probe_multi<2>), dim3((unsigned)((n + 511) / 512)), dim3(256), 0, s, digests, stride, n, dict, hits); return;
     case 9: hipLaunchKernelGGL((dict_probe_multi<4>), dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    case 10: hipLaunchKernelGGL((dict_probe_multi_lds<2>), dim3((unsigned)((n + 511) / 512)), dim3(256), 0, s, digests, stride, n, dict, hits); return;
+    case 11: hipLaunchKernelGGL((dict_probe_multi_lds<3>), dim3((unsigned)((n + 767) / 768)), dim3(256), 0, s, digests, stride, n, dict, hits); return;
     default: break;
   }
   hipLaunchKernelGGL(dict_probe_records, g, dim3(256), 0, s, digests, stride, n, dict, hits);

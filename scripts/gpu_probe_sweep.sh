@@ -15,13 +15,13 @@ timeout -k 10 300 python3 tools/probe_sweep.py 16 $SIZES > "$OUT/sweep.jsonl" 2>
 ok $? sweep
 cat "$OUT/sweep.jsonl"
 cd /tmp
-timeout -k 10 400 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --kernel-include-regex "dict_probe_records|dict_probe_variant" --output-format csv -d "$OUT/pmc" -o pmc -- python3 "$ROOT/tools/probe_sweep.py" 16 $SIZES > "$OUT/pmc.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --kernel-include-regex "dict_probe_records|dict_probe_variant|dict_probe_multi" --output-format csv -d "$OUT/pmc" -o pmc -- python3 "$ROOT/tools/probe_sweep.py" 16 $SIZES > "$OUT/pmc.log" 2>&1
 ok $? pmc
 python3 - "$OUT" <<'PY'
 import csv, glob, json, sys
 out = sys.argv[1]
 f = glob.glob(f"{out}/pmc/**/*counter_collection.csv", recursive=True)[0]
-rows = [r for r in csv.DictReader(open(f)) if "dict_probe_records" in r["Kernel_Name"] or "dict_probe_variant" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(f)) if "dict_probe_records" in r["Kernel_Name"] or "dict_probe_variant" in r["Kernel_Name"] or "dict_probe_multi" in r["Kernel_Name"]]
 disp = {}
 for r in rows:
     disp.setdefault(int(r["Dispatch_Id"]), {})[r["Counter_Name"]] = float(r["Counter_Value"])
