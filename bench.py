@@ -366,7 +366,8 @@ def probe_bench(torch, nydus_gpu, eng, dd, Q, build_s, reps=5):
                 lines_s = pm["read_request_bytes"] / 128 / t
                 tr["random_line_ceiling"] = {
                     "glines_s": round(ceil / 1e9, 2), "probe_glines_s": round(lines_s / 1e9, 2),
-                    "frac": round(lines_s / ceil, 4), "source": csrc}
+                    "frac": round(lines_s / ceil, 4), "source": csrc,
+                    "read_lines_per_probe": round(pm["read_request_bytes"] / 128 / Q, 3)}
     return {"kernel": "dict_probe_records", "queries": Q, "hits": nhit, "dict_entries": m, **tr,
             "ms": round(t * 1e3, 4), "gprobes_s": round(Q / t / 1e9, 2),
             "bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": round(PEAK_HBM / 1e9, 1),
