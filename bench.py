@@ -797,7 +797,7 @@ def node_e2e(torch, dist, nydus_gpu, buf, wl, stride, device, backend, sample_by
 SUB_KEYS = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "stage_ms", "roofline",
             "cpu_baseline", "speedup_vs_cpu", "speedup_vs_cpu_single_stream", "dict",
             "probe_roofline", "merge", "decisions", "digest_check_past_4gib", "n_gpus", "sharded_dict",
-            "e2e_pcie", "tar_host_path")
+            "e2e_pcie", "tar_host_path", "ranks")
 
 
 def child_line(cmd, timeout_s, env=None):
@@ -849,19 +849,10 @@ def c4_entry(world, layers, steps, backend="nccl", timeout_s=420):
     -> RCCL all_to_all_single probe routing (owner bucketing by
     ngpu_route_digests) -> per-layer dedup of every layer.  The other ranks
     wait in a gloo barrier meanwhile."""
-    import socket
-    sk = socket.socket()
-    sk.bind(("127.0.0.1", 0))
-    port = sk.getsockname()[1]
-    sk.close()
     env = dict(os.environ)
-    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
-              "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
-              "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "GROUP_WORLD_SIZE"):
+    for k in DIST_ENV:
         env.pop(k, None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--workload", "c4",
+    cmd = self_launch_cmd([], world, free_port()) + ["--gpus", str(world), "--workload", "c4",
            "--steps", str(steps), "--warmup", "15", "--no-sharded-extra", "--no-node-extra",
            "--no-e2e", "--no-c4", "--c4-layers", str(layers), "--dist-backend", backend]
     return child_line(cmd, timeout_s, env=env)
@@ -1245,6 +1236,81 @@ def node_bench(args):
         node.close()
 
 
+DIST_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+            "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+            "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "GROUP_WORLD_SIZE")
+
+
+def free_port() -> int:
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def self_launch_cmd(argv, gpus: int, port: int):
+    """The torchrun command `python bench.py --gpus N ...` (no WORLD_SIZE in
+    the environment) runs as: N ranks on this node, rendezvous on 127.0.0.1,
+    every argument passed through unchanged."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_self_launch(args, argv, env=None, runner=None):
+    """`--gpus N > 1` without a launcher around us: start the N worker processes
+    as a child torchrun and relay rank 0's line (the children inherit stdout).
+    Called before torch is imported, so this parent never touches the GPU: it
+    only waits, forwards SIGTERM / SIGINT to the child, and exits with the
+    child's status.  -> None when this process is itself a rank (or N = 1)."""
+    env = dict(os.environ if env is None else env)
+    if args.gpus <= 1 or env.get("WORLD_SIZE") or args.node:
+        return None
+    for k in DIST_ENV:
+        env.pop(k, None)
+    env["NYDUS_BENCH_LAUNCHER"] = "self"
+    cmd = self_launch_cmd(argv, args.gpus, free_port())
+    if runner is not None:
+        return runner(cmd, env)
+    import signal
+    import subprocess
+    p = subprocess.Popen(cmd, env=env)
+
+    def fwd(sig, _frame):
+        try:
+            p.send_signal(sig)
+        except OSError:
+            pass
+    for s in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(s, fwd)
+    return p.wait()
+
+
+def rank_check(args, dist, world, rank, local, backend, torch, group=None):
+    """Every rank: the world it joined must be the one asked for (`--gpus`);
+    a mismatch exits non-zero on every rank.  -> what the line reports about
+    the ranks: world size, RCCL world size (nccl backend), and how many
+    distinct GPUs the ranks sit on (by device UUID)."""
+    if world != args.gpus:
+        print(f"bench.py: rank {rank} joined a world of {world} ranks, --gpus {args.gpus}",
+              file=sys.stderr, flush=True)
+        raise SystemExit(4)
+    try:
+        dev = str(torch.cuda.get_device_properties(local).uuid)
+    except (AttributeError, RuntimeError):
+        dev = f"local{local}"
+    devs = [dev]
+    if dist is not None:
+        devs = [None] * world
+        dist.all_gather_object(devs, dev, group=group)
+    return {"world_size": world, "requested": args.gpus, "backend": backend if dist else None,
+            "rccl_world_size": world if dist is not None and backend == "nccl" else None,
+            "distinct_devices": len(set(devs)),
+            "launcher": os.environ.get("NYDUS_BENCH_LAUNCHER") or ("torchrun" if dist else "none")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1305,6 +1371,9 @@ def main():
     ap.add_argument("--node", default="", help="comma list of devices: one process drives them "
                     "through ngpu_node_* (a device may repeat: one-GPU rehearsal); see node_bench")
     args = ap.parse_args()
+    rc = maybe_self_launch(args, sys.argv[1:])
+    if rc is not None:
+        raise SystemExit(rc)
     if args.warmup is None:
         w = WORKLOADS[args.workload]
         args.warmup = 80 if (w.get("pool") or w.get("dict_entries")) else 20
@@ -1330,6 +1399,8 @@ def main():
         # host-side barriers (the closing one): while rank 0 runs the node child
         # on every GPU, the other ranks wait on the CPU, not in an RCCL kernel
         cpu_group = dist.new_group(backend="gloo")
+    ranks = rank_check(args, dist, world, rank, local, args.dist_backend, torch,
+                       cpu_group if dist else None)
 
     wl = dict(WORKLOADS[args.workload])
     if args.dict_entries:
@@ -1634,6 +1705,7 @@ def main():
         "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "ranks": ranks,
         "data": ("synthetic alpine-like layer tar built on the host (tests/golden/layers.py), "
                  "copied to HBM" if wl.get("tar") else
                  "synthetic (random bytes generated on the GPU, real GNU tar headers)"),

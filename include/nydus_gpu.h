@@ -484,8 +484,13 @@ int ngpu_node_process_device(ngpu_node *node, uint32_t i, ngpu_dict *dict, const
  * (ngpu_route_digests), every part's segments cross the node in ONE
  * all-to-all-v, each owner probes what it received against its partition,
  * the hits return in one all-to-all-v the other way, go back to their rows
- * and each part dedups its own layers.  The per-owner row counts reach the
- * host once per step (they size the all-to-all).
+ * and each part dedups its own layers.  Nothing in the step waits for the
+ * device (ABI 5, round 5): each part's digests are bucketed into padded
+ * per-owner segments of n rows, so every transfer size is known when the
+ * step is enqueued, and the per-owner counts cross in band (one u32 per
+ * pair) for the owners' probes to read on the device.  A caller can enqueue
+ * step k+1 behind step k; the cost is W x n x 32 B out per part instead of
+ * n x 32 B (csrc/a2a_plan.hpp).
  * flags NGPU_NODE_STEP_RCCL: the two all-to-alls are RCCL ncclAllToAllv
  * calls over a communicator of the node's devices (ncclCommInitAll, created on
  * the first such step; RCCL takes one rank per GPU, so a node listing a

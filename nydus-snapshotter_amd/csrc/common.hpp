@@ -268,6 +268,15 @@ void launch_route(const uint8_t *src, uint64_t stride, uint64_t n, uint32_t W, u
 void launch_dict_probe_routed(const uint8_t *q, const uint32_t *rows, const uint32_t *cnt,
                               uint64_t n_max, uint32_t owner, const DictDevice &dict,
                               ngpu_dict_hit *hits, hipStream_t s);
+// Owner side of the node step's padded all-to-all (a2a_plan.hpp): W blocks
+// of q (32-B rows), block i = rows [off[i], off[i + 1]), of which the first
+// rcnt[i] (device u32[W]) are probed into hits[row]; padding rows are skipped.
+struct ProbeBlocks {
+  uint32_t W;
+  uint64_t off[65];
+};
+void launch_dict_probe_blocks(const uint8_t *q, const uint32_t *rcnt, const ProbeBlocks &b,
+                              const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s);
 // Records [0, n) a dedup stage accepted get kind = NGPU_DIGESTED again
 // (rejected ones keep NGPU_UNHASHED): a later dedup over a longer prefix.
 void launch_remark_digested(ngpu_result *res, uint64_t n, hipStream_t s);

@@ -172,6 +172,15 @@ __global__ __launch_bounds__(256) void dict_probe_records(const uint8_t *__restr
   }
 }
 
+// Measured-losing A/B probes (dict_probe_multi, dict_probe_multi_lds,
+// dict_probe_variant, dict_probe_coop; DESIGN.md §3 "dict probe") are built
+// only with -DNGPU_PROBE_AB=1 (scripts/build_ab.sh), never into the product
+// library; their launch knobs (NGPU_PROBE_VARIANT / NGPU_PROBE_COOP) exist
+// only in such a build.
+#ifndef NGPU_PROBE_AB
+#define NGPU_PROBE_AB 0
+#endif
+#if NGPU_PROBE_AB
 // K queries per thread, their probe chains stepped in lockstep: each step
 // issues the K slot loads (and the K record loads of tag matches) together,
 // so a wave has K independent random requests in flight where
@@ -462,6 +471,8 @@ __global__ __launch_bounds__(256) void dict_probe_coop(const uint8_t *__restrict
   }
   if (live && sub == 0) hits[q] = dict_hit_of(dict, e);
 }
+
+#endif  // NGPU_PROBE_AB
 
 // RAFS v6 chunk-info records (80 B: block_id[32], blob_index, flags,
 // compressed_size, uncompressed_size, compressed_offset, uncompressed_offset,
@@ -1306,6 +1317,8 @@ void launch_dict_build(const DictRec *rec, uint64_t m, uint64_t *table, uint64_t
 void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
                        const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s) {
   if (n == 0) return;
+  const dim3 g((unsigned)((n + 255) / 256));
+#if NGPU_PROBE_AB
   // A/B knob, read per call (bench.py probe_roofline; 2.6x slower)
   const char *coop = getenv("NGPU_PROBE_COOP");
   if (coop && coop[0] == '1') {
@@ -1315,7 +1328,6 @@ void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
   }
   const char *var = getenv("NGPU_PROBE_VARIANT");
   const int v = var ? atoi(var) : 0;
-  const dim3 g((unsigned)((n + 255) / 256));
   switch (v) {
     case 1: hipLaunchKernelGGL((dict_probe_variant<1, 0>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
     case 2: hipLaunchKernelGGL((dict_probe_variant<0, 1>), g, dim3(256), 0, s, digests, stride, n, dict, hits); return;
@@ -1330,6 +1342,7 @@ void launch_dict_probe(const uint8_t *digests, uint64_t stride, uint64_t n,
     case 11: hipLaunchKernelGGL((dict_probe_multi_lds<3>), dim3((unsigned)((n + 767) / 768)), dim3(256), 0, s, digests, stride, n, dict, hits); return;
     default: break;
   }
+#endif
   hipLaunchKernelGGL(dict_probe_records, g, dim3(256), 0, s, digests, stride, n, dict, hits);
 }
 
@@ -1463,6 +1476,30 @@ __global__ __launch_bounds__(256) void dict_probe_routed(const uint8_t *__restri
   }
 }
 
+// An owner's probe of the node step's padded blocks (a2a_plan.hpp
+// PaddedStep): requester i's block is rows [off[i], off[i + 1]) of q, its
+// first rcnt[i] rows are digests this owner owns, the rest padding (not
+// probed, their hits left unwritten: the requester drops them by row id).
+// The counts arrived in band, so nothing here waits for the host.
+__global__ __launch_bounds__(256) void dict_probe_blocks(const uint8_t *__restrict__ q,
+                                                         const uint32_t *__restrict__ rcnt,
+                                                         ProbeBlocks b, DictDevice dict,
+                                                         ngpu_dict_hit *__restrict__ hits) {
+  const uint64_t r = blockIdx.x * 256ull + threadIdx.x;
+  if (r >= b.off[b.W]) return;
+  uint32_t i = 0;
+  while (i + 1 < b.W && b.off[i + 1] <= r) ++i;
+  if (r - b.off[i] >= rcnt[i]) return;
+  const uint4 *p = reinterpret_cast<const uint4 *>(q + 32 * r);
+  ngpu_dict_hit h{kNone, 0, 0, 0, 0};
+  if (dict.m) {
+    const uint4 x = p[0], y = p[1];
+    const uint32_t d[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+    h = dict_find(dict, d);
+  }
+  hits[r] = h;
+}
+
 // hits of routed rows back to their rows (dist.py: the all-to-all returns
 // them in routed order); padding rows (row id ~0) are skipped
 __global__ void hits_scatter(const ngpu_dict_hit *__restrict__ routed,
@@ -1509,6 +1546,14 @@ void launch_dict_probe_routed(const uint8_t *q, const uint32_t *rows, const uint
   const uint64_t b = std::min<uint64_t>((n_max + 255) / 256, 2048);
   hipLaunchKernelGGL(dict_probe_routed, dim3((unsigned)b), dim3(256), 0, s, q, rows, cnt, owner,
                      dict, hits);
+}
+
+void launch_dict_probe_blocks(const uint8_t *q, const uint32_t *rcnt, const ProbeBlocks &b,
+                              const DictDevice &dict, ngpu_dict_hit *hits, hipStream_t s) {
+  const uint64_t R = b.off[b.W];
+  if (R == 0) return;
+  hipLaunchKernelGGL(dict_probe_blocks, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, q, rcnt,
+                     b, dict, hits);
 }
 
 void launch_hits_scatter(const ngpu_dict_hit *routed, const uint32_t *rows, uint64_t m,
@@ -1587,11 +1632,15 @@ void launch_dedup(const ngpu_chunk *chunks, uint64_t n, const DictDevice &dict,
                     reinterpret_cast<uint64_t *>(st), nst, ws.intra, icap, ts, ntw,
                     ws.newflag, ws.uoff, ws.nbytes, ws.ndict, total, ws.stats};
   if (small && single && nbo <= kLdsBlobs) {  // one layer: the whole stage in LDS
+#if NGPU_PROBE_AB
     // NGPU_DEDUP_LDS_THREADS=1024: the wide workgroup for every size (A/B knob)
     static const bool wide = [] {
       const char *v = getenv("NGPU_DEDUP_LDS_THREADS");
       return v && atoi(v) == 1024;
     }();
+#else
+    constexpr bool wide = false;
+#endif
     if (n <= 256 && !wide)
       hipExtLaunchKernelGGL(dedup_small_lds<256>, dim3(1), dim3(256), 0, s, nullptr, ev_end, 0,
                             chunks, n, dict, hits, n_blobs, align, st, out, ws.stats);

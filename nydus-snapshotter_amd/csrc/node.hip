@@ -21,6 +21,12 @@
 // the DMA engines keep coarse-grained HBM coherent across the GPUs, and the
 // payload is tiny (16K chunks of a 16 GiB layer = 512 KiB out, 384 KiB back
 // per owner), so the exchange is latency-bound, not link-bound.
+//
+// The node step (ngpu_node_process_step) is the bulk form: every part at
+// once, one all-to-all-v of digests and one of hits, over RCCL or peer
+// copies.  It routes into padded per-owner segments (a2a_plan.hpp) so that
+// no transfer size depends on a device-side count: the counts cross in band
+// and the whole step enqueues without a host wait.
 #include <dlfcn.h>
 #include <stdio.h>
 #include <string.h>
@@ -30,6 +36,7 @@
 
 #include <rccl/rccl.h>
 
+#include "a2a_plan.hpp"
 #include "engine_internal.hpp"
 
 using namespace ngpu;
@@ -37,16 +44,16 @@ using namespace ngpu;
 namespace {
 // Buffers of one part of a node step (ngpu_node_process_step), on its device.
 struct StepBuf {
-  uint8_t *xq = nullptr;          // its digests bucketed by owner (n x 32)
-  uint32_t *xrow = nullptr;       // their row ids
-  ngpu_dict_hit *sh = nullptr;    // hits returned, same (owner-bucketed) order
+  uint8_t *xq = nullptr;          // its digests bucketed by owner, padded: W x n rows of 32 B
+  uint32_t *xrow = nullptr;       // their row ids (~0: padding)
+  ngpu_dict_hit *sh = nullptr;    // hits returned, same (owner-bucketed, padded) order
   ngpu_dict_hit *hits = nullptr;  // hits by row
-  uint64_t cap = 0;
+  uint64_t cap = 0;               // rows of xq / xrow / sh / hits
   uint8_t *rq = nullptr;          // digests it received as owner (R x 32)
   ngpu_dict_hit *rh = nullptr;    // its hits for them
   uint64_t rcap = 0;
   uint32_t *cnt = nullptr;        // 128 u32: per-owner counts (+ scatter cursors)
-  uint32_t *h_cnt = nullptr;      // pinned copy of the counts
+  uint32_t *rcnt = nullptr;       // 64 u32: as owner, each requester's count (in band)
   hipEvent_t counted = nullptr, sent = nullptr, returned = nullptr, done = nullptr;
 };
 }  // namespace
@@ -370,9 +377,8 @@ void step_free(ngpu_node *node) {
     DeviceGuard g(node->dev[i]);
     if (b.done) (void)hipEventSynchronize(b.done);
     for (void *p : {(void *)b.xq, (void *)b.xrow, (void *)b.sh, (void *)b.hits, (void *)b.rq,
-                    (void *)b.rh, (void *)b.cnt})
+                    (void *)b.rh, (void *)b.cnt, (void *)b.rcnt})
       if (p) (void)hipFree(p);
-    if (b.h_cnt) (void)hipHostFree(b.h_cnt);
     for (hipEvent_t ev : {b.counted, b.sent, b.returned, b.done})
       if (ev) (void)hipEventDestroy(ev);
   }
@@ -406,7 +412,7 @@ int step_comms(ngpu_node *node) {
 template <class Q>
 int step_grow(ngpu_engine *e, StepBuf &b, uint64_t n, uint64_t r, Q &&quiesce) {
   if (!b.cnt) HIP_TRY(e, hipMalloc((void **)&b.cnt, 128 * sizeof(uint32_t)));
-  if (!b.h_cnt) HIP_TRY(e, hipHostMalloc((void **)&b.h_cnt, 64 * sizeof(uint32_t), hipHostMallocDefault));
+  if (!b.rcnt) HIP_TRY(e, hipMalloc((void **)&b.rcnt, 64 * sizeof(uint32_t)));
   for (hipEvent_t *ev : {&b.counted, &b.sent, &b.returned, &b.done})
     if (!*ev) HIP_TRY(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
   if ((n > b.cap && b.xq) || (r > b.rcap && b.rq))
@@ -452,12 +458,7 @@ int step_alltoallv(ngpu_node *node, bool use_rccl, const std::vector<hipStream_t
     std::vector<size_t> sc(W), sd(W), rc(W), rd(W);
     NCCL_TRY(e0, rccl().group_start());
     for (uint32_t i = 0; i < W; ++i) {
-      for (uint32_t j = 0; j < W; ++j) {
-        sc[j] = cnt_send(i, j) * row;
-        sd[j] = sdis(i, j) * row;
-        rc[j] = cnt_send(j, i) * row;
-        rd[j] = rdis(i, j) * row;
-      }
+      a2a_rank_args(W, i, row, cnt_send, sdis, rdis, sc.data(), sd.data(), rc.data(), rd.data());
       const ncclResult_t r = rccl().alltoallv(src[i], sc.data(), sd.data(), dst[i], rc.data(),
                                               rd.data(), ncclUint8, node->comms[i], s[i]);
       if (r != ncclSuccess) {
@@ -547,14 +548,22 @@ int node_step_enqueue(ngpu_node *node, ngpu_dict *d, const ngpu_node_part *pt, u
   };
   std::vector<hipStream_t> s(W);
   for (uint32_t i = 0; i < W; ++i) s[i] = (hipStream_t)pt[i].stream;
+  // the padded layout (a2a_plan.hpp): every transfer size is known here, the
+  // per-owner counts travel in band, and nothing below waits for the device
+  std::vector<uint64_t> n(W), off(W + 1, 0);
+  for (uint32_t i = 0; i < W; ++i) n[i] = pt[i].n, off[i + 1] = off[i] + n[i];
+  if (W > 64) return fail(e0, NGPU_EINVAL, "node step: %u parts (at most 64)", W);
+  const PaddedStep ps{W, n.data(), off.data()};
   // buffers are reused: this step's streams start after every part of the last
   for (uint32_t i = 0; i < W; ++i) {
     DeviceGuard dg(node->dev[i]);
-    if (int rc = step_grow(node->eng[i], node->sb[i], pt[i].n, 0, quiesce)) return rc;
+    if (int rc = step_grow(node->eng[i], node->sb[i], (uint64_t)W * n[i], off[W], quiesce))
+      return rc;
     if (node->stepped)
       for (uint32_t j = 0; j < W; ++j) HIP_TRY(e0, hipStreamWaitEvent(s[i], node->sb[j].done, 0));
   }
-  // 1. digests; 2. bucket them by owner, counts to the host
+  // 1. digests; 2. bucketed by owner into padded segments (seg_cap = n), the
+  // padding rows' ids ~0
   for (uint32_t i = 0; i < W; ++i) {
     const ngpu_node_part &p = pt[i];
     StepBuf &b = node->sb[i];
@@ -562,59 +571,48 @@ int node_step_enqueue(ngpu_node *node, ngpu_dict *d, const ngpu_node_part *pt, u
       if (int rc = ngpu_digest_device(node->eng[i], p.d_data, p.len, p.d_chunks, p.n, p.d_out, p.stream))
         return rc;
     DeviceGuard dg(node->dev[i]);
-    launch_route(reinterpret_cast<const uint8_t *>(p.d_out), sizeof(ngpu_result), p.n, W, 0, b.cnt,
-                 b.xq, b.xrow, s[i]);
+    if (p.n) HIP_TRY(e0, hipMemsetAsync(b.xrow, 0xFF, (size_t)W * p.n * sizeof(uint32_t), s[i]));
+    launch_route(reinterpret_cast<const uint8_t *>(p.d_out), sizeof(ngpu_result), p.n, W, p.n,
+                 b.cnt, b.xq, b.xrow, s[i]);
     HIP_TRY(e0, hipGetLastError());
-    HIP_TRY(e0, hipMemcpyAsync(b.h_cnt, b.cnt, W * sizeof(uint32_t), hipMemcpyDeviceToHost, s[i]));
-    HIP_TRY(e0, hipEventRecord(b.counted, s[i]));
   }
-  std::vector<uint64_t> c((size_t)W * W), off((size_t)W * W), roff((size_t)W * W), R(W, 0);
-  for (uint32_t i = 0; i < W; ++i) {
-    HIP_TRY(e0, hipEventSynchronize(node->sb[i].counted));
-    uint64_t o = 0;
-    for (uint32_t j = 0; j < W; ++j) {
-      c[i * W + j] = node->sb[i].h_cnt[j];
-      off[i * W + j] = o;  // requester i's segment for owner j
-      o += c[i * W + j];
-    }
-    if (o != pt[i].n) return fail(e0, NGPU_EDEVICE, "node step: part %u routed %llu of %llu rows", i,
-                                  (unsigned long long)o, (unsigned long long)pt[i].n);
-  }
-  for (uint32_t j = 0; j < W; ++j)
-    for (uint32_t i = 0; i < W; ++i) {
-      roff[j * W + i] = R[j];  // owner j's segment from requester i
-      R[j] += c[i * W + j];
-    }
-  for (uint32_t j = 0; j < W; ++j) {
-    DeviceGuard dg(node->dev[j]);
-    if (int rc = step_grow(node->eng[j], node->sb[j], pt[j].n, R[j], quiesce)) return rc;
-  }
-  auto cnt_fwd = [&](uint32_t i, uint32_t j) { return c[i * W + j]; };
-  auto sdis_fwd = [&](uint32_t i, uint32_t j) { return off[i * W + j]; };
-  auto rdis_fwd = [&](uint32_t j, uint32_t i) { return roff[j * W + i]; };
   std::vector<const uint8_t *> src(W);
   std::vector<uint8_t *> dst(W);
-  // 3. digests to their owners
-  for (uint32_t i = 0; i < W; ++i) src[i] = node->sb[i].xq, dst[i] = node->sb[i].rq;
-  if (int rc = step_alltoallv(node, use_rccl, s, src, dst, 32, cnt_fwd, sdis_fwd, rdis_fwd, &StepBuf::sent))
+  // 3. counts (requester i's cnt[j] -> owner j's rcnt[i]) and digests to their owners
+  for (uint32_t i = 0; i < W; ++i)
+    src[i] = reinterpret_cast<const uint8_t *>(node->sb[i].cnt),
+    dst[i] = reinterpret_cast<uint8_t *>(node->sb[i].rcnt);
+  if (int rc = step_alltoallv(node, use_rccl, s, src, dst, sizeof(uint32_t), PaddedStep::cnt_cnt,
+                              PaddedStep::cnt_sdis, PaddedStep::cnt_rdis, &StepBuf::counted))
     return rc;
-  // 4. owners probe their partitions
+  for (uint32_t i = 0; i < W; ++i) src[i] = node->sb[i].xq, dst[i] = node->sb[i].rq;
+  if (int rc = step_alltoallv(
+          node, use_rccl, s, src, dst, 32, [&](uint32_t i, uint32_t j) { return ps.fwd_cnt(i, j); },
+          [&](uint32_t i, uint32_t j) { return ps.fwd_sdis(i, j); },
+          [&](uint32_t j, uint32_t i) { return ps.fwd_rdis(j, i); }, &StepBuf::sent))
+    return rc;
+  // 4. owners probe the counted rows of each requester's block
+  ProbeBlocks pb{};
+  pb.W = W;
+  for (uint32_t i = 0; i <= W; ++i) pb.off[i] = off[i];
   for (uint32_t j = 0; j < W; ++j) {
     DeviceGuard dg(node->dev[j]);
-    launch_dict_probe(node->sb[j].rq, 32, R[j], d->parts[j]->dev, node->sb[j].rh, s[j]);
+    launch_dict_probe_blocks(node->sb[j].rq, node->sb[j].rcnt, pb, d->parts[j]->dev, node->sb[j].rh,
+                             s[j]);
     HIP_TRY(e0, hipGetLastError());
   }
-  // 5. hits back: owner j sends requester i's rows from roff(j, i) to off(i, j)
+  // 5. hits back: owner j sends requester i's block to i's segment j
   for (uint32_t j = 0; j < W; ++j)
     src[j] = reinterpret_cast<const uint8_t *>(node->sb[j].rh),
     dst[j] = reinterpret_cast<uint8_t *>(node->sb[j].sh);
-  auto cnt_back = [&](uint32_t j, uint32_t i) { return c[i * W + j]; };
-  auto sdis_back = [&](uint32_t j, uint32_t i) { return roff[j * W + i]; };
-  auto rdis_back = [&](uint32_t i, uint32_t j) { return off[i * W + j]; };
-  if (int rc = step_alltoallv(node, use_rccl, s, src, dst, sizeof(ngpu_dict_hit), cnt_back, sdis_back,
-                              rdis_back, &StepBuf::returned))
+  if (int rc = step_alltoallv(
+          node, use_rccl, s, src, dst, sizeof(ngpu_dict_hit),
+          [&](uint32_t j, uint32_t i) { return ps.back_cnt(j, i); },
+          [&](uint32_t j, uint32_t i) { return ps.back_sdis(j, i); },
+          [&](uint32_t i, uint32_t j) { return ps.back_rdis(i, j); }, &StepBuf::returned))
     return rc;
-  // 6. hits to their rows, then each part's own dedup
+  // 6. hits to their rows (padding rows dropped by their ~0 id), then each
+  // part's own dedup
   const uint32_t nb = d->dev.n_blobs ? d->dev.n_blobs : 1;
   for (uint32_t i = 0; i < W; ++i) {
     const ngpu_node_part &p = pt[i];
@@ -622,7 +620,7 @@ int node_step_enqueue(ngpu_node *node, ngpu_dict *d, const ngpu_node_part *pt, u
     ngpu_engine *e = node->eng[i];
     if (p.n) {
       DeviceGuard dg(e->device);
-      launch_hits_scatter(b.sh, b.xrow, p.n, b.hits, s[i]);
+      launch_hits_scatter(b.sh, b.xrow, (uint64_t)W * p.n, b.hits, s[i]);
       HIP_TRY(e0, hipGetLastError());
       std::lock_guard<std::mutex> eg(e->mu);
       if (int rc = enqueue_dedup(e, nullptr, p.d_chunks, p.n, p.d_out, b.hits, nb, s[i],

@@ -1,17 +1,20 @@
 #!/bin/bash
-# Build A/B variants of libnydusgpu.so that differ only in blake3.hip compile
-# flags, into nydus-snapshotter_amd/build/ab/NAME.so (run here, on the CPU).
-# usage: scripts/build_ab.sh NAME "-DFLAG=V ..." [NAME "-D..."] ...
+# Build A/B variants of libnydusgpu.so that differ only in one source's
+# compile flags (AB_SRC, default blake3; AB_SRC=dedup with -DNGPU_PROBE_AB=1
+# for the dict-probe variants), into nydus-snapshotter_amd/build/ab/NAME.so
+# (run here, on the CPU).
+# usage: [AB_SRC=dedup] scripts/build_ab.sh NAME "-DFLAG=V ..." [NAME "-D..."] ...
 set -eu
 cd "$(dirname "$0")/../nydus-snapshotter_amd"
 make -s libnydusgpu.so
 mkdir -p build/ab
-OTHER=$(ls build/*.o | grep -v blake3.o)
+SRC=${AB_SRC:-blake3}
+OTHER=$(ls build/*.o | grep -v "/$SRC.o")
 while [ $# -ge 2 ]; do
   NAME=$1; FLAGS=$2; shift 2
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc $FLAGS \
-    -c csrc/blake3.hip -o build/ab/blake3_$NAME.o
+    -c csrc/$SRC.hip -o build/ab/${SRC}_$NAME.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/ab/$NAME.so \
-    build/ab/blake3_$NAME.o $OTHER -lcrypto -lz -ldl -lpthread
+    build/ab/${SRC}_$NAME.o $OTHER -lcrypto -lz -ldl -lpthread
   echo "built build/ab/$NAME.so ($FLAGS)"
 done

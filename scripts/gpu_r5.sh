@@ -1,0 +1,46 @@
+#!/bin/bash
+# Round-5 checks in one box; steps run in the order given, the first failure
+# ends the call.  usage: scripts/gpu_r5.sh TAG step...
+#   valu  : scripts/gpu_r5_valu.sh (VALU bank microbenchmark + SQ counters)
+#   suite : pytest -m gpu (optionally PYK="-k expr")
+#   smoke : __graft_entry__.smoke()
+#   bench : default bench line (N = 1)
+#   stats : rocprofv3 --kernel-trace --stats of the C2 bench
+#   n2    : python3 bench.py --gpus 2 over gloo (self-launched ranks)
+set -u
+TAG=${1:-r5}
+shift || true
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+export TMPDIR=/tmp
+ok() { local rc=$1 what=$2; echo "$what rc=$rc"; if [ "$rc" -ne 0 ]; then echo "stopping after $what"; exit "$rc"; fi; }
+for s in "$@"; do
+  case $s in
+    valu)
+      bash scripts/gpu_r5_valu.sh "$TAG/valu" > "$OUT/valu.log" 2>&1
+      ok $? valu
+      cat "$OUT/valu.log" | cut -c1-220 ;;
+    suite)
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ${PYK:-} > "$OUT/pytest_gpu.log" 2>&1
+      ok $? suite
+      tail -1 "$OUT/pytest_gpu.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      ok $? smoke
+      tail -1 "$OUT/smoke.log" ;;
+    bench)
+      timeout -k 10 600 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+      ok $? bench
+      python3 -c "import json; d=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1]); r=d['roofline']; print(d['value'], r['frac'], r.get('frac_mix'), r.get('frac_ceiling'), d['cpu_baseline']['value'], [d.get(k, {}).get('value') for k in ('c1', 'c3', 'c5_1000')])" ;;
+    stats)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c2 -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-sub > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err")
+      ok $? stats
+      python3 scripts/prof_agree.py "$OUT/prof" b3_groups "$OUT/prof_bench.json" "$OUT/rocprof_c2_agreement.json" | cut -c1-200 ;;
+    n2)
+      NYDUS_NODE_EXTRA_DEVICES=0,0 timeout -k 10 600 python3 bench.py --gpus 2 --steps 10 --warmup 5 --dist-backend gloo --c4-layers 4 > "$OUT/bench_c2_n2_gloo.json" 2> "$OUT/bench_c2_n2_gloo.err"
+      ok $? n2
+      python3 -c "import json; d=json.loads(open('$OUT/bench_c2_n2_gloo.json').read().strip().splitlines()[-1]); print(d['value'], d['n_gpus'], d.get('ranks'), json.dumps(d.get('node_cabi', {}).get('node_step')), d.get('c4', {}).get('value'))" ;;
+  esac
+done

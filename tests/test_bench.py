@@ -4,6 +4,7 @@ import io
 import tarfile
 
 import numpy as np
+import pytest
 
 import bench
 import nydus_gpu
@@ -76,3 +77,53 @@ def test_merge_extra_on_oracle_decisions():
     assert out["own_blobs"] == L
     assert out["dict_blobs"] == len(hit_blobs)
     assert out["layers"] == L and out["merged_bytes"] > 0
+
+
+def test_gpus_n_self_launches_n_ranks_before_any_gpu_call():
+    """`python bench.py --gpus N` (no WORLD_SIZE) becomes a child torchrun of N
+    ranks with every argument passed through; the parent
+    only relays the child's status.  The spawn is stubbed here."""
+    import argparse
+    seen = {}
+
+    def runner(cmd, env):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+
+    argv = ["--gpus", "2", "--dist-backend", "gloo", "--workload", "c1", "--steps", "3", "--no-sub"]
+    args = argparse.Namespace(gpus=2, node="")
+    env = {"PATH": "/usr/bin", "RANK": "3", "MASTER_PORT": "1", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    assert bench.maybe_self_launch(args, argv, env=env, runner=runner) == 7
+    cmd, cenv = seen["cmd"], seen["env"]
+    i = cmd.index("torch.distributed.run")
+    assert cmd[i - 1] == "-m" and "--nnodes=1" in cmd and "--nproc-per-node=2" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert int(cmd[cmd.index("--master-port") + 1]) > 0
+    j = [k for k, c in enumerate(cmd) if c.endswith("bench.py")][0]
+    assert cmd[j + 1:] == argv  # passed through unchanged, --gpus included
+    assert "RANK" not in cenv and "MASTER_PORT" not in cenv
+    assert cenv["NYDUS_BENCH_LAUNCHER"] == "self" and cenv["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # a rank (WORLD_SIZE set by the launcher), N = 1 and --node never relaunch
+    seen.clear()
+    assert bench.maybe_self_launch(args, argv, env={"WORLD_SIZE": "2"}, runner=runner) is None
+    assert bench.maybe_self_launch(argparse.Namespace(gpus=1, node=""), [], env={},
+                                   runner=runner) is None
+    assert bench.maybe_self_launch(argparse.Namespace(gpus=2, node="0,0"), [], env={},
+                                   runner=runner) is None
+    assert not seen
+
+
+def test_rank_check_refuses_a_world_other_than_gpus():
+    import argparse
+
+    class FakeTorch:
+        class cuda:
+            @staticmethod
+            def get_device_properties(i):
+                raise RuntimeError("no GPU here")
+    args = argparse.Namespace(gpus=2)
+    with pytest.raises(SystemExit) as ex:
+        bench.rank_check(args, None, 1, 0, 0, "nccl", FakeTorch)
+    assert ex.value.code == 4
+    r = bench.rank_check(argparse.Namespace(gpus=1), None, 1, 0, 0, "nccl", FakeTorch)
+    assert r["world_size"] == 1 and r["distinct_devices"] == 1 and r["rccl_world_size"] is None
