@@ -579,18 +579,39 @@ def mix_roofline(roof, achieved, kernel, workload, comp=0):
     if not kernel.startswith("b3_groups"):
         return
     mix, src = newest_profile("isa_mix_b3_groups.json")
-    if mix:
-        pm = mix["peak_mix_tops_at_2p4ghz"] * 1e12
+    issue, isrc_ = newest_profile("valu_issue_model.json")
+    pm = None
+    if issue:
+        # round 5: the measured issue cost of the kernel's
+        # own mixed 2-/4-cycle G stream, per SIMD with every wave's HW_ID
+        # (tools/valu_bank.hip): ~4 cycles per wave64 instruction at any
+        # occupancy; the linear 2-/4-cycle model below is not reachable
+        pm = issue["model"]["peak_tops_at_2p4ghz"] * 1e12
         roof.update({"peak_mix": round(pm / 1e12, 3), "frac_mix": round(achieved / pm, 4),
-                     "mix": {"four_cycle_ops_per_compression": mix["per_compression"]["four_cycle"],
-                             "two_cycle_ops_per_compression": mix["per_compression"]["two_cycle"],
-                             "cycles_per_algorithmic_op": mix["cycles_per_algorithmic_op"],
-                             "source": src}})
+                     "mix": {"model": "measured issue cost of the mixed G stream",
+                             "cycles_per_wave_instruction":
+                                 issue["model"]["cycles_per_wave_instruction_mixed_stream"],
+                             "kernel_cycles_per_valu_instruction_pmc":
+                                 issue["b3_groups_c2_pmc"]["cycles_per_valu_instruction_per_simd"],
+                             "source": isrc_}})
+    if mix:
+        lin = mix["peak_mix_tops_at_2p4ghz"] * 1e12
+        lin_d = {"peak": round(lin / 1e12, 3), "frac": round(achieved / lin, 4),
+                 "four_cycle_ops_per_compression": mix["per_compression"]["four_cycle"],
+                 "two_cycle_ops_per_compression": mix["per_compression"]["two_cycle"],
+                 "cycles_per_algorithmic_op": mix["cycles_per_algorithmic_op"], "source": src}
+        if pm is None:  # no issue study committed: the linear model
+            pm = lin
+            roof.update({"peak_mix": lin_d["peak"], "frac_mix": lin_d["frac"], "mix": lin_d})
+        else:
+            lin_d["note"] = ("linear 2-/4-cycle model: unreachable on gfx950, a mixed stream "
+                             "issues ~4 cycles per instruction (profiles/r5/valu_issue_model.json)")
+            roof["linear_mix_model"] = lin_d
     clk, csrc = newest_profile(f"pmc_clock_{workload}.json")
     if clk and clk.get("clock_ghz"):
         roof["held_clock_ghz"] = clk["clock_ghz"]
         roof["held_clock_source"] = csrc
-        if mix:
+        if pm:
             roof["frac_mix_at_held_clock"] = round(achieved / (pm * clk["clock_ghz"] / 2.4), 4)
     # where the rest goes: issued VALU wave-instructions
     # (PMC SQ_INSTS_VALU of the same command, scripts/gpu_r4_measure.sh insts)
@@ -605,7 +626,7 @@ def mix_roofline(roof, achieved, kernel, workload, comp=0):
         d = {"valu_wave_instructions_issued": int(issued),
              "valu_wave_instructions_algorithmic": int(alg_wi),
              "issued_over_algorithmic": round(issued / alg_wi, 4), "source": isrc}
-        if mix and clk and clk.get("clock_ghz"):
+        if pm and clk and clk.get("clock_ghz"):
             cf = clk["clock_ghz"] / 2.4
             d["clock_factor"] = round(cf, 4)
             d["issue_efficiency_left"] = round(roof["frac_mix"] / cf / (alg_wi / issued), 4)

@@ -13,12 +13,17 @@
 // (open addressing, dedup.hip).  The compressed placement a layer's DICT
 // records copy (offset, size, flags) stays on the host: only the blob writer
 // reads it.
+#include <errno.h>
+#include <fcntl.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
+#include <thread>
 
 #include "blob.hpp"
 #include "engine_internal.hpp"
@@ -277,7 +282,8 @@ int parse_v5_dict(ngpu_engine *e, const char *path, const std::vector<uint8_t> &
 // 6 engine, RAFS v5 for FsVersion 5; the other pairings are nydus-image's
 // "inconsistent RAFS version" error.
 int read_dict_bootstrap(ngpu_engine *e, const char *path, uint64_t file_size,
-                        std::vector<uint8_t> *recs_out, std::vector<uint8_t> *blobs_out) {
+                        std::vector<uint8_t> *recs_out, std::vector<uint8_t> *blobs_out,
+                        uint64_t *table_at) {
   FILE *f = fopen(path, "rb");
   if (!f) return fail(e, NGPU_EIO, "open chunk dict %s", path);
   uint8_t sb[kRafsV6ExtSuperBlockOffset + 256];
@@ -327,7 +333,14 @@ int read_dict_bootstrap(ngpu_engine *e, const char *path, uint64_t file_size,
   else if (cts % 80 || bts % 256 || cto > file_size || cts > file_size - cto || bto > file_size ||
            bts > file_size - bto)
     rc = fail(e, NGPU_EFORMAT, "chunk dict %s: bad chunk/blob table bounds", path);
-  if (!rc) {
+  if (!rc && table_at) {  // v6, records left in the file: the caller streams them
+    table_at[0] = cto;
+    table_at[1] = cts;
+    recs_out->clear();
+    blobs_out->resize(bts);
+    if (read_at(f, blobs_out->data(), bts, bto) != 0)
+      rc = fail(e, NGPU_EIO, "chunk dict %s: short read", path);
+  } else if (!rc) {
     recs_out->resize(cts);
     blobs_out->resize(bts);
     if (read_at(f, recs_out->data(), cts, cto) != 0 || read_at(f, blobs_out->data(), bts, bto) != 0)
@@ -339,15 +352,142 @@ int read_dict_bootstrap(ngpu_engine *e, const char *path, uint64_t file_size,
 
 namespace {
 
+// A RAFS v6 chunk table streamed from the file into HBM:
+// 1M-record pieces (80 MB) go through three pinned buffers; kReadThreads host
+// threads pread a piece (page cache or disk) and scan it (blob index bound,
+// the compressed placements the blob writer keeps on the host) while the
+// previous pieces cross PCIe and the unpack kernel turns them into dict
+// records, so the file read, the H2D copy and the unpack overlap instead of
+// following one another over the whole table.  Same records, same table
+// order, same checks as dict_from_records.
+constexpr uint64_t kStreamPiece = 1u << 20;      // records per piece
+constexpr uint64_t kStreamMinBytes = 256u << 20;  // smaller tables: one read, dict_from_records
+constexpr int kReadThreads = 8;
+
+int pread_full(int fd, uint8_t *dst, uint64_t n, uint64_t off) {
+  while (n) {
+    const ssize_t r = pread(fd, dst, n, (off_t)off);
+    if (r <= 0) {
+      if (r < 0 && errno == EINTR) continue;
+      return -1;
+    }
+    dst += r, n -= (uint64_t)r, off += (uint64_t)r;
+  }
+  return 0;
+}
+
+int dict_stream_v6(ngpu_engine *e, const char *path, uint64_t cto, uint64_t m,
+                   const std::vector<uint8_t> &blobs, ngpu_dict **out) {
+  DeviceGuard dg(e->device);
+  BuildStream bs(e->device);
+  if (!bs.s) return fail(e, NGPU_EHIP, "chunk dict: no build stream");
+  if (m >= 0xFFFFFFFFull)
+    return fail(e, NGPU_EINVAL, "chunk dict too large (%llu entries)", (unsigned long long)m);
+  const uint32_t n_blobs = (uint32_t)(blobs.size() / 256);
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return fail(e, NGPU_EIO, "open chunk dict %s", path);
+  ngpu_dict *d = dict_new(e);
+  uint8_t *pin[3] = {}, *tmp[2] = {};
+  hipEvent_t ev[3] = {};
+  int rc = dict_alloc(e, d, m, n_blobs);
+  for (int i = 0; i < 3 && !rc; ++i)
+    if (hipHostMalloc((void **)&pin[i], kStreamPiece * 80, hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
+      rc = fail(e, NGPU_ENOMEM, "chunk dict: pinned staging allocation failed");
+  for (int i = 0; i < 2 && !rc; ++i)
+    if (hipMalloc((void **)&tmp[i], kStreamPiece * 80) != hipSuccess)
+      rc = fail(e, NGPU_ENOMEM, "chunk dict: staging allocation failed");
+  if (!rc) d->place.resize(m);
+  if (!rc && n_blobs) d->blob_table.assign(blobs.begin(), blobs.end());
+  DictRec *rec = const_cast<DictRec *>(d->dev.rec);
+  uint32_t nb = 0;
+  for (uint64_t a = 0, k = 0; a < m && !rc; a += kStreamPiece, ++k) {
+    const uint64_t cnt = std::min(kStreamPiece, m - a);
+    uint8_t *h = pin[k % 3];
+    if (k >= 3 && hipEventSynchronize(ev[k % 3]) != hipSuccess) {  // its last copy is done
+      rc = fail(e, NGPU_EHIP, "chunk dict: upload failed");
+      break;
+    }
+    // read + scan the piece on kReadThreads threads (disjoint record ranges)
+    std::atomic<int> bad{0};
+    uint32_t tnb[kReadThreads] = {};
+    std::vector<std::thread> th;
+    const uint64_t per = (cnt + kReadThreads - 1) / kReadThreads;
+    for (int t = 0; t < kReadThreads; ++t) {
+      const uint64_t r0 = std::min(cnt, per * t), r1 = std::min(cnt, per * (t + 1));
+      if (r0 == r1) continue;
+      th.emplace_back([&, r0, r1, t] {
+        if (pread_full(fd, h + 80 * r0, 80 * (r1 - r0), cto + 80 * (a + r0))) {
+          bad = 1;
+          return;
+        }
+        uint32_t x = 0;
+        for (uint64_t i = r0; i < r1; ++i) {
+          const RafsV6ChunkInfo *r = reinterpret_cast<const RafsV6ChunkInfo *>(h + 80 * i);
+          x = std::max(x, r->blob_index + 1);
+          d->place[a + i] = DictPlace{r->compressed_offset, r->compressed_size, r->flags};
+        }
+        tnb[t] = x;
+      });
+    }
+    for (auto &x : th) x.join();
+    for (uint32_t x : tnb) nb = std::max(nb, x);
+    if (bad) {
+      rc = fail(e, NGPU_EIO, "chunk dict %s: short read", path);
+      break;
+    }
+    if (hipMemcpyAsync(tmp[k % 2], h, cnt * 80, hipMemcpyHostToDevice, bs.s) != hipSuccess) {
+      rc = fail(e, NGPU_EHIP, "chunk dict: upload failed");
+      break;
+    }
+    launch_dict_unpack(tmp[k % 2], cnt, nullptr, (uint32_t)a, rec + a, bs.s);
+    if (hipEventRecord(ev[k % 3], bs.s) != hipSuccess) rc = fail(e, NGPU_EHIP, "chunk dict: unpack failed");
+  }
+  close(fd);
+  if (!rc && hipStreamSynchronize(bs.s) != hipSuccess) rc = fail(e, NGPU_EHIP, "chunk dict: unpack failed");
+  if (rc) (void)hipStreamSynchronize(bs.s);
+  for (uint8_t *x : tmp)
+    if (x) (void)hipFree(x);
+  for (int i = 0; i < 3; ++i) {
+    if (pin[i]) (void)hipHostFree(pin[i]);
+    if (ev[i]) (void)hipEventDestroy(ev[i]);
+  }
+  if (!rc && n_blobs && nb > n_blobs)
+    rc = fail(e, NGPU_EFORMAT, "chunk dict record points at blob %u of %u", nb - 1, n_blobs);
+  if (!rc && nb > (1u << 20)) rc = fail(e, NGPU_EINVAL, "chunk dict blob index %u too large", nb - 1);
+  if (!rc && !n_blobs) d->dev.n_blobs = nb;
+  if (!rc) rc = dict_build(e, d, bs.s);
+  if (rc) {
+    dict_unref(d);
+    return rc;
+  }
+  *out = d;
+  return 0;
+}
+
 // Parse + check + load a RAFS v5/v6 chunk-dict bootstrap (no engine lock).
 int dict_load_file(ngpu_engine *e, const char *path, const struct stat &st, ngpu_dict **out) {
   std::vector<uint8_t> recs, blobs;
-  int rc = read_dict_bootstrap(e, path, (uint64_t)st.st_size, &recs, &blobs);
+  uint64_t table[2] = {0, 0};
+  int rc = read_dict_bootstrap(e, path, (uint64_t)st.st_size, &recs, &blobs, table);
   if (rc) return rc;
   ngpu_dict *d = nullptr;
-  if ((rc = dict_from_records(e, recs.data(), recs.size() / 80, blobs.data(), blobs.size() / 256, &d,
-                              nullptr)))
-    return rc;
+  if (table[1] >= kStreamMinBytes) {  // v6 and large: stream it
+    if ((rc = dict_stream_v6(e, path, table[0], table[1] / 80, blobs, &d))) return rc;
+  } else {
+    if (table[1]) {  // v6, small: one read
+      recs.resize(table[1]);
+      FILE *f = fopen(path, "rb");
+      rc = (!f || read_at(f, recs.data(), table[1], table[0]))
+               ? fail(e, NGPU_EIO, "chunk dict %s: short read", path)
+               : 0;
+      if (f) fclose(f);
+      if (rc) return rc;
+    }
+    if ((rc = dict_from_records(e, recs.data(), recs.size() / 80, blobs.data(), blobs.size() / 256,
+                                &d, nullptr)))
+      return rc;
+  }
   d->path = path;
   d->st_dev = st.st_dev;
   d->st_ino = st.st_ino;

@@ -236,7 +236,8 @@ uint64_t next_pow2(uint64_t x);
 int dict_from_records(ngpu_engine *e, const uint8_t *recs, uint64_t m, const uint8_t *blobs,
                       uint32_t n_blobs, ngpu_dict **out, const uint32_t *gids);
 int read_dict_bootstrap(ngpu_engine *e, const char *path, uint64_t file_size,
-                        std::vector<uint8_t> *recs, std::vector<uint8_t> *blobs);
+                        std::vector<uint8_t> *recs_out, std::vector<uint8_t> *blobs_out,
+                        uint64_t *table_at = nullptr);
 // Node dicts: the replica on e's device, or (partitioned) route the probe of
 // n digests (byte stride) over the parts into e's workspace hits, ordered on
 // stream s.  *hits = the per-chunk hits with global entry ids.

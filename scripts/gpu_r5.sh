@@ -22,8 +22,25 @@ for s in "$@"; do
       bash scripts/gpu_r5_valu.sh "$TAG/valu" > "$OUT/valu.log" 2>&1
       ok $? valu
       cat "$OUT/valu.log" | cut -c1-220 ;;
+    valu3)
+      for cfg in "512 1" "1024 1" "256 1"; do
+        set -- $cfg
+        for v in mix_s compiled_bar mix_x4a4_bar compiled; do
+          timeout -k 10 120 ./tools/valu_bank $v $1 $2 >> "$OUT/valu3.jsonl" 2>> "$OUT/valu3.err"
+          ok $? "valu3 $v $1 $2"
+        done
+      done
+      wc -l "$OUT/valu3.jsonl" ;;
+    valu2)
+      bash scripts/gpu_r5_valu2.sh "$TAG/valu2" > "$OUT/valu2.log" 2>&1
+      ok $? valu2
+      tail -3 "$OUT/valu2.log" ;;
     suite)
-      timeout -k 10 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ${PYK:-} > "$OUT/pytest_gpu.log" 2>&1
+      if [ -n "${PYK:-}" ]; then
+        timeout -k 10 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread -k "$PYK" > "$OUT/pytest_gpu.log" 2>&1
+      else
+        timeout -k 10 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+      fi
       ok $? suite
       tail -1 "$OUT/pytest_gpu.log" ;;
     smoke)

@@ -352,9 +352,13 @@ def _random_layer(rng, total, chunk_size):
     return data, np.array(chunks, dtype=nydus_gpu.CHUNK_DTYPE)
 
 
-def test_c3_sha256_dict_bootstrap_1m_entries_vs_oracle(oracle, tmp_path):
+@pytest.mark.parametrize("m", [1_200_000, 4_000_000])
+def test_c3_sha256_dict_bootstrap_1m_entries_vs_oracle(oracle, tmp_path, m):
     """BASELINE configs[2] shape at test size: sha256 digester, 1 MiB chunks,
-    a chunk dict of >= 1M entries loaded from a sha256 RAFS v6 bootstrap, with
+    a chunk dict of >= 1M entries loaded from a sha256 RAFS v6 bootstrap (4M
+    entries = 320 MB of chunk table: the streamed load, csrc/dict.hip
+    dict_stream_v6, four 1M-record pieces; the later duplicates sit in
+    other pieces than their first rows), with
     planted layer digests, keys duplicated later in the table (first wins),
     usize == 0 wildcards, size mismatches (miss) and 9 inner blobs; every
     decision, index, offset and blob equals the oracle's."""
@@ -368,7 +372,6 @@ def test_c3_sha256_dict_bootstrap_1m_entries_vs_oracle(oracle, tmp_path):
         ch["length"][i] = ln
         data[ch["offset"][i]:ch["offset"][i] + ln] = data[ch["offset"][j]:ch["offset"][j] + ln]
     dig = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "sha256")
-    m = 1_200_000
     recs = np.zeros(m, rafs.CHUNK_INFO_DTYPE)
     recs["block_id"] = rng.integers(0, 256, (m, 32), dtype=np.uint8)
     recs["uncompressed_size"] = S

@@ -75,6 +75,23 @@ def streams(compiled_s=None):
                            else f"v_alignbit_b32 v{i % 8}, v{i % 8}, v{i % 8}, 7") for i in range(256)]
     v["mix_x4a4_same"] = [(f"v_xor_b32 v{i % 8}, v{i % 8}, v{8 + i % 8}" if (i // 4) % 2 == 0
                            else f"v_alignbit_b32 v{i % 8}, v{i % 8}, v{i % 8}, 7") for i in range(256)]
+    # slow / fast runs of length n (alignbit then xor, 8 chains): the cost of
+    # a switch between the 4-cycle and the 2-cycle ops
+    for n in (1, 8, 16, 32):
+        ops = []
+        while len(ops) < 256:
+            ops += [f"v_alignbit_b32 v{i % 8}, v{i % 8}, v{i % 8}, 7" for i in range(n)]
+            ops += [f"v_xor_b32 v{i % 8}, v{i % 8}, v{9 + i % 8}" for i in range(n)]
+        v[f"mix_s{n}f{n}"] = ops[:256]
+    # the x4a4 mix with an s_barrier every k ops: waves of one workgroup
+    # that share a SIMD kept in phase, so both sit in a 2-cycle run together
+    for k in (32, 128):
+        ops = []
+        for i, o in enumerate(v["mix_x4a4_diff"]):
+            ops.append(o)
+            if (i + 1) % k == 0:
+                ops.append("s_barrier")
+        v[f"mix_x4a4_bar{k}"] = ops
     # one BLAKE3 compression (672 G ops) under three register assignments
     # state word k -> VGPR: "conflict" = k (a column step's a,b,c,d share a bank)
     v["comp_conflict"] = compression(list(range(16)), [16 + j for j in range(16)])
@@ -83,6 +100,13 @@ def streams(compiled_s=None):
     v["comp_distinct"] = compression(role, [16 + 4 * (j // 2) + 2 + (j % 2) for j in range(16)])
     if compiled_s:
         v["compiled"] = compiled_stream(compiled_s)
+        for k in (48, 96):  # a barrier after every (second) G4 step
+            ops = []
+            for i, o in enumerate(v["compiled"]):
+                ops.append(o)
+                if (i + 1) % k == 0:
+                    ops.append("s_barrier")
+            v[f"compiled_bar{k}"] = ops
     return v
 
 
@@ -144,7 +168,7 @@ def main():
                 "    rec[4 * w + 3] = __builtin_amdgcn_s_getreg(0x7814);  // HW_REG_XCC_ID, 16 bits",
                 "  }",
                 "}", ""]
-        names.append((name, len(ops), max(rs) + 1))
+        names.append((name, sum(1 for o in ops if o.startswith("v_")), max(rs) + 1))
     out.append("struct V { const char *name; void (*k)(uint64_t *, uint32_t); int ops; int regs; };")
     out.append("static const V kV[] = {")
     out += [f'  {{"{n}", k_{n}, {c}, {r}}},' for n, c, r in names]
