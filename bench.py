@@ -219,7 +219,7 @@ WORKLOADS = {
     "c3": dict(desc="C3: 16 GiB layer, 1 MiB chunks, sha256, vs 200M-entry chunk dict in HBM "
                     "(30% of the layer's chunks planted)",
                n_files=4096, file_size=4 * MiB, chunk=MiB, digester="sha256", layers=1,
-               dict_entries=200_000_000, plant=0.3),
+               dict_entries=200_000_000, plant=0.3, dict_file=True),
     "c3-64k": dict(desc="C3 layer with 64 KiB chunks: 16 GiB, sha256, 200M-entry chunk dict "
                         "(262144 chunks: one lane per chunk fills the chip)",
                    n_files=4096, file_size=4 * MiB, chunk=64 * 1024, digester="sha256", layers=1,
@@ -474,6 +474,64 @@ def sharded_dict_extra(torch, dist, eng, buf, d_ch, n, stream, rank, world, back
             "probe_enqueue_ms_median_max_rank": round(float(red[:, 3].max()) * 1e3, 3),
             "dict_hits_all_ranks": hits_all, "planted_all_ranks": planted_all,
             "hits_ok": hits_all == planted_all, "_elapsed": el_max}
+
+
+def dict_from_file(torch, nydus_gpu, eng, dd, us, bl, ix, wl, where):
+    """C3's chunk dict through PackOption.ChunkDictPath: the dict's m records
+    (digest, uncompressed size, blob, index: the arrays the device build
+    used, so the decisions do not change) written as a RAFS v6 bootstrap
+    (16 GB of chunk table for 200M entries; not timed), then ngpu_dict_open
+    timed end to end -- read (page cache), parse, H2D, unpack, table build
+    (csrc/dict.hip dict_stream_v6) -- and made the engine's dict for the
+    timed steps.  The file is deleted afterwards.  A write failure (disk
+    space) is reported and the device-built dict stays."""
+    import shutil
+    from nydus_gpu import rafs
+    m, S = dd.shape[0], wl["chunk"]
+    path = os.path.join(where or os.environ.get("TMPDIR") or "/tmp", f"nydus-c3-dict-{os.getpid()}.boot")
+    need = m * 80 + (1 << 20)
+    free = shutil.disk_usage(os.path.dirname(path)).free
+    if free < need * 1.1:
+        return {"skipped": f"{free / 1e9:.1f} GB free at {os.path.dirname(path)}, {need / 1e9:.1f} GB needed"}
+    sha = wl["digester"] == "sha256"
+    blobs = rafs.make_blob_table([f"{b:064x}" for b in range(8)], S, digester=wl["digester"])
+    step = 8 << 20
+
+    def pieces():
+        for a in range(0, m, step):
+            b = min(m, a + step)
+            r = torch.zeros((b - a, 80), dtype=torch.uint8, device="cuda")
+            r[:, :32] = dd[a:b]
+            r[:, 32:36] = bl[a:b].contiguous().view(torch.uint8).view(b - a, 4)
+            r[:, 40:44] = us[a:b].contiguous().view(torch.uint8).view(b - a, 4)  # compressed_size
+            r[:, 44:48] = us[a:b].contiguous().view(torch.uint8).view(b - a, 4)  # uncompressed_size
+            r[:, 72:76] = ix[a:b].contiguous().view(torch.uint8).view(b - a, 4)
+            yield r.cpu().numpy().view(rafs.CHUNK_INFO_DTYPE).reshape(-1)
+    try:
+        t0 = time.perf_counter()
+        size = rafs.write_v6_dict_file(path, m, S, pieces(), flags=0x8 if sha else 0x4, blobs=blobs)
+        write_s = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d = eng.dict_open(path)
+        open_s = time.perf_counter() - t0
+        entries = d.entries
+        eng.set_dict(d)  # the engine's dict for the timed steps (replaces the device build)
+        d.release()
+    except (OSError, nydus_gpu.NgpuError) as ex:
+        return {"error": f"{type(ex).__name__}: {ex}"[:300]}
+    finally:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
+    assert entries == m, (entries, m)
+    return {"path": "ngpu_dict_open (PackOption.ChunkDictPath, builder.go:122-124)", "entries": m,
+            "file_bytes": size, "chunk_table_bytes": m * 80, "open_s": round(open_s, 3),
+            "chunk_table_gbs": round(m * 80 / open_s / 1e9, 2),
+            "write_s_untimed": round(write_s, 2),
+            "note": "file just written (page cache); open = read + parse + H2D + unpack + "
+                    "table build, streamed in 1M-record pieces; this dict serves the timed steps"}
 
 
 def merge_extra(nydus_gpu, ch, res, n_layers, per_layer, S, dict_host):
@@ -818,7 +876,7 @@ def node_e2e(torch, dist, nydus_gpu, buf, wl, stride, device, backend, sample_by
 SUB_KEYS = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "stage_ms", "roofline",
             "cpu_baseline", "speedup_vs_cpu", "speedup_vs_cpu_single_stream", "dict",
             "probe_roofline", "merge", "decisions", "digest_check_past_4gib", "n_gpus", "sharded_dict",
-            "e2e_pcie", "tar_host_path", "ranks")
+            "e2e_pcie", "tar_host_path", "ranks", "modes", "speedup_vs_cpu_device", "bound")
 
 
 def child_line(cmd, timeout_s, env=None):
@@ -849,6 +907,11 @@ def sub_entries(args):
     each a full bench line of its own (value, ms_per_step, roofline,
     cpu_baseline), run as children after the headline is measured."""
     out = {}
+    for key, wl in (("packs_c1", "c1"), ("packs_c1_sha256", "c1-sha256")):
+        # K = 32 concurrent converter.Pack calls of C1-size layers (batched closes)
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", wl, "--packs", "32",
+               "--steps", "10", "--warmup", "3", "--no-sub"]
+        out[key] = child_line(cmd, 300)
     for key, wl in (("c1", "c1"), ("c3", "c3"), ("c5_1000", "c5-1000")):
         # C1 (configs[0], the reference's CPU-runnable case: one ~10 MB layer)
         # keeps its host path (ngpu_pack_tar from pinned host memory) and more
@@ -1018,6 +1081,156 @@ def concurrent_bench(args):
             "us_per_layer": round(elapsed / args.steps / K * 1e6, 2),
             "host_submit_us_per_layer": round(t_submit / args.steps / K * 1e6, 2),
             "decisions": {"NEW": int(kinds[0]), "INTRA": int(kinds[1]), "DICT": int(kinds[2])}}
+    print(json.dumps(line), flush=True)
+
+
+def packs_bench(args):
+    """`--packs K` (tar workloads, c1 / c1-sha256): K converter.Pack calls at
+    once on ONE engine, one host thread each (containerd converting an image's
+    layers concurrently: one LayerConvertFunc per layer, convert_unix.go:822),
+    each pack its own distinct C1-size layer (alpine-like, seeds differ) fed
+    from host memory in 1 MiB writes.  A round = the K packs opened, written,
+    closed together; their closes coalesce into shared launch sets
+    (csrc/batch.hip).  Modes, each `steps` rounds after
+    `warmup`:
+      decisions        -- close(): chunk list + digests + dedup decisions back;
+      decisions_no_batch -- the same with NGPU_FLAG_NO_BATCH (a launch set per pack);
+      stream_zstd      -- converter.Pack's own path: early emission
+                          (ngpu_pack_set_output) of the nydus stream, zstd, to
+                          a null sink.
+    value = all layers' file bytes / wall time (PCIe-inclusive: the tars start
+    in host memory).  device_gbs: the same bytes over the batched launch
+    sets' device time (digest + dedup, HIP events).  cpu_baseline: the CPU
+    digest+dedup stage on the same K layers, one layer per thread, on the
+    host's cores."""
+    import threading
+    import nydus_gpu
+    wl = dict(WORKLOADS[args.workload])
+    if not wl.get("tar"):
+        raise SystemExit("--packs takes a tar workload (c1, c1-sha256)")
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import layers
+    K = args.packs
+    tars = [layers.alpine_like_tar(0xA1F1E + i) for i in range(K)]
+    chs = [nydus_gpu.tar_chunks(t, wl["chunk"]) for t in tars]
+    file_bytes = sum(int(c["length"].sum()) for c in chs)
+    tar_bytes = sum(len(t) for t in tars)
+    arrs = [np.frombuffer(t, np.uint8) for t in tars]
+
+    class Null:
+        def write(self, b):
+            return len(b)
+
+    def run(flags, stream):
+        # 16 MiB staging slots: a C1 layer fits one (it closes in a batch),
+        # and 32 packs x 2 slots pin 1 GiB instead of 16
+        eng = nydus_gpu.Engine(device=0, digester=wl["digester"], chunk_size=wl["chunk"],
+                               flags=flags, timing=True, staging_bytes=16 << 20)
+        meet = threading.Barrier(K + 1)
+        errs = []
+        kinds = np.zeros(3, np.int64)
+        mu = threading.Lock()
+
+        def worker(i):
+            try:
+                for r in range(args.warmup + args.steps):
+                    meet.wait()
+                    w = eng.pack(retain=stream)
+                    if stream:
+                        w.set_output(Null(), compressor="zstd")
+                    a = arrs[i]
+                    for o in range(0, a.size, 1 << 20):
+                        w.write(a[o:o + (1 << 20)])
+                    if stream:
+                        _, rs, _, _ = w.finish(None)
+                    else:
+                        _, rs, _ = w.close()
+                    if r == args.warmup + args.steps - 1:
+                        with mu:
+                            kinds[:] += np.bincount(rs["kind"], minlength=3)[:3]
+                    meet.wait()
+            except Exception as ex:
+                errs.append(repr(ex))
+                meet.abort()
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(K)]
+        for t in th:
+            t.start()
+        try:
+            for r in range(args.warmup):
+                meet.wait()
+                meet.wait()
+            b0 = eng.batch_stats()
+            t0 = time.perf_counter()
+            for r in range(args.steps):
+                meet.wait()  # round r starts
+                meet.wait()  # every pack of round r closed
+            el = time.perf_counter() - t0
+        except threading.BrokenBarrierError:
+            el = None
+        for t in th:
+            t.join()
+        if errs or el is None:
+            eng.close()
+            raise RuntimeError(f"packs: {errs[:2]}")
+        b1 = eng.batch_stats()
+        nb = b1["batches"] - b0["batches"]
+        dev = None
+        if nb:
+            tms = [eng.timing_at(k) for k in range(min(nb, 64))]
+            dev_ms = sum(t["total_ms"] for t in tms)
+            packs_in = (b1["packs"] - b0["packs"]) * min(nb, 64) / nb
+            dev = round(file_bytes / K * packs_in / (dev_ms / 1e3) / 1e9, 2) if dev_ms else None
+        eng.close()
+        return {"gbs": round(file_bytes * args.steps / el / 1e9, 2),
+                "ms_per_round": round(el / args.steps * 1e3, 3),
+                "device_gbs": dev, "launch_sets": nb, "packs_batched": b1["packs"] - b0["packs"],
+                "most_packs_in_one_set": b1["max_packs"],
+                "decisions_last_round": {"NEW": int(kinds[0]), "INTRA": int(kinds[1]),
+                                         "DICT": int(kinds[2])}}
+
+    modes = {"decisions": run(0, False),
+             "decisions_no_batch": run(nydus_gpu.FLAG_NO_BATCH, False),
+             "stream_zstd": run(0, True)}
+    cpu = None
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_py
+        from concurrent.futures import ThreadPoolExecutor
+        aff, quota = host_cpus()
+        threads = args.cpu_threads or (min(aff, int(-(-quota // 1))) if quota else aff)
+        ochs = [c.view(oracle_py.CHUNK_DTYPE) for c in chs]
+        oracle_py.cpu_digest_dedup(arrs[0], ochs[0][:4], wl["digester"], 1)
+
+        def one_round(ex):
+            list(ex.map(lambda i: oracle_py.cpu_digest_dedup(arrs[i], ochs[i], wl["digester"], 1),
+                        range(K)))
+        with ThreadPoolExecutor(threads) as ex:
+            one_round(ex)
+            reps, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < 3.0 and reps < 200:
+                one_round(ex)
+                reps += 1
+            el = time.perf_counter() - t0
+        cpu = {"value": round(file_bytes * reps / el / 1e9, 2), "unit": "GB/s", "cores": threads,
+               "kind": "port", "sample": f"the same {K} layers ({file_bytes / MiB:.1f} MiB of file "
+                                         f"data), digest+dedup, one layer per thread, "
+                                         f"{oracle_py.cpu_impl()}; {reps} rounds"}
+    line = {"metric": "GB/s of layer data chunk-hashed+deduped (node)",
+            "value": modes["decisions"]["gbs"], "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": modes["decisions"]["ms_per_round"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic alpine-like layer tars (tests/golden/layers.py), host memory",
+            "config": {"workload": f"{K} concurrent converter.Pack calls of distinct C1-size "
+                                   f"layers on one engine ({wl['digester']}, 1 MiB chunks)",
+                       "name": args.workload, "packs": K, "file_bytes_per_round": file_bytes,
+                       "tar_bytes_per_round": tar_bytes, "batch_window_us": 250},
+            "modes": modes, "cpu_baseline": cpu,
+            "bound": "PCIe H2D of the tars (~50 GB/s) and the host copies into pinned staging; "
+                     "sha256: one 1 MiB chunk's chain per launch set (~21 ms)"}
+    if cpu:
+        line["speedup_vs_cpu"] = round(modes["decisions"]["gbs"] / cpu["value"], 2)
+        if modes["decisions"]["device_gbs"]:
+            line["speedup_vs_cpu_device"] = round(modes["decisions"]["device_gbs"] / cpu["value"], 2)
     print(json.dumps(line), flush=True)
 
 
@@ -1355,6 +1568,10 @@ def main():
     ap.add_argument("--digester", choices=["blake3", "sha256"], default=None,
                     help="override the workload's digester (e.g. the sha256 small-layer crossover sweep)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dict-file", action="store_true",
+                    help="c3: skip the ChunkDictPath file (build the dict from device arrays only)")
+    ap.add_argument("--dict-dir", default="", help="where c3 writes its ChunkDictPath file "
+                    "(default $TMPDIR or /tmp)")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--d2h", choices=["auto", "same", "copy"], default="auto",
                     help="result-table D2H: on the call's stream (same) or on a copy stream "
@@ -1380,6 +1597,9 @@ def main():
                     help="tar workloads: one engine converts K layers at once, one stream each")
     ap.add_argument("--threads", action="store_true",
                     help="--streams/--engines: one submitting host thread per stream")
+    ap.add_argument("--packs", type=int, default=0,
+                    help="tar workloads: K concurrent converter.Pack calls per round on one engine "
+                         "(batched closes); see packs_bench")
     ap.add_argument("--engines", type=int, default=1,
                     help="tar workloads: K engines on device 0 convert layers concurrently")
     ap.add_argument("--no-sub", action="store_true",
@@ -1402,6 +1622,8 @@ def main():
         return node_bench(args)
     if args.engines > 1 or args.streams > 1:
         return concurrent_bench(args)
+    if args.packs:
+        return packs_bench(args)
 
     import torch
     import nydus_gpu
@@ -1506,11 +1728,19 @@ def main():
         dict_host = None
         if wl.get("merge") and world == 1:  # the C5 Merge needs the dict bootstrap
             dict_host = (dd.cpu().numpy(), us.cpu().numpy(), bl.cpu().numpy(), ix.cpu().numpy())
+        dict_file = None
+        if wl.get("dict_file") and not args.no_dict_file and rank == 0:
+            # ChunkDictPath itself: the same m records as a
+            # RAFS v6 bootstrap on disk, opened through ngpu_dict_open (read,
+            # parse, H2D, build); that dict then serves the timed steps
+            dict_file = dict_from_file(torch, nydus_gpu, eng, dd, us, bl, ix, wl, args.dict_dir)
         del dd, us, bl, ix
         torch.cuda.empty_cache()
         extra["dict"] = {"entries": m, "entries_this_gpu": local_m, "build_s": round(build_s, 3),
                          "build_Mentries_s": round(local_m / build_s / 1e6, 1),
                          "expected_dict_hits": expect_dict}
+        if dict_file:
+            extra["dict"]["chunk_dict_path"] = dict_file
         if probe:
             extra["probe_roofline"] = probe
 

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define NGPU_ABI_VERSION 5
+#define NGPU_ABI_VERSION 6
 
 /* PackOption.Digester (API extension; maps to nydus-image --digester). */
 enum ngpu_digester { NGPU_DIGEST_BLAKE3 = 0, NGPU_DIGEST_SHA256 = 1 };
@@ -117,6 +117,13 @@ typedef struct {
  * compression on a quad of lanes; this flag keeps the multi-kernel grid path
  * and one lane per leaf (same results). */
 #define NGPU_FLAG_GRID_STAGES 0x4u
+/* Packs whose whole layer fit one staging slot and that close at about the
+ * same time on one engine share ONE digest + multi-layer dedup launch set
+ * (round 5: containerd converting an image's small layers concurrently);
+ * the first to close waits for every other pack open on the engine to close,
+ * at most 250 us.  This flag gives every pack its own launches (A/B, or a
+ * caller whose packs must never wait for each other).  Same results. */
+#define NGPU_FLAG_NO_BATCH 0x8u
 /* Tuning (benchmarks only): bits 8..10 = 1 + BLAKE3 load mode (0 plain loads
  * with the whole-leaf fast path, 1 non-temporal loads, 2 next-block prefetch,
  * 3 both, 5 plain loads without the fast path); 0 = library default.  Every
@@ -394,6 +401,9 @@ void ngpu_free_host(void *p);
 /* Stage timings of the last ngpu_process / ngpu_process_device call on this
  * engine (synchronises on the recorded events).  NGPU_EINVAL unless the
  * engine was created with NGPU_FLAG_TIMING. */
+/* Batched Pack closes so far (NGPU_FLAG_NO_BATCH): out[0] launch sets,
+ * out[1] packs closed in them, out[2] the most packs in one. */
+int ngpu_batch_stats(ngpu_engine *eng, uint64_t out[3]);
 int ngpu_last_timing(ngpu_engine *eng, ngpu_timing *out);
 /* The same for the call `back` calls before the last one (0 = the last).
  * The engine keeps the events of its last 64 calls, so a caller can time a
@@ -451,7 +461,14 @@ void ngpu_pack_abort(ngpu_pack *p);
  * NGPU_NODE_EXCHANGE_COPY in `mode` (or when peer access between two listed
  * devices is unavailable) the ABI 3 exchange runs instead: every digest to
  * every owner and every owner's n hits back by hipMemcpyPeerAsync (W x the
- * bytes).  Peer access between the listed devices is enabled at creation. */
+ * bytes).  Peer access between the listed devices is enabled at creation.
+ * UNVERIFIED ON DISTINCT GPUs: every test so far lists one GPU several times
+ * (the copies and peer stores then stay inside one HBM); the routed
+ * exchange's peer stores, the copy exchange and the RCCL node step first
+ * meet separate GPUs in the driver's multi-GPU bench, whose `node_cabi` entry
+ * runs all three against a replicated dict and reports whether their hits
+ * agree (hits_equal).  Until that has passed, a caller that needs certainty
+ * uses NGPU_NODE_DICT_REPLICATE (no exchange). */
 typedef struct ngpu_node ngpu_node;
 int ngpu_node_create(const int32_t *devices, uint32_t n, const ngpu_config *cfg, ngpu_node **out);
 void ngpu_node_destroy(ngpu_node *node);
@@ -626,8 +643,15 @@ int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
  * table and the 32 KiB dictionaries), blob.digest, image.boot and the TOC; the
  * bootstrap's own blob is the gzip blob (id = its sha256, the digest Merge
  * returns for the layer, converter_test.go TestPackRef), each chunk record
- * carrying the deflate range that produces it.  Layout restated (VERIFY).
- * ngpu_pack_reserve / ngpu_pack_commit are not available (EINVAL). */
+ * carrying the deflate range that produces it.
+ * EXPERIMENTAL: the blob.meta zran layout (ZranInflateContext records, the
+ * zran header words, super flag 0x40, the chunk entry's data word) is
+ * restated from nydus v2.3.0 and NOT pinned by any reference fixture; this
+ * library's own reader (ngpu_ref_chunk_read) round-trips it, nydusd has not
+ * read it.  A chunk whose deflate range or checkpoint offset does not fit its
+ * field (24-bit size, 40-bit offset, 32-bit offsets) fails with NGPU_EFORMAT,
+ * never truncated.  ngpu_pack_reserve / ngpu_pack_commit are not available
+ * (EINVAL). */
 #define NGPU_PACK_OCIREF 0x2u
 /* The reader side of an OCIRef layer (host; what nydusd does with a targz-ref
  * blob): chunk `index` of the layer's own blob, located through `blob_meta`
@@ -716,6 +740,17 @@ typedef struct ngpu_merge_options {
   /* PrefetchPatterns (the builder's stdin, builder.go:238-240, 269):
    * newline-separated paths; NULL or "" = "/" */
   const char *prefetch_patterns;
+  /* ABI 6: targz-ref layers (Layer.OriginalDigest; convert_unix.go:579-587
+   * hands nydus-image --blob-digests / --blob-sizes / --blob-toc-digests,
+   * builder.go:242-253).  NULL = none; else n entries, entry l NULL for a
+   * layer without OriginalDigest: 64 hex chars of the layer's RAFS blob (its
+   * nydus stream) digest, its size, and 64 hex chars of the sha256 of its TOC
+   * entry data (calcBlobTOCDigest, convert_unix.go:541-554).  Recorded in the
+   * layer's own blob record of the merged bootstrap (restated RafsV6Blob
+   * offsets, unpinned). */
+  const char *const *rafs_blob_digests;
+  const uint64_t *rafs_blob_sizes;
+  const char *const *rafs_blob_toc_digests;
 } ngpu_merge_options;
 
 /* ngpu_merge with MergeOption's parent bootstrap and prefetch patterns

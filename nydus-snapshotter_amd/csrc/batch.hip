@@ -1,0 +1,272 @@
+// batch.hip — concurrent small Packs closed as ONE multi-layer launch set
+// (VERDICT r4 item 3).
+//
+// The reference converts an image's layers concurrently, one goroutine and
+// one nydus-image process per layer (pkg/converter/convert_unix.go:467-538,
+// LayerConvertFunc :822).  Behind the ABI each of those layers is a Pack on
+// one shared engine, and a small layer (C1: ~10 MB, a few dozen chunks)
+// leaves most of the chip idle: its digest is bound by one chunk's chain (16
+// compressions per BLAKE3 leaf + the tree levels; for SHA-256 the whole
+// chunk, ~21 ms for 1 MiB), and at most GPU_MAX_HW_QUEUES (4) packs' kernels
+// run side by side.  So Packs that close within a short window share one
+// launch set: their layers' bytes are gathered into one HBM buffer (D2D),
+// their chunk tables concatenated with layer boundaries, and ONE digest
+// stage + ONE multi-layer dedup stage (the C5 path, per-layer semantics:
+// every layer keeps its own intra-layer dict, NEW indices, offsets and blob
+// order) decide them all; each pack gets its own results and stats back.
+// Decisions are identical to one launch per pack (the multi-layer dedup is
+// the per-layer algorithm with layer boundaries).
+//
+// Window: the first pack to close leads; it waits until every pack open on
+// the engine has joined, or kWindowUs, whichever comes first (a lone pack
+// goes at once).  Only packs whose layer fit one staging slot join (their
+// bytes are all in HBM at close); packs with another chunk dict than the
+// leader's wait for the next batch.  NGPU_FLAG_NO_BATCH turns it off.
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+
+#include "engine_internal.hpp"
+
+namespace ngpu {
+
+// The end of one batch: every pack in it waits for this event, the last one
+// to drop its reference destroys it.
+struct BatchEvent {
+  hipEvent_t ev = nullptr;
+  int device = 0;
+  ~BatchEvent() {
+    if (ev) {
+      DeviceGuard g(device);
+      (void)hipEventDestroy(ev);
+    }
+  }
+};
+
+struct Batcher {
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<BatchJob *> open;  // packs waiting for a batch
+  bool leading = false;
+  // the leader's buffers (used under e->mu, reused batch after batch: every
+  // batch runs on stream s, so the next one's copies follow the last kernels)
+  hipStream_t s = nullptr;
+  uint8_t *d_data = nullptr;
+  uint64_t data_cap = 0;
+  ngpu_chunk *d_ch = nullptr;
+  ngpu_result *d_res = nullptr;
+  uint64_t ch_cap = 0;
+  uint64_t *d_lfirst = nullptr;
+  ngpu_layer_stats *d_lst = nullptr;
+  uint64_t l_cap = 0;
+  uint8_t *h_tab = nullptr;  // pinned: chunk table + layer boundaries of one batch
+  uint64_t h_cap = 0;
+  hipEvent_t tab_sent = nullptr;  // the last batch's table upload
+  bool tab_pending = false;
+  uint64_t batches = 0, jobs = 0, max_jobs = 0;
+};
+
+namespace {
+
+constexpr int kWindowUs = 250;
+constexpr size_t kMaxJobs = 256;
+constexpr uint64_t kMaxBytes = 1ull << 30;
+constexpr uint64_t kMaxChunks = 1ull << 20;
+
+template <class T>
+int grow_dev(ngpu_engine *e, Batcher &b, T **p, uint64_t &cap, uint64_t want, bool *synced) {
+  if (want <= cap && *p) return 0;
+  if (!*synced) {  // the last batch may still read it
+    HIP_TRY(e, hipStreamSynchronize(b.s));
+    *synced = true;
+  }
+  if (*p) (void)hipFree(*p), *p = nullptr, cap = 0;
+  uint64_t c = 4096;
+  while (c < want) c *= 2;
+  if (hipMalloc((void **)p, c * sizeof(T)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(e, NGPU_ENOMEM, "batch: device buffer allocation failed");
+  }
+  cap = c;
+  return 0;
+}
+
+// Enqueue one batch (the leader, e->mu taken here).
+int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs) {
+  std::lock_guard<std::mutex> g(e->mu);
+  DeviceGuard dg(e->device);
+  if (!b.s) {
+    HIP_TRY(e, hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking));
+    HIP_TRY(e, hipEventCreateWithFlags(&b.tab_sent, hipEventDisableTiming));
+    e->streams.push_back(b.s);  // lives as long as the engine (ws_lazy_end)
+  }
+  const uint64_t K = jobs.size();
+  std::vector<uint64_t> off(K), first(K + 1, 0);
+  uint64_t bytes = 0;
+  for (uint64_t k = 0; k < K; ++k) {
+    off[k] = bytes;
+    bytes += (jobs[k]->len + 255) & ~255ull;
+    first[k + 1] = first[k] + jobs[k]->n;
+  }
+  const uint64_t N = first[K];
+  bool synced = false;
+  if (int rc = grow_dev(e, b, &b.d_data, b.data_cap, bytes + 64, &synced)) return rc;
+  if (int rc = grow_dev(e, b, &b.d_ch, b.ch_cap, N + 1, &synced)) return rc;
+  uint64_t rcap = b.ch_cap == 0 ? 0 : b.ch_cap;  // results sized with the chunk table
+  if (!b.d_res || synced) {
+    if (b.d_res) (void)hipFree(b.d_res), b.d_res = nullptr;
+    HIP_TRY(e, hipMalloc((void **)&b.d_res, rcap * sizeof(ngpu_result)));
+  }
+  if (int rc = grow_dev(e, b, &b.d_lfirst, b.l_cap, K + 2, &synced)) return rc;
+  if (!b.d_lst || synced) {
+    if (b.d_lst) (void)hipFree(b.d_lst), b.d_lst = nullptr;
+    HIP_TRY(e, hipMalloc((void **)&b.d_lst, b.l_cap * sizeof(ngpu_layer_stats)));
+  }
+  const uint64_t tab = N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t);
+  if (b.tab_pending) {  // the pinned table may still be on its way to the last batch
+    HIP_TRY(e, hipEventSynchronize(b.tab_sent));
+    b.tab_pending = false;
+  }
+  if (tab > b.h_cap) {
+    if (b.h_tab) (void)hipHostFree(b.h_tab), b.h_tab = nullptr, b.h_cap = 0;
+    uint64_t c = 64 << 10;
+    while (c < tab) c *= 2;
+    HIP_TRY(e, hipHostMalloc((void **)&b.h_tab, c, hipHostMallocDefault));
+    b.h_cap = c;
+  }
+  ngpu_chunk *hc = reinterpret_cast<ngpu_chunk *>(b.h_tab);
+  for (uint64_t k = 0; k < K; ++k)
+    for (uint64_t i = 0; i < jobs[k]->n; ++i) {
+      ngpu_chunk c = jobs[k]->h_ch[i];
+      c.offset += off[k];
+      hc[first[k] + i] = c;
+    }
+  memcpy(b.h_tab + N * sizeof(ngpu_chunk), first.data(), (K + 1) * sizeof(uint64_t));
+  // gather: every layer's bytes behind its own copy
+  for (uint64_t k = 0; k < K; ++k) {
+    HIP_TRY(e, hipStreamWaitEvent(b.s, jobs[k]->ready, 0));
+    if (jobs[k]->len)
+      HIP_TRY(e, hipMemcpyAsync(b.d_data + off[k], jobs[k]->d_data, jobs[k]->len,
+                                hipMemcpyDeviceToDevice, b.s));
+  }
+  if (N)
+    HIP_TRY(e, hipMemcpyAsync(b.d_ch, b.h_tab, N * sizeof(ngpu_chunk), hipMemcpyHostToDevice, b.s));
+  HIP_TRY(e, hipMemcpyAsync(b.d_lfirst, b.h_tab + N * sizeof(ngpu_chunk), (K + 1) * sizeof(uint64_t),
+                            hipMemcpyHostToDevice, b.s));
+  HIP_TRY(e, hipEventRecord(b.tab_sent, b.s));
+  b.tab_pending = true;
+  // ONE digest stage over all layers, ONE multi-layer dedup stage
+  if (int rc = enqueue_digest(e, b.d_data, bytes, b.d_ch, N, b.d_res, b.s, true)) return rc;
+  if (int rc = enqueue_dedup(e, jobs[0]->dict, b.d_ch, N, b.d_res, nullptr, 0, b.s, b.d_lfirst, K,
+                             b.d_lst)) {
+    (void)ws_release(e, b.s, nullptr, false);
+    return rc;
+  }
+  if (int rc = host_fence(e, b.s)) return rc;
+  // each pack's results (its device array and its pinned landing) and stats
+  const ngpu_ws_slot &sl = *e->cur;
+  for (uint64_t k = 0; k < K; ++k) {
+    BatchJob &j = *jobs[k];
+    if (j.n) {
+      HIP_TRY(e, hipMemcpyAsync(j.d_res, b.d_res + first[k], j.n * sizeof(ngpu_result),
+                                hipMemcpyDeviceToDevice, b.s));
+      HIP_TRY(e, hipMemcpyAsync(j.h_res, b.d_res + first[k], j.n * sizeof(ngpu_result),
+                                hipMemcpyDeviceToHost, b.s));
+    }
+    HIP_TRY(e, hipMemcpyAsync(j.h_stats, sl.ws.stats, kStWords * sizeof(uint64_t),
+                              hipMemcpyDeviceToHost, b.s));
+    HIP_TRY(e, hipMemcpyAsync(j.h_stats + kStatsLayer, b.d_lst + k, sizeof(ngpu_layer_stats),
+                              hipMemcpyDeviceToHost, b.s));
+    snprintf(j.path, sizeof j.path, "%s", sl.path);
+  }
+  auto done = std::make_shared<BatchEvent>();
+  done->device = e->device;
+  HIP_TRY(e, hipEventCreateWithFlags(&done->ev, hipEventDisableTiming));
+  HIP_TRY(e, hipEventRecord(done->ev, b.s));
+  for (BatchJob *j : jobs) {
+    j->done = done;
+    j->batch_layers = (uint32_t)K;
+  }
+  ++b.batches;
+  b.jobs += K;
+  b.max_jobs = std::max<uint64_t>(b.max_jobs, K);
+  return 0;
+}
+
+}  // namespace
+
+int batch_run(ngpu_engine *e, BatchJob &j) {
+  Batcher &b = *e->batcher;
+  std::unique_lock<std::mutex> lk(b.m);
+  b.open.push_back(&j);
+  b.cv.notify_all();  // a leader waiting for more packs
+  while (!j.enqueued) {
+    if (b.leading) {
+      b.cv.wait(lk);
+      continue;
+    }
+    b.leading = true;
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(kWindowUs);
+    while (b.open.size() < (size_t)e->open_packs.load() && b.open.size() < kMaxJobs &&
+           b.cv.wait_until(lk, until) == std::cv_status::no_timeout) {
+    }
+    // this leader's batch: the open packs sharing its dict, within the caps
+    std::vector<BatchJob *> take;
+    uint64_t bytes = 0, chunks = 0;
+    for (size_t i = 0; i < b.open.size();) {
+      BatchJob *x = b.open[i];
+      const bool fits = take.size() < kMaxJobs && bytes + x->len <= kMaxBytes &&
+                        chunks + x->n <= kMaxChunks;
+      if (x->dict == j.dict && (fits || x == &j)) {
+        take.push_back(x);
+        bytes += x->len;
+        chunks += x->n;
+        b.open.erase(b.open.begin() + (long)i);
+      } else {
+        ++i;
+      }
+    }
+    lk.unlock();
+    const int rc = launch_batch(e, b, take);
+    lk.lock();
+    for (BatchJob *x : take) {
+      x->rc = rc;
+      x->enqueued = true;
+    }
+    b.leading = false;
+    b.cv.notify_all();
+  }
+  lk.unlock();
+  if (j.rc) return j.rc;
+  DeviceGuard dg(e->device);
+  if (hipEventSynchronize(j.done->ev) != hipSuccess) return fail(e, NGPU_EHIP, "batch: stream failed");
+  return 0;
+}
+
+void batch_stats(ngpu_engine *e, uint64_t out[3]) {
+  out[0] = out[1] = out[2] = 0;
+  if (!e->batcher) return;
+  std::lock_guard<std::mutex> g(e->batcher->m);
+  out[0] = e->batcher->batches;
+  out[1] = e->batcher->jobs;
+  out[2] = e->batcher->max_jobs;
+}
+
+void batcher_free(ngpu_engine *e) {
+  Batcher *b = e->batcher;
+  if (!b) return;
+  DeviceGuard dg(e->device);
+  if (b->s) (void)hipStreamSynchronize(b->s);
+  for (void *p : {(void *)b->d_data, (void *)b->d_ch, (void *)b->d_res, (void *)b->d_lfirst,
+                  (void *)b->d_lst})
+    if (p) (void)hipFree(p);
+  if (b->h_tab) (void)hipHostFree(b->h_tab);
+  if (b->tab_sent) (void)hipEventDestroy(b->tab_sent);
+  // b->s is one of e->streams: destroyed with them
+  delete b;
+  e->batcher = nullptr;
+}
+
+Batcher *batcher_new() { return new Batcher(); }
+
+}  // namespace ngpu

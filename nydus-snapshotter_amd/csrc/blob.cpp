@@ -795,6 +795,15 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     memcpy(c.block_id, r.digest, 32);
     c.blob_index = r.blob_index;
     if (zr) {  // targz-ref: the chunk's deflate range in the original gzip blob
+      // (an oversized range is refused, never truncated: the
+      // chunk-info v2 entry holds compressed size - 1 in 24 bits and the
+      // offset in 40)
+      if (zr->csize[k] == 0 || zr->csize[k] > (1ull << 24) || zr->coff[k] >= (1ull << 40))
+        return host_fail(NGPU_EFORMAT,
+                         "targz-ref: chunk %llu's deflate range (%llu B at %llu) does not fit the "
+                         "blob.meta chunk entry (24-bit size, 40-bit offset)",
+                         (unsigned long long)i, (unsigned long long)zr->csize[k],
+                         (unsigned long long)zr->coff[k]);
       c.flags = 1;  // compressed (gzip, through its checkpoint)
       c.compressed_size = (uint32_t)zr->csize[k];
       c.compressed_offset = zr->coff[k];
@@ -979,6 +988,10 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     for (const RafsV6ChunkInfo &c : b.chunks) {
       if (c.blob_index != st.own_blob_index) continue;
       const uint64_t x = c.index;
+      if ((c.uncompressed_offset >> 12) > 0xFFFFFFFFull || c.compressed_offset >= (1ull << 40) ||
+          c.compressed_size == 0 || c.compressed_size > (1u << 24))
+        return host_fail(NGPU_EFORMAT, "pack: chunk %llu does not fit a blob.meta chunk entry",
+                         (unsigned long long)x);
       ci[3 * x] = ((c.uncompressed_offset >> 12) & 0xFFFFFFFFull) |
                   (((uint64_t)(c.uncompressed_size - 1) & 0xFFFFFF) << 32) |
                   ((uint64_t)(c.flags & 1) << 56);  // CHUNK_V2_FLAG_COMPRESSED
@@ -1493,6 +1506,24 @@ int ngpu_unpack(ngpu_read_at_fn ra, void *ctx, uint64_t size, ngpu_write_fn w, v
   return rc;
 }
 
+// 64 hex chars (an optional "sha256:" prefix) -> 32 bytes
+static bool unhex32(const char *s, uint8_t out[32]) {
+  if (!strncmp(s, "sha256:", 7)) s += 7;
+  if (strlen(s) != 64) return false;
+  for (int i = 0; i < 32; ++i) {
+    int v = 0;
+    for (int k = 0; k < 2; ++k) {
+      const char c = s[2 * i + k];
+      const int d = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10
+                  : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+      if (d < 0) return false;
+      v = v * 16 + d;
+    }
+    out[i] = (uint8_t)v;
+  }
+  return true;
+}
+
 int ngpu_merge_ex(const void *const *bootstraps, const uint64_t *sizes,
                   const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
                   uint64_t dict_size, const ngpu_merge_options *opt, ngpu_write_fn w, void *ctx,
@@ -1538,6 +1569,15 @@ int ngpu_merge_ex(const void *const *bootstraps, const uint64_t *sizes,
       // its whole nydus tar stream, which Merge receives as Layer.Digest and
       // uses as the bootstrap file name (convert_unix.go:567-573, 595-599).
       if (layer_digests && layer_digests[l]) m.own_name = layer_digests[l];
+      if (opt && opt->rafs_blob_digests && opt->rafs_blob_digests[l]) {  // targz-ref layer
+        if (!opt->rafs_blob_sizes || !opt->rafs_blob_toc_digests || !opt->rafs_blob_toc_digests[l] ||
+            !unhex32(opt->rafs_blob_digests[l], m.rafs_blob_digest) ||
+            !unhex32(opt->rafs_blob_toc_digests[l], m.toc_digest))
+          return host_fail(NGPU_EINVAL, "ngpu_merge: layer %llu: bad RAFS blob / TOC digest",
+                           (unsigned long long)l);
+        m.rafs_blob_size = opt->rafs_blob_sizes[l];
+        m.ref = true;
+      }
       in.push_back(m);
     }
     std::vector<uint8_t> boot;

@@ -405,6 +405,11 @@ void engine_unref(ngpu_engine *e) {
     if (b.h_io) (void)hipHostFree(b.h_io);
     blob_windows_free(b.win);
   }
+  batcher_free(e);  // syncs its stream (one of e->streams, destroyed below)
+  if (e->seg_pool) {  // every segment went back at its Pack's end (streams synced above)
+    (void)hipMemPoolTrimTo(e->seg_pool, 0);
+    (void)hipMemPoolDestroy(e->seg_pool);
+  }
   for (hipStream_t x : e->streams)  // every pack compute stream (+ the engine's)
     if (x != e->stream) (void)hipStreamDestroy(x);
   if (e->h_results) (void)hipHostFree(e->h_results);
@@ -517,6 +522,7 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NGPU_ENODEV;
   static std::atomic<uint64_t> next_uid{1};
   ngpu_engine *e = new ngpu_engine();
+  e->batcher = batcher_new();
   e->uid = next_uid.fetch_add(1, std::memory_order_relaxed);
   e->cfg = c;
   // NGPU_WS_SLOTS: workspace slots = calls on distinct streams that may run
@@ -542,16 +548,26 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
           ngpu_destroy(e);
           return NGPU_EHIP;
         }
-  // Retained Pack segments (pack.hip) come from the device's stream-ordered
-  // pool: a layer's 64 MiB segments go back to it at the Pack's end without
-  // hipFree's device-wide wait (~0.5 ms each), and the next Pack reuses them.
-  // The pool keeps up to NGPU_SEG_POOL_MIB (default 4096) cached.
+  // Retained Pack segments (pack.hip) come from the engine's own
+  // stream-ordered pool: a layer's 64 MiB segments go back to it at the
+  // Pack's end without hipFree's device-wide wait (~0.5 ms each), and the
+  // next Pack reuses them.  The pool keeps up to NGPU_SEG_POOL_MIB (default
+  // 4096) cached and is trimmed and destroyed with the engine; the device's
+  // default pool (the host application's) is left as it was.
   {
-    hipMemPool_t mp = nullptr;
+    hipMemPoolProps pp;
+    memset(&pp, 0, sizeof pp);
+    pp.allocType = hipMemAllocationTypePinned;
+    pp.handleTypes = hipMemHandleTypeNone;
+    pp.location.type = hipMemLocationTypeDevice;
+    pp.location.id = c.device;
     uint64_t keep = 4096ull << 20;
     if (const char *v = getenv("NGPU_SEG_POOL_MIB")) keep = strtoull(v, nullptr, 10) << 20;
-    if (hipDeviceGetDefaultMemPool(&mp, c.device) == hipSuccess && mp)
-      (void)hipMemPoolSetAttribute(mp, hipMemPoolAttrReleaseThreshold, &keep);
+    DeviceGuard g(c.device);
+    if (hipMemPoolCreate(&e->seg_pool, &pp) == hipSuccess && e->seg_pool)
+      (void)hipMemPoolSetAttribute(e->seg_pool, hipMemPoolAttrReleaseThreshold, &keep);
+    else
+      e->seg_pool = nullptr;  // segments then come from hipMallocAsync's default pool
     (void)hipGetLastError();
   }
   bool ok = hipEventCreateWithFlags(&e->host_ev, hipEventDisableTiming) == hipSuccess &&
@@ -892,5 +908,11 @@ int ngpu_timing_at(ngpu_engine *e, uint32_t back, ngpu_timing *out) {
 }
 
 int ngpu_last_timing(ngpu_engine *e, ngpu_timing *out) { return ngpu_timing_at(e, 0, out); }
+
+int ngpu_batch_stats(ngpu_engine *e, uint64_t out[3]) {
+  if (!e || !out) return NGPU_EINVAL;
+  batch_stats(e, out);
+  return 0;
+}
 
 }  // extern "C"

@@ -116,8 +116,34 @@ struct ngpu_ws_slot {
   char path[48] = "";            // digest kernels of its last digest stage (error messages)
 };
 
+namespace ngpu {
+struct Batcher;
+struct BatchEvent;
+// One pack's layer in a batch (batch.hip): its bytes and chunk table already
+// in HBM / pinned host memory, where its results and stats go.
+struct BatchJob {
+  const uint8_t *d_data = nullptr;  // the layer's bytes in HBM (slot-relative chunk offsets)
+  uint64_t len = 0;
+  const ngpu_chunk *h_ch = nullptr;  // n descriptors (host)
+  uint64_t n = 0;
+  hipEvent_t ready = nullptr;        // d_data is complete after this event
+  const ngpu_dict *dict = nullptr;
+  ngpu_result *d_res = nullptr;      // the pack's device results (n)
+  void *h_res = nullptr;             // pinned, n results
+  uint64_t *h_stats = nullptr;       // pinned, 32 words (read_stats_parse layout)
+  int rc = 0;
+  bool enqueued = false;
+  uint32_t batch_layers = 0;         // layers in the launch set it joined
+  char path[48] = "";                // the batch's digest kernels (error messages)
+  std::shared_ptr<BatchEvent> done;
+};
+}  // namespace ngpu
+
 struct ngpu_engine {
   std::atomic<int> refs{1};  // the creator + every open pack
+  ngpu::Batcher *batcher = nullptr;  // concurrent small Packs' launch sets (batch.hip)
+  hipMemPool_t seg_pool = nullptr;   // retained Pack segments (stream-ordered, own pool)
+  std::atomic<int> open_packs{0};    // packs opened and not yet ended
   uint64_t uid = 0;          // unique for the process's lifetime (node exchange channels)
   ngpu_config cfg{};
   int device = 0;
@@ -158,7 +184,11 @@ struct ngpu_engine {
   bool tshare_open = false;
   hipEvent_t host_ev = nullptr;  // host_fence marker (system scope)
   std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu, <= kStagingPool
-  static constexpr size_t kStagingPool = 32;   // 16 packs open at once keep theirs
+  // 32 packs open at once keep their two slots; the pinned bytes kept are
+  // bounded too (64 default 256 MiB slots would pin 16 GiB)
+  static constexpr size_t kStagingPool = 64;
+  static constexpr uint64_t kStagingPoolBytes = 8ull << 30;
+  uint64_t staging_pool_bytes = 0;  // guarded by pool_mu
   std::vector<ngpu_pack_bufs> pack_pool;        // guarded by pool_mu
   // pinned landing buffers of early-emission Packs that did not come from the
   // staging pool (ngpu_pack_set_output): kept, not hipHostFree'd (~5 ms each)
@@ -173,6 +203,12 @@ struct ngpu_engine {
 namespace ngpu {
 
 int fail(ngpu_engine *e, int code, const char *fmt, ...);
+// Batched close of a small Pack (batch.hip): blocks until the batch it joined
+// has run and its results / stats are in j.h_res / j.h_stats.
+int batch_run(ngpu_engine *e, BatchJob &j);
+void batch_stats(ngpu_engine *e, uint64_t out[3]);  // batches, layers, most layers in one
+Batcher *batcher_new();
+void batcher_free(ngpu_engine *e);
 // Pick the workspace slot for a stage on stream s and make it e->cur (e->mu
 // held): the slot s used last, else an idle slot, else the least recently
 // used one (ws_acquire then orders s after its last stage).

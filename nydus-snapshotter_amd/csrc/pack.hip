@@ -258,9 +258,11 @@ void release(ngpu_pack *p) {
     std::lock_guard<std::mutex> g(p->e->pool_mu);
     for (Slot &s : p->slot) {
       if (!s.h || !s.h_ch || !s.d_ch || !s.copied || !s.done ||
-          p->e->staging_pool.size() >= ngpu_engine::kStagingPool)
+          p->e->staging_pool.size() >= ngpu_engine::kStagingPool ||
+          p->e->staging_pool_bytes + p->cap > ngpu_engine::kStagingPoolBytes)
         continue;
       p->e->staging_pool.push_back({s.h, s.h_ch, s.d, s.d_ch, s.copied, s.done, p->cap});
+      p->e->staging_pool_bytes += p->cap;
       s = Slot{};
     }
   }
@@ -279,8 +281,10 @@ void release(ngpu_pack *p) {
     for (ngpu_staging_buf &b : em->land) {
       if (!b.h) continue;
       const bool whole = b.h_ch && b.d_ch && b.copied && b.done;  // a pool entry (else: own landing)
-      if (whole && e->staging_pool.size() < ngpu_engine::kStagingPool) {
+      if (whole && e->staging_pool.size() < ngpu_engine::kStagingPool &&
+          e->staging_pool_bytes + b.cap <= ngpu_engine::kStagingPoolBytes) {
         e->staging_pool.push_back(b);
+        e->staging_pool_bytes += b.cap;
       } else if (!whole && !b.d && e->land_pool.size() < ngpu_engine::kStagingPool) {
         e->land_pool.push_back({b.h, b.cap});  // an own landing: kept for the next Pack
       } else {
@@ -332,6 +336,7 @@ void release(ngpu_pack *p) {
   delete p->pool;
   delete p;
   dict_unref(dict);
+  e->open_packs.fetch_sub(1);
   engine_unref(e);  // may free the engine if its creator already destroyed it
 }
 
@@ -372,7 +377,10 @@ int grow_all(ngpu_pack *p, uint64_t want) {
 }
 
 // Copy the slot to HBM and digest chunks [a, b) (all inside the slot).
-int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
+// digest == false: the copies only (a batched close digests the slot's bytes
+// in its launch set, batch.hip); *dev_out = where the bytes land.
+int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b, bool digest = true,
+             uint8_t **dev_out = nullptr) {
   if (b == a) return 0;
   ngpu_engine *e = p->e;
   const uint64_t nch = b - a;
@@ -392,7 +400,10 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
       uint64_t cap = p->arenas.empty() ? p->cap : std::min<uint64_t>(2 * p->arenas.back().cap, 1ull << 30);
       if (cap < need) cap = need;
       ngpu_pack::Arena ar;
-      HIP_TRY(e, hipMallocAsync((void **)&ar.d, cap, p->copy));
+      if (e->seg_pool)
+        HIP_TRY(e, hipMallocFromPoolAsync((void **)&ar.d, cap, e->seg_pool, p->copy));
+      else
+        HIP_TRY(e, hipMallocAsync((void **)&ar.d, cap, p->copy));
       ar.cap = cap;
       p->arenas.push_back(ar);
     }
@@ -420,8 +431,11 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b) {
     HIP_TRY(e, hipMemcpyAsync(p->d_all + a, s.d_ch, nch * sizeof(ngpu_chunk),
                               hipMemcpyDeviceToDevice, p->stream));
   }
-  rc = enqueue_digest(e, dev, s.fill, s.d_ch, nch, p->d_res + a, p->stream);
-  if (rc) return rc;
+  if (dev_out) *dev_out = dev;
+  if (digest) {
+    rc = enqueue_digest(e, dev, s.fill, s.d_ch, nch, p->d_res + a, p->stream);
+    if (rc) return rc;
+  }
   HIP_TRY(e, hipEventRecord(s.done, p->stream));
   s.busy = true;
   p->dispatched = b;
@@ -780,6 +794,9 @@ int ref_finish(ngpu_pack *p, BlobWriter &bw, const ngpu_chunk *ch, const ngpu_re
     const uint64_t coff = x.in_offset - (x.bits ? 1 : 0);
     zr.coff.push_back(coff);
     zr.csize.push_back(gz.in_end_of(end) - coff);
+    if (k > 0xFFFFFFFFull || off - x.out_offset > 0xFFFFFFFFull)  // 32-bit fields: refused, not truncated
+      return fail(e, NGPU_EFORMAT, "pack: OCIRef chunk %llu lies %llu B past its checkpoint (32-bit field)",
+                  (unsigned long long)i, (unsigned long long)(off - x.out_offset));
     zr.ctx.push_back((uint32_t)k);
     zr.ctx_off.push_back((uint32_t)(off - x.out_offset));
   }
@@ -859,6 +876,7 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
   if (int rc = dict_check(e, dict)) return rc;
   ngpu_pack *p = new ngpu_pack(e);
   engine_ref(e);
+  e->open_packs.fetch_add(1);
   dict_ref(dict);
   p->dict = dict;
   p->retain = flags & NGPU_PACK_RETAIN;
@@ -893,6 +911,7 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
         if (pool[i].cap != cap) continue;
         const ngpu_staging_buf b = pool[i];
         pool.erase(pool.begin() + (long)i);
+        e->staging_pool_bytes -= b.cap;
         s.h = (uint8_t *)b.h;
         s.h_ch = (ngpu_chunk *)b.h_ch;
         s.d = (uint8_t *)b.d;
@@ -975,6 +994,7 @@ int ngpu_pack_set_output(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_
           if (pool[i].cap == p->cap) {
             b = pool[i];
             pool.erase(pool.begin() + (long)i);
+            e->staging_pool_bytes -= b.cap;
             break;
           }
         auto &lp = e->land_pool;  // else a landing kept by an earlier Pack
@@ -1131,6 +1151,8 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
   ngpu_result *res = nullptr;
   ngpu_layer_stats st{};
   std::string path;
+  bool batched = false;
+  uint8_t *batch_dev = nullptr;
   if (!rc) {
     DeviceGuard dg(e->device);
     {
@@ -1142,7 +1164,12 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
       // second copy of the table is skipped
       Slot &cs = p->slot[p->cur];
       const bool one_slot = p->dispatched == 0 && n > 0;
-      rc = dispatch(p, cs, p->dispatched, n);
+      // a layer that fit one staging slot, closing while other packs are
+      // open on the engine, joins a batch (batch.hip): ONE launch set for
+      // every such pack closing at about this time
+      batched = one_slot && !p->gz && !(e->cfg.flags & NGPU_FLAG_NO_BATCH) &&
+                e->open_packs.load() > 1;
+      rc = dispatch(p, cs, p->dispatched, n, !batched, &batch_dev);
       const ngpu_chunk *d_dedup = one_slot ? cs.d_ch : p->d_all;
       if (!rc) rc = grow_results(p, n + 1);
       if (!rc && !one_slot && p->all_cap < n + 1) {  // kept between packs (engine pack_pool)
@@ -1178,10 +1205,13 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
           rc = fail(e, NGPU_EHIP, "pack: chunk table copy failed");
         d_dedup = p->d_all;
       }
-      if (!rc && em) {  // records the emitter's last prefix stage decided get their mark back
+      if (!rc && em && !batched) {  // records the emitter's last prefix stage decided get their mark back
         launch_remark_digested(p->d_res, em->deduped, ps);
         if (hipGetLastError() != hipSuccess) rc = fail(e, NGPU_EHIP, "pack: remark failed");
       }
+      if (batched) {
+        // the rest runs in the batch, after the engine lock is let go
+      } else {
       if (!rc)
         rc = enqueue_dedup(e, p->dict, d_dedup, n, p->d_res, nullptr, 0, ps, nullptr, 1, nullptr);
       if (!rc) rc = host_fence(e, ps, p->fence);
@@ -1192,6 +1222,22 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
         rc = fail(e, NGPU_EHIP, "pack: result copy failed");
       if (!rc) rc = read_stats_enqueue(e, ps, p->h_stats);
       path = e->cur->path;  // the digest kernels, for a guard error (read outside the lock)
+      }
+    }
+    if (batched && !rc) {  // the slot's bytes are in HBM (or on their way: cs.copied)
+      Slot &cs = p->slot[p->cur];
+      BatchJob job;
+      job.d_data = batch_dev;
+      job.len = cs.fill;
+      job.h_ch = cs.h_ch;
+      job.n = n;
+      job.ready = cs.copied;
+      job.dict = p->dict;
+      job.d_res = p->d_res;
+      job.h_res = p->h_io;
+      job.h_stats = p->h_stats;
+      rc = batch_run(e, job);
+      path = job.path;
     }
     // wait for the pack's own stream without the engine lock (other packs
     // and calls keep enqueueing meanwhile), then check its stats

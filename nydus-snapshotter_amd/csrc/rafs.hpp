@@ -95,6 +95,13 @@ struct MergeInput {
   uint64_t n = 0;
   std::string own_name;  // "" = keep the blob id
   bool parent = false;   // MergeOption.ParentBootstrapPath: blobs keep their ids, any number
+  // a targz-ref layer (Layer.OriginalDigest): what Merge hands nydus-image as
+  // --blob-digests / --blob-sizes / --blob-toc-digests (convert_unix.go:
+  // 579-587, builder.go:242-253): the RAFS blob (the layer's nydus stream)
+  // digest and size and its TOC digest, recorded in the own blob's record
+  uint8_t rafs_blob_digest[32] = {}, toc_digest[32] = {};
+  uint64_t rafs_blob_size = 0;
+  bool ref = false;
 };
 int merge_rafs(const std::vector<MergeInput> &layers, const std::vector<std::string> &dict_ids,
                const std::string &prefetch, std::vector<uint8_t> *out, std::vector<std::string> *blob_ids);

@@ -1,6 +1,7 @@
 // converter.cpp — see converter.hpp.  Only the C ABI is used.
 #include "converter.hpp"
 
+#include <openssl/sha.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -378,7 +379,9 @@ Error Merge(const std::vector<Layer> &layers, Writer &dest, const MergeOption &o
             std::vector<std::string> *blobDigests) {
   blobDigests->clear();
   std::vector<BufferWriter> boots(layers.size());
-  std::vector<std::string> hexes(layers.size());
+  std::vector<std::string> hexes(layers.size()), ref_digest(layers.size()), ref_toc(layers.size());
+  std::vector<uint64_t> ref_size(layers.size(), 0);
+  bool any_ref = false;
   for (size_t i = 0; i < layers.size(); ++i) {
     if (!layers[i].ReaderAt) return err(NGPU_EINVAL, "layer without reader");
     if (Error e = UnpackEntry(*layers[i].ReaderAt, EntryBootstrap, boots[i], nullptr))
@@ -387,6 +390,24 @@ Error Merge(const std::vector<Layer> &layers, Writer &dest, const MergeOption &o
     // OriginalDigest (getBootstrapPath, convert_unix.go:567-573)
     const std::string &d = layers[i].OriginalDigest.empty() ? layers[i].Digest : layers[i].OriginalDigest;
     hexes[i] = d.compare(0, 7, "sha256:") == 0 ? d.substr(7) : d;
+    if (!layers[i].OriginalDigest.empty()) {
+      // --blob-digests / --blob-sizes / --blob-toc-digests (convert_unix.go:
+      // 579-587): the nydus stream's digest and size, and calcBlobTOCDigest
+      // (:541-554): sha256 of the TOC entry's data
+      BufferWriter toc;
+      if (Error e = UnpackEntry(*layers[i].ReaderAt, EntryTOC, toc, nullptr))
+        return err(e.code, "calc blob toc digest for layer " + layers[i].Digest + ": " + e.msg);
+      uint8_t md[32];
+      SHA256(toc.data.data(), toc.data.size(), md);
+      static const char *hx = "0123456789abcdef";
+      std::string th(64, '0');
+      for (int k = 0; k < 32; ++k) th[2 * k] = hx[md[k] >> 4], th[2 * k + 1] = hx[md[k] & 15];
+      const std::string &ld = layers[i].Digest;
+      ref_digest[i] = ld.compare(0, 7, "sha256:") == 0 ? ld.substr(7) : ld;
+      ref_toc[i] = th;
+      ref_size[i] = layers[i].ReaderAt->Size();
+      any_ref = true;
+    }
   }
   std::vector<uint8_t> dict;
   if (!opt.ChunkDictPath.empty()) {
@@ -419,6 +440,14 @@ Error Merge(const std::vector<Layer> &layers, Writer &dest, const MergeOption &o
   mo.parent_bootstrap = parent.empty() ? nullptr : parent.data();
   mo.parent_size = parent.size();
   mo.prefetch_patterns = opt.PrefetchPatterns.c_str();  // the builder's stdin (builder.go:238-240)
+  std::vector<const char *> rd(layers.size(), nullptr), rt(layers.size(), nullptr);
+  if (any_ref) {
+    for (size_t i = 0; i < layers.size(); ++i)
+      if (!ref_toc[i].empty()) rd[i] = ref_digest[i].c_str(), rt[i] = ref_toc[i].c_str();
+    mo.rafs_blob_digests = rd.data();
+    mo.rafs_blob_sizes = ref_size.data();
+    mo.rafs_blob_toc_digests = rt.data();
+  }
   BufferWriter merged;
   char *ids = nullptr;
   const int rc = ngpu_merge_ex(ptrs.data(), sizes.data(), names.data(), layers.size(),

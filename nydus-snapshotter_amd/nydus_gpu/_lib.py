@@ -72,7 +72,7 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_dict_create_device_gid", "ngpu_route_digests", "ngpu_route_hits",
            "ngpu_pack_set_output", "ngpu_ref_chunk_read",
            # ABI 5
-           "ngpu_node_process_step"]
+           "ngpu_node_process_step", "ngpu_batch_stats"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
@@ -94,6 +94,7 @@ class NgpuConfig(ctypes.Structure):
 FLAG_TIMING = 0x1
 FLAG_ALIGNED_CHUNK = 0x2
 FLAG_GRID_STAGES = 0x4  # no fused one-workgroup path for small calls (tests / tuning)
+FLAG_NO_BATCH = 0x8  # every Pack close its own launches (no batched close of small packs)
 
 
 class NgpuTiming(ctypes.Structure):
@@ -184,6 +185,7 @@ def lib():
     L.ngpu_chunk_table.argtypes = [vp, vp, u64, vp, u64, pu64]
     L.ngpu_last_timing.argtypes = [vp, ctypes.POINTER(NgpuTiming)]
     L.ngpu_timing_at.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(NgpuTiming)]
+    L.ngpu_batch_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.ngpu_digest_device.argtypes = [vp, vp, u64, vp, u64, vp, vp]
     L.ngpu_dict_probe_device.argtypes = [vp, vp, u64, u64, vp, vp]
     L.ngpu_dedup_device.argtypes = [vp, vp, u64, vp, vp, u32, vp, ctypes.POINTER(NgpuLayerStats)]
@@ -480,14 +482,20 @@ def route_hits(d_routed: int, d_rows: int, m: int, d_hits: int, stream: int = 0)
 
 class NgpuMergeOptions(ctypes.Structure):
     _fields_ = [("parent_bootstrap", ctypes.c_void_p), ("parent_size", ctypes.c_uint64),
-                ("prefetch_patterns", ctypes.c_char_p)]
+                ("prefetch_patterns", ctypes.c_char_p),
+                # ABI 6: targz-ref layers' RAFS blob digests / sizes / TOC digests
+                ("rafs_blob_digests", ctypes.c_void_p), ("rafs_blob_sizes", ctypes.c_void_p),
+                ("rafs_blob_toc_digests", ctypes.c_void_p)]
 
 
 def merge(bootstraps, layer_digests, dict_bootstrap: bytes = None, parent_bootstrap: bytes = None,
-          prefetch_patterns: str = ""):
+          prefetch_patterns: str = "", rafs_blobs=None):
     """ngpu_merge_ex: per-layer bootstraps (bytes, lowest first) + layer digest
     hex strings -> (merged bootstrap bytes, [blob ids in first-appearance
-    order]).  The merged bootstrap holds the overlaid inode tree."""
+    order]).  The merged bootstrap holds the overlaid inode tree.
+    rafs_blobs: per layer None, or (RAFS blob digest hex, size, TOC digest
+    hex) for a targz-ref layer (Merge's --blob-digests / --blob-sizes /
+    --blob-toc-digests, builder.go:242-253)."""
     L = lib()
     bufs = [_buf(b) for b in bootstraps]
     n = len(bufs)
@@ -501,6 +509,13 @@ def merge(bootstraps, layer_digests, dict_bootstrap: bytes = None, parent_bootst
     pbuf = _buf(parent_bootstrap) if parent_bootstrap is not None else None
     opt = NgpuMergeOptions(_ptr(pbuf) if pbuf is not None else None, pbuf.size if pbuf is not None else 0,
                            (prefetch_patterns or "").encode())
+    if rafs_blobs is not None and any(r is not None for r in rafs_blobs):
+        rd = (ctypes.c_char_p * max(1, n))(*[r[0].encode() if r else None for r in rafs_blobs])
+        rs = (ctypes.c_uint64 * max(1, n))(*[int(r[1]) if r else 0 for r in rafs_blobs])
+        rt = (ctypes.c_char_p * max(1, n))(*[r[2].encode() if r else None for r in rafs_blobs])
+        opt.rafs_blob_digests = ctypes.cast(rd, ctypes.c_void_p)
+        opt.rafs_blob_sizes = ctypes.cast(rs, ctypes.c_void_p)
+        opt.rafs_blob_toc_digests = ctypes.cast(rt, ctypes.c_void_p)
     rc = L.ngpu_merge_ex(ptrs, sizes, digs, n, _ptr(dbuf) if dbuf is not None else None,
                          dbuf.size if dbuf is not None else 0, ctypes.byref(opt), sink.fn, None,
                          ctypes.byref(ids))
@@ -745,6 +760,12 @@ class Engine:
         t = NgpuTiming()
         self._check(lib().ngpu_last_timing(self._h, ctypes.byref(t)), "last_timing")
         return t.as_dict()
+
+    def batch_stats(self) -> dict:
+        """Batched Pack closes (batch.hip): launch sets, packs in them, most in one."""
+        out = (ctypes.c_uint64 * 3)()
+        self._check(lib().ngpu_batch_stats(self._h, out), "batch_stats")
+        return {"batches": out[0], "packs": out[1], "max_packs": out[2]}
 
     def timing_at(self, back: int) -> dict:
         """Stage timings of the call `back` calls before the last one (the

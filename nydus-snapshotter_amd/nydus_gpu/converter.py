@@ -29,6 +29,7 @@ from typing import BinaryIO, List, Optional, Sequence
 
 import numpy as np
 
+import hashlib
 import io
 import tarfile
 
@@ -325,7 +326,7 @@ def UnpackEntry(ra: bytes, targetName: str, target: BinaryIO):
 def Merge(layers: Sequence[Layer], dest: BinaryIO, opt: MergeOption) -> List[str]:
     """convert_unix.go:560-666 — merge per-layer bootstraps; returns the
     referenced blob digests (sha256:<id>) in first-appearance order."""
-    boots, digests = [], []
+    boots, digests, refs = [], [], []
     for layer in layers:
         b = io.BytesIO()
         try:
@@ -336,6 +337,19 @@ def Merge(layers: Sequence[Layer], dest: BinaryIO, opt: MergeOption) -> List[str
         # an OCIRef layer's blob is its original gzip blob, named by its
         # OriginalDigest (getBootstrapPath, convert_unix.go:567-573)
         digests.append((layer.OriginalDigest or layer.Digest).split(":", 1)[-1])
+        if layer.OriginalDigest:
+            # --blob-digests / --blob-sizes / --blob-toc-digests
+            # (convert_unix.go:579-587): the nydus stream's digest and size,
+            # and calcBlobTOCDigest (:541-554): sha256 of the TOC entry data
+            toc = io.BytesIO()
+            try:
+                UnpackEntry(layer.ReaderAt, EntryTOC, toc)
+            except ConverterError as e:
+                raise ConverterError(f"calc blob toc digest for layer {layer.Digest}: {e}") from e
+            refs.append((layer.Digest.split(":", 1)[-1], len(layer.ReaderAt),
+                         hashlib.sha256(toc.getvalue()).hexdigest()))
+        else:
+            refs.append(None)
     dict_boot = parent = None
     if opt.ChunkDictPath:
         with open(opt.ChunkDictPath, "rb") as f:
@@ -345,7 +359,7 @@ def Merge(layers: Sequence[Layer], dest: BinaryIO, opt: MergeOption) -> List[str
             parent = f.read()
     try:
         merged, ids = merge(boots, digests, dict_boot, parent_bootstrap=parent,
-                            prefetch_patterns=opt.PrefetchPatterns)
+                            prefetch_patterns=opt.PrefetchPatterns, rafs_blobs=refs)
     except NgpuError as e:
         raise ConverterError(f"merge bootstrap: {e}") from e
     if opt.WithTar:  # packToTar (utils.go:92-160): image/ + image/image.boot

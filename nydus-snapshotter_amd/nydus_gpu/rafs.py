@@ -115,6 +115,27 @@ def write_v6_bootstrap(records: np.ndarray, chunk_size: int, flags: int = 0x4,
     return bytes(buf)
 
 
+def write_v6_dict_file(path: str, n_records: int, chunk_size: int, pieces, flags: int = 0x4,
+                       blobs: np.ndarray = None) -> int:
+    """The same minimal RAFS v6 bootstrap as write_v6_bootstrap, written to
+    `path` with its chunk table streamed from `pieces` (an iterable of
+    CHUNK_INFO_DTYPE arrays, n_records in all): a ChunkDictPath file of any
+    size without holding its table in memory.  -> bytes written."""
+    head = bytearray(write_v6_bootstrap(np.zeros(0, CHUNK_INFO_DTYPE), chunk_size, flags, blobs))
+    cto = len(head)
+    struct.pack_into("<Q", head, EXT_OFFSET + 32, n_records * 80)  # chunk_table_size
+    done = 0
+    with open(path, "wb") as f:
+        f.write(head)
+        for p in pieces:
+            p = np.ascontiguousarray(p).view(CHUNK_INFO_DTYPE).reshape(-1)
+            p.tofile(f)
+            done += len(p)
+    if done != n_records:
+        raise ValueError(f"{done} records written, {n_records} declared")
+    return cto + 80 * n_records
+
+
 def canonical(records: np.ndarray):
     """inspect-equivalent canonical form: sorted by digest."""
     recs = np.asarray(records).view(CHUNK_INFO_DTYPE).reshape(-1)

@@ -107,6 +107,17 @@ def test_testpackref_restated(oracle):
     blobs = cv.Merge([cv.Layer(Digest=res["digest"], ReaderAt=stream, OriginalDigest=gz_digest)],
                      merged, cv.MergeOption(OCIRef=True))
     assert blobs == [gz_digest]
+    # the layer's blob record carries Merge's --blob-digests / --blob-sizes /
+    # --blob-toc-digests (convert_unix.go:579-587; restated offsets, VERIFY)
+    from nydus_gpu import rafs
+    toc = io.BytesIO()
+    cv.UnpackEntry(stream, cv.EntryTOC, toc)
+    rec = rafs.read_v6(merged.getvalue())["blobs"]
+    assert rec["blob_id"][0].decode() == gz_digest.split(":")[1]
+    meta = bytes(rec["reserved"][0])
+    assert meta[32:64] == hashlib.sha256(toc.getvalue()).digest()
+    assert meta[64:96].hex() == res["digest"].split(":")[1]
+    assert int.from_bytes(meta[96:104], "little") == len(stream)
 
 
 @pytest.mark.parametrize("level", [1, 9])

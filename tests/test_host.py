@@ -23,7 +23,7 @@ def test_header_symbols_exported():
     L = nydus_gpu.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.ngpu_abi_version() == 5
+    assert L.ngpu_abi_version() == 6
 
 
 def test_struct_sizes():
@@ -159,6 +159,31 @@ def test_merge_blob_bookkeeping():
     # two layers carrying the same dict chunk record: one record per (digest, blob)
     merged, ids = nydus_gpu.merge([c, c], ["11" * 32, "22" * 32], d)
     assert ids == ["bb" * 32] and len(rafs.read_v6(merged)["chunks"]) == 1
+
+
+def test_merge_records_targz_ref_blob_digests():
+    """Merge of a targz-ref layer (Layer.OriginalDigest): its own blob record
+    in the merged bootstrap carries what Merge hands nydus-image as
+    --blob-digests / --blob-sizes / --blob-toc-digests (convert_unix.go:579-587,
+    builder.go:242-253) -- at the restated RafsV6Blob offsets (VERIFY,
+    unpinned: no reference fixture); a plain layer's record stays zero there."""
+    recs = np.zeros(2, rafs.CHUNK_INFO_DTYPE)
+    recs["block_id"][:, 0] = [1, 2]
+    gz, plain = "ab" * 32, "cd" * 32
+    a = rafs.write_v6_bootstrap(recs, 0x100000, blobs=rafs.make_blob_table(["ee" * 32], 0x100000))
+    b = rafs.write_v6_bootstrap(recs[:1], 0x100000, blobs=rafs.make_blob_table(["ff" * 32], 0x100000))
+    rafs_dig, toc_dig = "12" * 32, "34" * 32
+    merged, ids = nydus_gpu.merge([a, b], [gz, plain],
+                                  rafs_blobs=[("sha256:" + rafs_dig, 123456, toc_dig), None])
+    assert ids == [gz, plain]
+    m = rafs.read_v6(merged)
+    meta = m["blobs"]["reserved"]
+    assert bytes(meta[0][32:64]).hex() == toc_dig
+    assert bytes(meta[0][64:96]).hex() == rafs_dig
+    assert int.from_bytes(bytes(meta[0][96:104]), "little") == 123456
+    assert not bytes(meta[1][32:104]).strip(b"\0")
+    with pytest.raises(nydus_gpu.NgpuError):  # not 64 hex chars
+        nydus_gpu.merge([a], [gz], rafs_blobs=[("xyz", 1, toc_dig)])
 
 
 def test_tar_scanner_fuzz_agrees_with_oracle(tars, oracle):
