@@ -55,6 +55,11 @@ for s in "$@"; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c2 -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-sub > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err")
       ok $? stats
       python3 scripts/prof_agree.py "$OUT/prof" b3_groups "$OUT/prof_bench.json" "$OUT/rocprof_c2_agreement.json" | cut -c1-200 ;;
+    c3)
+      df -h /tmp "$ROOT" /dev/shm > "$OUT/df.txt" 2>&1 || true
+      timeout -k 10 600 python3 bench.py --workload c3 --steps 10 --no-cpu-baseline > "$OUT/c3.json" 2> "$OUT/c3.err"
+      ok $? c3
+      python3 -c "import json; d=json.loads(open('$OUT/c3.json').read().strip().splitlines()[-1]); print(d['value'], json.dumps(d['dict']))" ;;
     n2)
       NYDUS_NODE_EXTRA_DEVICES=0,0 timeout -k 10 600 python3 bench.py --gpus 2 --steps 10 --warmup 5 --dist-backend gloo --c4-layers 4 > "$OUT/bench_c2_n2_gloo.json" 2> "$OUT/bench_c2_n2_gloo.err"
       ok $? n2
