@@ -876,7 +876,8 @@ def node_e2e(torch, dist, nydus_gpu, buf, wl, stride, device, backend, sample_by
 SUB_KEYS = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "stage_ms", "roofline",
             "cpu_baseline", "speedup_vs_cpu", "speedup_vs_cpu_single_stream", "dict",
             "probe_roofline", "merge", "decisions", "digest_check_past_4gib", "n_gpus", "sharded_dict",
-            "e2e_pcie", "tar_host_path", "ranks", "modes", "speedup_vs_cpu_device", "bound")
+            "e2e_pcie", "tar_host_path", "ranks", "modes", "speedup_vs_cpu_device", "bound",
+            "stream_vs_cpu_pipeline")
 
 
 def child_line(cmd, timeout_s, env=None):
@@ -1215,6 +1216,22 @@ def packs_bench(args):
                "kind": "port", "sample": f"the same {K} layers ({file_bytes / MiB:.1f} MiB of file "
                                          f"data), digest+dedup, one layer per thread, "
                                          f"{oracle_py.cpu_impl()}; {reps} rounds"}
+        # the whole CPU converter pipeline per layer (digest + dedup + zstd of
+        # the NEW chunks + SHA-256 of the stream), against stream_zstd
+        if oracle_py.cpu_pack_pipeline(arrs[0], ochs[0][:4], wl["digester"]) is not None:
+            with ThreadPoolExecutor(threads) as ex:
+                def pipe_round():
+                    list(ex.map(lambda i: oracle_py.cpu_pack_pipeline(arrs[i], ochs[i], wl["digester"]),
+                                range(K)))
+                pipe_round()
+                reps, t0 = 0, time.perf_counter()
+                while time.perf_counter() - t0 < 3.0 and reps < 100:
+                    pipe_round()
+                    reps += 1
+                el = time.perf_counter() - t0
+            cpu["pipeline_gbs"] = round(file_bytes * reps / el / 1e9, 2)
+            cpu["pipeline"] = ("per layer on one thread: digests + stream dedup + zstd level 1 of the "
+                               "NEW chunks (libzstd) + SHA-256 of the compressed stream (OpenSSL)")
     line = {"metric": "GB/s of layer data chunk-hashed+deduped (node)",
             "value": modes["decisions"]["gbs"], "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": modes["decisions"]["ms_per_round"],
@@ -1229,6 +1246,8 @@ def packs_bench(args):
                      "sha256: one 1 MiB chunk's chain per launch set (~21 ms)"}
     if cpu:
         line["speedup_vs_cpu"] = round(modes["decisions"]["gbs"] / cpu["value"], 2)
+        if cpu.get("pipeline_gbs"):
+            line["stream_vs_cpu_pipeline"] = round(modes["stream_zstd"]["gbs"] / cpu["pipeline_gbs"], 2)
         if modes["decisions"]["device_gbs"]:
             line["speedup_vs_cpu_device"] = round(modes["decisions"]["device_gbs"] / cpu["value"], 2)
     print(json.dumps(line), flush=True)

@@ -90,6 +90,15 @@ uint64_t oracle_dedup(const uint8_t *digests, const uint32_t *sizes, uint64_t n,
 void oracle_digest_chunks(const uint8_t *data, const oracle_chunk *chunks,
                           uint64_t n, int digester, uint8_t *out);
 
+/* ---- timed CPU baseline (cpu_baseline.c; bench.py's cpu_baseline leg) ---- */
+int oracle_cpu_impl(void);
+uint64_t oracle_cpu_digest_dedup(const uint8_t *data, const oracle_chunk *chunks, uint64_t n,
+                                 int digester, int threads, uint8_t *digests,
+                                 const uint32_t *sizes, oracle_decision *decisions);
+uint64_t oracle_cpu_pack_pipeline(const uint8_t *data, const oracle_chunk *chunks, uint64_t n,
+                                  int digester, uint8_t *digests, const uint32_t *sizes,
+                                  oracle_decision *decisions, uint8_t stream_digest[32], int *ok);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,9 @@ def lib():
         L.oracle_digest_chunks.argtypes = [vp, vp, u64, ctypes.c_int, vp]
         L.oracle_cpu_digest_dedup.argtypes = [vp, vp, u64, ctypes.c_int, ctypes.c_int, vp, vp, vp]
         L.oracle_cpu_digest_dedup.restype = u64
+        L.oracle_cpu_pack_pipeline.argtypes = [vp, vp, u64, ctypes.c_int, vp, vp, vp, vp,
+                                               ctypes.POINTER(ctypes.c_int)]
+        L.oracle_cpu_pack_pipeline.restype = u64
         L.oracle_cpu_impl.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -123,6 +126,24 @@ def cpu_digest_dedup(data, chunks, digester: str, threads: int):
     lib().oracle_cpu_digest_dedup(_ptr(buf), _ptr(ch), len(ch), 1 if digester == "sha256" else 0,
                                   threads, _ptr(dig), _ptr(sizes), _ptr(dec))
     return dig, dec
+
+
+def cpu_pack_pipeline(data, chunks, digester: str):
+    """Timed CPU baseline of one layer's converter pipeline, single-threaded:
+    digests + stream dedup + zstd (level 1) of the NEW chunks in blob order +
+    SHA-256 of the compressed stream.  -> (compressed bytes, stream digest),
+    or None when libzstd / OpenSSL are absent."""
+    buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    ch = np.ascontiguousarray(chunks, dtype=CHUNK_DTYPE)
+    dig = np.zeros((len(ch), 32), dtype=np.uint8)
+    sizes = np.ascontiguousarray(ch["length"], dtype=np.uint32)
+    dec = np.zeros(len(ch), dtype=DECISION_DTYPE)
+    sd = np.zeros(32, dtype=np.uint8)
+    ok = ctypes.c_int(0)
+    total = lib().oracle_cpu_pack_pipeline(_ptr(buf), _ptr(ch), len(ch),
+                                           1 if digester == "sha256" else 0, _ptr(dig), _ptr(sizes),
+                                           _ptr(dec), _ptr(sd), ctypes.byref(ok))
+    return (int(total), sd.tobytes()) if ok.value else None
 
 
 def cpu_impl() -> str:
