@@ -228,6 +228,10 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     }
     lk.unlock();
     const int rc = launch_batch(e, b, take);
+    if (rc && b.s) {  // part of it may be enqueued: let it drain before the packs free their buffers
+      DeviceGuard dg(e->device);
+      (void)hipStreamSynchronize(b.s);
+    }
     lk.lock();
     for (BatchJob *x : take) {
       x->rc = rc;
