@@ -10,6 +10,7 @@
 #include <openssl/evp.h>
 #include <zlib.h>
 #include <stdio.h>
+#include <string.h>
 #include <stdlib.h>
 
 #include <string>
@@ -106,6 +107,13 @@ static Packed packLayer(const std::vector<uint8_t> &source, const std::string &c
   REQUIRE(p.digest == p.stats.Digest, "stream digest %s vs %s", p.digest.c_str(),
           p.stats.Digest.c_str());
   return p;
+}
+
+static std::string hex_of(const uint8_t *p, size_t n) {
+  static const char *hx = "0123456789abcdef";
+  std::string o;
+  for (size_t i = 0; i < n; ++i) o += hx[p[i] >> 4], o += hx[p[i] & 15];
+  return o;
 }
 
 int main(int argc, char **argv) {
@@ -239,6 +247,24 @@ int main(int argc, char **argv) {
     REQUIRE_NOERR(Merge(refLayers, merged, mo, &refBlobs));
     REQUIRE(refBlobs.size() == 1 && refBlobs[0] == gzDigest, "OCIRef Merge blobs: %s",
             refBlobs.empty() ? "-" : refBlobs[0].c_str());
+    // its blob record carries --blob-digests / --blob-sizes / --blob-toc-digests
+    // (convert_unix.go:579-587): RafsV6Blob bytes 136.. (after the 104-B head
+    // and the ci fields; restated offsets, VERIFY)
+    {
+      const std::vector<uint8_t> &mb = merged.data;
+      uint64_t bto = 0;
+      memcpy(&bto, mb.data() + 1152 + 8, 8);
+      const uint8_t *rec = mb.data() + bto;
+      BufferWriter tocData;
+      REQUIRE_NOERR(UnpackEntry(refRa, EntryTOC, tocData, nullptr));
+      REQUIRE(hex_of(rec + 104 + 32, 32) == sha256_digest(tocData.data).substr(7),
+              "OCIRef Merge: blob_toc_digest");
+      REQUIRE(hex_of(rec + 104 + 64, 32) == sha256_digest(refOut.data).substr(7),
+              "OCIRef Merge: RAFS blob digest");
+      uint64_t sz = 0;
+      memcpy(&sz, rec + 104 + 96, 8);
+      REQUIRE(sz == refOut.data.size(), "OCIRef Merge: RAFS blob size %llu", (unsigned long long)sz);
+    }
   }
   PackOption ref5;
   ref5.OCIRef = true;
