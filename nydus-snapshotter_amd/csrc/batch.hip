@@ -57,6 +57,8 @@ struct Batcher {
   ngpu_result *d_res = nullptr;
   uint64_t ch_cap = 0;
   uint64_t *d_lfirst = nullptr;
+  ngpu_result **d_dst = nullptr;  // each layer's results array (the packs' own)
+  uint64_t dst_cap = 0;
   ngpu_layer_stats *d_lst = nullptr;
   uint64_t l_cap = 0;
   uint8_t *h_tab = nullptr;  // pinned: chunk table + layer boundaries of one batch
@@ -67,6 +69,27 @@ struct Batcher {
 };
 
 namespace {
+
+// One layer's results out of the batch: a multi-layer call numbers chunks
+// across the whole call, so the chunk ids in NEW / INTRA `ref` fields are
+// rebased to the layer's own (what the layer packed alone reports).
+// One kernel for all layers: chunk i of the call belongs to layer k with
+// lfirst[k] <= i < lfirst[k + 1] (binary search) and goes to dst[k][i - lfirst[k]].
+__global__ void batch_results_out(const ngpu_result *__restrict__ src, uint64_t n,
+                                  const uint64_t *__restrict__ lfirst, uint32_t K,
+                                  ngpu_result *const *__restrict__ dst) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t lo = 0, hi = K;  // the last layer whose first chunk is <= i
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (lfirst[mid] <= i) lo = mid; else hi = mid;
+  }
+  const uint64_t base = lfirst[lo];
+  ngpu_result r = src[i];
+  if (r.kind == NGPU_NEW || r.kind == NGPU_INTRA) r.ref -= base;
+  dst[lo][i - base] = r;
+}
 
 constexpr int kWindowUs = 250;
 constexpr size_t kMaxJobs = 256;
@@ -122,7 +145,8 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
     if (b.d_lst) (void)hipFree(b.d_lst), b.d_lst = nullptr;
     HIP_TRY(e, hipMalloc((void **)&b.d_lst, b.l_cap * sizeof(ngpu_layer_stats)));
   }
-  const uint64_t tab = N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t);
+  if (int rc = grow_dev(e, b, &b.d_dst, b.dst_cap, K + 1, &synced)) return rc;
+  const uint64_t tab = N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t) + K * sizeof(void *);
   if (b.tab_pending) {  // the pinned table may still be on its way to the last batch
     HIP_TRY(e, hipEventSynchronize(b.tab_sent));
     b.tab_pending = false;
@@ -142,6 +166,9 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
       hc[first[k] + i] = c;
     }
   memcpy(b.h_tab + N * sizeof(ngpu_chunk), first.data(), (K + 1) * sizeof(uint64_t));
+  ngpu_result **hd = reinterpret_cast<ngpu_result **>(b.h_tab + N * sizeof(ngpu_chunk) +
+                                                      (K + 1) * sizeof(uint64_t));
+  for (uint64_t k = 0; k < K; ++k) hd[k] = jobs[k]->d_res;
   // gather: every layer's bytes behind its own copy
   for (uint64_t k = 0; k < K; ++k) {
     HIP_TRY(e, hipStreamWaitEvent(b.s, jobs[k]->ready, 0));
@@ -153,6 +180,7 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
     HIP_TRY(e, hipMemcpyAsync(b.d_ch, b.h_tab, N * sizeof(ngpu_chunk), hipMemcpyHostToDevice, b.s));
   HIP_TRY(e, hipMemcpyAsync(b.d_lfirst, b.h_tab + N * sizeof(ngpu_chunk), (K + 1) * sizeof(uint64_t),
                             hipMemcpyHostToDevice, b.s));
+  HIP_TRY(e, hipMemcpyAsync(b.d_dst, hd, K * sizeof(void *), hipMemcpyHostToDevice, b.s));
   HIP_TRY(e, hipEventRecord(b.tab_sent, b.s));
   b.tab_pending = true;
   // ONE digest stage over all layers, ONE multi-layer dedup stage
@@ -162,17 +190,20 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
     (void)ws_release(e, b.s, nullptr, false);
     return rc;
   }
-  if (int rc = host_fence(e, b.s)) return rc;
-  // each pack's results (its device array and its pinned landing) and stats
+  // each pack's results (its device array, chunk ids rebased to its layer,
+  // then its pinned landing) and stats
   const ngpu_ws_slot &sl = *e->cur;
+  if (N) {
+    hipLaunchKernelGGL(batch_results_out, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, b.s,
+                       b.d_res, N, b.d_lfirst, (uint32_t)K, b.d_dst);
+    HIP_TRY(e, hipGetLastError());
+  }
+  if (int rc = host_fence(e, b.s)) return rc;
   for (uint64_t k = 0; k < K; ++k) {
     BatchJob &j = *jobs[k];
-    if (j.n) {
-      HIP_TRY(e, hipMemcpyAsync(j.d_res, b.d_res + first[k], j.n * sizeof(ngpu_result),
-                                hipMemcpyDeviceToDevice, b.s));
-      HIP_TRY(e, hipMemcpyAsync(j.h_res, b.d_res + first[k], j.n * sizeof(ngpu_result),
-                                hipMemcpyDeviceToHost, b.s));
-    }
+    if (j.n)
+      HIP_TRY(e, hipMemcpyAsync(j.h_res, j.d_res, j.n * sizeof(ngpu_result), hipMemcpyDeviceToHost,
+                                b.s));
     HIP_TRY(e, hipMemcpyAsync(j.h_stats, sl.ws.stats, kStWords * sizeof(uint64_t),
                               hipMemcpyDeviceToHost, b.s));
     HIP_TRY(e, hipMemcpyAsync(j.h_stats + kStatsLayer, b.d_lst + k, sizeof(ngpu_layer_stats),
@@ -262,7 +293,7 @@ void batcher_free(ngpu_engine *e) {
   DeviceGuard dg(e->device);
   if (b->s) (void)hipStreamSynchronize(b->s);
   for (void *p : {(void *)b->d_data, (void *)b->d_ch, (void *)b->d_res, (void *)b->d_lfirst,
-                  (void *)b->d_lst})
+                  (void *)b->d_lst, (void *)b->d_dst})
     if (p) (void)hipFree(p);
   if (b->h_tab) (void)hipHostFree(b->h_tab);
   if (b->tab_sent) (void)hipEventDestroy(b->tab_sent);

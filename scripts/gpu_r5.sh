@@ -31,6 +31,12 @@ for s in "$@"; do
         done
       done
       wc -l "$OUT/valu3.jsonl" ;;
+    valu4)
+      for v in compiled comp_nop; do
+        timeout -k 10 150 ./tools/valu_bank $v 256 1 >> "$OUT/valu4.jsonl" 2>> "$OUT/valu4.err"
+        ok $? "valu4 $v"
+      done
+      wc -l "$OUT/valu4.jsonl" ;;
     valu2)
       bash scripts/gpu_r5_valu2.sh "$TAG/valu2" > "$OUT/valu2.log" 2>&1
       ok $? valu2

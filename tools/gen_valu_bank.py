@@ -100,6 +100,18 @@ def streams(compiled_s=None):
     v["comp_distinct"] = compression(role, [16 + 4 * (j // 2) + 2 + (j % 2) for j in range(16)])
     if compiled_s:
         v["compiled"] = compiled_stream(compiled_s)
+        # the same G stream with the compiler's hazard pads kept (s_nop 0
+        # after most pairs of ops, as the product kernel issues it), and with
+        # pads placed by rule: s_nop K after every N VALU ops
+        v["compiled_raw"] = compiled_stream(compiled_s, keep_nops=True)
+        g = v["compiled"]
+        for n_, k_ in ((1, 0), (2, 0), (4, 0), (2, 1), (2, 3), (8, 0)):
+            ops = []
+            for i, o in enumerate(g):
+                ops.append(o)
+                if (i + 1) % n_ == 0:
+                    ops.append(f"s_nop {k_}")
+            v[f"comp_nop{k_}_every{n_}"] = ops
         for k in (48, 96):  # a barrier after every (second) G4 step
             ops = []
             for i, o in enumerate(v["compiled"]):
@@ -110,7 +122,7 @@ def streams(compiled_s=None):
     return v
 
 
-def compiled_stream(path):
+def compiled_stream(path, keep_nops=False):
     """The product kernel's whole-leaf loop (b3_groups<3,0>, the block with
     the most v_alignbit) from 672 ops before its last G op: one compression's
     G stream with the compiler's registers."""
@@ -125,15 +137,18 @@ def compiled_stream(path):
             blocks.append(cur)
             cur = []
             continue
-        if s.startswith(("v_add3_u32", "v_xor_b32", "v_alignbit_b32", "v_add_u32")):
+        if s.startswith(("v_add3_u32", "v_xor_b32", "v_alignbit_b32", "v_add_u32")) or \
+                (keep_nops and s.startswith("s_nop")):
             cur.append(s.split(";")[0].strip())
     blocks.append(cur)
     best = max(blocks, key=lambda b: sum(1 for m in b if m.startswith("v_alignbit")))
     # first run of 672 ops that starts with 4 v_add3 and holds 224 alignbit
-    for i in range(len(best) - 672):
-        seg = best[i:i + 672]
+    valu = [j for j, x in enumerate(best) if not x.startswith("s_nop")]
+    for a in range(len(valu) - 672):
+        seg = [best[j] for j in valu[a:a + 672]]
         if all(x.startswith("v_add3") for x in seg[:4]) and \
                 sum(1 for x in seg if x.startswith("v_alignbit")) == 224:
+            seg = best[valu[a]:valu[a + 671] + 1]  # with the pads between them, if kept
             return [x.replace("_e32", "").replace("_e64", "") for x in seg]
     raise SystemExit("no 672-op G stream in the hot block")
 
