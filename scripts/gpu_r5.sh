@@ -66,6 +66,12 @@ for s in "$@"; do
       timeout -k 10 600 python3 bench.py --workload c3 --steps 10 --no-cpu-baseline > "$OUT/c3.json" 2> "$OUT/c3.err"
       ok $? c3
       python3 -c "import json; d=json.loads(open('$OUT/c3.json').read().strip().splitlines()[-1]); print(d['value'], json.dumps(d['dict']))" ;;
+    packs)
+      timeout -k 10 300 python3 bench.py --workload c1 --packs 32 --steps 10 --warmup 3 > "$OUT/packs_c1.json" 2> "$OUT/packs_c1.err"
+      ok $? packs_c1
+      timeout -k 10 300 python3 bench.py --workload c1-sha256 --packs 32 --steps 5 --warmup 2 > "$OUT/packs_sha.json" 2> "$OUT/packs_sha.err"
+      ok $? packs_sha
+      tail -c 600 "$OUT/packs_c1.json" ;;
     n2)
       NYDUS_NODE_EXTRA_DEVICES=0,0 timeout -k 10 600 python3 bench.py --gpus 2 --steps 10 --warmup 5 --dist-backend gloo --c4-layers 4 > "$OUT/bench_c2_n2_gloo.json" 2> "$OUT/bench_c2_n2_gloo.err"
       ok $? n2
