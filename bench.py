@@ -1122,11 +1122,58 @@ def packs_bench(args):
         def write(self, b):
             return len(b)
 
-    def run(flags, stream):
+    drive = None
+    dpath = os.path.join(ROOT, "nydus-snapshotter_amd", "build", "libpacks_drive.so")
+    if os.path.exists(dpath):
+        import ctypes
+        drive = ctypes.CDLL(dpath).packs_drive
+        drive.restype = ctypes.c_int
+        vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
+        drive.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u64), u64, u32, u32, u32, u32,
+                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.c_char_p, u64]
+        tar_ptrs = (vp * K)(*[a.ctypes.data for a in arrs])
+        tar_lens = (u64 * K)(*[a.size for a in arrs])
+
+    def run_native(eng, stream):
+        """The rounds on K native threads (tools/packs_drive.cpp: the cgo
+        caller's shape, no GIL on the submit path)."""
+        import ctypes
+        R = args.warmup + args.steps
+        rs = (ctypes.c_double * R)()
+        per = (ctypes.c_uint64 * (4 * K))()
+        err = ctypes.create_string_buffer(512)
+        rc = drive(eng._h, K, tar_ptrs, tar_lens, 1 << 20, 1 if stream else 0,
+                   nydus_gpu._lib.DIGESTERS[wl["digester"]], wl["chunk"], R, rs, per, err, 512)
+        if rc:
+            eng.close()
+            raise RuntimeError(f"packs_drive rc={rc}: {err.value.decode(errors='replace')}")
+        kinds = np.array(per, np.uint64).reshape(K, 4)[:, :3].sum(0)
+        return sum(rs[args.warmup:]), kinds, R
+
+    def run(flags, stream, native=False):
         # 16 MiB staging slots: a C1 layer fits one (it closes in a batch),
         # and 32 packs x 2 slots pin 1 GiB instead of 16
         eng = nydus_gpu.Engine(device=0, digester=wl["digester"], chunk_size=wl["chunk"],
                                flags=flags, timing=True, staging_bytes=16 << 20)
+        if native:
+            b_before = eng.batch_stats()  # (counted over every round: warmup included)
+            el, kinds, R = run_native(eng, stream)
+            b1 = eng.batch_stats()
+            nb = b1["batches"] - b_before["batches"]
+            dev = None
+            if nb:
+                tms = [eng.timing_at(k) for k in range(min(nb, 64))]
+                dev_ms = sum(t["total_ms"] for t in tms)
+                packs_in = (b1["packs"] - b_before["packs"]) * min(nb, 64) / nb
+                dev = round(file_bytes / K * packs_in / (dev_ms / 1e3) / 1e9, 2) if dev_ms else None
+            eng.close()
+            return {"gbs": round(file_bytes * args.steps / el / 1e9, 2),
+                    "ms_per_round": round(el / args.steps * 1e3, 3), "device_gbs": dev,
+                    "launch_sets_per_round": round(nb / R, 2),
+                    "packs_per_set": round((b1["packs"] - b_before["packs"]) / nb, 1) if nb else 0,
+                    "most_packs_in_one_set": b1["max_packs"],
+                    "decisions_last_round": {"NEW": int(kinds[0]), "INTRA": int(kinds[1]),
+                                             "DICT": int(kinds[2])}}
         meet = threading.Barrier(K + 1)
         errs = []
         kinds = np.zeros(3, np.int64)
@@ -1184,14 +1231,20 @@ def packs_bench(args):
         eng.close()
         return {"gbs": round(file_bytes * args.steps / el / 1e9, 2),
                 "ms_per_round": round(el / args.steps * 1e3, 3),
-                "device_gbs": dev, "launch_sets": nb, "packs_batched": b1["packs"] - b0["packs"],
+                "device_gbs": dev, "launch_sets_per_round": round(nb / args.steps, 2),
+                "packs_per_set": round((b1["packs"] - b0["packs"]) / nb, 1) if nb else 0,
                 "most_packs_in_one_set": b1["max_packs"],
                 "decisions_last_round": {"NEW": int(kinds[0]), "INTRA": int(kinds[1]),
                                          "DICT": int(kinds[2])}}
 
-    modes = {"decisions": run(0, False),
-             "decisions_no_batch": run(nydus_gpu.FLAG_NO_BATCH, False),
-             "stream_zstd": run(0, True)}
+    if drive is None:
+        raise SystemExit(f"{dpath} is missing: run `make -C nydus-snapshotter_amd`")
+    # native threads (the cgo caller's shape) are the line; Python threads beside
+    modes = {"decisions": run(0, False, native=True),
+             "decisions_no_batch": run(nydus_gpu.FLAG_NO_BATCH, False, native=True),
+             "stream_zstd": run(0, True, native=True),
+             "stream_zstd_no_batch": run(nydus_gpu.FLAG_NO_BATCH, True, native=True),
+             "decisions_python_threads": run(0, False)}
     cpu = None
     if not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -1240,7 +1293,9 @@ def packs_bench(args):
             "config": {"workload": f"{K} concurrent converter.Pack calls of distinct C1-size "
                                    f"layers on one engine ({wl['digester']}, 1 MiB chunks)",
                        "name": args.workload, "packs": K, "file_bytes_per_round": file_bytes,
-                       "tar_bytes_per_round": tar_bytes, "batch_window_us": 250},
+                       "tar_bytes_per_round": tar_bytes, "batch_window_us": 250,
+                       "caller": "K native threads (tools/packs_drive.cpp), 1 MiB writes from "
+                                 "pageable memory"},
             "modes": modes, "cpu_baseline": cpu,
             "bound": "PCIe H2D of the tars (~50 GB/s) and the host copies into pinned staging; "
                      "sha256: one 1 MiB chunk's chain per launch set (~21 ms)"}

@@ -57,7 +57,7 @@ struct Batcher {
   ngpu_result *d_res = nullptr;
   uint64_t ch_cap = 0;
   uint64_t *d_lfirst = nullptr;
-  ngpu_result **d_dst = nullptr;  // each layer's results array (the packs' own)
+  void **d_dst = nullptr;  // per layer: its pack's pinned results, then its pinned stats
   uint64_t dst_cap = 0;
   ngpu_layer_stats *d_lst = nullptr;
   uint64_t l_cap = 0;
@@ -65,6 +65,7 @@ struct Batcher {
   uint64_t h_cap = 0;
   hipEvent_t tab_sent = nullptr;  // the last batch's table upload
   bool tab_pending = false;
+  std::shared_ptr<BatchEvent> last;  // the end of the last batch enqueued
   uint64_t batches = 0, jobs = 0, max_jobs = 0;
 };
 
@@ -72,7 +73,9 @@ namespace {
 
 // One layer's results out of the batch: a multi-layer call numbers chunks
 // across the whole call, so the chunk ids in NEW / INTRA `ref` fields are
-// rebased to the layer's own (what the layer packed alone reports).
+// rebased to the layer's own (what the layer packed alone reports).  They go
+// straight into each pack's pinned read-back buffer (mapped host memory), so
+// a batch of K layers ends in two launches instead of 3K small D2H copies.
 // One kernel for all layers: chunk i of the call belongs to layer k with
 // lfirst[k] <= i < lfirst[k + 1] (binary search) and goes to dst[k][i - lfirst[k]].
 __global__ void batch_results_out(const ngpu_result *__restrict__ src, uint64_t n,
@@ -91,7 +94,19 @@ __global__ void batch_results_out(const ngpu_result *__restrict__ src, uint64_t 
   dst[lo][i - base] = r;
 }
 
+// Each layer's stats into its pack's pinned read-back words (block k: layer k):
+// the call's counters (kStWords) and the layer's own stats at kStatsLayer.
+__global__ void batch_stats_out(const uint64_t *__restrict__ st, const ngpu_layer_stats *__restrict__ lst,
+                                uint64_t *const *__restrict__ dst) {
+  const uint32_t k = blockIdx.x, t = threadIdx.x;
+  constexpr uint32_t kL = sizeof(ngpu_layer_stats) / sizeof(uint64_t);
+  static_assert(sizeof(ngpu_layer_stats) % sizeof(uint64_t) == 0, "layer stats are whole words");
+  if (t < (uint32_t)kStWords) dst[k][t] = st[t];
+  if (t < kL) dst[k][kStatsLayer + t] = reinterpret_cast<const uint64_t *>(lst + k)[t];
+}
+
 constexpr int kWindowUs = 250;
+constexpr int kPollUs = 50;  // the last batch's end, polled while packs gather
 constexpr size_t kMaxJobs = 256;
 constexpr uint64_t kMaxBytes = 1ull << 30;
 constexpr uint64_t kMaxChunks = 1ull << 20;
@@ -145,8 +160,8 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
     if (b.d_lst) (void)hipFree(b.d_lst), b.d_lst = nullptr;
     HIP_TRY(e, hipMalloc((void **)&b.d_lst, b.l_cap * sizeof(ngpu_layer_stats)));
   }
-  if (int rc = grow_dev(e, b, &b.d_dst, b.dst_cap, K + 1, &synced)) return rc;
-  const uint64_t tab = N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t) + K * sizeof(void *);
+  if (int rc = grow_dev(e, b, &b.d_dst, b.dst_cap, 2 * K + 2, &synced)) return rc;
+  const uint64_t tab = N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t) + 2 * K * sizeof(void *);
   if (b.tab_pending) {  // the pinned table may still be on its way to the last batch
     HIP_TRY(e, hipEventSynchronize(b.tab_sent));
     b.tab_pending = false;
@@ -166,9 +181,11 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
       hc[first[k] + i] = c;
     }
   memcpy(b.h_tab + N * sizeof(ngpu_chunk), first.data(), (K + 1) * sizeof(uint64_t));
-  ngpu_result **hd = reinterpret_cast<ngpu_result **>(b.h_tab + N * sizeof(ngpu_chunk) +
-                                                      (K + 1) * sizeof(uint64_t));
-  for (uint64_t k = 0; k < K; ++k) hd[k] = jobs[k]->d_res;
+  void **hd = reinterpret_cast<void **>(b.h_tab + N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t));
+  for (uint64_t k = 0; k < K; ++k) {  // the packs' pinned buffers as the device sees them
+    HIP_TRY(e, hipHostGetDevicePointer(&hd[k], jobs[k]->h_res, 0));
+    HIP_TRY(e, hipHostGetDevicePointer(&hd[K + k], jobs[k]->h_stats, 0));
+  }
   // gather: every layer's bytes behind its own copy
   for (uint64_t k = 0; k < K; ++k) {
     HIP_TRY(e, hipStreamWaitEvent(b.s, jobs[k]->ready, 0));
@@ -180,7 +197,7 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
     HIP_TRY(e, hipMemcpyAsync(b.d_ch, b.h_tab, N * sizeof(ngpu_chunk), hipMemcpyHostToDevice, b.s));
   HIP_TRY(e, hipMemcpyAsync(b.d_lfirst, b.h_tab + N * sizeof(ngpu_chunk), (K + 1) * sizeof(uint64_t),
                             hipMemcpyHostToDevice, b.s));
-  HIP_TRY(e, hipMemcpyAsync(b.d_dst, hd, K * sizeof(void *), hipMemcpyHostToDevice, b.s));
+  HIP_TRY(e, hipMemcpyAsync(b.d_dst, hd, 2 * K * sizeof(void *), hipMemcpyHostToDevice, b.s));
   HIP_TRY(e, hipEventRecord(b.tab_sent, b.s));
   b.tab_pending = true;
   // ONE digest stage over all layers, ONE multi-layer dedup stage
@@ -190,26 +207,19 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
     (void)ws_release(e, b.s, nullptr, false);
     return rc;
   }
-  // each pack's results (its device array, chunk ids rebased to its layer,
-  // then its pinned landing) and stats
+  // each pack's results (chunk ids rebased to its layer) and stats, into its
+  // pinned read-back buffers
   const ngpu_ws_slot &sl = *e->cur;
   if (N) {
     hipLaunchKernelGGL(batch_results_out, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, b.s,
-                       b.d_res, N, b.d_lfirst, (uint32_t)K, b.d_dst);
+                       b.d_res, N, b.d_lfirst, (uint32_t)K, reinterpret_cast<ngpu_result **>(b.d_dst));
     HIP_TRY(e, hipGetLastError());
   }
+  hipLaunchKernelGGL(batch_stats_out, dim3((unsigned)K), dim3(64), 0, b.s, sl.ws.stats, b.d_lst,
+                     reinterpret_cast<uint64_t **>(b.d_dst + K));
+  HIP_TRY(e, hipGetLastError());
   if (int rc = host_fence(e, b.s)) return rc;
-  for (uint64_t k = 0; k < K; ++k) {
-    BatchJob &j = *jobs[k];
-    if (j.n)
-      HIP_TRY(e, hipMemcpyAsync(j.h_res, j.d_res, j.n * sizeof(ngpu_result), hipMemcpyDeviceToHost,
-                                b.s));
-    HIP_TRY(e, hipMemcpyAsync(j.h_stats, sl.ws.stats, kStWords * sizeof(uint64_t),
-                              hipMemcpyDeviceToHost, b.s));
-    HIP_TRY(e, hipMemcpyAsync(j.h_stats + kStatsLayer, b.d_lst + k, sizeof(ngpu_layer_stats),
-                              hipMemcpyDeviceToHost, b.s));
-    snprintf(j.path, sizeof j.path, "%s", sl.path);
-  }
+  for (uint64_t k = 0; k < K; ++k) snprintf(jobs[k]->path, sizeof jobs[k]->path, "%s", sl.path);
   auto done = std::make_shared<BatchEvent>();
   done->device = e->device;
   HIP_TRY(e, hipEventCreateWithFlags(&done->ev, hipEventDisableTiming));
@@ -218,6 +228,7 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
     j->done = done;
     j->batch_layers = (uint32_t)K;
   }
+  b.last = done;
   ++b.batches;
   b.jobs += K;
   b.max_jobs = std::max<uint64_t>(b.max_jobs, K);
@@ -237,9 +248,20 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
       continue;
     }
     b.leading = true;
+    // wait for the open packs to join: until all have, or kWindowUs has passed
+    // and the last batch is off the device (while it runs, a new launch set
+    // would only queue behind it -- better to let more packs join this one)
     const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(kWindowUs);
-    while (b.open.size() < (size_t)e->open_packs.load() && b.open.size() < kMaxJobs &&
-           b.cv.wait_until(lk, until) == std::cv_status::no_timeout) {
+    for (;;) {
+      if (b.open.size() >= (size_t)e->open_packs.load() || b.open.size() >= kMaxJobs) break;
+      const auto now = std::chrono::steady_clock::now();
+      bool prev_running = false;
+      if (b.last) {
+        DeviceGuard dg(e->device);
+        prev_running = hipEventQuery(b.last->ev) == hipErrorNotReady;
+      }
+      if (!prev_running && now >= until) break;
+      b.cv.wait_until(lk, prev_running ? now + std::chrono::microseconds(kPollUs) : until);
     }
     // this leader's batch: the open packs sharing its dict, within the caps
     std::vector<BatchJob *> take;

@@ -252,7 +252,13 @@ bool read_header(const uint8_t h[512], std::string *name, int64_t *size) {
   return *size >= 0;
 }
 
-// ---- small thread pool for per-chunk compression ---------------------------
+// ---- shared thread pool for per-chunk compression -------------------------
+// One pool per thread count, process-wide and shared by every writer: K packs
+// closing at once (containerd converting an image's layers concurrently,
+// convert_unix.go:822) queue their batches on the same n threads instead of
+// K pools of n (32 concurrent C1 packs used to spawn, oversubscribe and join
+// 24 pools of 16 threads every round).  run() is a parallel-for any number of
+// callers may be inside at once; a caller works on its own batch too.
 class Pool {
  public:
   explicit Pool(unsigned n) {
@@ -270,43 +276,65 @@ class Pool {
   // Runs f(i) for i in [0, n) on the pool and the calling thread.
   template <typename F>
   void run(uint64_t n, F &&f) {
-    std::function<void(uint64_t)> fn = f;
-    std::atomic<uint64_t> next{0};
-    auto body = [&] {
-      for (uint64_t i; (i = next.fetch_add(1)) < n;) fn(i);
-    };
+    if (!n) return;
+    Job j;
+    j.n = n;
+    j.fn = f;
     {
       std::lock_guard<std::mutex> g(m_);
-      job_ = [&] { body(); };
-      gen_++;
-      active_ = (unsigned)th_.size();
+      q_.push_back(&j);
     }
     cv_.notify_all();
-    body();
+    work(j);
     std::unique_lock<std::mutex> g(m_);
-    done_.wait(g, [this] { return active_ == 0; });
-    job_ = nullptr;
+    done_.wait(g, [&] { return j.finished == j.n && j.users == 0; });
+    for (size_t i = 0; i < q_.size(); ++i)
+      if (q_[i] == &j) {
+        q_.erase(q_.begin() + (long)i);
+        break;
+      }
   }
 
  private:
+  struct Job {
+    uint64_t n = 0;
+    std::function<void(uint64_t)> fn;
+    std::atomic<uint64_t> next{0};
+    uint64_t finished = 0;  // items done (m_)
+    unsigned users = 0;     // pool threads inside work() (m_)
+  };
+  // claims items of j until none is left; j stays alive while this thread is
+  // counted in j.users (pool threads) or is its owner (the caller of run)
+  void work(Job &j) {
+    uint64_t did = 0;
+    for (uint64_t i; (i = j.next.fetch_add(1)) < j.n; ++did) j.fn(i);
+    std::lock_guard<std::mutex> g(m_);
+    j.finished += did;
+    if (j.finished == j.n) done_.notify_all();
+  }
   void loop() {
-    uint64_t seen = 0;
     std::unique_lock<std::mutex> g(m_);
     for (;;) {
-      cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+      Job *j = nullptr;
+      cv_.wait(g, [&] {
+        if (stop_) return true;
+        for (Job *x : q_)  // the oldest batch with items left
+          if (x->next.load() < x->n) {
+            j = x;
+            return true;
+          }
+        return false;
+      });
       if (stop_) return;
-      seen = gen_;
-      auto job = job_;
+      ++j->users;
       g.unlock();
-      job();
+      work(*j);
       g.lock();
-      if (--active_ == 0) done_.notify_all();
+      if (--j->users == 0) done_.notify_all();
     }
   }
   std::vector<std::thread> th_;
-  std::function<void()> job_;
-  uint64_t gen_ = 0;
-  unsigned active_ = 0;
+  std::vector<Job *> q_;  // batches with callers inside run()
   bool stop_ = false;
   std::mutex m_;
   std::condition_variable cv_, done_;
@@ -330,49 +358,45 @@ struct Batch {
   uint8_t &operator[](uint64_t i) { return p[i]; }
 };
 
-// A writer lives for one Pack; its compression pool and batch buffers stay
-// for the next writer (joining a 16-thread pool and unmapping three 64 MiB
-// buffers were ~20 ms of every early-emission Pack's close, and the next
-// writer's first batches paid the page faults again).  Process-wide, never
-// destroyed (no exit-time teardown of idle threads).
+// A writer lives for one Pack; the compression pools are shared and its
+// batch / scratch buffers stay for the next writers (joining a 16-thread pool
+// and unmapping three 64 MiB buffers were ~20 ms of every early-emission
+// Pack's close, the next writer's first batches paid the page faults again,
+// and 32 concurrent packs overflowed an 8-buffer cache every round).  Buffers
+// are kept up to kCacheBytes.  Process-wide, never destroyed (no exit-time
+// teardown of idle threads).
 struct WriterCache {
-  static constexpr size_t kPools = 8, kBufs = 8;
-  static constexpr uint64_t kBufMax = 64ull << 20;
+  static constexpr uint64_t kBufMax = 64ull << 20, kCacheBytes = 2ull << 30;
   std::mutex m;
   std::vector<std::unique_ptr<Pool>> pools;
   std::vector<Batch> bufs;
+  uint64_t cached = 0;  // bytes in bufs
   static WriterCache &get() {
     static WriterCache *c = new WriterCache;
     return *c;
   }
-  std::unique_ptr<Pool> take_pool(unsigned n) {
-    {
-      std::lock_guard<std::mutex> g(m);
-      for (size_t i = 0; i < pools.size(); ++i)
-        if (pools[i]->size() == n) {
-          std::unique_ptr<Pool> p = std::move(pools[i]);
-          pools.erase(pools.begin() + (long)i);
-          return p;
-        }
-    }
-    return std::unique_ptr<Pool>(new Pool(n));
-  }
-  void put_pool(std::unique_ptr<Pool> p) {
-    if (!p) return;
+  // the process-wide pool of n threads (created on first use, never destroyed)
+  Pool *pool(unsigned n) {
     std::lock_guard<std::mutex> g(m);
-    if (pools.size() < kPools) pools.push_back(std::move(p));
+    for (auto &p : pools)
+      if (p->size() == n) return p.get();
+    pools.emplace_back(new Pool(n));
+    return pools.back().get();
   }
   bool take_buf(Batch *b) {
     std::lock_guard<std::mutex> g(m);
     if (bufs.empty()) return false;
     *b = std::move(bufs.back());
     bufs.pop_back();
+    cached -= b->cap;
     return true;
   }
   void put_buf(Batch &&b) {
     if (!b.p || b.cap > kBufMax) return;
     std::lock_guard<std::mutex> g(m);
-    if (bufs.size() < kBufs) bufs.push_back(std::move(b));
+    if (cached + b.cap > kCacheBytes) return;
+    cached += b.cap;
+    bufs.push_back(std::move(b));
   }
 };
 
@@ -550,7 +574,7 @@ struct BlobWriter::Impl {
   uint64_t n_place = 0;
   const volatile int32_t *cancel = nullptr;
   const ZranRef *zref = nullptr;  // OCIRef: the own blob is the original gzip blob
-  std::unique_ptr<Pool> pool;
+  Pool *pool = nullptr;  // shared (WriterCache)
   Sha blob_sha;      // image.blob data
   Sha stream_sha;    // whole stream (continued from blob_sha)
   uint64_t written = 0;
@@ -558,7 +582,8 @@ struct BlobWriter::Impl {
   std::vector<uint8_t> cflag;
   uint64_t compressed_chunks = 0;
   // batch buffers: per-chunk scratch slots, compacted into an output batch
-  std::vector<uint8_t> scratch;
+  Batch scratch;  // from the cache at the first compressed batch
+  bool scratch_taken = false;
   std::vector<uint64_t> slot_off;
   std::vector<uint64_t> clen;
   int rc = 0;
@@ -654,7 +679,7 @@ struct BlobWriter::Impl {
     qcv.notify_all();
     if (sink.joinable()) sink.join();
     WriterCache &wc = WriterCache::get();
-    wc.put_pool(std::move(pool));
+    wc.put_buf(std::move(scratch));
     for (Batch &b : free_bufs) wc.put_buf(std::move(b));
     for (Batch &b : q) wc.put_buf(std::move(b));
     const char *v = getenv("NGPU_SINK_STATS");
@@ -700,7 +725,7 @@ int BlobWriter::init() {
     const unsigned hw = std::thread::hardware_concurrency();
     t = hw ? std::min(16u, hw) : 4u;
   }
-  im_->pool = WriterCache::get().take_pool(t);
+  im_->pool = WriterCache::get().pool(t);
   Impl *m = im_.get();
   m->sink = std::thread([m] { m->sink_loop(); });
   return 0;
@@ -734,6 +759,7 @@ int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) 
       m.slot_off[0] = 0;
       for (uint64_t i = 0; i < nb; ++i)
         m.slot_off[i + 1] = m.slot_off[i] + compress_bound(kind, len[a + i]);
+      if (!m.scratch_taken) m.scratch_taken = WriterCache::get().take_buf(&m.scratch) || true;
       m.scratch.resize(m.slot_off[nb]);
       m.clen.assign(nb, 0);
       m.pool->run(nb, [&](uint64_t i) {

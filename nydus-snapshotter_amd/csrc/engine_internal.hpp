@@ -128,9 +128,8 @@ struct BatchJob {
   uint64_t n = 0;
   hipEvent_t ready = nullptr;        // d_data is complete after this event
   const ngpu_dict *dict = nullptr;
-  ngpu_result *d_res = nullptr;      // the pack's device results (n)
-  void *h_res = nullptr;             // pinned, n results
-  uint64_t *h_stats = nullptr;       // pinned, 32 words (read_stats_parse layout)
+  void *h_res = nullptr;             // pinned (hipHostMalloc), n results, written by the batch
+  uint64_t *h_stats = nullptr;       // pinned (hipHostMalloc), 32 words (read_stats_parse layout)
   int rc = 0;
   bool enqueued = false;
   uint32_t batch_layers = 0;         // layers in the launch set it joined

@@ -1233,7 +1233,6 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
       job.n = n;
       job.ready = cs.copied;
       job.dict = p->dict;
-      job.d_res = p->d_res;
       job.h_res = p->h_io;
       job.h_stats = p->h_stats;
       rc = batch_run(e, job);

@@ -484,7 +484,9 @@ def test_blob_writer_threads_tsan(oracle, tars, tmp_path):
     """The host blob writer's compression pool + ordered sink (ngpu_blob_write
     with 8 threads, tests/cpp/blob_tsan.cpp) built under ThreadSanitizer:
     no data race reported, and the stream is byte-equal to the regular
-    build's for every compressor, with chunk-dict records in the bootstrap."""
+    build's for every compressor, with chunk-dict records in the bootstrap;
+    four writers at once on the process-wide shared pool give that same
+    stream each."""
     import subprocess
     from conftest import ROOT
     from nydus_gpu._lib import NgpuLayerStats
@@ -511,7 +513,9 @@ def test_blob_writer_threads_tsan(oracle, tars, tmp_path):
     for k, v in files.items():
         (tmp_path / k).write_bytes(v)
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66")
-    for name, code in (("zstd", 2), ("lz4_block", 4), ("none", 1)):
+    runs = (("zstd", 2, 1), ("lz4_block", 4, 1), ("none", 1, 1), ("zstd", 2, 4))
+    for name, code, writers in runs:  # writers > 1: concurrent writers on the shared pool
+        env["BLOB_TSAN_WRITERS"] = str(writers)
         p = tmp_path / f"out-{name}"
         r = subprocess.run([exe] + [str(tmp_path / k) for k in ("data", "ch", "res", "st")] +
                            [str(p), str(code), "8", str(cs), "0",

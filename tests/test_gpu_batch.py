@@ -136,3 +136,41 @@ def test_batched_stream_equals_unbatched():
     assert streams["batched_stats"]["max_packs"] >= 2, streams["batched_stats"]
     for a, b in zip(streams["batched"], streams["unbatched"]):
         assert a == b
+
+
+def test_native_threads_drive_concurrent_packs(oracle):
+    """tools/packs_drive.cpp (bench.py --packs's caller: K native threads, one
+    Pack each, as cgo goroutines would): decisions and early-emission streams
+    of 8 concurrent layers, counted per layer, equal the oracle's."""
+    import ctypes
+    import os
+    lib_path = os.path.join(os.path.dirname(nydus_gpu._lib.LIB_PATH), "build", "libpacks_drive.so")
+    drive = ctypes.CDLL(lib_path).packs_drive
+    vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
+    drive.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u64), u64, u32, u32, u32, u32,
+                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.c_char_p, u64]
+    S, K = 0x100000, 8
+    tars = [np.frombuffer(layers.alpine_like_tar(0xD0 + i), np.uint8) for i in range(K)]
+    want = []
+    for t in tars:
+        ch = oracle.tar_chunks(t.tobytes(), S)
+        dec, _ = oracle.dedup(oracle.digest_chunks(t.tobytes(), ch, "blake3"), ch["length"])
+        want.append(np.bincount(dec["kind"], minlength=3)[:3])
+    for mode in (0, 1):
+        eng = nydus_gpu.Engine(device=0, chunk_size=S, staging_bytes=16 << 20)
+        try:
+            rs = (ctypes.c_double * 3)()
+            per = (u64 * (4 * K))()
+            err = ctypes.create_string_buffer(256)
+            rc = drive(eng._h, K, (vp * K)(*[t.ctypes.data for t in tars]),
+                       (u64 * K)(*[t.size for t in tars]), 1 << 20, mode, 0, S, 3, rs, per, err, 256)
+            assert rc == 0, err.value
+            bs = eng.batch_stats()
+        finally:
+            eng.close()
+        got = np.array(per, np.uint64).reshape(K, 4)
+        for k in range(K):
+            assert list(got[k, :3]) == list(want[k]), (mode, k)
+            assert (got[k, 3] > 0) == (mode == 1)
+        assert all(x > 0 for x in rs)
+        assert bs["packs"] >= 2, bs
