@@ -1130,7 +1130,8 @@ def packs_bench(args):
         drive.restype = ctypes.c_int
         vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
         drive.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u64), u64, u32, u32, u32, u32,
-                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.c_char_p, u64]
+                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64),
+                          ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, u64]
         tar_ptrs = (vp * K)(*[a.ctypes.data for a in arrs])
         tar_lens = (u64 * K)(*[a.size for a in arrs])
 
@@ -1141,14 +1142,23 @@ def packs_bench(args):
         R = args.warmup + args.steps
         rs = (ctypes.c_double * R)()
         per = (ctypes.c_uint64 * (4 * K))()
+        tr = np.zeros((R, K, 3), np.float64)
         err = ctypes.create_string_buffer(512)
         rc = drive(eng._h, K, tar_ptrs, tar_lens, 1 << 20, 1 if stream else 0,
-                   nydus_gpu._lib.DIGESTERS[wl["digester"]], wl["chunk"], R, rs, per, err, 512)
+                   nydus_gpu._lib.DIGESTERS[wl["digester"]], wl["chunk"], R, rs, per,
+                   tr.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), err, 512)
         if rc:
             eng.close()
             raise RuntimeError(f"packs_drive rc={rc}: {err.value.decode(errors='replace')}")
         kinds = np.array(per, np.uint64).reshape(K, 4)[:, :3].sum(0)
-        return sum(rs[args.warmup:]), kinds, R
+        t = tr[args.warmup:] * 1e3  # timed rounds, ms from each round's start
+        phases = {"last_write_ms_median": round(float(np.median(t[:, :, 1].max(1))), 3),
+                  "write_ms_per_pack_median": round(float(np.median(t[:, :, 1] - t[:, :, 0])), 3),
+                  "close_ms_per_pack_median": round(float(np.median(t[:, :, 2] - t[:, :, 1])), 3),
+                  "close_ms_per_pack_max": round(float((t[:, :, 2] - t[:, :, 1]).max()), 3),
+                  "tail_after_last_write_ms_median":
+                      round(float(np.median(t[:, :, 2].max(1) - t[:, :, 1].max(1))), 3)}
+        return sum(rs[args.warmup:]), kinds, R, phases
 
     def run(flags, stream, native=False):
         # 16 MiB staging slots: a C1 layer fits one (it closes in a batch),
@@ -1157,7 +1167,7 @@ def packs_bench(args):
                                flags=flags, timing=True, staging_bytes=16 << 20)
         if native:
             b_before = eng.batch_stats()  # (counted over every round: warmup included)
-            el, kinds, R = run_native(eng, stream)
+            el, kinds, R, phases = run_native(eng, stream)
             b1 = eng.batch_stats()
             nb = b1["batches"] - b_before["batches"]
             dev = None
@@ -1171,7 +1181,7 @@ def packs_bench(args):
                     "ms_per_round": round(el / args.steps * 1e3, 3), "device_gbs": dev,
                     "launch_sets_per_round": round(nb / R, 2),
                     "packs_per_set": round((b1["packs"] - b_before["packs"]) / nb, 1) if nb else 0,
-                    "most_packs_in_one_set": b1["max_packs"],
+                    "most_packs_in_one_set": b1["max_packs"], "phases": phases,
                     "decisions_last_round": {"NEW": int(kinds[0]), "INTRA": int(kinds[1]),
                                              "DICT": int(kinds[2])}}
         meet = threading.Barrier(K + 1)

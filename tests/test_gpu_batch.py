@@ -148,7 +148,8 @@ def test_native_threads_drive_concurrent_packs(oracle):
     drive = ctypes.CDLL(lib_path).packs_drive
     vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
     drive.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u64), u64, u32, u32, u32, u32,
-                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.c_char_p, u64]
+                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64),
+                      ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, u64]
     S, K = 0x100000, 8
     tars = [np.frombuffer(layers.alpine_like_tar(0xD0 + i), np.uint8) for i in range(K)]
     want = []
@@ -163,7 +164,7 @@ def test_native_threads_drive_concurrent_packs(oracle):
             per = (u64 * (4 * K))()
             err = ctypes.create_string_buffer(256)
             rc = drive(eng._h, K, (vp * K)(*[t.ctypes.data for t in tars]),
-                       (u64 * K)(*[t.size for t in tars]), 1 << 20, mode, 0, S, 3, rs, per, err, 256)
+                       (u64 * K)(*[t.size for t in tars]), 1 << 20, mode, 0, S, 3, rs, per, None, err, 256)
             assert rc == 0, err.value
             bs = eng.batch_stats()
         finally:

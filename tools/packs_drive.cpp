@@ -9,7 +9,9 @@
 // `piece`-byte writes, closes it (mode 0: decisions back) or finishes the
 // early-emission stream (mode 1: ngpu_pack_set_output before the first write,
 // zstd, into a counting sink), then all meet; round_s[r] = the wall time from
-// the round's start (every thread released) to its last close.
+// the round's start (every thread released) to its last close.  trace (or
+// NULL): per round and layer, seconds from the round's start to the pack's
+// open, its last write and its close returning (rounds x k x 3).
 //
 // build: nydus-snapshotter_amd/Makefile (build/libpacks_drive.so)
 #include <stdio.h>
@@ -69,7 +71,7 @@ int count_sink(void *ctx, const void *, uint64_t len) {
 extern "C" int packs_drive(ngpu_engine *eng, uint32_t k, const uint8_t *const *tars,
                            const uint64_t *lens, uint64_t piece, uint32_t mode, uint32_t digester,
                            uint32_t chunk_size, uint32_t rounds, double *round_s,
-                           uint64_t *per_layer, char *err, uint64_t err_len) {
+                           uint64_t *per_layer, double *trace, char *err, uint64_t err_len) {
   if (!eng || !k || !tars || !lens || !piece || !rounds || !round_s || !per_layer) return NGPU_EINVAL;
   Barrier meet(k + 1);
   std::mutex em;
@@ -83,6 +85,13 @@ extern "C" int packs_drive(ngpu_engine *eng, uint32_t k, const uint8_t *const *t
     }
     meet.abort();
   };
+  using clk = std::chrono::steady_clock;
+  std::vector<clk::time_point> t_round(rounds);
+  auto mark = [&](uint32_t r, uint32_t i, int what) {
+    if (trace)
+      trace[((uint64_t)r * k + i) * 3 + what] =
+          std::chrono::duration<double>(clk::now() - t_round[r]).count();
+  };
   std::vector<std::thread> th;
   for (uint32_t i = 0; i < k; ++i)
     th.emplace_back([&, i] {
@@ -92,6 +101,7 @@ extern "C" int packs_drive(ngpu_engine *eng, uint32_t k, const uint8_t *const *t
         uint64_t out_bytes = 0;
         int rc = ngpu_pack_open_ex(eng, mode ? NGPU_PACK_RETAIN : 0, &p);
         if (rc) return fail(rc, "pack_open");
+        mark(r, i, 0);
         if (mode) {
           ngpu_blob_options o;
           memset(&o, 0, sizeof o);
@@ -111,6 +121,7 @@ extern "C" int packs_drive(ngpu_engine *eng, uint32_t k, const uint8_t *const *t
             return fail(rc, "pack_write");
           }
         }
+        mark(r, i, 1);
         ngpu_chunk *ch = nullptr;
         ngpu_result *res = nullptr;
         uint64_t n = 0;
@@ -122,6 +133,7 @@ extern "C" int packs_drive(ngpu_engine *eng, uint32_t k, const uint8_t *const *t
           rc = ngpu_pack_close(p, &ch, &res, &n, &st);
         }
         if (rc) return fail(rc, mode ? "pack_finish" : "pack_close");
+        mark(r, i, 2);
         if (r + 1 == rounds) {
           uint64_t *o = per_layer + 4 * (uint64_t)i;
           o[0] = o[1] = o[2] = 0;
@@ -134,10 +146,10 @@ extern "C" int packs_drive(ngpu_engine *eng, uint32_t k, const uint8_t *const *t
         if (!meet.wait()) return;
       }
     });
-  using clk = std::chrono::steady_clock;
   for (uint32_t r = 0; r < rounds; ++r) {
+    t_round[r] = clk::now();  // (before the release: the threads read it after the barrier)
     if (!meet.wait()) break;  // round r starts
-    const auto t0 = clk::now();
+    const auto t0 = t_round[r];
     if (!meet.wait()) break;  // every pack of round r closed
     round_s[r] = std::chrono::duration<double>(clk::now() - t0).count();
   }
