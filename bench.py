@@ -1250,11 +1250,15 @@ def packs_bench(args):
     if drive is None:
         raise SystemExit(f"{dpath} is missing: run `make -C nydus-snapshotter_amd`")
     # native threads (the cgo caller's shape) are the line; Python threads beside
-    modes = {"decisions": run(0, False, native=True),
-             "decisions_no_batch": run(nydus_gpu.FLAG_NO_BATCH, False, native=True),
-             "stream_zstd": run(0, True, native=True),
-             "stream_zstd_no_batch": run(nydus_gpu.FLAG_NO_BATCH, True, native=True),
-             "decisions_python_threads": run(0, False)}
+    plan = {"decisions": lambda: run(0, False, native=True),
+            "decisions_no_batch": lambda: run(nydus_gpu.FLAG_NO_BATCH, False, native=True),
+            "stream_zstd": lambda: run(0, True, native=True),
+            "stream_zstd_no_batch": lambda: run(nydus_gpu.FLAG_NO_BATCH, True, native=True),
+            "decisions_python_threads": lambda: run(0, False)}
+    pick = [m for m in args.packs_modes.split(",") if m] if args.packs_modes else list(plan)
+    if "decisions" not in pick or any(m not in plan for m in pick):
+        raise SystemExit(f"--packs-modes: a subset of {list(plan)} with 'decisions'")
+    modes = {m: plan[m]() for m in pick}
     cpu = None
     if not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -1311,7 +1315,7 @@ def packs_bench(args):
                      "sha256: one 1 MiB chunk's chain per launch set (~21 ms)"}
     if cpu:
         line["speedup_vs_cpu"] = round(modes["decisions"]["gbs"] / cpu["value"], 2)
-        if cpu.get("pipeline_gbs"):
+        if cpu.get("pipeline_gbs") and "stream_zstd" in modes:
             line["stream_vs_cpu_pipeline"] = round(modes["stream_zstd"]["gbs"] / cpu["pipeline_gbs"], 2)
         if modes["decisions"]["device_gbs"]:
             line["speedup_vs_cpu_device"] = round(modes["decisions"]["device_gbs"] / cpu["value"], 2)
@@ -1684,6 +1688,8 @@ def main():
     ap.add_argument("--packs", type=int, default=0,
                     help="tar workloads: K concurrent converter.Pack calls per round on one engine "
                          "(batched closes); see packs_bench")
+    ap.add_argument("--packs-modes", default="",
+                    help="--packs: comma-separated modes to run (default all; 'decisions' required)")
     ap.add_argument("--engines", type=int, default=1,
                     help="tar workloads: K engines on device 0 convert layers concurrently")
     ap.add_argument("--no-sub", action="store_true",

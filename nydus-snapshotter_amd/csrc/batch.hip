@@ -237,6 +237,22 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
 
 }  // namespace
 
+// NGPU_BATCH_TRACE=1: one line per launch set on stderr (diagnostic): when
+// its leader arrived, stopped waiting and had it enqueued, the layers it took
+// and how many packs were open, microseconds since the engine's first batch.
+static bool batch_trace_on() {
+  static const bool on = [] {
+    const char *v = getenv("NGPU_BATCH_TRACE");
+    return v && *v == '1';
+  }();
+  return on;
+}
+
+static double batch_now_us() {
+  static const auto t0 = std::chrono::steady_clock::now();
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int batch_run(ngpu_engine *e, BatchJob &j) {
   Batcher &b = *e->batcher;
   std::unique_lock<std::mutex> lk(b.m);
@@ -248,6 +264,7 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
       continue;
     }
     b.leading = true;
+    const double t_lead = batch_trace_on() ? batch_now_us() : 0;
     // wait for the open packs to join: until all have, or kWindowUs has passed
     // and the last batch is off the device (while it runs, a new launch set
     // would only queue behind it -- better to let more packs join this one)
@@ -279,8 +296,14 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
         ++i;
       }
     }
+    const int open_now = e->open_packs.load();
     lk.unlock();
+    const double t_take = batch_trace_on() ? batch_now_us() : 0;
     const int rc = launch_batch(e, b, take);
+    if (batch_trace_on())
+      fprintf(stderr, "{\"batch_trace\": %llu, \"lead_us\": %.1f, \"take_us\": %.1f, \"enqueued_us\": %.1f, "
+              "\"layers\": %zu, \"open_packs\": %d, \"rc\": %d}\n", (unsigned long long)b.batches,
+              t_lead, t_take, batch_now_us(), take.size(), open_now, rc);
     if (rc && b.s) {  // part of it may be enqueued: let it drain before the packs free their buffers
       DeviceGuard dg(e->device);
       (void)hipStreamSynchronize(b.s);

@@ -72,6 +72,12 @@ for s in "$@"; do
       timeout -k 10 300 python3 bench.py --workload c1-sha256 --packs 32 --steps 5 --warmup 2 > "$OUT/packs_sha.json" 2> "$OUT/packs_sha.err"
       ok $? packs_sha
       tail -c 600 "$OUT/packs_c1.json" ;;
+    ptrace)
+      NGPU_BATCH_TRACE=1 timeout -k 10 300 python3 bench.py --workload c1 --packs 32 --steps 6 --warmup 2 --packs-modes decisions --no-cpu-baseline > "$OUT/ptrace_c1.json" 2> "$OUT/ptrace_c1.err"
+      ok $? ptrace_c1
+      NGPU_BATCH_TRACE=1 timeout -k 10 300 python3 bench.py --workload c1-sha256 --packs 32 --steps 3 --warmup 1 --packs-modes decisions --no-cpu-baseline > "$OUT/ptrace_sha.json" 2> "$OUT/ptrace_sha.err"
+      ok $? ptrace_sha
+      grep -c batch_trace "$OUT/ptrace_c1.err" ;;
     n2)
       NYDUS_NODE_EXTRA_DEVICES=0,0 timeout -k 10 600 python3 bench.py --gpus 2 --steps 10 --warmup 5 --dist-backend gloo --c4-layers 4 > "$OUT/bench_c2_n2_gloo.json" 2> "$OUT/bench_c2_n2_gloo.err"
       ok $? n2
