@@ -78,6 +78,12 @@ for s in "$@"; do
       NGPU_BATCH_TRACE=1 timeout -k 10 300 python3 bench.py --workload c1-sha256 --packs 32 --steps 3 --warmup 1 --packs-modes decisions --no-cpu-baseline > "$OUT/ptrace_sha.json" 2> "$OUT/ptrace_sha.err"
       ok $? ptrace_sha
       grep -c batch_trace "$OUT/ptrace_c1.err" ;;
+    papi)
+      for w in c1 c1-sha256; do
+        (cd /tmp && timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/papi_$w" -o t -- python3 "$ROOT/bench.py" --workload $w --packs 32 --steps 2 --warmup 1 --packs-modes decisions --no-cpu-baseline > "$OUT/papi_$w.json" 2> "$OUT/papi_$w.err")
+        ok $? "papi $w"
+      done
+      ls -R "$OUT/papi_c1" | head -20 ;;
     n2)
       NYDUS_NODE_EXTRA_DEVICES=0,0 timeout -k 10 600 python3 bench.py --gpus 2 --steps 10 --warmup 5 --dist-backend gloo --c4-layers 4 > "$OUT/bench_c2_n2_gloo.json" 2> "$OUT/bench_c2_n2_gloo.err"
       ok $? n2
