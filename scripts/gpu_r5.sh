@@ -84,6 +84,14 @@ for s in "$@"; do
         ok $? "papi $w"
       done
       ls -R "$OUT/papi_c1" | head -20 ;;
+    h2d)
+      for env in "NGPU_H2D=default" "HSA_ENABLE_SDMA=0"; do
+        for cfg in "4" "8" "16" "32" "32 shared"; do
+          env $env timeout -k 10 60 ./tools/h2d_streams $cfg 5 >> "$OUT/h2d.jsonl" 2>> "$OUT/h2d.err"
+          ok $? "h2d $env $cfg"
+        done
+      done
+      cat "$OUT/h2d.jsonl" ;;
     n2)
       NYDUS_NODE_EXTRA_DEVICES=0,0 timeout -k 10 600 python3 bench.py --gpus 2 --steps 10 --warmup 5 --dist-backend gloo --c4-layers 4 > "$OUT/bench_c2_n2_gloo.json" 2> "$OUT/bench_c2_n2_gloo.err"
       ok $? n2
