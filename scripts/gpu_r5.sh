@@ -86,7 +86,7 @@ for s in "$@"; do
       ls -R "$OUT/papi_c1" | head -20 ;;
     h2d)
       for env in "NGPU_H2D=default" "HSA_ENABLE_SDMA=0"; do
-        for cfg in "4" "16" "32" "32 pool4" "32 shared"; do
+        for cfg in "4" "16" "32" "32 4" "32 1"; do
           env $env timeout -k 10 60 ./tools/h2d_streams $cfg 20 >> "$OUT/h2d.jsonl" 2>> "$OUT/h2d.err"
           ok $? "h2d $env $cfg"
         done

@@ -4,9 +4,9 @@
 // stream) and its own pinned buffer, enqueue `pieces` 1 MiB hipMemcpyAsync
 // H2D copies, then synchronize.  Prints one JSON line per config: wall ms per
 // round, GB/s, and the longest / median host time inside hipMemcpyAsync.
-// usage: h2d_streams T ROUNDS [shared|pool4]   (shared: one stream, enqueues
-// under a mutex; pool4: four streams, thread i on stream i % 4, same mutex
-// per stream)
+// usage: h2d_streams T ROUNDS [S]   (S < T: S submitting threads, each with
+// one stream, enqueue the T buffers' copies between them -- buffer i on
+// thread i % S; default S = T)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -30,16 +30,12 @@
 int main(int argc, char **argv) {
   if (argc < 3) return 2;
   const int T = atoi(argv[1]), rounds = atoi(argv[2]);
-  const bool shared = argc > 3 && strcmp(argv[3], "shared") == 0;
-  const bool pool4 = argc > 3 && strcmp(argv[3], "pool4") == 0;
-  const int NS = shared ? 1 : pool4 ? 4 : T;
-  std::vector<std::mutex> smu(NS);
+  const int NS = argc > 3 ? std::max(1, std::min(T, atoi(argv[3]))) : T;
   const size_t piece = 1 << 20, pieces = 11, bytes = piece * pieces;
   std::vector<hipStream_t> st(T);
   std::vector<uint8_t *> h(T), d(T);
   for (int i = 0; i < T; ++i) {
     if (i < NS) CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
-    else st[i] = st[i % NS];
     CK(hipHostMalloc((void **)&h[i], bytes, hipHostMallocDefault));
     memset(h[i], i, bytes);
     CK(hipMalloc((void **)&d[i], bytes));
@@ -53,33 +49,18 @@ int main(int argc, char **argv) {
     std::atomic<int> go{0};
     std::vector<std::thread> th;
     std::vector<double> mine_all;
-    for (int i = 0; i < T; ++i)
-      th.emplace_back([&, i] {
+    for (int w = 0; w < NS; ++w)
+      th.emplace_back([&, w] {
         while (!go.load()) {
         }
         std::vector<double> mine;
-        for (size_t p = 0; p < pieces; ++p) {
-          const auto a = clk::now();
-          if (NS < T) {
-            std::lock_guard<std::mutex> g(smu[i % NS]);
-            CK(hipMemcpyAsync(d[i] + p * piece, h[i] + p * piece, piece, hipMemcpyHostToDevice, st[i]));
-          } else {
-            CK(hipMemcpyAsync(d[i] + p * piece, h[i] + p * piece, piece, hipMemcpyHostToDevice, st[i]));
+        for (size_t p = 0; p < pieces; ++p)
+          for (int i = w; i < T; i += NS) {
+            const auto a = clk::now();
+            CK(hipMemcpyAsync(d[i] + p * piece, h[i] + p * piece, piece, hipMemcpyHostToDevice, st[w]));
+            mine.push_back(std::chrono::duration<double, std::micro>(clk::now() - a).count());
           }
-          mine.push_back(std::chrono::duration<double, std::micro>(clk::now() - a).count());
-        }
-        if (NS < T) {
-          hipEvent_t ev;  // this thread's copies are done when an event after them is
-          {
-            std::lock_guard<std::mutex> g(smu[i % NS]);
-            CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            CK(hipEventRecord(ev, st[i]));
-          }
-          CK(hipEventSynchronize(ev));
-          CK(hipEventDestroy(ev));
-        } else {
-          CK(hipStreamSynchronize(st[i]));
-        }
+        CK(hipStreamSynchronize(st[w]));
         std::lock_guard<std::mutex> g(m);
         if (r) call_us.insert(call_us.end(), mine.begin(), mine.end());
       });
