@@ -399,7 +399,6 @@ void engine_unref(ngpu_engine *e) {
   for (auto &b : e->pack_pool) {
     if (b.d_res) (void)hipFree(b.d_res);
     if (b.d_all) (void)hipFree(b.d_all);
-    if (b.copy) (void)hipStreamDestroy(b.copy);
     if (b.fence) (void)hipEventDestroy(b.fence);
     if (b.h_stats) (void)hipHostFree(b.h_stats);
     if (b.h_io) (void)hipHostFree(b.h_io);

@@ -32,13 +32,13 @@ struct ngpu_staging_buf {
 // staging-sized window each time).
 struct BlobWindows {
   uint8_t *dwin[2] = {}, *ddesc[2] = {}, *hdesc[2] = {};
-  hipEvent_t ev[2] = {};
+  hipEvent_t ev[2] = {};        // the window's bytes landed (D2H done)
+  hipEvent_t gathered[2] = {};  // the window's gather kernel done (its D2H may start)
   uint64_t cap = 0, kcap = 0;  // window bytes, descriptors per window
 };
 void blob_windows_free(BlobWindows &w);  // (pack.hip)
 
 struct ngpu_pack_bufs {
-  hipStream_t copy = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t fence = nullptr;  // the pack's host_fence marker
   uint64_t *h_stats = nullptr;  // pinned, 32 words: the pack's stats read back
@@ -142,6 +142,16 @@ struct ngpu_engine {
   std::atomic<int> refs{1};  // the creator + every open pack
   ngpu::Batcher *batcher = nullptr;  // concurrent small Packs' launch sets (batch.hip)
   hipMemPool_t seg_pool = nullptr;   // retained Pack segments (stream-ordered, own pool)
+  // The packs' bulk copies go through a few shared engine streams, each
+  // enqueued under its mutex: staging H2D on h2d[k], blob-window D2H on
+  // d2h[k], pack k-th opened on lane k % kCopyLanes.  Measured on MI355X
+  // (tools/h2d_streams, profiles/r5/h2d_streams_r5k4.jsonl): 32 streams
+  // copying at once stall hipMemcpyAsync on the host for up to 46 ms and
+  // carry 27 GB/s; 2 streams carry 45 GB/s with no call over 0.1 ms.
+  static constexpr int kCopyLanes = 2;
+  hipStream_t h2d[kCopyLanes] = {}, d2h[kCopyLanes] = {};
+  std::mutex h2d_mu[kCopyLanes], d2h_mu[kCopyLanes];
+  uint32_t copy_rr = 0;  // next pack's lane (e->mu)
   std::atomic<int> open_packs{0};    // packs opened and not yet ended
   uint64_t uid = 0;          // unique for the process's lifetime (node exchange channels)
   ngpu_config cfg{};

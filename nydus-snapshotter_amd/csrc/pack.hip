@@ -191,7 +191,10 @@ struct ngpu_pack : TarSink {
   uint64_t res_cap = 0;
   ngpu_chunk *d_all = nullptr;
   uint64_t all_cap = 0;
-  hipStream_t copy = nullptr;
+  hipStream_t copy = nullptr;    // shared H2D lane (engine h2d[k]), enqueued under *copy_mu
+  std::mutex *copy_mu = nullptr;
+  hipStream_t d2h = nullptr;     // shared D2H lane (engine d2h[k]), enqueued under *d2h_mu
+  std::mutex *d2h_mu = nullptr;
   hipStream_t stream = nullptr;  // compute: digest, dedup, gather (lives as long as the engine)
   hipEvent_t fence = nullptr;    // host_fence marker of this pack
   uint64_t *h_stats = nullptr;   // pinned: its stats, read after the engine lock is let go
@@ -251,7 +254,15 @@ void release(ngpu_pack *p) {
   for (Slot &s : p->slot) {
     if (s.done) (void)hipEventSynchronize(s.done);
   }
-  if (p->copy) (void)hipStreamSynchronize(p->copy);
+  if (p->copy) {  // this pack's copies on its shared lane: everything enqueued before this marker
+    hipEvent_t m = p->slot[0].copied;
+    bool marked = false;
+    if (m) {
+      std::lock_guard<std::mutex> g(*p->copy_mu);
+      marked = hipEventRecord(m, p->copy) == hipSuccess;
+    }
+    (void)(marked ? hipEventSynchronize(m) : hipStreamSynchronize(p->copy));
+  }
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   ptrace(p, "release_synced");
   {
@@ -314,11 +325,10 @@ void release(ngpu_pack *p) {
     // engine does.  The pool holds as many as packs were ever open at once.
     std::lock_guard<std::mutex> g(p->e->pool_mu);
     if (p->stream) {
-      p->e->pack_pool.push_back({p->copy, p->stream, p->fence, p->h_stats, p->h_io, p->io_cap,
+      p->e->pack_pool.push_back({p->stream, p->fence, p->h_stats, p->h_io, p->io_cap,
                                  p->d_res, p->res_cap, p->d_all, p->all_cap, p->win});
       p->win = BlobWindows{};
       p->h_io = nullptr;
-      p->copy = nullptr;
       p->stream = nullptr;
       p->fence = nullptr;
       p->h_stats = nullptr;
@@ -328,7 +338,6 @@ void release(ngpu_pack *p) {
   }
   if (p->d_res) (void)hipFree(p->d_res);
   if (p->d_all) (void)hipFree(p->d_all);
-  if (p->copy) (void)hipStreamDestroy(p->copy);
   if (p->fence) (void)hipEventDestroy(p->fence);
   if (p->h_stats) (void)hipHostFree(p->h_stats);
   if (p->h_io) (void)hipHostFree(p->h_io);
@@ -392,40 +401,43 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b, bool digest = true,
   int rc = grow_results(p, b);
   if (rc) return rc;
   uint8_t *dev = s.d;
-  if (p->retain) {  // this slot's bytes get their own resident segment
-    Seg g;
-    const uint64_t need = (s.fill + 255) & ~255ull;
-    if (p->arenas.empty() || p->arenas.back().cap - p->arenas.back().used < need) {
-      // stream-ordered (the device pool, engine.hip): freed without a device-wide wait
-      uint64_t cap = p->arenas.empty() ? p->cap : std::min<uint64_t>(2 * p->arenas.back().cap, 1ull << 30);
-      if (cap < need) cap = need;
-      ngpu_pack::Arena ar;
-      if (e->seg_pool)
-        HIP_TRY(e, hipMallocFromPoolAsync((void **)&ar.d, cap, e->seg_pool, p->copy));
-      else
-        HIP_TRY(e, hipMallocAsync((void **)&ar.d, cap, p->copy));
-      ar.cap = cap;
-      p->arenas.push_back(ar);
+  {  // the copies go out on the pack's shared H2D lane
+    std::lock_guard<std::mutex> cg(*p->copy_mu);
+    if (p->retain) {  // this slot's bytes get their own resident segment
+      Seg g;
+      const uint64_t need = (s.fill + 255) & ~255ull;
+      if (p->arenas.empty() || p->arenas.back().cap - p->arenas.back().used < need) {
+        // stream-ordered (the device pool, engine.hip): freed without a device-wide wait
+        uint64_t cap = p->arenas.empty() ? p->cap : std::min<uint64_t>(2 * p->arenas.back().cap, 1ull << 30);
+        if (cap < need) cap = need;
+        ngpu_pack::Arena ar;
+        if (e->seg_pool)
+          HIP_TRY(e, hipMallocFromPoolAsync((void **)&ar.d, cap, e->seg_pool, p->copy));
+        else
+          HIP_TRY(e, hipMallocAsync((void **)&ar.d, cap, p->copy));
+        ar.cap = cap;
+        p->arenas.push_back(ar);
+      }
+      ngpu_pack::Arena &ar = p->arenas.back();
+      g.d = ar.d + ar.used;
+      ar.used += need;
+      g.base = s.base;
+      g.a = a;
+      g.b = b;
+      p->segs.push_back(g);
+      dev = g.d;
     }
-    ngpu_pack::Arena &ar = p->arenas.back();
-    g.d = ar.d + ar.used;
-    ar.used += need;
-    g.base = s.base;
-    g.a = a;
-    g.b = b;
-    p->segs.push_back(g);
-    dev = g.d;
+    // bytes [0, sent) went H2D as they were committed (eager_copy); the copy
+    // stream is in order, so s.copied covers them too
+    const uint64_t from = p->retain ? 0 : s.sent;
+    if (s.fill > from)
+      HIP_TRY(e, hipMemcpyAsync(dev + from, s.h + from, s.fill - from, hipMemcpyHostToDevice, p->copy));
+    s.sent = s.fill;
+    HIP_TRY(e, hipMemcpyAsync(s.d_ch, s.h_ch, nch * sizeof(ngpu_chunk), hipMemcpyHostToDevice,
+                              p->copy));
+    HIP_TRY(e, hipEventRecord(s.copied, p->copy));
+    HIP_TRY(e, hipStreamWaitEvent(p->stream, s.copied, 0));  // (later copies of the lane are not waited for)
   }
-  // bytes [0, sent) went H2D as they were committed (eager_copy); the copy
-  // stream is in order, so s.copied covers them too
-  const uint64_t from = p->retain ? 0 : s.sent;
-  if (s.fill > from)
-    HIP_TRY(e, hipMemcpyAsync(dev + from, s.h + from, s.fill - from, hipMemcpyHostToDevice, p->copy));
-  s.sent = s.fill;
-  HIP_TRY(e, hipMemcpyAsync(s.d_ch, s.h_ch, nch * sizeof(ngpu_chunk), hipMemcpyHostToDevice,
-                            p->copy));
-  HIP_TRY(e, hipEventRecord(s.copied, p->copy));
-  HIP_TRY(e, hipStreamWaitEvent(p->stream, s.copied, 0));
   if (p->em && !p->gz) {  // the prefix dedups read lengths from the layer's device chunk table
     if ((rc = grow_all(p, b + 1))) return rc;
     HIP_TRY(e, hipMemcpyAsync(p->d_all + a, s.d_ch, nch * sizeof(ngpu_chunk),
@@ -504,6 +516,7 @@ uint64_t eager_granule() {
 int eager_copy(ngpu_pack *p, Slot &s) {
   if (p->retain || s.fill - s.sent < eager_granule()) return 0;
   DeviceGuard dg(p->e->device);
+  std::lock_guard<std::mutex> g(*p->copy_mu);
   HIP_TRY(p->e, hipMemcpyAsync(s.d + s.sent, s.h + s.sent, s.fill - s.sent, hipMemcpyHostToDevice,
                                p->copy));
   s.sent = s.fill;
@@ -580,15 +593,18 @@ int emit_range(ngpu_pack *p, BlobWriter &bw, const ngpu_chunk *ch, const uint64_
   uint64_t kneed = 4096;
   while (kneed < k && kneed < maxk) kneed *= 2;
   BlobWindows &bw_ = p->win;
-  if (nw && (bw_.cap < cap || bw_.kcap < kneed || !bw_.ev[0])) {
+  if (nw && (bw_.cap < cap || bw_.kcap < kneed || !bw_.ev[0] || !bw_.gathered[0])) {
     (void)hipStreamSynchronize(p->stream);  // a previous range's windows may still be read
+    for (int b = 0; b < 2; ++b)
+      if (bw_.ev[b]) (void)hipEventSynchronize(bw_.ev[b]);
     blob_windows_free(bw_);
     bool ok = true;
     for (int i = 0; i < 2 && ok; ++i)
       ok = hipMalloc((void **)&bw_.dwin[i], cap) == hipSuccess &&
            hipMalloc((void **)&bw_.ddesc[i], kneed * 20) == hipSuccess &&
            hipHostMalloc((void **)&bw_.hdesc[i], kneed * 20, hipHostMallocDefault) == hipSuccess &&
-           hipEventCreateWithFlags(&bw_.ev[i], hipEventDisableTiming) == hipSuccess;
+           hipEventCreateWithFlags(&bw_.ev[i], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&bw_.gathered[i], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
       (void)hipGetLastError();
       blob_windows_free(bw_);
@@ -598,30 +614,32 @@ int emit_range(ngpu_pack *p, BlobWriter &bw, const ngpu_chunk *ch, const uint64_
     bw_.kcap = kneed;
   }
   uint8_t *const *dwin = bw_.dwin, *const *ddesc = bw_.ddesc, *const *hdesc = bw_.hdesc;
-  const hipEvent_t *ev = bw_.ev;
-  const uint64_t kc = bw_.kcap;  // descriptor slots per window buffer
+  const hipEvent_t *ev = bw_.ev, *gathered = bw_.gathered;
   auto enqueue = [&](uint64_t wi) -> int {
     const int b = wi & 1;
     const uint64_t a = wstart[wi], c = wstart[wi + 1] - a;
+    // one descriptor block per window: c sources, c offsets, c lengths
     uint64_t *hs = (uint64_t *)hdesc[b];
-    uint64_t *ho = hs + kc;
-    uint32_t *hl = (uint32_t *)(ho + kc);
+    uint64_t *ho = hs + c;
+    uint32_t *hl = (uint32_t *)(ho + c);
     memcpy(hs, &src[a], c * 8);
     for (uint64_t i = 0; i < c; ++i) ho[i] = doff[a + i];
     memcpy(hl, &len[a], c * 4);
     uint64_t *ds = (uint64_t *)ddesc[b];
     hipStream_t ps = p->stream;
-    HIP_TRY(e, hipMemcpyAsync(ds, hs, c * 8, hipMemcpyHostToDevice, ps));
-    HIP_TRY(e, hipMemcpyAsync(ds + kc, ho, c * 8, hipMemcpyHostToDevice, ps));
-    HIP_TRY(e, hipMemcpyAsync(ds + 2 * kc, hl, c * 4, hipMemcpyHostToDevice, ps));
+    HIP_TRY(e, hipMemcpyAsync(ds, hs, c * 20, hipMemcpyHostToDevice, ps));
     const unsigned grid = (unsigned)(c < 2048 ? c : 2048);
-    hipLaunchKernelGGL(gather_chunks, dim3(grid), dim3(256), 0, ps, ds, (uint32_t *)(ds + 2 * kc),
-                       ds + kc, c, dwin[b]);
+    hipLaunchKernelGGL(gather_chunks, dim3(grid), dim3(256), 0, ps, ds, (uint32_t *)(ds + 2 * c),
+                       ds + c, c, dwin[b]);
     HIP_TRY(e, hipGetLastError());
     const uint64_t bytes = doff[a + c - 1] + len[a + c - 1];
     if (int rc = host_fence(e, ps, p->fence)) return rc;
-    HIP_TRY(e, hipMemcpyAsync(land[b], dwin[b], bytes, hipMemcpyDeviceToHost, ps));
-    HIP_TRY(e, hipEventRecord(ev[b], ps));
+    HIP_TRY(e, hipEventRecord(gathered[b], ps));
+    // the window's bytes come back on the pack's shared D2H lane
+    std::lock_guard<std::mutex> g(*p->d2h_mu);
+    HIP_TRY(e, hipStreamWaitEvent(p->d2h, gathered[b], 0));
+    HIP_TRY(e, hipMemcpyAsync(land[b], dwin[b], bytes, hipMemcpyDeviceToHost, p->d2h));
+    HIP_TRY(e, hipEventRecord(ev[b], p->d2h));
     return 0;
   };
   int rc = 0;
@@ -645,7 +663,10 @@ int emit_range(ngpu_pack *p, BlobWriter &bw, const ngpu_chunk *ch, const uint64_
   }
   // every window was waited for on success; after an error the next one may
   // still be in flight
-  if (rc) (void)hipStreamSynchronize(p->stream);
+  if (rc) {
+    (void)hipStreamSynchronize(p->stream);
+    for (int b = 0; b < 2; ++b) (void)hipEventSynchronize(ev[b]);
+  }
   return rc;
 }
 
@@ -848,6 +869,7 @@ void blob_windows_free(BlobWindows &w) {
     if (w.ddesc[i]) (void)hipFree(w.ddesc[i]);
     if (w.hdesc[i]) (void)hipHostFree(w.hdesc[i]);
     if (w.ev[i]) (void)hipEventDestroy(w.ev[i]);
+    if (w.gathered[i]) (void)hipEventDestroy(w.gathered[i]);
   }
   w = BlobWindows{};
 }
@@ -893,7 +915,6 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
     if (!e->pack_pool.empty()) {
       const ngpu_pack_bufs b = e->pack_pool.back();
       e->pack_pool.pop_back();
-      p->copy = b.copy;
       p->stream = b.stream;
       p->fence = b.fence;
       p->h_stats = b.h_stats;
@@ -922,7 +943,21 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
       }
     }
   }
-  if (!p->copy) ok = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking) == hipSuccess;
+  {  // the pack's shared copy lanes (created with the engine's first pack)
+    const uint32_t k = e->copy_rr++ % ngpu_engine::kCopyLanes;
+    if (!e->h2d[k]) {
+      ok = hipStreamCreateWithFlags(&e->h2d[k], hipStreamNonBlocking) == hipSuccess;
+      if (ok) e->streams.push_back(e->h2d[k]);  // destroyed with the engine
+    }
+    if (ok && !e->d2h[k]) {
+      ok = hipStreamCreateWithFlags(&e->d2h[k], hipStreamNonBlocking) == hipSuccess;
+      if (ok) e->streams.push_back(e->d2h[k]);
+    }
+    p->copy = e->h2d[k];
+    p->copy_mu = &e->h2d_mu[k];
+    p->d2h = e->d2h[k];
+    p->d2h_mu = &e->d2h_mu[k];
+  }
   if (ok && !p->fence) ok = hipEventCreateWithFlags(&p->fence, hipEventDisableTiming) == hipSuccess;
   if (ok && !p->h_stats)
     ok = hipHostMalloc((void **)&p->h_stats, 32 * sizeof(uint64_t), hipHostMallocDefault) ==
