@@ -19,9 +19,13 @@
 //
 // Window: the first pack to close leads; it waits until every pack open on
 // the engine has joined, or kWindowUs, whichever comes first (a lone pack
-// goes at once).  Only packs whose layer fit one staging slot join (their
-// bytes are all in HBM at close); packs with another chunk dict than the
-// leader's wait for the next batch.  NGPU_FLAG_NO_BATCH turns it off.
+// goes at once), and until one of the kLanes batch lanes is idle.  Batches on
+// different lanes run concurrently (each lane: its own stream, buffers and
+// workspace slot), so a small batch's chain latency -- a SHA-256 batch holds
+// the device ~21 ms whatever its size -- does not hold the next one back.
+// Only packs whose layer fit one staging slot join (their bytes are all in
+// HBM at close); packs with another chunk dict than the leader's wait for
+// the next batch.  NGPU_FLAG_NO_BATCH turns it off.
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -43,13 +47,10 @@ struct BatchEvent {
   }
 };
 
-struct Batcher {
-  std::mutex m;
-  std::condition_variable cv;
-  std::vector<BatchJob *> open;  // packs waiting for a batch
-  bool leading = false;
-  // the leader's buffers (used under e->mu, reused batch after batch: every
-  // batch runs on stream s, so the next one's copies follow the last kernels)
+// One batch lane: a stream and the buffers of the batch running on it
+// (reused batch after batch: a lane takes a new batch only when its last one
+// has ended).
+struct BatchLane {
   hipStream_t s = nullptr;
   uint8_t *d_data = nullptr;
   uint64_t data_cap = 0;
@@ -63,9 +64,17 @@ struct Batcher {
   uint64_t l_cap = 0;
   uint8_t *h_tab = nullptr;  // pinned: chunk table + layer boundaries of one batch
   uint64_t h_cap = 0;
-  hipEvent_t tab_sent = nullptr;  // the last batch's table upload
-  bool tab_pending = false;
-  std::shared_ptr<BatchEvent> last;  // the end of the last batch enqueued
+  std::shared_ptr<BatchEvent> last;  // the end of its last batch
+};
+
+constexpr int kLanes = 4;  // = GPU_MAX_HW_QUEUES: more lanes would share hardware queues
+
+struct Batcher {
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<BatchJob *> open;  // packs waiting for a batch
+  bool leading = false;
+  BatchLane lane[kLanes];
   uint64_t batches = 0, jobs = 0, max_jobs = 0;
 };
 
@@ -112,12 +121,8 @@ constexpr uint64_t kMaxBytes = 1ull << 30;
 constexpr uint64_t kMaxChunks = 1ull << 20;
 
 template <class T>
-int grow_dev(ngpu_engine *e, Batcher &b, T **p, uint64_t &cap, uint64_t want, bool *synced) {
-  if (want <= cap && *p) return 0;
-  if (!*synced) {  // the last batch may still read it
-    HIP_TRY(e, hipStreamSynchronize(b.s));
-    *synced = true;
-  }
+int grow_dev(ngpu_engine *e, T **p, uint64_t &cap, uint64_t want) {
+  if (want <= cap && *p) return 0;  // (the lane is idle: its last batch has ended)
   if (*p) (void)hipFree(*p), *p = nullptr, cap = 0;
   uint64_t c = 4096;
   while (c < want) c *= 2;
@@ -129,13 +134,22 @@ int grow_dev(ngpu_engine *e, Batcher &b, T **p, uint64_t &cap, uint64_t want, bo
   return 0;
 }
 
-// Enqueue one batch (the leader, e->mu taken here).
-int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs) {
+// A lane whose last batch has ended (or that never ran one), or -1.
+int idle_lane(ngpu_engine *e, Batcher &b) {
+  for (int k = 0; k < kLanes; ++k) {
+    if (!b.lane[k].last) return k;
+    DeviceGuard dg(e->device);
+    if (hipEventQuery(b.lane[k].last->ev) != hipErrorNotReady) return k;
+  }
+  return -1;
+}
+
+// Enqueue one batch on an idle lane (the leader, e->mu taken here).
+int launch_batch(ngpu_engine *e, Batcher &bt, BatchLane &b, const std::vector<BatchJob *> &jobs) {
   std::lock_guard<std::mutex> g(e->mu);
   DeviceGuard dg(e->device);
   if (!b.s) {
     HIP_TRY(e, hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking));
-    HIP_TRY(e, hipEventCreateWithFlags(&b.tab_sent, hipEventDisableTiming));
     e->streams.push_back(b.s);  // lives as long as the engine (ws_lazy_end)
   }
   const uint64_t K = jobs.size();
@@ -147,25 +161,21 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
     first[k + 1] = first[k] + jobs[k]->n;
   }
   const uint64_t N = first[K];
-  bool synced = false;
-  if (int rc = grow_dev(e, b, &b.d_data, b.data_cap, bytes + 64, &synced)) return rc;
-  if (int rc = grow_dev(e, b, &b.d_ch, b.ch_cap, N + 1, &synced)) return rc;
-  uint64_t rcap = b.ch_cap == 0 ? 0 : b.ch_cap;  // results sized with the chunk table
-  if (!b.d_res || synced) {
+  if (int rc = grow_dev(e, &b.d_data, b.data_cap, bytes + 64)) return rc;
+  const uint64_t ch_cap0 = b.ch_cap;
+  if (int rc = grow_dev(e, &b.d_ch, b.ch_cap, N + 1)) return rc;
+  if (!b.d_res || b.ch_cap != ch_cap0) {  // results sized with the chunk table
     if (b.d_res) (void)hipFree(b.d_res), b.d_res = nullptr;
-    HIP_TRY(e, hipMalloc((void **)&b.d_res, rcap * sizeof(ngpu_result)));
+    HIP_TRY(e, hipMalloc((void **)&b.d_res, b.ch_cap * sizeof(ngpu_result)));
   }
-  if (int rc = grow_dev(e, b, &b.d_lfirst, b.l_cap, K + 2, &synced)) return rc;
-  if (!b.d_lst || synced) {
+  const uint64_t l_cap0 = b.l_cap;
+  if (int rc = grow_dev(e, &b.d_lfirst, b.l_cap, K + 2)) return rc;
+  if (!b.d_lst || b.l_cap != l_cap0) {
     if (b.d_lst) (void)hipFree(b.d_lst), b.d_lst = nullptr;
     HIP_TRY(e, hipMalloc((void **)&b.d_lst, b.l_cap * sizeof(ngpu_layer_stats)));
   }
-  if (int rc = grow_dev(e, b, &b.d_dst, b.dst_cap, 2 * K + 2, &synced)) return rc;
+  if (int rc = grow_dev(e, &b.d_dst, b.dst_cap, 2 * K + 2)) return rc;
   const uint64_t tab = N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t) + 2 * K * sizeof(void *);
-  if (b.tab_pending) {  // the pinned table may still be on its way to the last batch
-    HIP_TRY(e, hipEventSynchronize(b.tab_sent));
-    b.tab_pending = false;
-  }
   if (tab > b.h_cap) {
     if (b.h_tab) (void)hipHostFree(b.h_tab), b.h_tab = nullptr, b.h_cap = 0;
     uint64_t c = 64 << 10;
@@ -198,8 +208,18 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
   HIP_TRY(e, hipMemcpyAsync(b.d_lfirst, b.h_tab + N * sizeof(ngpu_chunk), (K + 1) * sizeof(uint64_t),
                             hipMemcpyHostToDevice, b.s));
   HIP_TRY(e, hipMemcpyAsync(b.d_dst, hd, 2 * K * sizeof(void *), hipMemcpyHostToDevice, b.s));
-  HIP_TRY(e, hipEventRecord(b.tab_sent, b.s));
-  b.tab_pending = true;
+  // the lane's workspace sized with headroom (powers of two), so batches of
+  // varying size do not regrow it -- a regrow waits for the slot's last stage
+  {
+    use_slot(e, b.s);
+    const uint64_t n2 = next_pow2(N + 1), len2 = next_pow2(bytes + 1);
+    if (int rc = ensure_workspace(e, n2, len2, pick_group_log2(e, bytes), dict_blobs(jobs[0]->dict),
+                                  next_pow2(K)))
+      return rc;
+    // the slot is this lane's now (the digest below finds it by its stream)
+    if (int rc = ws_acquire(e, b.s)) return rc;
+    if (int rc = ws_release(e, b.s, nullptr, true)) return rc;
+  }
   // ONE digest stage over all layers, ONE multi-layer dedup stage
   if (int rc = enqueue_digest(e, b.d_data, bytes, b.d_ch, N, b.d_res, b.s, true)) return rc;
   if (int rc = enqueue_dedup(e, jobs[0]->dict, b.d_ch, N, b.d_res, nullptr, 0, b.s, b.d_lfirst, K,
@@ -229,9 +249,9 @@ int launch_batch(ngpu_engine *e, Batcher &b, const std::vector<BatchJob *> &jobs
     j->batch_layers = (uint32_t)K;
   }
   b.last = done;
-  ++b.batches;
-  b.jobs += K;
-  b.max_jobs = std::max<uint64_t>(b.max_jobs, K);
+  ++bt.batches;
+  bt.jobs += K;
+  bt.max_jobs = std::max<uint64_t>(bt.max_jobs, K);
   return 0;
 }
 
@@ -265,20 +285,17 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     }
     b.leading = true;
     const double t_lead = batch_trace_on() ? batch_now_us() : 0;
-    // wait for the open packs to join: until all have, or kWindowUs has passed
-    // and the last batch is off the device (while it runs, a new launch set
-    // would only queue behind it -- better to let more packs join this one)
+    // wait for the open packs to join -- until all have, or kWindowUs has
+    // passed -- and for an idle lane (while every lane runs a batch, a new
+    // one would only queue behind them: better to let more packs join it)
     const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(kWindowUs);
+    int ln = -1;
     for (;;) {
-      if (b.open.size() >= (size_t)e->open_packs.load() || b.open.size() >= kMaxJobs) break;
+      ln = idle_lane(e, b);
+      const bool all_in = b.open.size() >= (size_t)e->open_packs.load() || b.open.size() >= kMaxJobs;
       const auto now = std::chrono::steady_clock::now();
-      bool prev_running = false;
-      if (b.last) {
-        DeviceGuard dg(e->device);
-        prev_running = hipEventQuery(b.last->ev) == hipErrorNotReady;
-      }
-      if (!prev_running && now >= until) break;
-      b.cv.wait_until(lk, prev_running ? now + std::chrono::microseconds(kPollUs) : until);
+      if (ln >= 0 && (all_in || now >= until)) break;
+      b.cv.wait_until(lk, ln >= 0 ? until : now + std::chrono::microseconds(kPollUs));
     }
     // this leader's batch: the open packs sharing its dict, within the caps
     std::vector<BatchJob *> take;
@@ -299,14 +316,14 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     const int open_now = e->open_packs.load();
     lk.unlock();
     const double t_take = batch_trace_on() ? batch_now_us() : 0;
-    const int rc = launch_batch(e, b, take);
+    const int rc = launch_batch(e, b, b.lane[ln], take);
     if (batch_trace_on())
-      fprintf(stderr, "{\"batch_trace\": %llu, \"lead_us\": %.1f, \"take_us\": %.1f, \"enqueued_us\": %.1f, "
-              "\"layers\": %zu, \"open_packs\": %d, \"rc\": %d}\n", (unsigned long long)b.batches,
-              t_lead, t_take, batch_now_us(), take.size(), open_now, rc);
-    if (rc && b.s) {  // part of it may be enqueued: let it drain before the packs free their buffers
+      fprintf(stderr, "{\"batch_trace\": %llu, \"lane\": %d, \"lead_us\": %.1f, \"take_us\": %.1f, "
+              "\"enqueued_us\": %.1f, \"layers\": %zu, \"open_packs\": %d, \"rc\": %d}\n",
+              (unsigned long long)b.batches, ln, t_lead, t_take, batch_now_us(), take.size(), open_now, rc);
+    if (rc && b.lane[ln].s) {  // part of it may be enqueued: let it drain before the packs free their buffers
       DeviceGuard dg(e->device);
-      (void)hipStreamSynchronize(b.s);
+      (void)hipStreamSynchronize(b.lane[ln].s);
     }
     lk.lock();
     for (BatchJob *x : take) {
@@ -336,13 +353,15 @@ void batcher_free(ngpu_engine *e) {
   Batcher *b = e->batcher;
   if (!b) return;
   DeviceGuard dg(e->device);
-  if (b->s) (void)hipStreamSynchronize(b->s);
-  for (void *p : {(void *)b->d_data, (void *)b->d_ch, (void *)b->d_res, (void *)b->d_lfirst,
-                  (void *)b->d_lst, (void *)b->d_dst})
-    if (p) (void)hipFree(p);
-  if (b->h_tab) (void)hipHostFree(b->h_tab);
-  if (b->tab_sent) (void)hipEventDestroy(b->tab_sent);
-  // b->s is one of e->streams: destroyed with them
+  for (BatchLane &l : b->lane) {
+    if (l.s) (void)hipStreamSynchronize(l.s);
+    for (void *p : {(void *)l.d_data, (void *)l.d_ch, (void *)l.d_res, (void *)l.d_lfirst,
+                    (void *)l.d_lst, (void *)l.d_dst})
+      if (p) (void)hipFree(p);
+    if (l.h_tab) (void)hipHostFree(l.h_tab);
+    l.last.reset();
+    // l.s is one of e->streams: destroyed with them
+  }
   delete b;
   e->batcher = nullptr;
 }

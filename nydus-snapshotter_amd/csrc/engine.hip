@@ -525,8 +525,9 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   e->uid = next_uid.fetch_add(1, std::memory_order_relaxed);
   e->cfg = c;
   // NGPU_WS_SLOTS: workspace slots = calls on distinct streams that may run
-  // at once (default 4, the hardware queues HIP gives a process)
-  int nslots = 4;
+  // at once (default 8: the batcher's 4 lanes keep theirs while other calls
+  // and unbatched packs take the rest; a slot allocates on first use)
+  int nslots = 8;
   if (const char *v = getenv("NGPU_WS_SLOTS")) {
     const long x = strtol(v, nullptr, 10);
     if (x >= 1 && x <= 64) nslots = (int)x;

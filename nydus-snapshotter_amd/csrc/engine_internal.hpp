@@ -100,7 +100,7 @@ struct ngpu_dict {
 // recorded yet, only while `last` is a stream that lives as long as the
 // engine); a stage on another stream waits for it first, so calls on
 // different streams never run over one workspace concurrently.  An engine
-// keeps several (NGPU_WS_SLOTS, default 4): a call on a stream keeps the slot
+// keeps several (NGPU_WS_SLOTS, default 8): a call on a stream keeps the slot
 // its stream used last (stream order is the ordering), a call on another
 // stream takes an idle slot, so independent layers on different streams --
 // containerd converting an image's layers concurrently -- run side by side
@@ -195,7 +195,7 @@ struct ngpu_engine {
   std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu, <= kStagingPool
   // 32 packs open at once keep their two slots; the pinned bytes kept are
   // bounded too (64 default 256 MiB slots would pin 16 GiB)
-  static constexpr size_t kStagingPool = 64;
+  static constexpr size_t kStagingPool = 256;
   static constexpr uint64_t kStagingPoolBytes = 8ull << 30;
   uint64_t staging_pool_bytes = 0;  // guarded by pool_mu
   std::vector<ngpu_pack_bufs> pack_pool;        // guarded by pool_mu

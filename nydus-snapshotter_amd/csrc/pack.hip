@@ -203,6 +203,7 @@ struct ngpu_pack : TarSink {
   BlobWindows win;           // blob stream gather windows (kept by the engine's pack_pool)
   CopyPool *pool = nullptr;  // created on the first large write
   bool retain = false;       // NGPU_PACK_RETAIN: device segments kept to the end
+  bool ws_sized = false;     // its stream's workspace sized for a whole slot (first digest)
   std::vector<Seg> segs;
   // NGPU_PACK_RETAIN: the segments are carved out of arenas that double in
   // size (1 slot, 2, 4, ... up to 1 GiB): a 2 GiB layer frees 6 arenas at the end
@@ -388,6 +389,20 @@ int grow_all(ngpu_pack *p, uint64_t want) {
 // Copy the slot to HBM and digest chunks [a, b) (all inside the slot).
 // digest == false: the copies only (a batched close digests the slot's bytes
 // in its launch set, batch.hip); *dev_out = where the bytes land.
+// Take a workspace slot for the pack's stream and size it once for a whole
+// staging slot, so no later dispatch of the pack reallocates it (e->mu held).
+int size_workspace(ngpu_pack *p) {
+  if (p->ws_sized) return 0;
+  ngpu_engine *e = p->e;
+  use_slot(e, p->stream);
+  if (int rc = ensure_workspace(e, p->max_ch, p->cap, pick_group_log2(e, p->cap), dict_blobs(p->dict), 1))
+    return rc;
+  if (int rc = ws_acquire(e, p->stream)) return rc;
+  if (int rc = ws_release(e, p->stream, nullptr, true)) return rc;
+  p->ws_sized = true;
+  return 0;
+}
+
 int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b, bool digest = true,
              uint8_t **dev_out = nullptr) {
   if (b == a) return 0;
@@ -400,6 +415,7 @@ int dispatch(ngpu_pack *p, Slot &s, uint64_t a, uint64_t b, bool digest = true,
   }
   int rc = grow_results(p, b);
   if (rc) return rc;
+  if (digest && (rc = size_workspace(p))) return rc;
   uint8_t *dev = s.d;
   {  // the copies go out on the pack's shared H2D lane
     std::lock_guard<std::mutex> cg(*p->copy_mu);
@@ -979,13 +995,10 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
          hipEventCreateWithFlags(&s.copied, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
   }
-  // take a workspace slot for the pack's stream and size it once, so no
-  // staging-slot dispatch reallocates it
-  if (ok) {
-    use_slot(e, p->stream);
-    ok = ensure_workspace(e, p->max_ch, cap, pick_group_log2(e, cap), dict_blobs(dict), 1) == 0 &&
-         ws_acquire(e, p->stream) == 0 && ws_release(e, p->stream, nullptr, true) == 0;
-  }
+  // (the pack's workspace is sized at its first digest on its own stream,
+  // size_workspace: a pack whose close joins a batch never takes one -- at
+  // open, the GPU-side wait on the slot's last stage tied the pack's events
+  // to an unrelated running batch)
   if (!ok) {
     (void)hipGetLastError();
     release(p);
@@ -1247,6 +1260,7 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
       if (batched) {
         // the rest runs in the batch, after the engine lock is let go
       } else {
+      if (!rc) rc = size_workspace(p);
       if (!rc)
         rc = enqueue_dedup(e, p->dict, d_dedup, n, p->d_res, nullptr, 0, ps, nullptr, 1, nullptr);
       if (!rc) rc = host_fence(e, ps, p->fence);

@@ -72,6 +72,12 @@ for s in "$@"; do
       timeout -k 10 300 python3 bench.py --workload c1-sha256 --packs 32 --steps 5 --warmup 2 > "$OUT/packs_sha.json" 2> "$OUT/packs_sha.err"
       ok $? packs_sha
       tail -c 600 "$OUT/packs_c1.json" ;;
+    packs128)
+      timeout -k 10 400 python3 bench.py --workload c1-sha256 --packs 128 --steps 3 --warmup 1 --packs-modes decisions > "$OUT/packs128_sha.json" 2> "$OUT/packs128_sha.err"
+      ok $? packs128_sha
+      timeout -k 10 400 python3 bench.py --workload c1 --packs 128 --steps 5 --warmup 2 --packs-modes decisions > "$OUT/packs128_c1.json" 2> "$OUT/packs128_c1.err"
+      ok $? packs128_c1
+      tail -c 400 "$OUT/packs128_sha.json" ;;
     ptrace)
       NGPU_BATCH_TRACE=1 timeout -k 10 300 python3 bench.py --workload c1 --packs 32 --steps 6 --warmup 2 --packs-modes decisions --no-cpu-baseline > "$OUT/ptrace_c1.json" 2> "$OUT/ptrace_c1.err"
       ok $? ptrace_c1
