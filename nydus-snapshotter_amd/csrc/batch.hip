@@ -65,6 +65,7 @@ struct BatchLane {
   uint8_t *h_tab = nullptr;  // pinned: chunk table + layer boundaries of one batch
   uint64_t h_cap = 0;
   std::shared_ptr<BatchEvent> last;  // the end of its last batch
+  bool running = false;  // its last batch has not been seen to end (Batcher::m)
 };
 
 constexpr int kLanes = 4;  // = GPU_MAX_HW_QUEUES: more lanes would share hardware queues
@@ -115,7 +116,6 @@ __global__ void batch_stats_out(const uint64_t *__restrict__ st, const ngpu_laye
 }
 
 constexpr int kWindowUs = 250;
-constexpr int kPollUs = 50;  // the last batch's end, polled while packs gather
 constexpr size_t kMaxJobs = 256;
 constexpr uint64_t kMaxBytes = 1ull << 30;
 constexpr uint64_t kMaxChunks = 1ull << 20;
@@ -134,13 +134,14 @@ int grow_dev(ngpu_engine *e, T **p, uint64_t &cap, uint64_t want) {
   return 0;
 }
 
-// A lane whose last batch has ended (or that never ran one), or -1.
-int idle_lane(ngpu_engine *e, Batcher &b) {
-  for (int k = 0; k < kLanes; ++k) {
-    if (!b.lane[k].last) return k;
-    DeviceGuard dg(e->device);
-    if (hipEventQuery(b.lane[k].last->ev) != hipErrorNotReady) return k;
-  }
+// A lane whose last batch has ended (or that never ran one), or -1 (b.m
+// held).  A batch's end is seen by the first of its packs whose
+// hipEventSynchronize returns (batch_run), not by polling: hipEventQuery on
+// an event other threads synchronize on blocked for the whole batch (~30 ms
+// for SHA-256; HIP API trace, profiles/r5/pack_api_trace_r5j.md).
+int idle_lane(Batcher &b) {
+  for (int k = 0; k < kLanes; ++k)
+    if (!b.lane[k].running) return k;
   return -1;
 }
 
@@ -291,12 +292,15 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(kWindowUs);
     int ln = -1;
     for (;;) {
-      ln = idle_lane(e, b);
+      ln = idle_lane(b);
       const bool all_in = b.open.size() >= (size_t)e->open_packs.load() || b.open.size() >= kMaxJobs;
-      const auto now = std::chrono::steady_clock::now();
-      if (ln >= 0 && (all_in || now >= until)) break;
-      b.cv.wait_until(lk, ln >= 0 ? until : now + std::chrono::microseconds(kPollUs));
+      if (ln >= 0 && (all_in || std::chrono::steady_clock::now() >= until)) break;
+      if (ln >= 0)
+        b.cv.wait_until(lk, until);
+      else
+        b.cv.wait(lk);  // a lane's end (batch_run) or a new pack wakes it
     }
+    b.lane[ln].running = true;  // taken: no other leader picks it
     // this leader's batch: the open packs sharing its dict, within the caps
     std::vector<BatchJob *> take;
     uint64_t bytes = 0, chunks = 0;
@@ -317,6 +321,7 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     lk.unlock();
     const double t_take = batch_trace_on() ? batch_now_us() : 0;
     const int rc = launch_batch(e, b, b.lane[ln], take);
+    for (BatchJob *x : take) x->lane = ln;
     if (batch_trace_on())
       fprintf(stderr, "{\"batch_trace\": %llu, \"lane\": %d, \"lead_us\": %.1f, \"take_us\": %.1f, "
               "\"enqueued_us\": %.1f, \"layers\": %zu, \"open_packs\": %d, \"rc\": %d}\n",
@@ -326,6 +331,7 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
       (void)hipStreamSynchronize(b.lane[ln].s);
     }
     lk.lock();
+    if (rc) b.lane[ln].running = false;  // drained above
     for (BatchJob *x : take) {
       x->rc = rc;
       x->enqueued = true;
@@ -336,7 +342,16 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
   lk.unlock();
   if (j.rc) return j.rc;
   DeviceGuard dg(e->device);
-  if (hipEventSynchronize(j.done->ev) != hipSuccess) return fail(e, NGPU_EHIP, "batch: stream failed");
+  const bool ok = hipEventSynchronize(j.done->ev) == hipSuccess;
+  {
+    std::lock_guard<std::mutex> g(b.m);  // the first pack back frees the lane for the next leader
+    BatchLane &l = b.lane[j.lane];
+    if (l.running && l.last == j.done) {
+      l.running = false;
+      b.cv.notify_all();
+    }
+  }
+  if (!ok) return fail(e, NGPU_EHIP, "batch: stream failed");
   return 0;
 }
 

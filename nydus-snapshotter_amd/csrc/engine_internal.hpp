@@ -133,6 +133,7 @@ struct BatchJob {
   int rc = 0;
   bool enqueued = false;
   uint32_t batch_layers = 0;         // layers in the launch set it joined
+  int lane = 0;                      // the batch lane it ran on
   char path[48] = "";                // the batch's digest kernels (error messages)
   std::shared_ptr<BatchEvent> done;
 };
