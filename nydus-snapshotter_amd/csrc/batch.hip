@@ -64,8 +64,8 @@ struct BatchLane {
   uint64_t l_cap = 0;
   uint8_t *h_tab = nullptr;  // pinned: chunk table + layer boundaries of one batch
   uint64_t h_cap = 0;
-  std::shared_ptr<BatchEvent> last;  // the end of its last batch
-  bool running = false;  // its last batch has not been seen to end (Batcher::m)
+  bool running = false;  // its batch `seq` has not been seen to end (Batcher::m)
+  uint64_t seq = 0;      // the batch it was last taken for (Batcher::m)
 };
 
 constexpr int kLanes = 4;  // = GPU_MAX_HW_QUEUES: more lanes would share hardware queues
@@ -76,6 +76,7 @@ struct Batcher {
   std::vector<BatchJob *> open;  // packs waiting for a batch
   bool leading = false;
   BatchLane lane[kLanes];
+  uint64_t seq = 0;  // batches taken
   uint64_t batches = 0, jobs = 0, max_jobs = 0;
 };
 
@@ -146,7 +147,7 @@ int idle_lane(Batcher &b) {
 }
 
 // Enqueue one batch on an idle lane (the leader, e->mu taken here).
-int launch_batch(ngpu_engine *e, Batcher &bt, BatchLane &b, const std::vector<BatchJob *> &jobs) {
+int launch_batch(ngpu_engine *e, BatchLane &b, const std::vector<BatchJob *> &jobs) {
   std::lock_guard<std::mutex> g(e->mu);
   DeviceGuard dg(e->device);
   if (!b.s) {
@@ -249,10 +250,6 @@ int launch_batch(ngpu_engine *e, Batcher &bt, BatchLane &b, const std::vector<Ba
     j->done = done;
     j->batch_layers = (uint32_t)K;
   }
-  b.last = done;
-  ++bt.batches;
-  bt.jobs += K;
-  bt.max_jobs = std::max<uint64_t>(bt.max_jobs, K);
   return 0;
 }
 
@@ -300,7 +297,14 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
       else
         b.cv.wait(lk);  // a lane's end (batch_run) or a new pack wakes it
     }
-    b.lane[ln].running = true;  // taken: no other leader picks it
+    // taken, under b.m: no other leader picks the lane, and a pack of the
+    // lane's previous batch that returns only now (its seq is older) does
+    // not free it.  (Setting the lane's end marker later, in launch_batch
+    // without b.m, let such a late pack free a lane whose next batch was
+    // running; the leader after it reused the lane's buffers under it.)
+    const uint64_t seq = ++b.seq;
+    b.lane[ln].running = true;
+    b.lane[ln].seq = seq;
     // this leader's batch: the open packs sharing its dict, within the caps
     std::vector<BatchJob *> take;
     uint64_t bytes = 0, chunks = 0;
@@ -320,18 +324,27 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     const int open_now = e->open_packs.load();
     lk.unlock();
     const double t_take = batch_trace_on() ? batch_now_us() : 0;
-    const int rc = launch_batch(e, b, b.lane[ln], take);
-    for (BatchJob *x : take) x->lane = ln;
+    for (BatchJob *x : take) {  // (read by their packs only after `enqueued`, under b.m)
+      x->lane = ln;
+      x->seq = seq;
+    }
+    const int rc = launch_batch(e, b.lane[ln], take);
     if (batch_trace_on())
       fprintf(stderr, "{\"batch_trace\": %llu, \"lane\": %d, \"lead_us\": %.1f, \"take_us\": %.1f, "
               "\"enqueued_us\": %.1f, \"layers\": %zu, \"open_packs\": %d, \"rc\": %d}\n",
-              (unsigned long long)b.batches, ln, t_lead, t_take, batch_now_us(), take.size(), open_now, rc);
+              (unsigned long long)seq, ln, t_lead, t_take, batch_now_us(), take.size(), open_now, rc);
     if (rc && b.lane[ln].s) {  // part of it may be enqueued: let it drain before the packs free their buffers
       DeviceGuard dg(e->device);
       (void)hipStreamSynchronize(b.lane[ln].s);
     }
     lk.lock();
-    if (rc) b.lane[ln].running = false;  // drained above
+    if (rc) {
+      b.lane[ln].running = false;  // drained above
+    } else {
+      ++b.batches;
+      b.jobs += take.size();
+      b.max_jobs = std::max<uint64_t>(b.max_jobs, take.size());
+    }
     for (BatchJob *x : take) {
       x->rc = rc;
       x->enqueued = true;
@@ -346,7 +359,7 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
   {
     std::lock_guard<std::mutex> g(b.m);  // the first pack back frees the lane for the next leader
     BatchLane &l = b.lane[j.lane];
-    if (l.running && l.last == j.done) {
+    if (l.running && l.seq == j.seq) {
       l.running = false;
       b.cv.notify_all();
     }
@@ -374,7 +387,6 @@ void batcher_free(ngpu_engine *e) {
                     (void *)l.d_lst, (void *)l.d_dst})
       if (p) (void)hipFree(p);
     if (l.h_tab) (void)hipHostFree(l.h_tab);
-    l.last.reset();
     // l.s is one of e->streams: destroyed with them
   }
   delete b;

@@ -71,16 +71,30 @@ int pick_group_log2(const ngpu_engine *e, uint64_t data_len) {
   return D;
 }
 
+// The event after which nothing reads the slot any more, recorded into
+// sl.last_ev.  A stage's end event (a timing stop event, the dedup's last
+// kernel) does not cover the reads its call enqueues after it -- the stats
+// read-back copies, a batch's stats-out kernel -- so when the slot's last
+// stream lives as long as the engine (ws_lazy_end) the fence is recorded on
+// it now, after all of them.  (A regrow freed the stats of a slot whose
+// read-back copy was still queued behind a timing stop event: an illegal
+// memory access in the timed packs bench, r5n.)  A caller's stream may be
+// gone, so its stage's own end event stays the fence.
+int slot_fence(ngpu_engine *e, ngpu_ws_slot &sl) {
+  if (!sl.last_ev || ws_lazy_end(e, sl.last, false)) {
+    HIP_TRY(e, hipEventRecord(sl.done, sl.last));
+    sl.last_ev = sl.done;
+  }
+  return 0;
+}
+
 // Before a slot's buffers are freed: its last stage has finished.  (The
 // stage is on another stream; a buffer freed under it could be handed to
 // another slot's allocation and written by a stage unordered with it.)
 int slot_quiesce(ngpu_engine *e) {
   ngpu_ws_slot &sl = *e->cur;
   if (!sl.pending) return 0;
-  if (!sl.last_ev) {  // lazy end: record it on the stage's stream now
-    HIP_TRY(e, hipEventRecord(sl.done, sl.last));
-    sl.last_ev = sl.done;
-  }
+  if (int rc = slot_fence(e, sl)) return rc;
   HIP_TRY(e, hipEventSynchronize(sl.last_ev));
   return 0;
 }
@@ -189,10 +203,7 @@ ngpu_ws_slot *use_slot(ngpu_engine *e, hipStream_t s) {
 int ws_acquire(ngpu_engine *e, hipStream_t s) {
   ngpu_ws_slot &sl = *e->cur;
   if (!sl.pending || sl.last == s) return 0;
-  if (!sl.last_ev) {  // a lazy stage end (ws_lazy_end): record it now
-    HIP_TRY(e, hipEventRecord(sl.done, sl.last));
-    sl.last_ev = sl.done;
-  }
+  if (int rc = slot_fence(e, sl)) return rc;  // a lazy stage end, or reads after the end event
   HIP_TRY(e, hipStreamWaitEvent(s, sl.last_ev, 0));
   return 0;
 }
@@ -239,6 +250,10 @@ static int ring_reclaim(ngpu_engine *e, int k) {
     if (!sl.pending || !sl.last_ev) continue;
     for (hipEvent_t ev : e->ev[k])
       if (sl.last_ev == ev) {
+        if (ws_lazy_end(e, sl.last, false)) {  // an engine stream: fenced afresh when next needed
+          sl.last_ev = nullptr;                // (slot_fence), after every read of the slot
+          break;
+        }
         HIP_TRY(e, hipEventSynchronize(ev));
         sl.pending = false;
         sl.last_ev = nullptr;

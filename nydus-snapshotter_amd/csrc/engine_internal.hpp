@@ -134,6 +134,7 @@ struct BatchJob {
   bool enqueued = false;
   uint32_t batch_layers = 0;         // layers in the launch set it joined
   int lane = 0;                      // the batch lane it ran on
+  uint64_t seq = 0;                  // its batch's number (the lane's end marker)
   char path[48] = "";                // the batch's digest kernels (error messages)
   std::shared_ptr<BatchEvent> done;
 };
