@@ -1307,7 +1307,7 @@ def packs_bench(args):
             "config": {"workload": f"{K} concurrent converter.Pack calls of distinct C1-size "
                                    f"layers on one engine ({wl['digester']}, 1 MiB chunks)",
                        "name": args.workload, "packs": K, "file_bytes_per_round": file_bytes,
-                       "tar_bytes_per_round": tar_bytes, "batch_window_us": 250,
+                       "tar_bytes_per_round": tar_bytes, "batch_window_us": 2000 if wl["digester"] == "sha256" else 250, "batch_lanes": 4,
                        "caller": "K native threads (tools/packs_drive.cpp), 1 MiB writes from "
                                  "pageable memory"},
             "modes": modes, "cpu_baseline": cpu,

@@ -18,7 +18,8 @@
 // the per-layer algorithm with layer boundaries).
 //
 // Window: the first pack to close leads; it waits until every pack open on
-// the engine has joined, or kWindowUs, whichever comes first (a lone pack
+// the engine has joined, or kWindowUs (SHA-256: kWindowShaUs), whichever
+// comes first (a lone pack
 // goes at once), and until one of the kLanes batch lanes is idle.  Batches on
 // different lanes run concurrently (each lane: its own stream, buffers and
 // workspace slot), so a small batch's chain latency -- a SHA-256 batch holds
@@ -68,7 +69,7 @@ struct BatchLane {
   uint64_t seq = 0;      // the batch it was last taken for (Batcher::m)
 };
 
-constexpr int kLanes = 4;  // = GPU_MAX_HW_QUEUES: more lanes would share hardware queues
+constexpr int kLanes = kBatchLanes;  // = GPU_MAX_HW_QUEUES: more lanes would share hardware queues
 
 struct Batcher {
   std::mutex m;
@@ -117,6 +118,11 @@ __global__ void batch_stats_out(const uint64_t *__restrict__ st, const ngpu_laye
 }
 
 constexpr int kWindowUs = 250;
+// SHA-256: a batch holds its lane for one 1 MiB chunk's chain (~21 ms)
+// whatever its size, so a longer wait for more packs costs < 10 % of that and
+// saves a whole chain time for every pack it adds (32 C1 packs closing over
+// ~3 ms went out as 4-5 batches in 250 µs windows).
+constexpr int kWindowShaUs = 2000;
 constexpr size_t kMaxJobs = 256;
 constexpr uint64_t kMaxBytes = 1ull << 30;
 constexpr uint64_t kMaxChunks = 1ull << 20;
@@ -153,6 +159,11 @@ int launch_batch(ngpu_engine *e, BatchLane &b, const std::vector<BatchJob *> &jo
   if (!b.s) {
     HIP_TRY(e, hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking));
     e->streams.push_back(b.s);  // lives as long as the engine (ws_lazy_end)
+    for (auto &sl : e->slots)   // the lane's own workspace slot
+      if (sl.lane && !sl.owner) {
+        sl.owner = b.s;
+        break;
+      }
   }
   const uint64_t K = jobs.size();
   std::vector<uint64_t> off(K), first(K + 1, 0);
@@ -210,8 +221,8 @@ int launch_batch(ngpu_engine *e, BatchLane &b, const std::vector<BatchJob *> &jo
   HIP_TRY(e, hipMemcpyAsync(b.d_lfirst, b.h_tab + N * sizeof(ngpu_chunk), (K + 1) * sizeof(uint64_t),
                             hipMemcpyHostToDevice, b.s));
   HIP_TRY(e, hipMemcpyAsync(b.d_dst, hd, 2 * K * sizeof(void *), hipMemcpyHostToDevice, b.s));
-  // the lane's workspace sized with headroom (powers of two), so batches of
-  // varying size do not regrow it -- a regrow waits for the slot's last stage
+  // the lane's own workspace sized with headroom (powers of two), so batches
+  // of varying size seldom regrow it
   {
     use_slot(e, b.s);
     const uint64_t n2 = next_pow2(N + 1), len2 = next_pow2(bytes + 1);
@@ -286,7 +297,8 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     // wait for the open packs to join -- until all have, or kWindowUs has
     // passed -- and for an idle lane (while every lane runs a batch, a new
     // one would only queue behind them: better to let more packs join it)
-    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(kWindowUs);
+    const int window = e->cfg.digester == NGPU_DIGEST_SHA256 ? kWindowShaUs : kWindowUs;
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(window);
     int ln = -1;
     for (;;) {
       ln = idle_lane(b);

@@ -177,14 +177,20 @@ int ensure_workspace(ngpu_engine *e, uint64_t n, uint64_t data_len, int D,
 
 ngpu_ws_slot *use_slot(ngpu_engine *e, hipStream_t s) {
   ngpu_ws_slot *pick = nullptr;
-  for (auto &sl : e->slots)  // the slot this stream used last: stream order
-    if (sl.pending && sl.last == s) {
+  for (auto &sl : e->slots)  // a batch lane's own slot
+    if (sl.lane && sl.owner == s) {
       pick = &sl;
       break;
     }
+  if (!pick)
+    for (auto &sl : e->slots)  // the slot this stream used last: stream order
+      if (!sl.lane && sl.pending && sl.last == s) {
+        pick = &sl;
+        break;
+      }
   if (!pick)  // a slot never used yet
     for (auto &sl : e->slots)
-      if (!sl.pending) {
+      if (!sl.lane && !sl.pending) {
         pick = &sl;
         break;
       }
@@ -194,7 +200,7 @@ ngpu_ws_slot *use_slot(ngpu_engine *e, hipStream_t s) {
   // and call, on a path the host enqueue already bounds.)
   if (!pick)
     for (auto &sl : e->slots)
-      if (!pick || sl.tick < pick->tick) pick = &sl;
+      if (!sl.lane && (!pick || sl.tick < pick->tick)) pick = &sl;
   pick->tick = ++e->tick;
   e->cur = pick;
   return pick;
@@ -540,14 +546,16 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   e->uid = next_uid.fetch_add(1, std::memory_order_relaxed);
   e->cfg = c;
   // NGPU_WS_SLOTS: workspace slots = calls on distinct streams that may run
-  // at once (default 8: the batcher's 4 lanes keep theirs while other calls
-  // and unbatched packs take the rest; a slot allocates on first use)
-  int nslots = 8;
+  // at once (default 4, the hardware queues HIP gives a process), plus one
+  // slot of its own per batch lane (a lane never waits on another call's
+  // slot, nor regrows one under it; a slot allocates on first use)
+  int nslots = 4;
   if (const char *v = getenv("NGPU_WS_SLOTS")) {
     const long x = strtol(v, nullptr, 10);
     if (x >= 1 && x <= 64) nslots = (int)x;
   }
-  e->slots.resize((size_t)nslots);
+  e->slots.resize((size_t)nslots + kBatchLanes);
+  for (size_t i = (size_t)nslots; i < e->slots.size(); ++i) e->slots[i].lane = true;
   for (auto &sl : e->slots) sl.ws.grid_stages = (c.flags & NGPU_FLAG_GRID_STAGES) != 0;
   e->cur = &e->slots[0];
   e->device = c.device;

@@ -100,7 +100,8 @@ struct ngpu_dict {
 // recorded yet, only while `last` is a stream that lives as long as the
 // engine); a stage on another stream waits for it first, so calls on
 // different streams never run over one workspace concurrently.  An engine
-// keeps several (NGPU_WS_SLOTS, default 8): a call on a stream keeps the slot
+// keeps several (NGPU_WS_SLOTS, default 4, plus one of its own per batch lane,
+// batch.hip): a call on a stream keeps the slot
 // its stream used last (stream order is the ordering), a call on another
 // stream takes an idle slot, so independent layers on different streams --
 // containerd converting an image's layers concurrently -- run side by side
@@ -114,9 +115,12 @@ struct ngpu_ws_slot {
   uint64_t *h_stats = nullptr;   // pinned: counters + layer stats read back
   uint64_t tick = 0;             // last use (LRU)
   char path[48] = "";            // digest kernels of its last digest stage (error messages)
+  bool lane = false;             // one of the batch lanes' own slots (never taken by others)
+  hipStream_t owner = nullptr;   // lane slot: the batch lane stream it belongs to
 };
 
 namespace ngpu {
+constexpr int kBatchLanes = 4;  // concurrent batch lanes (batch.hip) = GPU_MAX_HW_QUEUES
 struct Batcher;
 struct BatchEvent;
 // One pack's layer in a batch (batch.hip): its bytes and chunk table already
