@@ -56,13 +56,14 @@ struct BatchLane {
   uint8_t *d_data = nullptr;
   uint64_t data_cap = 0;
   ngpu_chunk *d_ch = nullptr;
-  ngpu_result *d_res = nullptr;
   uint64_t ch_cap = 0;
+  ngpu_result *d_res = nullptr;
+  uint64_t res_cap = 0;
   uint64_t *d_lfirst = nullptr;
   void **d_dst = nullptr;  // per layer: its pack's pinned results, then its pinned stats
   uint64_t dst_cap = 0;
   ngpu_layer_stats *d_lst = nullptr;
-  uint64_t l_cap = 0;
+  uint64_t l_cap = 0, lst_cap = 0;
   uint8_t *h_tab = nullptr;  // pinned: chunk table + layer boundaries of one batch
   uint64_t h_cap = 0;
   bool running = false;  // its batch `seq` has not been seen to end (Batcher::m)
@@ -127,14 +128,21 @@ constexpr size_t kMaxJobs = 256;
 constexpr uint64_t kMaxBytes = 1ull << 30;
 constexpr uint64_t kMaxChunks = 1ull << 20;
 
+// A lane buffer of at least `want` elements (powers of two).  Stream-ordered
+// on the lane's own stream from the engine's pool: hipFree would wait for the
+// whole device -- every other lane's running batch and every pack's copies --
+// under the engine lock.
 template <class T>
-int grow_dev(ngpu_engine *e, T **p, uint64_t &cap, uint64_t want) {
+int grow_dev(ngpu_engine *e, hipStream_t s, T **p, uint64_t &cap, uint64_t want) {
   if (want <= cap && *p) return 0;  // (the lane is idle: its last batch has ended)
-  if (*p) (void)hipFree(*p), *p = nullptr, cap = 0;
+  if (*p) (void)hipFreeAsync(*p, s), *p = nullptr, cap = 0;
   uint64_t c = 4096;
   while (c < want) c *= 2;
-  if (hipMalloc((void **)p, c * sizeof(T)) != hipSuccess) {
+  const hipError_t r = e->seg_pool ? hipMallocFromPoolAsync((void **)p, c * sizeof(T), e->seg_pool, s)
+                                   : hipMallocAsync((void **)p, c * sizeof(T), s);
+  if (r != hipSuccess) {
     (void)hipGetLastError();
+    *p = nullptr;
     return fail(e, NGPU_ENOMEM, "batch: device buffer allocation failed");
   }
   cap = c;
@@ -174,20 +182,12 @@ int launch_batch(ngpu_engine *e, BatchLane &b, const std::vector<BatchJob *> &jo
     first[k + 1] = first[k] + jobs[k]->n;
   }
   const uint64_t N = first[K];
-  if (int rc = grow_dev(e, &b.d_data, b.data_cap, bytes + 64)) return rc;
-  const uint64_t ch_cap0 = b.ch_cap;
-  if (int rc = grow_dev(e, &b.d_ch, b.ch_cap, N + 1)) return rc;
-  if (!b.d_res || b.ch_cap != ch_cap0) {  // results sized with the chunk table
-    if (b.d_res) (void)hipFree(b.d_res), b.d_res = nullptr;
-    HIP_TRY(e, hipMalloc((void **)&b.d_res, b.ch_cap * sizeof(ngpu_result)));
-  }
-  const uint64_t l_cap0 = b.l_cap;
-  if (int rc = grow_dev(e, &b.d_lfirst, b.l_cap, K + 2)) return rc;
-  if (!b.d_lst || b.l_cap != l_cap0) {
-    if (b.d_lst) (void)hipFree(b.d_lst), b.d_lst = nullptr;
-    HIP_TRY(e, hipMalloc((void **)&b.d_lst, b.l_cap * sizeof(ngpu_layer_stats)));
-  }
-  if (int rc = grow_dev(e, &b.d_dst, b.dst_cap, 2 * K + 2)) return rc;
+  if (int rc = grow_dev(e, b.s, &b.d_data, b.data_cap, bytes + 64)) return rc;
+  if (int rc = grow_dev(e, b.s, &b.d_ch, b.ch_cap, N + 1)) return rc;
+  if (int rc = grow_dev(e, b.s, &b.d_res, b.res_cap, N + 1)) return rc;
+  if (int rc = grow_dev(e, b.s, &b.d_lfirst, b.l_cap, K + 2)) return rc;
+  if (int rc = grow_dev(e, b.s, &b.d_lst, b.lst_cap, K + 2)) return rc;
+  if (int rc = grow_dev(e, b.s, &b.d_dst, b.dst_cap, 2 * K + 2)) return rc;
   const uint64_t tab = N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t) + 2 * K * sizeof(void *);
   if (tab > b.h_cap) {
     if (b.h_tab) (void)hipHostFree(b.h_tab), b.h_tab = nullptr, b.h_cap = 0;
@@ -394,10 +394,11 @@ void batcher_free(ngpu_engine *e) {
   if (!b) return;
   DeviceGuard dg(e->device);
   for (BatchLane &l : b->lane) {
-    if (l.s) (void)hipStreamSynchronize(l.s);
+    if (!l.s) continue;  // (a lane that never ran has no buffers)
     for (void *p : {(void *)l.d_data, (void *)l.d_ch, (void *)l.d_res, (void *)l.d_lfirst,
                     (void *)l.d_lst, (void *)l.d_dst})
-      if (p) (void)hipFree(p);
+      if (p) (void)hipFreeAsync(p, l.s);
+    (void)hipStreamSynchronize(l.s);
     if (l.h_tab) (void)hipHostFree(l.h_tab);
     // l.s is one of e->streams: destroyed with them
   }

@@ -100,7 +100,7 @@ struct ngpu_dict {
 // recorded yet, only while `last` is a stream that lives as long as the
 // engine); a stage on another stream waits for it first, so calls on
 // different streams never run over one workspace concurrently.  An engine
-// keeps several (NGPU_WS_SLOTS, default 4, plus one of its own per batch lane,
+// keeps several (NGPU_WS_SLOTS, default 8, plus one of its own per batch lane,
 // batch.hip): a call on a stream keeps the slot
 // its stream used last (stream order is the ordering), a call on another
 // stream takes an idle slot, so independent layers on different streams --
