@@ -1311,8 +1311,9 @@ def packs_bench(args):
                        "caller": "K native threads (tools/packs_drive.cpp), 1 MiB writes from "
                                  "pageable memory"},
             "modes": modes, "cpu_baseline": cpu,
-            "bound": "PCIe H2D of the tars (~50 GB/s) and the host copies into pinned staging; "
-                     "sha256: one 1 MiB chunk's chain per launch set (~21 ms)"}
+            "bound": "blake3: PCIe H2D of the tars through 2 shared copy lanes (~45 GB/s, "
+                     "tools/h2d_streams); sha256: one 1 MiB chunk's chain per batch (21-40 ms) "
+                     "whatever its size; stream: host zstd level 1 on the 16-core quota"}
     if cpu:
         line["speedup_vs_cpu"] = round(modes["decisions"]["gbs"] / cpu["value"], 2)
         if cpu.get("pipeline_gbs") and "stream_zstd" in modes:
