@@ -72,6 +72,10 @@ for s in "$@"; do
       timeout -k 10 300 python3 bench.py --workload c1-sha256 --packs 32 --steps 5 --warmup 2 > "$OUT/packs_sha.json" 2> "$OUT/packs_sha.err"
       ok $? packs_sha
       tail -c 600 "$OUT/packs_c1.json" ;;
+    strace)
+      NGPU_PACK_TRACE=1 NGPU_SINK_STATS=1 timeout -k 10 300 python3 bench.py --workload c1 --packs 32 --steps 2 --warmup 2 --packs-modes decisions,stream_zstd --no-cpu-baseline > "$OUT/strace_c1.json" 2> "$OUT/strace_c1.err"
+      ok $? strace_c1
+      grep -c pack_trace "$OUT/strace_c1.err" ;;
     packs128)
       timeout -k 10 400 python3 bench.py --workload c1-sha256 --packs 128 --steps 3 --warmup 1 --packs-modes decisions > "$OUT/packs128_sha.json" 2> "$OUT/packs128_sha.err"
       ok $? packs128_sha
