@@ -581,6 +581,7 @@ struct BlobWriter::Impl {
   std::vector<uint32_t> csize;  // per NEW chunk (index order)
   std::vector<uint8_t> cflag;
   uint64_t compressed_chunks = 0;
+  uint64_t batches_added = 0;  // batches submitted by add()
   // batch buffers: per-chunk scratch slots, compacted into an output batch
   Batch scratch;  // from the cache at the first compressed batch
   bool scratch_taken = false;
@@ -735,13 +736,18 @@ int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) 
   Impl &m = *im_;
   if (m.rc) return m.rc;
   const uint32_t kind = m.opt.compressor;
-  // batches of <= 64 MiB of input keep the scratch bounded
+  // batches of <= 64 MiB of input keep the scratch bounded (smaller first ones, below)
   uint64_t a = 0;
   while (a < k) {
     if (m.cancel && __atomic_load_n(m.cancel, __ATOMIC_RELAXED))
       return m.rc = host_fail(NGPU_ECANCELED, "pack: cancelled");
     uint64_t b = a, bytes = 0;
-    while (b < k && (b == a || bytes + len[b] <= (64ull << 20))) bytes += len[b++];
+    // batches grow 4, 8, 16, 32, then 64 MiB of input: the sink starts hashing
+    // the first while the next compresses (a 10 MB layer used to compress all
+    // of it, then hash all of it), and big layers still run in large batches
+    const uint64_t lim = std::min<uint64_t>(64ull << 20, 4ull << (20 + std::min<uint64_t>(m.batches_added, 4)));
+    while (b < k && (b == a || bytes + len[b] <= lim)) bytes += len[b++];
+    ++m.batches_added;
     const uint64_t nb = b - a;
     Batch out = m.take_buffer();
     if (kind == NGPU_COMPRESSOR_NONE) {
