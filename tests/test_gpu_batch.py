@@ -175,3 +175,45 @@ def test_native_threads_drive_concurrent_packs(oracle):
             assert (got[k, 3] > 0) == (mode == 1)
         assert all(x > 0 for x in rs)
         assert bs["packs"] >= 2, bs
+
+
+@pytest.mark.parametrize("digester", ["blake3", "sha256"])
+def test_batch_lanes_stress_timed_engine(oracle, digester):
+    """32 native threads, 4 rounds each of decisions then streams, on ONE
+    timed engine (NGPU_FLAG_TIMING, as bench.py --packs): batches on the 4
+    lanes overlap, lanes are freed by the first pack back and retaken.  Every
+    layer's NEW / INTRA / DICT counts equal the oracle's in every mode (a lane
+    freed under its running batch once faulted exactly here, r5n)."""
+    import ctypes
+    import os
+    lib_path = os.path.join(os.path.dirname(nydus_gpu._lib.LIB_PATH), "build", "libpacks_drive.so")
+    drive = ctypes.CDLL(lib_path).packs_drive
+    vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
+    drive.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u64), u64, u32, u32, u32, u32,
+                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64),
+                      ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, u64]
+    S, K, R = 0x100000, 32, 4
+    tars = [np.frombuffer(layers.alpine_like_tar(0x5150 + i), np.uint8) for i in range(K)]
+    want = []
+    for t in tars:
+        ch = oracle.tar_chunks(t.tobytes(), S)
+        dec, _ = oracle.dedup(oracle.digest_chunks(t.tobytes(), ch, digester), ch["length"])
+        want.append(list(np.bincount(dec["kind"], minlength=3)[:3]))
+    eng = nydus_gpu.Engine(device=0, digester=digester, chunk_size=S, timing=True,
+                           staging_bytes=16 << 20)
+    try:
+        for mode in (0, 1):
+            rs = (ctypes.c_double * R)()
+            per = (u64 * (4 * K))()
+            err = ctypes.create_string_buffer(256)
+            rc = drive(eng._h, K, (vp * K)(*[t.ctypes.data for t in tars]),
+                       (u64 * K)(*[t.size for t in tars]), 1 << 20, mode,
+                       nydus_gpu._lib.DIGESTERS[digester], S, R, rs, per, None, err, 256)
+            assert rc == 0, err.value
+            got = np.array(per, np.uint64).reshape(K, 4)
+            for k in range(K):
+                assert list(got[k, :3]) == want[k], (mode, k)
+        bs = eng.batch_stats()
+    finally:
+        eng.close()
+    assert bs["packs"] >= 2 * K and bs["batches"] >= 2, bs
