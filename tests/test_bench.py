@@ -1,6 +1,7 @@
 """bench.py's synthetic layer layout equals what the real tar front end
 produces on the same bytes (small instance, CPU only)."""
 import io
+import os
 import tarfile
 
 import numpy as np
@@ -127,3 +128,23 @@ def test_rank_check_refuses_a_world_other_than_gpus():
     assert ex.value.code == 4
     r = bench.rank_check(argparse.Namespace(gpus=1), None, 1, 0, 0, "nccl", FakeTorch)
     assert r["world_size"] == 1 and r["distinct_devices"] == 1 and r["rccl_world_size"] is None
+
+
+def test_packs_drive_harness_loads_and_checks_its_arguments():
+    """bench.py --packs's native caller (tools/packs_drive.cpp ->
+    build/libpacks_drive.so): it loads beside libnydusgpu.so, exports
+    packs_drive, and refuses a null engine or empty layer set before any HIP
+    call (no GPU here)."""
+    import ctypes
+    from conftest import ROOT
+    path = os.path.join(ROOT, "nydus-snapshotter_amd", "build", "libpacks_drive.so")
+    assert os.path.exists(path), "run `make -C nydus-snapshotter_amd`"
+    drive = ctypes.CDLL(path).packs_drive
+    drive.restype = ctypes.c_int
+    rs = (ctypes.c_double * 1)()
+    per = (ctypes.c_uint64 * 4)()
+    null = ctypes.c_void_p()
+    assert drive(null, 1, null, null, ctypes.c_uint64(1 << 20), 0, 0, 0x100000, 1, rs, per, None,
+                 None, ctypes.c_uint64(0)) == -1  # NGPU_EINVAL
+    assert drive(ctypes.c_void_p(1), 0, null, null, ctypes.c_uint64(1 << 20), 0, 0, 0x100000, 1, rs,
+                 per, None, None, ctypes.c_uint64(0)) == -1
