@@ -72,6 +72,18 @@ for s in "$@"; do
       timeout -k 10 300 python3 bench.py --workload c1-sha256 --packs 32 --steps 5 --warmup 2 > "$OUT/packs_sha.json" 2> "$OUT/packs_sha.err"
       ok $? packs_sha
       tail -c 600 "$OUT/packs_c1.json" ;;
+    h2dp)
+      for cfg in "32 20 2 1" "32 20 2 2" "32 20 2 4" "32 20 1 4" "32 20 4 4" "32 20 2 12"; do
+        timeout -k 10 60 ./tools/h2d_streams $cfg >> "$OUT/h2dp.jsonl" 2>> "$OUT/h2dp.err"
+        ok $? "h2dp $cfg"
+      done
+      for g in 2097152 4194304; do
+        NGPU_EAGER_COPY=$g timeout -k 10 300 python3 bench.py --workload c1 --packs 32 --steps 10 --warmup 3 --packs-modes decisions --no-cpu-baseline > "$OUT/packs_eager_$g.json" 2> "$OUT/packs_eager_$g.err"
+        ok $? "packs eager $g"
+      done
+      timeout -k 10 300 python3 bench.py --workload c1 --packs 32 --steps 10 --warmup 3 --packs-modes decisions --no-cpu-baseline > "$OUT/packs_eager_default.json" 2> "$OUT/packs_eager_default.err"
+      ok $? "packs eager default"
+      cat "$OUT/h2dp.jsonl" ;;
     strace)
       NGPU_PACK_TRACE=1 NGPU_SINK_STATS=1 timeout -k 10 300 python3 bench.py --workload c1 --packs 32 --steps 2 --warmup 2 --packs-modes decisions,stream_zstd --no-cpu-baseline > "$OUT/strace_c1.json" 2> "$OUT/strace_c1.err"
       ok $? strace_c1
