@@ -765,7 +765,10 @@ int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) 
       m.slot_off[0] = 0;
       for (uint64_t i = 0; i < nb; ++i)
         m.slot_off[i + 1] = m.slot_off[i] + compress_bound(kind, len[a + i]);
-      if (!m.scratch_taken) m.scratch_taken = WriterCache::get().take_buf(&m.scratch) || true;
+      if (!m.scratch_taken) {  // one an earlier writer left, if any
+        (void)WriterCache::get().take_buf(&m.scratch);
+        m.scratch_taken = true;
+      }
       m.scratch.resize(m.slot_off[nb]);
       m.clen.assign(nb, 0);
       m.pool->run(nb, [&](uint64_t i) {
