@@ -112,6 +112,10 @@ for s in "$@"; do
         ok $? "h2d $cfg"
       done
       cat "$OUT/h2d.jsonl" ;;
+    n4)
+      NYDUS_NODE_EXTRA_DEVICES=0,0,0,0 timeout -k 10 900 python3 bench.py --gpus 4 --steps 5 --warmup 3 --dist-backend gloo --c4-layers 2 > "$OUT/bench_c2_n4_gloo.json" 2> "$OUT/bench_c2_n4_gloo.err"
+      ok $? n4
+      python3 -c "import json; d=json.loads(open('$OUT/bench_c2_n4_gloo.json').read().strip().splitlines()[-1]); print(d['value'], d['n_gpus'], d.get('ranks'), json.dumps(d.get('node_cabi', {}))[:300], json.dumps(d.get('c4', {}))[:200], json.dumps(d.get('sharded_dict', {}))[:200])" ;;
     n2)
       NYDUS_NODE_EXTRA_DEVICES=0,0 timeout -k 10 600 python3 bench.py --gpus 2 --steps 10 --warmup 5 --dist-backend gloo --c4-layers 4 > "$OUT/bench_c2_n2_gloo.json" 2> "$OUT/bench_c2_n2_gloo.err"
       ok $? n2
