@@ -31,6 +31,7 @@
 #include <chrono>
 #include <condition_variable>
 
+#include "batch_lanes.hpp"
 #include "engine_internal.hpp"
 
 namespace ngpu {
@@ -66,8 +67,6 @@ struct BatchLane {
   uint64_t l_cap = 0, lst_cap = 0;
   uint8_t *h_tab = nullptr;  // pinned: chunk table + layer boundaries of one batch
   uint64_t h_cap = 0;
-  bool running = false;  // its batch `seq` has not been seen to end (Batcher::m)
-  uint64_t seq = 0;      // the batch it was last taken for (Batcher::m)
 };
 
 constexpr int kLanes = kBatchLanes;  // = GPU_MAX_HW_QUEUES: more lanes would share hardware queues
@@ -78,7 +77,7 @@ struct Batcher {
   std::vector<BatchJob *> open;  // packs waiting for a batch
   bool leading = false;
   BatchLane lane[kLanes];
-  uint64_t seq = 0;  // batches taken
+  LaneTable<kLanes> lanes;  // which lane is free (batch_lanes.hpp), under m
   uint64_t batches = 0, jobs = 0, max_jobs = 0;
 };
 
@@ -149,16 +148,10 @@ int grow_dev(ngpu_engine *e, hipStream_t s, T **p, uint64_t &cap, uint64_t want)
   return 0;
 }
 
-// A lane whose last batch has ended (or that never ran one), or -1 (b.m
-// held).  A batch's end is seen by the first of its packs whose
-// hipEventSynchronize returns (batch_run), not by polling: hipEventQuery on
-// an event other threads synchronize on blocked for the whole batch (~30 ms
-// for SHA-256; HIP API trace, profiles/r5/pack_api_trace_r5j.md).
-int idle_lane(Batcher &b) {
-  for (int k = 0; k < kLanes; ++k)
-    if (!b.lane[k].running) return k;
-  return -1;
-}
+// (A batch's end is seen by the first of its packs whose hipEventSynchronize
+// returns, batch_run, not by polling: hipEventQuery on an event other threads
+// synchronize on blocked for the whole batch, ~30 ms for SHA-256; HIP API
+// trace, profiles/r5/pack_api_trace_r5j.md.)
 
 // Enqueue one batch on an idle lane (the leader, e->mu taken here).
 int launch_batch(ngpu_engine *e, BatchLane &b, const std::vector<BatchJob *> &jobs) {
@@ -301,7 +294,7 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(window);
     int ln = -1;
     for (;;) {
-      ln = idle_lane(b);
+      ln = b.lanes.idle();
       const bool all_in = b.open.size() >= (size_t)e->open_packs.load() || b.open.size() >= kMaxJobs;
       if (ln >= 0 && (all_in || std::chrono::steady_clock::now() >= until)) break;
       if (ln >= 0)
@@ -309,14 +302,7 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
       else
         b.cv.wait(lk);  // a lane's end (batch_run) or a new pack wakes it
     }
-    // taken, under b.m: no other leader picks the lane, and a pack of the
-    // lane's previous batch that returns only now (its seq is older) does
-    // not free it.  (Setting the lane's end marker later, in launch_batch
-    // without b.m, let such a late pack free a lane whose next batch was
-    // running; the leader after it reused the lane's buffers under it.)
-    const uint64_t seq = ++b.seq;
-    b.lane[ln].running = true;
-    b.lane[ln].seq = seq;
+    const uint64_t seq = b.lanes.take(ln);  // under b.m (batch_lanes.hpp: why)
     // this leader's batch: the open packs sharing its dict, within the caps
     std::vector<BatchJob *> take;
     uint64_t bytes = 0, chunks = 0;
@@ -351,7 +337,7 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     }
     lk.lock();
     if (rc) {
-      b.lane[ln].running = false;  // drained above
+      b.lanes.drop(ln);  // drained above
     } else {
       ++b.batches;
       b.jobs += take.size();
@@ -370,11 +356,7 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
   const bool ok = hipEventSynchronize(j.done->ev) == hipSuccess;
   {
     std::lock_guard<std::mutex> g(b.m);  // the first pack back frees the lane for the next leader
-    BatchLane &l = b.lane[j.lane];
-    if (l.running && l.seq == j.seq) {
-      l.running = false;
-      b.cv.notify_all();
-    }
+    if (b.lanes.end(j.lane, j.seq)) b.cv.notify_all();
   }
   if (!ok) return fail(e, NGPU_EHIP, "batch: stream failed");
   return 0;
