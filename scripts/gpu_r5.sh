@@ -112,6 +112,12 @@ for s in "$@"; do
         ok $? "h2d $cfg"
       done
       cat "$OUT/h2d.jsonl" ;;
+    soak)
+      timeout -k 10 600 python3 -u scripts/gpu_soak.py --threads 16 40 0x50A6 > "$OUT/soak_threads.log" 2>&1
+      ok $? soak_threads
+      timeout -k 10 300 python3 -u scripts/gpu_soak.py 150 0x50A7 > "$OUT/soak_single.log" 2>&1
+      ok $? soak_single
+      tail -1 "$OUT/soak_threads.log"; tail -1 "$OUT/soak_single.log" ;;
     n4)
       NYDUS_NODE_EXTRA_DEVICES=0,0,0,0 timeout -k 10 900 python3 bench.py --gpus 4 --steps 5 --warmup 3 --dist-backend gloo --c4-layers 2 > "$OUT/bench_c2_n4_gloo.json" 2> "$OUT/bench_c2_n4_gloo.err"
       ok $? n4
