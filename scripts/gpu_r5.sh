@@ -84,6 +84,10 @@ for s in "$@"; do
       timeout -k 10 300 python3 bench.py --workload c1 --packs 32 --steps 10 --warmup 3 --packs-modes decisions --no-cpu-baseline > "$OUT/packs_eager_default.json" 2> "$OUT/packs_eager_default.err"
       ok $? "packs eager default"
       cat "$OUT/h2dp.jsonl" ;;
+    pstream)
+      timeout -k 10 300 python3 bench.py --workload c1 --packs 32 --steps 10 --warmup 3 --packs-modes decisions,stream_zstd,stream_zstd_no_batch > "$OUT/pstream_c1.json" 2> "$OUT/pstream_c1.err"
+      ok $? pstream_c1
+      python3 -c "import json; d=json.loads(open('$OUT/pstream_c1.json').read().strip().splitlines()[-1]); print({m: (v['gbs'], v.get('phases')) for m, v in d['modes'].items()}, d['cpu_baseline'].get('pipeline_gbs'))" ;;
     strace)
       NGPU_PACK_TRACE=1 NGPU_SINK_STATS=1 timeout -k 10 300 python3 bench.py --workload c1 --packs 32 --steps 2 --warmup 2 --packs-modes decisions,stream_zstd --no-cpu-baseline > "$OUT/strace_c1.json" 2> "$OUT/strace_c1.err"
       ok $? strace_c1
