@@ -199,8 +199,9 @@ struct ngpu_engine {
   bool tshare_open = false;
   hipEvent_t host_ev = nullptr;  // host_fence marker (system scope)
   std::vector<ngpu_staging_buf> staging_pool;  // guarded by pool_mu, <= kStagingPool
-  // 32 packs open at once keep their two slots; the pinned bytes kept are
-  // bounded too (64 default 256 MiB slots would pin 16 GiB)
+  // 128 packs open at once keep their two slots (bench.py --packs 128 with
+  // 16 MiB slots); the pinned bytes kept are bounded too (64 default 256 MiB
+  // slots would pin 16 GiB)
   static constexpr size_t kStagingPool = 256;
   static constexpr uint64_t kStagingPoolBytes = 8ull << 30;
   uint64_t staging_pool_bytes = 0;  // guarded by pool_mu
