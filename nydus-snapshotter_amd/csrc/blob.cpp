@@ -346,6 +346,9 @@ class Pool {
 struct Batch {
   std::unique_ptr<uint8_t[]> p;
   uint64_t cap = 0, n = 0;
+  // non-empty: the batch's stream bytes are these pieces, in order (into p
+  // or into caller memory that outlives the writer's finish), not p[0, n)
+  std::vector<std::pair<const uint8_t *, uint64_t>> seg;
   void resize(uint64_t k) {
     if (k > cap) {
       p.reset(new uint8_t[k]);
@@ -366,7 +369,8 @@ struct Batch {
 // are kept up to kCacheBytes.  Process-wide, never destroyed (no exit-time
 // teardown of idle threads).
 struct WriterCache {
-  static constexpr uint64_t kBufMax = 64ull << 20, kCacheBytes = 2ull << 30;
+  // (a batch buffer holds <= 64 MiB of input at compressBound: a bit over)
+  static constexpr uint64_t kBufMax = 80ull << 20, kCacheBytes = 2ull << 30;
   std::mutex m;
   std::vector<std::unique_ptr<Pool>> pools;
   std::vector<Batch> bufs;
@@ -582,9 +586,7 @@ struct BlobWriter::Impl {
   std::vector<uint8_t> cflag;
   uint64_t compressed_chunks = 0;
   uint64_t batches_added = 0;  // batches submitted by add()
-  // batch buffers: per-chunk scratch slots, compacted into an output batch
-  Batch scratch;  // from the cache at the first compressed batch
-  bool scratch_taken = false;
+  // per batch: each chunk's bound-sized slot of the batch buffer (slot_off)
   std::vector<uint64_t> slot_off;
   std::vector<uint64_t> clen;
   int rc = 0;
@@ -629,9 +631,18 @@ struct BlobWriter::Impl {
       g.unlock();
       int r = 0;
       if (!failed) {
-        blob_sha.update(b.data(), b.size());
+        if (b.seg.empty()) {
+          blob_sha.update(b.data(), b.size());
+        } else {
+          for (const auto &sg : b.seg) blob_sha.update(sg.first, sg.second);
+        }
         const auto t2 = clk::now();
-        r = emit(b.data(), b.size());
+        if (b.seg.empty()) {
+          r = emit(b.data(), b.size());
+        } else {
+          for (const auto &sg : b.seg)
+            if ((r = emit(sg.first, sg.second))) break;
+        }
         t_sha += std::chrono::duration<double>(t2 - t1).count();
         t_emit += std::chrono::duration<double>(clk::now() - t2).count();
       }
@@ -680,7 +691,6 @@ struct BlobWriter::Impl {
     qcv.notify_all();
     if (sink.joinable()) sink.join();
     WriterCache &wc = WriterCache::get();
-    wc.put_buf(std::move(scratch));
     for (Batch &b : free_bufs) wc.put_buf(std::move(b));
     for (Batch &b : q) wc.put_buf(std::move(b));
     const char *v = getenv("NGPU_SINK_STATS");
@@ -732,11 +742,11 @@ int BlobWriter::init() {
   return 0;
 }
 
-int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) {
+int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k, bool src_stable) {
   Impl &m = *im_;
   if (m.rc) return m.rc;
   const uint32_t kind = m.opt.compressor;
-  // batches of <= 64 MiB of input keep the scratch bounded (smaller first ones, below)
+  // batches of <= 64 MiB of input keep the buffers bounded (smaller first ones, below)
   uint64_t a = 0;
   while (a < k) {
     if (m.cancel && __atomic_load_n(m.cancel, __ATOMIC_RELAXED))
@@ -750,7 +760,15 @@ int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) 
     ++m.batches_added;
     const uint64_t nb = b - a;
     Batch out = m.take_buffer();
-    if (kind == NGPU_COMPRESSOR_NONE) {
+    out.seg.clear();
+    if (kind == NGPU_COMPRESSOR_NONE && src_stable) {  // the caller's bytes are the stream
+      out.resize(0);
+      for (uint64_t i = 0; i < nb; ++i) {
+        out.seg.emplace_back(src[a + i], len[a + i]);
+        m.csize.push_back(len[a + i]);
+        m.cflag.push_back(0);
+      }
+    } else if (kind == NGPU_COMPRESSOR_NONE) {
       out.resize(bytes);
       m.slot_off.resize(nb + 1);
       m.slot_off[0] = 0;
@@ -765,25 +783,23 @@ int BlobWriter::add(const uint8_t *const *src, const uint32_t *len, uint64_t k) 
       m.slot_off[0] = 0;
       for (uint64_t i = 0; i < nb; ++i)
         m.slot_off[i + 1] = m.slot_off[i] + compress_bound(kind, len[a + i]);
-      if (!m.scratch_taken) {  // one an earlier writer left, if any
-        (void)WriterCache::get().take_buf(&m.scratch);
-        m.scratch_taken = true;
-      }
-      m.scratch.resize(m.slot_off[nb]);
+      // every chunk compresses into its own bound-sized slot of the batch
+      // buffer, and the batch is the list of those pieces: no compaction
+      // copy.  A chunk that does not shrink is stored raw: a piece of the
+      // caller's memory when it outlives the writer (src_stable: the pinned
+      // staging slot of a one-slot layer), else copied into its slot (the
+      // blob windows' landing buffers are reused by the next window).
+      out.resize(m.slot_off[nb]);
       m.clen.assign(nb, 0);
       m.pool->run(nb, [&](uint64_t i) {
-        m.clen[i] = compress_one(kind, m.opt.level, src[a + i], len[a + i], &m.scratch[m.slot_off[i]],
+        m.clen[i] = compress_one(kind, m.opt.level, src[a + i], len[a + i], &out[m.slot_off[i]],
                                  m.slot_off[i + 1] - m.slot_off[i]);
+        if (!m.clen[i] && !src_stable) memcpy(&out[m.slot_off[i]], src[a + i], len[a + i]);
       });
-      uint64_t total = 0;
-      for (uint64_t i = 0; i < nb; ++i) total += m.clen[i] ? m.clen[i] : len[a + i];
-      out.resize(total);
-      uint64_t o = 0;
       for (uint64_t i = 0; i < nb; ++i) {
         const bool z = m.clen[i] != 0;
         const uint64_t c = z ? m.clen[i] : len[a + i];
-        memcpy(&out[o], z ? &m.scratch[m.slot_off[i]] : src[a + i], c);
-        o += c;
+        out.seg.emplace_back(z || !src_stable ? &out[m.slot_off[i]] : src[a + i], c);
         m.csize.push_back((uint32_t)c);
         m.cflag.push_back(z ? 1 : 0);
         m.compressed_chunks += z;

@@ -166,7 +166,9 @@ class BlobWriter {
   int init();  // loads the compressor; NGPU_EUNSUPP if unavailable
   // NEW chunks in index order (src[k] = host bytes of chunk with index
   // base+k).  The bytes may be reused as soon as the call returns.
-  int add(const uint8_t *const *src, const uint32_t *len, uint64_t k);
+  // src_stable: the k chunks' bytes stay valid and unchanged until finish()
+  // returns (then raw pieces are written from there, not copied)
+  int add(const uint8_t *const *src, const uint32_t *len, uint64_t k, bool src_stable = false);
   // Writes image.blob's header, blob.meta (v6), image.boot -- the inode tree
   // of `entries`, the layer tar's entries (tarstream.hpp) -- and the TOC (v6).
   int finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_t n,

@@ -252,6 +252,9 @@ void release(ngpu_pack *p) {
   DeviceGuard dg(e->device);
   ptrace(p, "release");
   emit_stop(p);
+  // the stream's writer goes first: its sink may still hold raw pieces of the
+  // pinned staging slots (src_stable, emit_range_host) until it has drained
+  if (p->em) p->em->bw.reset();
   for (Slot &s : p->slot) {
     if (s.done) (void)hipEventSynchronize(s.done);
   }
@@ -731,7 +734,9 @@ int emit_range_host(ngpu_pack *p, BlobWriter &bw, const ngpu_chunk *ch, const ui
   }
   if (new_out) *new_out += src.size();
   if (src.empty()) return 0;
-  if (int rc = bw.add(src.data(), len.data(), src.size())) return fail(p->e, rc, "pack: %s", ngpu_host_error());
+  // (src_stable: the slot stays this pack's until release, after the writer's finish)
+  if (int rc = bw.add(src.data(), len.data(), src.size(), true))
+    return fail(p->e, rc, "pack: %s", ngpu_host_error());
   return 0;
 }
 
