@@ -1378,7 +1378,8 @@ int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
       src.push_back(base + chunks[i].offset);
       lens.push_back(chunks[i].length);
     }
-    rc = bw.add(src.data(), lens.data(), src.size());
+    // (the caller's data outlives bw: raw chunks are written from it in place)
+    rc = bw.add(src.data(), lens.data(), src.size(), true);
     if (!rc) rc = bw.finish(chunks, results, n, *stats, entries, info);
     return rc;
   });

@@ -486,17 +486,20 @@ def test_blob_writer_threads_tsan(oracle, tars, tmp_path):
     no data race reported, and the stream is byte-equal to the regular
     build's for every compressor, with chunk-dict records in the bootstrap;
     four writers at once on the process-wide shared pool give that same
-    stream each."""
+    stream each, also under AddressSanitizer (raw chunks are written from the
+    caller's data in place, src_stable)."""
     import subprocess
     from conftest import ROOT
     from nydus_gpu._lib import NgpuLayerStats
     exe = str(tmp_path / "blob_tsan")
+    exe_asan = str(tmp_path / "blob_asan")
     csrc = os.path.join(ROOT, "nydus-snapshotter_amd", "csrc")
-    subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=thread",
-                           "-I", os.path.join(ROOT, "include"), "-I", csrc,
-                           os.path.join(ROOT, "tests", "cpp", "blob_tsan.cpp"),
-                           os.path.join(csrc, "blob.cpp"), os.path.join(csrc, "rafs.cpp"), "-o", exe, "-lcrypto", "-ldl",
-                           "-lpthread"])
+    srcs = [os.path.join(ROOT, "tests", "cpp", "blob_tsan.cpp"), os.path.join(csrc, "blob.cpp"),
+            os.path.join(csrc, "rafs.cpp")]
+    for san, out in (("thread", exe), ("address", exe_asan)):
+        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", f"-fsanitize={san}",
+                               "-I", os.path.join(ROOT, "include"), "-I", csrc] + srcs +
+                              ["-o", out, "-lcrypto", "-ldl", "-lpthread"])
     cs, tar = 0x10000, tars["alpine_like"]
     ch, res, st = cpu_results(oracle, tar, cs)
     tab = nydus_gpu.chunk_table(ch, res).view(rafs.CHUNK_INFO_DTYPE).reshape(-1)[::3].copy()
@@ -512,17 +515,19 @@ def test_blob_writer_threads_tsan(oracle, tars, tmp_path):
              "dc": np.ascontiguousarray(d["chunks"]).tobytes()}
     for k, v in files.items():
         (tmp_path / k).write_bytes(v)
-    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66")
-    runs = (("zstd", 2, 1), ("lz4_block", 4, 1), ("none", 1, 1), ("zstd", 2, 4))
-    for name, code, writers in runs:  # writers > 1: concurrent writers on the shared pool
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66",
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=0")
+    runs = (("zstd", 2, 1, exe), ("lz4_block", 4, 1, exe), ("none", 1, 1, exe), ("zstd", 2, 4, exe),
+            ("zstd", 2, 4, exe_asan), ("none", 1, 4, exe_asan))
+    for name, code, writers, prog in runs:  # writers > 1: concurrent writers on the shared pool
         env["BLOB_TSAN_WRITERS"] = str(writers)
         p = tmp_path / f"out-{name}"
-        r = subprocess.run([exe] + [str(tmp_path / k) for k in ("data", "ch", "res", "st")] +
+        r = subprocess.run([prog] + [str(tmp_path / k) for k in ("data", "ch", "res", "st")] +
                            [str(p), str(code), "8", str(cs), "0",
                             str(tmp_path / "db"), str(tmp_path / "dc")],
                            capture_output=True, text=True, env=env, timeout=300)
         assert r.returncode == 0, r.stderr[-3000:]
-        assert "ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
+        assert "ThreadSanitizer" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-3000:]
         ref = io.BytesIO()
         nydus_gpu.blob_write(tar, ch, res, st, ref, compressor=name, threads=8, chunk_size=cs,
                              dict_blobs=d["blobs"], dict_chunks=d["chunks"])
