@@ -19,11 +19,12 @@
 //
 // Window: the first pack to close leads; it waits until every pack open on
 // the engine has joined, or kWindowUs (SHA-256: kWindowShaUs), whichever
-// comes first (a lone pack
-// goes at once), and until one of the kLanes batch lanes is idle.  Batches on
-// different lanes run concurrently (each lane: its own stream, buffers and
-// workspace slot), so a small batch's chain latency -- a SHA-256 batch holds
-// the device ~21 ms whatever its size -- does not hold the next one back.
+// comes first (a lone pack goes at once), and until one of the kLanes batch
+// lanes is idle.  Batches on different lanes run concurrently (each lane: its
+// own stream, buffers and workspace slot), so a small batch's chain latency
+// -- a SHA-256 batch holds the device ~21-40 ms whatever its size -- does not
+// hold the next one back.  Each pack's results and stats are written into
+// its pinned read-back buffers by the lane's last two kernels.
 // Only packs whose layer fit one staging slot join (their bytes are all in
 // HBM at close); packs with another chunk dict than the leader's wait for
 // the next batch.  NGPU_FLAG_NO_BATCH turns it off.
