@@ -117,7 +117,7 @@ for s in "$@"; do
       done
       cat "$OUT/h2d.jsonl" ;;
     soak)
-      timeout -k 10 600 python3 -u scripts/gpu_soak.py --threads 16 40 20646 > "$OUT/soak_threads.log" 2>&1
+      timeout -k 10 600 python3 -u scripts/gpu_soak.py --threads ${SOAK_THREADS:-16} ${SOAK_CASES:-40} 20646 > "$OUT/soak_threads.log" 2>&1
       ok $? soak_threads
       timeout -k 10 300 python3 -u scripts/gpu_soak.py 150 20647 > "$OUT/soak_single.log" 2>&1
       ok $? soak_single
