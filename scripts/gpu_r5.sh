@@ -120,6 +120,12 @@ for s in "$@"; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-include-regex sha256_pair --output-format csv -d "$OUT/shaclk" -o pmc -- python3 "$ROOT/bench.py" --workload c1-sha256 --packs 32 --steps 3 --warmup 1 --packs-modes decisions --no-cpu-baseline > "$OUT/shaclk.log" 2>&1)
       ok $? shaclk
       python3 scripts/pmc_summary.py "$OUT/pmc_clock_packs_sha.json" sha256_pair "$OUT/shaclk" | cut -c1-400 ;;
+    shamix)
+      for f in 0 6144 10240; do
+        timeout -k 10 200 python3 tools/sha_mix.py $f >> "$OUT/sha_mix.jsonl" 2>> "$OUT/sha_mix.err"
+        ok $? "shamix $f"
+      done
+      cat "$OUT/sha_mix.jsonl" ;;
     soak)
       timeout -k 10 600 python3 -u scripts/gpu_soak.py --threads ${SOAK_THREADS:-16} ${SOAK_CASES:-40} 20646 > "$OUT/soak_threads.log" 2>&1
       ok $? soak_threads
