@@ -1,7 +1,8 @@
 """SHA-256 digest time of one launch by chunk mix (diagnostic, runs on the GPU
 box): is a 1 MiB chunk's chain slower when its workgroup also holds short
 chunks, or when its bytes are not 16-B aligned?  One JSON line per case:
-the digest stage's ms (HIP events, timing engine), median of 7 launches.
+one digest call's wall ms (enqueue + device sync; the kernel is ms long),
+median of 7 launches.
 
 usage: python3 tools/sha_mix.py [sha-mode flags value]
 """
@@ -9,6 +10,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "nydus-snapshotter_amd"), os.path.join(ROOT, "tests", "golden")):
@@ -28,10 +30,12 @@ def run(eng, data, chunks, reps=7):
     ch = torch.from_numpy(np.ascontiguousarray(chunks).view(np.uint8).copy()).cuda()
     out = torch.zeros(len(chunks) * nydus_gpu.RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
     ms = []
+    torch.cuda.synchronize()
     for _ in range(reps + 1):
+        t0 = time.perf_counter()
         eng.digest_device(d.data_ptr(), d.numel(), ch.data_ptr(), len(chunks), out.data_ptr())
-        torch.cuda.synchronize()
-        ms.append(eng.last_timing().get("digest_ms", eng.last_timing().get("total_ms")))
+        torch.cuda.synchronize()  # (device-wide: the engine's stream included)
+        ms.append((time.perf_counter() - t0) * 1e3)
     return round(statistics.median(ms[1:]), 3)
 
 
