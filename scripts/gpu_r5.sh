@@ -126,6 +126,14 @@ for s in "$@"; do
         ok $? "shamix $f"
       done
       cat "$OUT/sha_mix.jsonl" ;;
+    shaab)
+      timeout -k 10 200 python3 tools/sha_mix.py 0 > "$OUT/sha_mix_new.jsonl" 2>> "$OUT/sha_mix.err"
+      ok $? "shamix new"
+      timeout -k 10 400 python3 bench.py --workload c3 --steps 10 --no-cpu-baseline --no-dict-file > "$OUT/c3.json" 2> "$OUT/c3.err"
+      ok $? c3
+      timeout -k 10 300 python3 bench.py --workload c1-sha256 --packs 32 --steps 5 --warmup 2 --packs-modes decisions --no-cpu-baseline > "$OUT/packs_sha.json" 2> "$OUT/packs_sha.err"
+      ok $? packs_sha
+      cat "$OUT/sha_mix_new.jsonl"; python3 -c "import json; d=json.loads(open('$OUT/c3.json').read().strip().splitlines()[-1]); print('c3', d['value'], d['ms_per_step'], d['roofline']['frac'])"; python3 -c "import json; d=json.loads(open('$OUT/packs_sha.json').read().strip().splitlines()[-1]); print('packs_sha', d['value'], d['modes']['decisions']['device_gbs'])" ;;
     soak)
       timeout -k 10 600 python3 -u scripts/gpu_soak.py --threads ${SOAK_THREADS:-16} ${SOAK_CASES:-40} 20646 > "$OUT/soak_threads.log" 2>&1
       ok $? soak_threads
