@@ -341,29 +341,17 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
   }
   const uint32_t phases = (nbmax + 1) / 2;
 
-  // Schedule wave state: its next two blocks (b and b + 2: the lane makes
-  // every other block) in registers, loaded two phases ahead.  One phase of
-  // prefetch (~2.6 us of rounds) hid the load while many chains kept the
-  // memory busy (C3: 16,384 chains), not for a lone chain: a 1 MiB chunk
-  // alone took 25.8 ms and with 63 short neighbours 30.3, against 20.9 among
-  // 64 long ones (tools/sha_mix.py, profiles/r5/sha_mix_r5j3.jsonl) -- a small
-  // layer's or a small batch's longest chain.
+  // Schedule wave state: its next block (b + 2) prefetched into registers.
   const uint32_t full = len >> 6;
   const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
-  u32x4 pf0 = {}, pf1 = {}, pf2 = {}, pf3 = {};  // block b
-  u32x4 pn0 = {}, pn1 = {}, pn2 = {}, pn3 = {};  // block b + 2
-  bool have_pf = false, have_pn = false;
-  auto load4 = [&](uint32_t b, u32x4 &x0, u32x4 &x1, u32x4 &x2, u32x4 &x3) {
-    const bool ok = aligned && b < full;
-    if (ok) {
+  u32x4 pf0 = {}, pf1 = {}, pf2 = {}, pf3 = {};
+  bool have_pf = false;
+  auto prefetch = [&](uint32_t b) {
+    have_pf = aligned && b < full;
+    if (have_pf) {
       const u32x4 *q = reinterpret_cast<const u32x4 *>(p + 64ull * b);
-      x0 = q[0]; x1 = q[1]; x2 = q[2]; x3 = q[3];
+      pf0 = q[0]; pf1 = q[1]; pf2 = q[2]; pf3 = q[3];
     }
-    return ok;
-  };
-  auto prefetch = [&](uint32_t b) {  // the first two blocks of the lane
-    have_pf = load4(b, pf0, pf1, pf2, pf3);
-    have_pn = load4(b + 2, pn0, pn1, pn2, pn3);
   };
   auto produce = [&](uint32_t b, int set) {
     if (b >= nb) return;
@@ -377,9 +365,7 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
     } else {
       sha_load_block(p, len, b, w);
     }
-    pf0 = pn0; pf1 = pn1; pf2 = pn2; pf3 = pn3;  // block b + 2 moves up,
-    have_pf = have_pn;
-    have_pn = load4(b + 4, pn0, pn1, pn2, pn3);  // block b + 4 is requested
+    prefetch(b + 2);
     u32x4 *dst = kw[set][half][ci];
     u32x4 q;
 #pragma unroll
@@ -419,7 +405,12 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
     if (rounds) {
 #pragma unroll 1
       for (uint32_t hb = 0; hb < 2; ++hb) {
-        if (2 * ph + hb < nb) {
+        // every lane runs the rounds while any lane of the wave has a block
+        // (a lane past its chunk's end computes on stale words and keeps its
+        // H): a lone long chain among finished lanes ran ~25 % slower with
+        // them masked off (tools/sha_mix.py, profiles/r5/sha_mix_r5j3.jsonl)
+        const bool mine = 2 * ph + hb < nb;
+        if (__any(mine)) {
           u32x4 kv[16];
 #pragma unroll
           for (int j = 0; j < 16; ++j) kv[j] = kw[set][hb][kcol][j];
@@ -445,8 +436,10 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
             P3 = P2; P2 = P1; P1 = P0; P0 = X;
             if (it == 63) { F0 = P0; F1 = P1; F2 = P2; F3 = P3; }  // E lane final e,f,g,h
           }
-          H0 += side ? P0 : F0; H1 += side ? P1 : F1;
-          H2 += side ? P2 : F2; H3 += side ? P3 : F3;
+          if (mine) {
+            H0 += side ? P0 : F0; H1 += side ? P1 : F1;
+            H2 += side ? P2 : F2; H3 += side ? P3 : F3;
+          }
         }
       }
     } else {
