@@ -1312,7 +1312,7 @@ def packs_bench(args):
                                  "pageable memory"},
             "modes": modes, "cpu_baseline": cpu,
             "bound": "blake3: PCIe H2D of the tars through 2 shared copy lanes (~45 GB/s, "
-                     "tools/h2d_streams); sha256: one 1 MiB chunk's chain per batch (21-40 ms) "
+                     "tools/h2d_streams); sha256: one 1 MiB chunk's chain per batch (~21 ms) "
                      "whatever its size; stream: host zstd level 1 on the 16-core quota"}
     if cpu:
         line["speedup_vs_cpu"] = round(modes["decisions"]["gbs"] / cpu["value"], 2)

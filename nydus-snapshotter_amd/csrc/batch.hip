@@ -22,7 +22,7 @@
 // comes first (a lone pack goes at once), and until one of the kLanes batch
 // lanes is idle.  Batches on different lanes run concurrently (each lane: its
 // own stream, buffers and workspace slot), so a small batch's chain latency
-// -- a SHA-256 batch holds the device ~21-40 ms whatever its size -- does not
+// -- a SHA-256 batch holds the device ~21 ms whatever its size -- does not
 // hold the next one back.  Each pack's results and stats are written into
 // its pinned read-back buffers by the lane's last two kernels.
 // Only packs whose layer fit one staging slot join (their bytes are all in
