@@ -126,6 +126,12 @@ for s in "$@"; do
         ok $? "shamix $f"
       done
       cat "$OUT/sha_mix.jsonl" ;;
+    c1ab)
+      for i in 1 2; do
+        timeout -k 10 300 python3 bench.py --workload c1 --steps 400 --no-sub --no-cpu-baseline --no-e2e > "$OUT/c1_$i.json" 2> "$OUT/c1_$i.err"
+        ok $? "c1 $i"
+        python3 -c "import json; d=json.loads(open('$OUT/c1_$i.json').read().strip().splitlines()[-1]); print('c1', d['value'], d['ms_per_step'], d['stage_ms'])"
+      done ;;
     shaab)
       timeout -k 10 200 python3 tools/sha_mix.py 0 > "$OUT/sha_mix_new.jsonl" 2>> "$OUT/sha_mix.err"
       ok $? "shamix new"
