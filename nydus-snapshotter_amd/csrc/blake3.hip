@@ -1068,22 +1068,14 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
             const uint32_t pi = qid + s * kTreeQuads;
-            // a wave that holds any parent of the level runs all its quads:
-            // the quads past p compress parent p - 1 again and store nothing
-            // (the narrow levels' dependent chains ran slower with the rest
-            // of the wave masked off; SHA-256 round waves showed the same)
-            const bool mine = pi < p;
-            if (__any(mine)) {
-              const uint32_t pj = mine ? pi : p - 1;
+            if (pi < p) {
               uint32_t m[28];
 #pragma unroll
-              for (int k2 = 0; k2 < 28; ++k2) m[k2] = t[16 * pj + wo[k2]];
+              for (int k2 = 0; k2 < 28; ++k2) m[k2] = t[16 * pi + wo[k2]];
               uint32_t rx = ivq, ry = ivh;
               compress_quad(rx, ry, m, ivq, dq);
-              if (mine) {
-                o[8 * pi + qlane] = rx;
-                o[8 * pi + 4 + qlane] = ry;
-              }
+              o[8 * pi + qlane] = rx;
+              o[8 * pi + 4 + qlane] = ry;
             }
           }
           if ((cnt & 1) && tid < 8) o[8 * p + tid] = t[8 * (cnt - 1) + tid];  // odd tail promoted
