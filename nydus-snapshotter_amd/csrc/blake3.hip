@@ -834,11 +834,7 @@ __device__ __forceinline__ void quad_leaf(const uint8_t *__restrict__ data, cons
   }
 #pragma unroll
   for (uint32_t b = 0; b < 16; ++b) {
-    // the wave runs block b while any of its quads has one; a quad past its
-    // leaf's end compresses stale words and keeps its chaining value (with
-    // those lanes masked off, SHA-256's lone chains ran 25-45 % slower)
-    const bool mine = b < nb;
-    if (!__any(mine)) continue;  // (not break: keeps the loop unrolled, wb in registers)
+    if (b >= nb) continue;  // (not break: keeps the loop unrolled, wb in registers)
     const u32x4 w = wb[b];
 #else
   u32x4 w = load16(src, valid(0));
@@ -857,12 +853,8 @@ __device__ __forceinline__ void quad_leaf(const uint8_t *__restrict__ data, cons
     const uint32_t flags = (b == 0 ? CHUNK_START : 0u) |
                            (b + 1 == nb ? (CHUNK_END | (root_group ? ROOT : 0u)) : 0u);
     const uint32_t dq = q == 0 ? j : q == 1 ? 0u : q == 2 ? bl : flags;
-#if B3_QUAD_PF
-    uint32_t cx = x, cy = y;
-    compress_quad(cx, cy, m, ivq, dq);
-    if (mine) x = cx, y = cy;
-#else
     compress_quad(x, y, m, ivq, dq);
+#if !B3_QUAD_PF
     w = nx;
 #endif
   }
