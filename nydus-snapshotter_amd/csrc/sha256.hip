@@ -295,6 +295,10 @@ __global__ __launch_bounds__(256) void sha256_lane(
 // in LDS; chunk row 32 holds the constant 1 the A lanes add (~x + 1 = -x).
 constexpr uint32_t kDppRowRor8 = 0x128;
 
+#ifndef NGPU_SHA_UNIFORM
+#define NGPU_SHA_UNIFORM 1  // round waves run wave-uniform (see the round loop)
+#endif
+
 // R round waves + R schedule waves per workgroup (R groups of 32 chunks), so
 // one workgroup per CU puts every wave on its own SIMD.
 template <int R>
@@ -410,7 +414,11 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
         // H): a lone long chain among finished lanes ran ~25 % slower with
         // them masked off (tools/sha_mix.py, profiles/r5/sha_mix_r5j3.jsonl)
         const bool mine = 2 * ph + hb < nb;
+#if NGPU_SHA_UNIFORM
         if (__any(mine)) {
+#else  // (A/B build only: lanes masked off as before round 5)
+        if (mine) {
+#endif
           u32x4 kv[16];
 #pragma unroll
           for (int j = 0; j < 16; ++j) kv[j] = kw[set][hb][kcol][j];
