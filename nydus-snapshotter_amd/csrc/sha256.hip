@@ -295,13 +295,13 @@ __global__ __launch_bounds__(256) void sha256_lane(
 // in LDS; chunk row 32 holds the constant 1 the A lanes add (~x + 1 = -x).
 constexpr uint32_t kDppRowRor8 = 0x128;
 
-#ifndef NGPU_SHA_UNIFORM
-#define NGPU_SHA_UNIFORM 1  // round waves run wave-uniform (see the round loop)
-#endif
-
 // R round waves + R schedule waves per workgroup (R groups of 32 chunks), so
-// one workgroup per CU puts every wave on its own SIMD.
-template <int R>
+// one workgroup per CU puts every wave on its own SIMD.  U: the round waves
+// run wave-uniform (see the round loop) -- for calls of few chunks, whose
+// longest chain shares its wave with finished or absent chunks; a call of
+// many equal chunks keeps every lane busy and runs 3 % faster masked (C3:
+// 21.4 vs 22.1 ms, same box, alternated twice; profiles/r5/c3_sha_uniform_ab_r5p2.log).
+template <int R, bool U>
 __global__ __launch_bounds__(128 * R) void sha256_pair(
     const uint8_t *__restrict__ data, uint64_t data_len,
     const ngpu_chunk *__restrict__ chunks, uint64_t n,
@@ -414,11 +414,7 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
         // H): a lone long chain among finished lanes ran ~25 % slower with
         // them masked off (tools/sha_mix.py, profiles/r5/sha_mix_r5j3.jsonl)
         const bool mine = 2 * ph + hb < nb;
-#if NGPU_SHA_UNIFORM
-        if (__any(mine)) {
-#else  // (A/B build only: lanes masked off as before round 5)
-        if (mine) {
-#endif
+        if (U ? __any(mine) : mine) {
           u32x4 kv[16];
 #pragma unroll
           for (int j = 0; j < 16; ++j) kv[j] = kw[set][hb][kcol][j];
@@ -464,6 +460,8 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
 
 }  // namespace
 
+constexpr uint64_t kShaUniformBelow = 4096;  // chunks per call (sha256_pair U)
+
 void launch_sha256(const uint8_t *data, uint64_t data_len,
                    const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
                    uint64_t *err, int variant, hipStream_t s) {
@@ -484,16 +482,25 @@ void launch_sha256(const uint8_t *data, uint64_t data_len,
   }
   if (variant >= 1) {
     const dim3 g2((unsigned)((n + 63) / 64)), g1((unsigned)((n + 31) / 32));
+    // wave-uniform round waves below 4,096 chunks: small layers and small
+    // batches (a lone long chain ran 25-45 % slower among masked lanes)
+    const bool few = n < kShaUniformBelow;
     switch (variant) {
       case 4:  // one group per workgroup
-        hipLaunchKernelGGL((sha256_pair<1>), g1, dim3(128), 0, s, data, data_len, chunks, n, out, err);
+        if (few)
+          hipLaunchKernelGGL((sha256_pair<1, true>), g1, dim3(128), 0, s, data, data_len, chunks, n, out, err);
+        else
+          hipLaunchKernelGGL((sha256_pair<1, false>), g1, dim3(128), 0, s, data, data_len, chunks, n, out, err);
         break;
       case 5:  // four groups per workgroup: a round and a schedule wave share each SIMD
-        hipLaunchKernelGGL((sha256_pair<4>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0, s,
+        hipLaunchKernelGGL((sha256_pair<4, false>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0, s,
                            data, data_len, chunks, n, out, err);
         break;
       default:
-        hipLaunchKernelGGL((sha256_pair<2>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
+        if (few)
+          hipLaunchKernelGGL((sha256_pair<2, true>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
+        else
+          hipLaunchKernelGGL((sha256_pair<2, false>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
     }
     return;
   }

@@ -132,13 +132,6 @@ for s in "$@"; do
         ok $? "c1 $i"
         python3 -c "import json; d=json.loads(open('$OUT/c1_$i.json').read().strip().splitlines()[-1]); print('c1', d['value'], d['ms_per_step'], d['stage_ms'])"
       done ;;
-    c3ab)
-      for v in new mask new mask; do
-        if [ $v = mask ]; then L="$ROOT/nydus-snapshotter_amd/build/abx/shamask.so"; else L="$ROOT/nydus-snapshotter_amd/libnydusgpu.so"; fi
-        NYDUS_GPU_LIB=$L timeout -k 10 300 python3 bench.py --workload c3 --steps 10 --no-cpu-baseline --no-dict-file --no-e2e > "$OUT/c3_$v.json" 2> "$OUT/c3_$v.err"
-        ok $? "c3 $v"
-        python3 -c "import json; d=json.loads(open('$OUT/c3_$v.json').read().strip().splitlines()[-1]); print('c3 $v', d['value'], d['ms_per_step'])"
-      done ;;
     shaab)
       timeout -k 10 200 python3 tools/sha_mix.py 0 > "$OUT/sha_mix_new.jsonl" 2>> "$OUT/sha_mix.err"
       ok $? "shamix new"
