@@ -124,6 +124,11 @@ constexpr int kWindowUs = 250;
 // saves a whole chain time for every pack it adds (32 C1 packs closing over
 // ~3 ms went out as 4-5 batches in 250 µs windows).
 constexpr int kWindowShaUs = 2000;
+// ... and each pack that joins restarts it, up to this much after the lead:
+// 32 C1 packs join over ~7 ms behind the shared H2D lanes, so a fixed 2 ms
+// window split them into 2-4 batches whose chains did not overlap
+// (37-42 ms a round against one chain's 21 ms)
+constexpr int kWindowShaCapUs = 12000;
 constexpr size_t kMaxJobs = 256;
 constexpr uint64_t kMaxBytes = 1ull << 30;
 constexpr uint64_t kMaxChunks = 1ull << 20;
@@ -291,12 +296,20 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     // wait for the open packs to join -- until all have, or kWindowUs has
     // passed -- and for an idle lane (while every lane runs a batch, a new
     // one would only queue behind them: better to let more packs join it)
-    const int window = e->cfg.digester == NGPU_DIGEST_SHA256 ? kWindowShaUs : kWindowUs;
-    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(window);
+    const bool sha = e->cfg.digester == NGPU_DIGEST_SHA256;
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto window = std::chrono::microseconds(sha ? kWindowShaUs : kWindowUs);
+    const auto cap = t0 + std::chrono::microseconds(sha ? kWindowShaCapUs : kWindowUs);
+    auto until = t0 + window;
+    size_t joined = b.open.size();
     int ln = -1;
     for (;;) {
       ln = b.lanes.idle();
       const bool all_in = b.open.size() >= (size_t)e->open_packs.load() || b.open.size() >= kMaxJobs;
+      if (sha && b.open.size() > joined) {  // a pack joined: restart the window
+        joined = b.open.size();
+        until = std::min(cap, std::chrono::steady_clock::now() + window);
+      }
       if (ln >= 0 && (all_in || std::chrono::steady_clock::now() >= until)) break;
       if (ln >= 0)
         b.cv.wait_until(lk, until);

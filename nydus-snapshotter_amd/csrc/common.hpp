@@ -208,9 +208,10 @@ bool blake3_planned_in_leaves(uint64_t n, uint64_t data_len, int group_log2, con
 // Leaves + chunks up to which D = 0 calls hash one leaf per lane quad.
 uint64_t blake3_quad_max_leaves();
 // sha256.hip
+// mixed: the chunks' lengths vary (round waves run wave-uniform, sha256_pair U)
 void launch_sha256(const uint8_t *data, uint64_t data_len,
                    const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
-                   uint64_t *err, int variant, hipStream_t s);
+                   uint64_t *err, int variant, bool mixed, hipStream_t s);
 
 // One chunk-dict entry in HBM (64 B, 64-B aligned): the key and every field
 // a hit returns, so a probe that hits reads one hash-slot line and one record

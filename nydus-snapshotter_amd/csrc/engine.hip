@@ -307,7 +307,12 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
     // tuning override: flags bits 11..13 = 1 + SHA-256 variant (0 split,
     // 1 pair, 2 lane, 4/5 pair layouts)
     const uint32_t sv = (e->cfg.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7;
-    launch_sha256(d_data, len, d_chunks, n, d_out, ws.stats + kStBadDesc, sv ? (int)sv - 1 : -1, s);
+    // mixed lengths unless the data averages >= 15/16 of a full chunk per
+    // chunk and fills every 32-chunk wave (a raw stream cut at chunk_size,
+    // C3); tar layers and batches mix file-sized chunks with full ones
+    const bool mixed = n % 32 != 0 || len < n * (uint64_t)e->cfg.chunk_size / 16 * 15;
+    launch_sha256(d_data, len, d_chunks, n, d_out, ws.stats + kStBadDesc, sv ? (int)sv - 1 : -1,
+                  mixed, s);
     snprintf(e->cur->path, sizeof e->cur->path, "sha256 variant %d, %llu chunks",
              sv ? (int)sv - 1 : -1, (unsigned long long)n);
     if (tm) {

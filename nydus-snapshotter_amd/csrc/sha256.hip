@@ -297,9 +297,9 @@ constexpr uint32_t kDppRowRor8 = 0x128;
 
 // R round waves + R schedule waves per workgroup (R groups of 32 chunks), so
 // one workgroup per CU puts every wave on its own SIMD.  U: the round waves
-// run wave-uniform (see the round loop) -- for calls of few chunks, whose
-// longest chain shares its wave with finished or absent chunks; a call of
-// many equal chunks keeps every lane busy and runs 3 % faster masked (C3:
+// run wave-uniform (see the round loop) -- for calls of mixed chunk lengths,
+// whose long chains share their waves with finished chunks; a call of
+// equal chunks keeps every lane busy and runs 3 % faster masked (C3:
 // 21.4 vs 22.1 ms, same box, alternated twice; profiles/r5/c3_sha_uniform_ab_r5p2.log).
 template <int R, bool U>
 __global__ __launch_bounds__(128 * R) void sha256_pair(
@@ -460,11 +460,9 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
 
 }  // namespace
 
-constexpr uint64_t kShaUniformBelow = 4096;  // chunks per call (sha256_pair U)
-
 void launch_sha256(const uint8_t *data, uint64_t data_len,
                    const ngpu_chunk *chunks, uint64_t n, ngpu_result *out,
-                   uint64_t *err, int variant, hipStream_t s) {
+                   uint64_t *err, int variant, bool mixed, hipStream_t s) {
   if (n == 0) return;
   // Auto (same-box sweep, profiles/r2/sha_variants_lane_r2sl.jsonl, GB/s):
   //  * <= 16384 chunks (one 64-chunk workgroup per CU): two lanes per chunk,
@@ -482,9 +480,9 @@ void launch_sha256(const uint8_t *data, uint64_t data_len,
   }
   if (variant >= 1) {
     const dim3 g2((unsigned)((n + 63) / 64)), g1((unsigned)((n + 31) / 32));
-    // wave-uniform round waves below 4,096 chunks: small layers and small
-    // batches (a lone long chain ran 25-45 % slower among masked lanes)
-    const bool few = n < kShaUniformBelow;
+    // wave-uniform round waves unless the chunks are (nearly) all full-size:
+    // a long chain among short neighbours ran 25-45 % slower masked
+    const bool few = mixed;
     switch (variant) {
       case 4:  // one group per workgroup
         if (few)

@@ -26,7 +26,9 @@ MiB = 1 << 20
 
 
 def run(eng, data, chunks, reps=7):
-    d = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).cuda()
+    # the buffer ends at the last chunk's end, as a layer's data would
+    end = int((chunks["offset"] + chunks["length"]).max())
+    d = torch.from_numpy(np.frombuffer(data, np.uint8)[:end].copy()).cuda()
     ch = torch.from_numpy(np.ascontiguousarray(chunks).view(np.uint8).copy()).cuda()
     out = torch.zeros(len(chunks) * nydus_gpu.RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
     ms = []
