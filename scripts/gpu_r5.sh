@@ -61,6 +61,10 @@ for s in "$@"; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c2 -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-sub > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err")
       ok $? stats
       python3 scripts/prof_agree.py "$OUT/prof" b3_groups "$OUT/prof_bench.json" "$OUT/rocprof_c2_agreement.json" | cut -c1-200 ;;
+    stats3)
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof3" -o c3 -- python3 "$ROOT/bench.py" --workload c3 --steps 10 --no-cpu-baseline --no-e2e --no-dict-file > "$OUT/prof3_bench.json" 2> "$OUT/prof3_bench.err")
+      ok $? stats3
+      python3 scripts/prof_agree.py "$OUT/prof3" sha256_pair "$OUT/prof3_bench.json" "$OUT/rocprof_c3_agreement.json" | cut -c1-200 ;;
     c3)
       df -h /tmp "$ROOT" /dev/shm > "$OUT/df.txt" 2>&1 || true
       timeout -k 10 600 python3 bench.py --workload c3 --steps 10 --no-cpu-baseline > "$OUT/c3.json" 2> "$OUT/c3.err"
