@@ -130,7 +130,7 @@ constexpr int kWindowShaUs = 2000;
 // (37-42 ms a round against one chain's 21 ms)
 constexpr int kWindowShaCapUs = 12000;
 constexpr size_t kMaxJobs = 256;
-constexpr uint64_t kMaxBytes = 1ull << 30;
+constexpr uint64_t kMaxBytes = 2ull << 30;  // a lane buffer (4 lanes: 8 GiB of HBM at most)
 constexpr uint64_t kMaxChunks = 1ull << 20;
 
 // A lane buffer of at least `want` elements (powers of two).  Stream-ordered
