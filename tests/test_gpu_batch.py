@@ -91,6 +91,41 @@ def test_32_concurrent_c1_packs_share_launch_sets(oracle, digester):
     assert bs["packs"] <= 32
 
 
+def _big_layer(seed):
+    """~49 MiB (one 64 MiB staging slot): two 20 MiB files (one shared by every layer: per-layer NEW
+    semantics across a batch), 300 small files with in-layer duplicates."""
+    rng = np.random.default_rng(seed)
+    shared = np.random.default_rng(1).integers(0, 256, 20 << 20, dtype=np.uint8).tobytes()
+    t = layers._TarBuilder()
+    t.dir("d")
+    t.file("d/shared.bin", shared)
+    t.file("d/own.bin", rng.integers(0, 256, 20 << 20, dtype=np.uint8).tobytes())
+    small = [rng.integers(0, 256, int(rng.integers(1, 60_000)), dtype=np.uint8).tobytes()
+             for _ in range(150)]
+    for i in range(300):
+        t.file(f"d/s{i}", small[i % 150])
+    return t.bytes()
+
+
+def test_sha256_batch_beyond_one_gib(oracle):
+    """24 layers of ~49 MiB (1.15 GiB) closed together on a sha256 engine:
+    batches may now hold 2 GiB (csrc/batch.hip kMaxBytes), so a launch set
+    can cover more than 1 GiB of gathered layers (r5x2: one batch of all 24,
+    1.14 GiB).  Every layer equals the oracle."""
+    S = 0x100000
+    tars = [_big_layer(0xB16 + i) for i in range(24)]
+    eng = nydus_gpu.Engine(device=0, digester="sha256", chunk_size=S, staging_bytes=64 << 20)
+    try:
+        got = _run_packs(eng, tars)
+        bs = eng.batch_stats()
+    finally:
+        eng.close()
+    for t, g in zip(tars, got):
+        _check(oracle, t, S, "sha256", g)
+    print("batch_stats", bs, "layer MiB", round(len(tars[0]) / 2**20, 1))
+    assert bs["packs"] >= 2 and bs["max_packs"] >= 2, bs
+
+
 def test_batched_packs_against_a_chunk_dict(oracle, tars):
     """The same layer set against one ChunkDict (records of a packed layer,
     planted into half of the others): DICT decisions, blob order and the
