@@ -55,6 +55,7 @@ struct BatchEvent {
 // has ended).
 struct BatchLane {
   hipStream_t s = nullptr;
+  double mark[6] = {};  // NGPU_BATCH_TRACE: launch_batch's steps (µs, batch_now_us)
   uint8_t *d_data = nullptr;
   uint64_t data_cap = 0;
   ngpu_chunk *d_ch = nullptr;
@@ -82,6 +83,9 @@ struct Batcher {
   uint64_t batches = 0, jobs = 0, max_jobs = 0;
 };
 
+static bool batch_trace_on();
+static double batch_now_us();
+
 namespace {
 
 // One layer's results out of the batch: a multi-layer call numbers chunks
@@ -105,6 +109,34 @@ __global__ void batch_results_out(const ngpu_result *__restrict__ src, uint64_t 
   ngpu_result r = src[i];
   if (r.kind == NGPU_NEW || r.kind == NGPU_INTRA) r.ref -= base;
   dst[lo][i - base] = r;
+}
+
+// The batch's inputs in ONE launch (row y = blockIdx.y): rows 0..K-1 copy the
+// layers' staged bytes into the lane buffer, the last rows the host-built
+// tables (chunk table, layer firsts, result pointers) straight from mapped
+// pinned memory.  32+ hipMemcpyAsync calls per batch stalled the leader's
+// enqueue for ~8 ms on every other round (NGPU_BATCH_TRACE steps, r5tr): the
+// copy engines are busy with the next packs' H2D.  A row's bytes move in
+// 16-B words when both ends are 16-B aligned, else bytewise.
+struct GatherRow {
+  const uint8_t *src;
+  uint8_t *dst;
+  uint64_t len;
+};
+
+__global__ __launch_bounds__(256) void batch_gather(const GatherRow *__restrict__ rows) {
+  const GatherRow r = rows[blockIdx.y];
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t head = 0;
+  if ((((uintptr_t)r.src | (uintptr_t)r.dst) & 15) == 0) {
+    const uint64_t w = r.len / 16;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(r.src);
+    uint4 *d4 = reinterpret_cast<uint4 *>(r.dst);
+    for (uint64_t i = t; i < w; i += stride) d4[i] = s4[i];
+    head = w * 16;
+  }
+  for (uint64_t i = head + t; i < r.len; i += stride) r.dst[i] = r.src[i];
 }
 
 // Each layer's stats into its pack's pinned read-back words (block k: layer k):
@@ -132,6 +164,9 @@ constexpr int kWindowShaCapUs = 12000;
 constexpr size_t kMaxJobs = 256;
 constexpr uint64_t kMaxBytes = 2ull << 30;  // a lane buffer (4 lanes: 8 GiB of HBM at most)
 constexpr uint64_t kMaxChunks = 1ull << 20;
+// a lane's buffers and workspace start at these sizes (4 lanes: ~1.1 GiB of HBM)
+constexpr uint64_t kLaneBytesMin = 256ull << 20;
+constexpr uint64_t kLaneChunksMin = 1ull << 16;
 
 // A lane buffer of at least `want` elements (powers of two).  Stream-ordered
 // on the lane's own stream from the engine's pool: hipFree would wait for the
@@ -161,7 +196,9 @@ int grow_dev(ngpu_engine *e, hipStream_t s, T **p, uint64_t &cap, uint64_t want)
 
 // Enqueue one batch on an idle lane (the leader, e->mu taken here).
 int launch_batch(ngpu_engine *e, BatchLane &b, const std::vector<BatchJob *> &jobs) {
+  const bool tr = batch_trace_on();
   std::lock_guard<std::mutex> g(e->mu);
+  if (tr) b.mark[0] = batch_now_us();
   DeviceGuard dg(e->device);
   if (!b.s) {
     HIP_TRY(e, hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking));
@@ -181,16 +218,20 @@ int launch_batch(ngpu_engine *e, BatchLane &b, const std::vector<BatchJob *> &jo
     first[k + 1] = first[k] + jobs[k]->n;
   }
   const uint64_t N = first[K];
-  if (int rc = grow_dev(e, b.s, &b.d_data, b.data_cap, bytes + 64)) return rc;
-  if (int rc = grow_dev(e, b.s, &b.d_ch, b.ch_cap, N + 1)) return rc;
-  if (int rc = grow_dev(e, b.s, &b.d_res, b.res_cap, N + 1)) return rc;
+  // floors: batches vary in size from one to the next, and each regrowth (or
+  // workspace growth below) held a leader's enqueue for 1-8 ms (r5g3 trace)
+  if (int rc = grow_dev(e, b.s, &b.d_data, b.data_cap, std::max<uint64_t>(bytes + 64, kLaneBytesMin))) return rc;
+  if (int rc = grow_dev(e, b.s, &b.d_ch, b.ch_cap, std::max<uint64_t>(N + 1, kLaneChunksMin))) return rc;
+  if (int rc = grow_dev(e, b.s, &b.d_res, b.res_cap, std::max<uint64_t>(N + 1, kLaneChunksMin))) return rc;
   if (int rc = grow_dev(e, b.s, &b.d_lfirst, b.l_cap, K + 2)) return rc;
   if (int rc = grow_dev(e, b.s, &b.d_lst, b.lst_cap, K + 2)) return rc;
   if (int rc = grow_dev(e, b.s, &b.d_dst, b.dst_cap, 2 * K + 2)) return rc;
-  const uint64_t tab = N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t) + 2 * K * sizeof(void *);
+  const uint64_t tab_data = N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t) + 2 * K * sizeof(void *);
+  const uint64_t rows_at = (tab_data + 15) & ~15ull;
+  const uint64_t tab = rows_at + (K + 3) * sizeof(GatherRow);
   if (tab > b.h_cap) {
     if (b.h_tab) (void)hipHostFree(b.h_tab), b.h_tab = nullptr, b.h_cap = 0;
-    uint64_t c = 64 << 10;
+    uint64_t c = 4 << 20;
     while (c < tab) c *= 2;
     HIP_TRY(e, hipHostMalloc((void **)&b.h_tab, c, hipHostMallocDefault));
     b.h_cap = c;
@@ -208,23 +249,36 @@ int launch_batch(ngpu_engine *e, BatchLane &b, const std::vector<BatchJob *> &jo
     HIP_TRY(e, hipHostGetDevicePointer(&hd[k], jobs[k]->h_res, 0));
     HIP_TRY(e, hipHostGetDevicePointer(&hd[K + k], jobs[k]->h_stats, 0));
   }
-  // gather: every layer's bytes behind its own copy
+  if (tr) b.mark[1] = batch_now_us();
+  // gather: every layer's bytes behind its own copy, and the tables, in one
+  // launch (batch_gather)
+  uint8_t *tab_dev = nullptr;  // h_tab as the device sees it
+  HIP_TRY(e, hipHostGetDevicePointer((void **)&tab_dev, b.h_tab, 0));
+  GatherRow *rows = reinterpret_cast<GatherRow *>(b.h_tab + rows_at);
+  uint64_t most = 0;
   for (uint64_t k = 0; k < K; ++k) {
     HIP_TRY(e, hipStreamWaitEvent(b.s, jobs[k]->ready, 0));
-    if (jobs[k]->len)
-      HIP_TRY(e, hipMemcpyAsync(b.d_data + off[k], jobs[k]->d_data, jobs[k]->len,
-                                hipMemcpyDeviceToDevice, b.s));
+    rows[k] = GatherRow{jobs[k]->d_data, b.d_data + off[k], jobs[k]->len};
+    most = std::max(most, jobs[k]->len);
   }
-  if (N)
-    HIP_TRY(e, hipMemcpyAsync(b.d_ch, b.h_tab, N * sizeof(ngpu_chunk), hipMemcpyHostToDevice, b.s));
-  HIP_TRY(e, hipMemcpyAsync(b.d_lfirst, b.h_tab + N * sizeof(ngpu_chunk), (K + 1) * sizeof(uint64_t),
-                            hipMemcpyHostToDevice, b.s));
-  HIP_TRY(e, hipMemcpyAsync(b.d_dst, hd, 2 * K * sizeof(void *), hipMemcpyHostToDevice, b.s));
+  rows[K] = GatherRow{tab_dev, reinterpret_cast<uint8_t *>(b.d_ch), N * sizeof(ngpu_chunk)};
+  rows[K + 1] = GatherRow{tab_dev + N * sizeof(ngpu_chunk), reinterpret_cast<uint8_t *>(b.d_lfirst),
+                          (K + 1) * sizeof(uint64_t)};
+  rows[K + 2] = GatherRow{tab_dev + N * sizeof(ngpu_chunk) + (K + 1) * sizeof(uint64_t),
+                          reinterpret_cast<uint8_t *>(b.d_dst), 2 * K * sizeof(void *)};
+  most = std::max(most, N * sizeof(ngpu_chunk));
+  // blocks per row: one 16-B word per thread per pass, at most 1,024 blocks
+  const uint64_t bx = std::min<uint64_t>(1024, std::max<uint64_t>(1, (most / 16 + 255) / 256));
+  hipLaunchKernelGGL(batch_gather, dim3((unsigned)bx, (unsigned)(K + 3)), dim3(256), 0, b.s,
+                     reinterpret_cast<const GatherRow *>(tab_dev + rows_at));
+  HIP_TRY(e, hipGetLastError());
+  if (tr) b.mark[2] = batch_now_us();
   // the lane's own workspace sized with headroom (powers of two), so batches
   // of varying size seldom regrow it
   {
     use_slot(e, b.s);
-    const uint64_t n2 = next_pow2(N + 1), len2 = next_pow2(bytes + 1);
+    const uint64_t n2 = next_pow2(std::max<uint64_t>(N + 1, kLaneChunksMin)),
+                   len2 = next_pow2(std::max<uint64_t>(bytes + 1, kLaneBytesMin));
     if (int rc = ensure_workspace(e, n2, len2, pick_group_log2(e, bytes), dict_blobs(jobs[0]->dict),
                                   next_pow2(K)))
       return rc;
@@ -232,13 +286,16 @@ int launch_batch(ngpu_engine *e, BatchLane &b, const std::vector<BatchJob *> &jo
     if (int rc = ws_acquire(e, b.s)) return rc;
     if (int rc = ws_release(e, b.s, nullptr, true)) return rc;
   }
+  if (tr) b.mark[3] = batch_now_us();
   // ONE digest stage over all layers, ONE multi-layer dedup stage
   if (int rc = enqueue_digest(e, b.d_data, bytes, b.d_ch, N, b.d_res, b.s, true)) return rc;
+  if (tr) b.mark[4] = batch_now_us();
   if (int rc = enqueue_dedup(e, jobs[0]->dict, b.d_ch, N, b.d_res, nullptr, 0, b.s, b.d_lfirst, K,
                              b.d_lst)) {
     (void)ws_release(e, b.s, nullptr, false);
     return rc;
   }
+  if (tr) b.mark[5] = batch_now_us();
   // each pack's results (chunk ids rebased to its layer) and stats, into its
   // pinned read-back buffers
   const ngpu_ws_slot &sl = *e->cur;
@@ -343,8 +400,11 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     const int rc = launch_batch(e, b.lane[ln], take);
     if (batch_trace_on())
       fprintf(stderr, "{\"batch_trace\": %llu, \"lane\": %d, \"lead_us\": %.1f, \"take_us\": %.1f, "
-              "\"enqueued_us\": %.1f, \"layers\": %zu, \"open_packs\": %d, \"rc\": %d}\n",
-              (unsigned long long)seq, ln, t_lead, t_take, batch_now_us(), take.size(), open_now, rc);
+              "\"enqueued_us\": %.1f, \"layers\": %zu, \"open_packs\": %d, \"rc\": %d, "
+              "\"steps_us\": [%.1f, %.1f, %.1f, %.1f, %.1f, %.1f]}\n",
+              (unsigned long long)seq, ln, t_lead, t_take, batch_now_us(), take.size(), open_now, rc,
+              b.lane[ln].mark[0], b.lane[ln].mark[1], b.lane[ln].mark[2], b.lane[ln].mark[3],
+              b.lane[ln].mark[4], b.lane[ln].mark[5]);
     if (rc && b.lane[ln].s) {  // part of it may be enqueued: let it drain before the packs free their buffers
       DeviceGuard dg(e->device);
       (void)hipStreamSynchronize(b.lane[ln].s);
