@@ -41,7 +41,7 @@ MiB = 1 << 20
 # 39.3 T int32 ops/s.  Measured, not assumed: a wave64 v_add3/v_xor/v_alignbit
 # takes 4 SIMD cycles (rocprofv3: SQ_INSTS_VALU x 4 / 1024 SIMDs = the whole
 # b3_groups duration at the GRBM clock; DESIGN.md §Roofline, profiles/).
-SHA_MODES = {"auto": 0, "split": 1, "pair": 2, "lane": 3}
+SHA_MODES = {"auto": 0, "split": 1, "pair": 2, "lane": 3, "pair_pf": 4, "pair_pf_asm": 7}
 SHA_PAIR_MAX_CHUNKS = 256 * 128  # launch_sha256's auto rule (sha256.hip)
 CLOCK_HZ = 2.4e9
 PEAK_INT_OPS = 256 * 4 * 16 * 2.4e9
@@ -409,6 +409,11 @@ def sharded_dict_extra(torch, dist, eng, buf, d_ch, n, stream, rank, world, back
         every.copy_(torch.cat(parts))
     else:
         dist.all_gather_into_tensor(every, mine)
+    # the DICT decisions this rank must see: every chunk of its layer whose
+    # digest any rank planted (a layer's duplicate chunks, and identical
+    # layers on several ranks -- the c1 rehearsal -- hit more than once)
+    planted = set(bytes(r) for r in every.cpu().numpy())
+    expect = sum(bytes(r) in planted for r in d_out.view(n, 64)[:, :32].cpu().numpy())
     m = max(entries, world * k)
     gd = torch.Generator(device="cuda").manual_seed(0xD1C7)  # same filler on every rank
     dd = torch.empty((m, 32), dtype=torch.uint8, device="cuda")
@@ -452,7 +457,7 @@ def sharded_dict_extra(torch, dist, eng, buf, d_ch, n, stream, rank, world, back
     dist.barrier()
     el = time.perf_counter() - t0
     kinds = torch.bincount(d_out.view(n, 64)[:, 32].to(torch.int64), minlength=3).cpu()  # kind u32 @32
-    agg = torch.tensor([el, float(kinds[2]), float(k), float(np.median(probe_s))],
+    agg = torch.tensor([el, float(kinds[2]), float(k), float(np.median(probe_s)), float(expect)],
                        dtype=torch.float64)
     red = [agg.clone() for _ in range(world)]
     if cdev:
@@ -463,7 +468,7 @@ def sharded_dict_extra(torch, dist, eng, buf, d_ch, n, stream, rank, world, back
         red = [r.cpu() for r in redc]
     red = torch.stack(red)
     el_max = float(red[:, 0].max())
-    hits_all, planted_all = int(red[:, 1].sum()), int(red[:, 2].sum())
+    hits_all, planted_all, expect_all = int(red[:, 1].sum()), int(red[:, 2].sum()), int(red[:, 4].sum())
     return {"what": "C4 exchange on this run's layers: digest -> all_to_all_single dict probe "
                     "(digest-prefix partition; RCCL over xGMI when backend is nccl) -> dedup",
             "backend": backend, "collectives": ["all_gather_into_tensor (dict build)",
@@ -473,7 +478,8 @@ def sharded_dict_extra(torch, dist, eng, buf, d_ch, n, stream, rank, world, back
             "ms_per_step": round(el_max / steps * 1e3, 3),
             "probe_enqueue_ms_median_max_rank": round(float(red[:, 3].max()) * 1e3, 3),
             "dict_hits_all_ranks": hits_all, "planted_all_ranks": planted_all,
-            "hits_ok": hits_all == planted_all, "_elapsed": el_max}
+            "expected_hits_all_ranks": expect_all,
+            "hits_ok": hits_all == expect_all, "_elapsed": el_max}
 
 
 def dict_from_file(torch, nydus_gpu, eng, dd, us, bl, ix, wl, where):
@@ -667,12 +673,13 @@ def mix_roofline(roof, achieved, kernel, workload, comp=0):
             roof["linear_mix_model"] = lin_d
     clk, csrc = newest_profile(f"pmc_clock_{workload}.json")
     if clk and clk.get("clock_ghz"):
-        roof["held_clock_ghz"] = clk["clock_ghz"]
+        # the clock a profiled pass held (another run than this line's): a
+        # pointer, not a factor of any frac here (a ratio
+        # of this run's time over another run's clock exceeded 1)
+        roof["held_clock_ghz_profiled_pass"] = clk["clock_ghz"]
         roof["held_clock_source"] = csrc
-        if pm:
-            roof["frac_mix_at_held_clock"] = round(achieved / (pm * clk["clock_ghz"] / 2.4), 4)
     # where the rest goes: issued VALU wave-instructions
-    # (PMC SQ_INSTS_VALU of the same command, scripts/gpu_r4_measure.sh insts)
+    # (PMC SQ_INSTS_VALU of the same command, profiles/r4/scripts/gpu_r4_measure.sh insts)
     # over the algorithmic ones (comp x 680 / 64 lanes); frac_mix factors into
     # clock (held / 2.4) x algorithmic / issued x the issue efficiency left
     # (the mixed 2- / 4-cycle stream against the linear cycle model)
@@ -707,12 +714,6 @@ def mix_roofline(roof, achieved, kernel, workload, comp=0):
         # cycles per launch (the clock pass; the cycle count, unlike the clock,
         # does not depend on the profiler slowing the launch down) against the
         # ceiling's ops per cycle
-        cyc = (clk or {}).get("counters", {}).get("GRBM_GUI_ACTIVE")
-        if comp and cyc and ceil_["held_clock_ghz"].get(w):
-            k_opc = comp * OPS_PER_COMPRESSION / (cyc / 8)
-            c_opc = ct / (ceil_["held_clock_ghz"][w] * 1e9)
-            roof["ops_per_cycle"] = {"kernel": round(k_opc), "ceiling": round(c_opc)}
-            roof["frac_ceiling_per_cycle"] = round(k_opc / c_opc, 4)
 
 
 def tar_host_path(nydus_gpu, tar, wl, device, file_bytes, reps=200):
@@ -924,6 +925,66 @@ def sub_entries(args):
     return out
 
 
+def multi_gpu_checks(line):
+    """N > 1 lines: every hit-equality check the extras ran,
+    in one summary.  True / False per check that ran; entries that failed to run
+    are listed under `errors` (not counted as a wrong exchange).  `ok` is False
+    when any check is False, and the run then exits non-zero after printing
+    its line, so a wrong exchange cannot hide inside a JSON field."""
+    checks, errors = {}, {}
+    sx = line.get("sharded_dict")
+    if isinstance(sx, dict):
+        if "hits_ok" in sx:
+            checks["sharded_dict.hits_ok"] = bool(sx["hits_ok"])
+        elif "error" in sx:
+            errors["sharded_dict"] = sx["error"]
+    nc = line.get("node_cabi")
+    if isinstance(nc, dict):
+        if "hits_equal" in nc:
+            checks["node_cabi.routed_copy_replicate.hits_equal"] = bool(nc["hits_equal"])
+        elif "error" in nc:
+            errors["node_cabi"] = nc["error"]
+        for k, v in (nc.get("node_step") or {}).items():
+            if isinstance(v, dict) and "hits_equal_partition" in v:
+                checks[f"node_cabi.node_step.{k}.hits_equal"] = bool(v["hits_equal_partition"])
+            elif isinstance(v, dict) and "error" in v:
+                errors[f"node_cabi.node_step.{k}"] = v["error"]
+    c4 = line.get("c4")
+    if isinstance(c4, dict):
+        dd = c4.get("dict") or {}
+        if "dict_hits" in dd and "expected_dict_hits" in dd:
+            checks["c4.dict_hits"] = dd["dict_hits"] >= 0.99 * dd["expected_dict_hits"]
+        elif "error" in c4:
+            errors["c4"] = c4["error"]
+    return {"checks": checks, "errors": errors, "ok": all(checks.values())}
+
+
+def fracs_over_one(obj, path=""):
+    """Every `frac*` field above 1 in a bench line (every
+    frac in the line must be <= 1; a ratio above 1 is not a fraction)."""
+    out = []
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            p = f"{path}.{k}" if path else k
+            if (k.startswith("frac") or k.endswith("_frac")) and isinstance(v, (int, float)) and v > 1:
+                out.append(p)
+            out += fracs_over_one(v, p)
+    elif isinstance(obj, list):
+        for i, v in enumerate(obj):
+            out += fracs_over_one(v, f"{path}[{i}]")
+    return out
+
+
+def exit_on_failed_checks(mg):
+    """After the line is printed (and the ranks have left their barrier): a
+    False multi-GPU check ends the run with status 4."""
+    if mg is None or mg["ok"]:
+        return
+    bad = [k for k, v in mg["checks"].items() if not v]
+    print(f"bench.py: multi-GPU check(s) failed: {', '.join(bad)}", file=sys.stderr, flush=True)
+    sys.exit(4)
+
+
 def c4_entry(world, layers, steps, backend="nccl", timeout_s=420):
     """N > 1, rank 0, after the headline: C4 itself on the
     run's GPUs -- a child `torchrun --nproc-per-node N bench.py --workload c4`:
@@ -1131,24 +1192,33 @@ def packs_bench(args):
         vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
         drive.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u64), u64, u32, u32, u32, u32,
                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64),
-                          ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, u64]
+                          ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, u64, vp,
+                          ctypes.POINTER(ctypes.c_int32)]
         tar_ptrs = (vp * K)(*[a.ctypes.data for a in arrs])
         tar_lens = (u64 * K)(*[a.size for a in arrs])
 
-    def run_native(eng, stream):
+    node_devs = [int(x) for x in args.node.split(",")] if args.node else None
+
+    def run_native(eng, stream, read_from, node=None):
         """The rounds on K native threads (tools/packs_drive.cpp: the cgo
-        caller's shape, no GIL on the submit path)."""
+        caller's shape, no GIL on the submit path).  read_from: the layers go
+        in through ngpu_pack_reserve / commit (Go's PackWriter.ReadFrom, what
+        io.Copy picks), else ngpu_pack_write from pageable memory.  node: the
+        packs open on its least-loaded engine."""
         import ctypes
         R = args.warmup + args.steps
         rs = (ctypes.c_double * R)()
         per = (ctypes.c_uint64 * (4 * K))()
+        part = (ctypes.c_int32 * K)()
         tr = np.zeros((R, K, 3), np.float64)
         err = ctypes.create_string_buffer(512)
-        rc = drive(eng._h, K, tar_ptrs, tar_lens, 1 << 20, 1 if stream else 0,
+        rc = drive(eng._h if node is None else None, K, tar_ptrs, tar_lens, 1 << 20,
+                   (1 if stream else 0) | (2 if read_from else 0),
                    nydus_gpu._lib.DIGESTERS[wl["digester"]], wl["chunk"], R, rs, per,
-                   tr.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), err, 512)
+                   tr.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), err, 512,
+                   node._h if node is not None else None, part)
         if rc:
-            eng.close()
+            (node or eng).close()
             raise RuntimeError(f"packs_drive rc={rc}: {err.value.decode(errors='replace')}")
         kinds = np.array(per, np.uint64).reshape(K, 4)[:, :3].sum(0)
         t = tr[args.warmup:] * 1e3  # timed rounds, ms from each round's start
@@ -1158,32 +1228,53 @@ def packs_bench(args):
                   "close_ms_per_pack_max": round(float((t[:, :, 2] - t[:, :, 1]).max()), 3),
                   "tail_after_last_write_ms_median":
                       round(float(np.median(t[:, :, 2].max(1) - t[:, :, 1].max(1))), 3)}
-        return sum(rs[args.warmup:]), kinds, R, phases
+        placed = None
+        if node is not None:
+            placed = [int((np.array(part) == j).sum()) for j in range(len(node_devs))]
+        return sum(rs[args.warmup:]), kinds, R, phases, placed
 
-    def run(flags, stream, native=False):
+    def run(flags, stream, native=False, read_from=True):
         # 16 MiB staging slots: a C1 layer fits one (it closes in a batch),
         # and 32 packs x 2 slots pin 1 GiB instead of 16
-        eng = nydus_gpu.Engine(device=0, digester=wl["digester"], chunk_size=wl["chunk"],
-                               flags=flags, timing=True, staging_bytes=16 << 20)
+        node = None
+        if native and node_devs:
+            node = nydus_gpu.Node(node_devs, digester=wl["digester"], chunk_size=wl["chunk"],
+                                  staging_bytes=16 << 20, timing=True, flags=flags)
+            engs = node.engines
+        else:
+            eng = nydus_gpu.Engine(device=0, digester=wl["digester"], chunk_size=wl["chunk"],
+                                   flags=flags, timing=True, staging_bytes=16 << 20)
+            engs = [eng]
         if native:
-            b_before = eng.batch_stats()  # (counted over every round: warmup included)
-            el, kinds, R, phases = run_native(eng, stream)
-            b1 = eng.batch_stats()
-            nb = b1["batches"] - b_before["batches"]
+            b_before = [e.batch_stats() for e in engs]  # (counted over every round: warmup included)
+            el, kinds, R, phases, placed = run_native(engs[0], stream, read_from, node)
+            b_after = [e.batch_stats() for e in engs]
+            nb = sum(b["batches"] - a["batches"] for a, b in zip(b_before, b_after))
+            npk = sum(b["packs"] - a["packs"] for a, b in zip(b_before, b_after))
             dev = None
-            if nb:
-                tms = [eng.timing_at(k) for k in range(min(nb, 64))]
-                dev_ms = sum(t["total_ms"] for t in tms)
-                packs_in = (b1["packs"] - b_before["packs"]) * min(nb, 64) / nb
-                dev = round(file_bytes / K * packs_in / (dev_ms / 1e3) / 1e9, 2) if dev_ms else None
-            eng.close()
-            return {"gbs": round(file_bytes * args.steps / el / 1e9, 2),
-                    "ms_per_round": round(el / args.steps * 1e3, 3), "device_gbs": dev,
-                    "launch_sets_per_round": round(nb / R, 2),
-                    "packs_per_set": round((b1["packs"] - b_before["packs"]) / nb, 1) if nb else 0,
-                    "most_packs_in_one_set": b1["max_packs"], "phases": phases,
-                    "decisions_last_round": {"NEW": int(kinds[0]), "INTRA": int(kinds[1]),
-                                             "DICT": int(kinds[2])}}
+            if nb:  # the launch sets' device time, each engine's own (they run side by side)
+                dev_s, packs_in = 0.0, 0.0
+                for e, a, b in zip(engs, b_before, b_after):
+                    m = b["batches"] - a["batches"]
+                    if not m:
+                        continue
+                    tms = [e.timing_at(k) for k in range(min(m, 64))]
+                    dev_s = max(dev_s, sum(t["total_ms"] for t in tms) / 1e3 * m / min(m, 64))
+                    packs_in += b["packs"] - a["packs"]
+                dev = round(file_bytes / K * packs_in / dev_s / 1e9, 2) if dev_s else None
+            (node or engs[0]).close()
+            out = {"gbs": round(file_bytes * args.steps / el / 1e9, 2),
+                   "ms_per_round": round(el / args.steps * 1e3, 3), "device_gbs": dev,
+                   "feed": "ReadFrom (ngpu_pack_reserve / commit, 1 MiB source reads)" if read_from
+                           else "Write (1 MiB ngpu_pack_write calls from pageable memory)",
+                   "launch_sets_per_round": round(nb / R, 2),
+                   "packs_per_set": round(npk / nb, 1) if nb else 0,
+                   "most_packs_in_one_set": max(b["max_packs"] for b in b_after), "phases": phases,
+                   "decisions_last_round": {"NEW": int(kinds[0]), "INTRA": int(kinds[1]),
+                                            "DICT": int(kinds[2])}}
+            if placed is not None:
+                out["packs_per_node_part_last_round"] = placed
+            return out
         meet = threading.Barrier(K + 1)
         errs = []
         kinds = np.zeros(3, np.int64)
@@ -1250,11 +1341,14 @@ def packs_bench(args):
     if drive is None:
         raise SystemExit(f"{dpath} is missing: run `make -C nydus-snapshotter_amd`")
     # native threads (the cgo caller's shape) are the line; Python threads beside
+    # (the reported mode is the drop-in's own feed, ReadFrom)
     plan = {"decisions": lambda: run(0, False, native=True),
+            "decisions_write": lambda: run(0, False, native=True, read_from=False),
             "decisions_no_batch": lambda: run(nydus_gpu.FLAG_NO_BATCH, False, native=True),
             "stream_zstd": lambda: run(0, True, native=True),
-            "stream_zstd_no_batch": lambda: run(nydus_gpu.FLAG_NO_BATCH, True, native=True),
-            "decisions_python_threads": lambda: run(0, False)}
+            "stream_zstd_no_batch": lambda: run(nydus_gpu.FLAG_NO_BATCH, True, native=True)}
+    if not node_devs:
+        plan["decisions_python_threads"] = lambda: run(0, False)
     pick = [m for m in args.packs_modes.split(",") if m] if args.packs_modes else list(plan)
     if "decisions" not in pick or any(m not in plan for m in pick):
         raise SystemExit(f"--packs-modes: a subset of {list(plan)} with 'decisions'")
@@ -1300,16 +1394,21 @@ def packs_bench(args):
             cpu["pipeline"] = ("per layer on one thread: digests + stream dedup + zstd level 1 of the "
                                "NEW chunks (libzstd) + SHA-256 of the compressed stream (OpenSSL)")
     line = {"metric": "GB/s of layer data chunk-hashed+deduped (node)",
-            "value": modes["decisions"]["gbs"], "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+            "value": modes["decisions"]["gbs"], "unit": "GB/s",
+            "n_gpus": len(set(node_devs)) if node_devs else 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": modes["decisions"]["ms_per_round"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic alpine-like layer tars (tests/golden/layers.py), host memory",
             "config": {"workload": f"{K} concurrent converter.Pack calls of distinct C1-size "
-                                   f"layers on one engine ({wl['digester']}, 1 MiB chunks)",
+                                   f"layers on " + (f"a node of devices {node_devs} (least-loaded "
+                                                    f"engine per Pack)" if node_devs else "one engine")
+                                   + f" ({wl['digester']}, 1 MiB chunks)",
                        "name": args.workload, "packs": K, "file_bytes_per_round": file_bytes,
                        "tar_bytes_per_round": tar_bytes, "batch_window_us": 2000 if wl["digester"] == "sha256" else 250, "batch_lanes": 4,
-                       "caller": "K native threads (tools/packs_drive.cpp), 1 MiB writes from "
-                                 "pageable memory"},
+                       "caller": "K native threads (tools/packs_drive.cpp); 'decisions' feeds "
+                                 "through ReadFrom (ngpu_pack_reserve / commit, the Go drop-in's "
+                                 "io.Copy path), 'decisions_write' through 1 MiB ngpu_pack_write "
+                                 "calls from pageable memory"},
             "modes": modes, "cpu_baseline": cpu,
             "bound": "blake3: PCIe H2D of the tars through 2 shared copy lanes (~45 GB/s, "
                      "tools/h2d_streams); sha256: one 1 MiB chunk's chain per batch (~21 ms) "
@@ -1393,7 +1492,7 @@ def node_bench(args):
                 p["stream"].synchronize()
 
         modes = {}
-        for name, mode in (("partition", nydus_gpu.NODE_DICT_PARTITION),
+        for name, mode in (("partition", nydus_gpu.NODE_DICT_PARTITION | nydus_gpu.NODE_EXCHANGE_ROUTED),
                            ("partition_copy", nydus_gpu.NODE_DICT_PARTITION | nydus_gpu.NODE_EXCHANGE_COPY),
                            ("replicate", nydus_gpu.NODE_DICT_REPLICATE)):
             t0 = time.perf_counter()
@@ -1545,10 +1644,11 @@ def node_bench(args):
                          "peer_bytes_per_step": routed_bytes,
                          "peer_bytes_per_step_copy": n_all * (32 + 24) * (W - 1),
                          "peer_bytes_ratio_copy_over_routed": round(n_all * 56 * (W - 1) / max(1, routed_bytes), 2),
-                         "note": "routed (default, ABI 4): each requester buckets its digests by owner; "
+                         "note": "'partition' = routed (opt-in since ABI 7, NGPU_NODE_EXCHANGE_ROUTED): "
+                                 "each requester buckets its digests by owner; "
                                  "owner o's probe kernel reads only its rows (32-B digest + 4-B row id, "
                                  "peer loads) and stores 24-B hits at their rows (peer stores), plus the "
-                                 "W counters it reads; copy (NGPU_NODE_EXCHANGE_COPY, ABI 3): every "
+                                 "W counters it reads; 'partition_copy' = copy (the default since ABI 7): every "
                                  "digest to each of the W-1 other owners, 24-B hits back from each. On a "
                                  "one-GPU rehearsal the peer traffic stays in one HBM and the W engines "
                                  "share the GPU"},
@@ -1650,7 +1750,7 @@ def main():
     ap.add_argument("--load-mode", type=int, default=-1,
                     help="BLAKE3 load mode override (diagnostics: 4 = no loads, needs a "
                          "-DNGPU_DIAG_NOLOAD=1 build via NYDUS_GPU_LIB; its digests are not BLAKE3)")
-    ap.add_argument("--sha-mode", choices=["auto", "split", "pair", "lane"], default="auto",
+    ap.add_argument("--sha-mode", choices=list(SHA_MODES), default="auto",
                     help="SHA-256 kernel: one lane per chunk (lane; split = schedule/round "
                          "waves) or two (pair)")
     ap.add_argument("--dict-entries", type=int, default=0, help="override dict size")
@@ -1709,12 +1809,12 @@ def main():
     if args.warmup is None:
         w = WORKLOADS[args.workload]
         args.warmup = 80 if (w.get("pool") or w.get("dict_entries")) else 20
+    if args.packs:  # (with --node: the packs spread over the node's engines)
+        return packs_bench(args)
     if args.node:
         return node_bench(args)
     if args.engines > 1 or args.streams > 1:
         return concurrent_bench(args)
-    if args.packs:
-        return packs_bench(args)
 
     import torch
     import nydus_gpu
@@ -1990,13 +2090,14 @@ def main():
         mode = args.sha_mode
         if mode == "auto":  # launch_sha256's rule
             mode = "pair" if n <= SHA_PAIR_MAX_CHUNKS else "lane"
-        pair = mode == "pair"
+        pair = mode.startswith("pair")
         # SHA-256 is serial within a chunk: with fewer chunks than the chip has
         # lanes, a chunk's round chain (VALU ops on its critical wave, 4 cycles
         # per wave64 op) bounds the kernel, not chip-wide VALU throughput.
         # VALU ops per block on the critical wave: pair/split round waves; the
         # lane kernel's wave does the whole block (schedule + rounds)
-        chain_ops = {"pair": 66 * 9, "split": 64 * 14, "lane": 1384}[mode]
+        chain_ops = {"pair": 66 * 9, "pair_pf": 66 * 9, "pair_pf_asm": 66 * 9, "split": 64 * 14,
+                     "lane": 1384}[mode]
         lanes_used = n * (2 if pair else 1)
         max_blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).max())
         chain_s = max_blocks * chain_ops * 4 / CLOCK_HZ
@@ -2127,6 +2228,13 @@ def main():
                 line["c4"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
     if rank == 0 and world == 1 and args.workload == "c2" and not args.no_sub:
         line.update(sub_entries(args))
+    mg = None
+    if rank == 0 and dist:
+        line["multi_gpu_checks"] = mg = multi_gpu_checks(line)
+    if rank == 0:
+        bad = fracs_over_one(line)
+        if bad:  # printed, never hidden: a frac > 1 means a wrong model or clock
+            line["fracs_over_one"] = bad
     if rank == 0:
         with print_mu:
             first = not printed[0]
@@ -2139,6 +2247,7 @@ def main():
         dist.destroy_process_group()
     if dog:
         dog.cancel()
+    exit_on_failed_checks(mg)
 
 
 if __name__ == "__main__":

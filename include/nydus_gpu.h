@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define NGPU_ABI_VERSION 6
+#define NGPU_ABI_VERSION 7
 
 /* PackOption.Digester (API extension; maps to nydus-image --digester). */
 enum ngpu_digester { NGPU_DIGEST_BLAKE3 = 0, NGPU_DIGEST_SHA256 = 1 };
@@ -119,10 +119,16 @@ typedef struct {
 #define NGPU_FLAG_GRID_STAGES 0x4u
 /* Packs whose whole layer fit one staging slot and that close at about the
  * same time on one engine share ONE digest + multi-layer dedup launch set
- * (round 5: containerd converting an image's small layers concurrently);
- * the first to close waits for every other pack open on the engine to close,
- * at most 250 us.  This flag gives every pack its own launches (A/B, or a
- * caller whose packs must never wait for each other).  Same results. */
+ * (round 5: containerd converting an image's small layers concurrently).
+ * The first to close waits for the other packs that may still join -- open,
+ * not OCIRef, and with no more than one staging slot of tar so far -- to
+ * close too: BLAKE3 at most 250 us; SHA-256 2 ms, restarted by every pack
+ * that joins, at most 12 ms after the first (a SHA-256 batch holds the GPU
+ * for one 1 MiB chunk's chain, ~21 ms, whatever its size).  A pack that cannot
+ * join (its layer outgrew one slot, an OCIRef pack, a pack closing without
+ * chunks) stops being waited for at that moment.  This flag gives every pack
+ * its own launches (A/B, or a caller whose packs must never wait for each
+ * other).  Same results. */
 #define NGPU_FLAG_NO_BATCH 0x8u
 /* Tuning (benchmarks only): bits 8..10 = 1 + BLAKE3 load mode (0 plain loads
  * with the whole-leaf fast path, 1 non-temporal loads, 2 next-block prefetch,
@@ -132,9 +138,11 @@ typedef struct {
 #define NGPU_FLAG_LOAD_MODE_SHIFT 8
 /* Tuning (benchmarks only): bits 11..13 = 1 + SHA-256 kernel (0: one lane per
  * chunk with schedule/round waves, 1: two lanes per chunk, 2: one lane per
- * chunk, each wave schedules its own blocks, 4: two lanes, one chunk group per
- * workgroup, 5: two lanes, four groups per workgroup); 0 = library default
- * (by chunk count); other values are rejected (NGPU_EINVAL). */
+ * chunk, each wave schedules its own blocks, 3: two lanes per chunk with the
+ * K+W loads off the round chain, 4: two lanes, one chunk group per
+ * workgroup, 5: two lanes, four groups per workgroup, 6: as 3 with the
+ * rounds in a fixed asm issue order); 0 = library default (by chunk count).
+ * Every kernel computes the same digests. (ABI 7: 3 and 6 added) */
 #define NGPU_FLAG_SHA_MODE_SHIFT 11
 
 /* The builder's exit status (builder.go:169-175) for work enqueued on a
@@ -398,12 +406,12 @@ int ngpu_pack_tar(ngpu_engine *eng, const void *tar, uint64_t len,
                   uint64_t *n_out, ngpu_layer_stats *stats);
 void ngpu_free_host(void *p);
 
-/* Stage timings of the last ngpu_process / ngpu_process_device call on this
- * engine (synchronises on the recorded events).  NGPU_EINVAL unless the
- * engine was created with NGPU_FLAG_TIMING. */
 /* Batched Pack closes so far (NGPU_FLAG_NO_BATCH): out[0] launch sets,
  * out[1] packs closed in them, out[2] the most packs in one. */
 int ngpu_batch_stats(ngpu_engine *eng, uint64_t out[3]);
+/* Stage timings of the last ngpu_process / ngpu_process_device call on this
+ * engine (synchronises on the recorded events).  NGPU_EINVAL unless the
+ * engine was created with NGPU_FLAG_TIMING. */
 int ngpu_last_timing(ngpu_engine *eng, ngpu_timing *out);
 /* The same for the call `back` calls before the last one (0 = the last).
  * The engine keeps the events of its last 64 calls, so a caller can time a
@@ -429,22 +437,48 @@ int ngpu_pack_open_dict(ngpu_engine *eng, ngpu_dict *dict, uint32_t flags, ngpu_
  * memory that must outlive the pack; once another thread stores a non-zero
  * value there, the pack's next write / commit / reserve, or the running
  * close / finish at its next slot, blob window or compression batch, fails
- * with NGPU_ECANCELED and releases the pack (the reference kills the
- * builder process, builder.go:153-174, convert_unix.go:530-535).  NULL
- * removes the flag. */
+ * with NGPU_ECANCELED (the reference kills the builder process,
+ * builder.go:153-174, convert_unix.go:530-535).  close / finish release the
+ * pack on every outcome; after a failed write / commit / reserve the pack
+ * stays open until the caller aborts it (ngpu_pack_abort).  NULL removes the
+ * flag. */
 int ngpu_pack_set_cancel(ngpu_pack *p, const volatile int32_t *flag);
 int ngpu_pack_write(ngpu_pack *p, const void *buf, uint64_t len);
 int ngpu_pack_reserve(ngpu_pack *p, void **ptr, uint64_t *avail);
 int ngpu_pack_commit(ngpu_pack *p, uint64_t n);
 int ngpu_pack_close(ngpu_pack *p, ngpu_chunk **chunks_out, ngpu_result **results_out,
                     uint64_t *n_out, ngpu_layer_stats *stats);
+/* Ends a pack without output: its staging, HBM and emitter thread are
+ * released.  A binding calls it on every path that will never reach close --
+ * a failed write, a source read error, ctx.Done() with no Close to follow
+ * (convert_unix.go:885-907 skips tw.Close() on those paths).  Not concurrently
+ * with another call on the same pack. */
 void ngpu_pack_abort(ngpu_pack *p);
+/* The engine a pack runs on (borrowed; e.g. to see where ngpu_node_pack_open
+ * placed it: compare with ngpu_node_engine).  (ABI 7) */
+ngpu_engine *ngpu_pack_engine(const ngpu_pack *p);
+
+/* What an engine holds right now (ABI 7): a leak check for the bindings'
+ * error paths (every aborted or finished pack gives all of it back). */
+typedef struct {
+  uint64_t open_packs;          /* packs opened and not yet ended */
+  uint64_t staging_pool_bufs;   /* pinned staging slots kept for the next packs */
+  uint64_t staging_pool_bytes;  /* their pinned bytes */
+  uint64_t pack_pool;           /* per-pack stream + buffer sets kept */
+  uint64_t land_pool;           /* early-emission landing buffers kept */
+  uint64_t batch_waitable;      /* open packs a batch leader would still wait for */
+  uint64_t reserved[2];
+} ngpu_engine_counters;
+int ngpu_engine_counters_get(ngpu_engine *eng, ngpu_engine_counters *out);
 
 /* ---- multi-GPU node ------------------------------------
  * One process drives the GPUs of a node: one engine per listed device (a
  * device may be listed twice, e.g. to rehearse a 2-GPU node on one GPU).
- * Layers are independent units: ngpu_node_pack_open spreads streaming Packs
- * over the engines round robin, ngpu_node_process_device runs device-resident
+ * Layers are independent units (north star: "the chunk stream is sharded by
+ * layer"): ngpu_node_pack_open places each streaming Pack on the engine with
+ * the fewest open packs (ties round robin) -- containerd's per-layer
+ * goroutines (convert_unix.go:467-538) then spread over every GPU and every
+ * GPU's own PCIe link -- and ngpu_node_process_device runs device-resident
  * layers on a chosen engine.  A node chunk dict is either partitioned by
  * digest prefix -- entry with digest d lives on device
  * ((d[0] << 8 | d[1]) * n) >> 16, keeping table order, so "first entry wins"
@@ -453,22 +487,24 @@ void ngpu_pack_abort(ngpu_pack *p);
  * owner, each owner probes the entries it owns and the hits come back with
  * GLOBAL entry ids, ordered by cross-device events -- the in-process form of
  * the north star's digest-prefix all-to-all (nydus_gpu/dist.py keeps the
- * one-process-per-GPU RCCL form).  Default exchange (ABI 4, "routed"): the
- * requester buckets its digests by owner in its own HBM; each owner's probe
- * kernel reads only its own rows (peer loads over xGMI) and writes each hit
- * into the requester's hit array at the row's id (peer stores), so a call
- * moves n x (32 + 4) bytes out and n x 24 back in total.  With
- * NGPU_NODE_EXCHANGE_COPY in `mode` (or when peer access between two listed
- * devices is unavailable) the ABI 3 exchange runs instead: every digest to
- * every owner and every owner's n hits back by hipMemcpyPeerAsync (W x the
- * bytes).  Peer access between the listed devices is enabled at creation.
+ * one-process-per-GPU RCCL form).  Default exchange (ABI 7, "copy"): every
+ * digest to every owner and every owner's n hits back by hipMemcpyPeerAsync
+ * (DMA engines; W x n x 56 bytes per call), merged by owner on the
+ * requester.  NGPU_NODE_EXCHANGE_ROUTED in `mode` (opt-in, the ABI 4-6
+ * default) runs the routed exchange instead when every pair of listed devices
+ * has peer access: the requester buckets its digests by owner in its own HBM;
+ * each owner's probe kernel reads only its own rows (peer loads over xGMI)
+ * and writes each hit into the requester's hit array at the row's id (peer
+ * stores), so a call moves n x (32 + 4) bytes out and n x 24 back in total.
+ * Peer access between the listed devices is enabled at creation.
  * UNVERIFIED ON DISTINCT GPUs: every test so far lists one GPU several times
  * (the copies and peer stores then stay inside one HBM); the routed
  * exchange's peer stores, the copy exchange and the RCCL node step first
  * meet separate GPUs in the driver's multi-GPU bench, whose `node_cabi` entry
- * runs all three against a replicated dict and reports whether their hits
- * agree (hits_equal).  Until that has passed, a caller that needs certainty
- * uses NGPU_NODE_DICT_REPLICATE (no exchange). */
+ * runs all three against a replicated dict, prints them in its
+ * `multi_gpu_checks` summary and fails the run if any disagrees.  Until that
+ * has passed, a caller that needs certainty uses NGPU_NODE_DICT_REPLICATE (no
+ * exchange), as the converter mirrors do for ChunkDictPath. */
 typedef struct ngpu_node ngpu_node;
 int ngpu_node_create(const int32_t *devices, uint32_t n, const ngpu_config *cfg, ngpu_node **out);
 void ngpu_node_destroy(ngpu_node *node);
@@ -477,15 +513,22 @@ uint32_t ngpu_node_size(const ngpu_node *node);
 ngpu_engine *ngpu_node_engine(ngpu_node *node, uint32_t i);
 #define NGPU_NODE_DICT_PARTITION 0u /* shard by digest prefix (default) */
 #define NGPU_NODE_DICT_REPLICATE 1u /* a full copy on every device */
-#define NGPU_NODE_EXCHANGE_COPY 0x100u /* | PARTITION: broadcast + DMA exchange */
+#define NGPU_NODE_EXCHANGE_COPY 0x100u   /* | PARTITION: broadcast + DMA exchange (default) */
+#define NGPU_NODE_EXCHANGE_ROUTED 0x200u /* | PARTITION: peer-kernel exchange (opt-in) */
 /* Node chunk dicts, usable by any engine of the node (ngpu_pack_open_dict,
- * ngpu_process_dict*, ngpu_node_*); checks as ngpu_dict_open. */
+ * ngpu_process_dict*, ngpu_node_*); checks as ngpu_dict_open.
+ * ngpu_node_dict_open caches what it opened, as ngpu_dict_open does per
+ * engine: opening an unchanged file (path, device, inode, size, mtime) with
+ * the same mode again returns the same dict with one more reference, so 1000
+ * Packs naming one ChunkDictPath load it once per node. */
 int ngpu_node_dict_open(ngpu_node *node, const char *path, uint32_t mode, ngpu_dict **out);
 int ngpu_node_dict_create(ngpu_node *node, const void *records, uint64_t n,
                           const void *blob_table, uint32_t n_blobs, uint32_t mode,
                           ngpu_dict **out);
 /* Device index of the node device that owns digests[32] (partitioned dicts). */
 uint32_t ngpu_node_owner(const ngpu_node *node, const uint8_t *digest);
+/* A Pack on the node's least-loaded engine (fewest open packs, ties round
+ * robin); flags as ngpu_pack_open_dict.  ngpu_pack_engine tells which. */
 int ngpu_node_pack_open(ngpu_node *node, ngpu_dict *dict, uint32_t flags, ngpu_pack **out);
 int ngpu_node_process_device(ngpu_node *node, uint32_t i, ngpu_dict *dict, const void *d_data,
                              uint64_t len, const ngpu_chunk *d_chunks, uint64_t n,
@@ -740,17 +783,9 @@ typedef struct ngpu_merge_options {
   /* PrefetchPatterns (the builder's stdin, builder.go:238-240, 269):
    * newline-separated paths; NULL or "" = "/" */
   const char *prefetch_patterns;
-  /* ABI 6: targz-ref layers (Layer.OriginalDigest; convert_unix.go:579-587
-   * hands nydus-image --blob-digests / --blob-sizes / --blob-toc-digests,
-   * builder.go:242-253).  NULL = none; else n entries, entry l NULL for a
-   * layer without OriginalDigest: 64 hex chars of the layer's RAFS blob (its
-   * nydus stream) digest, its size, and 64 hex chars of the sha256 of its TOC
-   * entry data (calcBlobTOCDigest, convert_unix.go:541-554).  Recorded in the
-   * layer's own blob record of the merged bootstrap (restated RafsV6Blob
-   * offsets, unpinned). */
-  const char *const *rafs_blob_digests;
-  const uint64_t *rafs_blob_sizes;
-  const char *const *rafs_blob_toc_digests;
+  /* (ABI 6 appended the targz-ref arrays here; ABI 7 takes them as arguments
+   * of ngpu_merge_ex2 instead, so a caller built against either header passes
+   * a struct this library reads no further than its end.) */
 } ngpu_merge_options;
 
 /* ngpu_merge with MergeOption's parent bootstrap and prefetch patterns
@@ -759,6 +794,22 @@ int ngpu_merge_ex(const void *const *bootstraps, const uint64_t *sizes,
                   const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
                   uint64_t dict_size, const ngpu_merge_options *opt, ngpu_write_fn w, void *ctx,
                   char **blob_ids_out);
+/* ngpu_merge_ex with targz-ref layers (ABI 7; Layer.OriginalDigest:
+ * convert_unix.go:577-590 hands nydus-image --blob-digests / --blob-sizes /
+ * --blob-toc-digests, builder.go:242-253).  The three arrays are NULL (no
+ * targz-ref layer) or n entries each, entry l NULL / ignored for a layer
+ * without OriginalDigest: 64 hex chars of the layer's RAFS blob (its nydus
+ * stream) digest, its size, and 64 hex chars of the sha256 of its TOC entry
+ * data (calcBlobTOCDigest, convert_unix.go:541-554).  Recorded in the layer's
+ * own blob record of the merged bootstrap (RafsV6Blob blob_toc_digest /
+ * blob_meta_digest / blob_meta_size; offsets restated from nydus v2.3.0,
+ * parity unpinned). */
+int ngpu_merge_ex2(const void *const *bootstraps, const uint64_t *sizes,
+                   const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
+                   uint64_t dict_size, const ngpu_merge_options *opt,
+                   const char *const *rafs_blob_digests, const uint64_t *rafs_blob_sizes,
+                   const char *const *rafs_blob_toc_digests, ngpu_write_fn w, void *ctx,
+                   char **blob_ids_out);
 
 #ifdef __cplusplus
 }

@@ -22,7 +22,9 @@ import (
 	"fmt"
 	"io"
 	"os"
+	"path/filepath"
 	"strconv"
+	"strings"
 	"sync"
 
 	"github.com/containerd/containerd/v2/core/content"
@@ -38,15 +40,35 @@ type gpuKey struct {
 }
 
 var (
-	gpuMu      sync.Mutex
-	gpuEngines = map[gpuKey]*gpu.Engine{}
-	gpuNext    int
+	gpuMu    sync.Mutex
+	gpuNodes = map[gpuKey]*gpu.Node{}
 )
 
-// gpuEngine returns the process's engine for this option set (engines are
-// safe for concurrent Packs: LayerConvertFunc runs one per layer goroutine);
-// new option sets land round robin on the host's GPUs.
-func gpuEngine(opt PackOption) (*gpu.Engine, error) {
+// gpuDevices: NYDUS_GPU_DEVICES ("0,1,2,3"; a device may repeat) or every
+// device the library sees.
+func gpuDevices() []int32 {
+	var devs []int32
+	if v := os.Getenv("NYDUS_GPU_DEVICES"); v != "" {
+		for _, f := range strings.Split(v, ",") {
+			if d, err := strconv.Atoi(strings.TrimSpace(f)); err == nil {
+				devs = append(devs, int32(d))
+			}
+		}
+	}
+	if len(devs) == 0 {
+		for i := 0; i < gpu.DeviceCount(); i++ {
+			devs = append(devs, int32(i))
+		}
+	}
+	return devs
+}
+
+// gpuNode returns the process's node for this option set: one engine per GPU
+// of the host, each Pack on the least-loaded one, so the layers of an image --
+// LayerConvertFunc runs one per goroutine (convert_unix.go:467-538) -- shard
+// over every GPU and every GPU's PCIe link (north star: "the chunk stream is
+// sharded by layer").
+func gpuNode(opt PackOption) (*gpu.Node, error) {
 	k := gpuKey{digester: gpu.Blake3, fsVersion: 6}
 	if opt.Digester == "sha256" {
 		k.digester = gpu.Sha256
@@ -63,21 +85,20 @@ func gpuEngine(opt PackOption) (*gpu.Engine, error) {
 		}
 		k.chunkSize = uint32(v) // the library enforces types.go:76's rule (NGPU_EINVAL)
 	}
-	if opt.AlignedChunk {
+	if opt.AlignedChunk && k.fsVersion == 5 {
 		k.flags |= gpu.AlignedChunk
 	}
 	gpuMu.Lock()
 	defer gpuMu.Unlock()
-	if e, ok := gpuEngines[k]; ok {
-		return e, nil
+	if nd, ok := gpuNodes[k]; ok {
+		return nd, nil
 	}
-	e, err := gpu.New(gpuNext%gpu.DeviceCount(), k.digester, k.chunkSize, k.fsVersion, k.flags)
+	nd, err := gpu.NewNode(gpuDevices(), k.digester, k.chunkSize, k.fsVersion, k.flags)
 	if err != nil {
 		return nil, err
 	}
-	gpuNext++
-	gpuEngines[k] = e
-	return e, nil
+	gpuNodes[k] = nd
+	return nd, nil
 }
 
 func compressorOf(name string) (uint32, error) {
@@ -113,20 +134,22 @@ func packGPU(ctx context.Context, dest io.Writer, opt PackOption) (io.WriteClose
 	if opt.OCIRef { // packFromTar passes nothing but the blob for targz-ref (builder.go:180-218)
 		opt = PackOption{Accelerator: opt.Accelerator, OCIRef: true, FsVersion: "6", Timeout: opt.Timeout}
 	}
-	eng, err := gpuEngine(opt)
+	nd, err := gpuNode(opt)
 	if err != nil {
-		return nil, errors.Wrap(err, "gpu engine")
+		return nil, errors.Wrap(err, "gpu node")
 	}
 	comp, err := compressorOf(opt.Compressor)
 	if err != nil {
 		return nil, err
 	}
-	var dict *gpu.ChunkDict // this Pack's own reference; the engine caches the load
+	// this Pack's own reference to a replica on every GPU of the node (a probe
+	// needs no exchange); the library loads an unchanged ChunkDictPath once per node
+	var dict *gpu.ChunkDict
 	if opt.ChunkDictPath != "" && !opt.OCIRef {
-		if dict, err = eng.OpenChunkDict(opt.ChunkDictPath); err != nil {
+		if dict, err = nd.OpenChunkDict(opt.ChunkDictPath, false); err != nil {
 			return nil, errors.Wrap(err, "load chunk dict")
 		}
-		defer dict.Release()
+		defer dict.Release() // the pack holds its own reference
 	}
 	cancel := context.CancelFunc(func() {})
 	if opt.Timeout != nil { // builder.go:153-158
@@ -136,7 +159,7 @@ func packGPU(ctx context.Context, dest io.Writer, opt PackOption) (io.WriteClose
 	if opt.FsVersion == "5" {
 		fsv = 5
 	}
-	pw, err := eng.Pack(ctx, dest, comp, fsv, opt.PrefetchPatterns, dict, opt.OCIRef)
+	pw, err := nd.Pack(ctx, dest, comp, fsv, opt.PrefetchPatterns, dict, opt.OCIRef)
 	if err != nil {
 		cancel()
 		return nil, err
@@ -144,13 +167,30 @@ func packGPU(ctx context.Context, dest io.Writer, opt PackOption) (io.WriteClose
 	return &gpuPackWriter{pw: pw, cancel: cancel}, nil
 }
 
+// gpuPackWriter: the PackOption.Timeout context is cancelled on every end of
+// the Pack (its AfterFunc then finds the pack already released), not only at
+// Close, which LayerConvertFunc skips on its error paths.
 type gpuPackWriter struct {
 	pw     *gpu.PackWriter
 	cancel context.CancelFunc
 }
 
-func (w *gpuPackWriter) Write(b []byte) (int, error)            { return w.pw.Write(b) }
-func (w *gpuPackWriter) ReadFrom(r io.Reader) (int64, error)    { return w.pw.ReadFrom(r) }
+func (w *gpuPackWriter) Write(b []byte) (int, error) {
+	n, err := w.pw.Write(b)
+	if err != nil {
+		w.cancel()
+	}
+	return n, err
+}
+
+func (w *gpuPackWriter) ReadFrom(r io.Reader) (int64, error) {
+	n, err := w.pw.ReadFrom(r)
+	if err != nil {
+		w.cancel()
+	}
+	return n, err
+}
+
 func (w *gpuPackWriter) Close() error {
 	defer w.cancel()
 	_, err := w.pw.Close()
@@ -161,8 +201,10 @@ func (w *gpuPackWriter) Close() error {
 // every layer's bootstrap exactly as today (UnpackEntry over the layer's
 // ReaderAt): the merged bootstrap goes to `target`, the referenced blob ids
 // come back as digests, as tool.Merge builds them from its output JSON
-// (builder.go:286-292).
-func mergeGPU(boots [][]byte, layerHexes []string, opt MergeOption, target io.Writer) ([]digest.Digest, error) {
+// (builder.go:286-292).  rafs[l]: layer l's --blob-digests / --blob-sizes /
+// --blob-toc-digests entry when it is a targz-ref layer (nil otherwise).
+func mergeGPU(boots [][]byte, layerHexes []string, opt MergeOption, rafs []*gpu.RafsBlob,
+	target io.Writer) ([]digest.Digest, error) {
 	var dictBoot, parentBoot []byte
 	var err error
 	if opt.ChunkDictPath != "" {
@@ -175,7 +217,7 @@ func mergeGPU(boots [][]byte, layerHexes []string, opt MergeOption, target io.Wr
 			return nil, errors.Wrap(err, "read parent bootstrap")
 		}
 	}
-	merged, ids, err := gpu.Merge(boots, layerHexes, dictBoot, parentBoot, opt.PrefetchPatterns)
+	merged, ids, err := gpu.Merge(boots, layerHexes, dictBoot, parentBoot, opt.PrefetchPatterns, rafs)
 	if err != nil {
 		return nil, errors.Wrap(err, "merge bootstrap")
 	}
@@ -192,24 +234,43 @@ func mergeGPU(boots [][]byte, layerHexes []string, opt MergeOption, target io.Wr
 }
 
 // mergeGPUFiles is Merge's call site of mergeGPU: the layers' bootstraps as
-// Merge unpacked them (sourceBootstrapPaths), their digests' hex as the layer
-// names, the merged bootstrap written to target.
-func mergeGPUFiles(paths []string, layers []Layer, opt MergeOption, target string) ([]digest.Digest, error) {
+// Merge unpacked them (sourceBootstrapPaths), their file names as the layer
+// names -- Digest.Hex(), or OriginalDigest.Hex() for a targz-ref layer
+// (getBootstrapPath, convert_unix.go:567-573), the names nydus-image merge
+// sees -- the merged bootstrap written to target.  rafsBlobDigests / Sizes /
+// TOCDigests are Merge's lists as it builds them for tool.Merge
+// (convert_unix.go:577-590): one entry per layer with an OriginalDigest, in
+// layer order.
+func mergeGPUFiles(paths []string, layers []Layer, opt MergeOption, target string,
+	rafsBlobDigests []string, rafsBlobSizes []int64, rafsBlobTOCDigests []string) ([]digest.Digest, error) {
 	boots := make([][]byte, len(paths))
 	hexes := make([]string, len(paths))
+	var rafs []*gpu.RafsBlob
+	j := 0
 	for i, p := range paths {
 		b, err := os.ReadFile(p)
 		if err != nil {
 			return nil, errors.Wrap(err, "read source bootstrap")
 		}
-		boots[i], hexes[i] = b, layers[i].Digest.Hex()
+		boots[i], hexes[i] = b, filepath.Base(p)
+		if layers[i].OriginalDigest != nil {
+			if j >= len(rafsBlobDigests) || j >= len(rafsBlobSizes) || j >= len(rafsBlobTOCDigests) {
+				return nil, fmt.Errorf("targz-ref layer %d without its RAFS blob entry", i)
+			}
+			if rafs == nil {
+				rafs = make([]*gpu.RafsBlob, len(paths))
+			}
+			rafs[i] = &gpu.RafsBlob{Digest: rafsBlobDigests[j], Size: rafsBlobSizes[j],
+				TOCDigest: rafsBlobTOCDigests[j]}
+			j++
+		}
 	}
 	f, err := os.Create(target)
 	if err != nil {
 		return nil, errors.Wrap(err, "create target bootstrap")
 	}
 	defer f.Close()
-	return mergeGPU(boots, hexes, opt, f)
+	return mergeGPU(boots, hexes, opt, rafs, f)
 }
 
 // unpackGPU replaces unpackNydusBlob + tool.Unpack (convert_unix.go:669-719)

@@ -33,10 +33,13 @@ import (
 	"bytes"
 	"context"
 	"encoding/hex"
+	"errors"
 	"fmt"
 	"io"
 	"os"
+	"runtime"
 	"strings"
+	"sync"
 	"sync/atomic"
 	"unsafe"
 
@@ -137,20 +140,71 @@ func (g *Engine) PackTar(tar []byte) ([]Chunk, []Result, error) {
 // (`data | tar_header | ... | toc | tar_header`) to dest.  The library writes
 // the stream to a file descriptor (ngpu_write_fd); a pipe + goroutine carries
 // it to dest, as the FIFO does in packFromTar (convert_unix.go:454-496).
+//
+// Every way a Pack can end releases it exactly once (packState.end): Close;
+// a failed Write / ReadFrom; a source read error inside ReadFrom; ctx.Done()
+// -- also when no Write or Close ever comes again, which is what the
+// reference's LayerConvertFunc does on its error paths (convert_unix.go:
+// 885-907 skips tw.Close() after a copy error or ctx.Done()); and, as a last
+// resort, a finalizer when the writer becomes unreachable unclosed (the
+// tr.Close() error path, with a context that is never cancelled).  The
+// library's retained HBM layer, pinned staging slots and emitter thread and
+// this package's pipe goroutine all go with it.
 type PackWriter struct {
-	g      *Engine
+	s    *packState
+	g    *C.ngpu_engine
+	Part int // node index of the engine the Pack runs on (-1: a single engine)
+}
+
+// packState is what the AfterFunc and the finalizer reach (never the
+// PackWriter itself, so that an unclosed writer can become unreachable).
+type packState struct {
+	mu     sync.Mutex // held across every library call on p
 	p      *C.ngpu_pack
-	dest   io.Writer
 	opt    C.ngpu_blob_options
 	cancel *C.int32_t // C memory: the library polls it (ngpu_pack_set_cancel)
 	stop   func() bool
-	pw     *os.File   // the stream's pipe: the library writes, a goroutine copies to dest
+	refs   int      // holders of cancel: the pack side and the AfterFunc side
+	pw     *os.File // the stream's pipe: the library writes, a goroutine copies to dest
 	copied chan error
 }
 
-// Pack opens a streaming pack against dict (nil = no chunk dict).  ctx.Done() -- including
-// PackOption.Timeout's deadline, builder.go:153-158 -- stores 1 into the cancel flag; the running
-// Write/Close then fails with NGPU_ECANCELED, as a killed builder fails the reference's Pack.
+// end releases the pack if it is still open (abort: it has not been
+// finished), closes the pipe so the copy goroutine ends, and drops the pack
+// side's hold on the cancel flag.  Called with mu held.
+func (s *packState) end(abort bool) {
+	if s.p != nil && abort {
+		C.ngpu_pack_abort(s.p)
+	}
+	s.p = nil
+	if s.pw != nil {
+		s.pw.Close()
+		s.pw = nil
+	}
+	if s.opt.prefetch_patterns != nil {
+		C.free(unsafe.Pointer(s.opt.prefetch_patterns))
+		s.opt.prefetch_patterns = nil
+	}
+	if s.stop != nil {
+		if s.stop() { // the AfterFunc will never run: its hold goes too
+			s.refs--
+		}
+		s.stop = nil
+		s.unrefFlag()
+	}
+}
+
+func (s *packState) unrefFlag() { // mu held
+	if s.refs--; s.refs == 0 {
+		C.free(unsafe.Pointer(s.cancel))
+		s.cancel = nil
+	}
+}
+
+// Pack opens a streaming pack against dict (nil = no chunk dict) on this engine.  ctx.Done() --
+// including PackOption.Timeout's deadline, builder.go:153-158 -- stores 1 into the cancel flag
+// (the running Write/ReadFrom/Close fails with NGPU_ECANCELED at its next staging slot, as a
+// killed builder fails the reference's Pack) and then releases the pack.
 // fsVersion 5 or 6 picks the bootstrap format; prefetch is PackOption.PrefetchPatterns (the
 // builder's stdin, "" = "/"), written as the bootstrap's prefetch table.
 // The output is given at open (ngpu_pack_set_output, ABI 4): the library writes the stream while
@@ -160,61 +214,87 @@ type PackWriter struct {
 func (g *Engine) Pack(ctx context.Context, dest io.Writer, compressor, fsVersion uint32, prefetch string,
 	dict *ChunkDict, ociRef bool) (*PackWriter, error) {
 	var p *C.ngpu_pack
-	var d *C.ngpu_dict
-	if dict != nil {
-		d = dict.d
-	}
-	flags := C.uint32_t(C.NGPU_PACK_RETAIN)
-	if ociRef {
-		flags = C.NGPU_PACK_OCIREF // no chunk data in the stream: nothing to retain
-	}
-	if rc := C.ngpu_pack_open_dict(g.e, d, flags, &p); rc != 0 {
+	if rc := C.ngpu_pack_open_dict(g.e, dictOf(dict), packFlags(ociRef), &p); rc != 0 {
 		return nil, errOf(g.e, rc, "pack open")
 	}
-	flag := (*C.int32_t)(C.calloc(1, 4))
-	C.ngpu_pack_set_cancel(p, flag)
-	stop := context.AfterFunc(ctx, func() { atomic.StoreInt32((*int32)(unsafe.Pointer(flag)), 1) })
-	w := &PackWriter{g: g, p: p, dest: dest, cancel: flag, stop: stop, copied: make(chan error, 1),
+	return startPack(ctx, p, -1, dest, compressor, fsVersion, prefetch)
+}
+
+func dictOf(d *ChunkDict) *C.ngpu_dict {
+	if d == nil {
+		return nil
+	}
+	return d.d
+}
+
+func packFlags(ociRef bool) C.uint32_t {
+	if ociRef {
+		return C.NGPU_PACK_OCIREF // no chunk data in the stream: nothing to retain
+	}
+	return C.NGPU_PACK_RETAIN
+}
+
+func startPack(ctx context.Context, p *C.ngpu_pack, part int, dest io.Writer, compressor, fsVersion uint32,
+	prefetch string) (*PackWriter, error) {
+	e := C.ngpu_pack_engine(p)
+	s := &packState{p: p, refs: 2, copied: make(chan error, 1),
+		cancel: (*C.int32_t)(C.calloc(1, 4)),
 		opt: C.ngpu_blob_options{compressor: C.uint32_t(compressor), fs_version: C.uint32_t(fsVersion),
-			prefetch_patterns: C.CString(prefetch)}} // freed in done()
+			prefetch_patterns: C.CString(prefetch)}}
+	C.ngpu_pack_set_cancel(p, s.cancel)
+	s.mu.Lock()
+	defer s.mu.Unlock()
+	s.stop = context.AfterFunc(ctx, func() {
+		atomic.StoreInt32((*int32)(unsafe.Pointer(s.cancel)), 1) // a running call returns soon
+		s.mu.Lock()
+		defer s.mu.Unlock()
+		s.end(true) // (after Close it finds nothing left to release)
+		s.unrefFlag()
+	})
 	r, pw, err := os.Pipe()
 	if err != nil {
-		C.ngpu_pack_abort(p)
-		w.done()
+		s.end(true)
 		return nil, err
 	}
-	w.pw = pw
-	go func() { _, err := io.Copy(dest, r); r.Close(); w.copied <- err }()
-	if rc := C.ngpu_pack_set_output(p, &w.opt, C.ngpu_write_fn(C.ngpu_write_fd),
+	s.pw = pw
+	copied := s.copied
+	go func() { _, err := io.Copy(dest, r); r.Close(); copied <- err }()
+	if rc := C.ngpu_pack_set_output(p, &s.opt, C.ngpu_write_fn(C.ngpu_write_fd),
 		unsafe.Pointer(uintptr(pw.Fd()))); rc != 0 {
-		err := errOf(g.e, rc, "pack output")
-		C.ngpu_pack_abort(p)
-		pw.Close()
-		<-w.copied
-		w.done()
+		err := errOf(e, rc, "pack output")
+		s.end(true)
+		<-copied
 		return nil, err
 	}
+	w := &PackWriter{s: s, g: e, Part: part}
+	runtime.SetFinalizer(w, func(w *PackWriter) {
+		w.s.mu.Lock()
+		w.s.end(true)
+		w.s.mu.Unlock()
+	})
 	return w, nil
 }
 
-func (w *PackWriter) done() {
-	C.free(unsafe.Pointer(w.opt.prefetch_patterns))
-	w.opt.prefetch_patterns = nil
-	if w.stop() { // AfterFunc did not run: nobody touches the flag any more
-		C.free(unsafe.Pointer(w.cancel))
-	} // else it ran; the flag leaks its 4 bytes rather than racing the store
+func (w *PackWriter) ended() error {
+	return fmt.Errorf("gpu pack: %w", errPackEnded)
 }
+
+var errPackEnded = errors.New("pack ended (cancelled, failed or closed)")
 
 // Write copies synchronously into engine-pinned staging (no Go pointer is retained).
 func (w *PackWriter) Write(b []byte) (int, error) {
+	s := w.s
+	s.mu.Lock()
+	defer s.mu.Unlock()
+	if s.p == nil {
+		return 0, w.ended()
+	}
 	if len(b) == 0 {
 		return 0, nil
 	}
-	if rc := C.ngpu_pack_write(w.p, unsafe.Pointer(&b[0]), C.uint64_t(len(b))); rc != 0 {
-		err := errOf(w.g.e, rc, "pack write")
-		C.ngpu_pack_abort(w.p) // a failed write leaves the pack open
-		w.p = nil
-		w.done()
+	if rc := C.ngpu_pack_write(s.p, unsafe.Pointer(&b[0]), C.uint64_t(len(b))); rc != 0 {
+		err := errOf(w.g, rc, "pack write")
+		s.end(true) // a failed write leaves the pack open
 		return 0, err
 	}
 	return len(b), nil
@@ -223,26 +303,31 @@ func (w *PackWriter) Write(b []byte) (int, error) {
 // ReadFrom lets io.Copy(w, src) -- how packLayer and LayerConvertFunc feed a Pack
 // (converter_test.go:283-291, convert_unix.go:870-914) -- read the tar straight into the
 // engine's pinned staging (ngpu_pack_reserve / ngpu_pack_commit): the reader fills C memory, so
-// there is neither io.Copy's intermediate buffer nor Write's copy into staging.
+// there is neither io.Copy's intermediate buffer nor Write's copy into staging.  The source reads
+// into the pack's staging, so the pack stays held (mu) while src.Read runs; a ctx.Done() meanwhile
+// takes effect when that read returns.  A source error ends the pack: LayerConvertFunc will not
+// call Close after it (convert_unix.go:894-897).
 func (w *PackWriter) ReadFrom(src io.Reader) (int64, error) {
+	s := w.s
+	s.mu.Lock()
+	defer s.mu.Unlock()
 	var total int64
 	for {
+		if s.p == nil {
+			return total, w.ended()
+		}
 		var p unsafe.Pointer
 		var avail C.uint64_t
-		if rc := C.ngpu_pack_reserve(w.p, &p, &avail); rc != 0 {
-			err := errOf(w.g.e, rc, "pack reserve")
-			C.ngpu_pack_abort(w.p)
-			w.p = nil
-			w.done()
+		if rc := C.ngpu_pack_reserve(s.p, &p, &avail); rc != 0 {
+			err := errOf(w.g, rc, "pack reserve")
+			s.end(true)
 			return total, err
 		}
 		n, err := src.Read(unsafe.Slice((*byte)(p), int(avail)))
 		if n > 0 {
-			if rc := C.ngpu_pack_commit(w.p, C.uint64_t(n)); rc != 0 {
-				e := errOf(w.g.e, rc, "pack commit")
-				C.ngpu_pack_abort(w.p)
-				w.p = nil
-				w.done()
+			if rc := C.ngpu_pack_commit(s.p, C.uint64_t(n)); rc != 0 {
+				e := errOf(w.g, rc, "pack commit")
+				s.end(true)
 				return total, e
 			}
 			total += int64(n)
@@ -251,6 +336,7 @@ func (w *PackWriter) ReadFrom(src io.Reader) (int64, error) {
 			return total, nil
 		}
 		if err != nil {
+			s.end(true)
 			return total, err
 		}
 	}
@@ -259,19 +345,26 @@ func (w *PackWriter) ReadFrom(src io.Reader) (int64, error) {
 // Close runs the final dedup, writes the rest of the stream and returns the layer digest
 // (sha256 of the stream).
 func (w *PackWriter) Close() (digest.Digest, error) {
+	s := w.s
+	s.mu.Lock()
+	defer s.mu.Unlock()
+	runtime.SetFinalizer(w, nil)
+	if s.p == nil {
+		return "", w.ended()
+	}
 	var pc *C.ngpu_chunk
 	var pr *C.ngpu_result
 	var n C.uint64_t
 	var st C.ngpu_layer_stats
 	var info C.ngpu_blob_info
-	rc := C.ngpu_pack_finish(w.p, nil, nil, nil, &pc, &pr, &n, &st, &info)
-	w.pw.Close()
-	w.done()
-	if err := <-w.copied; err != nil && rc == 0 {
+	rc := C.ngpu_pack_finish(s.p, nil, nil, nil, &pc, &pr, &n, &st, &info) // releases it
+	copied := s.copied
+	s.end(false)
+	if err := <-copied; err != nil && rc == 0 {
 		return "", err
 	}
 	if rc != 0 {
-		return "", errOf(w.g.e, rc, "pack close")
+		return "", errOf(w.g, rc, "pack close")
 	}
 	C.ngpu_free_host(unsafe.Pointer(pc))
 	C.ngpu_free_host(unsafe.Pointer(pr))
@@ -279,13 +372,25 @@ func (w *PackWriter) Close() (digest.Digest, error) {
 	return digest.NewDigestFromEncoded(digest.SHA256, hex.EncodeToString(sum)), nil
 }
 
+// RafsBlob is a targz-ref layer's entry of Merge's --blob-digests / --blob-sizes /
+// --blob-toc-digests (convert_unix.go:577-590, builder.go:242-253): the hex digest and size of its
+// RAFS blob (the nydus stream) and the hex sha256 of its TOC entry data (calcBlobTOCDigest).
+type RafsBlob struct {
+	Digest    string
+	Size      int64
+	TOCDigest string
+}
+
 // Merge replaces tool.Merge (builder.go:220-294): bootstraps are the layers'
-// image.boot entries (read with the reference's own UnpackEntry), digests the
-// layers' Digest.Hex(), lowest layer first; parentBoot is ParentBootstrapPath's
-// contents (nil = none), prefetch MergeOption.PrefetchPatterns.  Returns the
-// merged bootstrap (the overlaid inode tree, RAFS v5 or v6 as the layers) and
-// the blob ids.
-func Merge(boots [][]byte, digests []string, dictBoot, parentBoot []byte, prefetch string) ([]byte, []string, error) {
+// image.boot entries (read with the reference's own UnpackEntry), names the
+// bootstrap file names Merge gives nydus-image (Digest.Hex(), or
+// OriginalDigest.Hex() for a targz-ref layer, getBootstrapPath), lowest layer
+// first; parentBoot is ParentBootstrapPath's contents (nil = none), prefetch
+// MergeOption.PrefetchPatterns; rafs[l] is non-nil for a targz-ref layer (nil
+// slice: none).  Returns the merged bootstrap (the overlaid inode tree, RAFS v5
+// or v6 as the layers) and the blob ids.
+func Merge(boots [][]byte, digests []string, dictBoot, parentBoot []byte, prefetch string,
+	rafs []*RafsBlob) ([]byte, []string, error) {
 	n := len(boots)
 	ptrs := C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(uintptr(0))))
 	sizes := C.malloc(C.size_t(n) * 8)
@@ -316,14 +421,36 @@ func Merge(boots [][]byte, digests []string, dictBoot, parentBoot []byte, prefet
 	}
 	mo.prefetch_patterns = C.CString(prefetch)
 	defer C.free(unsafe.Pointer(mo.prefetch_patterns))
+	var rd, rs, rt unsafe.Pointer // targz-ref arrays (ngpu_merge_ex2), C memory
+	if len(rafs) == n && n > 0 {
+		rd = C.calloc(C.size_t(n), C.size_t(unsafe.Sizeof(uintptr(0))))
+		rs = C.calloc(C.size_t(n), 8)
+		rt = C.calloc(C.size_t(n), C.size_t(unsafe.Sizeof(uintptr(0))))
+		defer C.free(rd)
+		defer C.free(rs)
+		defer C.free(rt)
+		rdv := unsafe.Slice((**C.char)(rd), n)
+		rsv := unsafe.Slice((*C.uint64_t)(rs), n)
+		rtv := unsafe.Slice((**C.char)(rt), n)
+		for i, r := range rafs {
+			if r == nil {
+				continue
+			}
+			rdv[i] = C.CString(r.Digest)
+			defer C.free(unsafe.Pointer(rdv[i]))
+			rsv[i] = C.uint64_t(r.Size)
+			rtv[i] = C.CString(r.TOCDigest)
+			defer C.free(unsafe.Pointer(rtv[i]))
+		}
+	}
 	r, pw, _ := os.Pipe()
 	var out bytes.Buffer
 	done := make(chan struct{})
 	go func() { io.Copy(&out, r); r.Close(); close(done) }()
 	var ids *C.char
-	rc := C.ngpu_merge_ex((*unsafe.Pointer)(ptrs), (*C.uint64_t)(sizes), (**C.char)(names),
-		C.uint64_t(n), dict, C.uint64_t(len(dictBoot)), &mo, C.ngpu_write_fn(C.ngpu_write_fd),
-		unsafe.Pointer(uintptr(pw.Fd())), &ids)
+	rc := C.ngpu_merge_ex2((*unsafe.Pointer)(ptrs), (*C.uint64_t)(sizes), (**C.char)(names),
+		C.uint64_t(n), dict, C.uint64_t(len(dictBoot)), &mo, (**C.char)(rd), (*C.uint64_t)(rs),
+		(**C.char)(rt), C.ngpu_write_fn(C.ngpu_write_fd), unsafe.Pointer(uintptr(pw.Fd())), &ids)
 	pw.Close()
 	<-done
 	if rc != 0 {
@@ -373,13 +500,15 @@ func Available() bool { return os.Getenv("NYDUS_GPU") != "0" && C.ngpu_device_co
 func DeviceCount() int { return int(C.ngpu_device_count()) }
 
 // Node drives every GPU of the host from this process (SURVEY.md §8(e)): one engine per
-// device, Packs spread round robin, one chunk dict for all of them -- replicated on every GPU or
-// partitioned by digest prefix with the probe exchange over xGMI inside the library.
+// device, each Pack on the least-loaded one (north star: the chunk stream is sharded by layer;
+// containerd's per-layer goroutines, convert_unix.go:467-538, land on every GPU and every GPU's
+// own PCIe link), one chunk dict for all of them -- replicated on every GPU or partitioned by
+// digest prefix with the probe exchange over xGMI inside the library.
 type Node struct{ n *C.ngpu_node }
 
-func NewNode(devices []int32, digester, chunkSize, fsVersion uint32) (*Node, error) {
+func NewNode(devices []int32, digester, chunkSize, fsVersion, flags uint32) (*Node, error) {
 	cfg := C.ngpu_config{digester: C.uint32_t(digester), chunk_size: C.uint32_t(chunkSize),
-		fs_version: C.uint32_t(fsVersion)}
+		fs_version: C.uint32_t(fsVersion), flags: C.uint32_t(flags)}
 	var n *C.ngpu_node
 	if rc := C.ngpu_node_create((*C.int32_t)(unsafe.Pointer(&devices[0])), C.uint32_t(len(devices)), &cfg, &n); rc != 0 {
 		return nil, errOf(nil, rc, "node")
@@ -387,6 +516,9 @@ func NewNode(devices []int32, digester, chunkSize, fsVersion uint32) (*Node, err
 	return &Node{n}, nil
 }
 
+// OpenChunkDict opens `--chunk-dict bootstrap=P` for every engine of the node.  The library
+// caches it per node (an unchanged file opened again returns the same HBM dict), so each Pack can
+// open its own reference.  partition=false keeps a full replica on every GPU (no exchange).
 func (nd *Node) OpenChunkDict(bootstrap string, partition bool) (*ChunkDict, error) {
 	p := C.CString(bootstrap)
 	defer C.free(unsafe.Pointer(p))
@@ -401,8 +533,26 @@ func (nd *Node) OpenChunkDict(bootstrap string, partition bool) (*ChunkDict, err
 	return &ChunkDict{d}, nil
 }
 
-// Engine i of the node, for Pack: `nd.Engine(i % n).Pack(ctx, dest, comp, dict)`.
+// Engine i of the node.
 func (nd *Node) Engine(i int) *Engine { return &Engine{C.ngpu_node_engine(nd.n, C.uint32_t(i))} }
+
+// Pack opens a streaming Pack on the node's least-loaded engine (ngpu_node_pack_open); the
+// writer's Part says which.  Arguments and the writer's behaviour are Engine.Pack's.
+func (nd *Node) Pack(ctx context.Context, dest io.Writer, compressor, fsVersion uint32, prefetch string,
+	dict *ChunkDict, ociRef bool) (*PackWriter, error) {
+	var p *C.ngpu_pack
+	if rc := C.ngpu_node_pack_open(nd.n, dictOf(dict), packFlags(ociRef), &p); rc != 0 {
+		return nil, errOf(C.ngpu_node_engine(nd.n, 0), rc, "node pack open")
+	}
+	part := -1
+	e := C.ngpu_pack_engine(p)
+	for i := 0; i < int(C.ngpu_node_size(nd.n)); i++ {
+		if C.ngpu_node_engine(nd.n, C.uint32_t(i)) == e {
+			part = i
+		}
+	}
+	return startPack(ctx, p, part, dest, compressor, fsVersion, prefetch)
+}
 
 // Step runs one node step (ngpu_node_process_step, ABI 5): every device's part
 // digested, ONE all-to-all-v of digests to their owners and one of hits back

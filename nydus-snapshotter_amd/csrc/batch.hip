@@ -33,6 +33,7 @@
 #include <condition_variable>
 
 #include "batch_lanes.hpp"
+#include "batch_stats.hpp"
 #include "engine_internal.hpp"
 
 namespace ngpu {
@@ -137,17 +138,6 @@ __global__ __launch_bounds__(256) void batch_gather(const GatherRow *__restrict_
     head = w * 16;
   }
   for (uint64_t i = head + t; i < r.len; i += stride) r.dst[i] = r.src[i];
-}
-
-// Each layer's stats into its pack's pinned read-back words (block k: layer k):
-// the call's counters (kStWords) and the layer's own stats at kStatsLayer.
-__global__ void batch_stats_out(const uint64_t *__restrict__ st, const ngpu_layer_stats *__restrict__ lst,
-                                uint64_t *const *__restrict__ dst) {
-  const uint32_t k = blockIdx.x, t = threadIdx.x;
-  constexpr uint32_t kL = sizeof(ngpu_layer_stats) / sizeof(uint64_t);
-  static_assert(sizeof(ngpu_layer_stats) % sizeof(uint64_t) == 0, "layer stats are whole words");
-  if (t < (uint32_t)kStWords) dst[k][t] = st[t];
-  if (t < kL) dst[k][kStatsLayer + t] = reinterpret_cast<const uint64_t *>(lst + k)[t];
 }
 
 constexpr int kWindowUs = 250;
@@ -304,8 +294,9 @@ int launch_batch(ngpu_engine *e, BatchLane &b, const std::vector<BatchJob *> &jo
                        b.d_res, N, b.d_lfirst, (uint32_t)K, reinterpret_cast<ngpu_result **>(b.d_dst));
     HIP_TRY(e, hipGetLastError());
   }
-  hipLaunchKernelGGL(batch_stats_out, dim3((unsigned)K), dim3(64), 0, b.s, sl.ws.stats, b.d_lst,
-                     reinterpret_cast<uint64_t **>(b.d_dst + K));
+  // (each layer's own error words: batch_stats.hpp)
+  hipLaunchKernelGGL(batch_stats_out, dim3((unsigned)K), dim3(256), 0, b.s, sl.ws.stats, b.d_lst,
+                     b.d_res, b.d_lfirst, reinterpret_cast<uint64_t **>(b.d_dst + K));
   HIP_TRY(e, hipGetLastError());
   if (int rc = host_fence(e, b.s)) return rc;
   for (uint64_t k = 0; k < K; ++k) snprintf(jobs[k]->path, sizeof jobs[k]->path, "%s", sl.path);
@@ -362,7 +353,9 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
     int ln = -1;
     for (;;) {
       ln = b.lanes.idle();
-      const bool all_in = b.open.size() >= (size_t)e->open_packs.load() || b.open.size() >= kMaxJobs;
+      // every pack that may still join has (packs already in a running
+      // batch, grown past one slot, OCIRef or closing alone are not counted)
+      const bool all_in = (int)b.open.size() >= e->batch_waitable.load() || b.open.size() >= kMaxJobs;
       if (sha && b.open.size() > joined) {  // a pack joined: restart the window
         joined = b.open.size();
         until = std::min(cap, std::chrono::steady_clock::now() + window);
@@ -390,6 +383,8 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
         ++i;
       }
     }
+    for (BatchJob *x : take) x->uncounted = true;  // (read by its pack after `enqueued`)
+    e->batch_waitable.fetch_sub((int)take.size());
     const int open_now = e->open_packs.load();
     lk.unlock();
     const double t_take = batch_trace_on() ? batch_now_us() : 0;
@@ -434,6 +429,12 @@ int batch_run(ngpu_engine *e, BatchJob &j) {
   }
   if (!ok) return fail(e, NGPU_EHIP, "batch: stream failed");
   return 0;
+}
+
+void batch_wake(ngpu_engine *e) {
+  if (!e->batcher) return;
+  std::lock_guard<std::mutex> g(e->batcher->m);
+  e->batcher->cv.notify_all();
 }
 
 void batch_stats(ngpu_engine *e, uint64_t out[3]) {

@@ -27,6 +27,8 @@
 // decode every entry (tests/test_blob.py).
 #include <dlfcn.h>
 #include <errno.h>
+#include <pthread.h>
+#include <signal.h>
 #include <openssl/evp.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -1137,11 +1139,11 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
     RafsV6BlobInfo &ob = b.blobs[st.own_blob_index];
     uint8_t *bm = ob.meta;
     const uint32_t toc_size = 0;
-    memcpy(bm, &toc_size, 4);
-    memcpy(bm + 4, &ci_algo, 4);
-    memcpy(bm + 8, &ci_off, 8);
-    memcpy(bm + 16, &ci_size, 8);
-    memcpy(bm + 24, &ci_len, 8);
+    memcpy(bm + offsetof(RafsV6BlobMeta, blob_toc_size), &toc_size, 4);
+    memcpy(bm + offsetof(RafsV6BlobMeta, ci_compressor), &ci_algo, 4);
+    memcpy(bm + offsetof(RafsV6BlobMeta, ci_offset), &ci_off, 8);
+    memcpy(bm + offsetof(RafsV6BlobMeta, ci_compressed_size), &ci_size, 8);
+    memcpy(bm + offsetof(RafsV6BlobMeta, ci_uncompressed_size), &ci_len, 8);
     ob.features = feat;
   }
   // image.boot: the inode tree of the layer (rafs.cpp), RAFS v5 or v6
@@ -1293,19 +1295,39 @@ extern "C" {
 
 const char *ngpu_host_error(void) { return host_error(); }
 
+// A reader that went away (the Go side's pipe goroutine ending early, e.g.
+// its dest failed) must fail the write with EPIPE, not raise SIGPIPE in a
+// library thread: SIGPIPE is blocked in this thread around the write, and one
+// it raised is taken back before the mask is restored.
 int ngpu_write_fd(void *ctx, const void *buf, uint64_t len) {
   const int fd = (int)(intptr_t)ctx;
   const uint8_t *p = (const uint8_t *)buf;
+  sigset_t pipe_set, old;
+  sigemptyset(&pipe_set);
+  sigaddset(&pipe_set, SIGPIPE);
+  sigset_t pending;
+  sigemptyset(&pending);
+  sigpending(&pending);
+  const bool was_pending = sigismember(&pending, SIGPIPE) == 1;
+  pthread_sigmask(SIG_BLOCK, &pipe_set, &old);
+  int rc = 0;
   while (len) {
     const ssize_t r = write(fd, p, len > (1ull << 30) ? (1ull << 30) : len);
     if (r < 0) {
       if (errno == EINTR) continue;
-      return host_fail(NGPU_EIO, "write(fd %d): %s", fd, strerror(errno));
+      const int en = errno;
+      if (en == EPIPE && !was_pending) {
+        const struct timespec zero = {0, 0};
+        (void)sigtimedwait(&pipe_set, nullptr, &zero);  // ours: take it back
+      }
+      rc = host_fail(NGPU_EIO, "write(fd %d): %s", fd, strerror(en));
+      break;
     }
     p += r;
     len -= (uint64_t)r;
   }
-  return 0;
+  pthread_sigmask(SIG_SETMASK, &old, nullptr);
+  return rc;
 }
 
 int ngpu_blob_write(const void *data, uint64_t len, const ngpu_chunk *chunks,
@@ -1580,6 +1602,16 @@ int ngpu_merge_ex(const void *const *bootstraps, const uint64_t *sizes,
                   const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
                   uint64_t dict_size, const ngpu_merge_options *opt, ngpu_write_fn w, void *ctx,
                   char **blob_ids_out) {
+  return ngpu_merge_ex2(bootstraps, sizes, layer_digests, n, dict_bootstrap, dict_size, opt,
+                        nullptr, nullptr, nullptr, w, ctx, blob_ids_out);
+}
+
+int ngpu_merge_ex2(const void *const *bootstraps, const uint64_t *sizes,
+                   const char *const *layer_digests, uint64_t n, const void *dict_bootstrap,
+                   uint64_t dict_size, const ngpu_merge_options *opt,
+                   const char *const *rafs_blob_digests, const uint64_t *rafs_blob_sizes,
+                   const char *const *rafs_blob_toc_digests, ngpu_write_fn w, void *ctx,
+                   char **blob_ids_out) {
   const int rc = guarded([&]() -> int {
     if ((n && (!bootstraps || !sizes)) || !blob_ids_out ||
         (opt && opt->parent_size && !opt->parent_bootstrap))
@@ -1621,13 +1653,13 @@ int ngpu_merge_ex(const void *const *bootstraps, const uint64_t *sizes,
       // its whole nydus tar stream, which Merge receives as Layer.Digest and
       // uses as the bootstrap file name (convert_unix.go:567-573, 595-599).
       if (layer_digests && layer_digests[l]) m.own_name = layer_digests[l];
-      if (opt && opt->rafs_blob_digests && opt->rafs_blob_digests[l]) {  // targz-ref layer
-        if (!opt->rafs_blob_sizes || !opt->rafs_blob_toc_digests || !opt->rafs_blob_toc_digests[l] ||
-            !unhex32(opt->rafs_blob_digests[l], m.rafs_blob_digest) ||
-            !unhex32(opt->rafs_blob_toc_digests[l], m.toc_digest))
+      if (rafs_blob_digests && rafs_blob_digests[l]) {  // targz-ref layer
+        if (!rafs_blob_sizes || !rafs_blob_toc_digests || !rafs_blob_toc_digests[l] ||
+            !unhex32(rafs_blob_digests[l], m.rafs_blob_digest) ||
+            !unhex32(rafs_blob_toc_digests[l], m.toc_digest))
           return host_fail(NGPU_EINVAL, "ngpu_merge: layer %llu: bad RAFS blob / TOC digest",
                            (unsigned long long)l);
-        m.rafs_blob_size = opt->rafs_blob_sizes[l];
+        m.rafs_blob_size = rafs_blob_sizes[l];
         m.ref = true;
       }
       in.push_back(m);

@@ -6,6 +6,8 @@
 // Not installed.
 #pragma once
 
+#include <stddef.h>
+
 #include <stdint.h>
 
 #include <memory>
@@ -57,7 +59,34 @@ struct TocEntry {  // 128 B, pkg/converter/types.go:147-163
   uint64_t uncompressed_size;
   uint8_t reserved2[48];  // Go reads the first 124 B of each 128-B entry (types.go:147-163, convert_unix.go:220)
 };
+// RafsV6BlobInfo::meta, field by field ([nydus v2.3.0] RafsV6Blob,
+// rafs/src/metadata/layout/v6.rs, restated).  Bytes 104..135 are pinned by the
+// reference v6 fixture's blob record (blob_toc_size 0, ci_compressor 1,
+// ci_offset = the blob's compressed size, 35,949 / 40,240 ci bytes); the
+// toc / meta digests and blob_meta_size that follow (a merged targz-ref
+// bootstrap's --blob-toc-digests / --blob-digests / --blob-sizes) are
+// restated only: parity unpinned.
+struct RafsV6BlobMeta {
+  uint32_t blob_toc_size;
+  uint32_t ci_compressor;
+  uint64_t ci_offset;
+  uint64_t ci_compressed_size;
+  uint64_t ci_uncompressed_size;
+  uint8_t blob_toc_digest[32];
+  uint8_t blob_meta_digest[32];
+  uint64_t blob_meta_size;
+  uint8_t reserved[48];
+};
 #pragma pack(pop)
+static_assert(sizeof(RafsV6BlobMeta) == sizeof(((RafsV6BlobInfo *)0)->meta), "RafsV6Blob tail is 152 B");
+static_assert(offsetof(RafsV6BlobInfo, meta) == 104, "RafsV6Blob: ci fields start at 104");
+static_assert(offsetof(RafsV6BlobInfo, meta) + offsetof(RafsV6BlobMeta, ci_offset) == 112, "ci_offset @112");
+static_assert(offsetof(RafsV6BlobInfo, meta) + offsetof(RafsV6BlobMeta, blob_toc_digest) == 136,
+              "blob_toc_digest @136");
+static_assert(offsetof(RafsV6BlobInfo, meta) + offsetof(RafsV6BlobMeta, blob_meta_digest) == 168,
+              "blob_meta_digest @168");
+static_assert(offsetof(RafsV6BlobInfo, meta) + offsetof(RafsV6BlobMeta, blob_meta_size) == 200,
+              "blob_meta_size @200");
 static_assert(sizeof(RafsV6ChunkInfo) == 80, "RAFS v6 chunk info is 80 bytes");
 static_assert(sizeof(RafsV6BlobInfo) == 256, "RAFS v6 blob info is 256 bytes");
 static_assert(sizeof(TocEntry) == 128, "TOC entry is 128 bytes");

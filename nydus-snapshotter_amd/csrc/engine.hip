@@ -529,10 +529,11 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   if (c.fs_version != 5 && c.fs_version != 6) return NGPU_EINVAL;
   if (c.digester != NGPU_DIGEST_BLAKE3 && c.digester != NGPU_DIGEST_SHA256) return NGPU_EINVAL;
   if (c.leaves_per_lane & (c.leaves_per_lane - 1) || c.leaves_per_lane > 16) return NGPU_EINVAL;
-  // SHA-256 kernel override (benchmarks): 1 + {0 split, 1 pair, 2 lane, 4 pair
-  // one group per workgroup, 5 pair four groups}; anything else is rejected
+  // SHA-256 kernel override (benchmarks): 1 + {0 split, 1 pair, 2 lane, 3 pair
+  // with off-chain K+W loads, 4 pair one group per workgroup, 5 pair four
+  // groups, 6 = 3 with asm-ordered rounds}: every 3-bit value is a kernel
   switch ((c.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7) {
-    case 0: case 1: case 2: case 3: case 5: case 6: break;
+    case 0: case 1: case 2: case 3: case 4: case 5: case 6: case 7: break;
     default: return NGPU_EINVAL;
   }
   // BLAKE3 load-mode override: only modes this build has a kernel for, all of
@@ -942,6 +943,19 @@ int ngpu_last_timing(ngpu_engine *e, ngpu_timing *out) { return ngpu_timing_at(e
 int ngpu_batch_stats(ngpu_engine *e, uint64_t out[3]) {
   if (!e || !out) return NGPU_EINVAL;
   batch_stats(e, out);
+  return 0;
+}
+
+int ngpu_engine_counters_get(ngpu_engine *e, ngpu_engine_counters *out) {
+  if (!e || !out) return NGPU_EINVAL;
+  memset(out, 0, sizeof *out);
+  out->open_packs = (uint64_t)e->open_packs.load();
+  out->batch_waitable = (uint64_t)e->batch_waitable.load();
+  std::lock_guard<std::mutex> g(e->pool_mu);
+  out->staging_pool_bufs = e->staging_pool.size();
+  out->staging_pool_bytes = e->staging_pool_bytes;
+  out->pack_pool = e->pack_pool.size();
+  out->land_pool = e->land_pool.size();
   return 0;
 }
 

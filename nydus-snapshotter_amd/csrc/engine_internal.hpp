@@ -66,6 +66,7 @@ struct ngpu_dict {
   std::string path;
   uint64_t st_dev = 0, st_ino = 0, st_size = 0;
   int64_t st_mtime_ns = 0;
+  uint32_t node_mode = 0;  // ngpu_node_dict_open cache: the mode it was opened with
   // node dicts (node.hip): one part per node device -- a digest-prefix shard
   // (its records carry their global entry ids) or a full replica.
   // dev.m / dev.n_blobs are the global counts; dev.rec / dev.table stay null.
@@ -139,6 +140,7 @@ struct BatchJob {
   uint32_t batch_layers = 0;         // layers in the launch set it joined
   int lane = 0;                      // the batch lane it ran on
   uint64_t seq = 0;                  // its batch's number (the lane's end marker)
+  bool uncounted = false;            // taken: the leader took it out of e->batch_waitable
   char path[48] = "";                // the batch's digest kernels (error messages)
   std::shared_ptr<BatchEvent> done;
 };
@@ -159,6 +161,9 @@ struct ngpu_engine {
   std::mutex h2d_mu[kCopyLanes], d2h_mu[kCopyLanes];
   uint32_t copy_rr = 0;  // next pack's lane (e->mu)
   std::atomic<int> open_packs{0};    // packs opened and not yet ended
+  // open packs that may still join a batch at close (one staging slot of tar
+  // so far, not OCIRef, batching on): what a batch leader waits for
+  std::atomic<int> batch_waitable{0};
   uint64_t uid = 0;          // unique for the process's lifetime (node exchange channels)
   ngpu_config cfg{};
   int device = 0;
@@ -223,6 +228,8 @@ int fail(ngpu_engine *e, int code, const char *fmt, ...);
 // has run and its results / stats are in j.h_res / j.h_stats.
 int batch_run(ngpu_engine *e, BatchJob &j);
 void batch_stats(ngpu_engine *e, uint64_t out[3]);  // batches, layers, most layers in one
+// A waiting batch leader re-checks its wait (e->batch_waitable went down).
+void batch_wake(ngpu_engine *e);
 Batcher *batcher_new();
 void batcher_free(ngpu_engine *e);
 // Pick the workspace slot for a stage on stream s and make it e->cur (e->mu

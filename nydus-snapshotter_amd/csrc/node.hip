@@ -61,7 +61,11 @@ struct StepBuf {
 struct ngpu_node {
   std::vector<ngpu_engine *> eng;  // one per listed device (a reference each)
   std::vector<int> dev;
-  std::atomic<uint64_t> rr{0};     // round robin over the engines for Packs
+  std::atomic<uint64_t> rr{0};     // where a Pack's least-loaded search starts (ties)
+  std::mutex place_mu;             // one placement at a time: concurrent opens spread evenly
+  // node dicts opened by path (one reference each; ngpu_node_dict_open)
+  std::vector<ngpu_dict *> dict_cache;
+  std::mutex cache_mu;
   bool peer_ok = true;             // every pair of distinct devices has peer access
   // node steps (ngpu_node_process_step): one at a time, buffers per part,
   // the RCCL communicator of the node's devices once a step asked for it
@@ -253,8 +257,10 @@ namespace {
 int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint8_t *blobs,
                     uint32_t n_blobs, uint32_t mode, ngpu_dict **out) {
   ngpu_engine *e0 = node->eng[0];
-  const bool copy = (mode & NGPU_NODE_EXCHANGE_COPY) != 0;
-  mode &= ~NGPU_NODE_EXCHANGE_COPY;
+  const bool routed = (mode & NGPU_NODE_EXCHANGE_ROUTED) != 0;
+  if ((mode & NGPU_NODE_EXCHANGE_COPY) && routed)
+    return fail(e0, NGPU_EINVAL, "node dict: copy and routed exchange both asked for");
+  mode &= ~(NGPU_NODE_EXCHANGE_COPY | NGPU_NODE_EXCHANGE_ROUTED);
   if (mode != NGPU_NODE_DICT_PARTITION && mode != NGPU_NODE_DICT_REPLICATE)
     return fail(e0, NGPU_EINVAL, "bad node dict mode %u", mode);
   if (m >= 0xFFFFFFFFull) return fail(e0, NGPU_EINVAL, "chunk dict too large");
@@ -273,9 +279,11 @@ int node_dict_build(ngpu_node *node, const uint8_t *recs, uint64_t m, const uint
   d->digester = e0->cfg.digester;
   d->chunk_size = e0->cfg.chunk_size;
   d->replicated = mode == NGPU_NODE_DICT_REPLICATE;
-  // routed exchange unless asked for the copy exchange or a pair of devices
-  // lacks peer access (its kernels could not reach the requester's HBM)
-  d->routed = !d->replicated && !copy && node->peer_ok;
+  // the copy exchange (DMA peer copies) unless the routed one was asked for
+  // and every pair of devices has peer access (its kernels reach the
+  // requester's HBM): the routed exchange's peer stores have not met two
+  // distinct GPUs yet
+  d->routed = !d->replicated && routed && node->peer_ok;
   d->dev.m = m;
   d->dev.n_blobs = nb;
   d->place.resize(m);
@@ -682,6 +690,14 @@ int ngpu_node_create(const int32_t *devices, uint32_t n, const ngpu_config *cfg,
 
 void ngpu_node_destroy(ngpu_node *node) {
   if (!node) return;
+  {
+    std::vector<ngpu_dict *> cache;
+    {
+      std::lock_guard<std::mutex> g(node->cache_mu);
+      cache.swap(node->dict_cache);
+    }
+    for (ngpu_dict *d : cache) dict_unref(d);  // the cache's references (packs keep their own)
+  }
   step_free(node);
   for (ngpu_engine *e : node->eng) ngpu_destroy(e);
   delete node;
@@ -715,17 +731,82 @@ int ngpu_node_dict_open(ngpu_node *node, const char *path, uint32_t mode, ngpu_d
     struct stat st;
     ngpu_engine *e0 = node->eng[0];
     if (stat(path, &st) != 0) return fail(e0, NGPU_EIO, "stat chunk dict %s", path);
+    const int64_t mt = (int64_t)st.st_mtim.tv_sec * 1000000000 + st.st_mtim.tv_nsec;
+    auto same = [&](const ngpu_dict *d) {
+      return d->path == path && d->node_mode == mode && d->st_dev == (uint64_t)st.st_dev &&
+             d->st_ino == (uint64_t)st.st_ino && d->st_size == (uint64_t)st.st_size &&
+             d->st_mtime_ns == mt;
+    };
+    std::vector<ngpu_dict *> drop;
+    {
+      std::lock_guard<std::mutex> g(node->cache_mu);
+      for (ngpu_dict *d : node->dict_cache)
+        if (same(d)) {
+          dict_ref(d);
+          *out = d;
+          return 0;
+        }
+    }
     std::vector<uint8_t> recs, blobs;
     if (int rc = read_dict_bootstrap(e0, path, (uint64_t)st.st_size, &recs, &blobs)) return rc;
-    return node_dict_build(node, recs.data(), recs.size() / 80, blobs.data(),
-                           (uint32_t)(blobs.size() / 256), mode, out);
+    ngpu_dict *d = nullptr;
+    if (int rc = node_dict_build(node, recs.data(), recs.size() / 80, blobs.data(),
+                                 (uint32_t)(blobs.size() / 256), mode, &d))
+      return rc;
+    d->path = path;
+    d->node_mode = mode;
+    d->st_dev = (uint64_t)st.st_dev;
+    d->st_ino = (uint64_t)st.st_ino;
+    d->st_size = (uint64_t)st.st_size;
+    d->st_mtime_ns = mt;
+    {
+      std::lock_guard<std::mutex> g(node->cache_mu);
+      auto &c = node->dict_cache;
+      for (ngpu_dict *x : c)
+        if (same(x)) {  // another thread loaded it meanwhile: share that one
+          dict_ref(x);
+          drop.push_back(d);
+          d = x;
+          break;
+        }
+      if (std::find(c.begin(), c.end(), d) == c.end()) {
+        for (size_t i = 0; i < c.size();)  // older loads of the path (same mode) go
+          if (c[i]->path == path && c[i]->node_mode == mode) {
+            drop.push_back(c[i]);
+            c.erase(c.begin() + (long)i);
+          } else {
+            ++i;
+          }
+        if (c.size() >= 8) {
+          drop.push_back(c.front());
+          c.erase(c.begin());
+        }
+        dict_ref(d);  // the cache's reference
+        c.push_back(d);
+      }
+    }
+    for (ngpu_dict *x : drop) dict_unref(x);
+    *out = d;
+    return 0;
   });
 }
 
+// Layers shard over the node's GPUs (north star; convert_unix.go:467-538 runs
+// one per goroutine): each Pack goes to the engine with the fewest open packs,
+// the search starting one further each time so that ties rotate.
 int ngpu_node_pack_open(ngpu_node *node, ngpu_dict *dict, uint32_t flags, ngpu_pack **out) {
   if (!node || !out) return NGPU_EINVAL;
-  const uint64_t i = node->rr.fetch_add(1, std::memory_order_relaxed) % node->eng.size();
-  return ngpu_pack_open_dict(node->eng[i], dict, flags, out);
+  const size_t W = node->eng.size();
+  std::lock_guard<std::mutex> g(node->place_mu);
+  const uint64_t r = node->rr.fetch_add(1, std::memory_order_relaxed);
+  size_t best = r % W;
+  int load = node->eng[best]->open_packs.load();
+  for (size_t k = 1; k < W; ++k) {
+    const size_t i = (r + k) % W;
+    const int l = node->eng[i]->open_packs.load();
+    if (l < load) best = i, load = l;
+  }
+  return ngpu_pack_open_dict(node->eng[best], dict, flags, out);
 }
 
 int ngpu_node_process_device(ngpu_node *node, uint32_t i, ngpu_dict *dict, const void *d_data,

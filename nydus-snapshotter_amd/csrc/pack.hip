@@ -213,6 +213,9 @@ struct ngpu_pack : TarSink {
   std::vector<TarEntry> entries;  // NGPU_PACK_RETAIN: the tar's entries (the bootstrap's inode tree)
   Emit *em = nullptr;              // ngpu_pack_set_output: the stream leaves while the tar arrives
   std::unique_ptr<GzipIndexer> gz; // NGPU_PACK_OCIREF: the gzip blob is inflated and indexed
+  // counted in e->batch_waitable: it may still join a batch at its close, so
+  // a batch leader waits for it (batch.hip)
+  bool waitable = false;
   int err = 0;
 
   std::chrono::steady_clock::time_point born = std::chrono::steady_clock::now();
@@ -243,6 +246,15 @@ bool cancelled(const ngpu_pack *p) {
   return p->cancel && __atomic_load_n(p->cancel, __ATOMIC_RELAXED) != 0;
 }
 
+// The pack can no longer join a batch (its layer outgrew one staging slot, it
+// closes outside one, or it ends): a leader stops waiting for it.
+void not_waitable(ngpu_pack *p) {
+  if (!p->waitable) return;
+  p->waitable = false;
+  p->e->batch_waitable.fetch_sub(1);
+  batch_wake(p->e);
+}
+
 void emit_stop(ngpu_pack *p);  // below
 
 void release(ngpu_pack *p) {
@@ -251,6 +263,7 @@ void release(ngpu_pack *p) {
   ngpu_dict *dict = p->dict;
   DeviceGuard dg(e->device);
   ptrace(p, "release");
+  not_waitable(p);
   emit_stop(p);
   // the stream's writer goes first: its sink may still hold raw pieces of the
   // pinned staging slots (src_stable, emit_range_host) until it has drained
@@ -496,6 +509,7 @@ int switch_slot(ngpu_pack *p) {
   const uint64_t carry_from = k < p->chunks.size() ? p->chunks[k].offset : end;
   const uint64_t carry = end - carry_from;
   if (carry >= p->cap) return fail(p->e, NGPU_EINVAL, "chunk larger than a staging slot");
+  not_waitable(p);  // more than one slot of tar: its close cannot batch
   {
     std::lock_guard<std::mutex> g(p->e->mu);  // the engine lock covers the enqueue only
     int rc = dispatch(p, s, p->dispatched, k);
@@ -970,6 +984,10 @@ static int pack_open(ngpu_engine *e, ngpu_dict *dict, uint32_t flags, ngpu_pack 
   p->dict = dict;
   p->retain = flags & NGPU_PACK_RETAIN;
   p->gz = std::move(gz);
+  if (!p->gz && !(e->cfg.flags & NGPU_FLAG_NO_BATCH)) {
+    p->waitable = true;
+    e->batch_waitable.fetch_add(1);
+  }
   // the stream's bootstrap lists every entry (OCIRef: the bootstrap is all it carries)
   if (p->retain || p->gz) p->sc.record(&p->entries);
   uint64_t cap = e->cfg.staging_bytes;
@@ -1218,6 +1236,8 @@ static int pack_write_plain(ngpu_pack *p, const void *buf, uint64_t len) {
 
 void ngpu_pack_abort(ngpu_pack *p) { release(p); }
 
+ngpu_engine *ngpu_pack_engine(const ngpu_pack *p) { return p ? p->e : nullptr; }
+
 int ngpu_pack_close(ngpu_pack *p, ngpu_chunk **chunks_out, ngpu_result **results_out,
                     uint64_t *n_out, ngpu_layer_stats *stats) {
   return ngpu_pack_finish(p, nullptr, nullptr, nullptr, chunks_out, results_out, n_out, stats,
@@ -1267,7 +1287,7 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
       // open on the engine, joins a batch (batch.hip): ONE launch set for
       // every such pack closing at about this time
       batched = one_slot && !p->gz && !(e->cfg.flags & NGPU_FLAG_NO_BATCH) &&
-                e->open_packs.load() > 1;
+                e->batch_waitable.load() > 1;
       rc = dispatch(p, cs, p->dispatched, n, !batched, &batch_dev);
       const ngpu_chunk *d_dedup = one_slot ? cs.d_ch : p->d_all;
       if (!rc) rc = grow_results(p, n + 1);
@@ -1324,6 +1344,7 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
       path = e->cur->path;  // the digest kernels, for a guard error (read outside the lock)
       }
     }
+    if (!batched) not_waitable(p);  // a leader waiting for it stops now
     if (batched && !rc) {  // the slot's bytes are in HBM (or on their way: cs.copied)
       Slot &cs = p->slot[p->cur];
       BatchJob job;
@@ -1336,6 +1357,7 @@ static int pack_finish(ngpu_pack *p, const ngpu_blob_options *opt, ngpu_write_fn
       job.h_res = p->h_io;
       job.h_stats = p->h_stats;
       rc = batch_run(e, job);
+      if (job.uncounted) p->waitable = false;  // (batch_waitable dropped when its batch was taken)
       path = job.path;
     }
     // wait for the pack's own stream without the engine lock (other packs

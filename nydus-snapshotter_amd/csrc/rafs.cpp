@@ -1517,14 +1517,14 @@ int merge_rafs(const std::vector<MergeInput> &layers, const std::vector<std::str
         memset(nb.blob_id, 0, sizeof nb.blob_id);
         memcpy(nb.blob_id, id.data(), std::min<size_t>(id.size(), sizeof nb.blob_id));
         if (in.ref && !is_dict && !in.parent) {
-          // RafsV6Blob after ci_uncompressed_size ([nydus v2.3.0]
-          // rafs/src/metadata/layout/v6.rs, VERIFY, unpinned: the reference
-          // holds no merged targz-ref bootstrap): blob_toc_digest[32] at
-          // meta+32, blob_meta_digest[32] (the RAFS blob's digest) at meta+64,
-          // blob_meta_size u64 (its size) at meta+96
-          memcpy(nb.meta + 32, in.toc_digest, 32);
-          memcpy(nb.meta + 64, in.rafs_blob_digest, 32);
-          memcpy(nb.meta + 96, &in.rafs_blob_size, 8);
+          // RafsV6Blob after ci_uncompressed_size (blob.hpp RafsV6BlobMeta:
+          // [nydus v2.3.0] rafs/src/metadata/layout/v6.rs, VERIFY; parity
+          // unpinned: the reference holds no merged targz-ref bootstrap):
+          // blob_toc_digest, blob_meta_digest (the RAFS blob's digest) and
+          // blob_meta_size (its size)
+          memcpy(nb.meta + offsetof(RafsV6BlobMeta, blob_toc_digest), in.toc_digest, 32);
+          memcpy(nb.meta + offsetof(RafsV6BlobMeta, blob_meta_digest), in.rafs_blob_digest, 32);
+          memcpy(nb.meta + offsetof(RafsV6BlobMeta, blob_meta_size), &in.rafs_blob_size, 8);
         }
         nb.blob_index = (uint32_t)li.blobs.size();
         it = id_index.emplace(id, nb.blob_index).first;

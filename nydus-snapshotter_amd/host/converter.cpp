@@ -3,6 +3,7 @@
 
 #include <openssl/sha.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -104,13 +105,45 @@ Error detect_features(const std::vector<std::string> &required, std::vector<std:
   return {};
 }
 
-// One engine per (device, digester, chunk size, fs version, aligned chunk),
-// like the Python mirror; an engine serialises its own calls, and every Pack
-// holds its own chunk dict handle, so Packs share engines safely.
+// Where Packs run.  The reference runs one nydus-image process per layer,
+// concurrently (convert_unix.go:467-538 -- one goroutine per layer); here the
+// layers of a process shard over the node's GPUs (north star): one node per
+// option set (digester, chunk size, fs version, aligned chunk) over every
+// device -- NYDUS_GPU_DEVICES ("0,1,..."; a device may repeat, e.g. "0,0" to
+// rehearse a 2-GPU node on one) or all the devices the library sees -- and
+// each Pack goes to its least-loaded engine (ngpu_node_pack_open).
+// PackOption.Device >= 0 pins every Pack of the option set to one engine on
+// that device instead.  Engines serialise their own calls and every Pack holds
+// its own chunk dict handle, so Packs share engines safely.
+using OptKey = std::tuple<int, uint32_t, uint32_t, uint32_t, bool>;
 std::mutex g_mu;
-std::map<std::tuple<int, uint32_t, uint32_t, uint32_t, bool>, ngpu_engine *> g_engines;
+std::map<OptKey, ngpu_engine *> g_engines;  // PackOption.Device >= 0
+std::map<OptKey, ngpu_node *> g_nodes;      // PackOption.Device < 0 (default)
 
-Error engine_for(const PackOption &opt, ngpu_engine **out) {
+std::vector<int32_t> node_devices() {
+  std::vector<int32_t> d;
+  if (const char *v = getenv("NYDUS_GPU_DEVICES")) {
+    for (const char *p = v; *p;) {
+      char *end = nullptr;
+      const long x = strtol(p, &end, 10);
+      if (end == p) break;
+      d.push_back((int32_t)x);
+      p = *end == ',' ? end + 1 : end;
+    }
+  }
+  if (d.empty())
+    for (int i = 0, n = ngpu_device_count(); i < n; ++i) d.push_back(i);
+  return d;
+}
+
+// Where a Pack opens: the node of its option set, or one engine (Device >= 0).
+struct Target {
+  ngpu_node *node = nullptr;
+  ngpu_engine *eng = nullptr;
+  ngpu_engine *first() const { return node ? ngpu_node_engine(node, 0) : eng; }
+};
+
+Error target_for(const PackOption &opt, Target *out) {
   uint32_t cs = 0;
   if (Error e = parse_chunk_size(opt.ChunkSize, &cs)) return e;
   const std::string fv = opt.FsVersion.empty() ? "6" : opt.FsVersion;  // convert_unix.go:326-328
@@ -121,30 +154,61 @@ Error engine_for(const PackOption &opt, ngpu_engine **out) {
   else return err(NGPU_EINVAL, "unsupported digester " + opt.Digester);
   // AlignedChunk only matters for RAFS v5 (types.go:73-74; builder.go:131-133)
   const bool aligned = opt.AlignedChunk && fv == "5";
-  const auto key = std::make_tuple(opt.Device, dg, cs, (uint32_t)(fv[0] - '0'), aligned);
+  const int dev = opt.Device < 0 ? -1 : opt.Device;
+  const OptKey key = std::make_tuple(dev, dg, cs, (uint32_t)(fv[0] - '0'), aligned);
+  ngpu_config cfg;
+  memset(&cfg, 0, sizeof cfg);
+  cfg.device = dev < 0 ? 0 : dev;
+  cfg.digester = dg;
+  cfg.chunk_size = cs;
+  cfg.fs_version = std::get<3>(key);
+  if (aligned) cfg.flags |= NGPU_FLAG_ALIGNED_CHUNK;
   std::lock_guard<std::mutex> g(g_mu);
-  auto it = g_engines.find(key);
-  if (it == g_engines.end()) {
-    ngpu_config cfg;
-    memset(&cfg, 0, sizeof cfg);
-    cfg.device = opt.Device;
-    cfg.digester = dg;
-    cfg.chunk_size = cs;
-    cfg.fs_version = std::get<3>(key);
-    if (aligned) cfg.flags |= NGPU_FLAG_ALIGNED_CHUNK;
-    ngpu_engine *e = nullptr;
-    if (int rc = ngpu_create(&cfg, &e)) return err(rc, "gpu engine: create failed");
-    it = g_engines.emplace(key, e).first;
+  if (dev >= 0) {
+    auto it = g_engines.find(key);
+    if (it == g_engines.end()) {
+      ngpu_engine *e = nullptr;
+      if (int rc = ngpu_create(&cfg, &e)) return err(rc, "gpu engine: create failed");
+      it = g_engines.emplace(key, e).first;
+    }
+    out->eng = it->second;
+    return {};
   }
-  *out = it->second;
+  auto it = g_nodes.find(key);
+  if (it == g_nodes.end()) {
+    const std::vector<int32_t> devs = node_devices();
+    if (devs.empty()) return err(NGPU_ENODEV, "gpu node: no device");
+    ngpu_node *n = nullptr;
+    if (int rc = ngpu_node_create(devs.data(), (uint32_t)devs.size(), &cfg, &n))
+      return err(rc, "gpu node: create failed");
+    it = g_nodes.emplace(key, n).first;
+  }
+  out->node = it->second;
   return {};
 }
 
+// Node index of the engine a pack runs on (-1: a pinned engine).
+int part_of(const Target &t, ngpu_pack *p) {
+  if (!t.node) return -1;
+  ngpu_engine *e = ngpu_pack_engine(p);
+  for (uint32_t i = 0, n = ngpu_node_size(t.node); i < n; ++i)
+    if (ngpu_node_engine(t.node, i) == e) return (int)i;
+  return -1;
+}
+
+// Every end of a Pack releases it exactly once: Close (finish), a failed
+// Write / ReadFrom, a source read error, Cancel (ctx.Done() -- also when no
+// Close follows: LayerConvertFunc skips tw.Close() on its error paths,
+// convert_unix.go:885-907) and the destructor (the Go binding's finalizer).
+// mu_ is held across every call on the pack, so Cancel from another thread
+// aborts it only between them; the cancel flag, stored first, makes a running
+// Write or Close return at its next slot.
 class GpuPackWriteCloser : public PackWriteCloser {
  public:
-  GpuPackWriteCloser(ngpu_engine *e, ngpu_pack *p, Writer &dest, uint32_t comp, double timeout,
-                     std::string prefetch, bool ociref = false)
+  GpuPackWriteCloser(ngpu_engine *e, ngpu_pack *p, int part, Writer &dest, uint32_t comp,
+                     double timeout, std::string prefetch, bool ociref = false)
       : e_(e), p_(p), dest_(dest), comp_(comp), timeout_(timeout), prefetch_(std::move(prefetch)) {
+    stats_.Part = part;
     ngpu_pack_set_cancel(p_, &cancel_);
     // `dest` is known at Pack() (convert_unix.go:325): the stream leaves while
     // the tar arrives (ngpu_pack_set_output, early emission); Close finishes it.
@@ -157,52 +221,117 @@ class GpuPackWriteCloser : public PackWriteCloser {
     if (timeout_ > 0)  // builder.go:153-158: the builder runs under ctx.WithTimeout
       timer_ = std::thread([this] {
         std::unique_lock<std::mutex> g(tm_);
-        if (!tcv_.wait_for(g, std::chrono::duration<double>(timeout_), [this] { return done_; }))
+        if (!tcv_.wait_for(g, std::chrono::duration<double>(timeout_), [this] { return done_; })) {
+          g.unlock();
           Cancel();
+        }
       });
   }
   ~GpuPackWriteCloser() override {
     StopTimer();
-    if (p_) ngpu_pack_abort(p_);
+    std::lock_guard<std::mutex> g(mu_);
+    End();
   }
-  void Cancel() override { __atomic_store_n(&cancel_, 1, __ATOMIC_RELAXED); }
+  void Cancel() override {
+    __atomic_store_n(&cancel_, 1, __ATOMIC_RELAXED);
+    std::lock_guard<std::mutex> g(mu_);  // after the running call, if any
+    End();
+  }
   Error Write(const void *p, size_t n) override {
-    if (!p_) return err(NGPU_EINVAL, "write to a closed pack");
-    if (out_rc_) {
-      Error e = err(out_rc_, std::string("pack output: ") + ngpu_last_error(e_));
-      ngpu_pack_abort(p_);
-      p_ = nullptr;
-      StopTimer();
-      return e;
+    Error e;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      e = WriteLocked(p, n);
     }
+    if (e) StopTimer();
+    return e;
+  }
+  Error ReadFrom(Reader &src, uint64_t *total) override {
+    *total = 0;
+    Error e;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      e = ReadFromLocked(src, total);
+    }
+    if (e) StopTimer();
+    return e;
+  }
+  Error Close() override {
+    Error e;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      e = CloseLocked();
+    }
+    StopTimer();
+    return e;
+  }
+  const PackStats &Stats() const override { return stats_; }
+
+ private:
+  // the pack ends here (mu_ held): nothing more reads the flag or the staging
+  void End() {
+    if (p_) ngpu_pack_abort(p_);
+    p_ = nullptr;
+  }
+  Error Gone() const {
+    if (__atomic_load_n(&cancel_, __ATOMIC_RELAXED))
+      return Killed(NGPU_ECANCELED, "pack: cancelled");
+    return err(NGPU_EINVAL, "pack already ended");
+  }
+  Error OutputFailed() {
+    Error e = err(out_rc_, std::string("pack output: ") + ngpu_last_error(e_));
+    End();
+    return e;
+  }
+  Error WriteLocked(const void *p, size_t n) {
+    if (!p_) return Gone();
+    if (out_rc_) return OutputFailed();
     if (!n) return {};
     if (int rc = ngpu_pack_write(p_, p, n)) {
       Error e = Killed(rc, std::string("pack write: ") + ngpu_last_error(e_));
-      ngpu_pack_abort(p_);  // a failed write leaves the pack open
-      p_ = nullptr;
-      StopTimer();
+      End();  // a failed write leaves the pack open
       return e;
     }
     return {};
   }
-  Error Close() override {
-    if (!p_) return err(NGPU_EINVAL, "pack already closed");
-    if (out_rc_) {
-      Error e = err(out_rc_, std::string("pack output: ") + ngpu_last_error(e_));
-      ngpu_pack_abort(p_);
-      p_ = nullptr;
-      StopTimer();
-      return e;
+  // Go's PackWriter.ReadFrom (io.Copy's path into a Pack): the source reads
+  // straight into the engine's pinned staging (ngpu_pack_reserve / commit)
+  Error ReadFromLocked(Reader &src, uint64_t *total) {
+    if (!p_) return Gone();
+    if (out_rc_) return OutputFailed();
+    for (;;) {
+      void *dst = nullptr;
+      uint64_t avail = 0;
+      if (int rc = ngpu_pack_reserve(p_, &dst, &avail)) {
+        Error e = Killed(rc, std::string("pack reserve: ") + ngpu_last_error(e_));
+        End();
+        return e;
+      }
+      const int64_t r = src.Read(dst, (size_t)avail);
+      if (r < 0) {  // the source failed: no Close will come for this pack
+        End();
+        return err(NGPU_EIO, "read source");
+      }
+      if (r == 0) return {};  // io.EOF
+      if (int rc = ngpu_pack_commit(p_, (uint64_t)r)) {
+        Error e = Killed(rc, std::string("pack commit: ") + ngpu_last_error(e_));
+        End();
+        return e;
+      }
+      *total += (uint64_t)r;
     }
+  }
+  Error CloseLocked() {
+    if (!p_) return Gone();
+    if (out_rc_) return OutputFailed();
     ngpu_chunk *ch = nullptr;
     ngpu_result *res = nullptr;
     uint64_t n = 0;
     ngpu_layer_stats st;
     ngpu_blob_info info;
     ngpu_pack *p = p_;
-    p_ = nullptr;
+    p_ = nullptr;  // finish releases it on every outcome
     const int rc = ngpu_pack_finish(p, nullptr, nullptr, nullptr, &ch, &res, &n, &st, &info);
-    StopTimer();
     if (rc) return Killed(rc, std::string("convert nydus ref: ") + ngpu_last_error(e_));
     ngpu_free_host(ch);
     ngpu_free_host(res);
@@ -215,9 +344,6 @@ class GpuPackWriteCloser : public PackWriteCloser {
     stats_.BlobBytes = info.blob_bytes;
     return {};
   }
-  const PackStats &Stats() const override { return stats_; }
-
- private:
   // builder.go:169-171: a timed-out builder fails with "signal: killed"
   Error Killed(int rc, const std::string &msg) const {
     if (rc != NGPU_ECANCELED) return err(rc, msg);
@@ -226,7 +352,7 @@ class GpuPackWriteCloser : public PackWriteCloser {
     return err(rc, std::string("signal: killed") + b + ": " + msg);
   }
   void StopTimer() {
-    if (!timer_.joinable()) return;
+    if (!timer_.joinable() || timer_.get_id() == std::this_thread::get_id()) return;
     {
       std::lock_guard<std::mutex> g(tm_);
       done_ = true;
@@ -235,13 +361,14 @@ class GpuPackWriteCloser : public PackWriteCloser {
     timer_.join();
   }
   ngpu_engine *e_;
-  ngpu_pack *p_;
+  ngpu_pack *p_;  // mu_
   Writer &dest_;
   uint32_t comp_;
   double timeout_;
   std::string prefetch_;
   alignas(4) volatile int32_t cancel_ = 0;
   int out_rc_ = 0;  // ngpu_pack_set_output at construction
+  std::mutex mu_;   // held across every call on p_
   std::thread timer_;
   std::mutex tm_;
   std::condition_variable tcv_;
@@ -307,6 +434,21 @@ std::string TOCEntry::GetUncompressedDigest() const { return hex(UncompressedDig
 
 bool IsNotFound(const Error &e) { return e.code == NGPU_ENOTFOUND; }
 
+Error GpuCounters(const PackOption &opt, std::vector<EngineCounters> *out) {
+  out->clear();
+  Target t;
+  if (Error e = target_for(opt, &t)) return e;
+  const uint32_t n = t.node ? ngpu_node_size(t.node) : 1;
+  for (uint32_t i = 0; i < n; ++i) {
+    ngpu_engine_counters c;
+    if (int rc = ngpu_engine_counters_get(t.node ? ngpu_node_engine(t.node, i) : t.eng, &c))
+      return err(rc, "engine counters");
+    out->push_back(EngineCounters{c.open_packs, c.staging_pool_bufs, c.staging_pool_bytes,
+                                  c.pack_pool, c.land_pool});
+  }
+  return {};
+}
+
 Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser> *out) {
   out->reset();
   const std::string fv = opt.FsVersion.empty() ? "6" : opt.FsVersion;  // convert_unix.go:326-328
@@ -324,12 +466,14 @@ Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser>
     // stream holds blob.meta (chunk infos + gzip checkpoints), image.boot, TOC.
     PackOption ref;
     ref.Device = opt.Device;
-    ngpu_engine *e = nullptr;
-    if (Error x = engine_for(ref, &e)) return x;
+    Target t;
+    if (Error x = target_for(ref, &t)) return x;
     ngpu_pack *p = nullptr;
-    if (int rc = ngpu_pack_open_dict(e, nullptr, NGPU_PACK_OCIREF, &p))
-      return err(rc, std::string("pack open: ") + ngpu_last_error(e));
-    out->reset(new GpuPackWriteCloser(e, p, dest, NGPU_COMPRESSOR_NONE, opt.Timeout, "", true));
+    const int rc = t.node ? ngpu_node_pack_open(t.node, nullptr, NGPU_PACK_OCIREF, &p)
+                          : ngpu_pack_open_dict(t.eng, nullptr, NGPU_PACK_OCIREF, &p);
+    if (rc) return err(rc, std::string("pack open: ") + ngpu_last_error(t.first()));
+    out->reset(new GpuPackWriteCloser(ngpu_pack_engine(p), p, part_of(t, p), dest,
+                                      NGPU_COMPRESSOR_NONE, opt.Timeout, "", true));
     return {};
   }
   const bool batch = std::find(detected.begin(), detected.end(), kFeatureBatchSize) != detected.end();
@@ -343,19 +487,25 @@ Error Pack(Writer &dest, const PackOption &opt, std::unique_ptr<PackWriteCloser>
   if (opt.Encrypt) return err(NGPU_EUNSUPP, "blob encryption (--encrypt) not implemented by the GPU builder");
   uint32_t comp = 0;
   if (Error e = compressor_of(opt.Compressor, &comp)) return e;
-  ngpu_engine *e = nullptr;
-  if (Error x = engine_for(opt, &e)) return x;
+  Target t;
+  if (Error x = target_for(opt, &t)) return x;
   // the Pack's own dict handle (loaded once per unchanged ChunkDictPath and
-  // shared by every Pack naming it; builder.go:122-124 passes it per process)
+  // shared by every Pack naming it; builder.go:122-124 passes it per process).
+  // On a node: one replica on every GPU (a probe needs no exchange; the
+  // partitioned dict's exchange has not met two distinct GPUs yet).
   ngpu_dict *d = nullptr;
   int rc = 0;
-  if (!opt.ChunkDictPath.empty() && (rc = ngpu_dict_open(e, opt.ChunkDictPath.c_str(), &d)))
-    return err(rc, "load chunk dict " + opt.ChunkDictPath + ": " + ngpu_last_error(e));
+  if (!opt.ChunkDictPath.empty() &&
+      (rc = t.node ? ngpu_node_dict_open(t.node, opt.ChunkDictPath.c_str(), NGPU_NODE_DICT_REPLICATE, &d)
+                   : ngpu_dict_open(t.eng, opt.ChunkDictPath.c_str(), &d)))
+    return err(rc, "load chunk dict " + opt.ChunkDictPath + ": " + ngpu_last_error(t.first()));
   ngpu_pack *p = nullptr;
-  rc = ngpu_pack_open_dict(e, d, NGPU_PACK_RETAIN, &p);
+  rc = t.node ? ngpu_node_pack_open(t.node, d, NGPU_PACK_RETAIN, &p)
+              : ngpu_pack_open_dict(t.eng, d, NGPU_PACK_RETAIN, &p);
   ngpu_dict_release(d);  // the pack holds its own reference
-  if (rc) return err(rc, std::string("pack open: ") + ngpu_last_error(e));
-  out->reset(new GpuPackWriteCloser(e, p, dest, comp, opt.Timeout, opt.PrefetchPatterns));
+  if (rc) return err(rc, std::string("pack open: ") + ngpu_last_error(t.first()));
+  out->reset(new GpuPackWriteCloser(ngpu_pack_engine(p), p, part_of(t, p), dest, comp, opt.Timeout,
+                                    opt.PrefetchPatterns));
   return {};
 }
 
@@ -441,18 +591,14 @@ Error Merge(const std::vector<Layer> &layers, Writer &dest, const MergeOption &o
   mo.parent_size = parent.size();
   mo.prefetch_patterns = opt.PrefetchPatterns.c_str();  // the builder's stdin (builder.go:238-240)
   std::vector<const char *> rd(layers.size(), nullptr), rt(layers.size(), nullptr);
-  if (any_ref) {
-    for (size_t i = 0; i < layers.size(); ++i)
-      if (!ref_toc[i].empty()) rd[i] = ref_digest[i].c_str(), rt[i] = ref_toc[i].c_str();
-    mo.rafs_blob_digests = rd.data();
-    mo.rafs_blob_sizes = ref_size.data();
-    mo.rafs_blob_toc_digests = rt.data();
-  }
+  for (size_t i = 0; any_ref && i < layers.size(); ++i)
+    if (!ref_toc[i].empty()) rd[i] = ref_digest[i].c_str(), rt[i] = ref_toc[i].c_str();
   BufferWriter merged;
   char *ids = nullptr;
-  const int rc = ngpu_merge_ex(ptrs.data(), sizes.data(), names.data(), layers.size(),
-                               dict.empty() ? nullptr : dict.data(), dict.size(), &mo,
-                               write_trampoline, &merged, &ids);
+  const int rc = ngpu_merge_ex2(ptrs.data(), sizes.data(), names.data(), layers.size(),
+                                dict.empty() ? nullptr : dict.data(), dict.size(), &mo,
+                                any_ref ? rd.data() : nullptr, any_ref ? ref_size.data() : nullptr,
+                                any_ref ? rt.data() : nullptr, write_trampoline, &merged, &ids);
   if (rc) return err(rc, std::string("merge bootstrap: ") + ngpu_host_error());
   for (const char *s = ids; s && *s;) {
     const char *c = strchr(s, ',');

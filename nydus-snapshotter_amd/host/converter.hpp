@@ -38,6 +38,11 @@ class WriteCloser : public Writer {
  public:
   virtual Error Close() = 0;
 };
+class Reader {  // io.Reader: bytes read (> 0), 0 at io.EOF, < 0 on error
+ public:
+  virtual ~Reader() = default;
+  virtual int64_t Read(void *p, size_t n) = 0;
+};
 class ReaderAt {
  public:
   virtual ~ReaderAt() = default;
@@ -100,7 +105,11 @@ struct PackOption {  // types.go:58-90
   double Timeout = 0;           // seconds; 0 = none (the builder's ctx.WithTimeout)
   bool Encrypt = false;
   std::string Digester;        // API extension: "blake3" (default) | "sha256"
-  int Device = 0;              // GPU ordinal
+  // -1 (default): the process's node -- every GPU (or NYDUS_GPU_DEVICES,
+  // e.g. "0,1,2,3"), each Pack on the least-loaded one (layers shard over the
+  // node, as the reference's per-layer goroutines shard its builder processes);
+  // >= 0: every Pack of this option set on that one GPU
+  int Device = -1;
 };
 
 struct MergeOption {  // types.go:92-133
@@ -128,12 +137,20 @@ struct PackStats {
   std::string Digest;  // "sha256:<hex>" of everything written to dest
   uint64_t Chunks = 0, NewChunks = 0, IntraChunks = 0, DictChunks = 0;
   uint64_t StreamBytes = 0, BlobBytes = 0;
+  int Part = -1;  // node index of the GPU engine the Pack ran on (-1: a pinned Device)
 };
 class PackWriteCloser : public WriteCloser {
  public:
   virtual const PackStats &Stats() const = 0;  // valid after a nil Close()
-  // ctx.Done(): the running or next Write / Close fails ("signal: killed",
-  // code NGPU_ECANCELED).  Safe from any thread.
+  // io.ReaderFrom (what io.Copy(tw, tr) picks, convert_unix.go:881): src
+  // reads straight into the engine's pinned staging.  A source error ends the
+  // Pack (no Close will come for it) and is returned.
+  virtual Error ReadFrom(Reader &src, uint64_t *n) = 0;
+  // ctx.Done(): the running Write / ReadFrom / Close fails ("signal: killed",
+  // code NGPU_ECANCELED) at its next staging slot, and the Pack is released
+  // -- also when no Write or Close ever comes again (the reference's error
+  // paths skip tw.Close(), convert_unix.go:885-907).  Safe from any thread.
+  // Destroying the writer without Close releases the Pack too.
   virtual void Cancel() = 0;
 };
 
@@ -146,6 +163,17 @@ Error Unpack(ReaderAt &ra, Writer &dest, const UnpackOption &opt);
 
 // ErrNotFound (types.go:33-35) is code NGPU_ENOTFOUND.
 bool IsNotFound(const Error &e);
+
+// Leak check of the Pack paths (not in the Go API): what each GPU engine of
+// the option set's node (or its pinned engine) holds now.
+struct EngineCounters {
+  uint64_t OpenPacks, StagingPoolBufs, StagingPoolBytes, PackPool, LandPool;
+  bool operator==(const EngineCounters &o) const {
+    return OpenPacks == o.OpenPacks && StagingPoolBufs == o.StagingPoolBufs &&
+           StagingPoolBytes == o.StagingPoolBytes && PackPool == o.PackPool && LandPool == o.LandPool;
+  }
+};
+Error GpuCounters(const PackOption &opt, std::vector<EngineCounters> *out);
 
 }  // namespace converter
 }  // namespace nydus

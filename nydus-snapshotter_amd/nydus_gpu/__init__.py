@@ -8,11 +8,11 @@ from ._lib import (CHUNK_DTYPE, COMPRESSORS, DEFAULT_DICT, DICT, DIGESTED, DIGES
                    ECANCELED, EDEVICE, EFORMAT, EINVAL, ENODEV, EUNSUPP, UNHASHED,
                    ENOTFOUND, EXPORTS, FLAG_GRID_STAGES, FLAG_NO_BATCH, HIT_DTYPE, FdWriter, INTRA, KIND_NAMES, LAYER_STATS_DTYPE, MISS, NEW,
                    RESULT_DTYPE, TOC_ENTRY_DTYPE, ChunkDict, Engine, Node, NODE_DICT_PARTITION,
-                   NODE_DICT_REPLICATE, NODE_EXCHANGE_COPY, NODE_STEP_RCCL, NgpuError, blob_write, chunk_table,
+                   NODE_DICT_REPLICATE, NODE_EXCHANGE_COPY, NODE_EXCHANGE_ROUTED, NODE_STEP_RCCL, NgpuError, blob_write, chunk_table,
                    lib, merge, rafs_dump, ref_chunk_read, route_digests, route_hits, tar_chunks, unpack,
                    unpack_entry)
 
-__all__ = ["Engine", "Node", "NODE_DICT_PARTITION", "NODE_DICT_REPLICATE", "NODE_EXCHANGE_COPY", "NODE_STEP_RCCL",
+__all__ = ["Engine", "Node", "NODE_DICT_PARTITION", "NODE_DICT_REPLICATE", "NODE_EXCHANGE_COPY", "NODE_EXCHANGE_ROUTED", "NODE_STEP_RCCL",
            "route_digests", "route_hits", "ref_chunk_read", "ChunkDict", "DEFAULT_DICT", "NgpuError", "tar_chunks", "chunk_table", "lib", "CHUNK_DTYPE",
            "RESULT_DTYPE", "HIT_DTYPE", "MISS", "NEW", "INTRA", "DICT", "DIGESTED", "UNHASHED", "KIND_NAMES", "DIGESTERS", "EXPORTS",
            "COMPRESSORS", "TOC_ENTRY_DTYPE", "FdWriter", "blob_write", "unpack_entry", "unpack", "merge", "rafs_dump",

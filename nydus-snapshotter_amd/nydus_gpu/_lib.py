@@ -72,7 +72,9 @@ EXPORTS = ["ngpu_abi_version", "ngpu_create", "ngpu_destroy", "ngpu_last_error",
            "ngpu_dict_create_device_gid", "ngpu_route_digests", "ngpu_route_hits",
            "ngpu_pack_set_output", "ngpu_ref_chunk_read",
            # ABI 5
-           "ngpu_node_process_step", "ngpu_batch_stats"]
+           "ngpu_node_process_step", "ngpu_batch_stats",
+           # ABI 7
+           "ngpu_pack_engine", "ngpu_engine_counters_get", "ngpu_merge_ex2"]
 
 LAYER_STATS_DTYPE = np.dtype([("chunks", "<u8"), ("new_chunks", "<u8"), ("intra_chunks", "<u8"),
                               ("dict_chunks", "<u8"), ("new_bytes", "<u8"), ("own_blob_index", "<u4"),
@@ -215,6 +217,12 @@ def lib():
                              u64, WRITE_FN, vp, ctypes.POINTER(vp)]
     L.ngpu_merge_ex.argtypes = [ctypes.POINTER(vp), pu64, ctypes.POINTER(ctypes.c_char_p), u64, vp,
                                 u64, ctypes.POINTER(NgpuMergeOptions), WRITE_FN, vp, ctypes.POINTER(vp)]
+    L.ngpu_merge_ex2.argtypes = [ctypes.POINTER(vp), pu64, ctypes.POINTER(ctypes.c_char_p), u64, vp,
+                                 u64, ctypes.POINTER(NgpuMergeOptions), vp, vp, vp, WRITE_FN, vp,
+                                 ctypes.POINTER(vp)]
+    L.ngpu_pack_engine.argtypes = [vp]
+    L.ngpu_pack_engine.restype = vp
+    L.ngpu_engine_counters_get.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.ngpu_dict_open.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
     L.ngpu_dict_create.argtypes = [vp, vp, u64, vp, u32, ctypes.POINTER(vp)]
     L.ngpu_dict_create_device.argtypes = [vp, vp, vp, vp, vp, vp, u64, u32, ctypes.POINTER(vp)]
@@ -482,15 +490,12 @@ def route_hits(d_routed: int, d_rows: int, m: int, d_hits: int, stream: int = 0)
 
 class NgpuMergeOptions(ctypes.Structure):
     _fields_ = [("parent_bootstrap", ctypes.c_void_p), ("parent_size", ctypes.c_uint64),
-                ("prefetch_patterns", ctypes.c_char_p),
-                # ABI 6: targz-ref layers' RAFS blob digests / sizes / TOC digests
-                ("rafs_blob_digests", ctypes.c_void_p), ("rafs_blob_sizes", ctypes.c_void_p),
-                ("rafs_blob_toc_digests", ctypes.c_void_p)]
+                ("prefetch_patterns", ctypes.c_char_p)]
 
 
 def merge(bootstraps, layer_digests, dict_bootstrap: bytes = None, parent_bootstrap: bytes = None,
           prefetch_patterns: str = "", rafs_blobs=None):
-    """ngpu_merge_ex: per-layer bootstraps (bytes, lowest first) + layer digest
+    """ngpu_merge_ex2: per-layer bootstraps (bytes, lowest first) + layer digest
     hex strings -> (merged bootstrap bytes, [blob ids in first-appearance
     order]).  The merged bootstrap holds the overlaid inode tree.
     rafs_blobs: per layer None, or (RAFS blob digest hex, size, TOC digest
@@ -509,16 +514,14 @@ def merge(bootstraps, layer_digests, dict_bootstrap: bytes = None, parent_bootst
     pbuf = _buf(parent_bootstrap) if parent_bootstrap is not None else None
     opt = NgpuMergeOptions(_ptr(pbuf) if pbuf is not None else None, pbuf.size if pbuf is not None else 0,
                            (prefetch_patterns or "").encode())
+    rd = rs = rt = None
     if rafs_blobs is not None and any(r is not None for r in rafs_blobs):
         rd = (ctypes.c_char_p * max(1, n))(*[r[0].encode() if r else None for r in rafs_blobs])
         rs = (ctypes.c_uint64 * max(1, n))(*[int(r[1]) if r else 0 for r in rafs_blobs])
         rt = (ctypes.c_char_p * max(1, n))(*[r[2].encode() if r else None for r in rafs_blobs])
-        opt.rafs_blob_digests = ctypes.cast(rd, ctypes.c_void_p)
-        opt.rafs_blob_sizes = ctypes.cast(rs, ctypes.c_void_p)
-        opt.rafs_blob_toc_digests = ctypes.cast(rt, ctypes.c_void_p)
-    rc = L.ngpu_merge_ex(ptrs, sizes, digs, n, _ptr(dbuf) if dbuf is not None else None,
-                         dbuf.size if dbuf is not None else 0, ctypes.byref(opt), sink.fn, None,
-                         ctypes.byref(ids))
+    rc = L.ngpu_merge_ex2(ptrs, sizes, digs, n, _ptr(dbuf) if dbuf is not None else None,
+                          dbuf.size if dbuf is not None else 0, ctypes.byref(opt), rd, rs, rt,
+                          sink.fn, None, ctypes.byref(ids))
     sink.reraise()
     _host_check(rc, "merge")
     try:
@@ -767,6 +770,15 @@ class Engine:
         self._check(lib().ngpu_batch_stats(self._h, out), "batch_stats")
         return {"batches": out[0], "packs": out[1], "max_packs": out[2]}
 
+    def counters(self) -> dict:
+        """ngpu_engine_counters_get: what the engine holds now (open packs,
+        pooled staging / stream sets) -- the leak check of abort paths."""
+        out = (ctypes.c_uint64 * 8)()
+        self._check(lib().ngpu_engine_counters_get(self._h, out), "engine_counters")
+        keys = ("open_packs", "staging_pool_bufs", "staging_pool_bytes", "pack_pool", "land_pool",
+                "batch_waitable")
+        return {k: int(out[i]) for i, k in enumerate(keys)}
+
     def timing_at(self, back: int) -> dict:
         """Stage timings of the call `back` calls before the last one (the
         engine keeps its last 64); lets a caller time back-to-back calls
@@ -942,7 +954,8 @@ class NgpuNodePart(ctypes.Structure):
 
 NODE_STEP_RCCL = 1  # ngpu_node_process_step: the all-to-alls are RCCL ncclAllToAllv
 NODE_DICT_PARTITION, NODE_DICT_REPLICATE = 0, 1
-NODE_EXCHANGE_COPY = 0x100  # | PARTITION: the ABI 3 broadcast + DMA exchange
+NODE_EXCHANGE_COPY = 0x100  # | PARTITION: the broadcast + DMA exchange (the default since ABI 7)
+NODE_EXCHANGE_ROUTED = 0x200  # | PARTITION: the peer-kernel exchange (opt-in since ABI 7)
 
 
 class Node:
@@ -1011,13 +1024,16 @@ class Node:
         return ChunkDict(h)
 
     def pack(self, dict=None, retain: bool = False) -> "PackWriter":
-        """A streaming Pack on the next engine (round robin)."""
+        """A streaming Pack on the least-loaded engine (fewest open packs);
+        its `part` attribute is the node index it was placed on."""
         h = ctypes.c_void_p()
         self._err(lib().ngpu_node_pack_open(self._h, _dict_arg(dict), PACK_RETAIN if retain else 0,
                                             ctypes.byref(h)), "node_pack_open")
         w = PackWriter.__new__(PackWriter)
         # the pack's engine, for error messages and finish() options
-        w._eng = self.engines[0]
+        eh = lib().ngpu_pack_engine(h)
+        w.part = next(i for i, e in enumerate(self.engines) if e._h.value == eh)
+        w._eng = self.engines[w.part]
         w._p = h
         w._cancel = ctypes.c_int32(0)
         lib().ngpu_pack_set_cancel(w._p, ctypes.byref(w._cancel))

@@ -145,6 +145,42 @@ def test_packs_drive_harness_loads_and_checks_its_arguments():
     per = (ctypes.c_uint64 * 4)()
     null = ctypes.c_void_p()
     assert drive(null, 1, null, null, ctypes.c_uint64(1 << 20), 0, 0, 0x100000, 1, rs, per, None,
-                 None, ctypes.c_uint64(0)) == -1  # NGPU_EINVAL
+                 None, ctypes.c_uint64(0), null, None) == -1  # NGPU_EINVAL: no engine, no node
     assert drive(ctypes.c_void_p(1), 0, null, null, ctypes.c_uint64(1 << 20), 0, 0, 0x100000, 1, rs,
-                 per, None, None, ctypes.c_uint64(0)) == -1
+                 per, None, None, ctypes.c_uint64(0), null, None) == -1
+
+
+def test_multi_gpu_checks_summary_and_exit():
+    """an N > 1 line gathers every hit-equality check in
+    `multi_gpu_checks`; a False check makes the run exit 4 after printing,
+    entries that failed to run are listed as errors, not as wrong exchanges."""
+    line = {"sharded_dict": {"hits_ok": True},
+            "node_cabi": {"hits_equal": True,
+                          "node_step": {"copy": {"hits_equal_partition": True},
+                                        "rccl": {"error": "NGPU_EUNSUPP"}}},
+            "c4": {"dict": {"dict_hits": 995, "expected_dict_hits": 1000}}}
+    mg = bench.multi_gpu_checks(line)
+    assert mg["ok"] and set(mg["checks"]) == {
+        "sharded_dict.hits_ok", "node_cabi.routed_copy_replicate.hits_equal",
+        "node_cabi.node_step.copy.hits_equal", "c4.dict_hits"}
+    assert mg["errors"] == {"node_cabi.node_step.rccl": "NGPU_EUNSUPP"}
+    bench.exit_on_failed_checks(mg)  # returns
+    bench.exit_on_failed_checks(None)
+    line["node_cabi"]["node_step"]["copy"]["hits_equal_partition"] = False
+    mg = bench.multi_gpu_checks(line)
+    assert not mg["ok"]
+    with pytest.raises(SystemExit) as ex:
+        bench.exit_on_failed_checks(mg)
+    assert ex.value.code == 4
+    assert not bench.multi_gpu_checks({"sharded_dict": {"hits_ok": False}})["ok"]
+    assert bench.multi_gpu_checks({"c4": {"error": "timeout"}}) == {
+        "checks": {}, "errors": {"c4": "timeout"}, "ok": True}
+
+
+def test_fracs_over_one_are_listed():
+    """the line names every frac above 1 (none expected)."""
+    line = {"roofline": {"frac": 0.93, "frac_mix": 0.99, "mix": {"frac": 1.2}},
+            "c3": {"probe_roofline": {"traffic_frac": 1.01}}, "x": [{"frac": 2}]}
+    assert sorted(bench.fracs_over_one(line)) == ["c3.probe_roofline.traffic_frac", "roofline.mix.frac",
+                                                 "x[0].frac"]
+    assert bench.fracs_over_one({"roofline": {"frac": 1.0}}) == []

@@ -176,7 +176,9 @@ def test_batched_stream_equals_unbatched():
 def test_native_threads_drive_concurrent_packs(oracle):
     """tools/packs_drive.cpp (bench.py --packs's caller: K native threads, one
     Pack each, as cgo goroutines would): decisions and early-emission streams
-    of 8 concurrent layers, counted per layer, equal the oracle's."""
+    of 8 concurrent layers, fed by Write and by ReadFrom (reserve / commit),
+    on one engine and on a 2-part node (least-loaded placement: 4 + 4),
+    counted per layer, equal the oracle's."""
     import ctypes
     import os
     lib_path = os.path.join(os.path.dirname(nydus_gpu._lib.LIB_PATH), "build", "libpacks_drive.so")
@@ -184,7 +186,8 @@ def test_native_threads_drive_concurrent_packs(oracle):
     vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
     drive.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u64), u64, u32, u32, u32, u32,
                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64),
-                      ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, u64]
+                      ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, u64, vp,
+                      ctypes.POINTER(ctypes.c_int32)]
     S, K = 0x100000, 8
     tars = [np.frombuffer(layers.alpine_like_tar(0xD0 + i), np.uint8) for i in range(K)]
     want = []
@@ -192,24 +195,31 @@ def test_native_threads_drive_concurrent_packs(oracle):
         ch = oracle.tar_chunks(t.tobytes(), S)
         dec, _ = oracle.dedup(oracle.digest_chunks(t.tobytes(), ch, "blake3"), ch["length"])
         want.append(np.bincount(dec["kind"], minlength=3)[:3])
-    for mode in (0, 1):
-        eng = nydus_gpu.Engine(device=0, chunk_size=S, staging_bytes=16 << 20)
-        try:
-            rs = (ctypes.c_double * 3)()
-            per = (u64 * (4 * K))()
-            err = ctypes.create_string_buffer(256)
-            rc = drive(eng._h, K, (vp * K)(*[t.ctypes.data for t in tars]),
-                       (u64 * K)(*[t.size for t in tars]), 1 << 20, mode, 0, S, 3, rs, per, None, err, 256)
-            assert rc == 0, err.value
-            bs = eng.batch_stats()
-        finally:
-            eng.close()
-        got = np.array(per, np.uint64).reshape(K, 4)
-        for k in range(K):
-            assert list(got[k, :3]) == list(want[k]), (mode, k)
-            assert (got[k, 3] > 0) == (mode == 1)
-        assert all(x > 0 for x in rs)
-        assert bs["packs"] >= 2, bs
+    for mode in (0, 1, 2, 3):  # bit 0: stream, bit 1: ReadFrom feed
+        for on_node in (False, True):
+            node = nydus_gpu.Node([0, 0], chunk_size=S, staging_bytes=16 << 20) if on_node else None
+            eng = None if on_node else nydus_gpu.Engine(device=0, chunk_size=S, staging_bytes=16 << 20)
+            part = (ctypes.c_int32 * K)()
+            try:
+                rs = (ctypes.c_double * 3)()
+                per = (u64 * (4 * K))()
+                err = ctypes.create_string_buffer(256)
+                rc = drive(None if on_node else eng._h, K, (vp * K)(*[t.ctypes.data for t in tars]),
+                           (u64 * K)(*[t.size for t in tars]), 1 << 20, mode, 0, S, 3, rs, per, None,
+                           err, 256, node._h if on_node else None, part)
+                assert rc == 0, err.value
+                engs = node.engines if on_node else [eng]
+                bs = [e.batch_stats() for e in engs]
+            finally:
+                (node or eng).close()
+            got = np.array(per, np.uint64).reshape(K, 4)
+            for k in range(K):
+                assert list(got[k, :3]) == list(want[k]), (mode, on_node, k)
+                assert (got[k, 3] > 0) == (mode & 1 == 1)
+            assert all(x > 0 for x in rs)
+            assert sum(b["packs"] for b in bs) >= 2, bs
+            if on_node:
+                assert sorted(np.bincount(np.array(part), minlength=2).tolist()) == [4, 4], list(part)
 
 
 @pytest.mark.parametrize("digester", ["blake3", "sha256"])
@@ -226,7 +236,8 @@ def test_batch_lanes_stress_timed_engine(oracle, digester):
     vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
     drive.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u64), u64, u32, u32, u32, u32,
                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64),
-                      ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, u64]
+                      ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, u64, vp,
+                      ctypes.POINTER(ctypes.c_int32)]
     S, K, R = 0x100000, 32, 4
     tars = [np.frombuffer(layers.alpine_like_tar(0x5150 + i), np.uint8) for i in range(K)]
     want = []
@@ -242,8 +253,8 @@ def test_batch_lanes_stress_timed_engine(oracle, digester):
             per = (u64 * (4 * K))()
             err = ctypes.create_string_buffer(256)
             rc = drive(eng._h, K, (vp * K)(*[t.ctypes.data for t in tars]),
-                       (u64 * K)(*[t.size for t in tars]), 1 << 20, mode,
-                       nydus_gpu._lib.DIGESTERS[digester], S, R, rs, per, None, err, 256)
+                       (u64 * K)(*[t.size for t in tars]), 1 << 20, mode | 2,
+                       nydus_gpu._lib.DIGESTERS[digester], S, R, rs, per, None, err, 256, None, None)
             assert rc == 0, err.value
             got = np.array(per, np.uint64).reshape(K, 4)
             for k in range(K):
@@ -252,3 +263,58 @@ def test_batch_lanes_stress_timed_engine(oracle, digester):
     finally:
         eng.close()
     assert bs["packs"] >= 2 * K and bs["batches"] >= 2, bs
+
+
+def test_batch_per_layer_error_words():
+    """a batched launch set's error words go only to the layer that
+    raised them, with its own chunk id (tests/cpp/batch_stats_test.hip runs
+    csrc/batch_stats.hpp's kernel on a 3-layer set with one faulty layer)."""
+    import os
+    import subprocess
+    from conftest import ROOT
+    exe = os.path.join(ROOT, "nydus-snapshotter_amd", "build", "batch_stats_test")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "PASS", r.stdout + r.stderr
+
+
+def test_batch_leader_waits_only_for_packs_that_can_join(oracle):
+    """a batch leader waits for the open packs that may still join
+    (engine counter batch_waitable): a pack whose tar outgrew one staging slot
+    leaves the count at that moment, an OCIRef pack never enters it, and each
+    pack leaves it when it ends; the small packs still batch and still equal
+    the oracle."""
+    cs = 0x10000
+    eng = nydus_gpu.Engine(chunk_size=cs, staging_bytes=4 << 20)
+    try:
+        base = eng.counters()
+        assert base["open_packs"] == 0 and base["batch_waitable"] == 0
+        big = eng.pack()
+        small = [eng.pack() for _ in range(3)]
+        assert eng.counters()["batch_waitable"] == 4
+        tar_big = layers.alpine_like_tar()  # 10 MB > one 4 MiB slot
+        big.write(tar_big)
+        c = eng.counters()
+        assert c["open_packs"] == 4 and c["batch_waitable"] == 3
+        tars = [layers.oci_upper_tar(), layers.oci_lower_tar(), layers.chunk_dict_tar()]
+        got = [None] * 3
+        meet = threading.Barrier(3)
+
+        def one(i):
+            small[i].write(tars[i])
+            meet.wait()
+            got[i] = small[i].close()
+        th = [threading.Thread(target=one, args=(i,)) for i in range(3)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for t, g in zip(tars, got):
+            _check(oracle, t, cs, "blake3", g)
+        assert eng.batch_stats()["max_packs"] >= 2
+        assert eng.counters()["batch_waitable"] == 0
+        gb = big.close()
+        _check(oracle, tar_big, cs, "blake3", gb)
+        end = eng.counters()
+        assert end["open_packs"] == 0 and end["batch_waitable"] == 0
+    finally:
+        eng.close()

