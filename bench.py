@@ -41,7 +41,7 @@ MiB = 1 << 20
 # 39.3 T int32 ops/s.  Measured, not assumed: a wave64 v_add3/v_xor/v_alignbit
 # takes 4 SIMD cycles (rocprofv3: SQ_INSTS_VALU x 4 / 1024 SIMDs = the whole
 # b3_groups duration at the GRBM clock; DESIGN.md §Roofline, profiles/).
-SHA_MODES = {"auto": 0, "split": 1, "pair": 2, "lane": 3, "pair_pf": 4, "pair_pf_asm": 7}
+SHA_MODES = {"auto": 0, "split": 1, "pair": 2, "lane": 3}
 SHA_PAIR_MAX_CHUNKS = 256 * 128  # launch_sha256's auto rule (sha256.hip)
 CLOCK_HZ = 2.4e9
 PEAK_INT_OPS = 256 * 4 * 16 * 2.4e9
@@ -2076,13 +2076,37 @@ def main():
             chain_s = chain * QUAD_COMPRESS_DEP_OPS * DEP_OP_CYCLES / CLOCK_HZ
             launch_s = 3 * KERNEL_BOUNDARY_S
             step_s = elapsed / args.steps
-            roof.update({"latency_bound": {
+            lb = {
                 "critical_chain_compressions": chain, "chain_ms": round(chain_s * 1e3, 4),
                 "kernel_boundaries_ms": round(launch_s * 1e3, 4),
                 "bound_ms": round((chain_s + launch_s) * 1e3, 4),
                 "frac_of_step": round((chain_s + launch_s) / step_s, 3),
                 "model": "longest chunk: leaf blocks + tree levels, x ~190 dependent ops x 8.5 "
-                         "cycles at 2.4 GHz, + 3 kernel boundaries x 4.65 us"}})
+                         "cycles at 2.4 GHz, + 3 kernel boundaries x 4.65 us"}
+            # the whole step, measured in THIS run by the
+            # engine's own HIP stop events (digest = b3_quad_planned incl. its
+            # dispatch, tree = b3_tree, dedup = dedup_small_lds), the rest =
+            # the result table's D2H (HIP runs a 7 KB same-stream copy as the
+            # blit kernel __amd_rocclr_copyBuffer) + the boundary to the next
+            # step; the committed kernel trace gives the same split per kernel
+            med = lambda k: float(np.median([t[k] for t in timings]))
+            ker = {"digest": med("digest_ms"), "tree": med("tree_ms"), "dedup": med("dedup_ms")}
+            total = med("total_ms")
+            dec = {"step_ms": round(step_s * 1e3, 4),
+                   "kernels_ms_hip_events": {k: round(v, 4) for k, v in ker.items()},
+                   "call_first_to_last_kernel_ms": round(total, 4),
+                   "after_call_ms": round(step_s * 1e3 - total, 4),
+                   "explained_frac_of_step": round(min(total, step_s * 1e3) / (step_s * 1e3), 3),
+                   "chain_frac_of_leaf_and_tree_kernels": round(
+                       chain_s * 1e3 / max(1e-9, ker["digest"] + ker["tree"]), 3)}
+            tr, tsrc = newest_profile("c1_step_trace_r6c.json")
+            if tr:
+                dec["trace"] = {"kernel_us": tr["kernel_us_median"], "gap_us_profiled": tr["gap_us_median"],
+                                "source": tsrc,
+                                "note": "rocprofv3 adds ~3-5 us to every gap; unprofiled, the "
+                                        "kernels are ~90 % of the step"}
+            lb["step_decomposition"] = dec
+            roof.update({"latency_bound": lb})
     else:
         blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).sum())
         ops = blocks * 1384  # SURVEY.md §8(d) SHA-256 op count
@@ -2096,8 +2120,7 @@ def main():
         # per wave64 op) bounds the kernel, not chip-wide VALU throughput.
         # VALU ops per block on the critical wave: pair/split round waves; the
         # lane kernel's wave does the whole block (schedule + rounds)
-        chain_ops = {"pair": 66 * 9, "pair_pf": 66 * 9, "pair_pf_asm": 66 * 9, "split": 64 * 14,
-                     "lane": 1384}[mode]
+        chain_ops = {"pair": 66 * 9, "split": 64 * 14, "lane": 1384}[mode]
         lanes_used = n * (2 if pair else 1)
         max_blocks = int(((ch["length"].astype(np.int64) + 8) // 64 + 1).max())
         chain_s = max_blocks * chain_ops * 4 / CLOCK_HZ

@@ -138,11 +138,9 @@ typedef struct {
 #define NGPU_FLAG_LOAD_MODE_SHIFT 8
 /* Tuning (benchmarks only): bits 11..13 = 1 + SHA-256 kernel (0: one lane per
  * chunk with schedule/round waves, 1: two lanes per chunk, 2: one lane per
- * chunk, each wave schedules its own blocks, 3: two lanes per chunk with the
- * K+W loads off the round chain, 4: two lanes, one chunk group per
- * workgroup, 5: two lanes, four groups per workgroup, 6: as 3 with the
- * rounds in a fixed asm issue order); 0 = library default (by chunk count).
- * Every kernel computes the same digests. (ABI 7: 3 and 6 added) */
+ * chunk, each wave schedules its own blocks, 4: two lanes, one chunk group per
+ * workgroup, 5: two lanes, four groups per workgroup); 0 = library default
+ * (by chunk count); other values are rejected (NGPU_EINVAL). */
 #define NGPU_FLAG_SHA_MODE_SHIFT 11
 
 /* The builder's exit status (builder.go:169-175) for work enqueued on a

@@ -883,7 +883,9 @@ int BlobWriter::finish(const ngpu_chunk *chunks, const ngpu_result *res, uint64_
   li.chunk_size = m.opt.chunk_size;
   li.digester = m.opt.digester;
   li.flags = b.flags;
-  if (m.opt.prefetch_patterns) li.prefetch = m.opt.prefetch_patterns;
+  // NULL or "" -> "/" (nydus_gpu.h ngpu_blob_options; builder.go:125-127): an
+  // empty string from a binding must not drop the prefetch table
+  if (m.opt.prefetch_patterns && *m.opt.prefetch_patterns) li.prefetch = m.opt.prefetch_patterns;
   li.refs.resize(n);
   li.file_of.resize(n);
   for (uint64_t i = 0; i < n; ++i) {

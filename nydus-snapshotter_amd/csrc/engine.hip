@@ -529,11 +529,10 @@ int ngpu_create(const ngpu_config *cfg, ngpu_engine **out) {
   if (c.fs_version != 5 && c.fs_version != 6) return NGPU_EINVAL;
   if (c.digester != NGPU_DIGEST_BLAKE3 && c.digester != NGPU_DIGEST_SHA256) return NGPU_EINVAL;
   if (c.leaves_per_lane & (c.leaves_per_lane - 1) || c.leaves_per_lane > 16) return NGPU_EINVAL;
-  // SHA-256 kernel override (benchmarks): 1 + {0 split, 1 pair, 2 lane, 3 pair
-  // with off-chain K+W loads, 4 pair one group per workgroup, 5 pair four
-  // groups, 6 = 3 with asm-ordered rounds}: every 3-bit value is a kernel
+  // SHA-256 kernel override (benchmarks): 1 + {0 split, 1 pair, 2 lane, 4 pair
+  // one group per workgroup, 5 pair four groups}; anything else is rejected
   switch ((c.flags >> NGPU_FLAG_SHA_MODE_SHIFT) & 7) {
-    case 0: case 1: case 2: case 3: case 4: case 5: case 6: case 7: break;
+    case 0: case 1: case 2: case 3: case 5: case 6: break;
     default: return NGPU_EINVAL;
   }
   // BLAKE3 load-mode override: only modes this build has a kernel for, all of

@@ -531,8 +531,11 @@ int switch_slot(ngpu_pack *p) {
 // gathered, so the layer's copy runs while the caller is still writing and
 // only the tail is left for the dispatch (C1 through 1 MiB writes: the whole
 // 10 MB copy used to start at close).  Not with NGPU_PACK_RETAIN, whose
-// device segment is sized and allocated at dispatch.
-constexpr uint64_t kEagerCopy = 1ull << 20;
+// device segment is sized and allocated at dispatch.  4 MiB: 32 concurrent C1
+// Packs (ReadFrom) move 38.3 / 40.5 / 42.9 / 42.7 / 43.5 GB/s at 1 / 2 / 4 / 8
+// / 16 MiB granules (profiles/r6/packs_eager_granule_r6d.json; the copy lanes'
+// H2D rate grows with the piece size, profiles/r5/h2d_streams_granule_r5w.jsonl).
+constexpr uint64_t kEagerCopy = 4ull << 20;
 
 // NGPU_EAGER_COPY (bytes, tuning knob): the eager copy granule.
 uint64_t eager_granule() {

@@ -458,220 +458,6 @@ __global__ __launch_bounds__(128 * R) void sha256_pair(
   }
 }
 
-// Four rounds of the E/A two-lane recurrence (sha256_pair above) as ONE asm
-// block in a fixed issue order: in each round the three rotations of Sigma
-// are interleaved with the off-chain Y / Z / sel work instead of issued back
-// to back (a lone wave issues runs of v_alignbit at ~5.1 cycles each, mixed
-// with 2-cycle ops at ~4.2; profiles/r5/valu_issue_model.json).  Same 9 VALU
-// ops per round as the compiled round.  Four rounds per block because the
-// compiler pads every inline asm that reads a VGPR just written with an
-// s_nop (it cannot see what the asm does).  The DPP source of each round
-// (its P1) is the output of two rounds back, >= 9 VALU ops earlier.
-// In: P0..P3 (newest first), the rounds' K+W words k0..k3.  Out: X0..X3, the
-// four new values (X3 newest).
-__device__ __forceinline__ void sha_round4_ea(uint32_t P0, uint32_t P1, uint32_t P2, uint32_t P3,
-                                              uint32_t M, uint32_t k0, uint32_t k1, uint32_t k2,
-                                              uint32_t k3, uint32_t r1, uint32_t r2, uint32_t r3,
-                                              uint32_t &X0, uint32_t &X1, uint32_t &X2, uint32_t &X3) {
-  uint32_t s1, s2, s3, y, sel;
-#define SHA_EA_ROUND(x, p0, p1, p2, p3, kw)                                         \
-  "v_alignbit_b32 %[s1], %[" p0 "], %[" p0 "], %[r1]\n\t"                          \
-  "v_xad_u32 %[y], %[" p3 "], %[m], %[" kw "]\n\t"                                 \
-  "v_alignbit_b32 %[s2], %[" p0 "], %[" p0 "], %[r2]\n\t"                          \
-  "v_bitop3_b32 %[sel], %[" p0 "], %[" p2 "], %[m] bitop3:0x78\n\t"                \
-  "v_alignbit_b32 %[s3], %[" p0 "], %[" p0 "], %[r3]\n\t"                          \
-  "v_add_u32_dpp %[y], %[" p1 "], %[y] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"   \
-  "v_bitop3_b32 %[s1], %[s1], %[s2], %[s3] bitop3:0x96\n\t"                        \
-  "v_bitop3_b32 %[sel], %[" p1 "], %[" p2 "], %[sel] bitop3:0xe4\n\t"              \
-  "v_add3_u32 %[" x "], %[sel], %[s1], %[y]\n\t"
-  asm(SHA_EA_ROUND("x0", "p0", "p1", "p2", "p3", "k0")
-      SHA_EA_ROUND("x1", "x0", "p0", "p1", "p2", "k1")
-      SHA_EA_ROUND("x2", "x1", "x0", "p0", "p1", "k2")
-      SHA_EA_ROUND("x3", "x2", "x1", "x0", "p0", "k3")
-      : [s1] "=&v"(s1), [s2] "=&v"(s2), [s3] "=&v"(s3), [y] "=&v"(y), [sel] "=&v"(sel),
-        [x0] "=&v"(X0), [x1] "=&v"(X1), [x2] "=&v"(X2), [x3] "=&v"(X3)
-      : [p0] "v"(P0), [p1] "v"(P1), [p2] "v"(P2), [p3] "v"(P3), [m] "v"(M), [k0] "v"(k0),
-        [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3), [r1] "v"(r1), [r2] "v"(r2), [r3] "v"(r3));
-#undef SHA_EA_ROUND
-}
-
-// sha256_pair with the round waves' K+W reads taken off the chain (VERDICT r5
-// item 3).  sha256_pair reads a block's 64 K+W words (16 ds_read_b128) when
-// the block starts and waits for them; here the schedule waves run TWO phases
-// ahead (three K+W sets in LDS, set = phase % 3), so every block's words are
-// in LDS one block early and the round wave loads block k+1's words into the
-// other register bank while it runs block k's rounds.  A: the rounds in the
-// fixed issue order of sha_round_ea.  Same lanes, waves and results as
-// sha256_pair<R, U>.
-template <int R, bool U, bool A>
-__global__ __launch_bounds__(128 * R) void sha256_pair_pf(
-    const uint8_t *__restrict__ data, uint64_t data_len,
-    const ngpu_chunk *__restrict__ chunks, uint64_t n,
-    ngpu_result *__restrict__ out, uint64_t *__restrict__ err) {
-  __shared__ u32x4 kws[R][3][2][33][17];  // [group][set][half][chunk | 32 = ones][t/4]
-  __shared__ uint32_t s_nbmax;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave = threadIdx.x >> 6;
-  const bool rounds = wave < R;
-  const uint32_t grp = rounds ? wave : wave - R;
-  auto &kw = kws[grp];
-  if (rounds) __builtin_amdgcn_s_setprio(3);
-  const uint32_t side = rounds ? (lane >> 3) & 1 : 0;  // 1 = A lane
-  const uint32_t ci = rounds ? (lane >> 4) * 8 + (lane & 7) : lane & 31;
-  const uint32_t half = rounds ? 0 : lane >> 5;
-  const uint64_t c = (blockIdx.x * (uint64_t)R + grp) * 32ull + ci;
-  bool valid = c < n;
-  uint32_t len = 0;
-  const uint8_t *p = data;
-  if (threadIdx.x == 0) s_nbmax = 0;
-  if (valid) {
-    const ngpu_chunk ch = chunks[c];
-    if (ch.offset > data_len || ch.length > data_len - ch.offset) {
-      if (rounds && side == 0) note_bad_desc(err, 1);
-      valid = false;
-    } else {
-      len = ch.length;
-      p = data + ch.offset;
-    }
-  }
-  const uint32_t nb = valid ? (len + 8) / 64 + 1 : 0;
-  uint32_t nbmax = nb;
-#pragma unroll
-  for (int o = 32; o; o >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, o, 64));
-  if (R > 1) {
-    __syncthreads();
-    if (lane == 0) atomicMax(&s_nbmax, nbmax);
-    __syncthreads();
-    nbmax = s_nbmax;
-  }
-  const uint32_t phases = (nbmax + 1) / 2;
-
-  const uint32_t full = len >> 6;
-  const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
-  u32x4 pf0 = {}, pf1 = {}, pf2 = {}, pf3 = {};
-  bool have_pf = false;
-  auto prefetch = [&](uint32_t b) {
-    have_pf = aligned && b < full;
-    if (have_pf) {
-      const u32x4 *q = reinterpret_cast<const u32x4 *>(p + 64ull * b);
-      pf0 = q[0]; pf1 = q[1]; pf2 = q[2]; pf3 = q[3];
-    }
-  };
-  auto produce = [&](uint32_t b, int set) {
-    if (b >= nb) return;
-    uint32_t w[16];
-    if (have_pf) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        w[i] = bswap_words(pf0, i); w[4 + i] = bswap_words(pf1, i);
-        w[8 + i] = bswap_words(pf2, i); w[12 + i] = bswap_words(pf3, i);
-      }
-    } else {
-      sha_load_block(p, len, b, w);
-    }
-    prefetch(b + 2);
-    u32x4 *dst = kw[set][half][ci];
-    u32x4 q;
-#pragma unroll
-    for (int t = 0; t < 64; ++t) {
-      uint32_t wt;
-      if (t < 16) {
-        wt = w[t];
-      } else {
-        const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-        const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
-        const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
-        wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
-        w[t & 15] = wt;
-      }
-      q[t & 3] = wt + kK[t];
-      if ((t & 3) == 3) dst[t >> 2] = q;
-    }
-  };
-
-  if (!rounds) {  // phases 0 and 1 before the rounds start
-    for (uint32_t i = lane; i < 3 * 2 * 17; i += 64)
-      kw[i / 34][(i / 17) & 1][32][i % 17] = u32x4{1u, 1u, 1u, 1u};
-    if (nb > half) {
-      prefetch(half);
-      produce(half, 0);
-      produce(2 + half, 1);
-    }
-  }
-  __syncthreads();
-
-  const uint32_t M = side ? 0xFFFFFFFFu : 0u;
-  const uint32_t r1 = side ? 2 : 6, r2 = side ? 13 : 11, r3 = side ? 22 : 25;
-  uint32_t H0 = side ? 0x6a09e667u : 0x510e527fu, H1 = side ? 0xbb67ae85u : 0x9b05688cu;
-  uint32_t H2 = side ? 0x3c6ef372u : 0x1f83d9abu, H3 = side ? 0xa54ff53au : 0x5be0cd19u;
-  const uint32_t kcol = side ? 32 : ci;
-
-  // one block of 66 iterations on the K+W words in kv (see sha256_pair)
-  auto run_block = [&](const u32x4 (&kv)[16], bool mine) {
-    if (!(U ? __any(mine) : mine)) return;
-    uint32_t P0 = side ? H2 : H0, P1 = side ? H3 : H1, P2 = H2, P3 = H3;
-    uint32_t F0 = 0, F1 = 0, F2 = 0, F3 = 0;
-#pragma unroll
-    for (int it = 0; it < 66; ++it) {
-      if (it == 2) {  // the A lane starts its rounds: a,b,c,d = H0..H3
-        P0 = side ? H0 : P0; P1 = side ? H1 : P1;
-        P2 = side ? H2 : P2; P3 = side ? H3 : P3;
-      }
-      if (A && it >= 4 && it < 64) {  // rounds 4..63: four per asm block
-        if ((it & 3) == 0) {
-          uint32_t X0, X1, X2, X3;
-          const u32x4 k = kv[it >> 2];
-          sha_round4_ea(P0, P1, P2, P3, M, k.x, k.y, k.z, k.w, r1, r2, r3, X0, X1, X2, X3);
-          P3 = X0; P2 = X1; P1 = X2; P0 = X3;
-          if (it == 60) { F0 = P0; F1 = P1; F2 = P2; F3 = P3; }
-        }
-        continue;
-      }
-      const uint32_t kwv = it < 64 ? kv[it >> 2][it & 3] : side;
-      uint32_t Y = (P3 ^ M) + kwv;
-      asm("" : "+v"(Y));
-      uint32_t Z = Y + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P1, kDppRowRor8, 0xf, 0xf, false);
-      asm("" : "+v"(Z));
-      const uint32_t S = xor3(rotr32(P0, r1), rotr32(P0, r2), rotr32(P0, r3));
-      const uint32_t sel = __builtin_amdgcn_bitop3_b32(P0, P2, M, 0x78);
-      const uint32_t cm = (sel & P1) | (~sel & P2);
-      const uint32_t X = S + cm + Z;
-      P3 = P2; P2 = P1; P1 = P0; P0 = X;
-      if (it == 63) { F0 = P0; F1 = P1; F2 = P2; F3 = P3; }
-    }
-    if (mine) {
-      H0 += side ? P0 : F0; H1 += side ? P1 : F1;
-      H2 += side ? P2 : F2; H3 += side ? P3 : F3;
-    }
-  };
-
-  if (rounds) {
-    u32x4 ka[16], kb[16];  // two register banks: the block running, the next one loading
-#pragma unroll
-    for (int j = 0; j < 16; ++j) ka[j] = kw[0][0][kcol][j];
-    for (uint32_t ph = 0; ph < phases; ++ph) {
-      const int set = ph % 3, nset = (ph + 1) % 3;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) kb[j] = kw[set][1][kcol][j];  // this phase's odd block
-      run_block(ka, 2 * ph < nb);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) ka[j] = kw[nset][0][kcol][j];  // next phase's even block
-      run_block(kb, 2 * ph + 1 < nb);
-      __syncthreads();
-    }
-  } else {
-    for (uint32_t ph = 0; ph < phases; ++ph) {
-      produce(2 * ph + 4 + half, (ph + 2) % 3);
-      __syncthreads();
-    }
-  }
-  if (rounds && valid) {
-    uint4 *dd = reinterpret_cast<uint4 *>(out[c].digest) + (side ? 0 : 1);
-    *dd = make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));
-    if (side) out[c].kind = NGPU_DIGESTED;
-  }
-}
-
 }  // namespace
 
 void launch_sha256(const uint8_t *data, uint64_t data_len,
@@ -707,18 +493,6 @@ void launch_sha256(const uint8_t *data, uint64_t data_len,
       case 5:  // four groups per workgroup: a round and a schedule wave share each SIMD
         hipLaunchKernelGGL((sha256_pair<4, false>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0, s,
                            data, data_len, chunks, n, out, err);
-        break;
-      case 3:  // two groups, K+W loads off the chain (three sets)
-        if (few)
-          hipLaunchKernelGGL((sha256_pair_pf<2, true, false>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
-        else
-          hipLaunchKernelGGL((sha256_pair_pf<2, false, false>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
-        break;
-      case 6:  // the same with the asm-ordered rounds
-        if (few)
-          hipLaunchKernelGGL((sha256_pair_pf<2, true, true>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
-        else
-          hipLaunchKernelGGL((sha256_pair_pf<2, false, true>), g2, dim3(256), 0, s, data, data_len, chunks, n, out, err);
         break;
       default:
         if (few)

@@ -23,8 +23,7 @@ LANES = [1, 2, 4, 8, 16]
 # "pair" runs two chunk groups per workgroup; 5 forces one group, 6 four groups.
 SHA_SPLIT, SHA_PAIR, SHA_LANE = 1 << 11, 2 << 11, 3 << 11
 SHA_PAIR_R1, SHA_PAIR_R4 = 5 << 11, 6 << 11
-SHA_PAIR_PF, SHA_PAIR_PF_ASM = 4 << 11, 7 << 11  # ABI 7: K+W loads off the chain (+ asm rounds)
-SHA_FLAGS = [0, SHA_SPLIT, SHA_PAIR, SHA_LANE, SHA_PAIR_R1, SHA_PAIR_R4, SHA_PAIR_PF, SHA_PAIR_PF_ASM]
+SHA_FLAGS = [0, SHA_SPLIT, SHA_PAIR, SHA_LANE, SHA_PAIR_R1, SHA_PAIR_R4]
 # Calls with <= 4096 chunks plan and dedup in one fused workgroup; this flag
 # forces the multi-kernel grid path, so both are checked on the same inputs.
 GRID = nydus_gpu.FLAG_GRID_STAGES
@@ -215,8 +214,7 @@ def test_random_vs_oracle(engines, oracle, seed, chunk_size, unaligned, total):
             assert st["new_chunks"] == int((exp["kind"] == 0).sum())
 
 
-@pytest.mark.parametrize("fl", [SHA_SPLIT, SHA_PAIR, SHA_LANE, SHA_PAIR_R1, SHA_PAIR_R4, SHA_PAIR_PF,
-                                SHA_PAIR_PF_ASM])
+@pytest.mark.parametrize("fl", [SHA_SPLIT, SHA_PAIR, SHA_LANE, SHA_PAIR_R1, SHA_PAIR_R4])
 def test_sha256_ragged_wave(engines, oracle, fl):
     """Chunks of very different block counts in one wave (lanes finish at
     different blocks), lengths around the 55/56/64-byte padding edges, odd

@@ -72,9 +72,12 @@ def test_engine_option_validation():
         with pytest.raises(nydus_gpu.NgpuError) as e:
             nydus_gpu.Engine(chunk_size=bad)
         assert e.value.code == -1
-    # SHA-256 kernel override: field = 1 + {0 .. 6}: since ABI 7 every value
-    # of the 3-bit field names a kernel (3 / 6: the pipelined pair kernels),
-    # so no SHA field is rejected (the GPU suite runs each against the oracle)
+    # SHA-256 kernel override: field = 1 + {0, 1, 2, 4, 5}; fields 4 and 7
+    # (no such kernel) are rejected before any device call
+    for bad in (4 << 11, 7 << 11):
+        with pytest.raises(nydus_gpu.NgpuError) as e:
+            nydus_gpu.Engine(digester="sha256", flags=bad)
+        assert e.value.code == -1
     # BLAKE3 load-mode override: field = 1 + mode.  Field 5 (mode 4, the
     # no-load VALU diagnostic: wrong digests) and 7 (no such mode) are rejected
     # before any device call; the no-load kernel is not even built (VERDICT r2
