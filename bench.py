@@ -949,6 +949,12 @@ def multi_gpu_checks(line):
                 checks[f"node_cabi.node_step.{k}.hits_equal"] = bool(v["hits_equal_partition"])
             elif isinstance(v, dict) and "error" in v:
                 errors[f"node_cabi.node_step.{k}"] = v["error"]
+    pn = line.get("packs_node")
+    if isinstance(pn, dict):
+        if "placement_even" in pn:
+            checks["packs_node.placement_even"] = bool(pn["placement_even"])
+        elif "error" in pn:
+            errors["packs_node"] = pn["error"]
     c4 = line.get("c4")
     if isinstance(c4, dict):
         dd = c4.get("dict") or {}
@@ -1002,6 +1008,41 @@ def c4_entry(world, layers, steps, backend="nccl", timeout_s=420):
            "--steps", str(steps), "--warmup", "15", "--no-sharded-extra", "--no-node-extra",
            "--no-e2e", "--no-c4", "--c4-layers", str(layers), "--dist-backend", backend]
     return child_line(cmd, timeout_s, env=env)
+
+
+def packs_node_extra(world, timeout_s=240):
+    """N > 1, rank 0, after the headline: the Go drop-in's
+    own path over the whole node -- `bench.py --workload c1 --packs 32N --node
+    0,..,N-1` in a child process: 32 C1 converter.Pack calls per GPU from
+    native threads, fed through ReadFrom (ngpu_pack_reserve / commit), each
+    placed on the node's least-loaded engine (ngpu_node_pack_open), so every
+    GPU's own PCIe link carries its share.  value = the node's file bytes per
+    second, PCIe included; placement = Packs per GPU in the last round."""
+    env = dict(os.environ)
+    for k in DIST_ENV:
+        env.pop(k, None)
+    devs = os.environ.get("NYDUS_NODE_EXTRA_DEVICES") or ",".join(str(i) for i in range(world))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c1", "--packs", str(32 * world),
+           "--node", devs, "--packs-modes", "decisions", "--no-cpu-baseline", "--steps", "10",
+           "--warmup", "3"]
+    import subprocess
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timeout after {timeout_s} s", "devices": devs}
+    lines = [x for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    if r.returncode or not lines:
+        return {"error": f"rc {r.returncode}: {(r.stderr or '')[-300:]}", "devices": devs}
+    d = json.loads(lines[-1])
+    m = d["modes"]["decisions"]
+    placed = m.get("packs_per_node_part_last_round") or []
+    return {"devices": devs, "packs": 32 * world, "gbs": m["gbs"], "ms_per_round": m["ms_per_round"],
+            "device_gbs": m.get("device_gbs"), "per_gpu_gbs": round(m["gbs"] / world, 2),
+            "packs_per_gpu_last_round": placed,
+            "placement_even": bool(placed) and max(placed) - min(placed) <= 1,
+            "feed": m.get("feed"), "seconds": round(time.perf_counter() - t0, 1),
+            "cmd": " ".join(cmd[1:])}
 
 
 def node_cabi_extra(world, timeout_s=150):
@@ -2221,7 +2262,7 @@ def main():
                 print(json.dumps(dict(line, sharded_dict={"error": "timeout"})), flush=True)
             sys.stdout.flush()
             os._exit(3)
-        dog = threading.Timer((360.0 if node_cabi else 180.0) + (450.0 if c4x else 0.0), stuck)
+        dog = threading.Timer((600.0 if node_cabi else 180.0) + (450.0 if c4x else 0.0), stuck)
         dog.daemon = True
         dog.start()
         if sharded_extra:
@@ -2243,6 +2284,10 @@ def main():
                 line["node_cabi"] = node_cabi_extra(world)
             except Exception as ex:  # reported, never fatal to the headline line
                 line["node_cabi"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
+            try:  # the drop-in's Pack path over every GPU of the node
+                line["packs_node"] = packs_node_extra(world)
+            except Exception as ex:  # reported, never fatal to the headline line
+                line["packs_node"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
         if c4x and rank == 0:  # the other ranks wait in the closing barrier
             try:
                 line["c4"] = c4_entry(world, args.c4_layers, max(3, min(args.steps, 10)),
