@@ -2146,6 +2146,13 @@ def main():
                                 "source": tsrc,
                                 "note": "rocprofv3 adds ~3-5 us to every gap; unprofiled, the "
                                         "kernels are ~90 % of the step"}
+                # the call's kernels (this run's events) + the result D2H, which
+                # HIP runs as the copyBuffer blit kernel (the trace's duration):
+                # what is left is the four kernel boundaries of a step
+                d2h = tr["kernel_us_median"].get("copyBuffer", 0.0) / 1e3
+                dec["explained_with_d2h_frac_of_step"] = round(
+                    min(total + d2h, step_s * 1e3) / (step_s * 1e3), 3)
+                dec["boundaries_ms"] = round(max(0.0, step_s * 1e3 - total - d2h), 4)
             lb["step_decomposition"] = dec
             roof.update({"latency_bound": lb})
     else:
