@@ -951,8 +951,12 @@ def multi_gpu_checks(line):
                 errors[f"node_cabi.node_step.{k}"] = v["error"]
     pn = line.get("packs_node")
     if isinstance(pn, dict):
-        if "placement_even" in pn:
-            checks["packs_node.placement_even"] = bool(pn["placement_even"])
+        if "placement_all_parts" in pn:
+            # placement follows load (fewest open Packs), so an uneven split
+            # is not an error; a part left without Packs, or a lost chunk, is
+            checks["packs_node.placement_all_parts"] = bool(pn["placement_all_parts"])
+            if "chunks_ok" in pn:
+                checks["packs_node.chunks_ok"] = bool(pn["chunks_ok"])
         elif "error" in pn:
             errors["packs_node"] = pn["error"]
     c4 = line.get("c4")
@@ -1041,6 +1045,8 @@ def packs_node_extra(world, timeout_s=240):
             "device_gbs": m.get("device_gbs"), "per_gpu_gbs": round(m["gbs"] / world, 2),
             "packs_per_gpu_last_round": placed,
             "placement_even": bool(placed) and max(placed) - min(placed) <= 1,
+            "placement_all_parts": len(placed) == len(devs.split(",")) and min(placed) > 0,
+            "chunks_ok": sum(m["decisions_last_round"].values()) == m.get("chunks_per_round"),
             "feed": m.get("feed"), "seconds": round(time.perf_counter() - t0, 1),
             "cmd": " ".join(cmd[1:])}
 
@@ -1217,6 +1223,7 @@ def packs_bench(args):
     tars = [layers.alpine_like_tar(0xA1F1E + i) for i in range(K)]
     chs = [nydus_gpu.tar_chunks(t, wl["chunk"]) for t in tars]
     file_bytes = sum(int(c["length"].sum()) for c in chs)
+    n_chunks = sum(len(c["length"]) for c in chs)
     tar_bytes = sum(len(t) for t in tars)
     arrs = [np.frombuffer(t, np.uint8) for t in tars]
 
@@ -1312,7 +1319,8 @@ def packs_bench(args):
                    "packs_per_set": round(npk / nb, 1) if nb else 0,
                    "most_packs_in_one_set": max(b["max_packs"] for b in b_after), "phases": phases,
                    "decisions_last_round": {"NEW": int(kinds[0]), "INTRA": int(kinds[1]),
-                                            "DICT": int(kinds[2])}}
+                                            "DICT": int(kinds[2])},
+                   "chunks_per_round": n_chunks}
             if placed is not None:
                 out["packs_per_node_part_last_round"] = placed
             return out

@@ -175,9 +175,12 @@ def test_multi_gpu_checks_summary_and_exit():
     assert not bench.multi_gpu_checks({"sharded_dict": {"hits_ok": False}})["ok"]
     assert bench.multi_gpu_checks({"c4": {"error": "timeout"}}) == {
         "checks": {}, "errors": {"c4": "timeout"}, "ok": True}
-    # the drop-in's Packs over the node: uneven placement fails the run
-    assert bench.multi_gpu_checks({"packs_node": {"placement_even": True}})["ok"]
-    assert not bench.multi_gpu_checks({"packs_node": {"placement_even": False}})["ok"]
+    # the drop-in's Packs over the node: placement follows load, so an uneven
+    # split passes; a part without Packs, or a lost chunk, fails the run
+    assert bench.multi_gpu_checks({"packs_node": {"placement_even": False, "placement_all_parts": True,
+                                                  "chunks_ok": True}})["ok"]
+    assert not bench.multi_gpu_checks({"packs_node": {"placement_all_parts": False, "chunks_ok": True}})["ok"]
+    assert not bench.multi_gpu_checks({"packs_node": {"placement_all_parts": True, "chunks_ok": False}})["ok"]
 
 
 def test_fracs_over_one_are_listed():
