@@ -806,7 +806,7 @@ __device__ __forceinline__ u32x4 load16(const uint8_t *p, int valid) {
 __device__ __forceinline__ void quad_leaf(const uint8_t *__restrict__ data, const ngpu_chunk &ch,
                                           uint32_t c, uint32_t j, bool root_group, uint64_t g,
                                           uint32_t q, uint32_t *blk, uint32_t *__restrict__ cv_out,
-                                          ngpu_result *__restrict__ out) {
+                                          ngpu_result *__restrict__ out, uint32_t *lds_row = nullptr) {
   const uint32_t len = ch.length;
   uint32_t wo[28];  // this lane's schedule words: LDS word offsets in the quad's block
 #pragma unroll
@@ -863,6 +863,9 @@ __device__ __forceinline__ void quad_leaf(const uint8_t *__restrict__ data, cons
     d[q] = x;
     d[4 + q] = y;
     if (q == 0) out[c].kind = NGPU_DIGESTED;
+  } else if (lds_row) {  // b3_quad_planned: the CV stays in LDS for the in-wave levels
+    lds_row[q] = x;
+    lds_row[4 + q] = y;
   } else {
     cv_out[g * 8 + q] = x;
     cv_out[g * 8 + 4 + q] = y;
@@ -909,6 +912,192 @@ __global__ __launch_bounds__(kQuadThreads) void b3_quad_leaves(
   }
 }
 
+#ifndef B3_QUAD_GROUPS
+#define B3_QUAD_GROUPS 1
+#endif
+#if B3_QUAD_GROUPS
+// Small calls (<= kSmallPlanChunks chunks, quad path): the planning is done
+// by every workgroup for itself in LDS, so the call has no planning kernel,
+// and the two lowest tree levels of every multi-leaf chunk run inside the
+// wave that hashed their leaves.
+//   * Slots: the multi-leaf chunks first, in chunk order, each taking its leaf
+//     count rounded up to 4 slots (so its leaves 4i..4i+3 are 4 adjacent
+//     quads of one wave), then one slot per single-leaf chunk.  mpre / spre:
+//     exclusive prefixes of the two (a chunk has width in one of them only).
+//   * A leaf's CV stays in LDS (qcv, 8 words per quad, rows of adjacent quads
+//     adjacent).  Level 1: the quad of leaf 4i (4i+2) compresses the parent of
+//     rows 4i, 4i+1 (4i+2, 4i+3) -- two adjacent rows ARE the parent's
+//     16-word message -- and level 2 the parent of rows 4i and 4i+2; the odd
+//     tail is promoted.  Aligned groups of 4 leaves are complete BLAKE3
+//     subtrees, the last (ragged) group the tree's right edge, so b3_tree
+//     continues over ceil(leaves / 4) group CVs exactly as over the leaves;
+//     a chunk of <= 4 leaves ends here (ROOT on its last parent) and is not
+//     queued.  Group CVs sit at cv[mpre[c] / 4 + i] (groups[c] = mpre[c] / 4).
+// The in-wave levels need no barrier: one wave's LDS operations complete in
+// order.  Workgroup 0 writes what b3_tree reads: groups[0..n], the queue of
+// chunks with more than 4 leaves in chunk order, and the call's counters
+// (stats[7] = bad descriptors, stats[9] = queued chunks, the rest zero) --
+// deterministic, no atomics.  Round 6: the C1 tree stage dropped its two
+// widest levels.
+constexpr int kFusedItems = (int)(kSmallPlanChunks / kQuadThreads);
+static_assert(kFusedItems * kQuadThreads == (int)kSmallPlanChunks, "one item set");
+
+__global__ __launch_bounds__(kQuadThreads) void b3_quad_planned(
+    const uint8_t *__restrict__ data, uint64_t data_len, const ngpu_chunk *__restrict__ chunks,
+    uint64_t n, uint64_t cap_g, uint32_t *__restrict__ cv_out, ngpu_result *__restrict__ out,
+    uint64_t *__restrict__ groups, uint64_t *__restrict__ stats, uint32_t *__restrict__ tree_list) {
+  __shared__ __attribute__((aligned(16))) uint32_t qmsg[kQuadThreads / 4 * 16];
+  __shared__ __attribute__((aligned(16))) uint32_t qcv[kQuadThreads / 4 * 8];
+  __shared__ uint32_t mpre[kSmallPlanChunks + 1], spre[kSmallPlanChunks + 1];
+  __shared__ uint32_t wsum[4][kQuadThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  // this thread's chunks: c0 .. c0 + kFusedItems - 1 (contiguous)
+  const uint32_t c0 = (uint32_t)t * kFusedItems;
+  uint32_t lv[kFusedItems], sm = 0, ss = 0, sq = 0, bad = 0, mb = 0;
+#pragma unroll
+  for (int i = 0; i < kFusedItems; ++i) {
+    const uint32_t c = c0 + i;
+    lv[i] = 0;
+    if (c < n) {
+      const ngpu_chunk ch = chunks[c];
+      const uint32_t len = ch.length;
+      const bool bd = ch.offset > data_len || len > data_len - ch.offset;
+      lv[i] = len == 0 ? 1 : (len + kLeaf - 1) / kLeaf;
+      if (bd) mb |= 1u << i;  // a bad chunk keeps its slots but is never hashed
+      if (lv[i] > 1) sm += (lv[i] + 3) & ~3u;
+      else ss += 1;
+      sq += lv[i] > 4 && !bd;
+      bad += bd;
+    }
+  }
+  // four block scans in one pass (multi slots; single slots; queued chunks; bad)
+  uint32_t xm = sm, xs = ss, xq = sq, xb = bad;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t ym = __shfl_up(xm, o, 64), ys = __shfl_up(xs, o, 64);
+    const uint32_t yq = __shfl_up(xq, o, 64), yb = __shfl_up(xb, o, 64);
+    if (lane >= o) xm += ym, xs += ys, xq += yq, xb += yb;
+  }
+  if (lane == 63) wsum[0][wid] = xm, wsum[1][wid] = xs, wsum[2][wid] = xq, wsum[3][wid] = xb;
+  __syncthreads();
+  uint32_t pm = 0, ps = 0, pq = 0, tm = 0, ts = 0, tq = 0, tb = 0;
+#pragma unroll
+  for (int w = 0; w < kQuadThreads / 64; ++w) {
+    if (w < wid) pm += wsum[0][w], ps += wsum[1][w], pq += wsum[2][w];
+    tm += wsum[0][w];
+    ts += wsum[1][w];
+    tq += wsum[2][w];
+    tb += wsum[3][w];
+  }
+  uint32_t rm = pm + xm - sm, rs = ps + xs - ss, rq = pq + xq - sq;
+  const bool writer = blockIdx.x == 0;
+#pragma unroll
+  for (int i = 0; i < kFusedItems; ++i) {
+    const uint32_t c = c0 + i;
+    if (c < n) {
+      mpre[c] = rm;
+      spre[c] = rs;
+      if (writer) {
+        groups[c] = rm / 4;
+        if (lv[i] > 4 && !((mb >> i) & 1)) tree_list[rq++] = c;
+      }
+      if (lv[i] > 1) rm += (lv[i] + 3) & ~3u;
+      else rs += 1;
+    }
+  }
+  if (t == 0) {
+    mpre[n] = tm;
+    spre[n] = ts;
+    if (writer) groups[n] = tm / 4;
+  }
+  // stats[8]: more slots than the launch covers, or more group CVs than the
+  // workspace holds -- descriptors that overlap (a tar's file extents never
+  // do); the call then fails instead of leaving leaves unhashed
+  const uint64_t span = (uint64_t)gridDim.x * (kQuadThreads / 4);
+  const uint64_t total = (uint64_t)tm + ts;
+  const uint64_t over = total > span || tm / 4 > cap_g ? total : 0;
+  if (writer && t < 16)
+    stats[t] = t == kStBadDesc ? tb : t == kStTreeQueued ? tq : t == kStOverlap ? over : 0;
+  if (writer && t == 0 && tb)
+    atomicAdd((unsigned long long *)(stats + kStSticky), (unsigned long long)tb);
+  if (writer && t == 0 && over)
+    atomicMax((unsigned long long *)(stats + kStSticky + 1), (unsigned long long)over);
+  __syncthreads();
+  const uint32_t q = t & 3, quad = t >> 2;
+  const uint64_t g = blockIdx.x * (uint64_t)(kQuadThreads / 4) + quad;
+  if (g >= total || over) return;  // per quad: its four lanes leave together
+  // the chunk holding slot g: the last c whose prefix is <= g (a chunk of
+  // zero width in that prefix is never the last such c below the total)
+  const bool multi = g < tm;
+  const uint32_t *pre = multi ? mpre : spre;
+  const uint32_t key = multi ? (uint32_t)g : (uint32_t)(g - tm);
+  uint32_t lo = 0, hi = (uint32_t)n;  // pre[lo] <= key < pre[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= key) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t c = lo, j = key - pre[c];
+  const ngpu_chunk ch = chunks[c];
+  if (ch.offset > data_len || ch.length > data_len - ch.offset) return;  // counted above
+  const uint32_t nl = ch.length == 0 ? 1 : (ch.length + kLeaf - 1) / kLeaf;
+  if (j >= nl) return;  // a padding slot
+  uint32_t *row = qcv + quad * 8;
+  quad_leaf(data, ch, c, j, !multi, g, q, qmsg + quad * 16, cv_out, out, row);
+  if (!multi) return;
+  // schedule word offsets in a parent's message (two adjacent rows), from an
+  // opaque copy of q: sharing the leaf loop's kept 28 more VGPRs live through
+  // it (175 -> 134 VGPRs, 2 -> 3 waves per SIMD)
+  uint32_t ql = q;
+  asm volatile("" : "+v"(ql));
+  uint32_t wo[28];
+#pragma unroll
+  for (int r = 0; r < 7; ++r)
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) wo[4 * r + sl] = (kQuadSched.w[r][sl] >> (4 * ql)) & 15u;
+  const uint32_t ivq = q == 0 ? IV0 : q == 1 ? IV1 : q == 2 ? IV2 : IV3;
+  const uint32_t ivh = q == 0 ? IV4 : q == 1 ? IV5 : q == 2 ? IV6 : IV7;
+  const uint32_t jr = j & 3, rem = nl - (j - jr);  // leaves of this group of 4
+  asm volatile("" ::: "memory");
+  if ((jr & 1) == 0 && j + 1 < nl) {  // level 1: rows j, j + 1
+    uint32_t m[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) m[k] = row[wo[k]];
+    const uint32_t pf = PARENT | (nl == 2 ? ROOT : 0u);
+    uint32_t x = ivq, y = ivh;
+    compress_quad(x, y, m, ivq, q == 2 ? 64u : q == 3 ? pf : 0u);
+    row[q] = x;
+    row[4 + q] = y;
+  }
+  asm volatile("" ::: "memory");
+  if (jr == 0 && rem >= 3) {  // level 2: rows j, j + 2
+    uint32_t m[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) m[k] = row[wo[k] + (wo[k] & 8u)];  // words 8.. from row j + 2
+    const uint32_t pf = PARENT | (nl <= 4 ? ROOT : 0u);
+    uint32_t x = ivq, y = ivh;
+    compress_quad(x, y, m, ivq, q == 2 ? 64u : q == 3 ? pf : 0u);
+    row[q] = x;
+    row[4 + q] = y;
+  }
+  asm volatile("" ::: "memory");
+  if (jr != 0) return;
+  const uint32_t x = row[q], y = row[4 + q];
+  if (nl <= 4) {  // the chunk's root: its digest
+    uint32_t *d = reinterpret_cast<uint32_t *>(out[c].digest);
+    d[q] = x;
+    d[4 + q] = y;
+    if (q == 0) out[c].kind = NGPU_DIGESTED;
+  } else {  // group j / 4 of the chunk, for b3_tree
+    const uint64_t gc = mpre[c] / 4 + j / 4;
+    cv_out[gc * 8 + q] = x;
+    cv_out[gc * 8 + 4 + q] = y;
+  }
+}
+
+// Slots b3_quad_planned may need: every multi-leaf chunk rounded up to 4.
+uint64_t quad_planned_slots(uint64_t n, uint64_t data_len) { return data_len / kLeaf + 4 * n + 1; }
+#else
 // Small calls (<= kSmallPlanChunks chunks, quad path): the planning is done
 // by every workgroup for itself in LDS, so the call has no planning kernel
 // (one launch less: ~4 us of host enqueue and ~5 us of a small layer's GPU
@@ -1010,6 +1199,10 @@ __global__ __launch_bounds__(kQuadThreads) void b3_quad_planned(
   if (ch.offset > data_len || ch.length > data_len - ch.offset) return;  // counted above
   quad_leaf(data, ch, c, j, gpre[c + 1] - gpre[c] == 1, g, q, qmsg + quad * 16, cv_out, out);
 }
+
+// Slots b3_quad_planned may need.
+uint64_t quad_planned_slots(uint64_t n, uint64_t data_len) { return data_len / kLeaf + 2 * n + 1; }
+#endif
 
 // 1024 threads = 256 quads: every level of a 1024-CV tile (<= 512 parents)
 // runs as compress_quad in at most two passes.  A chain of ~10 levels is the
@@ -1176,7 +1369,7 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
     // with the call's first kernel (ev_first; ev_start is left unrecorded,
     // ngpu_timing_at reads ev_first instead)
     (void)ev_start;
-    const uint64_t blocks = (call_groups(n, data_len, D, ws) + kQuadThreads / 4 - 1) / (kQuadThreads / 4);
+    const uint64_t blocks = (quad_planned_slots(n, data_len) + kQuadThreads / 4 - 1) / (kQuadThreads / 4);
     hipExtLaunchKernelGGL(b3_quad_planned, dim3((unsigned)blocks), dim3(kQuadThreads), 0, s,
                           ev_first, ev_end_groups, 0, data, data_len, chunks, n, ws.cap_g, ws.cv,
                           out, ws.groups, ws.stats, ws.tree_list);
