@@ -3,7 +3,7 @@
 # device 0 twice: node_cabi, packs_node, c4, sharded_dict, multi_gpu_checks),
 # then the threaded oracle soak (16 threads on shared engines and a 4-part node).
 set -u
-TAG=r6g
+TAG=${TAG:-r6g}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
