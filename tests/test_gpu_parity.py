@@ -214,6 +214,42 @@ def test_random_vs_oracle(engines, oracle, seed, chunk_size, unaligned, total):
             assert st["new_chunks"] == int((exp["kind"] == 0).sum())
 
 
+def test_quad_groups_every_ragged_shape(engines, oracle):
+    """b3_quad_planned's in-wave tree levels (round 6): multi-leaf chunks padded
+    to groups of 4 slots, parents from adjacent LDS rows, chunks of <= 4 leaves
+    finished in the leaf kernel, the rest continued by b3_tree over group CVs.
+    Every leaf count 1..13 at k KiB - 1 / k KiB / k KiB + 1 bytes (ragged last
+    groups of 1, 2 and 3 leaves; roots at 2, 3 and 4 leaves), single-leaf chunks
+    interleaved so multi-leaf slots and single slots alternate in chunk order,
+    a few 64-leaf chunks, ~4,000 chunks (the planned path's limit is 4,096),
+    odd offsets; against the oracle and the grid-stage path."""
+    rng = np.random.default_rng(66)
+    lens = []
+    while len(lens) < 3900:
+        k = int(rng.integers(1, 14))
+        lens.append(max(1, 1024 * k + int(rng.integers(-1, 2))))
+        if rng.random() < 0.6:
+            lens.append(int(rng.integers(1, 1025)))
+        if rng.random() < 0.01:
+            lens.append(65536 + int(rng.integers(-1, 2)))
+    chunks, off = [], 0
+    for ln in lens:
+        off += int(rng.integers(0, 4))
+        chunks.append((off, ln, 0, 0))
+        off += ln
+    data = rng.integers(0, 256, off + 16, dtype=np.uint8).tobytes()
+    ch = np.array(chunks, dtype=nydus_gpu.CHUNK_DTYPE)
+    assert len(ch) <= 4096 and off // 1024 + len(ch) <= 40960  # the planned quad path
+    exp_d = oracle.digest_chunks(data, ch.view(oracle.CHUNK_DTYPE), "blake3")
+    exp, _ = oracle.dedup(exp_d, ch["length"])
+    for fl in (0, GRID):
+        out, _ = engines("blake3", 0x100000, 0, flags=fl).process(data, ch)
+        bad = np.nonzero((out["digest"] != exp_d).any(1))[0]
+        assert not len(bad), (fl, bad[:8], ch["length"][bad[:8]])
+        for f in ("kind", "index", "ref"):
+            assert np.array_equal(out[f], exp[f]), (fl, f)
+
+
 @pytest.mark.parametrize("fl", [SHA_SPLIT, SHA_PAIR, SHA_LANE, SHA_PAIR_R1, SHA_PAIR_R4])
 def test_sha256_ragged_wave(engines, oracle, fl):
     """Chunks of very different block counts in one wave (lanes finish at
