@@ -1210,21 +1210,35 @@ uint64_t quad_planned_slots(uint64_t n, uint64_t data_len) { return data_len / k
 // threads the two widest levels ran one 680-op compression per lane (2 and 1
 // per lane), ~6.8 K issued ops against 2 x 190 here (C1 tree 18.8 -> see
 // DESIGN.md §b3_quad_leaves).
+//
+// Round 6: b3_quad_planned leaves b3_tree at most 512 group CVs per chunk
+// (chunk_size <= 2 MiB), most chunks only a few.  For a layer of many chunks
+// a 256-thread workgroup with a 512-CV tile (32 KiB of LDS) does: four of
+// them fit a CU where one 1024-thread workgroup did, so its many small trees
+// run four times as wide (a 30 MB layer of log-normal files: tree 21 -> 11
+// us), for one more pass on the widest level of a 1 MiB chunk.
 constexpr int kTreeThreads = 1024;
-constexpr uint32_t kTreeQuads = kTreeThreads / 4;
 constexpr int kTile = 1024;  // CVs per LDS tile (32 KiB)
-static_assert(kTile / 2 <= 2 * kTreeQuads, "a tile level is at most two quad passes");
+#ifndef B3_TREE_NARROW
+#define B3_TREE_NARROW 1
+#endif
+constexpr int kTreeThreadsNarrow = 256;
+constexpr uint64_t kTreeNarrowMinChunks = 512;
+constexpr int kTileNarrow = 512;
 
 // all_queued: every multi-group chunk was queued (b3_quad_leaves), none was
 // finished inside a b3_groups workgroup.
-__global__ __launch_bounds__(kTreeThreads) void b3_tree(
+template <int TT, int TILE>
+__global__ __launch_bounds__(TT) void b3_tree(
     const uint64_t *__restrict__ gbase, const uint32_t *__restrict__ tree_list,
     const uint64_t *__restrict__ queued, uint64_t cap_g,
     uint32_t *__restrict__ cv, ngpu_result *__restrict__ out, bool all_queued) {
   // two tiles, ping-pong: a level reads one and writes the other, so it needs
   // one barrier (the chain of ~10 narrow levels is the kernel's time on a
   // small layer; with one tile each level read, barriered, wrote, barriered)
-  __shared__ uint32_t tt[2][kTile * 8];
+  constexpr uint32_t kQ = TT / 4;                         // quads
+  constexpr int kPasses = (int)((TILE / 2 + kQ - 1) / kQ);  // quad passes per level
+  __shared__ uint32_t tt[2][TILE * 8];
   const int tid = threadIdx.x;
   // a quad of lanes per parent: this lane's column and schedule word offsets
   // in a parent's 16-word message (the two child CVs, adjacent in t)
@@ -1244,12 +1258,12 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
     if (k <= 1 || base + k > cap_g || (!all_queued && tree_in_workgroup(base, k))) continue;
     uint32_t *a = cv + base * 8;
     for (;;) {
-      const bool final_pass = k <= kTile;
-      const uint64_t ntiles = (k + kTile - 1) / kTile;
+      const bool final_pass = k <= TILE;
+      const uint64_t ntiles = (k + TILE - 1) / TILE;
       for (uint64_t tile = 0; tile < ntiles; ++tile) {
-        uint32_t cnt = (uint32_t)min<uint64_t>(kTile, k - tile * kTile);
-        const uint32_t *src = a + tile * kTile * 8;
-        for (uint32_t w = tid; w < cnt * 8; w += kTreeThreads) tt[0][w] = src[w];
+        uint32_t cnt = (uint32_t)min<uint64_t>(TILE, k - tile * TILE);
+        const uint32_t *src = a + tile * TILE * 8;
+        for (uint32_t w = tid; w < cnt * 8; w += TT) tt[0][w] = src[w];
         __syncthreads();
         int cur = 0;
         while (cnt > 1) {
@@ -1259,8 +1273,8 @@ __global__ __launch_bounds__(kTreeThreads) void b3_tree(
           const uint32_t pflags = PARENT | ((final_pass && cnt == 2) ? ROOT : 0);
           const uint32_t dq = qlane == 2 ? 64u : qlane == 3 ? pflags : 0u;
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const uint32_t pi = qid + s * kTreeQuads;
+          for (int s = 0; s < kPasses; ++s) {
+            const uint32_t pi = qid + s * kQ;
             if (pi < p) {
               uint32_t m[28];
 #pragma unroll
@@ -1357,7 +1371,7 @@ uint64_t blake3_max_groups(uint64_t n, uint64_t data_len, int D) {
 bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
                    uint64_t data_len, int D, Workspace &ws, ngpu_result *out,
                    hipStream_t s, hipEvent_t ev_first, hipEvent_t ev_start, hipEvent_t ev_end_groups,
-                   hipEvent_t ev_end) {
+                   hipEvent_t ev_end, uint64_t chunk_size) {
   if (n == 0) {
     (void)hipMemsetAsync(ws.stats, 0, 16 * sizeof(uint64_t), s);
     return false;
@@ -1420,10 +1434,26 @@ bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
     }
     if (!ok) return false;  // (ngpu_create validates the mode; never taken)
   }
+  // group CVs of the planned path (at most chunk_size / 4 KiB per chunk) of a
+  // layer of many chunks: many small trees, four workgroups per CU.  A layer
+  // of few chunks keeps the wide workgroup: its longest tree's widest level
+  // is one pass there, two here (C1 206 -> 203, l32m 628 -> 608 narrow;
+  // log-normal 30 MB layers of ~2,500 chunks 298 -> 329 GB/s)
+  if (B3_QUAD_GROUPS && B3_TREE_NARROW && n >= kTreeNarrowMinChunks &&
+      blake3_planned_in_leaves(n, data_len, D, ws) && chunk_size &&
+      chunk_size / (4 * kLeaf) <= (uint64_t)kTileNarrow) {
+    const uint64_t blocks = n < 8192 ? n : 8192;
+    hipExtLaunchKernelGGL((b3_tree<kTreeThreadsNarrow, kTileNarrow>), dim3((unsigned)blocks),
+                          dim3(kTreeThreadsNarrow), 0, s, nullptr, ev_end, 0,
+                          (const uint64_t *)ws.groups, (const uint32_t *)ws.tree_list,
+                          (const uint64_t *)(ws.stats + 9), ws.cap_g, ws.cv, out, quad);
+    return true;
+  }
   const uint64_t blocks = n < 2048 ? n : 2048;
-  hipExtLaunchKernelGGL(b3_tree, dim3((unsigned)blocks), dim3(kTreeThreads), 0, s, nullptr, ev_end,
-                        0, (const uint64_t *)ws.groups, (const uint32_t *)ws.tree_list,
-                        (const uint64_t *)(ws.stats + 9), ws.cap_g, ws.cv, out, quad);
+  hipExtLaunchKernelGGL((b3_tree<kTreeThreads, kTile>), dim3((unsigned)blocks), dim3(kTreeThreads), 0,
+                        s, nullptr, ev_end, 0, (const uint64_t *)ws.groups,
+                        (const uint32_t *)ws.tree_list, (const uint64_t *)(ws.stats + 9), ws.cap_g,
+                        ws.cv, out, quad);
   return true;
 }
 

@@ -197,7 +197,8 @@ constexpr uint64_t kSmallDedupLayers = 64;
 bool launch_blake3(const uint8_t *data, const ngpu_chunk *chunks, uint64_t n,
                    uint64_t data_len, int group_log2, Workspace &ws,
                    ngpu_result *out, hipStream_t s, hipEvent_t ev_first,
-                   hipEvent_t ev_groups_start, hipEvent_t ev_groups_end, hipEvent_t ev_end);
+                   hipEvent_t ev_groups_start, hipEvent_t ev_groups_end, hipEvent_t ev_end,
+                   uint64_t chunk_size = 0);  // the engine's (0: unknown; picks b3_tree's width)
 uint64_t blake3_max_groups(uint64_t n, uint64_t data_len, int group_log2);
 // ngpu_config load-mode override (flags bits 8..10 minus one) this build runs.
 bool blake3_load_mode_ok(int lm);

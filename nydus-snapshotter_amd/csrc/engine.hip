@@ -324,7 +324,7 @@ int enqueue_digest(ngpu_engine *e, const uint8_t *d_data, uint64_t len,
     // events ride on the kernels: no marker packets between the launches
     hipEvent_t end = tm ? ev[3] : ws_lazy_end(e, s, chained) ? nullptr : e->cur->done;
     if (launch_blake3(d_data, d_chunks, n, len, D, ws, d_out, s, tm ? ev[0] : nullptr,
-                      tm ? ev[1] : nullptr, tm ? ev[2] : nullptr, end))
+                      tm ? ev[1] : nullptr, tm ? ev[2] : nullptr, end, e->cfg.chunk_size))
       bound = end;
     snprintf(e->cur->path, sizeof e->cur->path, "blake3 %s D=%d, %llu chunks",
              blake3_planned_in_leaves(n, len, D, ws) ? "quad_planned"
