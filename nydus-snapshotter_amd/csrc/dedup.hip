@@ -761,7 +761,7 @@ __device__ __forceinline__ void resolve_values(
       r.kind = NGPU_NEW;
       r.ref = c;
       v[0] = 1;
-      v[1] = ((uint64_t)len + align - 1) / align * align;
+      v[1] = ((uint64_t)len + align - 1) & ~(uint64_t)(align - 1);  // (align: 1 or 4096)
       v[2] = len;
     }
   }
@@ -1111,8 +1111,14 @@ __global__ __launch_bounds__(T) void dedup_small_lds(
   // digest's tag : bucket (overwritten by the chunk's offset prefix in B).
   constexpr uint32_t kDictBit = 0x80000000u;
   constexpr uint32_t kUnhashedBit = 0x20000000u;  // no digest (digest_unwritten)
+  // a dict hit's blob, per item: the first hit of every blob is found after
+  // the loop, one reduced atomic per wave and item row (wave_min_u32)
+  constexpr int kRows = (int)(kLdsChunks / T);
+  uint32_t hit_blob[kRows];
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) hit_blob[k] = kNone;
 #pragma unroll 1
-  for (int k = 0; k < (int)(kLdsChunks / T); ++k) {
+  for (int k = 0; k < kRows; ++k) {
     const uint64_t c = (uint64_t)k * T + t;
     if (c >= n) break;
     uint32_t dg[8];
@@ -1135,7 +1141,7 @@ __global__ __launch_bounds__(T) void dedup_small_lds(
       r.blob_index = h.blob;  // inner index; remapped below
       r.uncompressed_offset = h.uncompressed_offset;  // chunk.copy_from(cached_chunk)
       r.dict_blob = h.blob;
-      atomicMin(&bf[h.blob], (uint32_t)c);
+      hit_blob[k] = h.blob;
       continue;
     }
     len_s[c] = len;
@@ -1158,91 +1164,116 @@ __global__ __launch_bounds__(T) void dedup_small_lds(
       }
     }
   }
+  // (every lane of the wave is here: the rows' minima reduce in the wave)
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    if ((uint64_t)k * T >= n) break;  // (uniform)
+    wave_min_u32(bf, hit_blob[k] != kNone, hit_blob[k], (uint32_t)((uint64_t)k * T + t));
+  }
   __syncthreads();
-  // B: resolve INTRA / NEW and scan the four per-chunk quantities in chunk
-  // order, one row of T chunks at a time (one barrier per row).
-  // an INTRA chunk's len_s becomes kIntraBit | its first occurrence once
-  // resolved: no later chunk reads it (a first occurrence is always the
-  // smallest id of its digest, never an INTRA chunk)
+  // B: resolve INTRA / NEW and scan the four per-chunk quantities (NEW,
+  // aligned size, bytes, DICT) in chunk order.  Here thread t takes the
+  // CONTIGUOUS chunks [t R, t R + R): pass 1 resolves them and sums the four
+  // values, ONE block scan of the threads' sums follows, and pass 2 writes
+  // each chunk's prefix from its thread's.  (Rows of T chunks took a barrier,
+  // a wave-sum round and 64 broadcast LDS reads per thread each: 17 of a
+  // 30 us stage at ~2,800 chunks, profiles/r6/dedup_phases_r6ab.json.)
+  // An INTRA chunk's len_s becomes kIntraBit | its first occurrence once
+  // resolved: no other chunk reads it (a first occurrence is always the
+  // smallest id of its digest, never an INTRA chunk).
   constexpr uint32_t kIntraBit = 0x40000000u;
-  uint64_t carry[4] = {0, 0, 0, 0};
+  constexpr int W = (int)(T / 64);
   __shared__ uint32_t own_first;
   if (t == 0) own_first = kNone;
+  const uint32_t R = (uint32_t)((n + T - 1) / T);
+  const uint64_t c0 = (uint64_t)t * R;
+  uint64_t sum[4] = {0, 0, 0, 0};
+  // this chunk's four values, from its decision in len_s
+  auto values = [&](uint32_t lv, uint64_t v[4]) {
+    v[0] = v[1] = v[2] = v[3] = 0;
+    if (lv & kDictBit) {
+      v[3] = 1;
+    } else if (!(lv & (kUnhashedBit | kIntraBit))) {  // NEW
+      v[0] = 1;
+      v[1] = ((uint64_t)lv + align - 1) & ~(uint64_t)(align - 1);  // (align: 1 or 4096)
+      v[2] = lv;
+    }
+  };
 #pragma unroll 1
-  for (int k = 0; k < (int)(kLdsChunks / T); ++k) {
-    const uint64_t c = (uint64_t)k * T + t;
-    uint64_t v[4] = {0, 0, 0, 0};  // NEW, aligned size, bytes, DICT
-    if (c < n) {
-      const uint32_t lv = len_s[c];
-      if (lv & kDictBit) {
-        v[3] = 1;
-      } else if (lv & kUnhashedBit) {
-        // no digest: no decision (the call fails)
-      } else {
-        const uint64_t tb = off[c];
-        const uint32_t tag = (uint32_t)(tb >> 32);
-        uint32_t f = kNone;
-        for (uint32_t p = (uint32_t)tb & mask;; p = (p + 1) & mask) {
-          const uint64_t sv = table[p];
-          if (sv == kEmpty) break;
-          const uint32_t id = (uint32_t)sv;
-          if ((uint32_t)(sv >> 32) != tag) continue;
-          if (id == c) {
-            f = id;
-            break;
-          }
-          uint32_t dg[8];  // a tag match with another chunk: compare the digests
-          load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, dg);
-          if (digest_eq<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), id, dg)) {
-            f = id;
-            break;
-          }
+  for (uint32_t j = 0; j < R; ++j) {
+    const uint64_t c = c0 + j;
+    if (c >= n) break;
+    const uint32_t lv = len_s[c];
+    if (!(lv & (kDictBit | kUnhashedBit))) {
+      const uint64_t tb = off[c];
+      const uint32_t tag = (uint32_t)(tb >> 32);
+      uint32_t f = kNone;
+      for (uint32_t p = (uint32_t)tb & mask;; p = (p + 1) & mask) {
+        const uint64_t sv = table[p];
+        if (sv == kEmpty) break;
+        const uint32_t id = (uint32_t)sv;
+        if ((uint32_t)(sv >> 32) != tag) continue;
+        if (id == c) {
+          f = id;
+          break;
         }
-        const uint32_t len = lv;
-        if (f != (uint32_t)c && f != kNone && (len_s[f] & ~kDictBit) == len) {
-          len_s[c] = kIntraBit | f;  // INTRA
-        } else {
-          v[0] = 1;
-          v[1] = ((uint64_t)len + align - 1) / align * align;
-          v[2] = len;
+        uint32_t dg[8];  // a tag match with another chunk: compare the digests
+        load_digest<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), c, dg);
+        if (digest_eq<sizeof(ngpu_result)>(reinterpret_cast<const uint8_t *>(out), id, dg)) {
+          f = id;
+          break;
         }
       }
+      if (f != (uint32_t)c && f != kNone && (len_s[f] & ~kDictBit) == lv)
+        len_s[c] = kIntraBit | f;  // INTRA
     }
-    if ((uint64_t)k * T >= n) break;  // uniform: the row is empty
-    uint64_t x[4];
+    uint64_t v[4];
+    values(len_s[c], v);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] = v[q];
+    for (int q = 0; q < 4; ++q) sum[q] += v[q];
+  }
+  // one block scan of the threads' sums: in the wave, then across the W waves
+  uint64_t x[4];
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
+  for (int q = 0; q < 4; ++q) x[q] = sum[q];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint64_t y = __shfl_up(x[q], o, 64);
-        if (lane >= o) x[q] += y;
-      }
-    }
-    const uint32_t b = k & 1;  // double-buffered: one barrier per row
-    if (lane == 63) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) wsum[b][q][wid] = x[q];
-    }
-    __syncthreads();
-    uint64_t pre[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
+  for (int o = 1; o < 64; o <<= 1) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-#pragma unroll 4
-      for (int w = 0; w < (int)(T / 64); ++w) {
-        const uint64_t y = wsum[b][q][w];
-        if (w < (int)wid) pre[q] += y;
-        tot[q] += y;
-      }
+      const uint64_t y = __shfl_up(x[q], o, 64);
+      if (lane >= o) x[q] += y;
     }
-    if (c < n) {
-      nidx[c] = (uint32_t)(carry[0] + pre[0] + x[0] - v[0]);
-      off[c] = carry[1] + pre[1] + x[1] - v[1];
-      if (v[0]) atomicMin(&own_first, (uint32_t)c);
-    }
+  }
+  if (lane == 63) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) carry[q] += tot[q];
+    for (int q = 0; q < 4; ++q) wsum[0][q][wid] = x[q];
+  }
+  __syncthreads();
+  uint64_t run[4], carry[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint64_t y = lane < (uint32_t)W ? wsum[0][q][lane] : 0;  // lane w: wave w's sum
+#pragma unroll
+    for (int o = 1; o < W; o <<= 1) {
+      const uint64_t z = __shfl_up(y, o, 64);
+      if (lane >= (uint32_t)o) y += z;
+    }
+    carry[q] = __shfl(y, W - 1, 64);                         // the layer's total
+    const uint64_t wpre = __shfl(y, wid ? wid - 1 : 0, 64);  // waves before this one
+    run[q] = (wid ? wpre : 0) + x[q] - sum[q];               // chunks before c0
+  }
+#pragma unroll 1
+  for (uint32_t j = 0; j < R; ++j) {
+    const uint64_t c = c0 + j;
+    if (c >= n) break;
+    uint64_t v[4];
+    values(len_s[c], v);
+    nidx[c] = (uint32_t)run[0];
+    off[c] = run[1];
+    // the layer's first NEW chunk: the one NEW chunk with none before it
+    if (v[0] && run[0] == 0) own_first = (uint32_t)c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) run[q] += v[q];
   }
   __syncthreads();
   // C: blob order of the layer: dict blobs at their first hit, the own blob

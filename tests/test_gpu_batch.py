@@ -177,7 +177,7 @@ def test_native_threads_drive_concurrent_packs(oracle):
     """tools/packs_drive.cpp (bench.py --packs's caller: K native threads, one
     Pack each, as cgo goroutines would): decisions and early-emission streams
     of 8 concurrent layers, fed by Write and by ReadFrom (reserve / commit),
-    on one engine and on a 2-part node (least-loaded placement: 4 + 4),
+    on one engine and on a 2-part node (least-loaded placement: both parts take Packs),
     counted per layer, equal the oracle's."""
     import ctypes
     import os
@@ -218,8 +218,9 @@ def test_native_threads_drive_concurrent_packs(oracle):
                 assert (got[k, 3] > 0) == (mode & 1 == 1)
             assert all(x > 0 for x in rs)
             assert sum(b["packs"] for b in bs) >= 2, bs
-            if on_node:
-                assert sorted(np.bincount(np.array(part), minlength=2).tolist()) == [4, 4], list(part)
+            if on_node:  # placement follows load (open Packs per engine): not an exact split
+                placed = np.bincount(np.array(part), minlength=2).tolist()
+                assert len(placed) == 2 and min(placed) > 0 and sum(placed) == K, list(part)
 
 
 @pytest.mark.parametrize("digester", ["blake3", "sha256"])
