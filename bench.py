@@ -2148,7 +2148,7 @@ def main():
                    "explained_frac_of_step": round(min(total, step_s * 1e3) / (step_s * 1e3), 3),
                    "chain_frac_of_leaf_and_tree_kernels": round(
                        chain_s * 1e3 / max(1e-9, ker["digest"] + ker["tree"]), 3)}
-            tr, tsrc = newest_profile("c1_step_trace_r6s.json")
+            tr, tsrc = newest_profile("c1_step_trace_r6ae.json")
             if tr:
                 dec["trace"] = {"kernel_us": tr["kernel_us_median"], "gap_us_profiled": tr["gap_us_median"],
                                 "source": tsrc,
